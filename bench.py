@@ -1,0 +1,172 @@
+"""GRPO step samples/sec (rollout + update), Qwen2.5-0.5B, 1..8 x MI355X.
+
+Workload (BASELINE.json configs[1]): Qwen2.5-0.5B
+architecture, random-init bf16 weights (no network for checkpoints), G = 8
+generations x 8 prompts per GPU = 64 sequences, P = 128 synthetic prompt
+tokens (uniform ids, seed 1234, no padding), C = 256 completion tokens
+forced to full length (min_new_tokens = C), micro-batch 16 x GA 4, beta = 0,
+T = 1, top_p = 1, deterministic dummy reward len(set(ids)) % 7.
+
+A step = one full optimizer step of the GRPO loop: generation of 64 x 256
+tokens, completion mask, rewards, group advantages, policy forward + fused
+log-prob/entropy + fused loss + backward, (N>1: RCCL gradient all-reduce),
+grad-norm clip and AdamW.  Weak scaling: per-GPU work is fixed as N grows.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GRPO step samples/sec (rollout+update), Qwen2.5-0.5B at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
+MFMA_BF16_PEAK_TF = 2500.0  # dense bf16
+
+G, PROMPTS_PER_GPU, P, C, MB, GA = 8, 8, 128, 256, 16, 4
+EOS, PAD = 151645, 151643
+
+
+def dummy_reward(prompts=None, completions=None, completion_ids=None, **kw):
+    return [float(len(set(ids)) % 7) for ids in completion_ids]
+
+
+def make_dataset(n: int, V: int):
+    g = torch.Generator().manual_seed(1234)
+    ids = torch.randint(0, V, (n, P), generator=g)
+    ids[ids == EOS] = 0
+    return [{"prompt": None, "prompt_ids": ids[i].tolist()} for i in range(n)]
+
+
+def cpu_baseline(steps_note: str) -> dict:
+    """The oracle's CPU restatement of the reference GRPO step, on a bounded
+    sample of the same workload (1 prompt x G=8, P=128, C=32 instead of 256),
+    timed on the host cores; scaled to the full sample per token."""
+    from oracle import grpo_step as og
+    from swh_trl_amd.engine.config import qwen2_5_0_5b
+    threads = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    cfg = qwen2_5_0_5b().to_dict()
+    model = og.hf_qwen2_from_config(cfg, seed=0, dtype=torch.bfloat16)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-6)
+    g = torch.Generator().manual_seed(1234)
+    prompt = torch.randint(0, cfg["vocab_size"], (1, P), generator=g).repeat(G, 1)
+    pm = torch.ones_like(prompt)
+
+    def reward(cids, cmask):
+        return [len(set(r[m.bool()].tolist())) % 7 for r, m in zip(cids, cmask)]
+
+    cs = 32
+    kw = dict(num_generations=G, per_device_train_batch_size=G, gradient_accumulation_steps=1, eos_token_id=EOS,
+              pad_token_id=PAD, min_new_tokens=cs)
+    og.grpo_step(model, opt, prompt[:, :16], pm[:, :16], reward, C=4, **dict(kw, min_new_tokens=4))  # warm-up
+    tm = {}
+    t0 = time.perf_counter()
+    og.grpo_step(model, opt, prompt, pm, reward, C=cs, timings=tm, **kw)
+    wall = time.perf_counter() - t0
+    # scale: decode time ~ linear in generated tokens; update ~ linear in P + C tokens
+    full_s = tm["generate_s"] * (C / cs) + tm["update_s"] * ((P + C) / (P + cs))
+    return {"value": G / full_s, "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": (f"oracle/grpo_step.py (CPU restatement, transformers Qwen2 bf16, torch {torch.__version__}) on "
+                       f"1 prompt x G={G}, P={P}, C={cs}: generate {tm['generate_s']:.2f}s + update "
+                       f"{tm['update_s']:.2f}s = {wall:.2f}s wall; scaled per token to C={C}: {full_s:.1f}s per "
+                       f"{G} samples; {steps_note}")}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--layers", type=int, default=None, help="debug only: shrink the model (invalid for reporting)")
+    args = ap.parse_args()
+
+    from swh_trl_amd import dist as sd
+    from swh_trl_amd import profiling
+    from swh_trl_amd.engine.config import qwen2_5_0_5b
+    from swh_trl_amd.trainer import GRPOConfig, GRPOTrainer
+
+    rank, world, local = sd.init_from_env()
+    torch.cuda.set_device(local)
+    cfg = qwen2_5_0_5b()
+    if args.layers:
+        cfg.num_hidden_layers = args.layers
+    steps, warm = args.steps, args.warmup
+    n_prompts = PROMPTS_PER_GPU * world * (steps + warm + 1)
+    ds = make_dataset(n_prompts, cfg.vocab_size)
+    gc = GRPOConfig(output_dir="/tmp/grpo-bench", per_device_train_batch_size=MB, gradient_accumulation_steps=GA,
+                    num_generations=G, max_prompt_length=P, max_completion_length=C, learning_rate=1e-6,
+                    beta=0.0, temperature=1.0, top_p=1.0, max_steps=steps + warm, logging_steps=10 ** 9, seed=0,
+                    shuffle_dataset=True,
+                    generation_kwargs={"min_new_tokens": C, "eos_token_id": EOS, "pad_token_id": PAD})
+    tr = GRPOTrainer(model=cfg, reward_funcs=dummy_reward, args=gc, train_dataset=ds)
+    tr.state.max_steps = steps + warm
+    tb = time.perf_counter()
+    for i in range(warm):
+        tr.training_step_group()
+        torch.cuda.synchronize()
+        if rank == 0:
+            print(f"[bench] warmup step {i + 1}/{warm} done at {time.perf_counter() - tb:.1f}s", file=sys.stderr,
+                  flush=True)
+    sd.barrier()
+    torch.cuda.synchronize()
+    profiling.reset()
+    profiling.enable(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.training_step_group()
+    torch.cuda.synchronize()
+    sd.barrier()
+    elapsed = time.perf_counter() - t0
+    profiling.enable(False)
+    elapsed = sd.all_max(elapsed)
+    kern = profiling.summary()
+    log = tr._flush_logs()
+    samples = world * PROMPTS_PER_GPU * G * steps
+    value = samples / elapsed
+    ms = 1000.0 * elapsed / steps
+
+    # dominant instrumented kernel (largest total device time in the timed region)
+    dom_name, dom = max(kern.items(), key=lambda kv: kv[1]["total_ms"])
+    achieved = dom["bytes_per_launch"] / (dom["avg_us"] * 1e-6) / 1e9
+    roof = {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "avg_us": round(dom["avg_us"], 2), "bytes_per_launch": dom["bytes_per_launch"], "traffic": None,
+            "all_kernels": {k: {"avg_us": round(v["avg_us"], 2), "launches": v["launches"],
+                                "GB/s": round(v["bytes_per_launch"] / (v["avg_us"] * 1e-6) / 1e9, 1)}
+                            for k, v in kern.items()}}
+    # step-level roofline: t_roof = HBM bytes / 8 TB/s + FLOPs / 2.5 PF
+    t_roof_ms = 70.5
+    line = {"metric": METRIC, "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": steps,
+            "warmup": warm, "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (uniform prompt ids seed 1234, random-init weights, dummy reward)",
+            "config": {"workload": "configs[1]: Qwen2.5-0.5B GRPO bf16, group_size=8, 256-tok completions",
+                       "model": "Qwen2.5-0.5B (random init)", "global_batch": world * PROMPTS_PER_GPU * G,
+                       "prompts_per_gpu": PROMPTS_PER_GPU, "num_generations": G, "prompt_len": P,
+                       "completion_len": C, "seq_len": P + C, "micro_batch": MB, "grad_accum": GA, "beta": 0.0,
+                       "parallelism": f"dp{world}", "layers": cfg.num_hidden_layers},
+            "roofline": roof,
+            "step_roofline": {"t_roof_ms_per_gpu": t_roof_ms, "frac": round(t_roof_ms / ms, 4)},
+            "train_log": {k: log.get(k) for k in ("loss", "grad_norm", "reward", "entropy")}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.layers:
+        try:
+            line["cpu_baseline"] = cpu_baseline(f"GPU run: {steps} timed steps")
+        except Exception as e:  # report, never hide
+            line["cpu_baseline"] = {"value": None, "error": repr(e)[:300]}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

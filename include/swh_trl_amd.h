@@ -1,0 +1,262 @@
+/*
+ * swh_trl_amd — C-ABI of the MI355X-native GRPO/PPO rollout-and-update hot path.
+ *
+ * Every entry point is a stream-ordered device launch:
+ *   - all pointers are CALLER-OWNED DEVICE buffers (allocated by PyTorch in the
+ *     host layer); scratch comes in as an explicit workspace argument — the
+ *     library never calls hipMalloc, never synchronises, never copies to host;
+ *   - `stream` is a hipStream_t passed as void* (NULL = the null stream);
+ *   - return value: 0 = launched, <0 = error (see SWH_E_*); argument errors are
+ *     detected on the host before anything is launched;
+ *   - no global mutable state: re-entrant across streams and devices, and safe
+ *     to capture into a hipGraph (the decode step is captured and replayed).
+ *
+ * Each function cites the reference (shiwanghua/swh-trl @ TRL 0.21.0.dev0)
+ * symbol it replaces, `path:line` relative to the reference tree.
+ * Dtype codes: SWH_F32 = 0, SWH_BF16 = 1, SWH_F16 = 2.
+ */
+#ifndef SWH_TRL_AMD_H
+#define SWH_TRL_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SWH_OK 0
+#define SWH_E_ARG (-1)      /* invalid argument (shape, dtype, null pointer) */
+#define SWH_E_LAUNCH (-2)   /* hipGetLastError() after the launch was not hipSuccess */
+#define SWH_E_DTYPE (-3)    /* dtype not supported by this entry point */
+
+#define SWH_F32 0
+#define SWH_BF16 1
+#define SWH_F16 2
+
+/* ---- library ------------------------------------------------------------ */
+const char *swh_version(void);
+const char *swh_status_string(int status);
+
+/* ---- a6/a7/a8: log-probs + entropy of temperature-scaled logits ----------
+ * Replaces trl/trainer/utils.py:1430-1462 (selective_log_softmax),
+ * :1465-1490 (entropy_from_logits) and the `logits / self.temperature` of
+ * grpo_trainer.py:1254 / ppo_trainer.py:446,558.
+ * Rows are addressed as r = o*rows_inner + i with element offset
+ * o*stride_outer + i*stride_inner (lets the caller pass the [:, -C-1:-1]
+ * slice of a [B, L, V] logits tensor without a copy).  ids/logp/entropy/lse
+ * are contiguous [rows_outer*rows_inner].  z = logits / temperature.
+ *   logp[r]    = z[r, ids[r]] - logsumexp(z[r, :])
+ *   entropy[r] = -sum_j p_j log p_j          (entropy may be NULL)
+ *   lse[r]     = logsumexp(z[r, :])          (saved for the backward)
+ * flags: SWH_LOGP_ROUND_SCALED — round z to the logits dtype after the
+ * division, as the reference does when it divides bf16 logits in bf16. */
+#define SWH_LOGP_ROUND_SCALED 1
+int swh_logp_entropy_fwd(const void *logits, int dtype, int64_t rows_outer, int64_t rows_inner,
+                         int64_t stride_outer, int64_t stride_inner, int64_t V, const int64_t *ids,
+                         float temperature, int flags, float *logp, float *entropy, float *lse,
+                         void *stream);
+
+/* Backward of logp w.r.t. the logits (autograd of selective_log_softmax and
+ * of the temperature division): dlogits[r, j] = dlogp[r]/T * (1[j==ids[r]] - p_j).
+ * dlogits has the logits dtype and its own (outer, inner) strides; row
+ * stride between elements is 1. */
+int swh_logp_bwd(const void *logits, int dtype, int64_t rows_outer, int64_t rows_inner,
+                 int64_t stride_outer, int64_t stride_inner, int64_t V, const int64_t *ids,
+                 float temperature, int flags, const float *lse, const float *dlogp, void *dlogits,
+                 int64_t dstride_outer, int64_t dstride_inner, void *stream);
+
+/* ---- a4: one rollout sampling step ----------------------------------------
+ * Replaces the HF `_sample` body the reference reaches through
+ * grpo_trainer.py:1793-1810 (processors built from GenerationConfig
+ * :995-1014): repetition penalty -> min-new-tokens EOS suppression ->
+ * temperature -> top-k -> top-p -> min-p, then an exact categorical draw
+ * (Gumbel-max over a Philox4x32-10 stream) or argmax,
+ * then pad-after-EOS bookkeeping.  All step-dependent state lives on the
+ * device so the call can be graph-captured and replayed.
+ *   logits      [B, V] (row stride ld), dtype bf16/f32
+ *   rng         device uint64[2] = {seed (Philox key), counter base}; the
+ *               counter of token t is base + t, so a replayed graph draws
+ *               fresh numbers when the host bumps rng[1] between rollouts
+ *   step        device int32: index of the token being generated
+ *   finished    device int32 [B]  (in/out)
+ *   seen        device uint32 [B, ceil(V/32)] membership bitmap for the
+ *               repetition penalty (in/out; may be NULL when penalty == 1)
+ *   out_tokens  int64 [B, out_ld]; token written at column *step
+ *   cur_tokens  int64 [B]; the same token (next decode input)
+ *   out_logp    f32 [B, out_ld] or NULL: log-prob of the drawn token under the
+ *               processed distribution (the PPO rollout log-prob, utils.py:1094)
+ *   scores_out  f32 [B, V] or NULL: processed scores (HF output_scores)
+ *   workspace   >= swh_sample_workspace_bytes(B, V) bytes                   */
+typedef struct {
+    float temperature;        /* 1.0 = off */
+    float top_p;              /* 1.0 = off */
+    float min_p;              /* <= 0 = off */
+    float repetition_penalty; /* 1.0 = off */
+    int32_t top_k;            /* 0 = off */
+    int32_t greedy;           /* 1 = argmax (do_sample=False) */
+    int32_t min_new_tokens;   /* EOS suppressed while *step < min_new_tokens */
+    int32_t pad_token_id;     /* emitted by finished rows; -1 = no pad bookkeeping */
+    int32_t n_eos;            /* number of valid eos ids (0..4) */
+    int32_t eos_ids[4];
+} swh_sample_params;
+int64_t swh_sample_workspace_bytes(int64_t B, int64_t V);
+int swh_sample_step(const void *logits, int dtype, int64_t B, int64_t V, int64_t ld,
+                    const swh_sample_params *params, const uint64_t *rng, const int32_t *step,
+                    int32_t *finished,
+                    uint32_t *seen, int64_t *out_tokens, int64_t out_ld, int64_t *cur_tokens,
+                    float *out_logp, float *scores_out, void *workspace, void *stream);
+/* Sets the `seen` bitmap from prompt ids (ids < 0 or mask == 0 are skipped). */
+int swh_seen_init(const int64_t *ids, const int32_t *mask, int64_t B, int64_t L, int64_t V,
+                  uint32_t *seen, void *stream);
+/* Increments the device step counter (end of a captured decode step). */
+int swh_step_advance(int32_t *step, void *stream);
+
+/* ---- a5: completion mask ---------------------------------------------------
+ * Replaces grpo_trainer.py:1812-1831: mask[b,t] = t <= first EOS (EOS
+ * included), lengths[b] = sum_t mask, has_eos[b]; rows with no EOS are zeroed
+ * when mask_truncated != 0. */
+int swh_completion_mask(const int64_t *completion_ids, int64_t B, int64_t C, const int32_t *eos_ids,
+                        int32_t n_eos, int32_t mask_truncated, int32_t *mask, int32_t *lengths,
+                        int32_t *has_eos, void *stream);
+
+/* ---- a10: group-relative advantages -----------------------------------------
+ * Replaces grpo_trainer.py:1914-1930: r = nansum_f(rpf*w); per group of G
+ * rows mean and UNBIASED std; A = r - mean, /(std + 1e-4) if scale_rewards;
+ * zero_std[g] = isclose(std, 0).  Any of group_mean/group_std/zero_std/
+ * rewards may be NULL. */
+int swh_group_advantage(const float *rewards_per_func, const float *weights, int64_t N, int64_t F,
+                        int64_t G, int32_t scale_rewards, float *advantages, float *rewards,
+                        float *group_mean, float *group_std, int32_t *zero_std, void *stream);
+
+/* ---- a11: GRPO policy loss, forward + d loss / d logp in one pass -----------
+ * Replaces grpo_trainer.py:2058-2175 from the log-probs on: k3 KL (:2085),
+ * token/sequence importance weights (:2099-2111), two-sided clip and delta
+ * (:2113-2118), -min(c1 A, c2 A) (:2120), entropy mask (:2123), +beta KL
+ * (:2125), grpo/bnpo/dr_grpo aggregation (:2130-2137), and the metric sums
+ * behind :2139-2174.  Gradient conventions follow torch autograd exactly
+ * (min ties split 1/2-1/2, clamp passes the gradient on the closed interval).
+ *   logp/old/ref f32 [R, T] (old/ref nullable; old NULL == logp.detach())
+ *   adv f32 [R]; mask int32 [R, T]; ent_mask uint8 [R, T] nullable;
+ *   entropy f32 [R, T] nullable (metrics only); row_scale f32 [R] nullable:
+ *   extra per-row loss weight (used to fuse gradient-accumulation micro-
+ *   batches into one pass; NULL = 1).  seg [R] int32 nullable: normaliser
+ *   segment of each row (bnpo token counts are per segment; NULL = one).
+ * Outputs: loss f32[1] (sum over segments of each segment's loss, times
+ * row_scale), dlogp f32 [R, T] (d loss / d logp, may be NULL), metrics f32[8]:
+ * {tokens, kl_sum, entropy_sum, low_clip_sum, high_clip_sum, region_clip_sum,
+ *  seq_rows, 0}.  workspace >= swh_grpo_loss_workspace_bytes(R). */
+#define SWH_LOSS_GRPO 0
+#define SWH_LOSS_BNPO 1
+#define SWH_LOSS_DR_GRPO 2
+#define SWH_IS_TOKEN 0
+#define SWH_IS_SEQUENCE 1
+typedef struct {
+    float beta;
+    float epsilon_low;
+    float epsilon_high;
+    float delta;              /* <= 0 = off */
+    int32_t loss_type;        /* SWH_LOSS_* */
+    int32_t is_level;         /* SWH_IS_* */
+    int32_t max_completion_length;
+    int32_t num_segments;     /* >= 1 */
+} swh_grpo_loss_params;
+int64_t swh_grpo_loss_workspace_bytes(int64_t R);
+int swh_grpo_loss_fwd_bwd(const float *logp, const float *old_logp, const float *ref_logp,
+                          const float *adv, const int32_t *mask, const uint8_t *ent_mask,
+                          const float *entropy, const float *row_scale, const int32_t *seg, int64_t R,
+                          int64_t T, const swh_grpo_loss_params *p, float *loss, float *dlogp,
+                          float *metrics, void *workspace, void *stream);
+
+/* ---- a17: masked mean / var / whiten (trl/core.py:43-76) -----------------
+ * values f32 [N], mask int32 [N]; out f32 [N]; stats f32[3] = {mean, var,
+ * mask_sum}.  A zero mask sum yields NaN stats (the host raises ValueError
+ * like core.py:59).  workspace >= swh_masked_whiten_workspace_bytes(N). */
+int64_t swh_masked_whiten_workspace_bytes(int64_t N);
+int swh_masked_whiten(const float *values, const int32_t *mask, int64_t N, int32_t shift_mean,
+                      float *out, float *stats, void *workspace, void *stream);
+
+/* ---- a18: GAE reverse scan (ppo_trainer.py:523-535) --------------------
+ * rewards/values f32 [B, T] -> advantages, returns f32 [B, T]. */
+int swh_gae_scan(const float *rewards, const float *values, int64_t B, int64_t T, float gamma,
+                 float lam, float *advantages, float *returns, void *stream);
+
+/* ---- a19: PPO clipped policy + value loss, fwd + bwd (ppo_trainer.py:557-605)
+ * new_logp, old_logp, adv, vpred, old_values, returns f32 [B, T];
+ * pad_mask / pad_mask_p1 uint8 [B, T] (1 = padding, as the reference's
+ * padding_mask / padding_mask_p1).  Outputs: loss f32[1],
+ * dnew_logp / dvpred f32 [B,T] (nullable), stats f32[8] =
+ * {pg_loss, vf_loss, pg_clipfrac, vf_clipfrac, approxkl, ratio_mean, 0, 0}.
+ * workspace >= swh_ppo_loss_workspace_bytes(B*T). */
+int64_t swh_ppo_loss_workspace_bytes(int64_t N);
+int swh_ppo_loss_fwd_bwd(const float *new_logp, const float *old_logp, const float *adv,
+                         const float *vpred, const float *old_values, const float *returns,
+                         const uint8_t *pad_mask, const uint8_t *pad_mask_p1, int64_t B, int64_t T,
+                         float cliprange, float cliprange_value, float vf_coef, float *loss,
+                         float *dnew_logp, float *dvpred, float *stats, void *workspace, void *stream);
+
+/* ---- a20: value head (modeling_value_head.py:50-59; PPO score head
+ * ppo_trainer.py:95, utils.py:937): out[r] = sum_h hidden[r,h]*w[h] (+ bias).
+ * hidden bf16/f32 [R, H] row stride ld; w f32 [H]; bias nullable f32[1]. */
+int swh_value_head_fwd(const void *hidden, int dtype, int64_t R, int64_t H, int64_t ld, const float *w,
+                       const float *bias, float *out, void *stream);
+
+/* ---- a13: optimizer --------------------------------------------------------
+ * Squared-L2 partial sums of a flat gradient buffer: partials f32
+ * [swh_sqnorm_partials(N)]; then swh_finalize_clip reduces them to the total
+ * norm and the clip coefficient min(1, max_norm/(norm+1e-6)) on device
+ * (torch.nn.utils.clip_grad_norm_ semantics; max_norm <= 0 => coef 1).
+ * out2 f32[2] = {total_norm, clip_coef}. */
+int64_t swh_sqnorm_partials(int64_t N);
+int swh_grad_sqnorm(const void *grad, int dtype, int64_t N, float *partials, void *stream);
+int swh_finalize_clip(const float *partials, int64_t n_partials, float max_norm, float *out2,
+                      void *stream);
+/* Decoupled AdamW over flat buffers (torch.optim.AdamW update rule):
+ *   g = grad * clip[1] (clip NULL => 1) ; p *= 1 - lr*wd ;
+ *   m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2 ;
+ *   p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
+ * master/m/v f32 [N]; grad bf16/f32 [N]; model_out bf16 [N] or NULL
+ * (refreshed low-precision weights); step_count >= 1. */
+int swh_adamw(float *master, float *exp_avg, float *exp_avg_sq, const void *grad, int grad_dtype,
+              void *model_out, int64_t N, float lr, float beta1, float beta2, float eps,
+              float weight_decay, int64_t step_count, const float *clip, void *stream);
+/* dst_f32[i] += src[i] (bf16/f32) — accumulate micro-batch grads in fp32. */
+int swh_accumulate(float *dst, const void *src, int dtype, int64_t N, float scale, void *stream);
+
+/* ---- a4: decoder kernels of the rollout engine -----------------------------
+ * The transformer the reference runs through transformers' Qwen2/Llama
+ * modeling code (third-party); GEMMs stay on hipBLASLt (MFMA), everything
+ * between GEMMs is here.  bf16 in/out, fp32 math, rounding points as the
+ * transformers bf16 modules (RMSNorm casts before the weight multiply).   */
+/* y = bf16(w * bf16(s * rsqrt(mean(s^2) + eps))), s = x (+ residual), the sum
+ * s also written to residual_out when residual is given; rstd f32 [rows]
+ * nullable (saved for the backward). */
+int swh_rmsnorm_fwd(const void *x, const void *residual, void *residual_out, const void *weight,
+                    int64_t rows, int64_t H, float eps, void *y, float *rstd, void *stream);
+/* Backward: dx = rstd*(w*dy - n*mean(w*dy*n)), n = x*rstd; dw partial sums
+ * f32 [ceil(rows/rows_per_block) x H] reduced by the caller. */
+int swh_rmsnorm_bwd(const void *x, const void *weight, const float *rstd, const void *dy, int64_t rows,
+                    int64_t H, void *dx, float *dw_partial, int64_t rows_per_block, void *stream);
+/* out[r, i] = bf16(bf16(silu(gu[r, i])) * gu[r, I + i]) — gate/up packed. */
+int swh_silu_mul_fwd(const void *gu, int64_t rows, int64_t I, void *out, void *stream);
+int swh_silu_mul_bwd(const void *gu, const void *dout, int64_t rows, int64_t I, void *dgu, void *stream);
+/* x[b, :] = table[ids[b], :] (bf16 rows of width H). */
+int swh_embed_gather(const void *table, const int64_t *ids, int64_t B, int64_t H, void *x, void *stream);
+/* One decode step of attention for every sequence.  state = device int32[2]
+ * {s, P}: s is the index of the token the sampler produces in this step (the
+ * same counter swh_sample_step reads), so the attention input is token s-1:
+ * RoPE on its q/k at position prompt_len[b] + s - 1, k/v appended at cache
+ * slot P + s - 1, softmax(q k^T * scale) v over slots
+ * [P - prompt_len[b], P + s - 1].  Device-resident state lets one captured
+ * graph serve every step and every prompt width.  A slot outside the cache
+ * writes NaN outputs and leaves the cache untouched.
+ * qkv bf16 [B, (Hq + 2 Hkv) D] (bias included); caches bf16 [B, Hkv, Tmax, D];
+ * rope f32 [max_pos, D/2] cos and sin (already rounded to bf16 values);
+ * out bf16 [B, Hq D]. */
+int swh_attn_decode(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
+                    const float *rope_sin, const int32_t *prompt_len, const int32_t *state, int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax, float scale, void *out,
+                    void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SWH_TRL_AMD_H */

@@ -1,0 +1,28 @@
+#!/bin/bash
+# One GPU session: parity tests, then a short bench.  Stops at the first
+# fault / abort / timeout (exit codes 124/134/137/139), never retries.
+set -u
+mkdir -p gpurun_out
+run() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "[$name] rc=$rc"; tail -5 "gpurun_out/$name.log"
+  case $rc in 124|134|137|139) echo "stopping after $name (rc=$rc)"; exit $rc;; esac
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    kern) run kern 600 python -m pytest tests/test_kernels_gpu.py -q -m gpu ;;
+    engine) run engine 600 python -m pytest tests/test_engine_gpu.py -q -m gpu -x ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 900 python bench.py --steps 3 --warmup 2 ;;
+    benchq) run benchq 600 python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    dbg_eager) AMD_SERIALIZE_KERNEL=3 GRAPH=0 C=16 run dbg_eager 300 python tools/debug_decode.py ;;
+    dbg_graph) GRAPH=1 run dbg_graph 300 python tools/debug_decode.py ;;
+    serial2) AMD_SERIALIZE_KERNEL=3 SWH_TRACE=1 run serial2 500 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --layers 2 ;;
+    trace2) SWH_TRACE=1 run trace2 400 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --layers 2 ;;
+    prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null && run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
+    trace) SWH_TRACE=1 run trace 600 python bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
+  esac
+done

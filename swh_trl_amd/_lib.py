@@ -1,0 +1,111 @@
+"""ctypes binding of the C-ABI in include/swh_trl_amd.h.
+
+The shared library is the ONLY compute path of this package: there is no CPU
+fallback.  If `libswh_trl_amd.so` is missing the import of any op raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libswh_trl_amd.so")
+
+c_i32, c_i64, c_f32, c_vp, c_u64 = C.c_int32, C.c_int64, C.c_float, C.c_void_p, C.c_uint64
+
+SWH_F32, SWH_BF16, SWH_F16 = 0, 1, 2
+SWH_LOGP_ROUND_SCALED = 1
+LOSS_TYPES = {"grpo": 0, "bnpo": 1, "dr_grpo": 2}
+IS_LEVELS = {"token": 0, "sequence": 1}
+
+
+class SampleParams(C.Structure):
+    """swh_sample_params (include/swh_trl_amd.h)."""
+    _fields_ = [("temperature", c_f32), ("top_p", c_f32), ("min_p", c_f32), ("repetition_penalty", c_f32),
+                ("top_k", c_i32), ("greedy", c_i32), ("min_new_tokens", c_i32), ("pad_token_id", c_i32),
+                ("n_eos", c_i32), ("eos_ids", c_i32 * 4)]
+
+
+class GRPOLossParams(C.Structure):
+    """swh_grpo_loss_params (include/swh_trl_amd.h)."""
+    _fields_ = [("beta", c_f32), ("epsilon_low", c_f32), ("epsilon_high", c_f32), ("delta", c_f32),
+                ("loss_type", c_i32), ("is_level", c_i32), ("max_completion_length", c_i32),
+                ("num_segments", c_i32)]
+
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "swh_version": (C.c_char_p, []),
+    "swh_status_string": (C.c_char_p, [c_i32]),
+    "swh_logp_entropy_fwd": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_f32, c_i32,
+                                     c_vp, c_vp, c_vp, c_vp]),
+    "swh_logp_bwd": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_f32, c_i32, c_vp, c_vp,
+                             c_vp, c_i64, c_i64, c_vp]),
+    "swh_sample_workspace_bytes": (c_i64, [c_i64, c_i64]),
+    "swh_sample_step": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, C.POINTER(SampleParams), c_vp, c_vp, c_vp,
+                                c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "swh_seen_init": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
+    "swh_step_advance": (c_i32, [c_vp, c_vp]),
+    "swh_completion_mask": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp]),
+    "swh_group_advantage": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                    c_vp]),
+    "swh_grpo_loss_workspace_bytes": (c_i64, [c_i64]),
+    "swh_grpo_loss_fwd_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
+                                      C.POINTER(GRPOLossParams), c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "swh_masked_whiten_workspace_bytes": (c_i64, [c_i64]),
+    "swh_masked_whiten": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp]),
+    "swh_gae_scan": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_vp, c_vp, c_vp]),
+    "swh_ppo_loss_workspace_bytes": (c_i64, [c_i64]),
+    "swh_ppo_loss_fwd_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32,
+                                     c_f32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "swh_value_head_fwd": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "swh_sqnorm_partials": (c_i64, [c_i64]),
+    "swh_grad_sqnorm": (c_i32, [c_vp, c_i32, c_i64, c_vp, c_vp]),
+    "swh_finalize_clip": (c_i32, [c_vp, c_i64, c_f32, c_vp, c_vp]),
+    "swh_adamw": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32,
+                          c_i64, c_vp, c_vp]),
+    "swh_accumulate": (c_i32, [c_vp, c_vp, c_i32, c_i64, c_f32, c_vp]),
+    "swh_rmsnorm_fwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_vp, c_vp, c_vp]),
+    "swh_rmsnorm_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
+    "swh_silu_mul_fwd": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "swh_silu_mul_bwd": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "swh_embed_gather": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "swh_attn_decode": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32,
+                                c_f32, c_vp, c_vp]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load() -> C.CDLL:
+    """Load the HIP library (once).  Raises if it is not built: no fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(f"{LIB_PATH} is missing: build it with `python swh_trl_amd/build.py` "
+                                   "(the swh_trl_amd ops have no CPU fallback)")
+            lib = C.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def check(status: int, name: str) -> None:
+    if status == 0:
+        return
+    msg = load().swh_status_string(status).decode()
+    if status in (-1, -3):
+        raise ValueError(f"{name}: {msg} (status {status})")
+    raise RuntimeError(f"{name}: {msg} (status {status})")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(load(), name)(*args), name)

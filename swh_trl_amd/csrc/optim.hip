@@ -1,0 +1,191 @@
+// Flat-buffer optimizer kernels: global grad-norm clip + decoupled AdamW.
+//
+// Replaces the optimizer the reference gets from transformers'
+// Trainer.create_optimizer (torch.optim.AdamW) and the
+// `clip_grad_norm_(max_grad_norm=1.0)` of the Trainer loop.  All parameters
+// live in ONE flat buffer (the host lays every weight out as a view into it),
+// so the whole update is one HBM-bound streaming kernel instead of a
+// multi-tensor list, and the clip coefficient never leaves the device.
+// Algorithmic bytes per parameter: grad 2 (bf16) + master 8 + m 8 + v 8 +
+// model copy 2 = 28 B.
+#include "common.hpp"
+
+namespace swh {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxPartials = 1024;
+
+template <int DT>
+__global__ __launch_bounds__(kThreads) void sqnorm_kernel(const typename Elem<DT>::T *__restrict__ g, int64_t N,
+                                                          float *__restrict__ partials) {
+    __shared__ float red[kThreads / kWave];
+    float acc[1] = {0.f};
+    const int64_t stride = (int64_t)gridDim.x * kThreads;
+    row_foreach<DT, true>(g, (int64_t)0, N, (int)(blockIdx.x * kThreads + threadIdx.x), (int)stride,
+                          [&](int64_t, float x) { acc[0] = fmaf(x, x, acc[0]); });
+    block_sum<1>(acc, red);
+    if (threadIdx.x == 0) partials[blockIdx.x] = acc[0];
+}
+
+__global__ __launch_bounds__(kThreads) void finalize_clip_kernel(const float *__restrict__ partials, int64_t n,
+                                                                 float max_norm, float *__restrict__ out) {
+    __shared__ double red[kThreads / kWave];
+    double a[1] = {0.0};
+    for (int64_t i = threadIdx.x; i < n; i += kThreads) a[0] += (double)partials[i];
+    block_sum_d<1>(a, red);
+    if (threadIdx.x == 0) {
+        const float norm = (float)sqrt(a[0]);
+        out[0] = norm;
+        float coef = 1.f;
+        if (max_norm > 0.f) coef = fminf(1.f, max_norm / (norm + 1e-6f));
+        out[1] = coef;
+    }
+}
+
+template <int GDT, bool WRITE_MODEL>
+__global__ __launch_bounds__(kThreads) void adamw_kernel(float *__restrict__ p, float *__restrict__ m,
+                                                         float *__restrict__ v,
+                                                         const typename Elem<GDT>::T *__restrict__ g,
+                                                         uint16_t *__restrict__ model, int64_t N, float lr,
+                                                         float b1, float b2, float eps, float wd, float step_size,
+                                                         float bc2_sqrt, const float *__restrict__ clip) {
+    const float cf = clip ? clip[1] : 1.f;
+    const float decay = 1.f - lr * wd;
+    const int64_t n4 = N / 4;
+    const int64_t stride = (int64_t)gridDim.x * kThreads;
+    auto upd = [&](float &pp, float &mm, float &vv, float gg) {
+        gg *= cf;
+        pp *= decay;
+        mm = fmaf(1.f - b1, gg - mm, mm);       // exp_avg.lerp_(grad, 1 - beta1)
+        vv = fmaf((1.f - b2) * gg, gg, vv * b2);  // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
+        const float denom = sqrtf(vv) / bc2_sqrt + eps;
+        pp = pp - step_size * (mm / denom);
+    };
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n4; i += stride) {
+        float4 pp = reinterpret_cast<float4 *>(p)[i];
+        float4 mm = reinterpret_cast<float4 *>(m)[i];
+        float4 vv = reinterpret_cast<float4 *>(v)[i];
+        float gg[4];
+        if constexpr (GDT == SWH_F32) {
+            const float4 t = reinterpret_cast<const float4 *>(g)[i];
+            gg[0] = t.x; gg[1] = t.y; gg[2] = t.z; gg[3] = t.w;
+        } else {
+            const uint2 t = reinterpret_cast<const uint2 *>(g)[i];
+            gg[0] = Elem<GDT>::load(reinterpret_cast<const uint16_t *>(&t.x));
+            gg[1] = Elem<GDT>::load(reinterpret_cast<const uint16_t *>(&t.x) + 1);
+            gg[2] = Elem<GDT>::load(reinterpret_cast<const uint16_t *>(&t.y));
+            gg[3] = Elem<GDT>::load(reinterpret_cast<const uint16_t *>(&t.y) + 1);
+        }
+        upd(pp.x, mm.x, vv.x, gg[0]);
+        upd(pp.y, mm.y, vv.y, gg[1]);
+        upd(pp.z, mm.z, vv.z, gg[2]);
+        upd(pp.w, mm.w, vv.w, gg[3]);
+        reinterpret_cast<float4 *>(p)[i] = pp;
+        reinterpret_cast<float4 *>(m)[i] = mm;
+        reinterpret_cast<float4 *>(v)[i] = vv;
+        if constexpr (WRITE_MODEL) {
+            const uint32_t lo = (uint32_t)f32_to_bf16_bits(pp.x) | ((uint32_t)f32_to_bf16_bits(pp.y) << 16);
+            const uint32_t hi = (uint32_t)f32_to_bf16_bits(pp.z) | ((uint32_t)f32_to_bf16_bits(pp.w) << 16);
+            reinterpret_cast<uint2 *>(model)[i] = uint2{lo, hi};
+        }
+    }
+    for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * kThreads + threadIdx.x; i < N; i += stride) {
+        float pp = p[i], mm = m[i], vv = v[i];
+        upd(pp, mm, vv, Elem<GDT>::load(g + i));
+        p[i] = pp;
+        m[i] = mm;
+        v[i] = vv;
+        if constexpr (WRITE_MODEL) model[i] = f32_to_bf16_bits(pp);
+    }
+}
+
+template <int DT>
+__global__ __launch_bounds__(kThreads) void accumulate_kernel(float *__restrict__ dst,
+                                                              const typename Elem<DT>::T *__restrict__ src, int64_t N,
+                                                              float scale) {
+    const int64_t stride = (int64_t)gridDim.x * kThreads;
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < N; i += stride)
+        dst[i] = fmaf(Elem<DT>::load(src + i), scale, dst[i]);
+}
+
+unsigned grid_for(int64_t work_items) {
+    int64_t g = (work_items + kThreads - 1) / kThreads;
+    if (g > 256 * 16) g = 256 * 16;
+    if (g < 1) g = 1;
+    return (unsigned)g;
+}
+
+}  // namespace
+}  // namespace swh
+
+using namespace swh;
+
+extern "C" int64_t swh_sqnorm_partials(int64_t N) {
+    int64_t n = (N + kThreads * 8 - 1) / (kThreads * 8);
+    if (n > kMaxPartials) n = kMaxPartials;
+    return n < 1 ? 1 : n;
+}
+
+extern "C" int swh_grad_sqnorm(const void *grad, int dtype, int64_t N, float *partials, void *stream) {
+    if (!grad || !partials || N < 0) return SWH_E_ARG;
+    const unsigned nb = (unsigned)swh_sqnorm_partials(N);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (dtype) {
+    case SWH_BF16: sqnorm_kernel<SWH_BF16><<<nb, kThreads, 0, s>>>(static_cast<const uint16_t *>(grad), N, partials); break;
+    case SWH_F16: sqnorm_kernel<SWH_F16><<<nb, kThreads, 0, s>>>(static_cast<const uint16_t *>(grad), N, partials); break;
+    case SWH_F32: sqnorm_kernel<SWH_F32><<<nb, kThreads, 0, s>>>(static_cast<const float *>(grad), N, partials); break;
+    default: return SWH_E_DTYPE;
+    }
+    return launch_status();
+}
+
+extern "C" int swh_finalize_clip(const float *partials, int64_t n_partials, float max_norm, float *out2,
+                                 void *stream) {
+    if (!partials || !out2 || n_partials <= 0) return SWH_E_ARG;
+    finalize_clip_kernel<<<1, kThreads, 0, static_cast<hipStream_t>(stream)>>>(partials, n_partials, max_norm, out2);
+    return launch_status();
+}
+
+extern "C" int swh_adamw(float *master, float *exp_avg, float *exp_avg_sq, const void *grad, int grad_dtype,
+                         void *model_out, int64_t N, float lr, float beta1, float beta2, float eps,
+                         float weight_decay, int64_t step_count, const float *clip, void *stream) {
+    if (!master || !exp_avg || !exp_avg_sq || !grad || N < 0 || step_count < 1) return SWH_E_ARG;
+    if (((uintptr_t)master | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) & 15) return SWH_E_ARG;
+    if (N == 0) return SWH_OK;
+    const double bc1 = 1.0 - pow((double)beta1, (double)step_count);
+    const double bc2 = 1.0 - pow((double)beta2, (double)step_count);
+    const float step_size = (float)(lr / bc1);
+    const float bc2_sqrt = (float)sqrt(bc2);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const unsigned nb = grid_for((N + 3) / 4);
+    uint16_t *mo = static_cast<uint16_t *>(model_out);
+    if (mo && ((uintptr_t)mo & 7)) return SWH_E_ARG;
+#define SWH_ADAM(GDT, TY, WM)                                                                                     \
+    adamw_kernel<GDT, WM><<<nb, kThreads, 0, s>>>(master, exp_avg, exp_avg_sq, static_cast<const TY *>(grad), mo, N, \
+                                                  lr, beta1, beta2, eps, weight_decay, step_size, bc2_sqrt, clip)
+    if (grad_dtype == SWH_BF16) {
+        if ((uintptr_t)grad & 7) return SWH_E_ARG;
+        if (mo) SWH_ADAM(SWH_BF16, uint16_t, true); else SWH_ADAM(SWH_BF16, uint16_t, false);
+    } else if (grad_dtype == SWH_F32) {
+        if ((uintptr_t)grad & 15) return SWH_E_ARG;
+        if (mo) SWH_ADAM(SWH_F32, float, true); else SWH_ADAM(SWH_F32, float, false);
+    } else {
+        return SWH_E_DTYPE;
+    }
+#undef SWH_ADAM
+    return launch_status();
+}
+
+extern "C" int swh_accumulate(float *dst, const void *src, int dtype, int64_t N, float scale, void *stream) {
+    if (!dst || !src || N < 0) return SWH_E_ARG;
+    if (N == 0) return SWH_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const unsigned nb = grid_for(N);
+    switch (dtype) {
+    case SWH_BF16: accumulate_kernel<SWH_BF16><<<nb, kThreads, 0, s>>>(dst, static_cast<const uint16_t *>(src), N, scale); break;
+    case SWH_F32: accumulate_kernel<SWH_F32><<<nb, kThreads, 0, s>>>(dst, static_cast<const float *>(src), N, scale); break;
+    default: return SWH_E_DTYPE;
+    }
+    return launch_status();
+}

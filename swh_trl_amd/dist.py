@@ -1,0 +1,75 @@
+"""Data-parallel plumbing: one process per GPU, RCCL (torch "nccl") over xGMI.
+
+The reference gets DDP from accelerate (trl/accelerate_configs/multi_gpu.yaml):
+25 MB buckets all-reduced during backward.  Here every gradient is a view
+into one flat bf16 buffer, so the exchange is a handful of large contiguous
+all-reduces (bucket size chosen for per-link xGMI bandwidth, not NVSwitch):
+fewer, larger collectives let RCCL spread each one over all 7 links.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def init_from_env(backend: str | None = None):
+    """Initialise torch.distributed from RANK/WORLD_SIZE/MASTER_* (torchrun).
+    Returns (rank, world_size, local_rank).  No-op for a single process."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend, timeout=datetime.timedelta(minutes=10))
+    return rank, world, local
+
+
+def world_info():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def allreduce_mean_(flat: torch.Tensor, bucket_elems: int = 1 << 27):
+    """In-place mean over ranks of a flat buffer, in contiguous buckets
+    (default 128M elements = 256 MB of bf16)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    world = dist.get_world_size()
+    if world == 1:
+        return
+    backend = dist.get_backend()
+    use_avg = backend == "nccl"
+    works = []
+    n = flat.numel()
+    for s in range(0, n, bucket_elems):
+        chunk = flat[s:min(n, s + bucket_elems)]
+        works.append(dist.all_reduce(chunk, op=dist.ReduceOp.AVG if use_avg else dist.ReduceOp.SUM, async_op=True))
+    for w in works:
+        w.wait()
+    if not use_avg:
+        flat.div_(world)
+
+
+def barrier():
+    if dist.is_available() and dist.is_initialized():
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def all_max(x: float) -> float:
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return x
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

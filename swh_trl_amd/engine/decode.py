@@ -1,0 +1,188 @@
+"""Rollout engine: batched KV-cache generation with a graph-captured decode step.
+
+Replaces the HF `model.generate` loop the reference runs per rollout
+(grpo_trainer.py:1793-1810 -> transformers `_sample`; PPO: utils.py:1059-1128).
+Differences in mechanism, not in result:
+  * static bf16 KV cache [L, 2, B, Hkv, Tmax, D] sized once (288 GB HBM);
+  * the whole decode step — embedding gather, 24 x (RMSNorm, QKV GEMM,
+    RoPE+append+attention kernel, O GEMM, fused residual+RMSNorm, gate/up GEMM,
+    SiLU gate, down GEMM), final norm, lm-head GEMM, sampler, step advance —
+    is captured ONCE into a HIP graph and replayed, with every step-dependent
+    value (step index, prompt width, RNG counter, finished flags) in device
+    memory: no host sync per token (the reference pays one per token in
+    `unfinished_sequences.max()` and B*C more in `.item()` loops);
+  * optional early exit checked every `check_every` tokens.
+Prefill runs the full-sequence forward once over the prompt and writes the
+post-RoPE keys/values into the cache.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+
+from .. import nn_ops, ops
+from .model import CausalLM
+
+
+class DecodeEngine:
+    def __init__(self, model: CausalLM, batch_size: int, max_prompt_len: int, max_new_tokens: int,
+                 use_graph: bool = True):
+        c = model.cfg
+        self.model, self.cfg = model, c
+        self.B, self.Pmax, self.Cmax = batch_size, max_prompt_len, max_new_tokens
+        self.Tmax = max_prompt_len + max_new_tokens
+        dev = model.device
+        self.dev = dev
+        L, Hkv, D = c.num_hidden_layers, c.num_key_value_heads, c.head_dim
+        self.kv = torch.zeros(L, 2, batch_size, Hkv, self.Tmax, D, device=dev, dtype=torch.bfloat16)
+        B, H = batch_size, c.hidden_size
+        bf = dict(device=dev, dtype=torch.bfloat16)
+        self.x = torch.empty(B, H, **bf)          # embedding of the input token
+        self.s = torch.empty(B, H, **bf)          # residual stream
+        self.h = torch.empty(B, H, **bf)          # normed activations
+        self.qkv = torch.empty(B, c.qkv_dim, **bf)
+        self.att = torch.empty(B, c.q_dim, **bf)
+        self.o = torch.empty(B, H, **bf)
+        self.gu = torch.empty(B, 2 * c.intermediate_size, **bf)
+        self.act = torch.empty(B, c.intermediate_size, **bf)
+        self.d = torch.empty(B, H, **bf)
+        self.logits_buf = torch.empty(B, c.vocab_size, **bf)
+        self.state = torch.zeros(2, device=dev, dtype=torch.int32)   # {step, P}
+        self.rng = torch.zeros(2, device=dev, dtype=torch.int64)     # {seed, counter base}
+        self.finished = torch.zeros(B, device=dev, dtype=torch.int32)
+        self.cur = torch.zeros(B, device=dev, dtype=torch.int64)
+        self.out = torch.zeros(B, max_new_tokens, device=dev, dtype=torch.int64)
+        self.out_logp = torch.zeros(B, max_new_tokens, device=dev, dtype=torch.float32)
+        self.plen = torch.zeros(B, device=dev, dtype=torch.int32)
+        self.seen = torch.zeros(B, (c.vocab_size + 31) // 32, device=dev, dtype=torch.int32)
+        self.ws = torch.empty(ops._lib.load().swh_sample_workspace_bytes(B, c.vocab_size), device=dev,
+                              dtype=torch.uint8)
+        self.cos, self.sin = model.rope(self.Tmax + 1)
+        self.use_graph = use_graph and os.environ.get("SWH_DECODE_GRAPH", "1") != "0"
+        self.graph = None
+        self._graph_params = None
+        self.params = ops.make_sample_params()
+        self.want_logp = False
+
+    # ------------------------------------------------------------------ one decode step (capturable)
+    def _step(self):
+        c, m = self.cfg, self.model
+        p = m.p
+        nn_ops.embed_gather(p["embed"], self.cur, self.x)
+        nn_ops.rmsnorm_residual(self.x, None, p["l0.ln_in"], c.rms_norm_eps, y=self.h)
+        self.s.copy_(self.x)
+        for i in range(c.num_hidden_layers):
+            if c.attention_bias:
+                torch.addmm(p[f"l{i}.qkv_b"], self.h, p[f"l{i}.qkv_w"].t(), out=self.qkv)
+            else:
+                torch.mm(self.h, p[f"l{i}.qkv_w"].t(), out=self.qkv)
+            nn_ops.attn_decode(self.qkv, self.kv[i, 0], self.kv[i, 1], self.cos, self.sin, self.plen, self.state,
+                               c.num_attention_heads, c.num_key_value_heads, c.head_dim, c.head_dim ** -0.5,
+                               out=self.att)
+            torch.mm(self.att, p[f"l{i}.o_w"].t(), out=self.o)
+            nn_ops.rmsnorm_residual(self.o, self.s, p[f"l{i}.ln_post"], c.rms_norm_eps, y=self.h, s_out=self.s)
+            torch.mm(self.h, p[f"l{i}.gu_w"].t(), out=self.gu)
+            nn_ops.silu_mul(self.gu, out=self.act)
+            torch.mm(self.act, p[f"l{i}.down_w"].t(), out=self.d)
+            nxt = p[f"l{i + 1}.ln_in"] if i + 1 < c.num_hidden_layers else p["norm"]
+            nn_ops.rmsnorm_residual(self.d, self.s, nxt, c.rms_norm_eps, y=self.h, s_out=self.s)
+        torch.mm(self.h, m.lm_weight().t(), out=self.logits_buf)
+        self._sample()
+        ops.step_advance(self.state[0:1])
+
+    def _sample(self):
+        ops.sample_step(self.logits_buf, self.params, self.rng, self.state[0:1], self.finished, self.out, self.cur,
+                        self.seen if self.params.repetition_penalty != 1.0 else None,
+                        self.out_logp if self.want_logp else None, None, self.ws)
+
+    def _params_key(self):
+        p = self.params
+        return (p.temperature, p.top_p, p.min_p, p.repetition_penalty, p.top_k, p.greedy, p.min_new_tokens,
+                p.pad_token_id, p.n_eos, tuple(p.eos_ids), self.want_logp)
+
+    def _ensure_graph(self):
+        key = self._params_key()
+        if self.graph is not None and self._graph_params == key:
+            return
+        # warm-up outside capture (hipBLASLt heuristics / workspaces), then capture.
+        # The warm-up writes the cache at slot P + step - 1, so it runs on a
+        # scratch copy of the mutable state and restores it afterwards.
+        saved = [t.clone() for t in (self.state, self.finished, self.cur, self.out, self.out_logp, self.seen)]
+        kv_saved = None
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            kv_saved = self.kv.clone()
+            self._step()
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._step()
+        self._graph_params = key
+        for t, v in zip((self.state, self.finished, self.cur, self.out, self.out_logp, self.seen), saved):
+            t.copy_(v)
+        self.kv.copy_(kv_saved)
+        del kv_saved
+
+    # ------------------------------------------------------------------ prefill
+    def _prefill(self, prompt_ids: torch.Tensor, prompt_mask: torch.Tensor):
+        """Full forward over the prompt, K/V into cache slots [0, P), logits of the
+        last position.  Positions follow generate(): cumsum(mask) - 1."""
+        m = self.model
+        P = prompt_ids.shape[1]
+        pos = (prompt_mask.long().cumsum(-1) - 1).clamp(min=0)
+
+        def kv_out(i, k, v):
+            self.kv[i, 0, :, :, :P].copy_(k)
+            self.kv[i, 1, :, :, :P].copy_(v)
+
+        with torch.no_grad():
+            saved = m.grad
+            m.grad = None  # no grad accumulation in prefill
+            try:
+                h = m.hidden_states(prompt_ids, positions=pos, key_mask=prompt_mask, kv_out=kv_out)
+                torch.mm(h[:, -1], m.lm_weight().t(), out=self.logits_buf)
+            finally:
+                m.grad = saved
+
+    # ------------------------------------------------------------------ generate
+    @torch.no_grad()
+    def generate(self, prompt_ids: torch.Tensor, prompt_mask: torch.Tensor, max_new_tokens: int, *,
+                 temperature=1.0, top_p=1.0, top_k=None, min_p=None, repetition_penalty=1.0, greedy=False,
+                 min_new_tokens=0, eos_token_id=None, pad_token_id=None, seed: int = 0, offset: int = 0,
+                 return_logp: bool = False, check_every: int = 0):
+        """prompt_ids [B, P] left-padded (B == engine batch).  Returns completion ids
+        [B, max_new_tokens] (pad after EOS, like `_sample`) and optional per-token
+        log-probs of the drawn tokens under the processed distribution."""
+        B, P = prompt_ids.shape
+        if B != self.B or P > self.Pmax or max_new_tokens > self.Cmax:
+            raise ValueError(f"engine sized for B={self.B}, P<={self.Pmax}, C<={self.Cmax}; got {B}x{P}, "
+                             f"{max_new_tokens}")
+        eos = [] if eos_token_id is None else ([eos_token_id] if isinstance(eos_token_id, int) else list(eos_token_id))
+        self.params = ops.make_sample_params(temperature, top_p, top_k, min_p, repetition_penalty, greedy,
+                                             min_new_tokens, -1 if pad_token_id is None else pad_token_id, eos)
+        self.want_logp = return_logp
+        prompt_mask = prompt_mask.to(torch.int32)
+        self.plen.copy_(prompt_mask.sum(-1).to(torch.int32))
+        self.finished.zero_()
+        self.out.fill_(pad_token_id if pad_token_id is not None else 0)
+        self.rng[0], self.rng[1] = int(seed) & ((1 << 63) - 1), int(offset)
+        if repetition_penalty != 1.0:
+            ops.seen_init(prompt_ids.to(torch.int64), prompt_mask, self.cfg.vocab_size, self.seen)
+        if self.use_graph:
+            self._ensure_graph()
+        self.state[0], self.state[1] = 0, P
+        self._prefill(prompt_ids, prompt_mask)
+        self._sample()                      # token 0 from the prefill logits
+        ops.step_advance(self.state[0:1])
+        for s in range(1, max_new_tokens):
+            if self.use_graph:
+                self.graph.replay()
+            else:
+                self._step()
+            if check_every and s % check_every == 0 and bool(self.finished.all()):
+                break
+        comp = self.out[:, :max_new_tokens]
+        return comp.clone(), (self.out_logp[:, :max_new_tokens].clone() if return_logp else None)

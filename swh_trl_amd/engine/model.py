@@ -1,0 +1,393 @@
+"""Llama-style causal decoder (Qwen2 / Llama-3 families) with flat buffers.
+
+Every weight is a view into ONE bf16 buffer (`flat`), every weight gradient a
+view into ONE bf16 buffer (`grad`): the optimizer is one streaming kernel and
+the data-parallel all-reduce runs on a few large contiguous buckets.  The
+training forward uses autograd, but weight gradients never go through
+AccumulateGrad: the custom Functions below add them straight into the grad
+views with GEMM epilogue accumulation (beta = 1), so there is no extra pass
+and no per-parameter tensor churn.
+
+Semantics follow the transformers modeling code the reference runs
+(third-party; grpo_trainer.py:1249 scoring forward, :1804 generate):
+RMSNorm casts before the weight multiply, residual adds in bf16, SiLU-gated
+MLP, rotate-half RoPE with bf16 cos/sin, GQA attention scaled by D^-0.5.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from .. import nn_ops
+from .._lib import call
+from ..ops import _stream
+from .config import DecoderConfig
+
+_ALIGN = 64  # elements; keeps every view 128-byte aligned
+
+
+class _Linear(torch.autograd.Function):
+    """y = x W^T (+ b); backward returns dx and ACCUMULATES dW (and db) into the
+    flat-gradient views (hipBLASLt addmm with beta = 1)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, gw, gb):
+        ctx.save_for_backward(x, w)
+        ctx.gw, ctx.gb = gw, gb
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx = dy @ w if ctx.needs_input_grad[0] else None
+        if ctx.gw is not None:
+            dy2 = dy.reshape(-1, dy.shape[-1])
+            x2 = x.reshape(-1, x.shape[-1])
+            ctx.gw.addmm_(dy2.t(), x2)
+            if ctx.gb is not None:
+                ctx.gb.add_(dy2.sum(0, dtype=torch.float32).to(ctx.gb.dtype))
+        return dx, None, None, None, None
+
+
+class _Embedding(torch.autograd.Function):
+    """Embedding lookup.  `anchor` is a 0-d tensor with requires_grad=True: the
+    weights themselves are plain tensors (their gradients go to the flat
+    buffer by side effect), so the anchor is what makes autograd record the
+    graph at all."""
+
+    @staticmethod
+    def forward(ctx, ids, table, gtable, anchor):
+        ctx.save_for_backward(ids)
+        ctx.gtable = gtable
+        return F.embedding(ids, table)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (ids,) = ctx.saved_tensors
+        if ctx.gtable is not None:
+            ctx.gtable.index_add_(0, ids.reshape(-1), dy.reshape(-1, dy.shape[-1]))
+        return None, None, None, None
+
+
+class _RMSNorm(torch.autograd.Function):
+    """Fused HIP RMSNorm forward/backward; dw accumulated into the grad view."""
+
+    @staticmethod
+    def forward(ctx, x, w, gw, eps):
+        xc = x.contiguous()
+        H = xc.shape[-1]
+        rows = xc.numel() // H
+        rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+        y, _ = nn_ops.rmsnorm_residual(xc, None, w, eps, rstd=rstd)
+        ctx.save_for_backward(xc, w, rstd)
+        ctx.gw = gw
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, rstd = ctx.saved_tensors
+        H = x.shape[-1]
+        rows = x.numel() // H
+        rpb = 64
+        part = torch.empty((rows + rpb - 1) // rpb, H, device=x.device, dtype=torch.float32)
+        dx = torch.empty_like(x)
+        dyc = dy.contiguous()
+        call("swh_rmsnorm_bwd", x.data_ptr(), w.data_ptr(), rstd.data_ptr(), dyc.data_ptr(), rows, H, dx.data_ptr(),
+             part.data_ptr(), rpb, _stream())
+        if ctx.gw is not None:
+            ctx.gw.add_(part.sum(0).to(ctx.gw.dtype))
+        return dx, None, None, None
+
+
+class _LMHeadLogp(torch.autograd.Function):
+    """lm head GEMM + fused log-prob/entropy, row-chunked.
+
+    Each chunk's logits [rows, V] is a plain 2-D GEMM output kept below 2^30
+    elements (a single [B, C, V] logits tensor passes 2^31 elements at the
+    benchmark shape, beyond what the batched GEMM path indexes).  The chunks
+    stay resident for the backward (HBM is plentiful; no recompute), and the
+    backward overwrites each chunk in place with d logits before the two
+    GEMMs (dh = dlogits W, dW += dlogits^T h)."""
+
+    @staticmethod
+    def forward(ctx, h, w, gw, ids, temperature, compute_entropy, chunk_rows):
+        from .. import ops
+        H = h.shape[-1]
+        h2 = h.reshape(-1, H)
+        if not h2.is_contiguous():
+            h2 = h2.contiguous()
+        idx = ids.reshape(-1)
+        R = h2.shape[0]
+        logp = torch.empty(R, device=h.device, dtype=torch.float32)
+        ent = torch.empty(R, device=h.device, dtype=torch.float32) if compute_entropy else None
+        lse = torch.empty(R, device=h.device, dtype=torch.float32)
+        chunks = []
+        for r0 in range(0, R, chunk_rows):
+            r1 = min(R, r0 + chunk_rows)
+            lg = h2[r0:r1] @ w.t()
+            lp_c, en_c, ls_c = ops.logp_entropy(lg, idx[r0:r1], temperature, compute_entropy)
+            logp[r0:r1] = lp_c
+            lse[r0:r1] = ls_c
+            if compute_entropy:
+                ent[r0:r1] = en_c
+            chunks.append(lg)
+        ctx.chunks, ctx.gw, ctx.temperature, ctx.chunk_rows = chunks, gw, temperature, chunk_rows
+        ctx.hshape = h.shape
+        ctx.save_for_backward(h2, w, idx, lse)
+        shp = ids.shape
+        if ent is not None:
+            ctx.mark_non_differentiable(ent)
+            return logp.view(shp), ent.view(shp)
+        return logp.view(shp), torch.zeros((), device=h.device)
+
+    @staticmethod
+    def backward(ctx, dlogp, dent):
+        from .. import ops
+        h2, w, idx, lse = ctx.saved_tensors
+        g = dlogp.reshape(-1).contiguous()
+        dh = torch.empty_like(h2) if ctx.needs_input_grad[0] else None
+        for k, lg in enumerate(ctx.chunks):
+            r0 = k * ctx.chunk_rows
+            r1 = r0 + lg.shape[0]
+            ops.logp_backward(lg, idx[r0:r1], lse[r0:r1], g[r0:r1], ctx.temperature, out=lg)  # in place
+            if dh is not None:
+                torch.mm(lg, w, out=dh[r0:r1])
+            if ctx.gw is not None:
+                ctx.gw.addmm_(lg.t(), h2[r0:r1])
+        ctx.chunks = None
+        return (dh.view(ctx.hshape) if dh is not None else None), None, None, None, None, None, None
+
+
+def rope_tables(cfg: DecoderConfig, max_pos: int, device) -> tuple[torch.Tensor, torch.Tensor]:
+    """fp32 [max_pos, D/2] cos/sin holding bf16-rounded values (transformers computes
+    them in fp32 and casts to the activation dtype before the multiply)."""
+    D = cfg.head_dim
+    inv = 1.0 / (cfg.rope_theta ** (torch.arange(0, D, 2, dtype=torch.int64).float() / D))
+    pos = torch.arange(max_pos, dtype=torch.float32)
+    fr = torch.outer(pos, inv)
+    return (fr.cos().to(torch.bfloat16).float().to(device).contiguous(),
+            fr.sin().to(torch.bfloat16).float().to(device).contiguous())
+
+
+def _apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """x [B, H, L, D] bf16; cos/sin [B, 1, L, D] bf16 (rotate-half convention)."""
+    h = x.shape[-1] // 2
+    rot = torch.cat((-x[..., h:], x[..., :h]), dim=-1)
+    return x * cos + rot * sin
+
+
+class CausalLM:
+    """Weights + forward passes.  `head` is "lm" (vocabulary logits) or "score"
+    (one scalar per position: the PPO value / reward model head)."""
+
+    def __init__(self, cfg: DecoderConfig, device, head: str = "lm", dtype=torch.bfloat16, seed: Optional[int] = 0,
+                 init_std: float = 0.02, trainable: bool = True):
+        self.cfg, self.device, self.head, self.dtype = cfg, torch.device(device), head, dtype
+        self.layout: dict[str, tuple[int, tuple]] = {}
+        off = 0
+
+        def add(name, *shape):
+            nonlocal off
+            n = 1
+            for s in shape:
+                n *= s
+            self.layout[name] = (off, tuple(shape))
+            off += (n + _ALIGN - 1) // _ALIGN * _ALIGN
+
+        H, I, V = cfg.hidden_size, cfg.intermediate_size, cfg.vocab_size
+        add("embed", V, H)
+        for i in range(cfg.num_hidden_layers):
+            add(f"l{i}.ln_in", H)
+            add(f"l{i}.qkv_w", cfg.qkv_dim, H)
+            if cfg.attention_bias:
+                add(f"l{i}.qkv_b", cfg.qkv_dim)
+            add(f"l{i}.o_w", H, cfg.q_dim)
+            add(f"l{i}.ln_post", H)
+            add(f"l{i}.gu_w", 2 * I, H)
+            add(f"l{i}.down_w", H, I)
+        add("norm", H)
+        if head == "score":
+            add("score", 1, H)
+        elif not cfg.tie_word_embeddings:
+            add("lm_head", V, H)
+        self.numel = off
+        self.flat = torch.zeros(off, device=self.device, dtype=dtype)
+        self.p = {k: self.flat[o:o + math.prod(s)].view(s) for k, (o, s) in self.layout.items()}
+        self.grad: Optional[torch.Tensor] = None
+        self.g: dict[str, torch.Tensor] = {}
+        if seed is not None:
+            self.init_weights(seed, init_std)
+        self._anchor = torch.zeros((), device=self.device, requires_grad=True)
+        if trainable:
+            self.enable_grad_buffer()
+        self._rope = None
+
+    # ------------------------------------------------------------------ weights
+    def init_weights(self, seed: int, std: float = 0.02):
+        g = torch.Generator(device=self.device).manual_seed(seed)
+        for k, t in self.p.items():
+            if k.endswith(("ln_in", "ln_post")) or k == "norm":
+                t.fill_(1.0)
+            elif k.endswith("qkv_b"):
+                t.zero_()
+            else:
+                t.copy_(torch.randn(t.shape, generator=g, device=self.device, dtype=torch.float32).mul_(std))
+
+    def enable_grad_buffer(self):
+        if self.grad is None:
+            self.grad = torch.zeros(self.numel, device=self.device, dtype=self.dtype)
+            self.g = {k: self.grad[o:o + math.prod(s)].view(s) for k, (o, s) in self.layout.items()}
+
+    def zero_grad(self):
+        if self.grad is not None:
+            self.grad.zero_()
+
+    def lm_weight(self) -> torch.Tensor:
+        return self.p["embed"] if (self.cfg.tie_word_embeddings and self.head == "lm") else self.p.get("lm_head")
+
+    def _lm_grad(self):
+        if self.grad is None:
+            return None
+        return self.g["embed"] if (self.cfg.tie_word_embeddings and self.head == "lm") else self.g.get("lm_head")
+
+    def rope(self, max_pos: int):
+        if self._rope is None or self._rope[0].shape[0] < max_pos:
+            n = max(max_pos, 4096)
+            self._rope = rope_tables(self.cfg, n, self.device)
+        return self._rope
+
+    # ------------------------------------------------------------------ HF interop
+    def load_hf_state_dict(self, sd: dict):
+        """Load transformers Qwen2/Llama weights (q/k/v and gate/up are packed here)."""
+        c = self.cfg
+        with torch.no_grad():
+            self.p["embed"].copy_(sd["model.embed_tokens.weight"])
+            for i in range(c.num_hidden_layers):
+                pre = f"model.layers.{i}."
+                self.p[f"l{i}.ln_in"].copy_(sd[pre + "input_layernorm.weight"])
+                self.p[f"l{i}.ln_post"].copy_(sd[pre + "post_attention_layernorm.weight"])
+                self.p[f"l{i}.qkv_w"].copy_(torch.cat([sd[pre + f"self_attn.{n}_proj.weight"] for n in "qkv"], 0))
+                if c.attention_bias:
+                    self.p[f"l{i}.qkv_b"].copy_(torch.cat([sd[pre + f"self_attn.{n}_proj.bias"] for n in "qkv"], 0))
+                self.p[f"l{i}.o_w"].copy_(sd[pre + "self_attn.o_proj.weight"])
+                self.p[f"l{i}.gu_w"].copy_(torch.cat([sd[pre + "mlp.gate_proj.weight"], sd[pre + "mlp.up_proj.weight"]], 0))
+                self.p[f"l{i}.down_w"].copy_(sd[pre + "mlp.down_proj.weight"])
+            self.p["norm"].copy_(sd["model.norm.weight"])
+            if "lm_head" in self.p:
+                self.p["lm_head"].copy_(sd["lm_head.weight"])
+            if "score" in self.p and "score.weight" in sd:
+                self.p["score"].copy_(sd["score.weight"])
+
+    def hf_state_dict(self) -> dict:
+        c, out = self.cfg, {}
+        q, kv = c.q_dim, c.kv_dim
+        out["model.embed_tokens.weight"] = self.p["embed"]
+        for i in range(c.num_hidden_layers):
+            pre = f"model.layers.{i}."
+            out[pre + "input_layernorm.weight"] = self.p[f"l{i}.ln_in"]
+            out[pre + "post_attention_layernorm.weight"] = self.p[f"l{i}.ln_post"]
+            w = self.p[f"l{i}.qkv_w"]
+            out[pre + "self_attn.q_proj.weight"], out[pre + "self_attn.k_proj.weight"], \
+                out[pre + "self_attn.v_proj.weight"] = w[:q], w[q:q + kv], w[q + kv:]
+            if c.attention_bias:
+                b = self.p[f"l{i}.qkv_b"]
+                out[pre + "self_attn.q_proj.bias"], out[pre + "self_attn.k_proj.bias"], \
+                    out[pre + "self_attn.v_proj.bias"] = b[:q], b[q:q + kv], b[q + kv:]
+            out[pre + "self_attn.o_proj.weight"] = self.p[f"l{i}.o_w"]
+            gu = self.p[f"l{i}.gu_w"]
+            out[pre + "mlp.gate_proj.weight"], out[pre + "mlp.up_proj.weight"] = gu[:c.intermediate_size], \
+                gu[c.intermediate_size:]
+            out[pre + "mlp.down_proj.weight"] = self.p[f"l{i}.down_w"]
+        out["model.norm.weight"] = self.p["norm"]
+        if "lm_head" in self.p:
+            out["lm_head.weight"] = self.p["lm_head"]
+        elif self.head == "lm":
+            out["lm_head.weight"] = self.p["embed"]
+        if "score" in self.p:
+            out["score.weight"] = self.p["score"]
+        return out
+
+    def copy_from(self, other: "CausalLM"):
+        with torch.no_grad():
+            self.flat.copy_(other.flat)
+
+    # ------------------------------------------------------------------ full-sequence forward
+    def _gv(self, name):
+        return self.g.get(name) if self.grad is not None else None
+
+    def _layer(self, i: int, x: torch.Tensor, cos, sin, mask, kv_out=None):
+        c = self.cfg
+        B, L, _ = x.shape
+        Hq, Hkv, D = c.num_attention_heads, c.num_key_value_heads, c.head_dim
+        h = _RMSNorm.apply(x, self.p[f"l{i}.ln_in"], self._gv(f"l{i}.ln_in"), c.rms_norm_eps)
+        qkv = _Linear.apply(h, self.p[f"l{i}.qkv_w"], self.p.get(f"l{i}.qkv_b"), self._gv(f"l{i}.qkv_w"),
+                            self._gv(f"l{i}.qkv_b"))
+        q = qkv[..., :c.q_dim].view(B, L, Hq, D).transpose(1, 2)
+        k = qkv[..., c.q_dim:c.q_dim + c.kv_dim].view(B, L, Hkv, D).transpose(1, 2)
+        v = qkv[..., c.q_dim + c.kv_dim:].view(B, L, Hkv, D).transpose(1, 2)
+        q = _apply_rope(q, cos, sin)
+        k = _apply_rope(k, cos, sin)
+        if kv_out is not None:
+            kv_out(i, k, v)
+        rep = Hq // Hkv
+        if rep > 1:
+            k = k.repeat_interleave(rep, dim=1)
+            v = v.repeat_interleave(rep, dim=1)
+        if mask is None:
+            o = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=D ** -0.5)
+        else:
+            o = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, scale=D ** -0.5)
+        o = o.transpose(1, 2).reshape(B, L, c.q_dim)
+        o = _Linear.apply(o, self.p[f"l{i}.o_w"], None, self._gv(f"l{i}.o_w"), None)
+        x = x + o
+        h = _RMSNorm.apply(x, self.p[f"l{i}.ln_post"], self._gv(f"l{i}.ln_post"), c.rms_norm_eps)
+        gu = _Linear.apply(h, self.p[f"l{i}.gu_w"], None, self._gv(f"l{i}.gu_w"), None)
+        a = nn_ops.SiluMulFn.apply(gu)
+        d = _Linear.apply(a, self.p[f"l{i}.down_w"], None, self._gv(f"l{i}.down_w"), None)
+        return x + d
+
+    def hidden_states(self, ids: torch.Tensor, positions: Optional[torch.Tensor] = None,
+                      key_mask: Optional[torch.Tensor] = None, kv_out=None) -> torch.Tensor:
+        """Final-normed hidden states [B, L, H].
+
+        positions: [B, L] (default arange, the transformers training forward);
+        key_mask: [B, L] bool/int, 0 = padding key (left-padded prompts).
+        """
+        c = self.cfg
+        B, L = ids.shape
+        if positions is None:
+            positions = torch.arange(L, device=ids.device).expand(B, L)
+        cos_t, sin_t = self.rope(int(positions.max().item()) + 1 if positions.numel() else 1)
+        pc = positions.clamp(min=0)
+        cos = torch.cat([cos_t[pc], cos_t[pc]], -1).to(self.dtype).unsqueeze(1)
+        sin = torch.cat([sin_t[pc], sin_t[pc]], -1).to(self.dtype).unsqueeze(1)
+        mask = None
+        if key_mask is not None and not bool(key_mask.bool().all()):
+            causal = torch.ones(L, L, device=ids.device, dtype=torch.bool).tril()
+            eye = torch.eye(L, device=ids.device, dtype=torch.bool)
+            mask = (causal & (key_mask.bool()[:, None, None, :] | eye))  # pad queries see themselves
+        x = _Embedding.apply(ids, self.p["embed"], self._gv("embed"), self._anchor)
+        for i in range(c.num_hidden_layers):
+            x = self._layer(i, x, cos, sin, mask, kv_out)
+        return _RMSNorm.apply(x, self.p["norm"], self._gv("norm"), c.rms_norm_eps)
+
+    def logits(self, hidden: torch.Tensor) -> torch.Tensor:
+        """lm head (bf16 logits) on selected hidden states [.., H]."""
+        return _Linear.apply(hidden, self.lm_weight(), None, self._lm_grad(), None)
+
+    def logp_entropy(self, hidden: torch.Tensor, ids: torch.Tensor, temperature: float = 1.0,
+                     compute_entropy: bool = True, chunk_rows: Optional[int] = None):
+        """Per-token log-probs (differentiable, fp32) and entropies (no grad) of
+        `ids` under softmax(lm_head(hidden) / T), chunked over rows."""
+        if chunk_rows is None:
+            chunk_rows = max(1, min(4096, (1 << 30) // self.cfg.vocab_size))
+        lp, ent = _LMHeadLogp.apply(hidden, self.lm_weight(), self._lm_grad(), ids, float(temperature),
+                                    bool(compute_entropy), int(chunk_rows))
+        return lp, (ent if compute_entropy else None)
+
+    def scores(self, hidden: torch.Tensor) -> torch.Tensor:
+        """score head (value / reward), bf16 [..] as the transformers score Linear."""
+        return _Linear.apply(hidden, self.p["score"], None, self._gv("score"), None).squeeze(-1)

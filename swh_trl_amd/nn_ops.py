@@ -1,0 +1,114 @@
+"""Decoder-layer ops on the HIP library (RMSNorm, SiLU gate, embedding gather,
+decode attention), with autograd wrappers for the training forward.
+
+Numerics follow the transformers Qwen2 / Llama bf16 modules the reference
+runs (third-party code reached from grpo_trainer.py:1804 and :1249).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import call
+from .ops import _dev, _p, _stream
+
+
+def rmsnorm_residual(x: torch.Tensor, residual: Optional[torch.Tensor], weight: torch.Tensor, eps: float,
+                     y: Optional[torch.Tensor] = None, s_out: Optional[torch.Tensor] = None,
+                     rstd: Optional[torch.Tensor] = None):
+    """s = x (+ residual, bf16 add); y = bf16(w * bf16(s * rsqrt(mean(s^2)+eps))).
+    Returns (y, s)."""
+    _dev(x, "rmsnorm")
+    H = x.shape[-1]
+    rows = x.numel() // H
+    if y is None:
+        y = torch.empty_like(x)
+    if residual is not None and s_out is None:
+        s_out = torch.empty_like(x)
+    call("swh_rmsnorm_fwd", x.data_ptr(), _p(residual), _p(s_out), weight.data_ptr(), rows, H, float(eps),
+         y.data_ptr(), _p(rstd), _stream())
+    return y, (s_out if residual is not None else x)
+
+
+class RMSNormFn(torch.autograd.Function):
+    """y = RMSNorm(x) * w with the fused HIP forward and backward."""
+
+    @staticmethod
+    def forward(ctx, x, weight, eps):
+        xc = x.contiguous()
+        H = xc.shape[-1]
+        rows = xc.numel() // H
+        rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+        y, _ = rmsnorm_residual(xc, None, weight, eps, rstd=rstd)
+        ctx.save_for_backward(xc, weight, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, rstd = ctx.saved_tensors
+        H = x.shape[-1]
+        rows = x.numel() // H
+        rpb = 64
+        nb = (rows + rpb - 1) // rpb
+        dx = torch.empty_like(x)
+        part = torch.empty(nb, H, device=x.device, dtype=torch.float32)
+        dyc = dy.contiguous()
+        call("swh_rmsnorm_bwd", x.data_ptr(), w.data_ptr(), rstd.data_ptr(), dyc.data_ptr(), rows, H, dx.data_ptr(),
+             part.data_ptr(), rpb, _stream())
+        return dx, part.sum(0).to(w.dtype), None
+
+
+class SiluMulFn(torch.autograd.Function):
+    """out = silu(gu[..., :I]) * gu[..., I:] (gate/up packed by the fused GEMM)."""
+
+    @staticmethod
+    def forward(ctx, gu):
+        guc = gu.contiguous()
+        I2 = guc.shape[-1]
+        rows = guc.numel() // I2
+        out = torch.empty(*guc.shape[:-1], I2 // 2, device=gu.device, dtype=gu.dtype)
+        call("swh_silu_mul_fwd", guc.data_ptr(), rows, I2 // 2, out.data_ptr(), _stream())
+        ctx.save_for_backward(guc)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (gu,) = ctx.saved_tensors
+        I2 = gu.shape[-1]
+        rows = gu.numel() // I2
+        dgu = torch.empty_like(gu)
+        d = dout.contiguous()
+        call("swh_silu_mul_bwd", gu.data_ptr(), d.data_ptr(), rows, I2 // 2, dgu.data_ptr(), _stream())
+        return dgu
+
+
+def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    I2 = gu.shape[-1]
+    rows = gu.numel() // I2
+    if out is None:
+        out = torch.empty(*gu.shape[:-1], I2 // 2, device=gu.device, dtype=gu.dtype)
+    call("swh_silu_mul_fwd", gu.data_ptr(), rows, I2 // 2, out.data_ptr(), _stream())
+    return out
+
+
+def embed_gather(table: torch.Tensor, ids: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    call("swh_embed_gather", table.data_ptr(), ids.data_ptr(), ids.numel(), table.shape[1], out.data_ptr(), _stream())
+    return out
+
+
+def attn_decode(qkv: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, rope_cos: torch.Tensor,
+                rope_sin: torch.Tensor, prompt_len: torch.Tensor, state: torch.Tensor, Hq: int, Hkv: int, D: int,
+                scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One decode step of GQA attention with in-kernel RoPE and KV append.
+    k_cache / v_cache: [B, Hkv, Tmax, D] bf16 (one layer)."""
+    _dev(qkv, "attn_decode")
+    B = qkv.shape[0]
+    Tmax = k_cache.shape[2]
+    if out is None:
+        out = torch.empty(B, Hq * D, device=qkv.device, dtype=qkv.dtype)
+    call("swh_attn_decode", qkv.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), rope_cos.data_ptr(),
+         rope_sin.data_ptr(), prompt_len.data_ptr(), state.data_ptr(), B, Hq, Hkv, D, Tmax, float(scale),
+         out.data_ptr(), _stream())
+    return out

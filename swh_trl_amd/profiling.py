@@ -1,0 +1,48 @@
+"""Live per-kernel timing with HIP events (torch.cuda.Event records on the
+same stream the C-ABI kernels are launched on).  Off by default; bench.py
+switches it on for the timed region.  Replaces the reference's wall-clock
+`profiling_context` (trl/extras/profiling.py:31-100) for device work."""
+from __future__ import annotations
+
+from collections import defaultdict
+from contextlib import contextmanager
+
+import torch
+
+_enabled = False
+_events: dict[str, list] = defaultdict(list)
+_bytes: dict[str, float] = defaultdict(float)
+
+
+def enable(on: bool = True):
+    global _enabled
+    _enabled = on
+
+
+def reset():
+    _events.clear()
+    _bytes.clear()
+
+
+@contextmanager
+def kernel(name: str, nbytes: float = 0.0):
+    if not _enabled:
+        yield
+        return
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    yield
+    e.record()
+    _events[name].append((s, e))
+    _bytes[name] += nbytes
+
+
+def summary() -> dict:
+    """{name: {launches, total_ms, avg_us, bytes_per_launch}} (synchronises)."""
+    torch.cuda.synchronize()
+    out = {}
+    for k, ev in _events.items():
+        tot = sum(s.elapsed_time(e) for s, e in ev)
+        out[k] = {"launches": len(ev), "total_ms": tot, "avg_us": 1000.0 * tot / max(1, len(ev)),
+                  "bytes_per_launch": _bytes[k] / max(1, len(ev))}
+    return out

@@ -1,0 +1,468 @@
+"""GRPOTrainer — drop-in for trl.GRPOTrainer's per-step loop on MI355X.
+
+Constructor and config keep the reference's names (grpo_trainer.py:558-569,
+grpo_config.py); the loop keeps its semantics (grpo_trainer.py:1411-1444
+buffering, :1500-2003 rollout + scoring, :2058-2175 loss) while every
+per-token stage runs on the HIP engine:
+
+  rollout      DecodeEngine.generate        (graph-captured decode, device sampler)
+  mask         ops.completion_mask          (:1812-1831)
+  rewards      user callables on host       (:1446-1498, unchanged contract)
+  advantages   ops.group_advantages         (:1914-1930)
+  scoring      CausalLM forward -> lm head -> fused logp/entropy kernel
+  loss         fused GRPO loss fwd+bwd kernel (all GA micro-batches in one pass)
+  optimizer    flat-buffer AdamW + device grad-norm clip, RCCL all-reduce for DP
+
+Fork-only additions of the reference (unsloth loading, CrossEncoder, private
+validation JSON, OpenAI client) are not part of the drop-in.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from collections import defaultdict
+from typing import Any, Callable, Optional, Union
+
+import torch
+
+from .. import dist as swh_dist
+from .. import ops
+from ..engine.config import DecoderConfig, PRESETS, from_hf_config
+from ..engine.decode import DecodeEngine
+from ..engine.model import CausalLM
+from ..optim import FlatAdamW
+from .grpo_config import GRPOConfig
+from .utils import RepeatSampler, left_pad, linear_lr, pad_left_cat, split_tensor_dict, \
+    truncate_with_protected_tokens
+
+RewardFunc = Union[str, Callable, torch.nn.Module]
+_TRACE = os.environ.get("SWH_TRACE", "0") == "1"
+_T0 = [time.time()]
+
+
+def _trace(msg: str):
+    """SWH_TRACE=1: synchronised phase timings on stderr (diagnostics only)."""
+    if _TRACE:
+        torch.cuda.synchronize()
+        import sys
+        now = time.time()
+        print(f"[swh {now - _T0[0]:8.3f}s] {msg}", file=sys.stderr, flush=True)
+
+
+class TrainerState:
+    """The fields of transformers.TrainerState the loop and reward functions read."""
+
+    def __init__(self):
+        self.global_step = 0
+        self.epoch = 0.0
+        self.max_steps = 0
+        self.num_input_tokens_seen = 0
+        self.log_history: list[dict] = []
+
+
+def load_model(model, device, trainable=True, seed=0) -> CausalLM:
+    """`model` may be a CausalLM, a preset name ("qwen2.5-0.5b", "llama-3-8b",
+    "tiny"), a DecoderConfig (random init), a local directory holding a
+    transformers config.json + safetensors, or a transformers PreTrainedModel."""
+    if isinstance(model, CausalLM):
+        return model
+    if isinstance(model, DecoderConfig):
+        return CausalLM(model, device, seed=seed, trainable=trainable)
+    if isinstance(model, str):
+        if model in PRESETS:
+            return CausalLM(PRESETS[model](), device, seed=seed, trainable=trainable)
+        if os.path.isdir(model):
+            import json
+
+            from safetensors.torch import load_file
+            with open(os.path.join(model, "config.json")) as f:
+                cfg = from_hf_config(json.load(f))
+            m = CausalLM(cfg, device, seed=None, trainable=trainable)
+            sd = {}
+            for fn in sorted(os.listdir(model)):
+                if fn.endswith(".safetensors"):
+                    sd.update(load_file(os.path.join(model, fn), device=str(device)))
+            m.load_hf_state_dict(sd)
+            return m
+        raise ValueError(f"cannot load model {model!r}: no hub access; pass a preset, a local directory or a "
+                         "model object")
+    if hasattr(model, "config") and hasattr(model, "state_dict"):
+        cfg = from_hf_config(model.config)
+        m = CausalLM(cfg, device, seed=None, trainable=trainable)
+        m.load_hf_state_dict({k: v.to(device) for k, v in model.state_dict().items()})
+        return m
+    raise TypeError(f"unsupported model type {type(model)}")
+
+
+class GRPOTrainer:
+    _tag_names = ["trl", "grpo"]
+
+    def __init__(self, model, reward_funcs: Union[RewardFunc, list], args: Optional[GRPOConfig] = None,
+                 train_dataset=None, eval_dataset=None, processing_class=None, reward_processing_classes=None,
+                 callbacks=None, optimizers=(None, None), peft_config=None):
+        if peft_config is not None:
+            raise ValueError("peft_config: LoRA training is not part of the MI355X engine's scope")
+        self.args = args if args is not None else GRPOConfig(output_dir="grpo-out")
+        a = self.args
+        self.rank, self.world, self.local_rank = swh_dist.init_from_env()
+        if not torch.cuda.is_available():
+            raise RuntimeError("GRPOTrainer runs the MI355X engine and needs a ROCm device (no CPU fallback)")
+        self.device = torch.device("cuda", self.local_rank)
+        torch.cuda.set_device(self.device)
+        torch.manual_seed(a.seed)
+        self.model = load_model(model, self.device, trainable=True, seed=a.seed)
+        self.processing_class = processing_class
+        if not isinstance(reward_funcs, list):
+            reward_funcs = [reward_funcs]
+        self.reward_funcs = reward_funcs
+        self.reward_func_names = [getattr(f, "__name__", None) or type(f).__name__ for f in reward_funcs]
+        self.reward_processing_classes = reward_processing_classes or [None] * len(reward_funcs)
+        if a.reward_weights is not None:
+            if len(a.reward_weights) != len(reward_funcs):
+                raise ValueError(f"Number of reward weights ({len(a.reward_weights)}) must match number of reward "
+                                 f"functions ({len(reward_funcs)})")
+            self.reward_weights = torch.tensor(a.reward_weights, dtype=torch.float32, device=self.device)
+        else:
+            self.reward_weights = torch.ones(len(reward_funcs), dtype=torch.float32, device=self.device)
+        self.train_dataset, self.eval_dataset = train_dataset, eval_dataset
+        self.num_generations = a.num_generations
+        self.temperature = a.temperature
+        self.beta = a.beta
+        self.epsilon_low = a.epsilon
+        self.epsilon_high = a.epsilon_high if a.epsilon_high is not None else a.epsilon
+        self.num_iterations = a.num_iterations
+        self.loss_type = a.loss_type
+        self.scale_rewards = a.scale_rewards
+        self.importance_sampling_level = a.importance_sampling_level
+        self.mask_truncated_completions = a.mask_truncated_completions
+        self.top_entropy_quantile = a.top_entropy_quantile
+        self.max_prompt_length = a.max_prompt_length
+        self.max_completion_length = a.max_completion_length
+        tok = processing_class
+        self.pad_token_id = getattr(tok, "pad_token_id", None)
+        self.eos_token_id = getattr(tok, "eos_token_id", None)
+        gk = dict(a.generation_kwargs or {})
+        if "pad_token_id" in gk:
+            self.pad_token_id = gk["pad_token_id"]
+        if "eos_token_id" in gk:
+            self.eos_token_id = gk["eos_token_id"]
+        if self.pad_token_id is None:
+            self.pad_token_id = self.eos_token_id if self.eos_token_id is not None else 0
+        self.gen_kwargs = dict(temperature=a.temperature, top_p=a.top_p, top_k=a.top_k, min_p=a.min_p,
+                               repetition_penalty=a.repetition_penalty, greedy=not gk.get("do_sample", True),
+                               min_new_tokens=int(gk.get("min_new_tokens", 0) or 0))
+        self.ref_model = None
+        if self.beta != 0.0:
+            self.ref_model = CausalLM(self.model.cfg, self.device, seed=None, trainable=False)
+            self.ref_model.copy_from(self.model)
+        self.optimizer = FlatAdamW(self.model.numel, self.device, lr=a.learning_rate,
+                                   betas=(a.adam_beta1, a.adam_beta2), eps=a.adam_epsilon,
+                                   weight_decay=a.weight_decay, max_grad_norm=a.max_grad_norm)
+        self.optimizer.master.copy_(self.model.flat.float())
+        self.state = TrainerState()
+        self._step = 0
+        self._buffered_inputs = None
+        self._metrics = {"train": defaultdict(list), "eval": defaultdict(list)}
+        self._engine: Optional[DecodeEngine] = None
+        self._gen_count = 0
+        self._shuffle_gen = torch.Generator().manual_seed(a.seed + 17 * self.rank)
+        self._batches = None
+        self.callbacks = callbacks or []
+
+    # ------------------------------------------------------------------ data
+    def _local_gen_batch_size(self) -> int:
+        return self.args.per_device_train_batch_size * self.args.steps_per_generation
+
+    def _generation_batches(self):
+        """RepeatSampler stream (grpo_trainer.py:1096-1130) → this rank's slice of
+        every global generation batch (repeats collapsed: the loop regenerates
+        only once per steps_per_generation*num_iterations micro-steps)."""
+        a = self.args
+        ds = self.train_dataset
+        gbs = a.generation_batch_size
+        while True:
+            sampler = RepeatSampler(ds, mini_repeat_count=self.num_generations,
+                                    batch_size=gbs // self.num_generations, repeat_count=1,
+                                    shuffle=bool(a.shuffle_dataset), seed=a.seed)
+            idx = list(sampler)
+            local = self._local_gen_batch_size()
+            for s in range(0, len(idx) - gbs + 1, gbs):
+                mine = idx[s + self.rank * local:s + (self.rank + 1) * local]
+                yield [ds[i] for i in mine]
+            self.state.epoch += 1
+
+    def _tokenize_prompts(self, examples):
+        if "prompt_ids" in examples[0]:
+            ids, mask = left_pad([list(x["prompt_ids"]) for x in examples], self.pad_token_id, self.device)
+            texts = [x.get("prompt") for x in examples]
+        else:
+            tok = self.processing_class
+            if tok is None:
+                raise ValueError("text prompts need a processing_class (tokenizer)")
+            texts = []
+            for x in examples:
+                p = x["prompt"]
+                if isinstance(p, list) and hasattr(tok, "apply_chat_template"):
+                    p = tok.apply_chat_template(p, tokenize=False, add_generation_prompt=True)
+                texts.append(p)
+            enc = tok(text=texts, return_tensors="pt", padding=True, padding_side="left", add_special_tokens=False)
+            ids, mask = enc["input_ids"].to(self.device), enc["attention_mask"].to(self.device).int()
+        if self.max_prompt_length is not None and ids.shape[1] > self.max_prompt_length:
+            ids, mask = truncate_with_protected_tokens(ids, mask, self.max_prompt_length, [])
+        return ids, mask, texts
+
+    def _engine_for(self, B: int, P: int) -> DecodeEngine:
+        C = self.max_completion_length
+        e = self._engine
+        if e is None or e.B != B or e.Pmax < P:
+            Pmax = max(P, self.max_prompt_length or P) if (self.max_prompt_length or 0) <= 4096 else P
+            self._engine = DecodeEngine(self.model, B, Pmax, C)
+        return self._engine
+
+    # ------------------------------------------------------------------ rollout + scoring
+    @torch.no_grad()
+    def _generate_and_score_completions(self, examples: list[dict]) -> dict:
+        a = self.args
+        prompt_ids, prompt_mask, prompts_text = self._tokenize_prompts(examples)
+        B, P = prompt_ids.shape
+        _trace(f"prompts tokenized {B}x{P}")
+        eng = self._engine_for(B, P)
+        seed = a.seed * 1_000_003 + self.rank
+        completion_ids, _ = eng.generate(prompt_ids, prompt_mask, self.max_completion_length,
+                                         eos_token_id=self.eos_token_id, pad_token_id=self.pad_token_id,
+                                         seed=seed, offset=self._gen_count * (self.max_completion_length + 1),
+                                         check_every=a.decode_check_every, **self.gen_kwargs)
+        self._gen_count += 1
+        _trace("generated")
+        eos = [] if self.eos_token_id is None else self.eos_token_id
+        completion_mask, lengths, has_eos = ops.completion_mask(completion_ids, eos,
+                                                                self.mask_truncated_completions)
+        rewards_per_func = self._calculate_rewards(examples, prompts_text, prompt_ids, prompt_mask, completion_ids,
+                                                   completion_mask)
+        _trace("rewards")
+        adv, rewards, gmean, gstd, zstd = ops.group_advantages(rewards_per_func, self.reward_weights,
+                                                               self.num_generations, self.scale_rewards)
+        out = {"prompt_ids": prompt_ids, "prompt_mask": prompt_mask, "completion_ids": completion_ids,
+               "completion_mask": completion_mask, "advantages": adv}
+        generate_every = a.steps_per_generation * self.num_iterations
+        if a.gradient_accumulation_steps % generate_every != 0:
+            out["old_per_token_logps"] = self._score_logps(self.model, out)
+        if self.beta != 0.0:
+            out["ref_per_token_logps"] = self._score_logps(self.ref_model, out)
+        m = self._metrics["train"]
+        m["_lengths"].append(lengths.float())
+        m["_rewards"].append(gmean)
+        m["_reward_std"].append(gstd)
+        m["_zero_std"].append(zstd.float())
+        m["_rpf"].append(rewards_per_func)
+        self.state.num_input_tokens_seen += int(B * P + B * self.max_completion_length) * self.world
+        return out
+
+    def _calculate_rewards(self, examples, prompts_text, prompt_ids, prompt_mask, completion_ids, completion_mask):
+        """grpo_trainer.py:1446-1498: reward callables on host (None -> NaN)."""
+        B = completion_ids.shape[0]
+        F = len(self.reward_funcs)
+        rpf = torch.zeros(B, F, dtype=torch.float32)
+        ids_h = completion_ids.cpu()
+        mask_h = completion_mask.cpu().bool()
+        completion_ids_list = [row[m].tolist() for row, m in zip(ids_h, mask_h)]
+        tok = self.processing_class
+        if tok is not None and hasattr(tok, "batch_decode"):
+            completions = tok.batch_decode(ids_h, skip_special_tokens=True)
+        else:
+            completions = completion_ids_list
+        prompts = [x.get("prompt") for x in examples]
+        keys = [k for k in examples[0] if k not in ("prompt", "completion", "completion_ids")]
+        kw = {k: [x[k] for x in examples] for k in keys}
+        kw["trainer_state"] = self.state
+        for i, (fn, rtok) in enumerate(zip(self.reward_funcs, self.reward_processing_classes)):
+            if isinstance(fn, torch.nn.Module):
+                texts = [str(p) + str(c) for p, c in zip(prompts, completions)]
+                enc = rtok(text=texts, return_tensors="pt", padding=True, padding_side="right",
+                           add_special_tokens=False)
+                enc = {k: v.to(self.device) for k, v in enc.items()}
+                with torch.inference_mode():
+                    rpf[:, i] = fn(**enc).logits[:, 0].float().cpu()
+            else:
+                vals = fn(prompts=prompts, completions=completions, completion_ids=completion_ids_list, **kw)
+                rpf[:, i] = torch.tensor([float("nan") if v is None else float(v) for v in vals],
+                                         dtype=torch.float32)
+        return rpf.to(self.device)
+
+    # ------------------------------------------------------------------ scoring forward
+    def _completion_logps(self, model: CausalLM, batch: dict, compute_entropy: bool):
+        """grpo_trainer.py:1205-1272: forward over prompt+completion with
+        logits_to_keep=C+1, drop the last position, /T, selective_log_softmax
+        and entropy_from_logits — lm head + log-prob + entropy fused and
+        row-chunked (engine/model.py `_LMHeadLogp`)."""
+        ids = torch.cat([batch["prompt_ids"], batch["completion_ids"]], 1)
+        P = batch["prompt_ids"].shape[1]
+        C = batch["completion_ids"].shape[1]
+        key_mask = torch.cat([batch["prompt_mask"], torch.ones_like(batch["completion_ids"], dtype=torch.int32)], 1)
+        h = model.hidden_states(ids, key_mask=key_mask)
+        return model.logp_entropy(h[:, P - 1:P + C - 1], batch["completion_ids"], self.temperature, compute_entropy)
+
+    @torch.no_grad()
+    def _score_logps(self, model: CausalLM, batch: dict) -> torch.Tensor:
+        saved, model.grad = model.grad, None
+        try:
+            lp, _ = self._completion_logps(model, batch, False)
+        finally:
+            model.grad = saved
+        return lp
+
+    # ------------------------------------------------------------------ loss over fused micro-batches
+    def _loss_backward(self, micro: list[dict]) -> dict:
+        """One forward/backward over the given micro-batches.  Segment j keeps
+        micro-batch j's own normaliser (bnpo tokens / grpo rows), every row is
+        scaled by 1/GA as the Trainer's loss division — the gradient equals the
+        reference's GA separate backward passes."""
+        a = self.args
+        GA = a.gradient_accumulation_steps
+        R_each = [m["completion_ids"].shape[0] for m in micro]
+        batch = {
+            "prompt_ids": pad_left_cat([m["prompt_ids"] for m in micro], self.pad_token_id),
+            "prompt_mask": pad_left_cat([m["prompt_mask"] for m in micro], 0),
+            "completion_ids": torch.cat([m["completion_ids"] for m in micro]),
+            "completion_mask": torch.cat([m["completion_mask"] for m in micro]),
+            "advantages": torch.cat([m["advantages"] for m in micro]),
+        }
+        for k in ("old_per_token_logps", "ref_per_token_logps"):
+            if k in micro[0]:
+                batch[k] = torch.cat([m[k] for m in micro])
+        seg = torch.cat([torch.full((r,), j, dtype=torch.int32) for j, r in enumerate(R_each)]).to(self.device)
+        R = seg.numel()
+        row_scale = torch.full((R,), 1.0 / GA, device=self.device)
+        _trace("loss inputs ready")
+        logp, ent = self._completion_logps(self.model, batch, True)
+        _trace("policy forward + lm head + logp/entropy")
+        emask = None
+        if self.top_entropy_quantile < 1.0:
+            emask = torch.zeros_like(batch["completion_mask"], dtype=torch.bool)
+            from .utils import get_high_entropy_mask
+            for j in range(len(micro)):
+                sl = seg == j
+                emask[sl] = get_high_entropy_mask(ent[sl], batch["completion_mask"][sl], 1 - self.top_entropy_quantile)
+        loss, metrics = ops.grpo_loss(
+            logp, batch["advantages"], batch["completion_mask"],
+            old_per_token_logps=batch.get("old_per_token_logps"), ref_per_token_logps=batch.get("ref_per_token_logps"),
+            entropy_mask=emask, entropies=ent, row_scale=row_scale, segments=seg, num_segments=len(micro),
+            beta=self.beta, epsilon_low=self.epsilon_low, epsilon_high=self.epsilon_high, delta=a.delta,
+            loss_type=self.loss_type, importance_sampling_level=self.importance_sampling_level,
+            max_completion_length=self.max_completion_length)
+        _trace("loss")
+        loss.backward()
+        _trace("backward")
+        return {"loss": loss.detach(), "metrics": metrics}
+
+    # ------------------------------------------------------------------ the loop
+    def _next_micro_batch(self) -> dict:
+        """grpo_trainer.py:1411-1444 (_prepare_inputs, train mode)."""
+        a = self.args
+        generate_every = a.steps_per_generation * self.num_iterations
+        if self._step % generate_every == 0 or self._buffered_inputs is None:
+            if self._batches is None:
+                self._batches = self._generation_batches()
+            gen = self._generate_and_score_completions(next(self._batches))
+            n = gen["completion_ids"].shape[0]
+            perm = torch.randperm(n, generator=self._shuffle_gen).to(self.device)
+            gen = {k: v[perm] for k, v in gen.items()}
+            self._buffered_inputs = split_tensor_dict(gen, a.steps_per_generation)
+        inputs = self._buffered_inputs[self._step % a.steps_per_generation]
+        self._step += 1
+        return inputs
+
+    def training_step_group(self) -> dict:
+        """One optimizer step: GA micro-batches (fused), DP all-reduce, clip, AdamW."""
+        a = self.args
+        GA = a.gradient_accumulation_steps
+        self.model.zero_grad()
+        micro = [self._next_micro_batch() for _ in range(GA)]
+        outs = []
+        tokens = sum(m["completion_ids"].shape[0] * (m["prompt_ids"].shape[1] + m["completion_ids"].shape[1])
+                     for m in micro)
+        if a.fuse_micro_batches and tokens <= a.fuse_token_budget:
+            outs.append(self._loss_backward(micro))
+        else:
+            for m in micro:  # the reference schedule, one pass per micro-batch
+                o = self._loss_backward([m])
+                outs.append(o)
+        if self.world > 1:
+            swh_dist.allreduce_mean_(self.model.grad)
+        total = max(1, self.state.max_steps)
+        lr = linear_lr(self.state.global_step, total, a.learning_rate, a.warmup_steps) \
+            if a.lr_scheduler_type == "linear" else a.learning_rate
+        norm = self.optimizer.step(self.model.grad, model_out=self.model.flat, lr=lr)
+        self.state.global_step += 1
+        _trace(f"optimizer step {self.state.global_step}")
+        if self.ref_model is not None and a.sync_ref_model and self.state.global_step % a.ref_model_sync_steps == 0:
+            # TR-DPO mixup (callbacks.py:106-131): ref = alpha * policy + (1 - alpha) * ref
+            self.ref_model.flat.mul_(1 - a.ref_model_mixup_alpha).add_(self.model.flat, alpha=a.ref_model_mixup_alpha)
+        loss = sum(o["loss"] for o in outs) if len(outs) > 1 else outs[0]["loss"]
+        if len(outs) > 1:
+            loss = loss  # per-micro losses already carry the 1/GA row scale
+        met = sum(o["metrics"] for o in outs)
+        m = self._metrics["train"]
+        m["_loss"].append(loss)
+        m["_met"].append(met)
+        m["_grad_norm"].append(norm.clone())
+        m["_lr"].append(torch.tensor(lr))
+        return {"loss": loss, "grad_norm": norm}
+
+    def _flush_logs(self) -> dict:
+        """Average the device-side metric buffers (one host sync per log)."""
+        m = self._metrics["train"]
+        if not m.get("_loss"):
+            return {}
+        met = torch.stack(m["_met"]).sum(0).cpu()
+        tok = max(float(met[0]), 1.0)
+        lengths = torch.cat(m["_lengths"]).cpu()
+        log = {
+            "loss": float(torch.stack(m["_loss"]).mean()),
+            "grad_norm": float(torch.stack(m["_grad_norm"]).mean()),
+            "learning_rate": float(m["_lr"][-1]),
+            "num_tokens": self.state.num_input_tokens_seen,
+            "completions/mean_length": float(lengths.mean()),
+            "completions/min_length": float(lengths.min()),
+            "completions/max_length": float(lengths.max()),
+            "reward": float(torch.cat(m["_rewards"]).mean()) if m["_rewards"] else float("nan"),
+            "reward_std": float(torch.cat(m["_reward_std"]).mean()) if m["_reward_std"] else float("nan"),
+            "frac_reward_zero_std": float(torch.cat(m["_zero_std"]).mean()) if m["_zero_std"] else float("nan"),
+            "entropy": float(met[2]) / tok,
+            "clip_ratio/low_mean": float(met[3]) / tok,
+            "clip_ratio/high_mean": float(met[4]) / tok,
+            "clip_ratio/region_mean": float(met[5]) / tok,
+            "step": self.state.global_step,
+        }
+        if self.beta != 0.0:
+            log["kl"] = float(met[1]) / tok
+        if m["_rpf"]:
+            rpf = torch.cat(m["_rpf"]).cpu()
+            for i, name in enumerate(self.reward_func_names):
+                log[f"rewards/{name}/mean"] = float(torch.nanmean(rpf[:, i]))
+        m.clear()
+        self.state.log_history.append(log)
+        return log
+
+    def train(self, resume_from_checkpoint=None):
+        a = self.args
+        if self.train_dataset is None:
+            raise ValueError("train_dataset is required")
+        if a.max_steps and a.max_steps > 0:
+            total = a.max_steps
+        else:
+            per_epoch = len(self.train_dataset) // (a.generation_batch_size // self.num_generations)
+            total = max(1, int(math.ceil(per_epoch * a.steps_per_generation * self.num_iterations
+                                         / a.gradient_accumulation_steps * a.num_train_epochs)))
+        self.state.max_steps = total
+        log_every = int(a.logging_steps) if a.logging_steps >= 1 else max(1, int(total * a.logging_steps))
+        t0 = time.time()
+        for _ in range(total):
+            self.training_step_group()
+            if self.state.global_step % log_every == 0 or self.state.global_step == total:
+                log = self._flush_logs()
+                log["train_runtime"] = time.time() - t0
+                if self.rank == 0:
+                    print(log, flush=True)
+        return self.state

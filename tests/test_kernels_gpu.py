@@ -1,0 +1,544 @@
+"""Parity of every HIP kernel with the CPU oracle (run on an MI355X: -m gpu).
+
+Tolerances are written per test: bit-exact for integer/index work, the
+reference's own tolerances (1e-5, tests/test_utils.py:540-640) for fp32, and
+stated bounds for bf16 results.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import hf_sampling, trl_ref
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from swh_trl_amd import ops as _ops
+    from swh_trl_amd import _lib
+    _lib.load()
+    return _ops
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available()
+    return torch.device("cuda:0")
+
+
+def _gen(seed):
+    return torch.Generator().manual_seed(seed)
+
+
+# --------------------------------------------------------------------------- logp / entropy
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+def test_logp_entropy_reference_shape(ops, dev, dtype):
+    g = _gen(0)
+    logits = torch.randn(4, 32, 1024, generator=g).to(dtype)
+    ids = torch.randint(0, 1024, (4, 32), generator=g)
+    logp, ent, lse = ops.logp_entropy(logits.to(dev), ids.to(dev))
+    ref_lp = trl_ref.selective_log_softmax(logits.double(), ids)
+    ref_ent = trl_ref.entropy_from_logits(logits.double())
+    torch.testing.assert_close(logp.cpu().double(), ref_lp, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(ent.cpu().double(), ref_ent, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(lse.cpu().double(), torch.logsumexp(logits.double(), -1), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_selective_log_softmax_lowp_matches_torch(ops, dev, dtype):
+    """Reference test_utils.py:540-558 asks bf16/fp16 outputs to equal
+    gather(log_softmax) bit-for-bit.  The fused kernel reassociates the fp32
+    sum, so the bound here is: >= 99.9% bit-identical, the rest 1 ulp."""
+    g = _gen(1)
+    logits = torch.randn(4, 32, 1024, generator=g).to(dtype).to(dev)
+    ids = torch.randint(0, 1024, (4, 32), generator=g).to(dev)
+    got = ops.selective_log_softmax(logits, ids)
+    exp = torch.gather(logits.log_softmax(-1), -1, ids.unsqueeze(-1)).squeeze(-1)
+    assert got.dtype == dtype
+    same = (got == exp).float().mean().item()
+    assert same >= 0.999, same
+    ulp = (got.float() - exp.float()).abs() / exp.float().abs().clamp_min(1e-3)
+    assert (ulp <= 2 ** -7).all()
+
+
+@pytest.mark.parametrize("chunk", [1, 16])
+def test_entropy_reference_shape(ops, dev, chunk):
+    g = _gen(2)
+    logits = torch.randn(64, 384, 768, generator=g)
+    got = ops.entropy_from_logits(logits.to(dev), chunk_size=chunk)
+    p = logits.double().softmax(-1)
+    exp = -(p * p.log()).sum(-1)
+    torch.testing.assert_close(got.cpu().double(), exp, rtol=1e-5, atol=1e-5)
+
+
+def test_logp_full_vocab_strided_temperature(ops, dev):
+    """Qwen2.5 vocabulary, the [:, -C-1:-1] slice of a [B, L, V] bf16 tensor, T=0.7."""
+    g = _gen(3)
+    V, B, L, Cc = 151936, 2, 70, 64
+    logits = (torch.randn(B, L, V, generator=g) * 3).to(torch.bfloat16)
+    ids = torch.randint(0, V, (B, Cc), generator=g)
+    sl = logits.to(dev)[:, -Cc - 1:-1]
+    logp, ent, lse = ops.logp_entropy(sl, ids.to(dev), temperature=0.7)
+    z = logits[:, -Cc - 1:-1].double() / 0.7
+    torch.testing.assert_close(logp.cpu().double(), trl_ref.selective_log_softmax(z, ids), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(ent.cpu().double(), trl_ref.entropy_from_logits(z), rtol=1e-5, atol=2e-5)
+
+
+def test_logp_round_scaled_matches_bf16_division(ops, dev):
+    g = _gen(4)
+    logits = (torch.randn(3, 16, 4096, generator=g) * 2).to(torch.bfloat16)
+    ids = torch.randint(0, 4096, (3, 16), generator=g)
+    logp, _, _ = ops.logp_entropy(logits.to(dev), ids.to(dev), temperature=0.9, round_scaled=True)
+    z = (logits / 0.9)  # bf16 division, as the reference's `logits / self.temperature`
+    torch.testing.assert_close(logp.cpu().double(), trl_ref.selective_log_softmax(z.double(), ids),
+                               rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_logp_backward_matches_autograd(ops, dev, dtype):
+    g = _gen(5)
+    logits = torch.randn(2, 24, 3000, generator=g).to(dtype)
+    ids = torch.randint(0, 3000, (2, 24), generator=g)
+    w = torch.randn(2, 24, generator=g)
+    x = logits.double().requires_grad_(True)
+    (trl_ref.selective_log_softmax(x / 0.8, ids) * w).sum().backward()
+    xl = logits.to(dev).requires_grad_(True)
+    lp, _ = ops.logp_entropy_autograd(xl, ids.to(dev), temperature=0.8)
+    (lp * w.to(dev)).sum().backward()
+    tol = 1e-6 if dtype == torch.float32 else 4e-3
+    torch.testing.assert_close(xl.grad.cpu().double(), x.grad, rtol=tol, atol=tol)
+
+
+def test_logp_edge_rows(ops, dev):
+    """-inf entries (masked vocab), a one-hot row, V not a multiple of 8, unaligned base."""
+    V = 1003
+    logits = torch.randn(4, V + 1)
+    logits[0, 5:] = float("-inf")
+    logits[1, :] = -1e4
+    logits[1, 7] = 10.0
+    base = logits.to(dev)[:, 1:]  # 4-byte misaligned rows
+    ids = torch.tensor([3, 7, 0, V - 1])
+    logp, ent, _ = ops.logp_entropy(base, ids.to(dev))
+    ref = trl_ref.selective_log_softmax(logits[:, 1:].double(), ids)
+    torch.testing.assert_close(logp.cpu().double(), ref, rtol=1e-5, atol=1e-5)
+    lp = torch.log_softmax(logits[:, 1:].double(), -1)
+    ent_ref = -(lp.exp() * lp.nan_to_num(neginf=0.0)).sum(-1)
+    torch.testing.assert_close(ent.cpu().double(), ent_ref, rtol=1e-5, atol=1e-5)
+
+
+# --------------------------------------------------------------------------- completion mask / advantages
+def test_completion_mask_mock_kat(ops, dev):
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "reference_kats.json")) as f:
+        k = json.load(f)["mock_completion_masks"]
+    ids = torch.tensor(k["completion_ids"], device=dev)
+    m, lengths, has = ops.completion_mask(ids, k["eos"])
+    assert m.cpu().tolist() == k["expected_mask"]
+    assert lengths.cpu().tolist() == [8, 4, 8]
+    assert has.cpu().tolist() == [0, 1, 1]
+    mt, _, _ = ops.completion_mask(ids, k["eos"], mask_truncated=True)
+    assert mt.cpu().tolist() == k["expected_mask_truncated"]
+
+
+def test_completion_mask_random(ops, dev):
+    g = _gen(6)
+    ids = torch.randint(0, 20, (64, 256), generator=g)
+    m, lengths, has = ops.completion_mask(ids.to(dev), [3, 17], mask_truncated=True)
+    em, el, _ = trl_ref.completion_mask_from_eos(torch.where(ids == 17, 3, ids), 3, mask_truncated=True)
+    assert torch.equal(m.cpu(), em)
+    assert torch.equal(lengths.cpu().long(), el)
+
+
+@pytest.mark.parametrize("scale", [True, False])
+def test_group_advantage(ops, dev, scale):
+    g = _gen(7)
+    rpf = torch.rand(64, 3, generator=g)
+    rpf[5, 1] = float("nan")
+    rpf[8:16] = 0.25  # zero-std group
+    w = torch.tensor([1.0, 0.5, 2.0])
+    adv, rew, gm, gs, zs = ops.group_advantages(rpf.to(dev), w.to(dev), 8, scale)
+    eadv, erew, egm, egs, ezs = trl_ref.group_advantages(rpf.double(), w.double(), 8, scale)
+    torch.testing.assert_close(rew.cpu().double(), erew, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(gm.cpu().double(), egm, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(gs.cpu().double(), egs, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(adv.cpu().double(), eadv, rtol=1e-4, atol=1e-5)
+    assert torch.equal(zs.cpu(), ezs)
+
+
+# --------------------------------------------------------------------------- GRPO loss
+CONFIGS = [
+    dict(loss_type="bnpo", importance_sampling_level="token", beta=0.0, old=False),
+    dict(loss_type="bnpo", importance_sampling_level="token", beta=0.04, old=True),
+    dict(loss_type="grpo", importance_sampling_level="token", beta=0.1, old=True, delta=1.3),
+    dict(loss_type="dr_grpo", importance_sampling_level="token", beta=0.0, old=True, eh=0.28),
+    dict(loss_type="bnpo", importance_sampling_level="sequence", beta=0.1, old=True),
+    dict(loss_type="grpo", importance_sampling_level="sequence", beta=0.0, old=False),
+    dict(loss_type="bnpo", importance_sampling_level="token", beta=0.0, old=True, emask=True),
+]
+
+
+@pytest.mark.parametrize("cfg", CONFIGS, ids=[str(i) for i in range(len(CONFIGS))])
+def test_grpo_loss_and_grad(ops, dev, cfg):
+    g = _gen(8)
+    R, T = 16, 256
+    lp = -torch.rand(R, T, generator=g, dtype=torch.float64) * 4
+    old = (lp + 0.3 * torch.randn(R, T, generator=g, dtype=torch.float64)) if cfg["old"] else None
+    ref = lp + 0.2 * torch.randn(R, T, generator=g, dtype=torch.float64)
+    adv = torch.randn(R, generator=g, dtype=torch.float64)
+    adv[3] = 0.0
+    lens = torch.randint(1, T + 1, (R,), generator=g)
+    lens[0] = 0
+    mask = (torch.arange(T).view(1, -1) < lens.view(-1, 1)).int()
+    ent = torch.rand(R, T, generator=g, dtype=torch.float64)
+    em = (torch.rand(R, T, generator=g) > 0.5) if cfg.get("emask") else None
+    kw = dict(beta=cfg["beta"], epsilon_low=0.2, epsilon_high=cfg.get("eh", 0.2), delta=cfg.get("delta"),
+              loss_type=cfg["loss_type"], importance_sampling_level=cfg["importance_sampling_level"],
+              max_completion_length=T)
+    x = lp.clone().requires_grad_(True)
+    eloss, emet = trl_ref.grpo_loss(x, adv, mask, old, ref, em, ent, **kw)
+    eloss.backward()
+    loss, dlogp, met = ops.grpo_loss_fwd_bwd(lp.to(dev), adv.to(dev), mask.to(dev), old_per_token_logps=
+                                             None if old is None else old.to(dev), ref_per_token_logps=ref.to(dev),
+                                             entropy_mask=None if em is None else em.to(dev), entropies=ent.to(dev),
+                                             **kw)
+    torch.testing.assert_close(loss.cpu().double()[0], eloss.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(dlogp.cpu().double(), x.grad, rtol=1e-5, atol=1e-7)
+    met = met.cpu().double()
+    tok = met[0].clamp(min=1.0)
+    if cfg["importance_sampling_level"] == "token":
+        assert met[3].item() / tok.item() == pytest.approx(emet["clip_ratio/low_mean"], abs=1e-6)
+        assert met[5].item() / tok.item() == pytest.approx(emet["clip_ratio/region_mean"], abs=1e-6)
+    else:
+        assert met[3].item() / R == pytest.approx(emet["clip_ratio/low_mean"], abs=1e-6)
+    if cfg["beta"]:
+        assert met[1].item() / tok.item() == pytest.approx(emet["kl"], rel=1e-5)
+    assert met[2].item() / tok.item() == pytest.approx(emet["entropy"], rel=1e-5)
+
+
+def test_grpo_loss_segments_equal_separate_microbatches(ops, dev):
+    """GA micro-batches fused into one kernel call == per-micro-batch losses / GA."""
+    g = _gen(9)
+    R, T, GA = 16, 64, 4
+    lp = -torch.rand(R, T, generator=g) * 3
+    adv = torch.randn(R, generator=g)
+    mask = (torch.rand(R, T, generator=g) > 0.3).int()
+    seg = torch.arange(R) // (R // GA)
+    scale = torch.full((R,), 1.0 / GA)
+    loss, dl, _ = ops.grpo_loss_fwd_bwd(lp.to(dev), adv.to(dev), mask.to(dev), row_scale=scale.to(dev),
+                                        segments=seg.to(dev), num_segments=GA)
+    tot, grads = 0.0, []
+    for i in range(GA):
+        sl = slice(i * R // GA, (i + 1) * R // GA)
+        l_i, d_i, _ = ops.grpo_loss_fwd_bwd(lp[sl].to(dev), adv[sl].to(dev), mask[sl].to(dev))
+        tot += l_i.item() / GA
+        grads.append(d_i.cpu() / GA)
+    assert loss.item() == pytest.approx(tot, rel=1e-5, abs=1e-7)
+    torch.testing.assert_close(dl.cpu(), torch.cat(grads), rtol=1e-5, atol=1e-8)
+
+
+# --------------------------------------------------------------------------- PPO pieces
+def test_masked_whiten(ops, dev):
+    g = _gen(10)
+    v = torch.randn(8, 53, generator=g)
+    m = torch.rand(8, 53, generator=g) > 0.3
+    for shift in (True, False):
+        out, stats = ops.masked_whiten(v.to(dev), m.to(dev), shift_mean=shift)
+        exp = trl_ref.masked_whiten(v.double(), m.double(), shift_mean=shift)
+        torch.testing.assert_close(out.cpu().double(), exp, rtol=1e-5, atol=1e-5)
+    with pytest.raises(ValueError):
+        ops.masked_whiten_checked(v.to(dev), torch.zeros_like(m).to(dev))
+
+
+def test_gae(ops, dev):
+    g = _gen(11)
+    r = torch.randn(64, 53, generator=g)
+    v = torch.randn(64, 53, generator=g)
+    adv, ret = ops.gae(r.to(dev), v.to(dev), 1.0, 0.95)
+    eadv, eret = trl_ref.gae(r.double(), v.double(), 1.0, 0.95)
+    torch.testing.assert_close(adv.cpu().double(), eadv, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(ret.cpu().double(), eret, rtol=1e-5, atol=1e-5)
+
+
+def test_ppo_loss(ops, dev):
+    g = _gen(12)
+    B, T = 16, 53
+    new = -torch.rand(B, T, generator=g, dtype=torch.float64) * 3
+    old = new + 0.3 * torch.randn(B, T, generator=g, dtype=torch.float64)
+    adv = torch.randn(B, T, generator=g, dtype=torch.float64)
+    vp = torch.randn(B, T, generator=g, dtype=torch.float64)
+    ov = vp + 0.3 * torch.randn(B, T, generator=g, dtype=torch.float64)
+    ret = torch.randn(B, T, generator=g, dtype=torch.float64)
+    sl = torch.randint(0, T, (B,), generator=g)
+    idx = torch.arange(T).view(1, -1)
+    pm, pm1 = idx > sl.view(-1, 1), idx > (sl + 1).view(-1, 1)
+    new = new.masked_fill(pm, trl_ref.INVALID_LOGPROB)
+    vp = vp.masked_fill(pm1, 0.0)
+    x, y = new.clone().requires_grad_(True), vp.clone().requires_grad_(True)
+    eloss, _, _, est = trl_ref.ppo_losses(x, old, adv, y, ov, ret, pm, pm1, 0.2, 0.2, 0.1)
+    eloss.backward()
+    loss, dnl, dvp, st = ops.ppo_loss_fwd_bwd(new.to(dev), old.to(dev), adv.to(dev), vp.to(dev), ov.to(dev),
+                                              ret.to(dev), pm.to(dev), pm1.to(dev), 0.2, 0.2, 0.1)
+    torch.testing.assert_close(loss.cpu().double()[0], eloss.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(dnl.cpu().double(), x.grad.masked_fill(pm, 0), rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(dvp.cpu().double(), y.grad.masked_fill(pm1, 0), rtol=1e-5, atol=1e-7)
+    assert st[2].item() == pytest.approx(est["pg_clipfrac"], abs=1e-6)
+    assert st[4].item() == pytest.approx(est["approxkl"], rel=1e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_value_head(ops, dev, dtype):
+    g = _gen(13)
+    h = torch.randn(4, 33, 896, generator=g).to(dtype)
+    w = torch.randn(896, generator=g) * 0.02
+    b = torch.randn(1, generator=g)
+    got = ops.value_head(h.to(dev), w.to(dev), b.to(dev))
+    exp = trl_ref.value_head(h.double(), w.double(), b.double())
+    torch.testing.assert_close(got.cpu().double(), exp, rtol=1e-5, atol=1e-5)
+
+
+# --------------------------------------------------------------------------- optimizer
+def test_adamw_and_clip(dev):
+    from swh_trl_amd import optim
+    g = _gen(14)
+    N = 1_000_003
+    p0 = torch.randn(N, generator=g, dtype=torch.float64)
+    st = optim.FlatAdamW(N, dev, lr=1e-3, weight_decay=0.01, max_grad_norm=1.0)
+    st.master.copy_(p0.float().to(dev))
+    q, m, v = p0.float().double(), torch.zeros(N, dtype=torch.float64), torch.zeros(N, dtype=torch.float64)
+    model = torch.empty(N, dtype=torch.bfloat16, device=dev)
+    for step in range(1, 4):
+        gr = (torch.randn(N, generator=g) * 0.01).to(torch.bfloat16)
+        norm = st.step(gr.to(dev), model_out=model)
+        total, coef = trl_ref.clip_coef([gr.double()], 1.0)
+        assert norm.item() == pytest.approx(float(total), rel=1e-5)
+        q, m, v = trl_ref.adamw_step(q, gr.double() * coef, m, v, step, 1e-3, weight_decay=0.01)
+    torch.testing.assert_close(st.master.cpu().double(), q, rtol=1e-5, atol=1e-6)
+    assert torch.equal(model.cpu(), st.master.cpu().to(torch.bfloat16))
+
+
+# --------------------------------------------------------------------------- sampler
+def _oracle_lib():
+    so = os.path.join(ROOT, "oracle", "_build", "libswh_oracle.so")
+    if not os.path.exists(so):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
+    return ctypes.CDLL(so)
+
+
+def _uniforms(lib, seed, offset, row, V):
+    buf = (ctypes.c_float * V)()
+    lib.swh_ref_row_uniforms(ctypes.c_uint64(seed), ctypes.c_uint64(offset), ctypes.c_int64(row),
+                             ctypes.c_int64(V), buf)
+    return torch.from_numpy(np.frombuffer(buf, dtype=np.float32).copy())
+
+
+def _run_sampler(ops, dev, logits, params, seed=7, offset=11, step=0, seen=None, finished=None, C=4,
+                 scores=False):
+    B, V = logits.shape
+    rng = torch.tensor([seed, offset], dtype=torch.int64, device=dev)
+    stp = torch.tensor([step], dtype=torch.int32, device=dev)
+    fin = finished.to(dev).int() if finished is not None else torch.zeros(B, dtype=torch.int32, device=dev)
+    out = torch.full((B, C), -1, dtype=torch.int64, device=dev)
+    cur = torch.empty(B, dtype=torch.int64, device=dev)
+    olp = torch.zeros(B, C, dtype=torch.float32, device=dev)
+    sc = torch.empty(B, V, dtype=torch.float32, device=dev) if scores else None
+    ops.sample_step(logits.to(dev), params, rng, stp, fin, out, cur, seen, olp, sc)
+    return out[:, step].cpu(), fin.cpu(), olp[:, step].cpu(), (sc.cpu() if scores else None), cur.cpu()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_sampler_greedy_is_argmax(ops, dev, dtype):
+    g = _gen(15)
+    logits = torch.randn(64, 151936, generator=g).to(dtype)
+    logits[0, 100] = logits[0, 200] = 50.0  # tie -> first index (torch.argmax)
+    tok, _, _, _, cur = _run_sampler(ops, dev, logits, ops.make_sample_params(greedy=True))
+    assert torch.equal(tok, logits.float().argmax(-1))
+    assert torch.equal(cur, tok)
+
+
+@pytest.mark.parametrize("case", ["plain", "temp", "topk", "topp", "minp", "all", "rep"])
+def test_sampler_matches_oracle_draw(ops, dev, case):
+    """Same logits, same Philox stream: the device pick equals the oracle's
+    Gumbel-max pick on the oracle-processed scores (float64)."""
+    g = _gen(16)
+    B, V = 8, 32000
+    logits = torch.randn(B, V, generator=g) * 2  # fp32: no ties at the thresholds
+    kw = dict(plain={}, temp=dict(temperature=0.7), topk=dict(top_k=50), topp=dict(top_p=0.9),
+              minp=dict(min_p=0.05), all=dict(temperature=0.8, top_k=200, top_p=0.8, min_p=0.02),
+              rep=dict(repetition_penalty=1.3, top_p=0.95))[case]
+    seen = None
+    seen_mask = None
+    if case == "rep":
+        prev = torch.randint(0, V, (B, 40), generator=g)
+        seen = torch.zeros(B, (V + 31) // 32, dtype=torch.int32, device=dev)
+        ops.seen_init(prev.to(dev), None, V, seen)
+        seen_mask = torch.zeros(B, V, dtype=torch.bool).scatter_(1, prev, True)
+    params = ops.make_sample_params(**kw)
+    tok, _, lp, sc, _ = _run_sampler(ops, dev, logits, params, seen=seen, scores=True)
+    proc = hf_sampling.process_scores(logits, seen=seen_mask, rep_penalty=kw.get("repetition_penalty", 1.0),
+                                      t=kw.get("temperature", 1.0), k=kw.get("top_k"), p=kw.get("top_p", 1.0),
+                                      mp=kw.get("min_p"))
+    kept_dev, kept_ref = torch.isfinite(sc), torch.isfinite(proc)
+    assert torch.equal(kept_dev, kept_ref), (kept_dev ^ kept_ref).sum()
+    torch.testing.assert_close(sc[kept_ref], proc[kept_ref], rtol=0, atol=0)
+    lib = _oracle_lib()
+    u = torch.stack([_uniforms(lib, 7, 11, b, V) for b in range(B)])
+    exp = hf_sampling.gumbel_pick(proc, u)
+    assert torch.equal(tok, exp)
+    ref_lp = torch.log_softmax(proc.double(), -1).gather(1, exp.view(-1, 1)).squeeze(1)
+    torch.testing.assert_close(lp.double(), ref_lp, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("kw", [dict(top_p=0.9), dict(top_k=100), dict(top_p=0.8, min_p=0.05)])
+def test_sampler_bf16_ties(ops, dev, kw):
+    """bf16 logits have many equal values: at a threshold the device keeps the
+    whole tie group while transformers' sort keeps an arbitrary part of it.
+    Bound: device kept set == oracle kept set + (part of) the tie group at the
+    oracle's smallest kept value."""
+    g = _gen(21)
+    logits = (torch.randn(8, 32000, generator=g) * 2).to(torch.bfloat16)
+    _, _, _, sc, _ = _run_sampler(ops, dev, logits, ops.make_sample_params(**kw), scores=True)
+    proc = hf_sampling.process_scores(logits, k=kw.get("top_k"), p=kw.get("top_p", 1.0), mp=kw.get("min_p"))
+    kd, kr = torch.isfinite(sc), torch.isfinite(proc)
+    assert not (kr & ~kd).any()
+    for b in range(8):
+        extra = kd[b] & ~kr[b]
+        if extra.any():
+            assert (logits[b][extra].float() == logits[b][kr[b]].float().min()).all()
+
+
+def test_sampler_distribution_chi2(ops, dev):
+    """Empirical frequencies over 4096 independent draws match softmax(z)."""
+    V, N = 16, 4096
+    z = torch.linspace(-2, 2, V)
+    logits = z.repeat(N, 1)
+    tok, _, _, _, _ = _run_sampler(ops, dev, logits, ops.make_sample_params(), seed=123, offset=0)
+    counts = torch.bincount(tok, minlength=V).double()
+    p = torch.softmax(z.double(), 0)
+    chi2 = (((counts - N * p) ** 2) / (N * p)).sum().item()
+    assert chi2 < 45.0  # df=15, p ~ 1e-4
+
+
+def test_sampler_bookkeeping(ops, dev):
+    """Finished rows emit pad; EOS finishes a row; min_new_tokens suppresses EOS."""
+    V = 64
+    logits = torch.full((3, V), -10.0)
+    logits[:, 5] = 10.0  # EOS strongly preferred
+    fin = torch.tensor([1, 0, 0])
+    params = ops.make_sample_params(greedy=True, pad_token_id=9, eos_token_ids=[5])
+    tok, f, _, _, _ = _run_sampler(ops, dev, logits, params, finished=fin)
+    assert tok.tolist() == [9, 5, 5] and f.tolist() == [1, 1, 1]
+    params = ops.make_sample_params(greedy=True, pad_token_id=9, eos_token_ids=[5], min_new_tokens=3)
+    tok, f, _, _, _ = _run_sampler(ops, dev, logits, params, step=1)
+    assert 5 not in tok.tolist() and f.tolist() == [0, 0, 0]
+
+
+# --------------------------------------------------------------------------- decoder kernels
+def test_rmsnorm_matches_hf_bf16(ops, dev):
+    from swh_trl_amd import nn_ops
+    g = _gen(17)
+    x = torch.randn(37, 896, generator=g).to(torch.bfloat16).to(dev)
+    r = torch.randn(37, 896, generator=g).to(torch.bfloat16).to(dev)
+    w = (1 + 0.1 * torch.randn(896, generator=g)).to(torch.bfloat16).to(dev)
+    y, s = nn_ops.rmsnorm_residual(x, r, w, 1e-6)
+    s_ref = r + x
+    hs = s_ref.float()
+    hs = hs * torch.rsqrt(hs.pow(2).mean(-1, keepdim=True) + 1e-6)
+    y_ref = w * hs.to(torch.bfloat16)
+    assert torch.equal(s, s_ref)
+    diff = (y.float() - y_ref.float()).abs()
+    assert (diff <= y_ref.float().abs() * 2 ** -7 + 1e-6).all()
+    assert (y == y_ref).float().mean() > 0.99
+
+
+def test_rmsnorm_backward(ops, dev):
+    from swh_trl_amd import nn_ops
+    g = _gen(18)
+    x = torch.randn(130, 896, generator=g).to(torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(896, generator=g)).to(torch.bfloat16)
+    dy = torch.randn(130, 896, generator=g).to(torch.bfloat16)
+    xd, wd = x.to(dev).requires_grad_(True), w.to(dev).requires_grad_(True)
+    y = nn_ops.RMSNormFn.apply(xd, wd, 1e-6)
+    y.backward(dy.to(dev))
+    xr, wr = x.double().requires_grad_(True), w.double().requires_grad_(True)
+    yr = wr * (xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6))
+    yr.backward(dy.double())
+    torch.testing.assert_close(xd.grad.cpu().double(), xr.grad, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(wd.grad.cpu().double(), wr.grad, rtol=2e-2, atol=5e-2)
+
+
+def test_silu_mul(ops, dev):
+    from swh_trl_amd import nn_ops
+    g = _gen(19)
+    gu = torch.randn(33, 2 * 4864, generator=g).to(torch.bfloat16).to(dev).requires_grad_(True)
+    out = nn_ops.SiluMulFn.apply(gu)
+    gt, ut = gu.detach()[:, :4864], gu.detach()[:, 4864:]
+    ref = torch.nn.functional.silu(gt) * ut
+    assert torch.equal(out, ref)
+    dout = torch.randn_like(out)
+    out.backward(dout)
+    gg = gu.detach().double().requires_grad_(True)
+    rr = torch.nn.functional.silu(gg[:, :4864]) * gg[:, 4864:]
+    rr.backward(dout.double())
+    torch.testing.assert_close(gu.grad.double(), gg.grad, rtol=2e-2, atol=2e-2)
+
+
+def _rope_tables(D, max_pos, theta, dev):
+    inv = 1.0 / (theta ** (torch.arange(0, D, 2, dtype=torch.int64).float() / D))
+    pos = torch.arange(max_pos).float()
+    fr = torch.outer(pos, inv)
+    return fr.cos().to(torch.bfloat16).float().to(dev), fr.sin().to(torch.bfloat16).float().to(dev)
+
+
+@pytest.mark.parametrize("D,Hq,Hkv", [(64, 14, 2), (128, 32, 8)])
+def test_attn_decode(ops, dev, D, Hq, Hkv):
+    from swh_trl_amd import nn_ops
+    g = _gen(20)
+    B, P, Tmax, step = 5, 40, 320, 270
+    plen = torch.tensor([40, 33, 1, 40, 17], dtype=torch.int32)
+    kc = (torch.randn(B, Hkv, Tmax, D, generator=g)).to(torch.bfloat16)
+    vc = (torch.randn(B, Hkv, Tmax, D, generator=g)).to(torch.bfloat16)
+    qkv = torch.randn(B, (Hq + 2 * Hkv) * D, generator=g).to(torch.bfloat16)
+    cos, sin = _rope_tables(D, 1024, 1e6, dev)
+    state = torch.tensor([step + 1, P], dtype=torch.int32, device=dev)  # sampler index = input + 1
+    kcd, vcd = kc.to(dev), vc.to(dev)
+    out = nn_ops.attn_decode(qkv.to(dev), kcd, vcd, cos, sin, plen.to(dev), state, Hq, Hkv, D, D ** -0.5)
+    # reference: fp32 math on the same bf16 values
+    slot = P + step
+    q = qkv[:, :Hq * D].view(B, Hq, D).float()
+    k = qkv[:, Hq * D:(Hq + Hkv) * D].view(B, Hkv, D).float()
+    v = qkv[:, (Hq + Hkv) * D:].view(B, Hkv, D)
+    c, s = cos.cpu(), sin.cpu()
+    exp = torch.empty(B, Hq * D)
+    for b in range(B):
+        pos = int(plen[b]) + step
+        cc, ss = torch.cat([c[pos], c[pos]]), torch.cat([s[pos], s[pos]])
+
+        def rope(x):
+            rot = torch.cat([-x[..., D // 2:], x[..., :D // 2]], -1)
+            return ((x * cc).bfloat16().float() + (rot * ss).bfloat16().float()).bfloat16().float()
+
+        qb, kb = rope(q[b]), rope(k[b])
+        K = kc[b].float().clone()
+        Vv = vc[b].float().clone()
+        K[:, slot] = kb
+        Vv[:, slot] = v[b].float()
+        st = P - int(plen[b])
+        for h in range(Hq):
+            kvh = h // (Hq // Hkv)
+            sc = (K[kvh, st:slot + 1] @ qb[h]) * D ** -0.5
+            p = torch.softmax(sc, 0)
+            exp[b, h * D:(h + 1) * D] = p @ Vv[kvh, st:slot + 1]
+    torch.testing.assert_close(out.cpu().float(), exp, rtol=2e-2, atol=2e-2)
+    # the new k/v were appended to the cache
+    assert torch.equal(vcd[:, :, slot].cpu(), v)
+    # a slot past the cache end writes NaN and leaves the cache alone
+    bad = torch.tensor([Tmax - P + 1, P], dtype=torch.int32, device=dev)
+    before = kcd.clone()
+    out2 = nn_ops.attn_decode(qkv.to(dev), kcd, vcd, cos, sin, plen.to(dev), bad, Hq, Hkv, D, D ** -0.5)
+    assert torch.isnan(out2.float()).all() and torch.equal(before, kcd)
