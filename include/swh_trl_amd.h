@@ -256,6 +256,18 @@ int swh_attn_decode(const void *qkv, void *k_cache, void *v_cache, const float *
                     const float *rope_sin, const int32_t *prompt_len, const int32_t *state, int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax, float scale, void *out,
                     void *stream);
 
+/* Weight-streaming decode GEMM Y[M,N] = X[M,K] W[N,K]^T (bf16, fp32 MFMA
+ * accumulation, K % 128 == 0) with the decoder's neighbours fused:
+ *   norm_w != NULL : X is replaced by RMSNorm(X) * norm_w (eps) in the prologue
+ *   bias   != NULL : + bias[N]
+ *   residual != NULL: residual[M,N] = bf16(residual + bf16(XW^T)) in place
+ *                     (row stride ldy; y unused)
+ *   silu != 0      : W has 2N rows (gate then up); y = bf16(bf16(silu(g)) * u)
+ * Replaces the transformers q/k/v, o, gate/up, down and lm-head projections of
+ * one decode step (plus their RMSNorm / SiLU / residual neighbours). */
+int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, const void *norm_w, float eps,
+                    const void *bias, void *residual, int32_t silu, void *y, int64_t ldy, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

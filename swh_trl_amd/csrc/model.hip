@@ -183,178 +183,6 @@ __global__ __launch_bounds__(256) void embed_gather_kernel(const uint16_t *__res
         reinterpret_cast<uint4 *>(x + b * H)[v] = reinterpret_cast<const uint4 *>(table + id * H)[v];
 }
 
-// ---------------------------------------------------------------------------
-// Attention decode (GQA), one workgroup per (kv head, sequence).
-// ---------------------------------------------------------------------------
-constexpr int kAttnThreads = 256;
-constexpr int kTile = 256;
-constexpr int kMaxGq = 16;
-
-template <int D>
-__global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
-    const uint16_t *__restrict__ qkv, uint16_t *__restrict__ kc, uint16_t *__restrict__ vc,
-    const float *__restrict__ rcos, const float *__restrict__ rsin, const int32_t *__restrict__ plen,
-    const int32_t *__restrict__ state, int Hq, int Hkv, int Tmax, float scale, uint16_t *__restrict__ out) {
-    constexpr int LPK = D / 8;         // lanes per key (8 dims per lane)
-    constexpr int KPW = 64 / LPK;      // keys per wave per iteration
-    constexpr int NW = kAttnThreads / 64;
-    __shared__ float q_s[kMaxGq * D];
-    __shared__ float sc[kMaxGq * (kTile + 1)];
-    __shared__ float m_s[kMaxGq], l_s[kMaxGq], f_s[kMaxGq];
-    __shared__ uint16_t knew[D], vnew[D];
-
-    const int kvh = blockIdx.x;
-    const int64_t b = blockIdx.y;
-    const int Gq = Hq / Hkv;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    // state[0] = index of the token the sampler produces in this decode step;
-    // the attention input is the previous token, index state[0] - 1.
-    const int step = state[0] - 1, P = state[1];
-    const int pl = plen[b];
-    const int slot_new = P + step;
-    const int start = P - pl;
-    const int pos = pl + step;
-    if (step < 0 || slot_new >= Tmax || pl < 0 || pl > P) {  // never write outside the cache
-        const int Gq0 = Hq / Hkv;
-        for (int idx = threadIdx.x; idx < Gq0 * D; idx += kAttnThreads)
-            out[b * (int64_t)Hq * D + kvh * Gq0 * D + idx] = 0x7fc0;  // NaN: fail loudly
-        return;
-    }
-    const int W = (Hq + 2 * Hkv) * D;
-    const uint16_t *row = qkv + b * (int64_t)W;
-    const int64_t cbase = ((b * Hkv + kvh) * (int64_t)Tmax) * D;
-
-    // RoPE on q (Gq heads) and the new k; v copied.  Thread i < D/2 handles pair (i, i + D/2).
-    constexpr int HD = D / 2;
-    for (int idx = tid; idx < (Gq + 1) * HD; idx += kAttnThreads) {
-        const int hh = idx / HD, i = idx - hh * HD;
-        const float c = rcos[(int64_t)pos * HD + i], s = rsin[(int64_t)pos * HD + i];
-        const uint16_t *src = (hh < Gq) ? row + (kvh * Gq + hh) * D : row + (Hq + kvh) * D;
-        const float x1 = bf16_bits_to_f32(src[i]), x2 = bf16_bits_to_f32(src[i + HD]);
-        const float o1 = round_bf16(round_bf16(x1 * c) + round_bf16(-x2 * s));
-        const float o2 = round_bf16(round_bf16(x2 * c) + round_bf16(x1 * s));
-        if (hh < Gq) {
-            q_s[hh * D + i] = o1;
-            q_s[hh * D + i + HD] = o2;
-        } else {
-            knew[i] = f32_to_bf16_bits(o1);
-            knew[i + HD] = f32_to_bf16_bits(o2);
-        }
-    }
-    for (int d = tid; d < D; d += kAttnThreads) vnew[d] = row[(Hq + Hkv + kvh) * D + d];
-    if (tid < kMaxGq) {
-        m_s[tid] = kNegInf;
-        l_s[tid] = 0.f;
-    }
-    __syncthreads();
-    for (int d = tid; d < D; d += kAttnThreads) {
-        kc[cbase + (int64_t)slot_new * D + d] = knew[d];
-        vc[cbase + (int64_t)slot_new * D + d] = vnew[d];
-    }
-
-    // this lane's q slice for every head of the group
-    const int part = lane % LPK, kin = lane / LPK;
-    float qreg[kMaxGq][8];
-#pragma unroll
-    for (int h = 0; h < kMaxGq; ++h)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) qreg[h][k] = (h < Gq) ? q_s[h * D + part * 8 + k] : 0.f;
-
-    // output accumulators: thread owns (h, d) for idx = tid + j*256 < Gq*D
-    constexpr int kAcc = (kMaxGq * D + kAttnThreads - 1) / kAttnThreads;
-    float acc[kAcc];
-#pragma unroll
-    for (int j = 0; j < kAcc; ++j) acc[j] = 0.f;
-
-    for (int ts = start; ts <= slot_new; ts += kTile) {
-        const int te = (ts + kTile - 1 < slot_new) ? ts + kTile - 1 : slot_new;  // inclusive
-        const int n = te - ts + 1;
-        // phase A: scores
-        for (int base = wid * KPW; base < n; base += NW * KPW) {
-            const int kk = base + kin;
-            float part_dot[kMaxGq];
-#pragma unroll
-            for (int h = 0; h < kMaxGq; ++h) part_dot[h] = 0.f;
-            if (kk < n) {
-                const int slot = ts + kk;
-                float kv[8];
-                if (slot == slot_new) {
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) kv[k] = bf16_bits_to_f32(knew[part * 8 + k]);
-                } else {
-                    unpack16<SWH_BF16>(*reinterpret_cast<const uint4 *>(kc + cbase + (int64_t)slot * D + part * 8), kv);
-                }
-#pragma unroll
-                for (int h = 0; h < kMaxGq; ++h) {
-                    float s = 0.f;
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) s = fmaf(qreg[h][k], kv[k], s);
-                    part_dot[h] = s;
-                }
-            }
-#pragma unroll
-            for (int h = 0; h < kMaxGq; ++h) {
-                float s = part_dot[h];
-#pragma unroll
-                for (int o = 1; o < LPK; o <<= 1) s += __shfl_xor(s, o, kWave);
-                part_dot[h] = s;
-            }
-            if (part == 0 && kk < n) {
-#pragma unroll
-                for (int h = 0; h < kMaxGq; ++h)
-                    if (h < Gq) sc[h * (kTile + 1) + kk] = part_dot[h] * scale;
-            }
-        }
-        __syncthreads();
-        // phase B: online softmax per head
-        for (int h = wid; h < Gq; h += NW) {
-            float mx = kNegInf;
-            for (int k = lane; k < n; k += 64) mx = fmaxf(mx, sc[h * (kTile + 1) + k]);
-            mx = wave_max(mx);
-            const float mo = m_s[h];
-            const float mn = fmaxf(mo, mx);
-            const float f = (mo == kNegInf) ? 0.f : expf(mo - mn);
-            float sum = 0.f;
-            for (int k = lane; k < n; k += 64) {
-                const float pv = expf(sc[h * (kTile + 1) + k] - mn);
-                sc[h * (kTile + 1) + k] = pv;
-                sum += pv;
-            }
-            sum = wave_sum(sum);
-            if (lane == 0) {
-                m_s[h] = mn;
-                l_s[h] = l_s[h] * f + sum;
-                f_s[h] = f;
-            }
-        }
-        __syncthreads();
-        // phase C: P V
-#pragma unroll
-        for (int j = 0; j < kAcc; ++j) {
-            const int idx = tid + j * kAttnThreads;
-            if (idx < Gq * D) {
-                const int h = idx / D, d = idx - h * D;
-                float a = acc[j] * f_s[h];
-                const float *ph = sc + h * (kTile + 1);
-                const uint16_t *vp = vc + cbase + (int64_t)ts * D + d;
-                const int nc = (te == slot_new) ? n - 1 : n;
-                for (int k = 0; k < nc; ++k) a = fmaf(ph[k], bf16_bits_to_f32(vp[(int64_t)k * D]), a);
-                if (nc < n) a = fmaf(ph[n - 1], bf16_bits_to_f32(vnew[d]), a);
-                acc[j] = a;
-            }
-        }
-        __syncthreads();
-    }
-#pragma unroll
-    for (int j = 0; j < kAcc; ++j) {
-        const int idx = tid + j * kAttnThreads;
-        if (idx < Gq * D) {
-            const int h = idx / D, d = idx - h * D;
-            out[b * (int64_t)Hq * D + (kvh * Gq + h) * D + d] = f32_to_bf16_bits(acc[j] / l_s[h]);
-        }
-    }
-}
-
 }  // namespace
 }  // namespace swh
 
@@ -411,29 +239,5 @@ extern "C" int swh_embed_gather(const void *table, const int64_t *ids, int64_t B
     if (B == 0) return SWH_OK;
     embed_gather_kernel<<<dim3((unsigned)B), 128, 0, static_cast<hipStream_t>(stream)>>>(
         static_cast<const uint16_t *>(table), ids, H, static_cast<uint16_t *>(x));
-    return launch_status();
-}
-
-extern "C" int swh_attn_decode(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
-                               const float *rope_sin, const int32_t *prompt_len, const int32_t *state, int64_t B,
-                               int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax, float scale, void *out,
-                               void *stream) {
-    if (!qkv || !k_cache || !v_cache || !rope_cos || !rope_sin || !prompt_len || !state || !out || B < 0 || Hkv <= 0 ||
-        Hq % Hkv || Hq / Hkv > kMaxGq || Tmax <= 0)
-        return SWH_E_ARG;
-    if (B == 0) return SWH_OK;
-    dim3 grid((unsigned)Hkv, (unsigned)B), block(kAttnThreads);
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    const uint16_t *q = static_cast<const uint16_t *>(qkv);
-    uint16_t *kc = static_cast<uint16_t *>(k_cache), *vc = static_cast<uint16_t *>(v_cache);
-    uint16_t *o = static_cast<uint16_t *>(out);
-    if (D == 64)
-        attn_decode_kernel<64><<<grid, block, 0, s>>>(q, kc, vc, rope_cos, rope_sin, prompt_len, state, Hq, Hkv, Tmax,
-                                                      scale, o);
-    else if (D == 128)
-        attn_decode_kernel<128><<<grid, block, 0, s>>>(q, kc, vc, rope_cos, rope_sin, prompt_len, state, Hq, Hkv, Tmax,
-                                                       scale, o);
-    else
-        return SWH_E_ARG;
     return launch_status();
 }

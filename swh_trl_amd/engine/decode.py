@@ -28,7 +28,7 @@ from .model import CausalLM
 
 class DecodeEngine:
     def __init__(self, model: CausalLM, batch_size: int, max_prompt_len: int, max_new_tokens: int,
-                 use_graph: bool = True):
+                 use_graph: bool = True, fused: Optional[bool] = None):
         c = model.cfg
         self.model, self.cfg = model, c
         self.B, self.Pmax, self.Cmax = batch_size, max_prompt_len, max_new_tokens
@@ -61,6 +61,9 @@ class DecodeEngine:
                               dtype=torch.uint8)
         self.cos, self.sin = model.rope(self.Tmax + 1)
         self.use_graph = use_graph and os.environ.get("SWH_DECODE_GRAPH", "1") != "0"
+        ks = (c.hidden_size, c.intermediate_size, c.q_dim)
+        self.fused = (fused if fused is not None else os.environ.get("SWH_DECODE_FUSED", "1") != "0") and \
+            all(k % 128 == 0 for k in ks) and c.hidden_size % 16 == 0 and c.qkv_dim % 16 == 0
         self.graph = None
         self._graph_params = None
         self.params = ops.make_sample_params()
@@ -68,6 +71,33 @@ class DecodeEngine:
 
     # ------------------------------------------------------------------ one decode step (capturable)
     def _step(self):
+        """One decode step: 5 fused kernels per layer when K % 128 == 0
+        (norm+QKV+bias, RoPE+append+attention, O+residual, norm+gate/up+SiLU,
+        down+residual), then norm+lm head, sampler, step advance."""
+        if self.fused:
+            self._step_fused()
+        else:
+            self._step_unfused()
+        self._sample()
+        ops.step_advance(self.state[0:1])
+
+    def _step_fused(self):
+        c, m = self.cfg, self.model
+        p = m.p
+        eps = c.rms_norm_eps
+        nn_ops.embed_gather(p["embed"], self.cur, self.s)
+        for i in range(c.num_hidden_layers):
+            nn_ops.decode_gemm(self.s, p[f"l{i}.qkv_w"], norm_w=p[f"l{i}.ln_in"], eps=eps,
+                               bias=p.get(f"l{i}.qkv_b"), y=self.qkv)
+            nn_ops.attn_decode(self.qkv, self.kv[i, 0], self.kv[i, 1], self.cos, self.sin, self.plen, self.state,
+                               c.num_attention_heads, c.num_key_value_heads, c.head_dim, c.head_dim ** -0.5,
+                               out=self.att)
+            nn_ops.decode_gemm(self.att, p[f"l{i}.o_w"], residual=self.s)
+            nn_ops.decode_gemm(self.s, p[f"l{i}.gu_w"], norm_w=p[f"l{i}.ln_post"], eps=eps, silu=True, y=self.act)
+            nn_ops.decode_gemm(self.act, p[f"l{i}.down_w"], residual=self.s)
+        nn_ops.decode_gemm(self.s, m.lm_weight(), norm_w=p["norm"], eps=eps, y=self.logits_buf)
+
+    def _step_unfused(self):
         c, m = self.cfg, self.model
         p = m.p
         nn_ops.embed_gather(p["embed"], self.cur, self.x)
@@ -89,8 +119,6 @@ class DecodeEngine:
             nxt = p[f"l{i + 1}.ln_in"] if i + 1 < c.num_hidden_layers else p["norm"]
             nn_ops.rmsnorm_residual(self.d, self.s, nxt, c.rms_norm_eps, y=self.h, s_out=self.s)
         torch.mm(self.h, m.lm_weight().t(), out=self.logits_buf)
-        self._sample()
-        ops.step_advance(self.state[0:1])
 
     def _sample(self):
         ops.sample_step(self.logits_buf, self.params, self.rng, self.state[0:1], self.finished, self.out, self.cur,

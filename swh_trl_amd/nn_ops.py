@@ -112,3 +112,20 @@ def attn_decode(qkv: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
          rope_sin.data_ptr(), prompt_len.data_ptr(), state.data_ptr(), B, Hq, Hkv, D, Tmax, float(scale),
          out.data_ptr(), _stream())
     return out
+
+
+def decode_gemm(x: torch.Tensor, w: torch.Tensor, *, norm_w: Optional[torch.Tensor] = None, eps: float = 1e-6,
+                bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None, silu: bool = False,
+                y: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Weight-streaming decode GEMM with fused RMSNorm prologue and bias /
+    residual / SiLU-gate epilogues (include/swh_trl_amd.h swh_decode_gemm).
+    x [M, K] bf16; w [N, K] (or [2N, K] with silu)."""
+    _dev(x, "decode_gemm")
+    M, K = x.shape
+    N = w.shape[0] // 2 if silu else w.shape[0]
+    if residual is None and y is None:
+        y = torch.empty(M, N, device=x.device, dtype=x.dtype)
+    ldy = residual.stride(0) if residual is not None else y.stride(0)
+    call("swh_decode_gemm", x.data_ptr(), w.data_ptr(), M, N, K, _p(norm_w), float(eps), _p(bias), _p(residual),
+         int(bool(silu)), _p(y), ldy, _stream())
+    return residual if residual is not None else y

@@ -33,7 +33,7 @@ from ..engine.decode import DecodeEngine
 from ..engine.model import CausalLM
 from ..optim import FlatAdamW
 from .grpo_config import GRPOConfig
-from .utils import RepeatSampler, left_pad, linear_lr, pad_left_cat, split_tensor_dict, \
+from .utils import generation_batch_indices, left_pad, linear_lr, pad_left_cat, split_tensor_dict, \
     truncate_with_protected_tokens
 
 RewardFunc = Union[str, Callable, torch.nn.Module]
@@ -175,22 +175,13 @@ class GRPOTrainer:
         return self.args.per_device_train_batch_size * self.args.steps_per_generation
 
     def _generation_batches(self):
-        """RepeatSampler stream (grpo_trainer.py:1096-1130) → this rank's slice of
-        every global generation batch (repeats collapsed: the loop regenerates
-        only once per steps_per_generation*num_iterations micro-steps)."""
+        """This rank's slice of every global generation batch (trainer/utils.py
+        `generation_batch_indices`, the RepeatSampler + accelerate sharding)."""
         a = self.args
-        ds = self.train_dataset
-        gbs = a.generation_batch_size
-        while True:
-            sampler = RepeatSampler(ds, mini_repeat_count=self.num_generations,
-                                    batch_size=gbs // self.num_generations, repeat_count=1,
-                                    shuffle=bool(a.shuffle_dataset), seed=a.seed)
-            idx = list(sampler)
-            local = self._local_gen_batch_size()
-            for s in range(0, len(idx) - gbs + 1, gbs):
-                mine = idx[s + self.rank * local:s + (self.rank + 1) * local]
-                yield [ds[i] for i in mine]
-            self.state.epoch += 1
+        for mine in generation_batch_indices(len(self.train_dataset), self.num_generations, a.generation_batch_size,
+                                             self._local_gen_batch_size(), self.rank, a.seed,
+                                             bool(a.shuffle_dataset)):
+            yield [self.train_dataset[i] for i in mine]
 
     def _tokenize_prompts(self, examples):
         if "prompt_ids" in examples[0]:

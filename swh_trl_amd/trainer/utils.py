@@ -38,6 +38,27 @@ class RepeatSampler:
         return (self.num_samples // self.batch_size) * self.batch_size * self.mini_repeat_count * self.repeat_count
 
 
+def generation_batch_indices(n: int, num_generations: int, generation_batch_size: int, local_batch_size: int,
+                             rank: int, seed: Optional[int], shuffle: bool = True, epochs: Optional[int] = None):
+    """This rank's dataset indices of every global generation batch.
+
+    The reference feeds `RepeatSampler(mini_repeat_count=G, batch_size=gbs/G,
+    repeat_count=num_iterations*steps_per_generation)` (grpo_trainer.py:1096-1130)
+    through accelerate's per-process batch sharding: rank r receives the r-th
+    contiguous local chunk of each global generation batch, and the repeats are
+    consumed without regenerating (`_prepare_inputs` :1411-1444).  Here the
+    repeats are collapsed and each yielded list is one local generation batch
+    (whole groups of G: local_batch_size is a multiple of G)."""
+    ep = 0
+    while epochs is None or ep < epochs:
+        idx = list(RepeatSampler(range(n), mini_repeat_count=num_generations,
+                                 batch_size=generation_batch_size // num_generations, repeat_count=1,
+                                 shuffle=shuffle, seed=seed))
+        for s in range(0, len(idx) - generation_batch_size + 1, generation_batch_size):
+            yield idx[s + rank * local_batch_size:s + (rank + 1) * local_batch_size]
+        ep += 1
+
+
 def truncate_with_protected_tokens(ids: torch.Tensor, mask: torch.Tensor, target_length: int,
                                    protected_tokens: Sequence[int]):
     """grpo_trainer.py:367-421, vectorised: keep every protected id plus the

@@ -93,6 +93,24 @@ def test_decode_graph_equals_eager_and_full_forward(dev):
     assert agree.all(), (~agree).nonzero()[:5]
 
 
+def test_fused_decode_step_matches_unfused(dev):
+    """The 5-kernel fused decode layer equals the unfused (hipBLASLt + separate
+    norm/SiLU/residual) step on the same state, within bf16 rounding."""
+    from swh_trl_amd.engine import DecodeEngine
+    m = _tiny(dev, seed=7, layers=2)
+    B, P, C = 6, 9, 4
+    ids = torch.randint(0, m.cfg.vocab_size, (B, P), device=dev)
+    mask = torch.ones(B, P, dtype=torch.int32, device=dev)
+    outs = []
+    for fused in (True, False):
+        e = DecodeEngine(m, B, P, C, use_graph=False, fused=fused)
+        assert e.fused == fused
+        e.generate(ids, mask, 2, greedy=True)  # prefill + one decode step
+        outs.append(e.logits_buf.float().clone())
+    err = (outs[0] - outs[1]).abs().max().item()
+    assert err <= 0.02 * outs[1].abs().max().item() + 0.02, err
+
+
 def test_greedy_matches_transformers_generate(dev):
     """First-divergence index vs transformers generate (bf16 both sides)."""
     from swh_trl_amd.engine import DecodeEngine

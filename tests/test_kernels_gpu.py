@@ -542,3 +542,46 @@ def test_attn_decode(ops, dev, D, Hq, Hkv):
     before = kcd.clone()
     out2 = nn_ops.attn_decode(qkv.to(dev), kcd, vcd, cos, sin, plen.to(dev), bad, Hq, Hkv, D, D ** -0.5)
     assert torch.isnan(out2.float()).all() and torch.equal(before, kcd)
+
+
+# --------------------------------------------------------------------------- fused decode GEMM
+def _ref_norm(x, w, eps):
+    xf = x.float()
+    n = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)).to(torch.bfloat16)
+    return (w * n)  # bf16 * bf16 -> bf16 (transformers Qwen2RMSNorm)
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 1152, 896), (5, 896, 896), (130, 256, 4864), (64, 151936, 896)])
+@pytest.mark.parametrize("norm", [False, True])
+def test_decode_gemm_plain(ops, dev, M, N, K, norm):
+    from swh_trl_amd import nn_ops
+    g = _gen(30)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(dev)
+    nw = (1 + 0.1 * torch.randn(K, generator=g)).to(torch.bfloat16).to(dev)
+    b = torch.randn(N, generator=g).to(torch.bfloat16).to(dev) if N == 1152 else None
+    y = nn_ops.decode_gemm(x, w, norm_w=nw if norm else None, eps=1e-6, bias=b)
+    xa = _ref_norm(x, nw, 1e-6) if norm else x
+    ref = xa.float() @ w.float().t()
+    if b is not None:
+        ref = ref + b.float()
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2)
+
+
+def test_decode_gemm_residual_and_silu(ops, dev):
+    from swh_trl_amd import nn_ops
+    g = _gen(31)
+    M, H, I = 64, 896, 4864
+    s = torch.randn(M, H, generator=g).to(torch.bfloat16).to(dev)
+    a = torch.randn(M, I, generator=g).to(torch.bfloat16).to(dev)
+    wd = (torch.randn(H, I, generator=g) * I ** -0.5).to(torch.bfloat16).to(dev)
+    s0 = s.clone()
+    nn_ops.decode_gemm(a, wd, residual=s)
+    ref = s0 + (a.float() @ wd.float().t()).to(torch.bfloat16)
+    torch.testing.assert_close(s.float(), ref.float(), rtol=1e-2, atol=2e-2)
+    wgu = (torch.randn(2 * I, H, generator=g) * H ** -0.5).to(torch.bfloat16).to(dev)
+    nw = (1 + 0.1 * torch.randn(H, generator=g)).to(torch.bfloat16).to(dev)
+    act = nn_ops.decode_gemm(s, wgu, norm_w=nw, eps=1e-6, silu=True)
+    gu = (_ref_norm(s, nw, 1e-6).float() @ wgu.float().t()).to(torch.bfloat16)
+    ref = torch.nn.functional.silu(gu[:, :I]) * gu[:, I:]
+    torch.testing.assert_close(act.float(), ref.float(), rtol=2e-2, atol=2e-2)
