@@ -264,9 +264,14 @@ int swh_attn_decode(const void *qkv, void *k_cache, void *v_cache, const float *
  *                     (row stride ldy; y unused)
  *   silu != 0      : W has 2N rows (gate then up); y = bf16(bf16(silu(g)) * u)
  * Replaces the transformers q/k/v, o, gate/up, down and lm-head projections of
- * one decode step (plus their RMSNorm / SiLU / residual neighbours). */
+ * one decode step (plus their RMSNorm / SiLU / residual neighbours).
+ * Small-N shapes split K over workgroups; the workspace (>=
+ * swh_decode_gemm_workspace_bytes, ZEROED once at allocation, self-resetting
+ * afterwards) holds the split counters and fp32 partial slabs. */
+int64_t swh_decode_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K);
 int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, const void *norm_w, float eps,
-                    const void *bias, void *residual, int32_t silu, void *y, int64_t ldy, void *stream);
+                    const void *bias, void *residual, int32_t silu, void *y, int64_t ldy, void *workspace,
+                    int64_t workspace_bytes, void *stream);
 
 #ifdef __cplusplus
 }

@@ -47,52 +47,80 @@ __device__ __forceinline__ uint4 norm_frag(const uint4 &xv, const uint4 &wv, flo
 }
 
 // NB = output columns per workgroup (multiple of 16); CB = NB / 16 column blocks.
+// grid = (column blocks, M tiles, S k-splits).  The 4*S waves of a column
+// block split its K/32 k-steps evenly.  S > 1: every workgroup publishes its
+// [64 x NB] fp32 partial with write-through (sc1) stores, drains, and one lane
+// takes a ticket on the block's counter (agent-scope atomic); the workgroup
+// that draws S-1 sums the S slabs in fixed order (sc1 loads: deterministic,
+// placement-independent — MI355X_MICROARCH.md §Workgroup dispatch, table row 1)
+// and runs the epilogue, then resets the counter for the next launch.
+constexpr int kU = 4;  // k-steps whose loads are issued together
+constexpr int kMaxNormK = 8192;
+constexpr int64_t kCounterBytes = 1 << 16;  // split-K ticket counters (16384 column blocks)
+
 template <int NB, bool NORM, int EPI, bool BIAS>
 __global__ __launch_bounds__(kGemmThreads) void decode_gemm_kernel(
     const uint16_t *__restrict__ x, const uint16_t *__restrict__ w, int M, int N, int K,
     const uint16_t *__restrict__ norm_w, float eps, const uint16_t *__restrict__ bias, uint16_t *__restrict__ res,
-    uint16_t *__restrict__ y, int ldy) {
+    uint16_t *__restrict__ y, int ldy, float *__restrict__ slabs, int *__restrict__ counters) {
     constexpr int CB = NB / 16;
     __shared__ float rstd_s[kRows];
     __shared__ float part[4][kRows][NB + 1];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __shared__ uint4 nw_s[NORM ? kMaxNormK / 8 : 1];  // RMSNorm weight, staged once
+    __shared__ int last_s;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int S = gridDim.z, sidx = blockIdx.z;
     const int m0 = blockIdx.y * kRows;
     const int n0 = blockIdx.x * (EPI == EPI_SILU ? NB / 2 : NB);
 
-    // ---- prologue: per-row rstd of X (fused RMSNorm)
+    // ---- prologue: per-row rstd of X, 4 threads per row, loads issued in bulk
     if constexpr (NORM) {
-        for (int rr = wid; rr < kRows; rr += 4) {
-            const int r = min(m0 + rr, M - 1);
-            const uint4 *xr = reinterpret_cast<const uint4 *>(x + (int64_t)r * K);
-            float ss = 0.f;
-            for (int v = lane; v < K / 8; v += 64) {
+        const int r = tid >> 2, q = tid & 3;
+        const int gr = min(m0 + r, M - 1);
+        const int nv = K / 8, v0 = q * (nv / 4), v1 = (q == 3) ? nv : v0 + nv / 4;
+        const uint4 *xr = reinterpret_cast<const uint4 *>(x + (int64_t)gr * K);
+        float ss = 0.f;
+        int v = v0;
+        for (; v + 8 <= v1; v += 8) {
+            uint4 t[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) t[u] = xr[v + u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
                 float a[8];
-                unpack16<SWH_BF16>(xr[v], a);
+                unpack16<SWH_BF16>(t[u], a);
 #pragma unroll
                 for (int k = 0; k < 8; ++k) ss = fmaf(a[k], a[k], ss);
             }
-            ss = wave_sum(ss);
-            if (lane == 0) rstd_s[rr] = rsqrtf(ss / (float)K + eps);
         }
+        for (; v < v1; ++v) {
+            float a[8];
+            unpack16<SWH_BF16>(xr[v], a);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) ss = fmaf(a[k], a[k], ss);
+        }
+        ss += __shfl_xor(ss, 1, kWave);
+        ss += __shfl_xor(ss, 2, kWave);
+        if (q == 0) rstd_s[r] = rsqrtf(ss / (float)K + eps);
+        for (int i = tid; i < K / 8; i += kGemmThreads) nw_s[i] = reinterpret_cast<const uint4 *>(norm_w)[i];
         __syncthreads();
     }
 
-    // ---- main loop: wave `wid` owns k in [kb, ke)
-    const int kw = K / 4;
-    const int kb = wid * kw, ke = kb + kw;
-    const int rl = lane & 15, kq = (lane >> 4) * 8;  // fragment row/col within 16, k offset within 32
+    // ---- main loop over this wave's k-steps
+    const int KS = K / 32, parts = 4 * S, pidx = sidx * 4 + wid;
+    const int ks0 = (int)((int64_t)KS * pidx / parts), ks1 = (int)((int64_t)KS * (pidx + 1) / parts);
+    const int rl = lane & 15, kq = (lane >> 4) * 8;
     f32x4 acc[4][CB];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < CB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
     const uint16_t *xrow[4];
     float rs[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int r = min(m0 + i * 16 + rl, M - 1);
-        xrow[i] = x + (int64_t)r * K;
+        xrow[i] = x + (int64_t)r * K + kq;
         rs[i] = NORM ? rstd_s[i * 16 + rl] : 1.f;
     }
     const uint16_t *wrow[CB];
@@ -100,38 +128,54 @@ __global__ __launch_bounds__(kGemmThreads) void decode_gemm_kernel(
     for (int j = 0; j < CB; ++j) {
         int n;
         if constexpr (EPI == EPI_SILU) {
-            // column block j: first 8 columns gate rows, last 8 the matching up rows
             const int c = j * 8 + (rl & 7);
             n = (rl < 8) ? n0 + c : N + n0 + c;
         } else {
             n = n0 + j * 16 + rl;
         }
-        wrow[j] = w + (int64_t)n * K;
+        wrow[j] = w + (int64_t)n * K + kq;
     }
-
-#pragma unroll 2
-    for (int k0 = kb; k0 < ke; k0 += 32) {
-        const int k = k0 + kq;
-        uint4 bv[CB];
-#pragma unroll
-        for (int j = 0; j < CB; ++j) bv[j] = ld_nt(reinterpret_cast<const uint4 *>(wrow[j] + k));
-        uint4 av[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) av[i] = *reinterpret_cast<const uint4 *>(xrow[i] + k);
+    auto mma_step = [&](const uint4 (&av)[4], const uint4 (&bv)[CB], int kk) {
+        uint4 a2[4];
         if constexpr (NORM) {
-            const uint4 nw = *reinterpret_cast<const uint4 *>(norm_w + k);
+            const uint4 nw = nw_s[(kk + kq) >> 3];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) av[i] = norm_frag(av[i], nw, rs[i]);
+            for (int i = 0; i < 4; ++i) a2[i] = norm_frag(av[i], nw, rs[i]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a2[i] = av[i];
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < CB; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(av[i]), as_bf16x8(bv[j]), acc[i][j],
-                                                                    0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a2[i]), as_bf16x8(bv[j]), acc[i][j], 0,
+                                                                    0, 0);
+    };
+    int ks = ks0;
+    for (; ks + kU <= ks1; ks += kU) {
+        uint4 bv[kU][CB], av[kU][4];
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+#pragma unroll
+            for (int j = 0; j < CB; ++j) bv[u][j] = ld_nt(reinterpret_cast<const uint4 *>(wrow[j] + (ks + u) * 32));
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) av[u][i] = *reinterpret_cast<const uint4 *>(xrow[i] + (ks + u) * 32);
+#pragma unroll
+        for (int u = 0; u < kU; ++u) mma_step(av[u], bv[u], (ks + u) * 32);
+    }
+    for (; ks < ks1; ++ks) {
+        uint4 bv[CB], av[4];
+#pragma unroll
+        for (int j = 0; j < CB; ++j) bv[j] = ld_nt(reinterpret_cast<const uint4 *>(wrow[j] + ks * 32));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) av[i] = *reinterpret_cast<const uint4 *>(xrow[i] + ks * 32);
+        mma_step(av, bv, ks * 32);
     }
 
-    // ---- cross-wave split-K merge in LDS
+    // ---- merge the 4 waves in LDS -> part[0]
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -139,33 +183,57 @@ __global__ __launch_bounds__(kGemmThreads) void decode_gemm_kernel(
 #pragma unroll
             for (int e = 0; e < 4; ++e) part[wid][i * 16 + (lane >> 4) * 4 + e][j * 16 + rl] = acc[i][j][e];
     __syncthreads();
+    for (int idx = tid; idx < kRows * NB; idx += kGemmThreads) {
+        const int r = idx / NB, c = idx - r * NB;
+        part[0][r][c] = part[0][r][c] + part[1][r][c] + part[2][r][c] + part[3][r][c];
+    }
+    __syncthreads();
+
+    // ---- cross-workgroup split-K: publish, ticket, last arriver reduces
+    if (S > 1) {
+        const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+        float *my = slabs + ((int64_t)blk * S + sidx) * (kRows * NB);
+        for (int idx = tid; idx < kRows * NB; idx += kGemmThreads)
+            __hip_atomic_store(my + idx, part[0][idx / NB][idx % NB], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            const int t = __hip_atomic_fetch_add(counters + blk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last_s = (t == S - 1);
+        }
+        __syncthreads();
+        if (!last_s) return;
+        const float *base = slabs + (int64_t)blk * S * (kRows * NB);
+        for (int idx = tid; idx < kRows * NB; idx += kGemmThreads) {
+            float v = 0.f;
+            for (int q = 0; q < S; ++q)
+                v += __hip_atomic_load(base + (int64_t)q * kRows * NB + idx, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            part[0][idx / NB][idx % NB] = v;
+        }
+        if (tid == 0) __hip_atomic_store(counters + blk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+    }
 
     // ---- epilogue
     if constexpr (EPI == EPI_SILU) {
-        constexpr int NO = NB / 2;  // output columns of this tile
-        for (int idx = threadIdx.x; idx < kRows * NO; idx += kGemmThreads) {
+        constexpr int NO = NB / 2;
+        for (int idx = tid; idx < kRows * NO; idx += kGemmThreads) {
             const int r = idx / NO, c = idx - r * NO;
             const int gr = m0 + r;
             if (gr >= M) continue;
             const int jb = c / 8, cc = c - jb * 8;
-            const int cg = jb * 16 + cc, cu = cg + 8;
-            float g = 0.f, u = 0.f;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                g += part[q][r][cg];
-                u += part[q][r][cu];
-            }
-            g = round_bf16(g);
-            u = round_bf16(u);
+            const int cg = jb * 16 + cc;
+            const float g = round_bf16(part[0][r][cg]), u = round_bf16(part[0][r][cg + 8]);
             const float a = round_bf16(g / (1.f + expf(-g))) * u;
             y[(int64_t)gr * ldy + n0 + c] = f32_to_bf16_bits(a);
         }
     } else {
-        for (int idx = threadIdx.x; idx < kRows * NB; idx += kGemmThreads) {
+        for (int idx = tid; idx < kRows * NB; idx += kGemmThreads) {
             const int r = idx / NB, c = idx - r * NB;
             const int gr = m0 + r, gc = n0 + c;
             if (gr >= M || gc >= N) continue;
-            float v = part[0][r][c] + part[1][r][c] + part[2][r][c] + part[3][r][c];
+            float v = part[0][r][c];
             if constexpr (BIAS) v += bf16_bits_to_f32(bias[gc]);
             if constexpr (EPI == EPI_RESIDUAL) {
                 uint16_t *s = res + (int64_t)gr * ldy + gc;
@@ -386,15 +454,36 @@ extern "C" int swh_attn_decode(const void *qkv, void *k_cache, void *v_cache, co
     return SWH_E_ARG;
 }
 
+extern "C" int64_t swh_decode_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K) {
+    const int64_t mt = (M + kRows - 1) / kRows;
+    const int64_t ncb = (N + 15) / 16;
+    const int64_t S = 16;  // upper bound of the split the host picks
+    return kCounterBytes + mt * ncb * S * kRows * 16 * (int64_t)sizeof(float);
+    (void)K;
+}
+
+namespace swh {
+namespace {
+// split-K factor: aim at >= ~384 workgroups with >= 2 k-steps per wave
+int pick_split(int64_t blocks, int64_t K) {
+    const int64_t KS = K / 32;
+    int64_t S = (384 + blocks - 1) / blocks;
+    if (S > KS / 8) S = KS / 8;
+    if (S > 16) S = 16;
+    return S < 1 ? 1 : (int)S;
+}
+}  // namespace
+}  // namespace swh
+
 extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, const void *norm_w,
                                float eps, const void *bias, void *residual, int32_t silu, void *y, int64_t ldy,
-                               void *stream) {
-    if (!x || !w || M <= 0 || N <= 0 || K <= 0 || K % 128 || M > (1 << 20) || N >= (1 << 30) || K >= (1 << 30))
+                               void *workspace, int64_t workspace_bytes, void *stream) {
+    if (!x || !w || M <= 0 || N <= 0 || K <= 0 || K % 32 || M > (1 << 20) || N >= (1 << 30) || K >= (1 << 30))
         return SWH_E_ARG;
     if (residual && (silu || bias)) return SWH_E_ARG;
     if (!residual && !y) return SWH_E_ARG;
     if (((uintptr_t)x | (uintptr_t)w) & 15) return SWH_E_ARG;
-    if (norm_w && ((uintptr_t)norm_w & 15)) return SWH_E_ARG;
+    if (norm_w && (((uintptr_t)norm_w & 15) || K > kMaxNormK)) return SWH_E_ARG;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const auto *X = static_cast<const uint16_t *>(x);
     const auto *W = static_cast<const uint16_t *>(w);
@@ -404,37 +493,53 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
     auto *Y = static_cast<uint16_t *>(y);
     const unsigned gy = (unsigned)((M + kRows - 1) / kRows);
     const int m = (int)M, n = (int)N, k = (int)K, ld = (int)ldy;
+    // workspace: [counters (zeroed, int32) | slabs (fp32)]
+    int *ctr = static_cast<int *>(workspace);
+    float *slab = nullptr;
+    auto prep = [&](int64_t blocks, int S, int nb) -> bool {
+        if (S == 1) return true;
+        const int64_t need = kCounterBytes + blocks * gy * S * kRows * nb * 4;
+        if (blocks * gy * (int64_t)sizeof(int) > kCounterBytes) return false;
+        if (!workspace || workspace_bytes < need) return false;
+        // counters live in a FIXED region at the start (never overlapped by any
+        // call's slabs, whatever its shape), so a self-reset counter stays zero
+        slab = reinterpret_cast<float *>(static_cast<char *>(workspace) + kCounterBytes);
+        return true;
+    };
+#define SWH_GEMM(NB_, NORM_, EPI_, BIAS_, GX, S_)                                                                  \
+    decode_gemm_kernel<NB_, NORM_, EPI_, BIAS_><<<dim3((unsigned)(GX), gy, (unsigned)(S_)), kGemmThreads, 0, s>>>( \
+        X, W, m, n, k, NW, eps, Bs, R, Y, ld, slab, ctr)
     if (silu) {
-        // W holds 2N rows (gate then up); each tile produces 8 outputs per 16-column block
         if (N % 8) return SWH_E_ARG;
-        constexpr int NB = 16;
-        const dim3 grid((unsigned)(N / (NB / 2)), gy);
-        if (NW) decode_gemm_kernel<NB, true, EPI_SILU, false><<<grid, kGemmThreads, 0, s>>>(X, W, m, n, k, NW, eps, nullptr, nullptr, Y, ld);
-        else decode_gemm_kernel<NB, false, EPI_SILU, false><<<grid, kGemmThreads, 0, s>>>(X, W, m, n, k, NW, eps, nullptr, nullptr, Y, ld);
-        return launch_status();
-    }
-    if (residual) {
-        constexpr int NB = 16;
-        const dim3 grid((unsigned)((N + NB - 1) / NB), gy);
-        if (N % 16) return SWH_E_ARG;
-        if (NW) decode_gemm_kernel<NB, true, EPI_RESIDUAL, false><<<grid, kGemmThreads, 0, s>>>(X, W, m, n, k, NW, eps, nullptr, R, nullptr, ld);
-        else decode_gemm_kernel<NB, false, EPI_RESIDUAL, false><<<grid, kGemmThreads, 0, s>>>(X, W, m, n, k, NW, eps, nullptr, R, nullptr, ld);
+        const int64_t blocks = N / 8;
+        const int S = pick_split(blocks, K);
+        if (!prep(blocks, S, 16)) return SWH_E_ARG;
+        if (NW) SWH_GEMM(16, true, EPI_SILU, false, blocks, S);
+        else SWH_GEMM(16, false, EPI_SILU, false, blocks, S);
         return launch_status();
     }
     if (N % 16) return SWH_E_ARG;
-    if (N >= 65536) {  // lm head: wide tiles keep the L2 re-reads of X below the W stream
-        constexpr int NB = 64;
-        if (N % NB) return SWH_E_ARG;
-        const dim3 grid((unsigned)(N / NB), gy);
-        if (NW) decode_gemm_kernel<NB, true, EPI_PLAIN, false><<<grid, kGemmThreads, 0, s>>>(X, W, m, n, k, NW, eps, nullptr, nullptr, Y, ld);
-        else decode_gemm_kernel<NB, false, EPI_PLAIN, false><<<grid, kGemmThreads, 0, s>>>(X, W, m, n, k, NW, eps, nullptr, nullptr, Y, ld);
+    if (residual) {
+        const int64_t blocks = N / 16;
+        const int S = pick_split(blocks, K);
+        if (!prep(blocks, S, 16)) return SWH_E_ARG;
+        if (NW) SWH_GEMM(16, true, EPI_RESIDUAL, false, blocks, S);
+        else SWH_GEMM(16, false, EPI_RESIDUAL, false, blocks, S);
         return launch_status();
     }
-    constexpr int NB = 16;
-    const dim3 grid((unsigned)(N / NB), gy);
-    if (NW && Bs) decode_gemm_kernel<NB, true, EPI_PLAIN, true><<<grid, kGemmThreads, 0, s>>>(X, W, m, n, k, NW, eps, Bs, nullptr, Y, ld);
-    else if (NW) decode_gemm_kernel<NB, true, EPI_PLAIN, false><<<grid, kGemmThreads, 0, s>>>(X, W, m, n, k, NW, eps, nullptr, nullptr, Y, ld);
-    else if (Bs) decode_gemm_kernel<NB, false, EPI_PLAIN, true><<<grid, kGemmThreads, 0, s>>>(X, W, m, n, k, NW, eps, Bs, nullptr, Y, ld);
-    else decode_gemm_kernel<NB, false, EPI_PLAIN, false><<<grid, kGemmThreads, 0, s>>>(X, W, m, n, k, NW, eps, nullptr, nullptr, Y, ld);
+    if (N >= 65536 && N % 64 == 0) {  // lm head: wide tiles keep X re-reads below the W stream
+        const int64_t blocks = N / 64;
+        if (NW) SWH_GEMM(64, true, EPI_PLAIN, false, blocks, 1);
+        else SWH_GEMM(64, false, EPI_PLAIN, false, blocks, 1);
+        return launch_status();
+    }
+    const int64_t blocks = N / 16;
+    const int S = pick_split(blocks, K);
+    if (!prep(blocks, S, 16)) return SWH_E_ARG;
+    if (NW && Bs) SWH_GEMM(16, true, EPI_PLAIN, true, blocks, S);
+    else if (NW) SWH_GEMM(16, true, EPI_PLAIN, false, blocks, S);
+    else if (Bs) SWH_GEMM(16, false, EPI_PLAIN, true, blocks, S);
+    else SWH_GEMM(16, false, EPI_PLAIN, false, blocks, S);
+#undef SWH_GEMM
     return launch_status();
 }

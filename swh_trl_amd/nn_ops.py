@@ -114,9 +114,20 @@ def attn_decode(qkv: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
     return out
 
 
+_GEMM_WS: dict = {}
+
+
+def gemm_workspace(device, nbytes: int = 64 << 20) -> torch.Tensor:
+    """Zero-initialised split-K workspace (counters reset themselves after use)."""
+    key = (str(device), nbytes)
+    if key not in _GEMM_WS:
+        _GEMM_WS[key] = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+    return _GEMM_WS[key]
+
+
 def decode_gemm(x: torch.Tensor, w: torch.Tensor, *, norm_w: Optional[torch.Tensor] = None, eps: float = 1e-6,
                 bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None, silu: bool = False,
-                y: Optional[torch.Tensor] = None) -> torch.Tensor:
+                y: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Weight-streaming decode GEMM with fused RMSNorm prologue and bias /
     residual / SiLU-gate epilogues (include/swh_trl_amd.h swh_decode_gemm).
     x [M, K] bf16; w [N, K] (or [2N, K] with silu)."""
@@ -126,6 +137,7 @@ def decode_gemm(x: torch.Tensor, w: torch.Tensor, *, norm_w: Optional[torch.Tens
     if residual is None and y is None:
         y = torch.empty(M, N, device=x.device, dtype=x.dtype)
     ldy = residual.stride(0) if residual is not None else y.stride(0)
+    ws = workspace if workspace is not None else gemm_workspace(x.device)
     call("swh_decode_gemm", x.data_ptr(), w.data_ptr(), M, N, K, _p(norm_w), float(eps), _p(bias), _p(residual),
-         int(bool(silu)), _p(y), ldy, _stream())
+         int(bool(silu)), _p(y), ldy, ws.data_ptr(), ws.numel(), _stream())
     return residual if residual is not None else y

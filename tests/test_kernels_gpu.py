@@ -585,3 +585,16 @@ def test_decode_gemm_residual_and_silu(ops, dev):
     gu = (_ref_norm(s, nw, 1e-6).float() @ wgu.float().t()).to(torch.bfloat16)
     ref = torch.nn.functional.silu(gu[:, :I]) * gu[:, I:]
     torch.testing.assert_close(act.float(), ref.float(), rtol=2e-2, atol=2e-2)
+
+
+def test_decode_gemm_split_k_is_deterministic_across_launches(ops, dev):
+    """The cross-workgroup split-K reduction sums slabs in a fixed order and
+    resets its counters: repeated launches give bit-identical results."""
+    from swh_trl_amd import nn_ops
+    g = _gen(32)
+    x = torch.randn(64, 4864, generator=g).to(torch.bfloat16).to(dev)
+    w = (torch.randn(896, 4864, generator=g) * 0.02).to(torch.bfloat16).to(dev)
+    outs = [nn_ops.decode_gemm(x, w).clone() for _ in range(4)]
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    torch.testing.assert_close(outs[0].float(), x.float() @ w.float().t(), rtol=1e-2, atol=1e-2)
