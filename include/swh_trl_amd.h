@@ -239,8 +239,11 @@ int swh_rmsnorm_bwd(const void *x, const void *weight, const float *rstd, const 
 /* out[r, i] = bf16(bf16(silu(gu[r, i])) * gu[r, I + i]) — gate/up packed. */
 int swh_silu_mul_fwd(const void *gu, int64_t rows, int64_t I, void *out, void *stream);
 int swh_silu_mul_bwd(const void *gu, const void *dout, int64_t rows, int64_t I, void *dgu, void *stream);
-/* x[b, :] = table[ids[b], :] (bf16 rows of width H). */
-int swh_embed_gather(const void *table, const int64_t *ids, int64_t B, int64_t H, void *x, void *stream);
+/* x[b, :] = table[ids[b], :] (bf16 rows of width H, H % 16 == 0); ss_out f32
+ * [B, H/16] nullable: per 16-column chunk sums of squares of each row (the
+ * RMSNorm statistic swh_decode_gemm takes as ss_in). */
+int swh_embed_gather(const void *table, const int64_t *ids, int64_t B, int64_t H, void *x, float *ss_out,
+                     void *stream);
 /* One decode step of attention for every sequence.  state = device int32[2]
  * {s, P}: s is the index of the token the sampler produces in this step (the
  * same counter swh_sample_step reads), so the attention input is token s-1:
@@ -257,11 +260,15 @@ int swh_attn_decode(const void *qkv, void *k_cache, void *v_cache, const float *
                     void *stream);
 
 /* Weight-streaming decode GEMM Y[M,N] = X[M,K] W[N,K]^T (bf16, fp32 MFMA
- * accumulation, K % 128 == 0) with the decoder's neighbours fused:
- *   norm_w != NULL : X is replaced by RMSNorm(X) * norm_w (eps) in the prologue
+ * accumulation, K % 64 == 0, 16-B aligned operands, ldy % 8 == 0) with the
+ * decoder's neighbours fused:
+ *   norm_w != NULL : X is replaced by RMSNorm(X) * norm_w (eps) in the prologue;
+ *                    ss_in f32 [M, K/16] (nullable) = the producer's per
+ *                    16-column chunk sums of squares of X (else computed here)
  *   bias   != NULL : + bias[N]
  *   residual != NULL: residual[M,N] = bf16(residual + bf16(XW^T)) in place
- *                     (row stride ldy; y unused)
+ *                     (row stride ldy; y unused); ss_out f32 [M, N/16]
+ *                     (nullable) receives the new rows' chunk sums of squares
  *   silu != 0      : W has 2N rows (gate then up); y = bf16(bf16(silu(g)) * u)
  * Replaces the transformers q/k/v, o, gate/up, down and lm-head projections of
  * one decode step (plus their RMSNorm / SiLU / residual neighbours).
@@ -270,8 +277,8 @@ int swh_attn_decode(const void *qkv, void *k_cache, void *v_cache, const float *
  * afterwards) holds the split counters and fp32 partial slabs. */
 int64_t swh_decode_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K);
 int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, const void *norm_w, float eps,
-                    const void *bias, void *residual, int32_t silu, void *y, int64_t ldy, void *workspace,
-                    int64_t workspace_bytes, void *stream);
+                    const void *bias, void *residual, int32_t silu, void *y, int64_t ldy, const float *ss_in,
+                    float *ss_out, void *workspace, int64_t workspace_bytes, void *stream);
 
 #ifdef __cplusplus
 }

@@ -14,6 +14,11 @@ run() {  # name timeout cmd...
 for step in "$@"; do
   case $step in
     kern) run kern 600 python -m pytest tests/test_kernels_gpu.py -q -m gpu ;;
+    kernx) run kernx 600 python -m pytest tests/test_kernels_gpu.py -q -m gpu -x ;;
+    dec) run dec 300 python tools/bench_decode.py ;;
+    sweep) run sweep 300 python tools/bench_decode.py --sweep ;;
+    probe) run probe 300 python tools/gemm_probe.py ;;
+    profdec) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null && run profdec 400 rocprofv3 --kernel-trace --stats -d gpurun_out/profdec -o run --output-format csv -- python3 tools/bench_decode.py ;;
     engine) run engine 600 python -m pytest tests/test_engine_gpu.py -q -m gpu -x ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py --steps 3 --warmup 2 ;;

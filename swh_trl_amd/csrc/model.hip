@@ -173,14 +173,32 @@ __global__ __launch_bounds__(256) void silu_mul_bwd_kernel(const uint16_t *__res
     }
 }
 
+// ss_out (nullable): per 16-column chunk sums of squares of the gathered row,
+// the RMSNorm statistic the decode GEMM prologue consumes (swh_decode_gemm ss_in)
 __global__ __launch_bounds__(256) void embed_gather_kernel(const uint16_t *__restrict__ table,
                                                            const int64_t *__restrict__ ids, int64_t H,
-                                                           uint16_t *__restrict__ x) {
+                                                           uint16_t *__restrict__ x, float *__restrict__ ss_out) {
     const int64_t b = blockIdx.x;
     const int64_t id = ids[b];
-    const int64_t nv = H / 8;
-    for (int64_t v = threadIdx.x; v < nv; v += blockDim.x)
-        reinterpret_cast<uint4 *>(x + b * H)[v] = reinterpret_cast<const uint4 *>(table + id * H)[v];
+    const int64_t nch = H / 16;
+    for (int64_t c = threadIdx.x; c < nch; c += blockDim.x) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(table + id * H) + 2 * c;
+        const uint4 lo = src[0], hi = src[1];
+        uint4 *dst = reinterpret_cast<uint4 *>(x + b * H) + 2 * c;
+        dst[0] = lo;
+        dst[1] = hi;
+        if (ss_out) {
+            float a[8], e[8];
+            unpack16<SWH_BF16>(lo, a);
+            unpack16<SWH_BF16>(hi, e);
+            float ss = 0.f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) ss = fmaf(a[k], a[k], ss);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) ss = fmaf(e[k], e[k], ss);
+            ss_out[b * nch + c] = ss;
+        }
+    }
 }
 
 }  // namespace
@@ -234,10 +252,11 @@ extern "C" int swh_silu_mul_bwd(const void *gu, const void *dout, int64_t rows, 
     return launch_status();
 }
 
-extern "C" int swh_embed_gather(const void *table, const int64_t *ids, int64_t B, int64_t H, void *x, void *stream) {
-    if (!table || !ids || !x || B < 0 || H <= 0 || H % 8) return SWH_E_ARG;
+extern "C" int swh_embed_gather(const void *table, const int64_t *ids, int64_t B, int64_t H, void *x, float *ss_out,
+                                void *stream) {
+    if (!table || !ids || !x || B < 0 || H <= 0 || H % 16) return SWH_E_ARG;
     if (B == 0) return SWH_OK;
     embed_gather_kernel<<<dim3((unsigned)B), 128, 0, static_cast<hipStream_t>(stream)>>>(
-        static_cast<const uint16_t *>(table), ids, H, static_cast<uint16_t *>(x));
+        static_cast<const uint16_t *>(table), ids, H, static_cast<uint16_t *>(x), ss_out);
     return launch_status();
 }

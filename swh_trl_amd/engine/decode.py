@@ -49,6 +49,7 @@ class DecodeEngine:
         self.act = torch.empty(B, c.intermediate_size, **bf)
         self.d = torch.empty(B, H, **bf)
         self.logits_buf = torch.empty(B, c.vocab_size, **bf)
+        self.ss = torch.empty(B, H // 16, device=dev, dtype=torch.float32)  # RMSNorm partial sums of s
         self.state = torch.zeros(2, device=dev, dtype=torch.int32)   # {step, P}
         self.rng = torch.zeros(2, device=dev, dtype=torch.int64)     # {seed, counter base}
         self.finished = torch.zeros(B, device=dev, dtype=torch.int32)
@@ -85,17 +86,19 @@ class DecodeEngine:
         c, m = self.cfg, self.model
         p = m.p
         eps = c.rms_norm_eps
-        nn_ops.embed_gather(p["embed"], self.cur, self.s)
+        ss = self.ss  # every producer of s writes its RMSNorm partial sums, every normed GEMM reads them
+        nn_ops.embed_gather(p["embed"], self.cur, self.s, ss_out=ss)
         for i in range(c.num_hidden_layers):
             nn_ops.decode_gemm(self.s, p[f"l{i}.qkv_w"], norm_w=p[f"l{i}.ln_in"], eps=eps,
-                               bias=p.get(f"l{i}.qkv_b"), y=self.qkv)
+                               bias=p.get(f"l{i}.qkv_b"), y=self.qkv, ss_in=ss)
             nn_ops.attn_decode(self.qkv, self.kv[i, 0], self.kv[i, 1], self.cos, self.sin, self.plen, self.state,
                                c.num_attention_heads, c.num_key_value_heads, c.head_dim, c.head_dim ** -0.5,
                                out=self.att)
-            nn_ops.decode_gemm(self.att, p[f"l{i}.o_w"], residual=self.s)
-            nn_ops.decode_gemm(self.s, p[f"l{i}.gu_w"], norm_w=p[f"l{i}.ln_post"], eps=eps, silu=True, y=self.act)
-            nn_ops.decode_gemm(self.act, p[f"l{i}.down_w"], residual=self.s)
-        nn_ops.decode_gemm(self.s, m.lm_weight(), norm_w=p["norm"], eps=eps, y=self.logits_buf)
+            nn_ops.decode_gemm(self.att, p[f"l{i}.o_w"], residual=self.s, ss_out=ss)
+            nn_ops.decode_gemm(self.s, p[f"l{i}.gu_w"], norm_w=p[f"l{i}.ln_post"], eps=eps, silu=True, y=self.act,
+                               ss_in=ss)
+            nn_ops.decode_gemm(self.act, p[f"l{i}.down_w"], residual=self.s, ss_out=ss)
+        nn_ops.decode_gemm(self.s, m.lm_weight(), norm_w=p["norm"], eps=eps, y=self.logits_buf, ss_in=ss)
 
     def _step_unfused(self):
         c, m = self.cfg, self.model
@@ -153,6 +156,81 @@ class DecodeEngine:
             t.copy_(v)
         self.kv.copy_(kv_saved)
         del kv_saved
+
+    # ------------------------------------------------------------------ live kernel timing
+    @torch.no_grad()
+    def kernel_timings(self, step_index: int, reps: int = 20, iters: int = 3) -> dict:
+        """Device time of each kernel of one fused decode step at sampler index
+        `step_index` (attention over P + step_index keys), plus the whole step.
+        Each op is captured `reps` times into a HIP graph and replayed `iters`
+        times between HIP events on the capture stream, so a figure is the
+        kernel plus its in-graph launch boundary (what the decode graph pays).
+        Clobbers the decode scratch buffers and one cache slot: call between
+        generations.  Returns {name: {avg_us, bytes_per_launch,
+        launches_per_step}}; bytes are algorithmic."""
+        if not self.fused:
+            raise RuntimeError("kernel_timings needs the fused decode path")
+        c, m = self.cfg, self.model
+        p = m.p
+        eps, B, H, I = c.rms_norm_eps, self.B, c.hidden_size, c.intermediate_size
+        L = c.num_hidden_layers
+        P = int(self.state[1])
+        self.state[0] = step_index
+        keys = P + step_index  # upper bound over rows (left padding shortens some)
+        bf = 2
+        att_bytes = B * c.num_key_value_heads * keys * c.head_dim * bf * 2 + B * (c.qkv_dim + c.q_dim) * bf
+
+        def gemm_bytes(N, K, silu=False):
+            wN = 2 * N if silu else N
+            return wN * K * bf + B * K * bf + B * N * bf * (2 if not silu and N == H else 1)
+
+        ss = self.ss
+        ops_ = {
+            "decode_gemm.qkv": (lambda: nn_ops.decode_gemm(self.s, p["l0.qkv_w"], norm_w=p["l0.ln_in"], eps=eps,
+                                                           bias=p.get("l0.qkv_b"), y=self.qkv, ss_in=ss),
+                                gemm_bytes(c.qkv_dim, H), L),
+            "attn_decode": (lambda: nn_ops.attn_decode(self.qkv, self.kv[0, 0], self.kv[0, 1], self.cos, self.sin,
+                                                       self.plen, self.state, c.num_attention_heads,
+                                                       c.num_key_value_heads, c.head_dim, c.head_dim ** -0.5,
+                                                       out=self.att),
+                            att_bytes, L),
+            "decode_gemm.o": (lambda: nn_ops.decode_gemm(self.att, p["l0.o_w"], residual=self.s, ss_out=ss),
+                              gemm_bytes(H, c.q_dim), L),
+            "decode_gemm.gate_up": (lambda: nn_ops.decode_gemm(self.s, p["l0.gu_w"], norm_w=p["l0.ln_post"], eps=eps,
+                                                               silu=True, y=self.act, ss_in=ss),
+                                    gemm_bytes(I, H, silu=True), L),
+            "decode_gemm.down": (lambda: nn_ops.decode_gemm(self.act, p["l0.down_w"], residual=self.s, ss_out=ss),
+                                 gemm_bytes(H, I), L),
+            "decode_gemm.lm_head": (lambda: nn_ops.decode_gemm(self.s, m.lm_weight(), norm_w=p["norm"], eps=eps,
+                                                               y=self.logits_buf, ss_in=ss),
+                                    c.vocab_size * H * bf + B * c.vocab_size * bf, 1),
+            "sample_step": (self._sample, B * c.vocab_size * bf, 1),
+        }
+        nn_ops.embed_gather(p["embed"], self.cur, self.s, ss_out=ss)
+        out = {}
+        stream = torch.cuda.current_stream()
+
+        def timed(fn, n):
+            fn()
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(n):
+                    fn()
+            g.replay()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(iters):
+                g.replay()
+            e1.record(stream)
+            e1.synchronize()
+            return 1000.0 * e0.elapsed_time(e1) / (n * iters)
+
+        for name, (fn, nbytes, per_step) in ops_.items():
+            out[name] = {"avg_us": timed(fn, reps), "bytes_per_launch": float(nbytes), "launches_per_step": per_step}
+        self.state[0] = step_index
+        out["decode_step"] = {"avg_us": timed(self._step_fused, 2), "bytes_per_launch": None, "launches_per_step": 1}
+        return out
 
     # ------------------------------------------------------------------ prefill
     def _prefill(self, prompt_ids: torch.Tensor, prompt_mask: torch.Tensor):

@@ -93,8 +93,12 @@ def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tens
     return out
 
 
-def embed_gather(table: torch.Tensor, ids: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
-    call("swh_embed_gather", table.data_ptr(), ids.data_ptr(), ids.numel(), table.shape[1], out.data_ptr(), _stream())
+def embed_gather(table: torch.Tensor, ids: torch.Tensor, out: torch.Tensor,
+                 ss_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[b] = table[ids[b]]; ss_out f32 [B, H/16] (optional) gets the rows'
+    per 16-column sums of squares for the next fused RMSNorm."""
+    call("swh_embed_gather", table.data_ptr(), ids.data_ptr(), ids.numel(), table.shape[1], out.data_ptr(),
+         _p(ss_out), _stream())
     return out
 
 
@@ -127,10 +131,13 @@ def gemm_workspace(device, nbytes: int = 64 << 20) -> torch.Tensor:
 
 def decode_gemm(x: torch.Tensor, w: torch.Tensor, *, norm_w: Optional[torch.Tensor] = None, eps: float = 1e-6,
                 bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None, silu: bool = False,
-                y: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+                y: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
+                ss_in: Optional[torch.Tensor] = None, ss_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Weight-streaming decode GEMM with fused RMSNorm prologue and bias /
     residual / SiLU-gate epilogues (include/swh_trl_amd.h swh_decode_gemm).
-    x [M, K] bf16; w [N, K] (or [2N, K] with silu)."""
+    x [M, K] bf16; w [N, K] (or [2N, K] with silu).  ss_in f32 [M, K/16]: the
+    producer's chunk sums of squares of x (with norm_w); ss_out f32 [M, N/16]:
+    written with residual."""
     _dev(x, "decode_gemm")
     M, K = x.shape
     N = w.shape[0] // 2 if silu else w.shape[0]
@@ -139,5 +146,5 @@ def decode_gemm(x: torch.Tensor, w: torch.Tensor, *, norm_w: Optional[torch.Tens
     ldy = residual.stride(0) if residual is not None else y.stride(0)
     ws = workspace if workspace is not None else gemm_workspace(x.device)
     call("swh_decode_gemm", x.data_ptr(), w.data_ptr(), M, N, K, _p(norm_w), float(eps), _p(bias), _p(residual),
-         int(bool(silu)), _p(y), ldy, ws.data_ptr(), ws.numel(), _stream())
+         int(bool(silu)), _p(y), ldy, _p(ss_in), _p(ss_out), ws.data_ptr(), ws.numel(), _stream())
     return residual if residual is not None else y

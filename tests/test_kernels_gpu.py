@@ -495,16 +495,18 @@ def _rope_tables(D, max_pos, theta, dev):
     return fr.cos().to(torch.bfloat16).float().to(dev), fr.sin().to(torch.bfloat16).float().to(dev)
 
 
-@pytest.mark.parametrize("D,Hq,Hkv", [(64, 14, 2), (128, 32, 8)])
-def test_attn_decode(ops, dev, D, Hq, Hkv):
+@pytest.mark.parametrize("D,Hq,Hkv,Tmax,step", [(64, 14, 2, 320, 270), (128, 32, 8, 320, 270),
+                                                (64, 14, 2, 1280, 1200), (128, 32, 8, 700, 600)])
+def test_attn_decode(ops, dev, D, Hq, Hkv, Tmax, step):
+    """One key round (<= 512 keys for D=64, 256 for D=128) and several."""
     from swh_trl_amd import nn_ops
     g = _gen(20)
-    B, P, Tmax, step = 5, 40, 320, 270
+    B, P = 5, 40
     plen = torch.tensor([40, 33, 1, 40, 17], dtype=torch.int32)
     kc = (torch.randn(B, Hkv, Tmax, D, generator=g)).to(torch.bfloat16)
     vc = (torch.randn(B, Hkv, Tmax, D, generator=g)).to(torch.bfloat16)
     qkv = torch.randn(B, (Hq + 2 * Hkv) * D, generator=g).to(torch.bfloat16)
-    cos, sin = _rope_tables(D, 1024, 1e6, dev)
+    cos, sin = _rope_tables(D, 2048, 1e6, dev)
     state = torch.tensor([step + 1, P], dtype=torch.int32, device=dev)  # sampler index = input + 1
     kcd, vcd = kc.to(dev), vc.to(dev)
     out = nn_ops.attn_decode(qkv.to(dev), kcd, vcd, cos, sin, plen.to(dev), state, Hq, Hkv, D, D ** -0.5)
@@ -551,7 +553,8 @@ def _ref_norm(x, w, eps):
     return (w * n)  # bf16 * bf16 -> bf16 (transformers Qwen2RMSNorm)
 
 
-@pytest.mark.parametrize("M,N,K", [(64, 1152, 896), (5, 896, 896), (130, 256, 4864), (64, 151936, 896)])
+@pytest.mark.parametrize("M,N,K", [(64, 1152, 896), (5, 896, 896), (130, 256, 4864), (64, 151936, 896),
+                                   (100, 32768, 896)])
 @pytest.mark.parametrize("norm", [False, True])
 def test_decode_gemm_plain(ops, dev, M, N, K, norm):
     from swh_trl_amd import nn_ops
@@ -598,3 +601,94 @@ def test_decode_gemm_split_k_is_deterministic_across_launches(ops, dev):
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
     torch.testing.assert_close(outs[0].float(), x.float() @ w.float().t(), rtol=1e-2, atol=1e-2)
+
+
+def _chunk_ss(t):
+    """Per 16-column chunk sums of squares (fp32) of a bf16 [M, H] tensor."""
+    M, H = t.shape
+    return t.float().view(M, H // 16, 16).pow(2).sum(-1)
+
+
+def test_rmsnorm_statistic_handoff(ops, dev):
+    """embed_gather / residual epilogues publish per-chunk sums of squares;
+    the normed GEMM consuming them (ss_in) matches the in-kernel statistic."""
+    from swh_trl_amd import nn_ops
+    g = _gen(33)
+    V, M, H, I = 1000, 64, 896, 4864
+    table = torch.randn(V, H, generator=g).to(torch.bfloat16).to(dev)
+    ids = torch.randint(0, V, (M,), generator=g).to(dev)
+    s = torch.empty(M, H, dtype=torch.bfloat16, device=dev)
+    ss = torch.empty(M, H // 16, dtype=torch.float32, device=dev)
+    nn_ops.embed_gather(table, ids, s, ss_out=ss)
+    assert torch.equal(s, table[ids])
+    torch.testing.assert_close(ss, _chunk_ss(s), rtol=1e-5, atol=1e-5)
+    a = torch.randn(M, I, generator=g).to(torch.bfloat16).to(dev)
+    wd = (torch.randn(H, I, generator=g) * I ** -0.5).to(torch.bfloat16).to(dev)
+    nn_ops.decode_gemm(a, wd, residual=s, ss_out=ss)
+    torch.testing.assert_close(ss, _chunk_ss(s), rtol=1e-5, atol=1e-5)
+    w = (torch.randn(1152, H, generator=g) * H ** -0.5).to(torch.bfloat16).to(dev)
+    nw = (1 + 0.1 * torch.randn(H, generator=g)).to(torch.bfloat16).to(dev)
+    b = torch.randn(1152, generator=g).to(torch.bfloat16).to(dev)
+    y1 = nn_ops.decode_gemm(s, w, norm_w=nw, eps=1e-6, bias=b, ss_in=ss)
+    y0 = nn_ops.decode_gemm(s, w, norm_w=nw, eps=1e-6, bias=b)
+    ref = _ref_norm(s, nw, 1e-6).float() @ w.float().t() + b.float()
+    torch.testing.assert_close(y1.float(), ref, rtol=1e-2, atol=1e-2)
+    # the two statistics differ only in fp32 summation order
+    assert (y1 != y0).float().mean().item() < 0.01
+
+
+@pytest.mark.parametrize("cfg", ["1,4,1", "1,8,3", "1,8,1", "2,4,2", "2,8,1", "4,4,1", "4,8,3", "4,8,1"])
+def test_decode_gemm_launch_configs(ops, dev, cfg, monkeypatch):
+    """Every (column blocks, waves, K split) geometry computes the same GEMM:
+    normed + bias, residual + statistic, and SiLU-gate epilogues."""
+    from swh_trl_amd import nn_ops
+    monkeypatch.setenv("SWH_GEMM_CFG", cfg)
+    g = _gen(34)
+    M, H, I = 40, 896, 1024
+    s = torch.randn(M, H, generator=g).to(torch.bfloat16).to(dev)
+    nw = (1 + 0.1 * torch.randn(H, generator=g)).to(torch.bfloat16).to(dev)
+    w = (torch.randn(1152, H, generator=g) * H ** -0.5).to(torch.bfloat16).to(dev)
+    b = torch.randn(1152, generator=g).to(torch.bfloat16).to(dev)
+    y = nn_ops.decode_gemm(s, w, norm_w=nw, eps=1e-6, bias=b)
+    xn = _ref_norm(s, nw, 1e-6).float()
+    torch.testing.assert_close(y.float(), xn @ w.float().t() + b.float(), rtol=1e-2, atol=1e-2)
+    wgu = (torch.randn(2 * I, H, generator=g) * H ** -0.5).to(torch.bfloat16).to(dev)
+    act = nn_ops.decode_gemm(s, wgu, norm_w=nw, eps=1e-6, silu=True)
+    gu = (xn @ wgu.float().t()).to(torch.bfloat16)
+    torch.testing.assert_close(act.float(), (torch.nn.functional.silu(gu[:, :I]) * gu[:, I:]).float(),
+                               rtol=2e-2, atol=2e-2)
+    wd = (torch.randn(H, I, generator=g) * I ** -0.5).to(torch.bfloat16).to(dev)
+    ss = torch.empty(M, H // 16, dtype=torch.float32, device=dev)
+    s0 = s.clone()
+    nn_ops.decode_gemm(act, wd, residual=s, ss_out=ss)
+    ref = s0 + (act.float() @ wd.float().t()).to(torch.bfloat16)
+    torch.testing.assert_close(s.float(), ref.float(), rtol=1e-2, atol=2e-2)
+    torch.testing.assert_close(ss, _chunk_ss(s), rtol=1e-5, atol=1e-5)
+
+
+def test_decode_gemm_persistent_epilogues(ops, dev):
+    """Workgroups looping over column blocks (more blocks than CUs) run every
+    epilogue: bias, residual + statistic, SiLU gate; two M tiles."""
+    from swh_trl_amd import nn_ops
+    g = _gen(35)
+    M, H, N = 70, 896, 8192
+    s = torch.randn(M, H, generator=g).to(torch.bfloat16).to(dev)
+    nw = (1 + 0.1 * torch.randn(H, generator=g)).to(torch.bfloat16).to(dev)
+    w = (torch.randn(N, H, generator=g) * H ** -0.5).to(torch.bfloat16).to(dev)
+    b = torch.randn(N, generator=g).to(torch.bfloat16).to(dev)
+    xn = _ref_norm(s, nw, 1e-6).float()
+    y = nn_ops.decode_gemm(s, w, norm_w=nw, eps=1e-6, bias=b)
+    torch.testing.assert_close(y.float(), xn @ w.float().t() + b.float(), rtol=1e-2, atol=1e-2)
+    wgu = (torch.randn(2 * N, H, generator=g) * H ** -0.5).to(torch.bfloat16).to(dev)
+    act = nn_ops.decode_gemm(s, wgu, norm_w=nw, eps=1e-6, silu=True)
+    gu = (xn @ wgu.float().t()).to(torch.bfloat16)
+    torch.testing.assert_close(act.float(), (torch.nn.functional.silu(gu[:, :N]) * gu[:, N:]).float(),
+                               rtol=2e-2, atol=2e-2)
+    a = torch.randn(M, H, generator=g).to(torch.bfloat16).to(dev)
+    r = torch.randn(M, N, generator=g).to(torch.bfloat16).to(dev)
+    ss = torch.empty(M, N // 16, dtype=torch.float32, device=dev)
+    r0 = r.clone()
+    nn_ops.decode_gemm(a, w, residual=r, ss_out=ss)
+    ref = r0 + (a.float() @ w.float().t()).to(torch.bfloat16)
+    torch.testing.assert_close(r.float(), ref.float(), rtol=1e-2, atol=2e-2)
+    torch.testing.assert_close(ss, _chunk_ss(r), rtol=1e-5, atol=1e-5)

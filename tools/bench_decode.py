@@ -1,0 +1,114 @@
+"""Per-kernel timing of one decode step at the bench configuration
+(Qwen2.5-0.5B random init, B=64, P=128, C=256) — DecodeEngine.kernel_timings
+at the middle of the completion.  Tuning aid, not part of the product.
+
+    python tools/bench_decode.py [--step 128] [--gemm-cfg cb,nw,s]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _time(fn, reps=20, iters=3):
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        g.replay()
+    e1.record()
+    e1.synchronize()
+    return 1000.0 * e0.elapsed_time(e1) / (reps * iters)
+
+
+def sweep(eng, m):
+    from swh_trl_amd import nn_ops
+    c, p = eng.cfg, m.p
+    eps, ss = c.rms_norm_eps, eng.ss
+    shapes = {
+        "qkv": lambda: nn_ops.decode_gemm(eng.s, p["l0.qkv_w"], norm_w=p["l0.ln_in"], eps=eps, bias=p["l0.qkv_b"],
+                                          y=eng.qkv, ss_in=ss),
+        "o": lambda: nn_ops.decode_gemm(eng.att, p["l0.o_w"], residual=eng.s, ss_out=ss),
+        "gate_up": lambda: nn_ops.decode_gemm(eng.s, p["l0.gu_w"], norm_w=p["l0.ln_post"], eps=eps, silu=True,
+                                              y=eng.act, ss_in=ss),
+        "gate_up_nonorm": lambda: nn_ops.decode_gemm(eng.s, p["l0.gu_w"], silu=True, y=eng.act),
+        "down": lambda: nn_ops.decode_gemm(eng.act, p["l0.down_w"], residual=eng.s, ss_out=ss),
+        "lm": lambda: nn_ops.decode_gemm(eng.s, m.lm_weight(), norm_w=p["norm"], eps=eps, y=eng.logits_buf,
+                                         ss_in=ss),
+        "lm_nonorm": lambda: nn_ops.decode_gemm(eng.s, m.lm_weight(), y=eng.logits_buf),
+    }
+    cfgs = [None, "1,4,1", "1,8,1", "2,4,1", "2,8,1", "4,4,1", "4,8,1", "1,8,2", "1,8,4", "2,8,2", "2,8,5",
+            "1,8,5", "4,8,5", "2,4,8"]
+    print("cfg      " + " ".join(f"{k:>14s}" for k in shapes), flush=True)
+    for cf in cfgs:
+        if cf is None:
+            os.environ.pop("SWH_GEMM_CFG", None)
+        else:
+            os.environ["SWH_GEMM_CFG"] = cf
+        row = []
+        for k, fn in shapes.items():
+            if k.startswith("lm") and cf not in (None, "4,4,1", "4,8,1", "2,4,1", "2,8,1", "1,8,1"):
+                row.append(float("nan"))
+                continue
+            try:
+                row.append(_time(fn, reps=10 if k.startswith("lm") else 20))
+            except Exception as e:  # a geometry the shape does not divide into
+                row.append(float("nan"))
+        print(f"{str(cf):8s} " + " ".join(f"{v:14.2f}" for v in row), flush=True)
+    os.environ.pop("SWH_GEMM_CFG", None)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--step", type=int, default=128)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--gemm-cfg", default=None)
+    ap.add_argument("--sweep", action="store_true", help="time the GEMM shapes under several launch geometries")
+    args = ap.parse_args()
+    if args.gemm_cfg:
+        os.environ["SWH_GEMM_CFG"] = args.gemm_cfg
+    from swh_trl_amd.engine.config import qwen2_5_0_5b
+    from swh_trl_amd.engine.decode import DecodeEngine
+    from swh_trl_amd.engine.model import CausalLM
+
+    t0 = time.time()
+    cfg = qwen2_5_0_5b()
+    m = CausalLM(cfg, torch.device("cuda:0"), trainable=False)
+    B, P, C = args.batch, 128, 256
+    eng = DecodeEngine(m, B, P, C)
+    g = torch.Generator().manual_seed(0)
+    ids = torch.randint(0, cfg.vocab_size, (B, P), generator=g).cuda()
+    mask = torch.ones(B, P, dtype=torch.int32, device="cuda")
+    eng.generate(ids, mask, 8, seed=1, min_new_tokens=8, eos_token_id=151645, pad_token_id=151643)
+    torch.cuda.synchronize()
+    print(f"[bench_decode] setup {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
+    if args.sweep:
+        sweep(eng, m)
+        return
+    res = eng.kernel_timings(args.step)
+    tot = 0.0
+    for k, v in res.items():
+        gbs = v["bytes_per_launch"] / (v["avg_us"] * 1e-6) / 1e9 if v["bytes_per_launch"] else float("nan")
+        per_step = v["avg_us"] * v["launches_per_step"]
+        if k != "decode_step":
+            tot += per_step
+        print(f"{k:24s} {v['avg_us']:9.2f} us  x{v['launches_per_step']:3d} = {per_step:8.1f} us/step  "
+              f"{gbs:8.1f} GB/s")
+    print(f"{'sum of kernels':24s} {tot:9.1f} us/step (decode_step graph w/o sampler: "
+          f"{res['decode_step']['avg_us']:.1f} us)")
+    print(json.dumps({k: round(v["avg_us"], 2) for k, v in res.items()}))
+
+
+if __name__ == "__main__":
+    main()
