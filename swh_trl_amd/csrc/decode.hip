@@ -56,19 +56,19 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 
 __device__ __forceinline__ bf16x8 as_bf16x8(const uint4 &v) { return __builtin_bit_cast(bf16x8, v); }
 
-// A fragment of normalised X: bf16(w * bf16(x * rstd)) for 8 consecutive k.
-__device__ __forceinline__ uint4 norm_frag(const uint4 &xv, const uint4 &wv, float rs) {
-    float x[8], w[8];
-    unpack16<SWH_BF16>(xv, x);
-    unpack16<SWH_BF16>(wv, w);
-    uint32_t o[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const float a = w[2 * k] * round_bf16(x[2 * k] * rs);
-        const float b = w[2 * k + 1] * round_bf16(x[2 * k + 1] * rs);
-        o[k] = (uint32_t)f32_to_bf16_bits(a) | ((uint32_t)f32_to_bf16_bits(b) << 16);
-    }
-    return uint4{o[0], o[1], o[2], o[3]};
+// Normalised X: bf16(w * bf16(x * rstd)) for 8 consecutive k (Qwen2RMSNorm's
+// two roundings), packed f32 math: 4 VALU per element.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t norm_pair(uint32_t xv, f32x2 w, float rs) {
+    const f32x2 xf = {__uint_as_float(xv << 16), __uint_as_float(xv & 0xffff0000u)};
+    const uint32_t tb = __builtin_bit_cast(uint32_t, __builtin_convertvector(xf * rs, bf16x2));
+    const f32x2 tf = {__uint_as_float(tb << 16), __uint_as_float(tb & 0xffff0000u)};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(tf * w, bf16x2));
+}
+__device__ __forceinline__ uint4 norm_frag(const uint4 &xv, const float4 &w0, const float4 &w1, float rs) {
+    return uint4{norm_pair(xv.x, f32x2{w0.x, w0.y}, rs), norm_pair(xv.y, f32x2{w0.z, w0.w}, rs),
+                 norm_pair(xv.z, f32x2{w1.x, w1.y}, rs), norm_pair(xv.w, f32x2{w1.z, w1.w}, rs)};
 }
 
 __device__ __forceinline__ uint4 pack8(const float *v) {
@@ -81,76 +81,93 @@ __device__ __forceinline__ uint4 pack8(const float *v) {
 
 
 // LDS layout of the GEMM kernel (bytes; host and device compute it alike):
-//   [0,256) rstd[64] | [256,272) flag | [512, 512+nwb) norm-weight slice (bf16)
-//   | body: RMSNorm partials (phase 1), then the X image [64][Kr*2+16 B];
-//     the merge slots [NW/2][64][NB+1] f32 reuse the image, or follow it when
+//   [0,256) rstd[64] | [256,272) flag | [512, ...) norm-weight slice (f32)
+//   | RMSNorm partials [MR][K/64] f32 | the X image [MR][Kr*2+16 B] (LDS-DMA);
+//     the merge slots [NW/2][NB][MR+4] f32 reuse the image, or follow it when
 //     the workgroup loops over several column blocks (the image must persist).
 struct GemmLds {
-    int64_t nw_off, body_off, xs_bytes, slots_off, total;
+    int64_t nw_off, ss_off, body_off, xs_bytes, slots_off, total;
 };
-__host__ __device__ inline GemmLds gemm_lds(int cb, int nw, int krmax, bool norm, bool persist) {
+__host__ __device__ inline GemmLds gemm_lds(int cb, int mr, int nw, int krmax, int K, bool norm, bool persist) {
     GemmLds L;
     L.nw_off = 512;
-    L.body_off = L.nw_off + (norm ? ((int64_t)krmax * 2 + 15) / 16 * 16 : 0);
-    L.xs_bytes = (int64_t)kRows * (krmax * 2 + 16);
-    const int64_t slots = (int64_t)(nw > 1 ? nw / 2 : 1) * kRows * (16 * cb + 1) * 4;
-    const int64_t ssb = norm ? (int64_t)krmax * 4 : 0;  // upper bound of the partials (K <= 4 * threads)
+    L.ss_off = L.nw_off + (norm ? (int64_t)krmax * 4 : 0);  // norm weights as f32
+    L.body_off = L.ss_off + (norm ? ((int64_t)mr * (K / 64) * 4 + 15) / 16 * 16 : 0);  // partials beside the DMA'd image
+    L.xs_bytes = (int64_t)mr * (krmax * 2 + 16);
+    const int64_t slots = (int64_t)(nw > 1 ? nw / 2 : 1) * 16 * cb * (mr + 4) * 4;  // [NW/2][NB][MR+4]
     L.slots_off = L.body_off + (persist ? L.xs_bytes : 0);
-    int64_t end = L.body_off + (L.xs_bytes > ssb ? L.xs_bytes : ssb);
+    int64_t end = L.body_off + L.xs_bytes;
     if (L.slots_off + slots > end) end = L.slots_off + slots;
     L.total = end;
     return L;
 }
 
-// grid = (column-block slots, M tiles, S k-splits), block = 64*NW threads (NW 4/8).
-// A workgroup stages its X slice [64 rows x Kr] into LDS ONCE — full-line 16-B
-// loads, RMSNorm applied on the way in — then covers column blocks of NB =
-// 16*CB outputs (several when gridDim.x < column blocks: the lm head loops,
-// prefetching the next block's weights before merging the current one).
-// The NW waves split the slice's k-steps; each issues all weight loads of a
-// round of kU k-steps at once (fragment order, nontemporal: read once) and
-// takes its A fragments from the LDS image.  Waves merge through a fixed-order
-// LDS tree.  S > 1: write-through (sc1) fp32 slabs, an agent-scope ticket, the
+// Tile = MR (16 * MS) rows x NB (16 * CB) output columns x one K slice.
+// A workgroup stages its X slice [MR rows x Kr] into LDS ONCE — every wave
+// whole rows, lanes along the row (full-line 16-B loads), RMSNorm applied on
+// the way in — then covers one column block, or several when the grid is
+// smaller than the column blocks (the lm head loops, prefetching the next
+// block's weights before merging the current one).  The NW waves split the
+// slice's k-steps; each issues all weight loads of a round of kU k-steps at
+// once (fragment order) and takes its A fragments from the LDS image.  Waves
+// merge through a fixed-order LDS tree.  Tiles are numbered so the M tiles of
+// one column block land on one XCD (dispatch is round-robin over the 8 XCDs):
+// their shared weight rows are fetched from HBM once and re-read from that
+// XCD's L2.  S > 1: write-through (sc1) fp32 slabs, an agent-scope ticket, the
 // last arriver sums the S slabs in fixed order (deterministic, placement-
 // independent — MI355X_MICROARCH.md §Workgroup dispatch) and runs the epilogue.
-constexpr int kU = 4;   // k-steps whose loads are issued together
-constexpr int kXP = 16; // X pieces (16 B) per thread per staging chunk
+constexpr int kU = 4;    // k-steps whose loads are issued together
 
-template <int CB, bool NORM, int EPI, bool BIAS>
+template <int CB, int MS, bool NORM, int EPI, bool BIAS>
 __global__ __launch_bounds__(512) void decode_gemm_kernel(
     const uint16_t *__restrict__ x, const uint16_t *__restrict__ w, int M, int N, int K,
     const uint16_t *__restrict__ norm_w, float eps, const float *__restrict__ ss_in,
     const uint16_t *__restrict__ bias, uint16_t *__restrict__ res, float *__restrict__ ss_out,
-    uint16_t *__restrict__ y, int ldy, float *__restrict__ slabs, int *__restrict__ counters) {
-    constexpr int NB = 16 * CB, LD = NB + 1;
+    uint16_t *__restrict__ y, int ldy, float *__restrict__ slabs, int *__restrict__ counters, int persist) {
+    constexpr int NB = 16 * CB, MR = 16 * MS, LDR = MR + 4;  // merge slots column-major: b128 parks
     constexpr int G8 = (EPI == EPI_SILU) ? CB : NB / 8;  // 8-column output groups per row
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, NT = blockDim.x, NW = NT >> 6;
-    const int S = gridDim.z, sidx = blockIdx.z, m0 = blockIdx.y * kRows;
+    const int S = gridDim.z, sidx = blockIdx.z;
     const int ncb = (EPI == EPI_SILU) ? N / (NB / 2) : N / NB;
-    const bool persist = (int)gridDim.x < ncb;
+    const int nmt = (M + MR - 1) / MR;
+    // ---- tile of this workgroup
+    int cb_first, cb_step, mt;
+    if (persist) {  // gridDim.x % nmt == 0
+        mt = blockIdx.x % nmt;
+        cb_first = blockIdx.x / nmt;
+        cb_step = gridDim.x / nmt;
+        if (cb_first >= ncb) return;
+    } else {        // the nmt M tiles of a column block on one XCD
+        const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+        cb_first = (j / nmt) * 8 + xcd;
+        mt = j % nmt;
+        cb_step = ncb;
+        if (cb_first >= ncb) return;
+    }
+    const int m0 = mt * MR;
     const int KS = K / 32, kb0 = (int)((int64_t)KS * sidx / S), kb1 = (int)((int64_t)KS * (sidx + 1) / S);
     const int Kr = (kb1 - kb0) * 32, k0 = kb0 * 32, RS = Kr * 2 + 16;
-    const GemmLds L = gemm_lds(CB, NW, (KS + S - 1) / S * 32, NORM, persist);
+    const GemmLds L = gemm_lds(CB, MR, NW, (KS + S - 1) / S * 32, K, NORM, persist != 0);
     float *rstd_s = reinterpret_cast<float *>(lds);
     int *flag_s = reinterpret_cast<int *>(lds + 256);
-    uint16_t *nw_s = reinterpret_cast<uint16_t *>(lds + L.nw_off);
+    float *nw_s = reinterpret_cast<float *>(lds + L.nw_off);
     unsigned char *xs = lds + L.body_off;
-    float *ssp = reinterpret_cast<float *>(lds + L.body_off);
+    float *ssp = reinterpret_cast<float *>(lds + L.ss_off);
     float *part = reinterpret_cast<float *>(lds + L.slots_off);
     const int rl = lane & 15, kq = (lane >> 4) * 8;
     SWH_GEMM_TRACE(0);
 
     // ---- (a) RMSNorm partial sums and the norm-weight slice (L2), first in the queue
     const int nc = K / 64;
-    const bool use_ss = NORM && ss_in && K <= 4 * NT;
+    const bool use_ss = NORM && ss_in && MR * nc <= 4 * NT;
     float4 ssv[4];
     uint4 nwv[2];
     if constexpr (NORM) {
         if (use_ss) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int idx = min(tid + q * NT, kRows * nc - 1);
+                const int idx = min(tid + q * NT, MR * nc - 1);
                 const int r = idx / nc, c = idx - r * nc;
                 ssv[q] = reinterpret_cast<const float4 *>(ss_in + (int64_t)min(m0 + r, M - 1) * (K / 16))[c];
             }
@@ -159,18 +176,35 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
         for (int q = 0; q < 2; ++q)
             nwv[q] = reinterpret_cast<const uint4 *>(norm_w + k0)[min(tid + q * NT, Kr / 8 - 1)];
     }
-    // ---- (b) X slice: 16-B pieces, consecutive lanes along a row (whole lines)
-    const int ppr = Kr / 8, npc = kRows * ppr;
-    uint4 xv[kXP];
-    auto xload = [&](int base) {
+    // ---- (b) epilogue operands of a single-block workgroup (L2): <= 2 per thread in every geometry
+    const int ncol0 = cb_first * (EPI == EPI_SILU ? NB / 2 : NB);
+    uint4 pre_res[2], pre_bias[2];
+    if constexpr (EPI == EPI_RESIDUAL || BIAS) {
+        if (!persist) {
 #pragma unroll
-        for (int j = 0; j < kXP; ++j) {
-            const int p = min(base + tid + j * NT, npc - 1);
-            const int r = p / ppr, c = p - r * ppr;
-            xv[j] = reinterpret_cast<const uint4 *>(x + (int64_t)min(m0 + r, M - 1) * K + k0)[c];
+            for (int q = 0; q < 2; ++q) {
+                const int idx = min(tid + q * NT, MR * G8 - 1);
+                const int r = idx / G8, gc = ncol0 + (idx - r * G8) * 8;
+                if constexpr (EPI == EPI_RESIDUAL)
+                    pre_res[q] = *reinterpret_cast<const uint4 *>(res + (int64_t)min(m0 + r, M - 1) * ldy + gc);
+                if constexpr (BIAS) pre_bias[q] = *reinterpret_cast<const uint4 *>(bias + gc);
+            }
         }
-    };
-    xload(0);
+    }
+    // ---- X slice -> LDS image by LDS-DMA (no registers): each wave whole rows
+    // wid, wid+NW, ...; one instruction = 64 lanes x 16 B = 1 KB of a row
+    const int ppr = Kr / 8, jpl = (ppr + 63) >> 6;  // 16-B pieces per row, instructions per row
+    for (int r = wid; r < MR; r += NW) {
+        const uint16_t *src = x + (int64_t)min(m0 + r, M - 1) * K + k0;
+        for (int j = 0; j < jpl; ++j) {
+            const int c = lane + 64 * j;
+            if (c < ppr)
+                __builtin_amdgcn_global_load_lds(src + c * 8,
+                                                 (__attribute__((address_space(3))) void *)(xs + r * RS + j * 1024),
+                                                 16, 0, 0);
+        }
+    }
+    asm volatile("" ::: "memory");  // the weight loads below stay younger than every DMA
     // ---- (c) this wave's weights for the first column block (HBM)
     const int ksw0 = kb0 + (kb1 - kb0) * wid / NW, ksw1 = kb0 + (kb1 - kb0) * (wid + 1) / NW;
     const uint16_t *wrow[CB];
@@ -193,26 +227,15 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
         for (int u = 0; u < kU; ++u) {
             const int kk = max(min(ks + u, ksw1 - 1), 0) * 32;
 #pragma unroll
-            for (int j = 0; j < CB; ++j) bv[u][j] = ld_nt(reinterpret_cast<const uint4 *>(wrow[j] + kk));
+            for (int j = 0; j < CB; ++j) {
+                const uint4 *pw = reinterpret_cast<const uint4 *>(wrow[j] + kk);
+                bv[u][j] = *pw;  // plain: the line's other half is the next k-step's load
+            }
         }
     };
     auto col0 = [&](int cbk) { return cbk * (EPI == EPI_SILU ? NB / 2 : NB); };
-    set_rows(col0(blockIdx.x));
-    issue(ksw0);
-    // epilogue operands of a single-block workgroup (L2): <= 2 per thread in every geometry
-    uint4 pre_res[2], pre_bias[2];
-    if constexpr (EPI == EPI_RESIDUAL || BIAS) {
-        if (!persist) {
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const int idx = min(tid + q * NT, kRows * G8 - 1);
-                const int r = idx / G8, gc = col0(blockIdx.x) + (idx - r * G8) * 8;
-                if constexpr (EPI == EPI_RESIDUAL)
-                    pre_res[q] = *reinterpret_cast<const uint4 *>(res + (int64_t)min(m0 + r, M - 1) * ldy + gc);
-                if constexpr (BIAS) pre_bias[q] = *reinterpret_cast<const uint4 *>(bias + gc);
-            }
-        }
-    }
+    set_rows(col0(cb_first));
+    issue(ksw0);  // exactly kU * CB loads: the DMA wait below counts on it
     SWH_GEMM_TRACE(1);
 
     // ---- (d) row statistic and norm weights into LDS
@@ -221,15 +244,20 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int idx = tid + q * NT;
-                if (idx < kRows * nc) ssp[idx] = ((ssv[q].x + ssv[q].y) + ssv[q].z) + ssv[q].w;
+                if (idx < MR * nc) ssp[idx] = ((ssv[q].x + ssv[q].y) + ssv[q].z) + ssv[q].w;
             }
         }
 #pragma unroll
         for (int q = 0; q < 2; ++q)
-            if (tid + q * NT < Kr / 8) reinterpret_cast<uint4 *>(nw_s)[tid + q * NT] = nwv[q];
+            if (tid + q * NT < Kr / 8) {
+                float f[8];
+                unpack16<SWH_BF16>(nwv[q], f);
+                reinterpret_cast<float4 *>(nw_s)[2 * (tid + q * NT)] = float4{f[0], f[1], f[2], f[3]};
+                reinterpret_cast<float4 *>(nw_s)[2 * (tid + q * NT) + 1] = float4{f[4], f[5], f[6], f[7]};
+            }
         lds_barrier();
         if (use_ss) {
-            if (tid < kRows) {
+            if (tid < MR) {
                 float ssum = 0.f;
                 for (int c = 0; c < nc; ++c) ssum += ssp[tid * nc + c];
                 rstd_s[tid] = rsqrtf(ssum / (float)K + eps);
@@ -237,7 +265,7 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
         } else {
             // whole-row pass over X in global memory, one wave per row (coalesced)
             const int nv = K / 8;
-            for (int r = wid; r < kRows; r += NW) {
+            for (int r = wid; r < MR; r += NW) {
                 const uint4 *xr = reinterpret_cast<const uint4 *>(x + (int64_t)min(m0 + r, M - 1) * K);
                 float ss = 0.f;
                 for (int v = lane; v < nv; v += 64) {
@@ -254,34 +282,34 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
     }
     SWH_GEMM_TRACE(2);
 
-    // ---- (e) normalise and write the X image
-    auto xstore = [&](int base) {
-#pragma unroll
-        for (int j = 0; j < kXP; ++j) {
-            const int p = base + tid + j * NT;
-            if (p < npc) {
-                const int r = p / ppr, c = p - r * ppr;
-                uint4 v = xv[j];
-                if constexpr (NORM) v = norm_frag(v, reinterpret_cast<const uint4 *>(nw_s)[c], rstd_s[r]);
-                *reinterpret_cast<uint4 *>(xs + r * RS + c * 16) = v;
+    // ---- (e) X image landed (all but the kU * CB weight loads retired), normalised in place
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kU * CB) : "memory");
+    lds_barrier();
+    if constexpr (NORM) {
+        int r = tid / ppr, c = tid - r * ppr;
+        const int rstep = NT / ppr, cstep = NT - rstep * ppr;
+        for (; r < MR;) {
+            uint4 *pv = reinterpret_cast<uint4 *>(xs + r * RS + c * 16);
+            const float4 *wv = reinterpret_cast<const float4 *>(nw_s) + 2 * c;
+            *pv = norm_frag(*pv, wv[0], wv[1], rstd_s[r]);
+            r += rstep;
+            c += cstep;
+            if (c >= ppr) {
+                c -= ppr;
+                ++r;
             }
         }
-    };
-    xstore(0);
-    for (int base = kXP * NT; base < npc; base += kXP * NT) {
-        xload(base);
-        xstore(base);
+        lds_barrier();
     }
-    lds_barrier();
     SWH_GEMM_TRACE(3);
 
     // ---- (f) column blocks
-    auto slot = [&](int s, int r, int c) -> float & { return part[(s * kRows + r) * LD + c]; };
-    for (int cbk = blockIdx.x; cbk < ncb; cbk += gridDim.x) {
+    auto slot = [&](int s, int r, int c) -> float & { return part[(s * NB + c) * LDR + r]; };
+    for (int cbk = cb_first; cbk < ncb; cbk += cb_step) {
         const int n0 = col0(cbk);
-        f32x4 acc[4][CB];
+        f32x4 acc[MS][CB];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < MS; ++i)
 #pragma unroll
             for (int j = 0; j < CB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         for (int ks = ksw0; ks < ksw1; ks += kU) {
@@ -290,11 +318,11 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
             for (int u = 0; u < kU; ++u) {
                 if (ks + u >= ksw1) break;
                 const int kl = ((ks + u - kb0) * 32 + kq) * 2;
-                uint4 a[4];
+                uint4 a[MS];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const uint4 *>(xs + (i * 16 + rl) * RS + kl);
+                for (int i = 0; i < MS; ++i) a[i] = *reinterpret_cast<const uint4 *>(xs + (i * 16 + rl) * RS + kl);
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < MS; ++i)
 #pragma unroll
                     for (int j = 0; j < CB; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[i]), as_bf16x8(bv[u][j]),
@@ -302,33 +330,31 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
             }
         }
         // the next column block's first weight round overlaps this block's merge
-        if (cbk + (int)gridDim.x < ncb) {
-            set_rows(col0(cbk + gridDim.x));
+        if (cbk + cb_step < ncb) {
+            set_rows(col0(cbk + cb_step));
             issue(ksw0);
         }
         SWH_GEMM_TRACE(4);
 
         // ---- merge the NW waves: fixed-order tree through NW/2 LDS slots -> slot 0
-        if (!persist) __syncthreads();  // the slots reuse the X image
+        if (!persist) lds_barrier();  // the slots reuse the X image
+        // C layout: lane holds rows 16 i + 4 g .. +3 of column 16 j + rl -> one 16-B store each
         auto park = [&](int s) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < MS; ++i)
 #pragma unroll
                 for (int j = 0; j < CB; ++j)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) slot(s, i * 16 + (lane >> 4) * 4 + e, j * 16 + rl) = acc[i][j][e];
+                    *reinterpret_cast<f32x4 *>(&slot(s, i * 16 + (lane >> 4) * 4, j * 16 + rl)) = acc[i][j];
         };
         for (int h = NW >> 1; h >= 1; h >>= 1) {
             if (wid >= h && wid < 2 * h) park(wid - h);
             lds_barrier();
             if (wid < h) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < MS; ++i)
 #pragma unroll
                     for (int j = 0; j < CB; ++j)
-#pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            acc[i][j][e] += slot(wid, i * 16 + (lane >> 4) * 4 + e, j * 16 + rl);
+                        acc[i][j] += *reinterpret_cast<const f32x4 *>(&slot(wid, i * 16 + (lane >> 4) * 4, j * 16 + rl));
             }
             lds_barrier();
         }
@@ -338,9 +364,9 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
 
         // ---- cross-workgroup split-K: publish, ticket, last arriver reduces
         if (S > 1) {
-            const int blk = blockIdx.y * ncb + cbk;
-            float *my = slabs + ((int64_t)blk * S + sidx) * (kRows * NB);
-            for (int idx = tid; idx < kRows * NB; idx += NT)
+            const int blk = mt * ncb + cbk;
+            float *my = slabs + ((int64_t)blk * S + sidx) * (MR * NB);
+            for (int idx = tid; idx < MR * NB; idx += NT)
                 __hip_atomic_store(my + idx, slot(0, idx / NB, idx % NB), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
@@ -350,11 +376,11 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
             }
             __syncthreads();
             if (!flag_s[0]) return;  // S > 1 never loops over column blocks
-            const float *base = slabs + (int64_t)blk * S * (kRows * NB);
-            for (int idx = tid; idx < kRows * NB; idx += NT) {
+            const float *base = slabs + (int64_t)blk * S * (MR * NB);
+            for (int idx = tid; idx < MR * NB; idx += NT) {
                 float v = 0.f;
                 for (int q = 0; q < S; ++q)
-                    v += __hip_atomic_load(base + (int64_t)q * kRows * NB + idx, __ATOMIC_RELAXED,
+                    v += __hip_atomic_load(base + (int64_t)q * MR * NB + idx, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                 slot(0, idx / NB, idx % NB) = v;
             }
@@ -364,7 +390,7 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
 
         // ---- epilogue, 8 output columns (16 B) per thread
         if constexpr (EPI == EPI_SILU) {
-            for (int idx = tid; idx < kRows * G8; idx += NT) {
+            for (int idx = tid; idx < MR * G8; idx += NT) {
                 const int r = idx / G8, jb = idx - r * G8;
                 const int gr = m0 + r;
                 if (gr >= M) continue;
@@ -380,7 +406,7 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const int idx = tid + q * NT;
-                if (idx >= kRows * G8) break;
+                if (idx >= MR * G8) break;
                 const int r = idx / G8, c8 = (idx - r * G8) * 8;
                 const int gr = m0 + r, gc = n0 + c8;
                 if (gr >= M) continue;
@@ -410,7 +436,7 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
             if constexpr (EPI == EPI_RESIDUAL) {
                 if (ss_out) {  // partial sums of squares of the new rows, per 16-column chunk
                     __syncthreads();
-                    for (int idx = tid; idx < kRows * CB; idx += NT) {
+                    for (int idx = tid; idx < MR * CB; idx += NT) {
                         const int r = idx / CB, j = idx - r * CB;
                         if (m0 + r >= M) continue;
                         float ss = 0.f;
@@ -424,6 +450,147 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
         if (persist) __syncthreads();  // slot 0 is rewritten by the next block
     }
     SWH_GEMM_TRACE(6);
+}
+
+// ---------------------------------------------------------------------------
+// lm head (column blocks >> CUs, K <= 1024): persistent workgroups, one per CU
+// (per M tile); the X image [64 x K] is staged and normalised once, then
+// every wave owns whole 16-column tiles over the full K — all K/32 weight
+// loads of a tile in flight at once, the next tile's issued as soon as the
+// MFMAs have consumed the current one, no cross-wave merge.  8 independent
+// waves per CU keep ~200 KB of weights in flight: HBM-bound.
+// ---------------------------------------------------------------------------
+constexpr int kLmMaxKS = 32;  // K <= 1024
+
+template <bool NORM>
+__global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict__ x, const uint16_t *__restrict__ w,
+                                                      int M, int N, int K, const uint16_t *__restrict__ norm_w,
+                                                      float eps, const float *__restrict__ ss_in,
+                                                      uint16_t *__restrict__ y, int ldy) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, NT = blockDim.x, NW = NT >> 6;
+    const int rl = lane & 15, kq = (lane >> 4) * 8, g = lane >> 4;
+    const int nmt = (M + 63) / 64, mt = blockIdx.x % nmt, m0 = mt * 64;
+    const int wgs = gridDim.x / nmt, wg = blockIdx.x / nmt;
+    const int ntile = N / 16, KS = K / 32, RS = K * 2 + 16;
+    const GemmLds L = gemm_lds(1, 64, NW, K, K, NORM, false);
+    float *rstd_s = reinterpret_cast<float *>(lds);
+    float *nw_s = reinterpret_cast<float *>(lds + L.nw_off);
+    float *ssp = reinterpret_cast<float *>(lds + L.ss_off);
+    unsigned char *xs = lds + L.body_off;
+    const int tstep = wgs * NW;
+    int t = wg * NW + wid;
+
+    uint4 bv[kLmMaxKS];
+    auto issue = [&](int tile) {
+        const uint16_t *wr = w + (int64_t)(tile * 16 + rl) * K + kq;
+#pragma unroll
+        for (int ks = 0; ks < kLmMaxKS; ++ks)
+            if (ks < KS) bv[ks] = *reinterpret_cast<const uint4 *>(wr + ks * 32);
+    };
+    if (t < ntile) issue(t);  // the weight stream first
+    // RMSNorm partials and norm weights (L2), then the X image by LDS-DMA
+    const int nc = K / 64;
+    const bool use_ss = NORM && ss_in && 64 * nc <= 4 * NT;
+    float4 ssv[4];
+    uint4 nwv[2];
+    if constexpr (NORM) {
+        if (use_ss) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int idx = min(tid + q * NT, 64 * nc - 1);
+                const int r = idx / nc, c = idx - r * nc;
+                ssv[q] = reinterpret_cast<const float4 *>(ss_in + (int64_t)min(m0 + r, M - 1) * (K / 16))[c];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) nwv[q] = reinterpret_cast<const uint4 *>(norm_w)[min(tid + q * NT, K / 8 - 1)];
+    }
+    const int ppr = K / 8, jpl = (ppr + 63) >> 6;
+    for (int r = wid; r < 64; r += NW) {
+        const uint16_t *src = x + (int64_t)min(m0 + r, M - 1) * K;
+        for (int j = 0; j < jpl; ++j) {
+            const int c = lane + 64 * j;
+            if (c < ppr)
+                __builtin_amdgcn_global_load_lds(src + c * 8,
+                                                 (__attribute__((address_space(3))) void *)(xs + r * RS + j * 1024),
+                                                 16, 0, 0);
+        }
+    }
+    if constexpr (NORM) {
+        if (use_ss) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int idx = tid + q * NT;
+                if (idx < 64 * nc) ssp[idx] = ((ssv[q].x + ssv[q].y) + ssv[q].z) + ssv[q].w;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            if (tid + q * NT < K / 8) {
+                float f[8];
+                unpack16<SWH_BF16>(nwv[q], f);
+                reinterpret_cast<float4 *>(nw_s)[2 * (tid + q * NT)] = float4{f[0], f[1], f[2], f[3]};
+                reinterpret_cast<float4 *>(nw_s)[2 * (tid + q * NT) + 1] = float4{f[4], f[5], f[6], f[7]};
+            }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // image (and this wave's first tile) landed
+    lds_barrier();
+    if constexpr (NORM) {
+        if (tid < 64) {
+            float ssum = 0.f;
+            if (use_ss) {
+                for (int c = 0; c < nc; ++c) ssum += ssp[tid * nc + c];
+            } else {  // from the (raw) image: the whole row is here
+                for (int c = 0; c < ppr; ++c) {
+                    float a[8];
+                    unpack16<SWH_BF16>(*reinterpret_cast<const uint4 *>(xs + tid * RS + c * 16), a);
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) ssum = fmaf(a[k], a[k], ssum);
+                }
+            }
+            rstd_s[tid] = rsqrtf(ssum / (float)K + eps);
+        }
+        lds_barrier();
+        int r = tid / ppr, c = tid - r * ppr;
+        const int rstep = NT / ppr, cstep = NT - rstep * ppr;
+        while (r < 64) {
+            uint4 *pv = reinterpret_cast<uint4 *>(xs + r * RS + c * 16);
+            const float4 *wv = reinterpret_cast<const float4 *>(nw_s) + 2 * c;
+            *pv = norm_frag(*pv, wv[0], wv[1], rstd_s[r]);
+            r += rstep;
+            c += cstep;
+            if (c >= ppr) {
+                c -= ppr;
+                ++r;
+            }
+        }
+        lds_barrier();
+    }
+    for (; t < ntile; t += tstep) {
+        f32x4 acc[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < kLmMaxKS; ++ks) {
+            if (ks < KS) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint4 a = *reinterpret_cast<const uint4 *>(xs + (i * 16 + rl) * RS + (ks * 32 + kq) * 2);
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(bv[ks]), acc[i], 0, 0, 0);
+                }
+            }
+        }
+        if (t + tstep < ntile) issue(t + tstep);
+        // C layout: lane holds rows 16 i + 4 g + e of column rl
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int row = m0 + i * 16 + 4 * g + e;
+                if (row < M) y[(int64_t)row * ldy + t * 16 + rl] = f32_to_bf16_bits(acc[i][e]);
+            }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -656,7 +823,7 @@ int attn_dispatch_gq(int gq, const uint16_t *q, uint16_t *kc, uint16_t *vc, cons
 
 // ---- GEMM launch configuration -------------------------------------------
 struct GemmCfg {
-    int cb, nw, s, gx;  // 16-col blocks per workgroup, waves, K split, grid.x
+    int ms, cb, nw, s, gx;  // 16-row blocks, 16-col blocks, waves, K split, grid.x
     bool persist;
 };
 
@@ -671,63 +838,116 @@ int cu_count() {
     return n;
 }
 
-// K slices of <= 1024 (the X image fits LDS); the narrowest column block that
-// keeps every workgroup on its own CU; when even 64-column blocks are more
-// than the CUs (the lm head) the workgroups loop over column blocks instead.
-GemmCfg pick_cfg(int64_t M, int64_t wcols, int64_t K, bool silu) {
-    const int64_t mt = (M + kRows - 1) / kRows, KS = K / 32, ncu = cu_count();
-    const int64_t align = silu ? 2 : 1;
-    GemmCfg c{4, 8, (int)((K + 1023) / 1024), 0, false};
-    bool fits = false;
-    for (int cb : {1, 2, 4}) {
-        if (wcols % (16 * cb * align)) continue;
-        if (wcols / (16 * cb) * mt * c.s <= ncu) {
-            c.cb = cb;
-            fits = true;
-            break;
+inline int gemm_waves(int ms) { return ms == 4 ? 8 : 4; }
+
+// Modelled launch time (us) of one geometry — measured shape of the cost on
+// MI355X (tools/gemm_probe.py, tools/bench_decode.py --sweep): a fixed
+// ~3 us, the bytes one CU pulls through its load path at ~60 GB/s (weights in
+// fragment order count twice), ~1 us per 10k elements of in-LDS RMSNorm,
+// +9 us for a cross-workgroup split, +3 us per extra wave of workgroups.
+double gemm_cost(const GemmCfg &c, int64_t M, int64_t wcols, int64_t K, bool norm) {
+    const int64_t MR = 16 * c.ms, KS = K / 32, ncu = cu_count();
+    const int64_t krmax = (KS + c.s - 1) / c.s * 32;
+    const GemmLds L = gemm_lds(c.cb, (int)MR, c.nw, (int)krmax, (int)K, norm, c.persist);
+    if (L.total > 160 * 1024) return 1e30;
+    const int64_t ncb = wcols / (16 * c.cb), nmt = (M + MR - 1) / MR;
+    const int64_t xbytes = MR * krmax * 2, wbytes = 2 * 16 * c.cb * krmax * 2;
+    if (c.persist) {
+        const int64_t wgs = c.gx, per = (ncb + wgs / nmt - 1) / (wgs / nmt);
+        return 3.0 + (xbytes + per * wbytes) / 60e3;
+    }
+    const int64_t wgs = 8 * nmt * ((ncb + 7) / 8) * c.s;
+    int64_t res = (160 * 1024) / L.total;
+    res = res < 1 ? 1 : (res > 2 ? 2 : res);
+    const int64_t per_cu = (wgs + ncu - 1) / ncu, waves = (wgs + ncu * res - 1) / (ncu * res);
+    const double norm_us = norm ? (double)(MR * krmax) / 10e3 : 0.0;  // in-LDS RMSNorm pass
+    return 3.0 + per_cu * ((xbytes + wbytes) / 60e3 + norm_us) + (c.s > 1 ? 9.0 : 0.0) + (waves - 1) * 3.0;
+}
+
+GemmCfg pick_cfg(int64_t M, int64_t wcols, int64_t K, bool silu, bool norm) {
+    const int64_t KS = K / 32, align = silu ? 2 : 1, ncu = cu_count();
+    GemmCfg best{4, 4, 8, 1, 0, false};
+    double best_cost = 1e31;
+    for (int ms : {1, 2, 4})
+        for (int cb : {1, 2, 4}) {
+            if (wcols % (16 * cb * align)) continue;
+            for (int sp = 1; sp <= 8; ++sp) {
+                if (sp > KS) break;
+                GemmCfg c{ms, cb, gemm_waves(ms), sp, 0, false};
+                const double t = gemm_cost(c, M, wcols, K, norm);
+                if (t < best_cost) {
+                    best_cost = t;
+                    best = c;
+                }
+            }
+        }
+    // persistent: all 64 rows, 32-column blocks, grid = the CUs, weights streamed once
+    const int64_t nmt64 = (M + 63) / 64;
+    if (wcols % (32 * align) == 0 && ncu / nmt64 >= 1) {
+        GemmCfg c{4, 2, 8, 1, (int)((ncu / nmt64) * nmt64), true};
+        if (c.gx > wcols / 32 * nmt64) c.gx = (int)(wcols / 32 * nmt64);
+        if (gemm_cost(c, M, wcols, K, norm) < best_cost) best = c;
+    }
+    if (const char *e = getenv("SWH_GEMM_CFG")) {  // tuning override "ms,cb,s[,p]"
+        int a = 0, b = 0, d = 0, pz = 0;
+        const int got = sscanf(e, "%d,%d,%d,%d", &a, &b, &d, &pz);
+        if (got >= 3 && (a == 1 || a == 2 || a == 4) && (b == 1 || b == 2 || b == 4) && d >= 1 && d <= KS &&
+            wcols % (16 * b * align) == 0 && !(pz && d != 1)) {
+            const int64_t nmt = (M + 16 * a - 1) / (16 * a);
+            GemmCfg c{a, b, gemm_waves(a), d, 0, pz != 0};
+            if (c.persist) {
+                const int64_t per = ncu / nmt > 0 ? ncu / nmt : 1, ncb = wcols / (16 * b);
+                c.gx = (int)((per < ncb ? per : ncb) * nmt);
+            }
+            if (gemm_cost(c, M, wcols, K, norm) < 1e29) best = c;
         }
     }
-    if (!fits && c.s == 1 && wcols % (32 * align) == 0) {  // persistent over column blocks
-        c.cb = 2;
-        c.persist = true;
-    }
-    if (const char *e = getenv("SWH_GEMM_CFG")) {  // tuning override "cb,nw,s"
-        int a = 0, b = 0, d = 0;
-        if (sscanf(e, "%d,%d,%d", &a, &b, &d) == 3 && (a == 1 || a == 2 || a == 4) && (b == 4 || b == 8) && d >= 1 &&
-            d <= KS && wcols % (16 * a * align) == 0 && K / d <= 1024) {
-            c.cb = a;
-            c.nw = b;
-            c.s = d;
-            c.persist = (d == 1) && wcols / (16 * a) * mt > ncu;
-        }
-    }
-    const int64_t ncb = wcols / (16 * c.cb);
-    c.gx = (int)(c.persist ? (ncu / mt > 0 ? ncu / mt : 1) : ncb);
-    if (c.gx > ncb) c.gx = (int)ncb;
-    (void)KS;
-    return c;
+    if (!best.persist) best.gx = (int)(8 * ((M + 16 * best.ms - 1) / (16 * best.ms)) * ((wcols / (16 * best.cb) + 7) / 8));
+    return best;
 }
 
 int64_t slab_bytes(const GemmCfg &c, int64_t M, int64_t wcols) {
     if (c.s == 1) return 0;
-    const int64_t mt = (M + kRows - 1) / kRows;
-    return mt * wcols * c.s * kRows * (int64_t)sizeof(float);  // tiles * NB == mt * wcols
+    const int64_t MR = 16 * c.ms, nmt = (M + MR - 1) / MR;
+    return nmt * wcols * c.s * MR * (int64_t)sizeof(float);  // tiles * NB == nmt * wcols
 }
 
-template <int CB, bool NORM, int EPI, bool BIAS>
+template <int CB, int MS, bool NORM, int EPI, bool BIAS>
 int launch_gemm(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W, int m,
                 int n, int k, const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs, uint16_t *R,
                 float *ss_out, uint16_t *Y, int ld, float *slab, int *ctr) {
     static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in once per kernel
     if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&decode_gemm_kernel<CB, NORM, EPI, BIAS>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&decode_gemm_kernel<CB, MS, NORM, EPI, BIAS>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
             return SWH_E_LAUNCH;
         attr = true;
     }
-    decode_gemm_kernel<CB, NORM, EPI, BIAS><<<grid, 64u * c.nw, lds, s>>>(X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out,
-                                                                         Y, ld, slab, ctr);
+    decode_gemm_kernel<CB, MS, NORM, EPI, BIAS><<<grid, 64u * c.nw, lds, s>>>(
+        X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr, c.persist ? 1 : 0);
     return launch_status();
+}
+
+template <int MS, bool NORM, int EPI, bool BIAS>
+int launch_gemm_cb(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W,
+                   int m, int n, int k, const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs,
+                   uint16_t *R, float *ss_out, uint16_t *Y, int ld, float *slab, int *ctr) {
+    switch (c.cb) {
+    case 1: return launch_gemm<1, MS, NORM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
+    case 2: return launch_gemm<2, MS, NORM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
+    default: return launch_gemm<4, MS, NORM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
+    }
+}
+
+template <bool NORM, int EPI, bool BIAS>
+int launch_gemm_ms(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W,
+                   int m, int n, int k, const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs,
+                   uint16_t *R, float *ss_out, uint16_t *Y, int ld, float *slab, int *ctr) {
+    switch (c.ms) {
+    case 1: return launch_gemm_cb<1, NORM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
+    case 2: return launch_gemm_cb<2, NORM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
+    default: return launch_gemm_cb<4, NORM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
+    }
 }
 
 }  // namespace
@@ -755,8 +975,13 @@ extern "C" int swh_attn_decode(const void *qkv, void *k_cache, void *v_cache, co
 
 extern "C" int64_t swh_decode_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K) {
     if (M <= 0 || N <= 0 || K <= 0) return kCounterBytes;
-    const int64_t a = slab_bytes(pick_cfg(M, N, K, false), M, N);
-    const int64_t b = slab_bytes(pick_cfg(M, 2 * N, K, true), M, 2 * N);
+    int64_t a = 0, b = 0;
+    for (bool nrm : {false, true}) {
+        const int64_t a1 = slab_bytes(pick_cfg(M, N, K, false, nrm), M, N);
+        const int64_t b1 = slab_bytes(pick_cfg(M, 2 * N, K, true, nrm), M, 2 * N);
+        a = a1 > a ? a1 : a;
+        b = b1 > b ? b1 : b;
+    }
     return kCounterBytes + (a > b ? a : b);
 }
 
@@ -778,14 +1003,42 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
         return SWH_E_ARG;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int64_t wcols = silu ? 2 * N : N;
-    const GemmCfg c = pick_cfg(M, wcols, K, silu != 0);
-    const unsigned gy = (unsigned)((M + kRows - 1) / kRows);
-    const int64_t blocks = wcols / (16 * c.cb);
+    if (!silu && !residual && !bias && N / 16 > 8 * (int64_t)cu_count() && K <= 32 * kLmMaxKS &&
+        !getenv("SWH_GEMM_CFG")) {  // the lm head: persistent, waves own tiles
+        const int64_t nmt = (M + 63) / 64;
+        const GemmLds L = gemm_lds(1, 64, 8, (int)K, (int)K, norm_w != nullptr, false);
+        const int64_t per = cu_count() / nmt > 0 ? cu_count() / nmt : 1;
+        const dim3 grid((unsigned)(per * nmt));
+        auto *Y = static_cast<uint16_t *>(y);
+        const auto *X = static_cast<const uint16_t *>(x);
+        const auto *W = static_cast<const uint16_t *>(w);
+        const auto *NWt = static_cast<const uint16_t *>(norm_w);
+        if (NWt) {
+            static bool attr = false;
+            if (!attr && hipFuncSetAttribute(reinterpret_cast<const void *>(&lm_head_kernel<true>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+                return SWH_E_LAUNCH;
+            attr = true;
+            lm_head_kernel<true><<<grid, 512, (size_t)L.total, s>>>(X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Y,
+                                                                    (int)ldy);
+        } else {
+            static bool attr = false;
+            if (!attr && hipFuncSetAttribute(reinterpret_cast<const void *>(&lm_head_kernel<false>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+                return SWH_E_LAUNCH;
+            attr = true;
+            lm_head_kernel<false><<<grid, 512, (size_t)L.total, s>>>(X, W, (int)M, (int)N, (int)K, nullptr, eps,
+                                                                     nullptr, Y, (int)ldy);
+        }
+        return launch_status();
+    }
+    const GemmCfg c = pick_cfg(M, wcols, K, silu != 0, norm_w != nullptr);
+    const int64_t MR = 16 * c.ms, nmt = (M + MR - 1) / MR, ncb = wcols / (16 * c.cb);
     // workspace: [counters (zeroed once, self-resetting) | fp32 slabs]
     int *ctr = static_cast<int *>(workspace);
     float *slab = nullptr;
     if (c.s > 1) {
-        if (blocks * gy * (int64_t)sizeof(int) > kCounterBytes) return SWH_E_ARG;
+        if (ncb * nmt * (int64_t)sizeof(int) > kCounterBytes) return SWH_E_ARG;
         if (!workspace || workspace_bytes < kCounterBytes + slab_bytes(c, M, wcols)) return SWH_E_ARG;
         // counters live in a FIXED region at the start (never overlapped by any
         // call's slabs, whatever its shape), so a self-reset counter stays zero
@@ -798,31 +1051,23 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
     auto *R = static_cast<uint16_t *>(residual);
     auto *Y = static_cast<uint16_t *>(y);
     const int m = (int)M, n = (int)N, k = (int)K, ld = (int)ldy;
-    const GemmLds L = gemm_lds(c.cb, c.nw, (int)((K / 32 + c.s - 1) / c.s * 32), NWt != nullptr, c.persist);
-    if (L.total > 160 * 1024) return SWH_E_ARG;
-    const dim3 grid((unsigned)c.gx, gy, (unsigned)c.s);
+    const GemmLds L = gemm_lds(c.cb, (int)MR, c.nw, (int)((K / 32 + c.s - 1) / c.s * 32), (int)K, NWt != nullptr, c.persist);
+    if (L.total > 160 * 1024 || c.gx <= 0) return SWH_E_ARG;
+    const dim3 grid((unsigned)c.gx, 1u, (unsigned)c.s);
     const size_t lds = (size_t)L.total;
-#define SWH_GEMM(CB_, NORM_, EPI_, BIAS_) \
-    launch_gemm<CB_, NORM_, EPI_, BIAS_>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr)
-#define SWH_GEMM_CB(NORM_, EPI_, BIAS_)                                 \
-    switch (c.cb) {                                                     \
-    case 1: return SWH_GEMM(1, NORM_, EPI_, BIAS_);                     \
-    case 2: return SWH_GEMM(2, NORM_, EPI_, BIAS_);                     \
-    default: return SWH_GEMM(4, NORM_, EPI_, BIAS_);                    \
-    }
+#define SWH_GEMM(NORM_, EPI_, BIAS_) \
+    return launch_gemm_ms<NORM_, EPI_, BIAS_>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr)
     if (silu) {
-        if (NWt) SWH_GEMM_CB(true, EPI_SILU, false) else SWH_GEMM_CB(false, EPI_SILU, false)
-    } else if (residual) {
-        if (NWt) SWH_GEMM_CB(true, EPI_RESIDUAL, false) else SWH_GEMM_CB(false, EPI_RESIDUAL, false)
-    } else if (NWt && Bs) {
-        SWH_GEMM_CB(true, EPI_PLAIN, true)
-    } else if (NWt) {
-        SWH_GEMM_CB(true, EPI_PLAIN, false)
-    } else if (Bs) {
-        SWH_GEMM_CB(false, EPI_PLAIN, true)
-    } else {
-        SWH_GEMM_CB(false, EPI_PLAIN, false)
+        if (NWt) SWH_GEMM(true, EPI_SILU, false);
+        SWH_GEMM(false, EPI_SILU, false);
     }
-#undef SWH_GEMM_CB
+    if (residual) {
+        if (NWt) SWH_GEMM(true, EPI_RESIDUAL, false);
+        SWH_GEMM(false, EPI_RESIDUAL, false);
+    }
+    if (NWt && Bs) SWH_GEMM(true, EPI_PLAIN, true);
+    if (NWt) SWH_GEMM(true, EPI_PLAIN, false);
+    if (Bs) SWH_GEMM(false, EPI_PLAIN, true);
+    SWH_GEMM(false, EPI_PLAIN, false);
 #undef SWH_GEMM
 }

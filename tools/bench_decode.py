@@ -48,8 +48,8 @@ def sweep(eng, m):
                                          ss_in=ss),
         "lm_nonorm": lambda: nn_ops.decode_gemm(eng.s, m.lm_weight(), y=eng.logits_buf),
     }
-    cfgs = [None, "1,4,1", "1,8,1", "2,4,1", "2,8,1", "4,4,1", "4,8,1", "1,8,2", "1,8,4", "2,8,2", "2,8,5",
-            "1,8,5", "4,8,5", "2,4,8"]
+    cfgs = [None, "1,1,1", "2,1,1", "4,1,1", "1,2,1", "2,2,1", "4,2,1", "4,4,1", "2,4,1", "1,1,2", "2,1,2",
+            "4,1,4", "4,2,5", "1,1,4", "4,2,1,1", "4,4,1,1"]
     print("cfg      " + " ".join(f"{k:>14s}" for k in shapes), flush=True)
     for cf in cfgs:
         if cf is None:
@@ -58,7 +58,7 @@ def sweep(eng, m):
             os.environ["SWH_GEMM_CFG"] = cf
         row = []
         for k, fn in shapes.items():
-            if k.startswith("lm") and cf not in (None, "4,4,1", "4,8,1", "2,4,1", "2,8,1", "1,8,1"):
+            if k.startswith("lm") and cf not in (None, "4,2,1,1", "4,4,1,1"):
                 row.append(float("nan"))
                 continue
             try:

@@ -86,6 +86,9 @@ def main():
         lib.swh_probe_set_trace(None)
         t = trace.view(-1, 8).cpu()
         t = t[t[:, 0] > 0]
+        if t.shape[0] == 0:
+            print(f"{name:8s} (no trace: a kernel without phase stamps)")
+            continue
         entry = t[:, 0]
         t0 = int(entry.min())
         span = (int(t[:, 1:7].max()) - t0) / 100.0
