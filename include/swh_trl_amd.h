@@ -280,6 +280,22 @@ int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t 
                     const void *bias, void *residual, int32_t silu, void *y, int64_t ldy, const float *ss_in,
                     float *ss_out, void *workspace, int64_t workspace_bytes, void *stream);
 
+/* Decode lm head with the sampler fused into its epilogue: RMSNorm(X) W^T
+ * (as swh_decode_gemm with norm_w / ss_in) and, per row, the token that
+ * swh_sample_step would draw from those logits with the same rng / step
+ * (Gumbel-max over bf16 logits, EOS suppression, temperature, greedy) —
+ * without materialising the [M, V] logits.  Bookkeeping (finished, pad, EOS,
+ * out_tokens[:, *step], cur_tokens) as swh_sample_step.  Unfiltered sampling
+ * only: top-k / top-p / min-p / repetition penalty return SWH_E_ARG (use the
+ * logits + swh_sample_step path).  K % 64 == 0, K <= 1024, V % 16 == 0.
+ * Replaces the reference's per-step lm_head + LogitsProcessorList +
+ * torch.multinomial of transformers `_sample` (grpo_trainer.py:1804). */
+int64_t swh_lm_head_sample_workspace_bytes(int64_t M, int64_t V, int64_t K);
+int swh_lm_head_sample(const void *x, const void *w, int64_t M, int64_t V, int64_t K, const void *norm_w, float eps,
+                       const float *ss_in, const swh_sample_params *params, const uint64_t *rng, const int32_t *step,
+                       int32_t *finished, int64_t *out_tokens, int64_t out_ld, int64_t *cur_tokens, void *workspace,
+                       int64_t workspace_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

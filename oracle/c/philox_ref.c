@@ -42,14 +42,14 @@ void swh_ref_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], u
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
-/* Uniforms u[j], j in [0, V), of one sampler row. */
+/* Uniforms u[j], j in [0, V), of one sampler row: word (row & 3) of the
+ * block at counter {j, row >> 2, offset} (swh_trl_amd/csrc/sampler.hip gumbel_at). */
 void swh_ref_row_uniforms(uint64_t seed, uint64_t offset, int64_t row, int64_t V, float *u) {
     uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
-    for (int64_t q = 0; q * 4 < V; ++q) {
-        uint32_t ctr[4] = {(uint32_t)q, (uint32_t)row, (uint32_t)offset, (uint32_t)(offset >> 32)};
+    for (int64_t j = 0; j < V; ++j) {
+        uint32_t ctr[4] = {(uint32_t)j, (uint32_t)(row >> 2), (uint32_t)offset, (uint32_t)(offset >> 32)};
         uint32_t w[4];
         swh_ref_philox4x32_10(ctr, key, w);
-        for (int i = 0; i < 4 && q * 4 + i < V; ++i)
-            u[q * 4 + i] = ((float)(w[i] >> 8) + 0.5f) * (1.0f / 16777216.0f);
+        u[j] = ((float)(w[row & 3] >> 8) + 0.5f) * (1.0f / 16777216.0f);
     }
 }

@@ -462,11 +462,27 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
 // ---------------------------------------------------------------------------
 constexpr int kLmMaxKS = 32;  // K <= 1024
 
-template <bool NORM>
+// Fused sampler (SAMPLE): instead of storing logits, each wave folds its
+// tiles into per-row Gumbel-max bests (the unfiltered swh_sample_step: EOS
+// suppression, temperature, greedy) and writes one partial per row; the
+// Philox block at counter {col, row >> 2} holds the four rows a lane owns.
+struct LmPart {
+    float key;
+    int32_t idx;
+};
+struct LmSample {
+    swh_sample_params p;
+    const uint64_t *rng;
+    const int32_t *step;
+    LmPart *part;  // [M][pstride]
+    int pstride;
+};
+
+template <bool NORM, bool SAMPLE>
 __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict__ x, const uint16_t *__restrict__ w,
                                                       int M, int N, int K, const uint16_t *__restrict__ norm_w,
                                                       float eps, const float *__restrict__ ss_in,
-                                                      uint16_t *__restrict__ y, int ldy) {
+                                                      uint16_t *__restrict__ y, int ldy, LmSample smp) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, NT = blockDim.x, NW = NT >> 6;
     const int rl = lane & 15, kq = (lane >> 4) * 8, g = lane >> 4;
@@ -567,6 +583,29 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
         }
         lds_barrier();
     }
+    // sampler state: per lane the best (key, column) of its 16 rows 16 i + 4 g + e
+    float bk[4][4];
+    int32_t bi[4][4];
+    uint32_t k0 = 0, k1 = 0, clo = 0, chi = 0;
+    bool suppress = false;
+    float temp = 1.f;
+    if constexpr (SAMPLE) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                bk[i][e] = kNegInf;
+                bi[i][e] = 0x7fffffff;
+            }
+        const int32_t step = *smp.step;
+        const uint64_t seed = smp.rng[0], ctr = smp.rng[1] + (uint64_t)step;
+        k0 = (uint32_t)seed;
+        k1 = (uint32_t)(seed >> 32);
+        clo = (uint32_t)ctr;
+        chi = (uint32_t)(ctr >> 32);
+        suppress = step < smp.p.min_new_tokens;
+        temp = (!smp.p.greedy && smp.p.temperature != 1.0f) ? smp.p.temperature : 1.f;
+    }
     for (; t < ntile; t += tstep) {
         f32x4 acc[4];
 #pragma unroll
@@ -582,15 +621,114 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
             }
         }
         if (t + tstep < ntile) issue(t + tstep);
-        // C layout: lane holds rows 16 i + 4 g + e of column rl
+        if constexpr (SAMPLE) {
+            const int col = t * 16 + rl;
+            bool masked = false;
+            if (suppress) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) masked |= (e < smp.p.n_eos && col == smp.p.eos_ids[e]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                U4 rw{0u, 0u, 0u, 0u};
+                if (!smp.p.greedy) rw = philox4x32_10(U4{(uint32_t)col, (uint32_t)((m0 >> 2) + 4 * i + g), clo, chi}, k0, k1);
+                const uint32_t wd[4] = {rw.x, rw.y, rw.z, rw.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float z = round_bf16(acc[i][e]);  // the bf16 logit
+                    if (temp != 1.f) z = z / temp;
+                    const float key = masked ? kNegInf
+                                     : smp.p.greedy ? z
+                                                    : z - fast_log(-fast_log(u01_from_bits(wd[e])));
+                    if (key > bk[i][e] || (key == bk[i][e] && col < bi[i][e])) {
+                        bk[i][e] = key;
+                        bi[i][e] = col;
+                    }
+                }
+            }
+        } else {
+            // C layout: lane holds rows 16 i + 4 g + e of column rl
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int row = m0 + i * 16 + 4 * g + e;
+                    if (row < M) y[(int64_t)row * ldy + t * 16 + rl] = f32_to_bf16_bits(acc[i][e]);
+                }
+        }
+    }
+    if constexpr (SAMPLE) {  // best over the 16 column lanes, one partial per (row, wave)
+        const int pq = wg * NW + wid;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
+                float k = bk[i][e];
+                int32_t c = bi[i][e];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    const float k2 = __shfl_xor(k, o, kWave);
+                    const int32_t c2 = __shfl_xor(c, o, kWave);
+                    if (k2 > k || (k2 == k && (uint32_t)c2 < (uint32_t)c)) {
+                        k = k2;
+                        c = c2;
+                    }
+                }
                 const int row = m0 + i * 16 + 4 * g + e;
-                if (row < M) y[(int64_t)row * ldy + t * 16 + rl] = f32_to_bf16_bits(acc[i][e]);
+                if (rl == 0 && row < M) smp.part[(int64_t)row * smp.pstride + pq] = LmPart{k, c};
             }
     }
+}
+
+// Merge the per-wave partials of a row; EOS / pad bookkeeping as
+// swh_sample_step's finalize (csrc/sampler.hip).
+__global__ __launch_bounds__(256) void lm_sample_finalize_kernel(const LmPart *__restrict__ part, int P,
+                                                                 swh_sample_params p, const int32_t *__restrict__ step_p,
+                                                                 int32_t *__restrict__ finished,
+                                                                 int64_t *__restrict__ out_tokens, int64_t out_ld,
+                                                                 int64_t *__restrict__ cur_tokens, int V) {
+    __shared__ float kk[4];
+    __shared__ int32_t ii[4];
+    const int64_t b = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    float k = kNegInf;
+    int32_t c = 0x7fffffff;
+    for (int q = tid; q < P; q += 256) {
+        const LmPart v = part[b * P + q];
+        if (v.key > k || (v.key == k && (uint32_t)v.idx < (uint32_t)c)) {
+            k = v.key;
+            c = v.idx;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float k2 = __shfl_xor(k, o, kWave);
+        const int32_t c2 = __shfl_xor(c, o, kWave);
+        if (k2 > k || (k2 == k && (uint32_t)c2 < (uint32_t)c)) {
+            k = k2;
+            c = c2;
+        }
+    }
+    if (lane == 0) {
+        kk[wid] = k;
+        ii[wid] = c;
+    }
+    __syncthreads();
+    if (tid != 0) return;
+    for (int q = 1; q < 4; ++q)
+        if (kk[q] > k || (kk[q] == k && (uint32_t)ii[q] < (uint32_t)c)) {
+            k = kk[q];
+            c = ii[q];
+        }
+    if (c < 0 || c >= V) c = 0;  // fully masked row (cannot happen with min_tokens_to_keep=1)
+    const int32_t step = *step_p;
+    int64_t tok = c;
+    if (p.pad_token_id >= 0 && finished[b] != 0) tok = p.pad_token_id;
+    bool is_eos = false;
+    for (int e = 0; e < p.n_eos && e < 4; ++e) is_eos |= (tok == p.eos_ids[e]);
+    if (is_eos) finished[b] = 1;
+    out_tokens[b * out_ld + step] = tok;
+    if (cur_tokens) cur_tokens[b] = tok;
 }
 
 // ---------------------------------------------------------------------------
@@ -950,6 +1088,20 @@ int launch_gemm_ms(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const
     }
 }
 
+template <bool NORM, bool SAMPLE>
+int launch_lm(dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W, int M, int N, int K,
+              const uint16_t *NWt, float eps, const float *ss_in, uint16_t *Y, int ldy, const LmSample &smp) {
+    static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in once per kernel
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&lm_head_kernel<NORM, SAMPLE>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+            return SWH_E_LAUNCH;
+        attr = true;
+    }
+    lm_head_kernel<NORM, SAMPLE><<<grid, 512, lds, s>>>(X, W, M, N, K, NWt, eps, ss_in, Y, ldy, smp);
+    return launch_status();
+}
+
 }  // namespace
 }  // namespace swh
 
@@ -1013,24 +1165,11 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
         const auto *X = static_cast<const uint16_t *>(x);
         const auto *W = static_cast<const uint16_t *>(w);
         const auto *NWt = static_cast<const uint16_t *>(norm_w);
-        if (NWt) {
-            static bool attr = false;
-            if (!attr && hipFuncSetAttribute(reinterpret_cast<const void *>(&lm_head_kernel<true>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-                return SWH_E_LAUNCH;
-            attr = true;
-            lm_head_kernel<true><<<grid, 512, (size_t)L.total, s>>>(X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Y,
-                                                                    (int)ldy);
-        } else {
-            static bool attr = false;
-            if (!attr && hipFuncSetAttribute(reinterpret_cast<const void *>(&lm_head_kernel<false>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-                return SWH_E_LAUNCH;
-            attr = true;
-            lm_head_kernel<false><<<grid, 512, (size_t)L.total, s>>>(X, W, (int)M, (int)N, (int)K, nullptr, eps,
-                                                                     nullptr, Y, (int)ldy);
-        }
-        return launch_status();
+        const LmSample none{};
+        return NWt ? launch_lm<true, false>(grid, (size_t)L.total, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Y,
+                                            (int)ldy, none)
+                   : launch_lm<false, false>(grid, (size_t)L.total, s, X, W, (int)M, (int)N, (int)K, nullptr, eps,
+                                             nullptr, Y, (int)ldy, none);
     }
     const GemmCfg c = pick_cfg(M, wcols, K, silu != 0, norm_w != nullptr);
     const int64_t MR = 16 * c.ms, nmt = (M + MR - 1) / MR, ncb = wcols / (16 * c.cb);
@@ -1070,4 +1209,44 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
     if (Bs) SWH_GEMM(false, EPI_PLAIN, true);
     SWH_GEMM(false, EPI_PLAIN, false);
 #undef SWH_GEMM
+}
+
+extern "C" int64_t swh_lm_head_sample_workspace_bytes(int64_t M, int64_t V, int64_t K) {
+    (void)V;
+    (void)K;
+    const int64_t nmt = (M + 63) / 64, per = cu_count() / nmt > 0 ? cu_count() / nmt : 1;
+    return M * per * 8 * (int64_t)sizeof(LmPart);
+}
+
+extern "C" int swh_lm_head_sample(const void *x, const void *w, int64_t M, int64_t V, int64_t K, const void *norm_w,
+                                  float eps, const float *ss_in, const swh_sample_params *params, const uint64_t *rng,
+                                  const int32_t *step, int32_t *finished, int64_t *out_tokens, int64_t out_ld,
+                                  int64_t *cur_tokens, void *workspace, int64_t workspace_bytes, void *stream) {
+    if (!x || !w || !params || !rng || !step || !finished || !out_tokens || !workspace || M <= 0 || V <= 0 ||
+        K <= 0 || K % 64 || K > 32 * kLmMaxKS || V % 16 || V >= ((int64_t)1 << 31) || M > (1 << 20))
+        return SWH_E_ARG;
+    const swh_sample_params p = *params;
+    const bool filtered = !p.greedy && ((p.top_k > 0 && p.top_k < V) || p.top_p < 1.0f || p.min_p > 0.f);
+    if (filtered || p.repetition_penalty != 1.0f || p.n_eos < 0 || p.n_eos > 4 || !(p.temperature > 0.f))
+        return SWH_E_ARG;  // the caller takes logits + swh_sample_step
+    if (workspace_bytes < swh_lm_head_sample_workspace_bytes(M, V, K)) return SWH_E_ARG;
+    if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w)) & 15) return SWH_E_ARG;
+    if ((norm_w && (reinterpret_cast<uintptr_t>(norm_w) & 15)) || (ss_in && (reinterpret_cast<uintptr_t>(ss_in) & 15)))
+        return SWH_E_ARG;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int64_t nmt = (M + 63) / 64, per = cu_count() / nmt > 0 ? cu_count() / nmt : 1;
+    const GemmLds L = gemm_lds(1, 64, 8, (int)K, (int)K, norm_w != nullptr, false);
+    const dim3 grid((unsigned)(per * nmt));
+    LmSample smp{p, rng, step, static_cast<LmPart *>(workspace), (int)(per * 8)};
+    const auto *X = static_cast<const uint16_t *>(x);
+    const auto *W = static_cast<const uint16_t *>(w);
+    const auto *NWt = static_cast<const uint16_t *>(norm_w);
+    const int rc = NWt ? launch_lm<true, true>(grid, (size_t)L.total, s, X, W, (int)M, (int)V, (int)K, NWt, eps, ss_in,
+                                                nullptr, 0, smp)
+                       : launch_lm<false, true>(grid, (size_t)L.total, s, X, W, (int)M, (int)V, (int)K, nullptr, eps,
+                                                 nullptr, nullptr, 0, smp);
+    if (rc != SWH_OK) return rc;
+    lm_sample_finalize_kernel<<<dim3((unsigned)M), 256, 0, s>>>(smp.part, smp.pstride, p, step, finished, out_tokens,
+                                                               out_ld, cur_tokens, (int)V);
+    return launch_status();
 }

@@ -73,44 +73,90 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const uint16_t *__rest
     }
 }
 
-// Backward.  Pass 1 (wave per row): c_r = mean(dy*w*n).  Pass 2 (thread per
-// column, loop over the block's rows): dx and the dw partial of this block.
+// Backward, one pass: a wave owns whole rows (16-B loads, the row stays in
+// registers): c_r = mean(dy*w*n), dx = rstd*(dy*w - n*c_r), and each lane
+// accumulates dw = sum dy*bf16(n) for its columns over the wave's rows; the
+// block's waves meet in LDS and write one dw partial row per block.
 constexpr int kNormBwdThreads = 256;
+constexpr int kNormBwdVec = 8;  // max 16-B vectors per lane per row: H <= 64 * 8 * 8 = 4096
+template <int VEC>
 __global__ __launch_bounds__(kNormBwdThreads) void rmsnorm_bwd_kernel(
     const uint16_t *__restrict__ x, const uint16_t *__restrict__ w, const float *__restrict__ rstd,
     const uint16_t *__restrict__ dy, int64_t rows, int64_t H, uint16_t *__restrict__ dx,
     float *__restrict__ dw_part, int64_t rpb) {
-    extern __shared__ float cvals[];  // [rpb]
-    const int64_t r0 = (int64_t)blockIdx.x * rpb;
+    extern __shared__ float dws[];  // [waves][H]
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int64_t i = wid; i < rpb; i += kNormBwdThreads / 64) {
-        const int64_t r = r0 + i;
-        float c = 0.f;
-        if (r < rows) {
-            const float rs = rstd[r];
-            for (int64_t h = lane; h < H; h += 64) {
-                const float n = bf16_bits_to_f32(x[r * H + h]) * rs;
-                c = fmaf(bf16_bits_to_f32(dy[r * H + h]) * bf16_bits_to_f32(w[h]), n, c);
+    constexpr int NWV = kNormBwdThreads / 64;
+    const int nv = (int)(H / 8);
+    const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+    float wv[VEC][8], dwa[VEC][8];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+        const int v = lane + 64 * j;
+        if (v < nv) unpack16<SWH_BF16>(reinterpret_cast<const uint4 *>(w)[v], wv[j]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) dwa[j][k] = 0.f;
+    }
+    for (int64_t r = r0 + wid; r < r1; r += NWV) {
+        const uint4 *xr = reinterpret_cast<const uint4 *>(x + r * H);
+        const uint4 *gr = reinterpret_cast<const uint4 *>(dy + r * H);
+        uint4 xv[VEC], gv[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            const int v = lane + 64 * j;
+            if (v < nv) {
+                xv[j] = xr[v];
+                gv[j] = gr[v];
             }
         }
-        c = wave_sum(c);
-        if (lane == 0) cvals[i] = c / (float)H;
+        const float rs = rstd[r];
+        float c = 0.f;
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            if (lane + 64 * j < nv) {
+                float a[8], g[8];
+                unpack16<SWH_BF16>(xv[j], a);
+                unpack16<SWH_BF16>(gv[j], g);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) c = fmaf(g[k] * wv[j][k], a[k] * rs, c);
+            }
+        }
+        c = wave_sum(c) / (float)H;
+        uint4 *dxr = reinterpret_cast<uint4 *>(dx + r * H);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            if (lane + 64 * j < nv) {
+                float a[8], g[8];
+                unpack16<SWH_BF16>(xv[j], a);
+                unpack16<SWH_BF16>(gv[j], g);
+                uint32_t o[4];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const float n = a[k] * rs;
+                    dwa[j][k] = fmaf(g[k], round_bf16(n), dwa[j][k]);
+                    a[k] = rs * (g[k] * wv[j][k] - n * c);
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    o[k] = (uint32_t)f32_to_bf16_bits(a[2 * k]) | ((uint32_t)f32_to_bf16_bits(a[2 * k + 1]) << 16);
+                dxr[lane + 64 * j] = uint4{o[0], o[1], o[2], o[3]};
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+        const int v = lane + 64 * j;
+        if (v < nv) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) dws[wid * H + v * 8 + k] = dwa[j][k];
+        }
     }
     __syncthreads();
     for (int64_t h = threadIdx.x; h < H; h += kNormBwdThreads) {
-        const float wh = bf16_bits_to_f32(w[h]);
-        float dwa = 0.f;
-        for (int64_t i = 0; i < rpb; ++i) {
-            const int64_t r = r0 + i;
-            if (r >= rows) break;
-            const float rs = rstd[r];
-            const float xv = bf16_bits_to_f32(x[r * H + h]);
-            const float n = xv * rs;
-            const float g = bf16_bits_to_f32(dy[r * H + h]);
-            dx[r * H + h] = f32_to_bf16_bits(rs * (g * wh - n * cvals[i]));
-            dwa = fmaf(g, round_bf16(n), dwa);
-        }
-        dw_part[(int64_t)blockIdx.x * H + h] = dwa;
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < NWV; ++q) t += dws[q * H + h];
+        dw_part[(int64_t)blockIdx.x * H + h] = t;
     }
 }
 
@@ -218,15 +264,22 @@ extern "C" int swh_rmsnorm_fwd(const void *x, const void *residual, void *residu
 
 extern "C" int swh_rmsnorm_bwd(const void *x, const void *weight, const float *rstd, const void *dy, int64_t rows,
                                int64_t H, void *dx, float *dw_partial, int64_t rows_per_block, void *stream) {
-    if (!x || !weight || !rstd || !dy || !dx || !dw_partial || rows < 0 || H <= 0 || rows_per_block <= 0 ||
-        rows_per_block > 4096)
+    if (!x || !weight || !rstd || !dy || !dx || !dw_partial || rows < 0 || H <= 0 || H % 8 ||
+        H > 64 * 8 * kNormBwdVec || rows_per_block <= 0 || rows_per_block > 4096)
         return SWH_E_ARG;
     if (rows == 0) return SWH_OK;
     const unsigned nb = (unsigned)((rows + rows_per_block - 1) / rows_per_block);
-    rmsnorm_bwd_kernel<<<dim3(nb), dim3(kNormBwdThreads), rows_per_block * sizeof(float),
-                         static_cast<hipStream_t>(stream)>>>(
-        static_cast<const uint16_t *>(x), static_cast<const uint16_t *>(weight), rstd, static_cast<const uint16_t *>(dy),
-        rows, H, static_cast<uint16_t *>(dx), dw_partial, rows_per_block);
+    const size_t lds = (kNormBwdThreads / 64) * H * sizeof(float);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const auto *X = static_cast<const uint16_t *>(x), *Wt = static_cast<const uint16_t *>(weight);
+    const auto *DY = static_cast<const uint16_t *>(dy);
+    auto *DX = static_cast<uint16_t *>(dx);
+#define SWH_NORM_BWD(V) \
+    rmsnorm_bwd_kernel<V><<<dim3(nb), dim3(kNormBwdThreads), lds, st>>>(X, Wt, rstd, DY, rows, H, DX, dw_partial, rows_per_block)
+    if (H <= 64 * 8 * 2) SWH_NORM_BWD(2);
+    else if (H <= 64 * 8 * 4) SWH_NORM_BWD(4);
+    else SWH_NORM_BWD(8);
+#undef SWH_NORM_BWD
     return launch_status();
 }
 

@@ -64,11 +64,14 @@ __device__ __forceinline__ Proc make_proc(const swh_sample_params &p, int32_t st
     return pr;
 }
 
+// Gumbel noise of element j of row `row`: word (row & 3) of Philox4x32-10 at
+// counter {j, row >> 2, ctr_lo, ctr_hi} — one Philox call serves four rows of
+// one column (the fused lm-head sampler's C layout holds exactly those).
 __device__ __forceinline__ float gumbel_at(uint32_t k0, uint32_t k1, int64_t j, int64_t row, uint64_t ctr_hi) {
-    const U4 w = philox4x32_10(U4{(uint32_t)(j >> 2), (uint32_t)row, (uint32_t)ctr_hi, (uint32_t)(ctr_hi >> 32)},
+    const U4 w = philox4x32_10(U4{(uint32_t)j, (uint32_t)(row >> 2), (uint32_t)ctr_hi, (uint32_t)(ctr_hi >> 32)},
                                k0, k1);
-    const int lane = (int)(j & 3);
-    const uint32_t bits = lane == 0 ? w.x : lane == 1 ? w.y : lane == 2 ? w.z : w.w;
+    const int q = (int)(row & 3);
+    const uint32_t bits = q == 0 ? w.x : q == 1 ? w.y : q == 2 ? w.z : w.w;
     const float u = u01_from_bits(bits);
     return -fast_log(-fast_log(u));
 }

@@ -50,6 +50,8 @@ class DecodeEngine:
         self.d = torch.empty(B, H, **bf)
         self.logits_buf = torch.empty(B, c.vocab_size, **bf)
         self.ss = torch.empty(B, H // 16, device=dev, dtype=torch.float32)  # RMSNorm partial sums of s
+        self.sample_ws = torch.empty(ops._lib.load().swh_lm_head_sample_workspace_bytes(B, c.vocab_size, H),
+                                     device=dev, dtype=torch.uint8)
         self.state = torch.zeros(2, device=dev, dtype=torch.int32)   # {step, P}
         self.rng = torch.zeros(2, device=dev, dtype=torch.int64)     # {seed, counter base}
         self.finished = torch.zeros(B, device=dev, dtype=torch.int32)
@@ -79,8 +81,15 @@ class DecodeEngine:
             self._step_fused()
         else:
             self._step_unfused()
-        self._sample()
+        if not self._fused_sample():
+            self._sample()
         ops.step_advance(self.state[0:1])
+
+    def _fused_sample(self) -> bool:
+        """lm head + sampler in one kernel (no logits): unfiltered sampling
+        without the per-token log-prob output."""
+        return (self.fused and not self.want_logp and os.environ.get("SWH_FUSED_SAMPLE", "1") != "0" and
+                nn_ops.lm_head_sample_supported(self.params, self.cfg.vocab_size, self.cfg.hidden_size))
 
     def _step_fused(self):
         c, m = self.cfg, self.model
@@ -98,7 +107,11 @@ class DecodeEngine:
             nn_ops.decode_gemm(self.s, p[f"l{i}.gu_w"], norm_w=p[f"l{i}.ln_post"], eps=eps, silu=True, y=self.act,
                                ss_in=ss)
             nn_ops.decode_gemm(self.act, p[f"l{i}.down_w"], residual=self.s, ss_out=ss)
-        nn_ops.decode_gemm(self.s, m.lm_weight(), norm_w=p["norm"], eps=eps, y=self.logits_buf, ss_in=ss)
+        if self._fused_sample():
+            nn_ops.lm_head_sample(self.s, m.lm_weight(), self.params, self.rng, self.state[0:1], self.finished,
+                                  self.out, self.cur, norm_w=p["norm"], eps=eps, ss_in=ss, workspace=self.sample_ws)
+        else:
+            nn_ops.decode_gemm(self.s, m.lm_weight(), norm_w=p["norm"], eps=eps, y=self.logits_buf, ss_in=ss)
 
     def _step_unfused(self):
         c, m = self.cfg, self.model
@@ -206,6 +219,13 @@ class DecodeEngine:
                                     c.vocab_size * H * bf + B * c.vocab_size * bf, 1),
             "sample_step": (self._sample, B * c.vocab_size * bf, 1),
         }
+        if self._fused_sample():  # what the decode graph runs instead of lm head + sample_step
+            del ops_["decode_gemm.lm_head"], ops_["sample_step"]
+            ops_["lm_head_sample"] = (
+                lambda: nn_ops.lm_head_sample(self.s, m.lm_weight(), self.params, self.rng, self.state[0:1],
+                                              self.finished, self.out, self.cur, norm_w=p["norm"], eps=eps,
+                                              ss_in=ss, workspace=self.sample_ws),
+                c.vocab_size * H * bf, 1)
         nn_ops.embed_gather(p["embed"], self.cur, self.s, ss_out=ss)
         out = {}
         stream = torch.cuda.current_stream()

@@ -332,14 +332,13 @@ class CausalLM:
         k = _apply_rope(k, cos, sin)
         if kv_out is not None:
             kv_out(i, k, v)
-        rep = Hq // Hkv
-        if rep > 1:
-            k = k.repeat_interleave(rep, dim=1)
-            v = v.repeat_interleave(rep, dim=1)
+        # GQA inside the attention kernel: materialising repeat_interleave'd K/V
+        # (and summing its gradient back) costs 5x the attention itself
+        gqa = Hq != Hkv
         if mask is None:
-            o = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=D ** -0.5)
+            o = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=D ** -0.5, enable_gqa=gqa)
         else:
-            o = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, scale=D ** -0.5)
+            o = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, scale=D ** -0.5, enable_gqa=gqa)
         o = o.transpose(1, 2).reshape(B, L, c.q_dim)
         o = _Linear.apply(o, self.p[f"l{i}.o_w"], None, self._gv(f"l{i}.o_w"), None)
         x = x + o

@@ -148,3 +148,30 @@ def decode_gemm(x: torch.Tensor, w: torch.Tensor, *, norm_w: Optional[torch.Tens
     call("swh_decode_gemm", x.data_ptr(), w.data_ptr(), M, N, K, _p(norm_w), float(eps), _p(bias), _p(residual),
          int(bool(silu)), _p(y), ldy, _p(ss_in), _p(ss_out), ws.data_ptr(), ws.numel(), _stream())
     return residual if residual is not None else y
+
+
+def lm_head_sample_supported(params, V: int, K: int) -> bool:
+    """The fused lm-head sampler covers unfiltered sampling (temperature,
+    greedy, EOS suppression); the rest goes through logits + sample_step."""
+    filtered = not params.greedy and ((0 < params.top_k < V) or params.top_p < 1.0 or params.min_p > 0.0)
+    return (not filtered and params.repetition_penalty == 1.0 and K % 64 == 0 and K <= 1024 and V % 16 == 0)
+
+
+def lm_head_sample(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Tensor, step: torch.Tensor,
+                   finished: torch.Tensor, out_tokens: torch.Tensor, cur_tokens: Optional[torch.Tensor] = None, *,
+                   norm_w: Optional[torch.Tensor] = None, eps: float = 1e-6, ss_in: Optional[torch.Tensor] = None,
+                   workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """lm head + the unfiltered sampler in one pass, no logits tensor
+    (include/swh_trl_amd.h swh_lm_head_sample).  Writes out_tokens[:, *step],
+    cur_tokens, finished; returns out_tokens."""
+    import ctypes
+    _dev(x, "lm_head_sample")
+    M, K = x.shape
+    V = w.shape[0]
+    need = _lib.load().swh_lm_head_sample_workspace_bytes(M, V, K)
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=x.device)
+    call("swh_lm_head_sample", x.data_ptr(), w.data_ptr(), M, V, K, _p(norm_w), float(eps), _p(ss_in),
+         ctypes.byref(params), rng.data_ptr(), step.data_ptr(), finished.data_ptr(), out_tokens.data_ptr(),
+         out_tokens.stride(0), _p(cur_tokens), workspace.data_ptr(), workspace.numel(), _stream())
+    return out_tokens

@@ -93,10 +93,11 @@ def test_decode_graph_equals_eager_and_full_forward(dev):
     assert agree.all(), (~agree).nonzero()[:5]
 
 
-def test_fused_decode_step_matches_unfused(dev):
+def test_fused_decode_step_matches_unfused(dev, monkeypatch):
     """The 5-kernel fused decode layer equals the unfused (hipBLASLt + separate
     norm/SiLU/residual) step on the same state, within bf16 rounding."""
     from swh_trl_amd.engine import DecodeEngine
+    monkeypatch.setenv("SWH_FUSED_SAMPLE", "0")  # keep the logits of the decode step
     m = _tiny(dev, seed=7, layers=2)
     B, P, C = 6, 9, 4
     ids = torch.randint(0, m.cfg.vocab_size, (B, P), device=dev)
@@ -109,6 +110,26 @@ def test_fused_decode_step_matches_unfused(dev):
         outs.append(e.logits_buf.float().clone())
     err = (outs[0] - outs[1]).abs().max().item()
     assert err <= 0.02 * outs[1].abs().max().item() + 0.02, err
+
+
+@pytest.mark.parametrize("kw", [dict(greedy=True), dict(temperature=0.9, min_new_tokens=3)])
+def test_fused_sampler_generation_equals_logits_path(dev, monkeypatch, kw):
+    """Whole graph-captured generations: lm head + sampler fused (no logits)
+    and lm head -> logits -> sample_step draw identical token sequences."""
+    from swh_trl_amd.engine import DecodeEngine
+    m = _tiny(dev, seed=8, layers=2)
+    B, P, C = 8, 12, 16
+    g = torch.Generator().manual_seed(8)
+    ids = torch.randint(0, m.cfg.vocab_size, (B, P), generator=g).to(dev)
+    mask = torch.ones(B, P, dtype=torch.int32, device=dev)
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SWH_FUSED_SAMPLE", flag)
+        e = DecodeEngine(m, B, P, C)
+        assert e._fused_sample() == (flag == "1") or not e.fused
+        toks, _ = e.generate(ids, mask, C, seed=5, eos_token_id=2, pad_token_id=0, **kw)
+        outs.append(toks)
+    assert torch.equal(outs[0], outs[1])
 
 
 def test_greedy_matches_transformers_generate(dev):

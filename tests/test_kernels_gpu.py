@@ -693,3 +693,55 @@ def test_decode_gemm_persistent_epilogues(ops, dev):
     ref = r0 + (a.float() @ w.float().t()).to(torch.bfloat16)
     torch.testing.assert_close(r.float(), ref.float(), rtol=1e-2, atol=2e-2)
     torch.testing.assert_close(ss, _chunk_ss(r), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(temperature=0.7), dict(greedy=True), dict(min_new_tokens=5),
+                                dict(temperature=1.3, min_new_tokens=1)])
+@pytest.mark.parametrize("M,V", [(64, 151936), (70, 32768)])
+def test_lm_head_sample_equals_logits_then_sampler(ops, dev, kw, M, V):
+    """The fused lm head + sampler draws, bit for bit, the token swh_sample_step
+    draws from the materialised bf16 logits (same rng, same step), including
+    EOS suppression, pad-after-EOS and the finished flags."""
+    from swh_trl_amd import nn_ops
+    g = _gen(36)
+    H = 896
+    x = torch.randn(M, H, generator=g).to(torch.bfloat16).to(dev)
+    w = (torch.randn(V, H, generator=g) * 0.5).to(torch.bfloat16).to(dev)
+    nw = (1 + 0.1 * torch.randn(H, generator=g)).to(torch.bfloat16).to(dev)
+    ss = x.float().view(M, H // 16, 16).pow(2).sum(-1).contiguous()
+    eos = [3, 77]
+    w[3] += 0.2  # make EOS likely so suppression and bookkeeping matter
+    params = ops.make_sample_params(eos_token_ids=eos, pad_token_id=5, **kw)
+    step = 2
+    rng = torch.tensor([123, 45], dtype=torch.int64, device=dev)
+    stp = torch.tensor([step], dtype=torch.int32, device=dev)
+    fin0 = (torch.arange(M) % 7 == 0).int().to(dev)
+    logits = nn_ops.decode_gemm(x, w, norm_w=nw, eps=1e-6, ss_in=ss)
+    out_a = torch.full((M, 4), -1, dtype=torch.int64, device=dev)
+    cur_a = torch.empty(M, dtype=torch.int64, device=dev)
+    fin_a = fin0.clone()
+    ops.sample_step(logits, params, rng, stp, fin_a, out_a, cur_a)
+    out_b = torch.full((M, 4), -1, dtype=torch.int64, device=dev)
+    cur_b = torch.empty(M, dtype=torch.int64, device=dev)
+    fin_b = fin0.clone()
+    nn_ops.lm_head_sample(x, w, params, rng, stp, fin_b, out_b, cur_b, norm_w=nw, eps=1e-6, ss_in=ss)
+    assert torch.equal(out_b, out_a)
+    assert torch.equal(cur_b, cur_a)
+    assert torch.equal(fin_b, fin_a)
+    if kw.get("min_new_tokens", 0) > step:
+        assert not torch.isin(out_b[:, step], torch.tensor(eos, device=dev)).any()
+
+
+def test_lm_head_sample_refuses_filtered(ops, dev):
+    from swh_trl_amd import nn_ops
+    x = torch.zeros(4, 896, dtype=torch.bfloat16, device=dev)
+    w = torch.zeros(1024, 896, dtype=torch.bfloat16, device=dev)
+    rng = torch.zeros(2, dtype=torch.int64, device=dev)
+    stp = torch.zeros(1, dtype=torch.int32, device=dev)
+    fin = torch.zeros(4, dtype=torch.int32, device=dev)
+    out = torch.zeros(4, 2, dtype=torch.int64, device=dev)
+    for kw in (dict(top_k=5), dict(top_p=0.9), dict(min_p=0.1), dict(repetition_penalty=1.2)):
+        p = ops.make_sample_params(**kw)
+        assert not nn_ops.lm_head_sample_supported(p, 1024, 896)
+        with pytest.raises(ValueError):
+            nn_ops.lm_head_sample(x, w, p, rng, stp, fin, out)
