@@ -88,11 +88,12 @@ __device__ __forceinline__ uint4 pack8(const float *v) {
 struct GemmLds {
     int64_t nw_off, ss_off, body_off, xs_bytes, slots_off, total;
 };
-__host__ __device__ inline GemmLds gemm_lds(int cb, int mr, int nw, int krmax, int K, bool norm, bool persist) {
+// nm: 0 = plain X, 1 = RMSNorm applied to the X image, 2 = rstd row scale in the epilogue
+__host__ __device__ inline GemmLds gemm_lds(int cb, int mr, int nw, int krmax, int K, int nm, bool persist) {
     GemmLds L;
     L.nw_off = 512;
-    L.ss_off = L.nw_off + (norm ? (int64_t)krmax * 4 : 0);  // norm weights as f32
-    L.body_off = L.ss_off + (norm ? ((int64_t)mr * (K / 64) * 4 + 15) / 16 * 16 : 0);  // partials beside the DMA'd image
+    L.ss_off = L.nw_off + (nm == 1 ? (int64_t)krmax * 4 : 0);  // norm weights as f32
+    L.body_off = L.ss_off + (nm ? ((int64_t)mr * (K / 64) * 4 + 15) / 16 * 16 : 0);  // partials beside the DMA'd image
     L.xs_bytes = (int64_t)mr * (krmax * 2 + 16);
     const int64_t slots = (int64_t)(nw > 1 ? nw / 2 : 1) * 16 * cb * (mr + 4) * 4;  // [NW/2][NB][MR+4]
     L.slots_off = L.body_off + (persist ? L.xs_bytes : 0);
@@ -118,7 +119,7 @@ __host__ __device__ inline GemmLds gemm_lds(int cb, int mr, int nw, int krmax, i
 // independent — MI355X_MICROARCH.md §Workgroup dispatch) and runs the epilogue.
 constexpr int kU = 4;    // k-steps whose loads are issued together
 
-template <int CB, int MS, bool NORM, int EPI, bool BIAS>
+template <int CB, int MS, int NM, int EPI, bool BIAS>
 __global__ __launch_bounds__(512) void decode_gemm_kernel(
     const uint16_t *__restrict__ x, const uint16_t *__restrict__ w, int M, int N, int K,
     const uint16_t *__restrict__ norm_w, float eps, const float *__restrict__ ss_in,
@@ -148,7 +149,7 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
     const int m0 = mt * MR;
     const int KS = K / 32, kb0 = (int)((int64_t)KS * sidx / S), kb1 = (int)((int64_t)KS * (sidx + 1) / S);
     const int Kr = (kb1 - kb0) * 32, k0 = kb0 * 32, RS = Kr * 2 + 16;
-    const GemmLds L = gemm_lds(CB, MR, NW, (KS + S - 1) / S * 32, K, NORM, persist != 0);
+    const GemmLds L = gemm_lds(CB, MR, NW, (KS + S - 1) / S * 32, K, NM, persist != 0);
     float *rstd_s = reinterpret_cast<float *>(lds);
     int *flag_s = reinterpret_cast<int *>(lds + 256);
     float *nw_s = reinterpret_cast<float *>(lds + L.nw_off);
@@ -160,10 +161,10 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
 
     // ---- (a) RMSNorm partial sums and the norm-weight slice (L2), first in the queue
     const int nc = K / 64;
-    const bool use_ss = NORM && ss_in && MR * nc <= 4 * NT;
+    const bool use_ss = NM && ss_in && MR * nc <= 4 * NT;
     float4 ssv[4];
     uint4 nwv[2];
-    if constexpr (NORM) {
+    if constexpr (NM != 0) {
         if (use_ss) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -172,9 +173,11 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
                 ssv[q] = reinterpret_cast<const float4 *>(ss_in + (int64_t)min(m0 + r, M - 1) * (K / 16))[c];
             }
         }
+        if constexpr (NM == 1) {
 #pragma unroll
-        for (int q = 0; q < 2; ++q)
-            nwv[q] = reinterpret_cast<const uint4 *>(norm_w + k0)[min(tid + q * NT, Kr / 8 - 1)];
+            for (int q = 0; q < 2; ++q)
+                nwv[q] = reinterpret_cast<const uint4 *>(norm_w + k0)[min(tid + q * NT, Kr / 8 - 1)];
+        }
     }
     // ---- (b) epilogue operands of a single-block workgroup (L2): <= 2 per thread in every geometry
     const int ncol0 = cb_first * (EPI == EPI_SILU ? NB / 2 : NB);
@@ -239,7 +242,7 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
     SWH_GEMM_TRACE(1);
 
     // ---- (d) row statistic and norm weights into LDS
-    if constexpr (NORM) {
+    if constexpr (NM != 0) {
         if (use_ss) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -249,7 +252,7 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
         }
 #pragma unroll
         for (int q = 0; q < 2; ++q)
-            if (tid + q * NT < Kr / 8) {
+            if (NM == 1 && tid + q * NT < Kr / 8) {
                 float f[8];
                 unpack16<SWH_BF16>(nwv[q], f);
                 reinterpret_cast<float4 *>(nw_s)[2 * (tid + q * NT)] = float4{f[0], f[1], f[2], f[3]};
@@ -285,7 +288,7 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
     // ---- (e) X image landed (all but the kU * CB weight loads retired), normalised in place
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kU * CB) : "memory");
     lds_barrier();
-    if constexpr (NORM) {
+    if constexpr (NM == 1) {
         int r = tid / ppr, c = tid - r * ppr;
         const int rstep = NT / ppr, cstep = NT - rstep * ppr;
         for (; r < MR;) {
@@ -395,9 +398,11 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
                 const int gr = m0 + r;
                 if (gr >= M) continue;
                 float o[8];
+                const float sc = (NM == 2) ? rstd_s[r] : 1.f;  // folded RMSNorm: y = rstd * (x W'^T)
 #pragma unroll
                 for (int cc = 0; cc < 8; ++cc) {
-                    const float g = round_bf16(slot(0, r, jb * 16 + cc)), u = round_bf16(slot(0, r, jb * 16 + 8 + cc));
+                    const float g = round_bf16(slot(0, r, jb * 16 + cc) * sc);
+                    const float u = round_bf16(slot(0, r, jb * 16 + 8 + cc) * sc);
                     o[cc] = round_bf16(g / (1.f + expf(-g))) * u;
                 }
                 *reinterpret_cast<uint4 *>(y + (int64_t)gr * ldy + n0 + jb * 8) = pack8(o);
@@ -411,8 +416,9 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
                 const int gr = m0 + r, gc = n0 + c8;
                 if (gr >= M) continue;
                 float v[8];
+                const float sc = (NM == 2) ? rstd_s[r] : 1.f;  // folded RMSNorm: y = rstd * (x W'^T)
 #pragma unroll
-                for (int cc = 0; cc < 8; ++cc) v[cc] = slot(0, r, c8 + cc);
+                for (int cc = 0; cc < 8; ++cc) v[cc] = slot(0, r, c8 + cc) * sc;
                 if constexpr (BIAS) {
                     float b[8];
                     unpack16<SWH_BF16>(persist ? *reinterpret_cast<const uint4 *>(bias + gc) : pre_bias[q], b);
@@ -478,7 +484,7 @@ struct LmSample {
     int pstride;
 };
 
-template <bool NORM, bool SAMPLE>
+template <int NM, bool SAMPLE>
 __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict__ x, const uint16_t *__restrict__ w,
                                                       int M, int N, int K, const uint16_t *__restrict__ norm_w,
                                                       float eps, const float *__restrict__ ss_in,
@@ -489,7 +495,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
     const int nmt = (M + 63) / 64, mt = blockIdx.x % nmt, m0 = mt * 64;
     const int wgs = gridDim.x / nmt, wg = blockIdx.x / nmt;
     const int ntile = N / 16, KS = K / 32, RS = K * 2 + 16;
-    const GemmLds L = gemm_lds(1, 64, NW, K, K, NORM, false);
+    const GemmLds L = gemm_lds(1, 64, NW, K, K, NM, false);
     float *rstd_s = reinterpret_cast<float *>(lds);
     float *nw_s = reinterpret_cast<float *>(lds + L.nw_off);
     float *ssp = reinterpret_cast<float *>(lds + L.ss_off);
@@ -507,10 +513,10 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
     if (t < ntile) issue(t);  // the weight stream first
     // RMSNorm partials and norm weights (L2), then the X image by LDS-DMA
     const int nc = K / 64;
-    const bool use_ss = NORM && ss_in && 64 * nc <= 4 * NT;
+    const bool use_ss = NM && ss_in && 64 * nc <= 4 * NT;
     float4 ssv[4];
     uint4 nwv[2];
-    if constexpr (NORM) {
+    if constexpr (NM != 0) {
         if (use_ss) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -519,8 +525,10 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
                 ssv[q] = reinterpret_cast<const float4 *>(ss_in + (int64_t)min(m0 + r, M - 1) * (K / 16))[c];
             }
         }
+        if constexpr (NM == 1) {
 #pragma unroll
-        for (int q = 0; q < 2; ++q) nwv[q] = reinterpret_cast<const uint4 *>(norm_w)[min(tid + q * NT, K / 8 - 1)];
+            for (int q = 0; q < 2; ++q) nwv[q] = reinterpret_cast<const uint4 *>(norm_w)[min(tid + q * NT, K / 8 - 1)];
+        }
     }
     const int ppr = K / 8, jpl = (ppr + 63) >> 6;
     for (int r = wid; r < 64; r += NW) {
@@ -533,7 +541,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
                                                  16, 0, 0);
         }
     }
-    if constexpr (NORM) {
+    if constexpr (NM != 0) {
         if (use_ss) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -543,7 +551,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
         }
 #pragma unroll
         for (int q = 0; q < 2; ++q)
-            if (tid + q * NT < K / 8) {
+            if (NM == 1 && tid + q * NT < K / 8) {
                 float f[8];
                 unpack16<SWH_BF16>(nwv[q], f);
                 reinterpret_cast<float4 *>(nw_s)[2 * (tid + q * NT)] = float4{f[0], f[1], f[2], f[3]};
@@ -552,7 +560,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // image (and this wave's first tile) landed
     lds_barrier();
-    if constexpr (NORM) {
+    if constexpr (NM != 0) {
         if (tid < 64) {
             float ssum = 0.f;
             if (use_ss) {
@@ -568,6 +576,13 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
             rstd_s[tid] = rsqrtf(ssum / (float)K + eps);
         }
         lds_barrier();
+    }
+    float rsr[4][4];  // folded RMSNorm (NM 2): the row scale of each accumulator row
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) rsr[i][e] = (NM == 2) ? rstd_s[i * 16 + 4 * g + e] : 1.f;
+    if constexpr (NM == 1) {
         int r = tid / ppr, c = tid - r * ppr;
         const int rstep = NT / ppr, cstep = NT - rstep * ppr;
         while (r < 64) {
@@ -635,7 +650,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
                 const uint32_t wd[4] = {rw.x, rw.y, rw.z, rw.w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    float z = round_bf16(acc[i][e]);  // the bf16 logit
+                    float z = round_bf16(acc[i][e] * rsr[i][e]);  // the bf16 logit
                     if (temp != 1.f) z = z / temp;
                     const float key = masked ? kNegInf
                                      : smp.p.greedy ? z
@@ -653,7 +668,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int row = m0 + i * 16 + 4 * g + e;
-                    if (row < M) y[(int64_t)row * ldy + t * 16 + rl] = f32_to_bf16_bits(acc[i][e]);
+                    if (row < M) y[(int64_t)row * ldy + t * 16 + rl] = f32_to_bf16_bits(acc[i][e] * rsr[i][e]);
                 }
         }
     }
@@ -983,10 +998,10 @@ inline int gemm_waves(int ms) { return ms == 4 ? 8 : 4; }
 // ~3 us, the bytes one CU pulls through its load path at ~60 GB/s (weights in
 // fragment order count twice), ~1 us per 10k elements of in-LDS RMSNorm,
 // +9 us for a cross-workgroup split, +3 us per extra wave of workgroups.
-double gemm_cost(const GemmCfg &c, int64_t M, int64_t wcols, int64_t K, bool norm) {
+double gemm_cost(const GemmCfg &c, int64_t M, int64_t wcols, int64_t K, int nm) {
     const int64_t MR = 16 * c.ms, KS = K / 32, ncu = cu_count();
     const int64_t krmax = (KS + c.s - 1) / c.s * 32;
-    const GemmLds L = gemm_lds(c.cb, (int)MR, c.nw, (int)krmax, (int)K, norm, c.persist);
+    const GemmLds L = gemm_lds(c.cb, (int)MR, c.nw, (int)krmax, (int)K, nm, c.persist);
     if (L.total > 160 * 1024) return 1e30;
     const int64_t ncb = wcols / (16 * c.cb), nmt = (M + MR - 1) / MR;
     const int64_t xbytes = MR * krmax * 2, wbytes = 2 * 16 * c.cb * krmax * 2;
@@ -998,11 +1013,11 @@ double gemm_cost(const GemmCfg &c, int64_t M, int64_t wcols, int64_t K, bool nor
     int64_t res = (160 * 1024) / L.total;
     res = res < 1 ? 1 : (res > 2 ? 2 : res);
     const int64_t per_cu = (wgs + ncu - 1) / ncu, waves = (wgs + ncu * res - 1) / (ncu * res);
-    const double norm_us = norm ? (double)(MR * krmax) / 10e3 : 0.0;  // in-LDS RMSNorm pass
+    const double norm_us = nm == 1 ? (double)(MR * krmax) / 10e3 : 0.0;  // in-LDS RMSNorm pass
     return 3.0 + per_cu * ((xbytes + wbytes) / 60e3 + norm_us) + (c.s > 1 ? 9.0 : 0.0) + (waves - 1) * 3.0;
 }
 
-GemmCfg pick_cfg(int64_t M, int64_t wcols, int64_t K, bool silu, bool norm) {
+GemmCfg pick_cfg(int64_t M, int64_t wcols, int64_t K, bool silu, int nm) {
     const int64_t KS = K / 32, align = silu ? 2 : 1, ncu = cu_count();
     GemmCfg best{4, 4, 8, 1, 0, false};
     double best_cost = 1e31;
@@ -1012,7 +1027,7 @@ GemmCfg pick_cfg(int64_t M, int64_t wcols, int64_t K, bool silu, bool norm) {
             for (int sp = 1; sp <= 8; ++sp) {
                 if (sp > KS) break;
                 GemmCfg c{ms, cb, gemm_waves(ms), sp, 0, false};
-                const double t = gemm_cost(c, M, wcols, K, norm);
+                const double t = gemm_cost(c, M, wcols, K, nm);
                 if (t < best_cost) {
                     best_cost = t;
                     best = c;
@@ -1024,7 +1039,7 @@ GemmCfg pick_cfg(int64_t M, int64_t wcols, int64_t K, bool silu, bool norm) {
     if (wcols % (32 * align) == 0 && ncu / nmt64 >= 1) {
         GemmCfg c{4, 2, 8, 1, (int)((ncu / nmt64) * nmt64), true};
         if (c.gx > wcols / 32 * nmt64) c.gx = (int)(wcols / 32 * nmt64);
-        if (gemm_cost(c, M, wcols, K, norm) < best_cost) best = c;
+        if (gemm_cost(c, M, wcols, K, nm) < best_cost) best = c;
     }
     if (const char *e = getenv("SWH_GEMM_CFG")) {  // tuning override "ms,cb,s[,p]"
         int a = 0, b = 0, d = 0, pz = 0;
@@ -1037,7 +1052,7 @@ GemmCfg pick_cfg(int64_t M, int64_t wcols, int64_t K, bool silu, bool norm) {
                 const int64_t per = ncu / nmt > 0 ? ncu / nmt : 1, ncb = wcols / (16 * b);
                 c.gx = (int)((per < ncb ? per : ncb) * nmt);
             }
-            if (gemm_cost(c, M, wcols, K, norm) < 1e29) best = c;
+            if (gemm_cost(c, M, wcols, K, nm) < 1e29) best = c;
         }
     }
     if (!best.persist) best.gx = (int)(8 * ((M + 16 * best.ms - 1) / (16 * best.ms)) * ((wcols / (16 * best.cb) + 7) / 8));
@@ -1050,55 +1065,55 @@ int64_t slab_bytes(const GemmCfg &c, int64_t M, int64_t wcols) {
     return nmt * wcols * c.s * MR * (int64_t)sizeof(float);  // tiles * NB == nmt * wcols
 }
 
-template <int CB, int MS, bool NORM, int EPI, bool BIAS>
+template <int CB, int MS, int NM, int EPI, bool BIAS>
 int launch_gemm(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W, int m,
                 int n, int k, const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs, uint16_t *R,
                 float *ss_out, uint16_t *Y, int ld, float *slab, int *ctr) {
     static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in once per kernel
     if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&decode_gemm_kernel<CB, MS, NORM, EPI, BIAS>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&decode_gemm_kernel<CB, MS, NM, EPI, BIAS>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
             return SWH_E_LAUNCH;
         attr = true;
     }
-    decode_gemm_kernel<CB, MS, NORM, EPI, BIAS><<<grid, 64u * c.nw, lds, s>>>(
+    decode_gemm_kernel<CB, MS, NM, EPI, BIAS><<<grid, 64u * c.nw, lds, s>>>(
         X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr, c.persist ? 1 : 0);
     return launch_status();
 }
 
-template <int MS, bool NORM, int EPI, bool BIAS>
+template <int MS, int NM, int EPI, bool BIAS>
 int launch_gemm_cb(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W,
                    int m, int n, int k, const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs,
                    uint16_t *R, float *ss_out, uint16_t *Y, int ld, float *slab, int *ctr) {
     switch (c.cb) {
-    case 1: return launch_gemm<1, MS, NORM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
-    case 2: return launch_gemm<2, MS, NORM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
-    default: return launch_gemm<4, MS, NORM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
+    case 1: return launch_gemm<1, MS, NM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
+    case 2: return launch_gemm<2, MS, NM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
+    default: return launch_gemm<4, MS, NM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
     }
 }
 
-template <bool NORM, int EPI, bool BIAS>
+template <int NM, int EPI, bool BIAS>
 int launch_gemm_ms(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W,
                    int m, int n, int k, const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs,
                    uint16_t *R, float *ss_out, uint16_t *Y, int ld, float *slab, int *ctr) {
     switch (c.ms) {
-    case 1: return launch_gemm_cb<1, NORM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
-    case 2: return launch_gemm_cb<2, NORM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
-    default: return launch_gemm_cb<4, NORM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
+    case 1: return launch_gemm_cb<1, NM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
+    case 2: return launch_gemm_cb<2, NM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
+    default: return launch_gemm_cb<4, NM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
     }
 }
 
-template <bool NORM, bool SAMPLE>
+template <int NM, bool SAMPLE>
 int launch_lm(dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W, int M, int N, int K,
               const uint16_t *NWt, float eps, const float *ss_in, uint16_t *Y, int ldy, const LmSample &smp) {
     static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in once per kernel
     if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&lm_head_kernel<NORM, SAMPLE>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&lm_head_kernel<NM, SAMPLE>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
             return SWH_E_LAUNCH;
         attr = true;
     }
-    lm_head_kernel<NORM, SAMPLE><<<grid, 512, lds, s>>>(X, W, M, N, K, NWt, eps, ss_in, Y, ldy, smp);
+    lm_head_kernel<NM, SAMPLE><<<grid, 512, lds, s>>>(X, W, M, N, K, NWt, eps, ss_in, Y, ldy, smp);
     return launch_status();
 }
 
@@ -1128,7 +1143,7 @@ extern "C" int swh_attn_decode(const void *qkv, void *k_cache, void *v_cache, co
 extern "C" int64_t swh_decode_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K) {
     if (M <= 0 || N <= 0 || K <= 0) return kCounterBytes;
     int64_t a = 0, b = 0;
-    for (bool nrm : {false, true}) {
+    for (int nrm : {0, 1, 2}) {
         const int64_t a1 = slab_bytes(pick_cfg(M, N, K, false, nrm), M, N);
         const int64_t b1 = slab_bytes(pick_cfg(M, 2 * N, K, true, nrm), M, 2 * N);
         a = a1 > a ? a1 : a;
@@ -1145,7 +1160,7 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
         return SWH_E_ARG;
     if (residual && (silu || bias)) return SWH_E_ARG;
     if (!residual && !y) return SWH_E_ARG;
-    if (ss_in && !norm_w) return SWH_E_ARG;
+    if (ss_in && !norm_w && residual) return SWH_E_ARG;  // folded-norm row scale: plain / SiLU epilogues
     if (ss_out && !residual) return SWH_E_ARG;
     if (N % (silu ? 8 : 16) || ldy % 8 || ldy < N) return SWH_E_ARG;
     const uintptr_t out_ptr = reinterpret_cast<uintptr_t>(residual ? residual : y);
@@ -1158,7 +1173,8 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
     if (!silu && !residual && !bias && N / 16 > 8 * (int64_t)cu_count() && K <= 32 * kLmMaxKS &&
         !getenv("SWH_GEMM_CFG")) {  // the lm head: persistent, waves own tiles
         const int64_t nmt = (M + 63) / 64;
-        const GemmLds L = gemm_lds(1, 64, 8, (int)K, (int)K, norm_w != nullptr, false);
+        const int nm = norm_w ? 1 : (ss_in ? 2 : 0);
+        const GemmLds L = gemm_lds(1, 64, 8, (int)K, (int)K, nm, false);
         const int64_t per = cu_count() / nmt > 0 ? cu_count() / nmt : 1;
         const dim3 grid((unsigned)(per * nmt));
         auto *Y = static_cast<uint16_t *>(y);
@@ -1166,12 +1182,17 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
         const auto *W = static_cast<const uint16_t *>(w);
         const auto *NWt = static_cast<const uint16_t *>(norm_w);
         const LmSample none{};
-        return NWt ? launch_lm<true, false>(grid, (size_t)L.total, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Y,
-                                            (int)ldy, none)
-                   : launch_lm<false, false>(grid, (size_t)L.total, s, X, W, (int)M, (int)N, (int)K, nullptr, eps,
-                                             nullptr, Y, (int)ldy, none);
+        if (nm == 1)
+            return launch_lm<1, false>(grid, (size_t)L.total, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Y,
+                                       (int)ldy, none);
+        if (nm == 2)
+            return launch_lm<2, false>(grid, (size_t)L.total, s, X, W, (int)M, (int)N, (int)K, nullptr, eps, ss_in, Y,
+                                       (int)ldy, none);
+        return launch_lm<0, false>(grid, (size_t)L.total, s, X, W, (int)M, (int)N, (int)K, nullptr, eps, nullptr, Y,
+                                   (int)ldy, none);
     }
-    const GemmCfg c = pick_cfg(M, wcols, K, silu != 0, norm_w != nullptr);
+    const int nm = norm_w ? 1 : (ss_in ? 2 : 0);
+    const GemmCfg c = pick_cfg(M, wcols, K, silu != 0, nm);
     const int64_t MR = 16 * c.ms, nmt = (M + MR - 1) / MR, ncb = wcols / (16 * c.cb);
     // workspace: [counters (zeroed once, self-resetting) | fp32 slabs]
     int *ctr = static_cast<int *>(workspace);
@@ -1190,24 +1211,29 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
     auto *R = static_cast<uint16_t *>(residual);
     auto *Y = static_cast<uint16_t *>(y);
     const int m = (int)M, n = (int)N, k = (int)K, ld = (int)ldy;
-    const GemmLds L = gemm_lds(c.cb, (int)MR, c.nw, (int)((K / 32 + c.s - 1) / c.s * 32), (int)K, NWt != nullptr, c.persist);
+    const GemmLds L = gemm_lds(c.cb, (int)MR, c.nw, (int)((K / 32 + c.s - 1) / c.s * 32), (int)K, nm, c.persist);
     if (L.total > 160 * 1024 || c.gx <= 0) return SWH_E_ARG;
     const dim3 grid((unsigned)c.gx, 1u, (unsigned)c.s);
     const size_t lds = (size_t)L.total;
 #define SWH_GEMM(NORM_, EPI_, BIAS_) \
     return launch_gemm_ms<NORM_, EPI_, BIAS_>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr)
     if (silu) {
-        if (NWt) SWH_GEMM(true, EPI_SILU, false);
-        SWH_GEMM(false, EPI_SILU, false);
+        if (nm == 1) SWH_GEMM(1, EPI_SILU, false);
+        if (nm == 2) SWH_GEMM(2, EPI_SILU, false);
+        SWH_GEMM(0, EPI_SILU, false);
     }
     if (residual) {
-        if (NWt) SWH_GEMM(true, EPI_RESIDUAL, false);
-        SWH_GEMM(false, EPI_RESIDUAL, false);
+        if (nm == 1) SWH_GEMM(1, EPI_RESIDUAL, false);
+        SWH_GEMM(0, EPI_RESIDUAL, false);
     }
-    if (NWt && Bs) SWH_GEMM(true, EPI_PLAIN, true);
-    if (NWt) SWH_GEMM(true, EPI_PLAIN, false);
-    if (Bs) SWH_GEMM(false, EPI_PLAIN, true);
-    SWH_GEMM(false, EPI_PLAIN, false);
+    if (Bs) {
+        if (nm == 1) SWH_GEMM(1, EPI_PLAIN, true);
+        if (nm == 2) SWH_GEMM(2, EPI_PLAIN, true);
+        SWH_GEMM(0, EPI_PLAIN, true);
+    }
+    if (nm == 1) SWH_GEMM(1, EPI_PLAIN, false);
+    if (nm == 2) SWH_GEMM(2, EPI_PLAIN, false);
+    SWH_GEMM(0, EPI_PLAIN, false);
 #undef SWH_GEMM
 }
 
@@ -1235,16 +1261,19 @@ extern "C" int swh_lm_head_sample(const void *x, const void *w, int64_t M, int64
         return SWH_E_ARG;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int64_t nmt = (M + 63) / 64, per = cu_count() / nmt > 0 ? cu_count() / nmt : 1;
-    const GemmLds L = gemm_lds(1, 64, 8, (int)K, (int)K, norm_w != nullptr, false);
+    const int nm = norm_w ? 1 : (ss_in ? 2 : 0);
+    const GemmLds L = gemm_lds(1, 64, 8, (int)K, (int)K, nm, false);
     const dim3 grid((unsigned)(per * nmt));
     LmSample smp{p, rng, step, static_cast<LmPart *>(workspace), (int)(per * 8)};
     const auto *X = static_cast<const uint16_t *>(x);
     const auto *W = static_cast<const uint16_t *>(w);
     const auto *NWt = static_cast<const uint16_t *>(norm_w);
-    const int rc = NWt ? launch_lm<true, true>(grid, (size_t)L.total, s, X, W, (int)M, (int)V, (int)K, NWt, eps, ss_in,
-                                                nullptr, 0, smp)
-                       : launch_lm<false, true>(grid, (size_t)L.total, s, X, W, (int)M, (int)V, (int)K, nullptr, eps,
-                                                 nullptr, nullptr, 0, smp);
+    const int rc = nm == 1   ? launch_lm<1, true>(grid, (size_t)L.total, s, X, W, (int)M, (int)V, (int)K, NWt, eps,
+                                                   ss_in, nullptr, 0, smp)
+                   : nm == 2 ? launch_lm<2, true>(grid, (size_t)L.total, s, X, W, (int)M, (int)V, (int)K, nullptr, eps,
+                                                   ss_in, nullptr, 0, smp)
+                             : launch_lm<0, true>(grid, (size_t)L.total, s, X, W, (int)M, (int)V, (int)K, nullptr, eps,
+                                                   nullptr, nullptr, 0, smp);
     if (rc != SWH_OK) return rc;
     lm_sample_finalize_kernel<<<dim3((unsigned)M), 256, 0, s>>>(smp.part, smp.pstride, p, step, finished, out_tokens,
                                                                out_ld, cur_tokens, (int)V);

@@ -67,6 +67,18 @@ class DecodeEngine:
         ks = (c.hidden_size, c.intermediate_size, c.q_dim)
         self.fused = (fused if fused is not None else os.environ.get("SWH_DECODE_FUSED", "1") != "0") and \
             all(k % 128 == 0 for k in ks) and c.hidden_size % 16 == 0 and c.qkv_dim % 16 == 0
+        # Folded RMSNorm weights: W' = bf16(W * w_norm) for the normed projections,
+        # so the decode GEMMs scale rows by rstd in the epilogue instead of
+        # normalising X in every workgroup (rounding differs from transformers'
+        # bf16(w * bf16(x * rstd)) at the last bf16 bit; SWH_DECODE_FOLD=0 keeps it)
+        self.fold = self.fused and os.environ.get("SWH_DECODE_FOLD", "1") != "0"
+        self.fw = {}
+        if self.fold:
+            L = c.num_hidden_layers
+            for i in range(L):
+                self.fw[f"l{i}.qkv_w"] = torch.empty_like(model.p[f"l{i}.qkv_w"])
+                self.fw[f"l{i}.gu_w"] = torch.empty_like(model.p[f"l{i}.gu_w"])
+            self.fw["lm"] = torch.empty_like(model.lm_weight())
         self.graph = None
         self._graph_params = None
         self.params = ops.make_sample_params()
@@ -91,6 +103,26 @@ class DecodeEngine:
         return (self.fused and not self.want_logp and os.environ.get("SWH_FUSED_SAMPLE", "1") != "0" and
                 nn_ops.lm_head_sample_supported(self.params, self.cfg.vocab_size, self.cfg.hidden_size))
 
+    @torch.no_grad()
+    def refresh_folded(self):
+        """Re-derive the folded weights from the current parameters (once per
+        generate(): the optimizer changes both W and the norm weights)."""
+        if not self.fold:
+            return
+        p = self.model.p
+        for i in range(self.cfg.num_hidden_layers):
+            torch.mul(p[f"l{i}.qkv_w"], p[f"l{i}.ln_in"], out=self.fw[f"l{i}.qkv_w"])
+            torch.mul(p[f"l{i}.gu_w"], p[f"l{i}.ln_post"], out=self.fw[f"l{i}.gu_w"])
+        torch.mul(self.model.lm_weight(), p["norm"], out=self.fw["lm"])
+
+    def _normed(self, name: str, norm: str):
+        """(weight, norm_w) of a normed projection: folded weight + row scale,
+        or the raw weight + in-kernel RMSNorm."""
+        if self.fold:
+            return self.fw[name], None
+        w = self.model.lm_weight() if name == "lm" else self.model.p[name]
+        return w, self.model.p[norm]
+
     def _step_fused(self):
         c, m = self.cfg, self.model
         p = m.p
@@ -98,20 +130,21 @@ class DecodeEngine:
         ss = self.ss  # every producer of s writes its RMSNorm partial sums, every normed GEMM reads them
         nn_ops.embed_gather(p["embed"], self.cur, self.s, ss_out=ss)
         for i in range(c.num_hidden_layers):
-            nn_ops.decode_gemm(self.s, p[f"l{i}.qkv_w"], norm_w=p[f"l{i}.ln_in"], eps=eps,
-                               bias=p.get(f"l{i}.qkv_b"), y=self.qkv, ss_in=ss)
+            w, nw = self._normed(f"l{i}.qkv_w", f"l{i}.ln_in")
+            nn_ops.decode_gemm(self.s, w, norm_w=nw, eps=eps, bias=p.get(f"l{i}.qkv_b"), y=self.qkv, ss_in=ss)
             nn_ops.attn_decode(self.qkv, self.kv[i, 0], self.kv[i, 1], self.cos, self.sin, self.plen, self.state,
                                c.num_attention_heads, c.num_key_value_heads, c.head_dim, c.head_dim ** -0.5,
                                out=self.att)
             nn_ops.decode_gemm(self.att, p[f"l{i}.o_w"], residual=self.s, ss_out=ss)
-            nn_ops.decode_gemm(self.s, p[f"l{i}.gu_w"], norm_w=p[f"l{i}.ln_post"], eps=eps, silu=True, y=self.act,
-                               ss_in=ss)
+            w, nw = self._normed(f"l{i}.gu_w", f"l{i}.ln_post")
+            nn_ops.decode_gemm(self.s, w, norm_w=nw, eps=eps, silu=True, y=self.act, ss_in=ss)
             nn_ops.decode_gemm(self.act, p[f"l{i}.down_w"], residual=self.s, ss_out=ss)
+        w, nw = self._normed("lm", "norm")
         if self._fused_sample():
-            nn_ops.lm_head_sample(self.s, m.lm_weight(), self.params, self.rng, self.state[0:1], self.finished,
-                                  self.out, self.cur, norm_w=p["norm"], eps=eps, ss_in=ss, workspace=self.sample_ws)
+            nn_ops.lm_head_sample(self.s, w, self.params, self.rng, self.state[0:1], self.finished,
+                                  self.out, self.cur, norm_w=nw, eps=eps, ss_in=ss, workspace=self.sample_ws)
         else:
-            nn_ops.decode_gemm(self.s, m.lm_weight(), norm_w=p["norm"], eps=eps, y=self.logits_buf, ss_in=ss)
+            nn_ops.decode_gemm(self.s, w, norm_w=nw, eps=eps, y=self.logits_buf, ss_in=ss)
 
     def _step_unfused(self):
         c, m = self.cfg, self.model
@@ -199,7 +232,8 @@ class DecodeEngine:
 
         ss = self.ss
         ops_ = {
-            "decode_gemm.qkv": (lambda: nn_ops.decode_gemm(self.s, p["l0.qkv_w"], norm_w=p["l0.ln_in"], eps=eps,
+            "decode_gemm.qkv": (lambda: nn_ops.decode_gemm(self.s, self._normed("l0.qkv_w", "l0.ln_in")[0],
+                                                           norm_w=self._normed("l0.qkv_w", "l0.ln_in")[1], eps=eps,
                                                            bias=p.get("l0.qkv_b"), y=self.qkv, ss_in=ss),
                                 gemm_bytes(c.qkv_dim, H), L),
             "attn_decode": (lambda: nn_ops.attn_decode(self.qkv, self.kv[0, 0], self.kv[0, 1], self.cos, self.sin,
@@ -209,12 +243,14 @@ class DecodeEngine:
                             att_bytes, L),
             "decode_gemm.o": (lambda: nn_ops.decode_gemm(self.att, p["l0.o_w"], residual=self.s, ss_out=ss),
                               gemm_bytes(H, c.q_dim), L),
-            "decode_gemm.gate_up": (lambda: nn_ops.decode_gemm(self.s, p["l0.gu_w"], norm_w=p["l0.ln_post"], eps=eps,
-                                                               silu=True, y=self.act, ss_in=ss),
+            "decode_gemm.gate_up": (lambda: nn_ops.decode_gemm(self.s, self._normed("l0.gu_w", "l0.ln_post")[0],
+                                                               norm_w=self._normed("l0.gu_w", "l0.ln_post")[1],
+                                                               eps=eps, silu=True, y=self.act, ss_in=ss),
                                     gemm_bytes(I, H, silu=True), L),
             "decode_gemm.down": (lambda: nn_ops.decode_gemm(self.act, p["l0.down_w"], residual=self.s, ss_out=ss),
                                  gemm_bytes(H, I), L),
-            "decode_gemm.lm_head": (lambda: nn_ops.decode_gemm(self.s, m.lm_weight(), norm_w=p["norm"], eps=eps,
+            "decode_gemm.lm_head": (lambda: nn_ops.decode_gemm(self.s, self._normed("lm", "norm")[0],
+                                                               norm_w=self._normed("lm", "norm")[1], eps=eps,
                                                                y=self.logits_buf, ss_in=ss),
                                     c.vocab_size * H * bf + B * c.vocab_size * bf, 1),
             "sample_step": (self._sample, B * c.vocab_size * bf, 1),
@@ -222,9 +258,10 @@ class DecodeEngine:
         if self._fused_sample():  # what the decode graph runs instead of lm head + sample_step
             del ops_["decode_gemm.lm_head"], ops_["sample_step"]
             ops_["lm_head_sample"] = (
-                lambda: nn_ops.lm_head_sample(self.s, m.lm_weight(), self.params, self.rng, self.state[0:1],
-                                              self.finished, self.out, self.cur, norm_w=p["norm"], eps=eps,
-                                              ss_in=ss, workspace=self.sample_ws),
+                lambda: nn_ops.lm_head_sample(self.s, self._normed("lm", "norm")[0], self.params, self.rng,
+                                              self.state[0:1], self.finished, self.out, self.cur,
+                                              norm_w=self._normed("lm", "norm")[1], eps=eps, ss_in=ss,
+                                              workspace=self.sample_ws),
                 c.vocab_size * H * bf, 1)
         nn_ops.embed_gather(p["embed"], self.cur, self.s, ss_out=ss)
         out = {}
@@ -297,6 +334,7 @@ class DecodeEngine:
         self.rng[0], self.rng[1] = int(seed) & ((1 << 63) - 1), int(offset)
         if repetition_penalty != 1.0:
             ops.seen_init(prompt_ids.to(torch.int64), prompt_mask, self.cfg.vocab_size, self.seen)
+        self.refresh_folded()
         if self.use_graph:
             self._ensure_graph()
         self.state[0], self.state[1] = 0, P

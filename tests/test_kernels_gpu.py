@@ -697,8 +697,8 @@ def test_decode_gemm_persistent_epilogues(ops, dev):
 
 @pytest.mark.parametrize("kw", [dict(), dict(temperature=0.7), dict(greedy=True), dict(min_new_tokens=5),
                                 dict(temperature=1.3, min_new_tokens=1)])
-@pytest.mark.parametrize("M,V", [(64, 151936), (70, 32768)])
-def test_lm_head_sample_equals_logits_then_sampler(ops, dev, kw, M, V):
+@pytest.mark.parametrize("M,V,fold", [(64, 151936, False), (70, 32768, False), (64, 151936, True)])
+def test_lm_head_sample_equals_logits_then_sampler(ops, dev, kw, M, V, fold):
     """The fused lm head + sampler draws, bit for bit, the token swh_sample_step
     draws from the materialised bf16 logits (same rng, same step), including
     EOS suppression, pad-after-EOS and the finished flags."""
@@ -716,6 +716,9 @@ def test_lm_head_sample_equals_logits_then_sampler(ops, dev, kw, M, V):
     rng = torch.tensor([123, 45], dtype=torch.int64, device=dev)
     stp = torch.tensor([step], dtype=torch.int32, device=dev)
     fin0 = (torch.arange(M) % 7 == 0).int().to(dev)
+    if fold:  # folded norm weight, rstd row scale in the epilogue
+        w = w * nw
+        nw = None
     logits = nn_ops.decode_gemm(x, w, norm_w=nw, eps=1e-6, ss_in=ss)
     out_a = torch.full((M, 4), -1, dtype=torch.int64, device=dev)
     cur_a = torch.empty(M, dtype=torch.int64, device=dev)
@@ -745,3 +748,22 @@ def test_lm_head_sample_refuses_filtered(ops, dev):
         assert not nn_ops.lm_head_sample_supported(p, 1024, 896)
         with pytest.raises(ValueError):
             nn_ops.lm_head_sample(x, w, p, rng, stp, fin, out)
+
+
+@pytest.mark.parametrize("M,N,K,silu", [(64, 1152, 896, False), (64, 4864, 896, True), (20, 151936, 896, False)])
+def test_decode_gemm_folded_norm(ops, dev, M, N, K, silu):
+    """ss_in without norm_w: y = rstd * (x W'^T), W' = bf16(W * w) — the decode
+    engine's folded RMSNorm; equals the reference within bf16 rounding."""
+    from swh_trl_amd import nn_ops
+    g = _gen(37)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
+    wrows = 2 * N if silu else N
+    w = (torch.randn(wrows, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(dev)
+    nw = (1 + 0.1 * torch.randn(K, generator=g)).to(torch.bfloat16).to(dev)
+    ss = _chunk_ss(x)
+    y = nn_ops.decode_gemm(x, w * nw, ss_in=ss, eps=1e-6, silu=silu)
+    ref = _ref_norm(x, nw, 1e-6).float() @ w.float().t()
+    if silu:
+        gu = ref.to(torch.bfloat16)
+        ref = (torch.nn.functional.silu(gu[:, :N]) * gu[:, N:]).float()
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=3e-2)  # rounding of the fold, then SiLU's
