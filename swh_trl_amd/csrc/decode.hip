@@ -747,18 +747,24 @@ __global__ __launch_bounds__(256) void lm_sample_finalize_kernel(const LmPart *_
 }
 
 // ---------------------------------------------------------------------------
-// Attention decode (GQA) on MFMA: one workgroup (4 waves) per (kv head,
-// sequence).  The GQ query heads of the kv head are the 16 rows (zero-padded)
-// of both products: S = Q K^T on v_mfma_f32_16x16x32_bf16 with the cached K
-// rows loaded straight into B fragments; online softmax in the C layout (the
-// 16 keys of a block sit in 16 lanes); P V on v_mfma_f32_16x16x16_bf16 with P
-// and the V block transposed through a per-wave LDS tile.  Waves take
-// interleaved 16-key blocks and issue every K/V load of a round before the
-// RoPE prologue, so the KV stream is one round trip per 384 (D 64) keys.
+// Attention decode (GQA) on MFMA, swapped orientation: one workgroup (8 waves)
+// per (kv head, sequence).  S^T = K Q^T on v_mfma_f32_16x16x32_bf16 (A = 16
+// cached keys straight from HBM, B = the GQ <= 16 query heads, zero-padded),
+// so each lane holds ONE head (lane & 15) and four keys: the softmax max / sum
+// reduce over registers and two lane groups only, and P^T, packed to bf16
+// pairwise, is the B operand of O^T = V^T P^T as it stands (no LDS round
+// trip).  V^T comes from the wave's V tile in LDS through ds_read_b64_tr_b16
+// (4 keys x 1 dim per lane).  Waves take interleaved 16-key blocks; every K/V
+// load of a round is issued before the RoPE prologue.
 // ---------------------------------------------------------------------------
 typedef short bf16x4s __attribute__((ext_vector_type(4)));
-constexpr int kAttnThreads = 256;
+constexpr int kAttnThreads = 512;
 constexpr int kAttnWaves = kAttnThreads / 64;
+
+__device__ __forceinline__ bf16x4s lds_read_tr16(const uint16_t *p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) bf16x4s *)(const_cast<uint16_t *>(p)));
+}
 
 template <int D, int GQ>
 __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
@@ -766,16 +772,16 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
     const float *__restrict__ rcos, const float *__restrict__ rsin, const int32_t *__restrict__ plen,
     const int32_t *__restrict__ state, int Hq, int Hkv, int Tmax, float scale, uint16_t *__restrict__ out) {
     static_assert(GQ <= 16, "a kv head serves at most 16 query heads");
-    constexpr int DC = D / 32;                   // 32-dim chunks: k-steps of Q K^T
-    constexpr int DB = D / 16;                   // 16-dim blocks of the output
-    constexpr int JB = (D == 64) ? 6 : 3;        // key blocks per wave per round
-    constexpr int KPR = JB * 16 * kAttnWaves;    // keys per round
+    constexpr int DC = D / 32;                 // 32-dim chunks: k-steps of K Q^T
+    constexpr int DB = D / 16;                 // 16-dim blocks of O^T
+    constexpr int JB = (D == 64) ? 4 : 2;      // key blocks per wave per round (pairs for P V)
+    constexpr int KPR = JB * 16 * kAttnWaves;  // keys per round
     constexpr int HD = D / 2;
+    constexpr int VS = D + (D == 64 ? 8 : 16);  // V tile row stride (elements): conflict-free transposed reads
     __shared__ __attribute__((aligned(16))) uint16_t q_s[16 * D];
     __shared__ __attribute__((aligned(16))) uint16_t kn_s[D];
     __shared__ __attribute__((aligned(16))) uint16_t vn_s[D];
-    __shared__ __attribute__((aligned(16))) uint16_t pt_s[kAttnWaves][16 * 16];
-    __shared__ __attribute__((aligned(16))) uint16_t vt_s[kAttnWaves][16 * D];
+    __shared__ __attribute__((aligned(16))) uint16_t vt_s[kAttnWaves][32 * VS];
     __shared__ float red_s[kAttnWaves][16][D + 2];
 
     const int kvh = blockIdx.x;
@@ -798,13 +804,17 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
     const uint16_t *kb = kc + cbase + (int64_t)start * D + g * 8;
     const uint16_t *vb = vc + cbase + (int64_t)start * D + g * 8;
 
+    // lane (g, c16) loads key c16 of each block, dims 32 c + 8 g: the A fragment of K Q^T
     u32x4 kr[JB][DC], vr[JB][DC];  // vector types: uint4 structs defeat SROA under selects
 #define SWH_ATTN_ISSUE(base_)                                                                  \
     _Pragma("unroll") for (int i = 0; i < JB; ++i) {                                           \
-        const int kk = max(min((base_) + (wid + i * kAttnWaves) * 16 + c16, n - 2), 0);        \
-        _Pragma("unroll") for (int c = 0; c < DC; ++c) {                                       \
-            kr[i][c] = *reinterpret_cast<const u32x4 *>(kb + (int64_t)kk * D + c * 32);        \
-            vr[i][c] = *reinterpret_cast<const u32x4 *>(vb + (int64_t)kk * D + c * 32);        \
+        const int k0_ = (base_) + (wid + i * kAttnWaves) * 16;                                 \
+        if (k0_ < n) {                                                                         \
+            const int kk = max(min(k0_ + c16, n - 2), 0);                                      \
+            _Pragma("unroll") for (int c = 0; c < DC; ++c) {                                   \
+                kr[i][c] = *reinterpret_cast<const u32x4 *>(kb + (int64_t)kk * D + c * 32);    \
+                vr[i][c] = *reinterpret_cast<const u32x4 *>(vb + (int64_t)kk * D + c * 32);    \
+            }                                                                                  \
         }                                                                                      \
     }
     SWH_ATTN_ISSUE(0)  // the KV stream is in flight during RoPE
@@ -833,118 +843,121 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
         vc[cbase + (int64_t)slot_new * D + d] = vn_s[d];
     }
 
-    u32x4 qa[DC];
+    // B operand of K Q^T: lane holds head c16, dims 32 c + 8 g
+    u32x4 qb[DC];
 #pragma unroll
-    for (int c = 0; c < DC; ++c) qa[c] = *reinterpret_cast<const u32x4 *>(q_s + c16 * D + c * 32 + g * 8);
-    float m[4], l[4];
-    f32x4 o[DB];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        m[r] = kNegInf;
-        l[r] = 0.f;
-    }
+    for (int c = 0; c < DC; ++c) qb[c] = *reinterpret_cast<const u32x4 *>(q_s + c16 * D + c * 32 + g * 8);
+    float m = kNegInf, l = 0.f;  // of head c16
+    f32x4 o[DB];                 // O^T: dims 16 db + 4 g + r, head c16
 #pragma unroll
     for (int d = 0; d < DB; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-    uint16_t *pt = pt_s[wid];
     uint16_t *vt = vt_s[wid];
 
     for (int base = 0; base < n; base += KPR) {
         if (base) {
             SWH_ATTN_ISSUE(base)
         }
-        f32x4 sc[JB];
+        f32x4 sc[JB];  // S^T: keys k0 + 4 g + r, head c16
+        float mx = m;
 #pragma unroll
         for (int i = 0; i < JB; ++i) {
             const int k0 = base + (wid + i * kAttnWaves) * 16;
-            const bool fresh = (k0 + c16 == n - 1);  // the new key/value: from LDS, not the cache
-#pragma unroll
-            for (int c = 0; c < DC; ++c) {
-                const u32x4 kn = *reinterpret_cast<const u32x4 *>(kn_s + c * 32 + g * 8);
-                const u32x4 vn = *reinterpret_cast<const u32x4 *>(vn_s + c * 32 + g * 8);
-                kr[i][c] = fresh ? kn : kr[i][c];
-                vr[i][c] = fresh ? vn : vr[i][c];
-            }
-            sc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int c = 0; c < DC; ++c)
-                sc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, qa[c]),
-                                                                __builtin_bit_cast(bf16x8, kr[i][c]), sc[i], 0, 0, 0);
-            const bool live = k0 + c16 < n;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) sc[i][r] = live ? sc[i][r] * scale : kNegInf;
-        }
-        // online softmax: rows = heads 4g+r, a block's 16 keys across the 16 lanes of the group
-        float mx[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            mx[r] = m[r];
-#pragma unroll
-            for (int i = 0; i < JB; ++i) mx[r] = fmaxf(mx[r], sc[i][r]);
-#pragma unroll
-            for (int off = 1; off < 16; off <<= 1) mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], off, kWave));
-            const float corr = (mx[r] == kNegInf) ? 1.f : expf(m[r] - mx[r]);
-            l[r] *= corr;
-#pragma unroll
-            for (int d = 0; d < DB; ++d) o[d][r] *= corr;
-            m[r] = mx[r];
-#pragma unroll
-            for (int i = 0; i < JB; ++i) {
-                const float pj = (mx[r] == kNegInf) ? 0.f : expf(sc[i][r] - mx[r]);
-                sc[i][r] = pj;
-                l[r] += pj;
-            }
-        }
-        // P V, one 16-key block at a time through the wave's LDS tiles
-#pragma unroll
-        for (int i = 0; i < JB; ++i) {
-            const int k0 = base + (wid + i * kAttnWaves) * 16;
+            sc[i] = f32x4{kNegInf, kNegInf, kNegInf, kNegInf};
             if (k0 < n) {  // wave-uniform
+                const bool fresh = (k0 + c16 == n - 1);  // the new key/value: from LDS, not the cache
 #pragma unroll
-                for (int r = 0; r < 4; ++r) pt[(4 * g + r) * 16 + c16] = f32_to_bf16_bits(sc[i][r]);
+                for (int c = 0; c < DC; ++c) {
+                    const u32x4 kn = *reinterpret_cast<const u32x4 *>(kn_s + c * 32 + g * 8);
+                    const u32x4 vn = *reinterpret_cast<const u32x4 *>(vn_s + c * 32 + g * 8);
+                    kr[i][c] = fresh ? kn : kr[i][c];
+                    vr[i][c] = fresh ? vn : vr[i][c];
+                }
+                f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int c = 0; c < DC; ++c) *reinterpret_cast<u32x4 *>(vt + c16 * D + c * 32 + g * 8) = vr[i][c];
-                const bf16x4s pa =
-                    __builtin_bit_cast(bf16x4s, *reinterpret_cast<const uint2 *>(pt + c16 * 16 + 4 * g));
+                for (int c = 0; c < DC; ++c)
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kr[i][c]),
+                                                                  __builtin_bit_cast(bf16x8, qb[c]), acc, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    sc[i][r] = (k0 + 4 * g + r < n) ? acc[r] * scale : kNegInf;
+                    mx = fmaxf(mx, sc[i][r]);
+                }
+            }
+        }
+        // online softmax of head c16: its keys sit in 4 registers x JB blocks x the 4 lane groups
+        mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+        const float corr = (mx == kNegInf) ? 1.f : expf(m - mx);
+        l *= corr;
+#pragma unroll
+        for (int d = 0; d < DB; ++d) o[d] *= corr;
+        m = mx;
+        // P V: blocks in pairs -> 32 keys per MFMA; P^T (bf16 pairs) is the B operand as it stands
+#pragma unroll
+        for (int i = 0; i < JB; i += 2) {
+            const int k0 = base + (wid + i * kAttnWaves) * 16;
+            const int k1 = base + (wid + (i + 1) * kAttnWaves) * 16;
+            if (k0 < n) {  // wave-uniform
+                float pj[8];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    pj[r] = (mx == kNegInf) ? 0.f : expf(sc[i][r] - mx);
+                    pj[4 + r] = (mx == kNegInf) ? 0.f : expf(sc[i + 1][r] - mx);
+                    l += pj[r] + pj[4 + r];
+                }
+                // the pair's V rows into the wave's tile (rows 0-15: block i, 16-31: block i+1; zeros past n)
+#pragma unroll
+                for (int c = 0; c < DC; ++c) {
+                    *reinterpret_cast<u32x4 *>(vt + c16 * VS + c * 32 + g * 8) = vr[i][c];
+                    *reinterpret_cast<u32x4 *>(vt + (16 + c16) * VS + c * 32 + g * 8) =
+                        (k1 < n) ? vr[i + 1][c] : u32x4{0u, 0u, 0u, 0u};
+                }
+                uint32_t pb[4];
+#pragma unroll
+                for (int h = 0; h < 4; ++h)
+                    pb[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{pj[2 * h], pj[2 * h + 1]}, bf16x2));
+                const bf16x8 pbf = __builtin_bit_cast(bf16x8, u32x4{pb[0], pb[1], pb[2], pb[3]});
+                // V^T fragment: lane (g, c16) <- dims 16 db + c16 of keys {4 g .. 4 g + 3} and {16 + 4 g ..}
+                const int q = c16 >> 2, pq = c16 & 3;
 #pragma unroll
                 for (int d = 0; d < DB; ++d) {
-                    bf16x4s vbv;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) vbv[j] = (short)vt[(4 * g + j) * D + d * 16 + c16];
-                    o[d] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(pa, vbv, o[d], 0, 0, 0);
+                    const bf16x4s lo = lds_read_tr16(vt + (4 * g + q) * VS + d * 16 + 4 * pq);
+                    const bf16x4s hi = lds_read_tr16(vt + (16 + 4 * g + q) * VS + d * 16 + 4 * pq);
+                    const bf16x8 va = __builtin_bit_cast(
+                        bf16x8, u32x4{__builtin_bit_cast(uint2, lo).x, __builtin_bit_cast(uint2, lo).y,
+                                      __builtin_bit_cast(uint2, hi).x, __builtin_bit_cast(uint2, hi).y});
+                    o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pbf, o[d], 0, 0, 0);
                 }
             }
         }
     }
-    // row sums across the 16 key lanes, then the waves merge through LDS
+    // row sums across the 4 lane groups, then the waves merge through LDS
+    l += __shfl_xor(l, 16, kWave);
+    l += __shfl_xor(l, 32, kWave);
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int d = 0; d < DB; ++d)
 #pragma unroll
-        for (int off = 1; off < 16; off <<= 1) l[r] += __shfl_xor(l[r], off, kWave);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-#pragma unroll
-        for (int d = 0; d < DB; ++d) red_s[wid][4 * g + r][d * 16 + c16] = o[d][r];
-        if (c16 == 0) {
-            red_s[wid][4 * g + r][D] = m[r];
-            red_s[wid][4 * g + r][D + 1] = l[r];
-        }
+        for (int r = 0; r < 4; ++r) red_s[wid][c16][d * 16 + 4 * g + r] = o[d][r];
+    if (g == 0) {
+        red_s[wid][c16][D] = m;
+        red_s[wid][c16][D + 1] = l;
     }
     __syncthreads();
     for (int idx = tid; idx < GQ * D; idx += kAttnThreads) {
         const int h = idx / D, d = idx - h * D;
         float mxw = kNegInf;
 #pragma unroll
-        for (int q = 0; q < kAttnWaves; ++q) mxw = fmaxf(mxw, red_s[q][h][D]);
-        float L = 0.f, A = 0.f;
+        for (int w2 = 0; w2 < kAttnWaves; ++w2) mxw = fmaxf(mxw, red_s[w2][h][D]);
+        float Ls = 0.f, A = 0.f;
 #pragma unroll
-        for (int q = 0; q < kAttnWaves; ++q) {
-            const float mq = red_s[q][h][D];
+        for (int w2 = 0; w2 < kAttnWaves; ++w2) {
+            const float mq = red_s[w2][h][D];
             if (mq == kNegInf) continue;
             const float cq = expf(mq - mxw);
-            L = fmaf(red_s[q][h][D + 1], cq, L);
-            A = fmaf(red_s[q][h][d], cq, A);
+            Ls = fmaf(red_s[w2][h][D + 1], cq, Ls);
+            A = fmaf(red_s[w2][h][d], cq, A);
         }
-        ob[idx] = f32_to_bf16_bits(A / L);
+        ob[idx] = f32_to_bf16_bits(A / Ls);
     }
 #undef SWH_ATTN_ISSUE
 }
