@@ -109,7 +109,7 @@ __host__ __device__ inline GemmLds gemm_lds(int cb, int mr, int nw, int krmax, i
 // the way in — then covers one column block, or several when the grid is
 // smaller than the column blocks (the lm head loops, prefetching the next
 // block's weights before merging the current one).  The NW waves split the
-// slice's k-steps; each issues all weight loads of a round of kU k-steps at
+// slice's k-steps; each issues all weight loads of a round of U k-steps at
 // once (fragment order) and takes its A fragments from the LDS image.  Waves
 // merge through a fixed-order LDS tree.  Tiles are numbered so the M tiles of
 // one column block land on one XCD (dispatch is round-robin over the 8 XCDs):
@@ -117,7 +117,6 @@ __host__ __device__ inline GemmLds gemm_lds(int cb, int mr, int nw, int krmax, i
 // XCD's L2.  S > 1: write-through (sc1) fp32 slabs, an agent-scope ticket, the
 // last arriver sums the S slabs in fixed order (deterministic, placement-
 // independent — MI355X_MICROARCH.md §Workgroup dispatch) and runs the epilogue.
-constexpr int kU = 4;    // k-steps whose loads are issued together
 
 template <int CB, int MS, int NM, int EPI, bool BIAS>
 __global__ __launch_bounds__(512) void decode_gemm_kernel(
@@ -126,6 +125,7 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
     const uint16_t *__restrict__ bias, uint16_t *__restrict__ res, float *__restrict__ ss_out,
     uint16_t *__restrict__ y, int ldy, float *__restrict__ slabs, int *__restrict__ counters, int persist) {
     constexpr int NB = 16 * CB, MR = 16 * MS, LDR = MR + 4;  // merge slots column-major: b128 parks
+    constexpr int kU = 4;                                     // k-steps whose loads are issued together
     constexpr int G8 = (EPI == EPI_SILU) ? CB : NB / 8;  // 8-column output groups per row
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, NT = blockDim.x, NW = NT >> 6;
@@ -159,7 +159,37 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
     const int rl = lane & 15, kq = (lane >> 4) * 8;
     SWH_GEMM_TRACE(0);
 
-    // ---- (a) RMSNorm partial sums and the norm-weight slice (L2), first in the queue
+    // ---- (a) this wave's weights for the first column block (HBM, the long pole: first in the queue)
+    const int ksw0 = kb0 + (kb1 - kb0) * wid / NW, ksw1 = kb0 + (kb1 - kb0) * (wid + 1) / NW;
+    const uint16_t *wrow[CB];
+    auto set_rows = [&](int n0) {
+#pragma unroll
+        for (int j = 0; j < CB; ++j) {
+            int n;
+            if constexpr (EPI == EPI_SILU) {
+                const int c = j * 8 + (rl & 7);
+                n = (rl < 8) ? n0 + c : N + n0 + c;  // gate rows, then the matching up rows
+            } else {
+                n = n0 + j * 16 + rl;
+            }
+            wrow[j] = w + (int64_t)n * K + kq;
+        }
+    };
+    uint4 bv[kU][CB];
+    auto issue = [&](int ks) {  // only this wave's k-steps: no duplicate loads
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            if (ks + u < ksw1) {
+#pragma unroll
+                for (int j = 0; j < CB; ++j)  // plain loads: the line's other half is the next k-step's load
+                    bv[u][j] = *reinterpret_cast<const uint4 *>(wrow[j] + (ks + u) * 32);
+            }
+        }
+    };
+    auto col0 = [&](int cbk) { return cbk * (EPI == EPI_SILU ? NB / 2 : NB); };
+    set_rows(col0(cb_first));
+    issue(ksw0);
+    // ---- (b) RMSNorm partial sums and the norm-weight slice (L2)
     const int nc = K / 64;
     const bool use_ss = NM && ss_in && MR * nc <= 4 * NT;
     float4 ssv[4];
@@ -179,8 +209,8 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
                 nwv[q] = reinterpret_cast<const uint4 *>(norm_w + k0)[min(tid + q * NT, Kr / 8 - 1)];
         }
     }
-    // ---- (b) epilogue operands of a single-block workgroup (L2): <= 2 per thread in every geometry
-    const int ncol0 = cb_first * (EPI == EPI_SILU ? NB / 2 : NB);
+    // epilogue operands of a single-block workgroup (L2): <= 2 per thread in every geometry
+    const int ncol0 = col0(cb_first);
     uint4 pre_res[2], pre_bias[2];
     if constexpr (EPI == EPI_RESIDUAL || BIAS) {
         if (!persist) {
@@ -194,7 +224,7 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
             }
         }
     }
-    // ---- X slice -> LDS image by LDS-DMA (no registers): each wave whole rows
+    // ---- (c) X slice -> LDS image by LDS-DMA (no registers): each wave whole rows
     // wid, wid+NW, ...; one instruction = 64 lanes x 16 B = 1 KB of a row
     const int ppr = Kr / 8, jpl = (ppr + 63) >> 6;  // 16-B pieces per row, instructions per row
     for (int r = wid; r < MR; r += NW) {
@@ -207,38 +237,9 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
                                                  16, 0, 0);
         }
     }
-    asm volatile("" ::: "memory");  // the weight loads below stay younger than every DMA
-    // ---- (c) this wave's weights for the first column block (HBM)
-    const int ksw0 = kb0 + (kb1 - kb0) * wid / NW, ksw1 = kb0 + (kb1 - kb0) * (wid + 1) / NW;
-    const uint16_t *wrow[CB];
-    auto set_rows = [&](int n0) {
-#pragma unroll
-        for (int j = 0; j < CB; ++j) {
-            int n;
-            if constexpr (EPI == EPI_SILU) {
-                const int c = j * 8 + (rl & 7);
-                n = (rl < 8) ? n0 + c : N + n0 + c;  // gate rows, then the matching up rows
-            } else {
-                n = n0 + j * 16 + rl;
-            }
-            wrow[j] = w + (int64_t)n * K + kq;
-        }
-    };
-    uint4 bv[kU][CB];
-    auto issue = [&](int ks) {
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const int kk = max(min(ks + u, ksw1 - 1), 0) * 32;
-#pragma unroll
-            for (int j = 0; j < CB; ++j) {
-                const uint4 *pw = reinterpret_cast<const uint4 *>(wrow[j] + kk);
-                bv[u][j] = *pw;  // plain: the line's other half is the next k-step's load
-            }
-        }
-    };
-    auto col0 = [&](int cbk) { return cbk * (EPI == EPI_SILU ? NB / 2 : NB); };
-    set_rows(col0(cb_first));
-    issue(ksw0);  // exactly kU * CB loads: the DMA wait below counts on it
+    // everything this workgroup streams is in flight; the image is usable once all of it landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
     SWH_GEMM_TRACE(1);
 
     // ---- (d) row statistic and norm weights into LDS
@@ -285,9 +286,7 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
     }
     SWH_GEMM_TRACE(2);
 
-    // ---- (e) X image landed (all but the kU * CB weight loads retired), normalised in place
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kU * CB) : "memory");
-    lds_barrier();
+    // ---- (e) the X image normalised in place
     if constexpr (NM == 1) {
         int r = tid / ppr, c = tid - r * ppr;
         const int rstep = NT / ppr, cstep = NT - rstep * ppr;
@@ -459,12 +458,14 @@ __global__ __launch_bounds__(512) void decode_gemm_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// lm head (column blocks >> CUs, K <= 1024): persistent workgroups, one per CU
-// (per M tile); the X image [64 x K] is staged and normalised once, then
-// every wave owns whole 16-column tiles over the full K — all K/32 weight
-// loads of a tile in flight at once, the next tile's issued as soon as the
-// MFMAs have consumed the current one, no cross-wave merge.  8 independent
-// waves per CU keep ~200 KB of weights in flight: HBM-bound.
+// Tile kernel (many 16-column tiles, K <= 1024: the lm head, gate/up):
+// persistent workgroups, one per CU (per M tile); the X image [64 x K] is
+// staged (and normalised) once, then every wave owns whole 16-column tiles
+// over the full K — all K/32 weight loads of a tile in flight at once, the
+// next tile's issued as soon as the MFMAs have consumed the current one, no
+// cross-wave merge.  Tile t goes to workgroup t % wgs, so every CU gets work
+// even when tiles are few.  Epilogues: plain (+ bias), SiLU gate (a tile is
+// 8 gate + 8 up columns), or the fused sampler.
 // ---------------------------------------------------------------------------
 constexpr int kLmMaxKS = 32;  // K <= 1024
 
@@ -484,28 +485,34 @@ struct LmSample {
     int pstride;
 };
 
-template <int NM, bool SAMPLE>
+template <int NM, int EPI, bool BIAS, bool SAMPLE>
 __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict__ x, const uint16_t *__restrict__ w,
                                                       int M, int N, int K, const uint16_t *__restrict__ norm_w,
                                                       float eps, const float *__restrict__ ss_in,
-                                                      uint16_t *__restrict__ y, int ldy, LmSample smp) {
+                                                      const uint16_t *__restrict__ bias, uint16_t *__restrict__ y,
+                                                      int ldy, LmSample smp) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, NT = blockDim.x, NW = NT >> 6;
     const int rl = lane & 15, kq = (lane >> 4) * 8, g = lane >> 4;
     const int nmt = (M + 63) / 64, mt = blockIdx.x % nmt, m0 = mt * 64;
     const int wgs = gridDim.x / nmt, wg = blockIdx.x / nmt;
-    const int ntile = N / 16, KS = K / 32, RS = K * 2 + 16;
+    const int ntile = (EPI == EPI_SILU) ? N / 8 : N / 16, KS = K / 32, RS = K * 2 + 16;
     const GemmLds L = gemm_lds(1, 64, NW, K, K, NM, false);
     float *rstd_s = reinterpret_cast<float *>(lds);
     float *nw_s = reinterpret_cast<float *>(lds + L.nw_off);
     float *ssp = reinterpret_cast<float *>(lds + L.ss_off);
     unsigned char *xs = lds + L.body_off;
     const int tstep = wgs * NW;
-    int t = wg * NW + wid;
+    int t = wg + wgs * wid;  // tile t -> workgroup t % wgs
+    SWH_GEMM_TRACE(0);
 
     uint4 bv[kLmMaxKS];
+    auto wrow_of = [&](int tile) -> int64_t {
+        if constexpr (EPI == EPI_SILU) return (rl < 8) ? tile * 8 + rl : N + tile * 8 + rl - 8;  // gate, then up
+        return (int64_t)tile * 16 + rl;
+    };
     auto issue = [&](int tile) {
-        const uint16_t *wr = w + (int64_t)(tile * 16 + rl) * K + kq;
+        const uint16_t *wr = w + wrow_of(tile) * K + kq;
 #pragma unroll
         for (int ks = 0; ks < kLmMaxKS; ++ks)
             if (ks < KS) bv[ks] = *reinterpret_cast<const uint4 *>(wr + ks * 32);
@@ -558,8 +565,10 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
                 reinterpret_cast<float4 *>(nw_s)[2 * (tid + q * NT) + 1] = float4{f[4], f[5], f[6], f[7]};
             }
     }
+    SWH_GEMM_TRACE(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // image (and this wave's first tile) landed
     lds_barrier();
+    SWH_GEMM_TRACE(2);
     if constexpr (NM != 0) {
         if (tid < 64) {
             float ssum = 0.f;
@@ -577,6 +586,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
         }
         lds_barrier();
     }
+    SWH_GEMM_TRACE(3);
     float rsr[4][4];  // folded RMSNorm (NM 2): the row scale of each accumulator row
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -636,6 +646,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
             }
         }
         if (t + tstep < ntile) issue(t + tstep);
+        SWH_GEMM_TRACE(4);
         if constexpr (SAMPLE) {
             const int col = t * 16 + rl;
             bool masked = false;
@@ -661,17 +672,32 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
                     }
                 }
             }
+        } else if constexpr (EPI == EPI_SILU) {
+            // lanes rl < 8 hold gate column t*8+rl, lanes rl+8 the matching up column
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float v = round_bf16(acc[i][e] * rsr[i][e]);
+                    const float u = __shfl_xor(v, 8, kWave);
+                    const int row = m0 + i * 16 + 4 * g + e;
+                    if (rl < 8 && row < M)
+                        y[(int64_t)row * ldy + t * 8 + rl] = f32_to_bf16_bits(round_bf16(v / (1.f + expf(-v))) * u);
+                }
         } else {
             // C layout: lane holds rows 16 i + 4 g + e of column rl
+            const float bz = BIAS ? bf16_bits_to_f32(bias[t * 16 + rl]) : 0.f;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int row = m0 + i * 16 + 4 * g + e;
-                    if (row < M) y[(int64_t)row * ldy + t * 16 + rl] = f32_to_bf16_bits(acc[i][e] * rsr[i][e]);
+                    if (row < M)
+                        y[(int64_t)row * ldy + t * 16 + rl] = f32_to_bf16_bits(acc[i][e] * rsr[i][e] + bz);
                 }
         }
     }
+    SWH_GEMM_TRACE(5);
     if constexpr (SAMPLE) {  // best over the 16 column lanes, one partial per (row, wave)
         const int pq = wg * NW + wid;
 #pragma unroll
@@ -693,6 +719,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
                 if (rl == 0 && row < M) smp.part[(int64_t)row * smp.pstride + pq] = LmPart{k, c};
             }
     }
+    SWH_GEMM_TRACE(6);
 }
 
 // Merge the per-wave partials of a row; EOS / pad bookkeeping as
@@ -1116,18 +1143,29 @@ int launch_gemm_ms(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const
     }
 }
 
-template <int NM, bool SAMPLE>
+template <int NM, int EPI, bool BIAS, bool SAMPLE>
 int launch_lm(dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W, int M, int N, int K,
-              const uint16_t *NWt, float eps, const float *ss_in, uint16_t *Y, int ldy, const LmSample &smp) {
+              const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs, uint16_t *Y, int ldy,
+              const LmSample &smp) {
     static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in once per kernel
     if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&lm_head_kernel<NM, SAMPLE>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&lm_head_kernel<NM, EPI, BIAS, SAMPLE>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
             return SWH_E_LAUNCH;
         attr = true;
     }
-    lm_head_kernel<NM, SAMPLE><<<grid, 512, lds, s>>>(X, W, M, N, K, NWt, eps, ss_in, Y, ldy, smp);
+    lm_head_kernel<NM, EPI, BIAS, SAMPLE><<<grid, 512, lds, s>>>(X, W, M, N, K, NWt, eps, ss_in, Bs, Y, ldy, smp);
     return launch_status();
+}
+
+// the tile kernel for plain / bias / SiLU epilogues
+template <int EPI, bool BIAS>
+int launch_tiles(int nm, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W, int M, int N,
+                 int K, const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs, uint16_t *Y, int ldy) {
+    const LmSample none{};
+    if (nm == 1) return launch_lm<1, EPI, BIAS, false>(grid, lds, s, X, W, M, N, K, NWt, eps, ss_in, Bs, Y, ldy, none);
+    if (nm == 2) return launch_lm<2, EPI, BIAS, false>(grid, lds, s, X, W, M, N, K, nullptr, eps, ss_in, Bs, Y, ldy, none);
+    return launch_lm<0, EPI, BIAS, false>(grid, lds, s, X, W, M, N, K, nullptr, eps, nullptr, Bs, Y, ldy, none);
 }
 
 }  // namespace
@@ -1183,28 +1221,28 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
         return SWH_E_ARG;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int64_t wcols = silu ? 2 * N : N;
-    if (!silu && !residual && !bias && N / 16 > 8 * (int64_t)cu_count() && K <= 32 * kLmMaxKS &&
-        !getenv("SWH_GEMM_CFG")) {  // the lm head: persistent, waves own tiles
-        const int64_t nmt = (M + 63) / 64;
-        const int nm = norm_w ? 1 : (ss_in ? 2 : 0);
-        const GemmLds L = gemm_lds(1, 64, 8, (int)K, (int)K, nm, false);
-        const int64_t per = cu_count() / nmt > 0 ? cu_count() / nmt : 1;
-        const dim3 grid((unsigned)(per * nmt));
-        auto *Y = static_cast<uint16_t *>(y);
-        const auto *X = static_cast<const uint16_t *>(x);
-        const auto *W = static_cast<const uint16_t *>(w);
-        const auto *NWt = static_cast<const uint16_t *>(norm_w);
-        const LmSample none{};
-        if (nm == 1)
-            return launch_lm<1, false>(grid, (size_t)L.total, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Y,
-                                       (int)ldy, none);
-        if (nm == 2)
-            return launch_lm<2, false>(grid, (size_t)L.total, s, X, W, (int)M, (int)N, (int)K, nullptr, eps, ss_in, Y,
-                                       (int)ldy, none);
-        return launch_lm<0, false>(grid, (size_t)L.total, s, X, W, (int)M, (int)N, (int)K, nullptr, eps, nullptr, Y,
-                                   (int)ldy, none);
-    }
     const int nm = norm_w ? 1 : (ss_in ? 2 : 0);
+    {  // many 16-column tiles and a K that fits the X image: the tile kernel (lm head, gate/up)
+        const int64_t ntile = silu ? N / 8 : N / 16;
+        const char *e = getenv("SWH_GEMM_CFG");
+        const bool force = e && e[0] == 't';  // tuning: "t" forces the tile kernel
+        if (!residual && K <= 32 * kLmMaxKS && (force || (!e && ntile >= 8 * (int64_t)cu_count()))) {
+            const int64_t nmt = (M + 63) / 64;
+            const GemmLds L = gemm_lds(1, 64, 8, (int)K, (int)K, nm, false);
+            int64_t per = cu_count() / nmt > 0 ? cu_count() / nmt : 1;
+            if (per > ntile) per = ntile;
+            const dim3 grid((unsigned)(per * nmt));
+            const auto *X = static_cast<const uint16_t *>(x);
+            const auto *W = static_cast<const uint16_t *>(w);
+            const auto *NWt = static_cast<const uint16_t *>(norm_w);
+            const auto *Bs = static_cast<const uint16_t *>(bias);
+            auto *Y = static_cast<uint16_t *>(y);
+            const size_t lds = (size_t)L.total;
+            if (silu) return launch_tiles<EPI_SILU, false>(nm, grid, lds, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Bs, Y, (int)ldy);
+            if (Bs) return launch_tiles<EPI_PLAIN, true>(nm, grid, lds, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Bs, Y, (int)ldy);
+            return launch_tiles<EPI_PLAIN, false>(nm, grid, lds, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Bs, Y, (int)ldy);
+        }
+    }
     const GemmCfg c = pick_cfg(M, wcols, K, silu != 0, nm);
     const int64_t MR = 16 * c.ms, nmt = (M + MR - 1) / MR, ncb = wcols / (16 * c.cb);
     // workspace: [counters (zeroed once, self-resetting) | fp32 slabs]
@@ -1281,12 +1319,12 @@ extern "C" int swh_lm_head_sample(const void *x, const void *w, int64_t M, int64
     const auto *X = static_cast<const uint16_t *>(x);
     const auto *W = static_cast<const uint16_t *>(w);
     const auto *NWt = static_cast<const uint16_t *>(norm_w);
-    const int rc = nm == 1   ? launch_lm<1, true>(grid, (size_t)L.total, s, X, W, (int)M, (int)V, (int)K, NWt, eps,
-                                                   ss_in, nullptr, 0, smp)
-                   : nm == 2 ? launch_lm<2, true>(grid, (size_t)L.total, s, X, W, (int)M, (int)V, (int)K, nullptr, eps,
-                                                   ss_in, nullptr, 0, smp)
-                             : launch_lm<0, true>(grid, (size_t)L.total, s, X, W, (int)M, (int)V, (int)K, nullptr, eps,
-                                                   nullptr, nullptr, 0, smp);
+    const int rc = nm == 1   ? launch_lm<1, EPI_PLAIN, false, true>(grid, (size_t)L.total, s, X, W, (int)M, (int)V, (int)K,
+                                                                   NWt, eps, ss_in, nullptr, nullptr, 0, smp)
+                   : nm == 2 ? launch_lm<2, EPI_PLAIN, false, true>(grid, (size_t)L.total, s, X, W, (int)M, (int)V, (int)K,
+                                                                   nullptr, eps, ss_in, nullptr, nullptr, 0, smp)
+                             : launch_lm<0, EPI_PLAIN, false, true>(grid, (size_t)L.total, s, X, W, (int)M, (int)V, (int)K,
+                                                                   nullptr, eps, nullptr, nullptr, nullptr, 0, smp);
     if (rc != SWH_OK) return rc;
     lm_sample_finalize_kernel<<<dim3((unsigned)M), 256, 0, s>>>(smp.part, smp.pstride, p, step, finished, out_tokens,
                                                                out_ld, cur_tokens, (int)V);

@@ -14,7 +14,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SO = os.path.join(ROOT, "tools", "_build", "libgemm_probe.so")
-PHASES = ["issued", "stat", "ximage", "mfma", "merged", "exit"]
+PHASES = ["p1", "p2", "p3", "p4", "p5", "exit"]
 
 
 def build():
@@ -61,11 +61,11 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
     shapes = {
-        "qkv": (s, wq, 1152, H, nw, bq, None, 0, qkv, 1152, ss, None),
+        "qkv": (s, wq, 1152, H, None, bq, None, 0, qkv, 1152, ss, None),  # folded norm: rstd row scale
         "o": (att, wo, H, H, None, None, s, 0, None, H, None, ssout),
-        "gate_up": (s, wgu, I, H, nw, None, None, 1, y_act, I, ss, None),
+        "gate_up": (s, wgu, I, H, None, None, None, 1, y_act, I, ss, None),
         "down": (act, wd, H, I, None, None, s, 0, None, H, None, ssout),
-        "lm": (s, wl, V, H, nw, None, None, 0, logits, V, ss, None),
+        "lm": (s, wl, V, H, None, None, None, 0, logits, V, ss, None),
     }
     for name, (x, w, N, K, nrm, b, res, silu, y, ldy, ssin, sso) in shapes.items():
         def call():
