@@ -239,6 +239,17 @@ int swh_rmsnorm_bwd(const void *x, const void *weight, const float *rstd, const 
 /* out[r, i] = bf16(bf16(silu(gu[r, i])) * gu[r, I + i]) — gate/up packed. */
 int swh_silu_mul_fwd(const void *gu, int64_t rows, int64_t I, void *out, void *stream);
 int swh_silu_mul_bwd(const void *gu, const void *dout, int64_t rows, int64_t I, void *dgu, void *stream);
+/* QKV split + rotate-half RoPE of the full-sequence forward (transformers
+ * apply_rotary_pos_emb in bf16, with bf16-rounded cos/sin; the reference's
+ * training / scoring forward, grpo_trainer.py:1249):
+ *   forward  (backward = 0): qkv [B*L, (Hq+2Hkv) D] -> q [B,Hq,L,D],
+ *            k [B,Hkv,L,D] rotated at positions[b*L + l], v [B,Hkv,L,D] copied;
+ *   backward (backward = 1): q/k/v hold dq/dk/dv, qkv receives d qkv (the
+ *            autograd of the bf16 ops: dx1 = bf16(bf16(dy1 c) + bf16(dy2 s)),
+ *            dx2 = bf16(bf16(dy2 c) - bf16(dy1 s))).  D % 16 == 0. */
+int swh_qkv_rope(void *qkv, const int64_t *positions, const float *rope_cos, const float *rope_sin, int64_t B,
+                 int64_t L, int32_t Hq, int32_t Hkv, int32_t D, void *q, void *k, void *v, int32_t backward,
+                 void *stream);
 /* x[b, :] = table[ids[b], :] (bf16 rows of width H, H % 16 == 0); ss_out f32
  * [B, H/16] nullable: per 16-column chunk sums of squares of each row (the
  * RMSNorm statistic swh_decode_gemm takes as ss_in). */

@@ -247,6 +247,72 @@ __global__ __launch_bounds__(256) void embed_gather_kernel(const uint16_t *__res
     }
 }
 
+// ---------------------------------------------------------------------------
+// QKV split + RoPE for the full-sequence forward (training / prefill):
+// qkv [R = B*L, (Hq + 2 Hkv) D] -> q [B, Hq, L, D], k [B, Hkv, L, D] (rotated),
+// v [B, Hkv, L, D]; transformers' bf16 rotate-half: y1 = bf16(bf16(x1 c) +
+// bf16(-x2 s)), y2 = bf16(bf16(x2 c) + bf16(x1 s)).  One thread = 8 pairs.
+// Backward (torch autograd of those bf16 ops): dx1 = bf16(bf16(dy1 c) +
+// bf16(dy2 s)), dx2 = bf16(bf16(dy2 c) - bf16(dy1 s)); v passes through.
+// ---------------------------------------------------------------------------
+template <bool BWD>
+__global__ __launch_bounds__(256) void qkv_rope_kernel(uint16_t *__restrict__ qkv, const int64_t *__restrict__ pos,
+                                                       const float *__restrict__ rc, const float *__restrict__ rs,
+                                                       int64_t R, int L, int Hq, int Hkv, int D,
+                                                       uint16_t *__restrict__ q, uint16_t *__restrict__ k,
+                                                       uint16_t *__restrict__ v) {
+    const int HD = D / 2, G = HD / 8;  // 8-pair groups per head
+    const int H3 = Hq + 2 * Hkv;
+    const int64_t total = R * H3 * G;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int gi = (int)(idx % G);
+        const int h = (int)((idx / G) % H3);
+        const int64_t r = idx / ((int64_t)G * H3);
+        const int64_t b = r / L, l = r - b * L;
+        uint16_t *src = qkv + r * (int64_t)H3 * D + (int64_t)h * D + gi * 8;
+        uint16_t *dst;
+        if (h < Hq) dst = q + ((b * Hq + h) * (int64_t)L + l) * D + gi * 8;
+        else if (h < Hq + Hkv) dst = k + ((b * Hkv + (h - Hq)) * (int64_t)L + l) * D + gi * 8;
+        else dst = v + ((b * Hkv + (h - Hq - Hkv)) * (int64_t)L + l) * D + gi * 8;
+        uint4 *a1 = reinterpret_cast<uint4 *>(BWD ? src : dst), *a2 = reinterpret_cast<uint4 *>((BWD ? src : dst) + HD);
+        const uint4 *i1 = reinterpret_cast<const uint4 *>(BWD ? dst : src);
+        const uint4 *i2 = reinterpret_cast<const uint4 *>((BWD ? dst : src) + HD);
+        if (h >= Hq + Hkv) {  // v: copy
+            *a1 = *i1;
+            *a2 = *i2;
+            continue;
+        }
+        const int64_t p = pos[r] < 0 ? 0 : pos[r];
+        const float4 *cp = reinterpret_cast<const float4 *>(rc + p * HD + gi * 8);
+        const float4 *sp = reinterpret_cast<const float4 *>(rs + p * HD + gi * 8);
+        const float4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
+        const float c[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        float x1[8], x2[8], y1[8], y2[8];
+        unpack16<SWH_BF16>(*i1, x1);
+        unpack16<SWH_BF16>(*i2, x2);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            if constexpr (!BWD) {
+                y1[e] = round_bf16(x1[e] * c[e]) + round_bf16(-x2[e] * sn[e]);
+                y2[e] = round_bf16(x2[e] * c[e]) + round_bf16(x1[e] * sn[e]);
+            } else {  // x = dy here, y = dx
+                y1[e] = round_bf16(x1[e] * c[e]) + round_bf16(x2[e] * sn[e]);
+                y2[e] = round_bf16(x2[e] * c[e]) - round_bf16(x1[e] * sn[e]);
+            }
+        }
+        uint32_t o1[4], o2[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            o1[e] = (uint32_t)f32_to_bf16_bits(y1[2 * e]) | ((uint32_t)f32_to_bf16_bits(y1[2 * e + 1]) << 16);
+            o2[e] = (uint32_t)f32_to_bf16_bits(y2[2 * e]) | ((uint32_t)f32_to_bf16_bits(y2[2 * e + 1]) << 16);
+        }
+        *a1 = uint4{o1[0], o1[1], o1[2], o1[3]};
+        *a2 = uint4{o2[0], o2[1], o2[2], o2[3]};
+    }
+}
+
 }  // namespace
 }  // namespace swh
 
@@ -311,5 +377,27 @@ extern "C" int swh_embed_gather(const void *table, const int64_t *ids, int64_t B
     if (B == 0) return SWH_OK;
     embed_gather_kernel<<<dim3((unsigned)B), 128, 0, static_cast<hipStream_t>(stream)>>>(
         static_cast<const uint16_t *>(table), ids, H, static_cast<uint16_t *>(x), ss_out);
+    return launch_status();
+}
+
+extern "C" int swh_qkv_rope(void *qkv, const int64_t *positions, const float *rope_cos, const float *rope_sin,
+                            int64_t B, int64_t L, int32_t Hq, int32_t Hkv, int32_t D, void *q, void *k, void *v,
+                            int32_t backward, void *stream) {
+    if (!qkv || !positions || !rope_cos || !rope_sin || !q || !k || !v || B < 0 || L < 0 || Hq <= 0 || Hkv <= 0 ||
+        D <= 0 || D % 16)
+        return SWH_E_ARG;
+    const int64_t R = B * L;
+    if (R == 0) return SWH_OK;
+    const int64_t work = R * (Hq + 2 * Hkv) * (D / 16);
+    int64_t grid = (work + 255) / 256;
+    if (grid > 256 * 32) grid = 256 * 32;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    auto *Q = static_cast<uint16_t *>(q), *K = static_cast<uint16_t *>(k), *V = static_cast<uint16_t *>(v);
+    if (backward)
+        qkv_rope_kernel<true><<<dim3((unsigned)grid), 256, 0, s>>>(static_cast<uint16_t *>(qkv), positions, rope_cos,
+                                                                  rope_sin, R, (int)L, Hq, Hkv, D, Q, K, V);
+    else
+        qkv_rope_kernel<false><<<dim3((unsigned)grid), 256, 0, s>>>(static_cast<uint16_t *>(qkv), positions, rope_cos,
+                                                                   rope_sin, R, (int)L, Hq, Hkv, D, Q, K, V);
     return launch_status();
 }

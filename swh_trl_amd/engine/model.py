@@ -318,18 +318,15 @@ class CausalLM:
     def _gv(self, name):
         return self.g.get(name) if self.grad is not None else None
 
-    def _layer(self, i: int, x: torch.Tensor, cos, sin, mask, kv_out=None):
+    def _layer(self, i: int, x: torch.Tensor, positions, cos_t, sin_t, mask, kv_out=None):
         c = self.cfg
         B, L, _ = x.shape
         Hq, Hkv, D = c.num_attention_heads, c.num_key_value_heads, c.head_dim
         h = _RMSNorm.apply(x, self.p[f"l{i}.ln_in"], self._gv(f"l{i}.ln_in"), c.rms_norm_eps)
         qkv = _Linear.apply(h, self.p[f"l{i}.qkv_w"], self.p.get(f"l{i}.qkv_b"), self._gv(f"l{i}.qkv_w"),
                             self._gv(f"l{i}.qkv_b"))
-        q = qkv[..., :c.q_dim].view(B, L, Hq, D).transpose(1, 2)
-        k = qkv[..., c.q_dim:c.q_dim + c.kv_dim].view(B, L, Hkv, D).transpose(1, 2)
-        v = qkv[..., c.q_dim + c.kv_dim:].view(B, L, Hkv, D).transpose(1, 2)
-        q = _apply_rope(q, cos, sin)
-        k = _apply_rope(k, cos, sin)
+        # split + rotate-half RoPE + [B, H, L, D] layout in one kernel each way
+        q, k, v = nn_ops.QKVRopeFn.apply(qkv, positions, cos_t, sin_t, Hq, Hkv, D)
         if kv_out is not None:
             kv_out(i, k, v)
         # GQA inside the attention kernel: materialising repeat_interleave'd K/V
@@ -360,9 +357,7 @@ class CausalLM:
         if positions is None:
             positions = torch.arange(L, device=ids.device).expand(B, L)
         cos_t, sin_t = self.rope(int(positions.max().item()) + 1 if positions.numel() else 1)
-        pc = positions.clamp(min=0)
-        cos = torch.cat([cos_t[pc], cos_t[pc]], -1).to(self.dtype).unsqueeze(1)
-        sin = torch.cat([sin_t[pc], sin_t[pc]], -1).to(self.dtype).unsqueeze(1)
+        positions = positions.to(torch.int64).contiguous()
         mask = None
         if key_mask is not None and not bool(key_mask.bool().all()):
             causal = torch.ones(L, L, device=ids.device, dtype=torch.bool).tril()
@@ -370,7 +365,7 @@ class CausalLM:
             mask = (causal & (key_mask.bool()[:, None, None, :] | eye))  # pad queries see themselves
         x = _Embedding.apply(ids, self.p["embed"], self._gv("embed"), self._anchor)
         for i in range(c.num_hidden_layers):
-            x = self._layer(i, x, cos, sin, mask, kv_out)
+            x = self._layer(i, x, positions, cos_t, sin_t, mask, kv_out)
         return _RMSNorm.apply(x, self.p["norm"], self._gv("norm"), c.rms_norm_eps)
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:

@@ -175,3 +175,35 @@ def lm_head_sample(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Tensor, 
          ctypes.byref(params), rng.data_ptr(), step.data_ptr(), finished.data_ptr(), out_tokens.data_ptr(),
          out_tokens.stride(0), _p(cur_tokens), workspace.data_ptr(), workspace.numel(), _stream())
     return out_tokens
+
+
+class QKVRopeFn(torch.autograd.Function):
+    """qkv [B, L, (Hq+2Hkv) D] -> q, k (rotated), v as contiguous [B, H, L, D]
+    (include/swh_trl_amd.h swh_qkv_rope); backward writes d qkv in one pass."""
+
+    @staticmethod
+    def forward(ctx, qkv, positions, cos, sin, Hq: int, Hkv: int, D: int):
+        _dev(qkv, "qkv_rope")
+        B, L, _ = qkv.shape
+        qkv_c = qkv.contiguous()
+        pos = positions.reshape(-1).to(torch.int64).contiguous()
+        q = torch.empty(B, Hq, L, D, device=qkv.device, dtype=qkv.dtype)
+        k = torch.empty(B, Hkv, L, D, device=qkv.device, dtype=qkv.dtype)
+        v = torch.empty(B, Hkv, L, D, device=qkv.device, dtype=qkv.dtype)
+        call("swh_qkv_rope", qkv_c.data_ptr(), pos.data_ptr(), cos.data_ptr(), sin.data_ptr(), B, L, Hq, Hkv, D,
+             q.data_ptr(), k.data_ptr(), v.data_ptr(), 0, _stream())
+        ctx.save_for_backward(pos, cos, sin)
+        ctx.dims = (B, L, Hq, Hkv, D)
+        return q, k, v
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        pos, cos, sin = ctx.saved_tensors
+        B, L, Hq, Hkv, D = ctx.dims
+        dq = torch.zeros(B, Hq, L, D, device=pos.device, dtype=torch.bfloat16) if dq is None else dq.contiguous()
+        dk = torch.zeros(B, Hkv, L, D, device=pos.device, dtype=torch.bfloat16) if dk is None else dk.contiguous()
+        dv = torch.zeros(B, Hkv, L, D, device=pos.device, dtype=torch.bfloat16) if dv is None else dv.contiguous()
+        dqkv = torch.empty(B, L, (Hq + 2 * Hkv) * D, device=pos.device, dtype=dq.dtype)
+        call("swh_qkv_rope", dqkv.data_ptr(), pos.data_ptr(), cos.data_ptr(), sin.data_ptr(), B, L, Hq, Hkv, D,
+             dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), 1, _stream())
+        return dqkv, None, None, None, None, None, None

@@ -495,6 +495,43 @@ def _rope_tables(D, max_pos, theta, dev):
     return fr.cos().to(torch.bfloat16).float().to(dev), fr.sin().to(torch.bfloat16).float().to(dev)
 
 
+@pytest.mark.parametrize("B,L,Hq,Hkv,D,left_pad", [(3, 37, 14, 2, 64, False), (2, 50, 4, 4, 128, True),
+                                                   (1, 1, 2, 1, 32, False)])
+def test_qkv_rope_matches_torch_rotate_half(ops, dev, B, L, Hq, Hkv, D, left_pad):
+    """Fused split + RoPE vs the torch bf16 ops it replaces (transformers'
+    apply_rotary_pos_emb on q/k slices of the packed projection), forward and
+    autograd backward: bit-exact."""
+    from swh_trl_amd import nn_ops
+    from swh_trl_amd.engine.model import _apply_rope
+    g = _gen(23)
+    W = (Hq + 2 * Hkv) * D
+    qkv = torch.randn(B, L, W, generator=g).to(torch.bfloat16).to(dev)
+    pos = torch.arange(L).expand(B, L).clone()
+    if left_pad:  # left-padded prompts: positions = cumsum(mask) - 1, negative on pads
+        pos = pos - torch.randint(0, L // 2, (B, 1), generator=g)
+    pos = pos.to(dev)
+    cos_t, sin_t = _rope_tables(D, L + 4, 1e6, dev)
+    dq = torch.randn(B, Hq, L, D, generator=g).to(torch.bfloat16).to(dev)
+    dk = torch.randn(B, Hkv, L, D, generator=g).to(torch.bfloat16).to(dev)
+    dv = torch.randn(B, Hkv, L, D, generator=g).to(torch.bfloat16).to(dev)
+
+    a = qkv.clone().requires_grad_(True)
+    q, k, v = nn_ops.QKVRopeFn.apply(a, pos, cos_t, sin_t, Hq, Hkv, D)
+    assert q.is_contiguous() and k.is_contiguous() and v.is_contiguous()
+    torch.autograd.backward((q, k, v), (dq, dk, dv))
+
+    b = qkv.clone().requires_grad_(True)
+    pc = pos.clamp(min=0)
+    cos = torch.cat([cos_t[pc], cos_t[pc]], -1).to(torch.bfloat16).unsqueeze(1)
+    sin = torch.cat([sin_t[pc], sin_t[pc]], -1).to(torch.bfloat16).unsqueeze(1)
+    qr = _apply_rope(b[..., :Hq * D].view(B, L, Hq, D).transpose(1, 2), cos, sin)
+    kr = _apply_rope(b[..., Hq * D:(Hq + Hkv) * D].view(B, L, Hkv, D).transpose(1, 2), cos, sin)
+    vr = b[..., (Hq + Hkv) * D:].view(B, L, Hkv, D).transpose(1, 2)
+    torch.autograd.backward((qr, kr, vr), (dq, dk, dv))
+    assert torch.equal(q, qr) and torch.equal(k, kr) and torch.equal(v, vr)
+    assert torch.equal(a.grad, b.grad)
+
+
 @pytest.mark.parametrize("D,Hq,Hkv,Tmax,step", [(64, 14, 2, 320, 270), (128, 32, 8, 320, 270),
                                                 (64, 14, 2, 1280, 1200), (128, 32, 8, 700, 600)])
 def test_attn_decode(ops, dev, D, Hq, Hkv, Tmax, step):
