@@ -30,6 +30,8 @@ for step in "$@"; do
     serial2) AMD_SERIALIZE_KERNEL=3 SWH_TRACE=1 run serial2 500 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --layers 2 ;;
     trace2) SWH_TRACE=1 run trace2 400 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --layers 2 ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null && run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
+    pmcf) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null && run pmcf 400 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmcf -o run --output-format csv -- python3 tools/bench_decode.py ;;
+    pmcw) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null && run pmcw 400 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmcw -o run --output-format csv -- python3 tools/bench_decode.py ;;
     trace) SWH_TRACE=1 run trace 600 python bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
   esac
 done

@@ -208,7 +208,8 @@ class DecodeEngine:
     def kernel_timings(self, step_index: int, reps: int = 20, iters: int = 3) -> dict:
         """Device time of each kernel of one fused decode step at sampler index
         `step_index` (attention over P + step_index keys), plus the whole step.
-        Each op is captured `reps` times into a HIP graph and replayed `iters`
+        Each per-layer op is captured once per layer (layer i's weights and
+        cache), the lm head `reps` times, into a HIP graph replayed `iters`
         times between HIP events on the capture stream, so a figure is the
         kernel plus its in-graph launch boundary (what the decode graph pays).
         Clobbers the decode scratch buffers and one cache slot: call between
@@ -231,49 +232,55 @@ class DecodeEngine:
             return wN * K * bf + B * K * bf + B * N * bf * (2 if not silu and N == H else 1)
 
         ss = self.ss
+        # every per-layer op cycles through the L layers' weights / caches as the
+        # decode step does: the figures carry the step's cache state (~1 GB of
+        # weights per step streams from HBM; one layer's alone would sit in the
+        # 256 MiB Infinity Cache and time optimistically)
         ops_ = {
-            "decode_gemm.qkv": (lambda: nn_ops.decode_gemm(self.s, self._normed("l0.qkv_w", "l0.ln_in")[0],
-                                                           norm_w=self._normed("l0.qkv_w", "l0.ln_in")[1], eps=eps,
-                                                           bias=p.get("l0.qkv_b"), y=self.qkv, ss_in=ss),
+            "decode_gemm.qkv": (lambda i: nn_ops.decode_gemm(self.s, self._normed(f"l{i}.qkv_w", f"l{i}.ln_in")[0],
+                                                             norm_w=self._normed(f"l{i}.qkv_w", f"l{i}.ln_in")[1],
+                                                             eps=eps, bias=p.get(f"l{i}.qkv_b"), y=self.qkv,
+                                                             ss_in=ss),
                                 gemm_bytes(c.qkv_dim, H), L),
-            "attn_decode": (lambda: nn_ops.attn_decode(self.qkv, self.kv[0, 0], self.kv[0, 1], self.cos, self.sin,
-                                                       self.plen, self.state, c.num_attention_heads,
-                                                       c.num_key_value_heads, c.head_dim, c.head_dim ** -0.5,
-                                                       out=self.att),
+            "attn_decode": (lambda i: nn_ops.attn_decode(self.qkv, self.kv[i, 0], self.kv[i, 1], self.cos, self.sin,
+                                                         self.plen, self.state, c.num_attention_heads,
+                                                         c.num_key_value_heads, c.head_dim, c.head_dim ** -0.5,
+                                                         out=self.att),
                             att_bytes, L),
-            "decode_gemm.o": (lambda: nn_ops.decode_gemm(self.att, p["l0.o_w"], residual=self.s, ss_out=ss),
+            "decode_gemm.o": (lambda i: nn_ops.decode_gemm(self.att, p[f"l{i}.o_w"], residual=self.s, ss_out=ss),
                               gemm_bytes(H, c.q_dim), L),
-            "decode_gemm.gate_up": (lambda: nn_ops.decode_gemm(self.s, self._normed("l0.gu_w", "l0.ln_post")[0],
-                                                               norm_w=self._normed("l0.gu_w", "l0.ln_post")[1],
-                                                               eps=eps, silu=True, y=self.act, ss_in=ss),
+            "decode_gemm.gate_up": (lambda i: nn_ops.decode_gemm(self.s, self._normed(f"l{i}.gu_w", f"l{i}.ln_post")[0],
+                                                                 norm_w=self._normed(f"l{i}.gu_w", f"l{i}.ln_post")[1],
+                                                                 eps=eps, silu=True, y=self.act, ss_in=ss),
                                     gemm_bytes(I, H, silu=True), L),
-            "decode_gemm.down": (lambda: nn_ops.decode_gemm(self.act, p["l0.down_w"], residual=self.s, ss_out=ss),
+            "decode_gemm.down": (lambda i: nn_ops.decode_gemm(self.act, p[f"l{i}.down_w"], residual=self.s,
+                                                              ss_out=ss),
                                  gemm_bytes(H, I), L),
-            "decode_gemm.lm_head": (lambda: nn_ops.decode_gemm(self.s, self._normed("lm", "norm")[0],
-                                                               norm_w=self._normed("lm", "norm")[1], eps=eps,
-                                                               y=self.logits_buf, ss_in=ss),
+            "decode_gemm.lm_head": (lambda i: nn_ops.decode_gemm(self.s, self._normed("lm", "norm")[0],
+                                                                 norm_w=self._normed("lm", "norm")[1], eps=eps,
+                                                                 y=self.logits_buf, ss_in=ss),
                                     c.vocab_size * H * bf + B * c.vocab_size * bf, 1),
-            "sample_step": (self._sample, B * c.vocab_size * bf, 1),
+            "sample_step": (lambda i: self._sample(), B * c.vocab_size * bf, 1),
         }
         if self._fused_sample():  # what the decode graph runs instead of lm head + sample_step
             del ops_["decode_gemm.lm_head"], ops_["sample_step"]
             ops_["lm_head_sample"] = (
-                lambda: nn_ops.lm_head_sample(self.s, self._normed("lm", "norm")[0], self.params, self.rng,
-                                              self.state[0:1], self.finished, self.out, self.cur,
-                                              norm_w=self._normed("lm", "norm")[1], eps=eps, ss_in=ss,
-                                              workspace=self.sample_ws),
+                lambda i: nn_ops.lm_head_sample(self.s, self._normed("lm", "norm")[0], self.params, self.rng,
+                                                self.state[0:1], self.finished, self.out, self.cur,
+                                                norm_w=self._normed("lm", "norm")[1], eps=eps, ss_in=ss,
+                                                workspace=self.sample_ws),
                 c.vocab_size * H * bf, 1)
         nn_ops.embed_gather(p["embed"], self.cur, self.s, ss_out=ss)
         out = {}
         stream = torch.cuda.current_stream()
 
-        def timed(fn, n):
-            fn()
+        def timed(fn, n, cycle):
+            fn(0)
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                for _ in range(n):
-                    fn()
+                for r in range(n):
+                    fn(r % cycle)
             g.replay()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
@@ -284,9 +291,12 @@ class DecodeEngine:
             return 1000.0 * e0.elapsed_time(e1) / (n * iters)
 
         for name, (fn, nbytes, per_step) in ops_.items():
-            out[name] = {"avg_us": timed(fn, reps), "bytes_per_launch": float(nbytes), "launches_per_step": per_step}
+            n = L if per_step == L else reps
+            out[name] = {"avg_us": timed(fn, n, per_step), "bytes_per_launch": float(nbytes),
+                         "launches_per_step": per_step}
         self.state[0] = step_index
-        out["decode_step"] = {"avg_us": timed(self._step_fused, 2), "bytes_per_launch": None, "launches_per_step": 1}
+        out["decode_step"] = {"avg_us": timed(lambda i: self._step_fused(), 2, 1), "bytes_per_launch": None,
+                              "launches_per_step": 1}
         return out
 
     # ------------------------------------------------------------------ prefill
