@@ -360,9 +360,14 @@ class CausalLM:
         positions = positions.to(torch.int64).contiguous()
         mask = None
         if key_mask is not None and not bool(key_mask.bool().all()):
+            km = key_mask.bool()
             causal = torch.ones(L, L, device=ids.device, dtype=torch.bool).tril()
+            # a query with no valid key at all (left padding) sees itself, so no
+            # softmax row is empty; any other padded query (right padding after
+            # a stop token) sees exactly the valid keys before it, as transformers
+            no_key = km.cumsum(-1) == 0
             eye = torch.eye(L, device=ids.device, dtype=torch.bool)
-            mask = (causal & (key_mask.bool()[:, None, None, :] | eye))  # pad queries see themselves
+            mask = causal & (km[:, None, None, :] | (eye & no_key[:, None, :, None]))
         x = _Embedding.apply(ids, self.p["embed"], self._gv("embed"), self._anchor)
         for i in range(c.num_hidden_layers):
             x = self._layer(i, x, positions, cos_t, sin_t, mask, kv_out)

@@ -61,24 +61,28 @@ class TrainerState:
         self.log_history: list[dict] = []
 
 
-def load_model(model, device, trainable=True, seed=0) -> CausalLM:
+def load_model(model, device, trainable=True, seed=0, head: str = "lm") -> CausalLM:
     """`model` may be a CausalLM, a preset name ("qwen2.5-0.5b", "llama-3-8b",
     "tiny"), a DecoderConfig (random init), a local directory holding a
-    transformers config.json + safetensors, or a transformers PreTrainedModel."""
+    transformers config.json + safetensors, or a transformers PreTrainedModel.
+    head="score": a sequence-classification model (value / reward model, one
+    output), as transformers' *ForSequenceClassification."""
     if isinstance(model, CausalLM):
+        if model.head != head:
+            raise ValueError(f"expected a model with a {head!r} head, got {model.head!r}")
         return model
     if isinstance(model, DecoderConfig):
-        return CausalLM(model, device, seed=seed, trainable=trainable)
+        return CausalLM(model, device, head=head, seed=seed, trainable=trainable)
     if isinstance(model, str):
         if model in PRESETS:
-            return CausalLM(PRESETS[model](), device, seed=seed, trainable=trainable)
+            return CausalLM(PRESETS[model](), device, head=head, seed=seed, trainable=trainable)
         if os.path.isdir(model):
             import json
 
             from safetensors.torch import load_file
             with open(os.path.join(model, "config.json")) as f:
                 cfg = from_hf_config(json.load(f))
-            m = CausalLM(cfg, device, seed=None, trainable=trainable)
+            m = CausalLM(cfg, device, head=head, seed=None, trainable=trainable)
             sd = {}
             for fn in sorted(os.listdir(model)):
                 if fn.endswith(".safetensors"):
@@ -89,7 +93,7 @@ def load_model(model, device, trainable=True, seed=0) -> CausalLM:
                          "model object")
     if hasattr(model, "config") and hasattr(model, "state_dict"):
         cfg = from_hf_config(model.config)
-        m = CausalLM(cfg, device, seed=None, trainable=trainable)
+        m = CausalLM(cfg, device, head=head, seed=None, trainable=trainable)
         m.load_hf_state_dict({k: v.to(device) for k, v in model.state_dict().items()})
         return m
     raise TypeError(f"unsupported model type {type(model)}")

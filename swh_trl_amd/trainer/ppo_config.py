@@ -1,0 +1,92 @@
+"""PPOConfig — field names and defaults of trl/trainer/ppo_config.py:22-135 and
+the OnPolicyConfig it extends (trl/trainer/utils.py:744-870), plus the
+TrainingArguments fields the loop reads.  The derived batch sizes
+(`local_batch_size`, `mini_batch_size`, ... ) are filled by PPOTrainer exactly
+as ppo_trainer.py:228-250 does.  Unknown keyword arguments are kept (and
+ignored) so reference configs construct unchanged."""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+from typing import Any, Optional
+
+
+@dataclass
+class PPOConfig:
+    # TrainingArguments subset
+    output_dir: Optional[str] = None
+    per_device_train_batch_size: int = 8
+    per_device_eval_batch_size: int = 8
+    gradient_accumulation_steps: int = 1
+    num_train_epochs: float = 3.0
+    learning_rate: float = 5e-5
+    weight_decay: float = 0.0
+    adam_beta1: float = 0.9
+    adam_beta2: float = 0.999
+    adam_epsilon: float = 1e-8
+    lr_scheduler_type: str = "linear"
+    warmup_steps: int = 0
+    warmup_ratio: float = 0.0
+    logging_steps: float = 10              # OnPolicyConfig (utils.py:759)
+    eval_steps: Optional[float] = None
+    save_steps: float = 500
+    seed: int = 42
+    bf16: Optional[bool] = None            # OnPolicyConfig: not fp16 when unset (utils.py:870-873)
+    fp16: bool = False
+    report_to: Any = None
+    # OnPolicyConfig (utils.py:744-870)
+    run_name: Optional[str] = None
+    dataset_num_proc: Optional[int] = None
+    num_mini_batches: int = 1
+    total_episodes: Optional[int] = None
+    local_rollout_forward_batch_size: int = 64
+    num_sample_generations: int = 10
+    response_length: int = 53
+    stop_token: Optional[str] = None
+    stop_token_id: Optional[int] = None
+    temperature: float = 0.7
+    missing_eos_penalty: Optional[float] = None
+    sft_model_path: str = "EleutherAI/pythia-160m"
+    world_size: Optional[int] = None
+    num_total_batches: Optional[int] = None
+    micro_batch_size: Optional[int] = None
+    local_batch_size: Optional[int] = None
+    batch_size: Optional[int] = None
+    local_mini_batch_size: Optional[int] = None
+    mini_batch_size: Optional[int] = None
+    push_to_hub: bool = False
+    # PPOConfig (ppo_config.py:22-135)
+    exp_name: str = "ppo_config"
+    reward_model_path: str = "EleutherAI/pythia-160m"
+    model_adapter_name: Optional[str] = None
+    ref_adapter_name: Optional[str] = None
+    num_ppo_epochs: int = 4
+    whiten_rewards: bool = False
+    kl_coef: float = 0.05
+    kl_estimator: str = "k1"
+    cliprange: float = 0.2
+    vf_coef: float = 0.1
+    cliprange_value: float = 0.2
+    gamma: float = 1.0
+    lam: float = 0.95
+    ds3_gather_for_generation: bool = True
+    # engine knobs (not in the reference)
+    decode_check_every: int = 8            # host check of "all finished" every k decode steps (0 = never)
+    extra: dict = field(default_factory=dict)
+
+    def __init__(self, **kwargs):
+        known = {f for f in self.__dataclass_fields__ if f != "extra"}
+        extra = {k: kwargs.pop(k) for k in list(kwargs) if k not in known}
+        for name, f in self.__dataclass_fields__.items():
+            if name != "extra":
+                setattr(self, name, kwargs.get(name, f.default))
+        self.extra = extra
+        self.__post_init__()
+
+    def __post_init__(self):
+        self.bf16 = (not self.fp16) if self.bf16 is None else self.bf16
+        if self.output_dir is None:
+            self.output_dir = "trainer_output"
+
+    def to_dict(self) -> dict:
+        return {k: getattr(self, k) for k in self.__dataclass_fields__}

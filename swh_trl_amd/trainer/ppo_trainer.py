@@ -1,0 +1,427 @@
+"""PPOTrainer — drop-in for trl.PPOTrainer's training loop on MI355X.
+
+Constructor and config keep the reference's names (ppo_trainer.py:102-119,
+ppo_config.py); `train()` keeps the semantics of ppo_trainer.py:347-646 while
+every per-token stage runs on the HIP engine:
+
+  rollout       DecodeEngine.generate, log-probs of the drawn tokens from the
+                sampler's processed fp32 scores (utils.py:1094, :1119 — the
+                reference's `selective_log_softmax(logitss, response)`)
+  ref log-prob  no-grad full forward -> fused lm head + log-prob kernel
+  value / score score-head forwards (get_reward, utils.py:900-947)
+  rewards       KL-shaped token rewards + score at the sequence end (:496-516)
+  whiten / GAE  ops.masked_whiten, ops.gae (reverse scan kernel) (:518-535)
+  update        num_ppo_epochs x mini-batches x GA micro-batches: policy and
+                value forwards, fused clipped PG + value loss fwd/bwd kernel,
+                flat-buffer AdamW per mini-batch (:537-617), RCCL all-reduce
+                of both models' gradients for DP
+
+Out of scope: PEFT adapters, DeepSpeed, sample-generation
+tables, hub pushes, checkpoints.
+"""
+from __future__ import annotations
+
+import math
+import time
+from collections import defaultdict
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .. import dist as swh_dist
+from .. import ops
+from ..engine.decode import DecodeEngine
+from ..engine.model import CausalLM
+from ..optim import FlatAdamW
+from .grpo_trainer import TrainerState, _trace, load_model
+from .ppo_config import PPOConfig
+from .utils import left_pad, linear_lr
+
+INVALID_LOGPROB = 1.0  # ppo_trainer.py:81
+
+
+def exact_div(a: int, b: int, msg: str) -> int:
+    """trl/trainer/utils.py exact_div."""
+    q = a // b
+    if a != q * b:
+        raise ValueError(f"{msg}, {a} / {b} = {a / b}")
+    return q
+
+
+def fill_batch_sizes(args: PPOConfig, dataset_len: int, world_size: int) -> PPOConfig:
+    """ppo_trainer.py:224-250: the derived batch sizes, in place."""
+    if args.total_episodes is None:
+        args.total_episodes = int(args.num_train_epochs * dataset_len)
+    args.world_size = world_size
+    args.local_batch_size = args.per_device_train_batch_size * args.gradient_accumulation_steps
+    args.micro_batch_size = int(args.per_device_train_batch_size * args.world_size)
+    args.batch_size = int(args.local_batch_size * args.world_size)
+    args.mini_batch_size = exact_div(args.batch_size, args.num_mini_batches,
+                                     "`batch_size` must be a multiple of `num_mini_batches`")
+    args.local_mini_batch_size = exact_div(args.local_batch_size, args.num_mini_batches,
+                                           "`local_batch_size` must be a multiple of `num_mini_batches`")
+    if args.whiten_rewards and args.local_mini_batch_size < 8:
+        raise ValueError(f"Per-rank minibatch size {args.local_mini_batch_size} is insufficient for whitening")
+    args.num_total_batches = math.ceil(args.total_episodes / args.batch_size)
+    return args
+
+
+def first_true_indices(bools: torch.Tensor, dtype=torch.long) -> torch.Tensor:
+    """utils.py:877-897: index of the first True per row, the row length if none."""
+    row_len = bools.size(-1)
+    zero_or_index = row_len * (~bools).type(dtype) + torch.arange(row_len, dtype=dtype, device=bools.device)
+    return torch.min(zero_or_index, dim=-1).values
+
+
+def truncate_response(stop_token_id: int, pad_token_id: int, responses: torch.Tensor) -> torch.Tensor:
+    """utils.py:1036-1056: pad everything after the first stop token."""
+    trunc_idxs = first_true_indices(responses == stop_token_id).unsqueeze(-1)
+    idxs = torch.arange(responses.shape[1], device=responses.device).view(1, -1)
+    return torch.masked_fill(responses, idxs > trunc_idxs, pad_token_id)
+
+
+def _forward_inputs(query_responses: torch.Tensor, pad_token_id: int):
+    """utils.py:900-979 `forward` / `get_reward` inputs: mask = ids != pad,
+    exclusive-cumsum positions, pad ids replaced by 0."""
+    attention_mask = query_responses != pad_token_id
+    position_ids = attention_mask.cumsum(1) - attention_mask.long()
+    input_ids = torch.masked_fill(query_responses, ~attention_mask, 0)
+    return input_ids, attention_mask, position_ids
+
+
+class PPOTrainer:
+    _tag_names = ["trl", "ppo"]
+
+    def __init__(self, args: PPOConfig, processing_class, model, ref_model, reward_model, train_dataset,
+                 value_model, data_collator=None, eval_dataset=None, optimizers=(None, None), callbacks=None,
+                 peft_config=None):
+        if ref_model is model and model is not None:
+            raise ValueError("`model` and `ref_model` cannot be the same object. If you want `ref_model` to be the "
+                             "same as `model`, you must make a copy of it, or `None` if you use peft.")
+        if peft_config is not None:
+            raise ValueError("peft_config: LoRA training is not part of the MI355X engine's scope")
+        self.args = args
+        self.processing_class = processing_class
+        tok = processing_class
+        self.pad_token_id = getattr(tok, "pad_token_id", None)
+        self.eos_token_id = getattr(tok, "eos_token_id", None)
+        if args.extra.get("pad_token_id") is not None:  # token ids without a tokenizer object
+            self.pad_token_id = args.extra["pad_token_id"]
+        if args.extra.get("eos_token_id") is not None:
+            self.eos_token_id = args.extra["eos_token_id"]
+        if self.pad_token_id is None:
+            raise ValueError("PPOTrainer needs a pad token id (processing_class.pad_token_id)")
+        # stop token (ppo_trainer.py:134-145)
+        if args.stop_token and args.stop_token_id:
+            raise ValueError("You cannot set both `stop_token` and `stop_token_id`.")
+        elif args.stop_token:
+            if args.stop_token == "eos":
+                self.stop_token_id = self.eos_token_id
+            else:
+                raise ValueError(f"Unknown `stop_token` {args.stop_token}. Allowed values are: `'eos'` and `None` "
+                                 "(no stop token).")
+        else:
+            self.stop_token_id = args.stop_token_id
+        if args.kl_estimator not in {"k1", "k3"}:
+            raise ValueError("kl_estimator must be either 'k1' (straightforward, unbiased) or 'k3' (lower variance, "
+                             "unbiased, appears to be a strictly better estimator). See [Approximating KL "
+                             "Divergence](http://joschu.net/blog/kl-approx.html) for details.")
+        self.rank, self.world, self.local_rank = swh_dist.init_from_env()
+        if not torch.cuda.is_available():
+            raise RuntimeError("PPOTrainer runs the MI355X engine and needs a ROCm device (no CPU fallback)")
+        self.device = torch.device("cuda", self.local_rank)
+        torch.cuda.set_device(self.device)
+        # models: policy (lm head), frozen ref copy, value model + reward model (score heads)
+        self.policy_model = load_model(model, self.device, trainable=True, seed=args.seed)
+        if ref_model is not None:
+            self.ref_model = load_model(ref_model, self.device, trainable=False, seed=args.seed)
+        else:  # create_reference_model (modeling_base.py:592-664): a frozen deep copy
+            self.ref_model = CausalLM(self.policy_model.cfg, self.device, seed=None, trainable=False)
+            self.ref_model.copy_from(self.policy_model)
+        self.value_model = load_model(value_model, self.device, trainable=True, seed=args.seed + 1, head="score")
+        self.reward_model = load_model(reward_model, self.device, trainable=False, seed=args.seed + 2, head="score")
+        self.train_dataset, self.eval_dataset = train_dataset, eval_dataset
+        self.train_dataset_len = len(train_dataset)
+        fill_batch_sizes(args, self.train_dataset_len, self.world)
+        self.local_seed = args.seed + self.rank * 100003  # ppo_trainer.py:251
+        # one AdamW over policy + value parameters (PolicyAndValueWrapper), no
+        # gradient clipping in the reference loop: two flat buffers, same update
+        mk = lambda m: FlatAdamW(m.numel, self.device, lr=args.learning_rate,  # noqa: E731
+                                 betas=(args.adam_beta1, args.adam_beta2), eps=args.adam_epsilon,
+                                 weight_decay=args.weight_decay, max_grad_norm=None)
+        self.opt_policy, self.opt_value = mk(self.policy_model), mk(self.value_model)
+        self.opt_policy.master.copy_(self.policy_model.flat.float())
+        self.opt_value.master.copy_(self.value_model.flat.float())
+        self.state = TrainerState()
+        self.state.episode = 0
+        self.callbacks = callbacks or []
+        self._engine: Optional[DecodeEngine] = None
+        self._gen_count = 0
+        self._np_rng = np.random.default_rng(self.local_seed)
+        self._data_gen = torch.Generator().manual_seed(args.seed)
+        self._metrics = defaultdict(list)
+
+    # ------------------------------------------------------------------ data
+    def _batches(self):
+        """DataLoader(shuffle=True, drop_last=True, batch_size=local_batch_size)
+        sharded over ranks, repeated forever (ppo_trainer.py:311-318, :358-362)."""
+        a = self.args
+        n, per = self.train_dataset_len, a.local_batch_size
+        glob = per * self.world
+        while True:
+            perm = torch.randperm(n, generator=self._data_gen).tolist()
+            for s in range(0, n - glob + 1, glob):
+                mine = perm[s + self.rank * per: s + (self.rank + 1) * per]
+                yield [self.train_dataset[i] for i in mine]
+
+    def _queries(self, examples) -> torch.Tensor:
+        if "input_ids" not in examples[0]:
+            raise ValueError("PPO datasets carry tokenized `input_ids` (ppo_trainer.py:364)")
+        ids, _ = left_pad([list(x["input_ids"]) for x in examples], self.pad_token_id, self.device)
+        return ids
+
+    def _engine_for(self, B: int, P: int) -> DecodeEngine:
+        e = self._engine
+        C = self.args.response_length
+        if e is None or e.B != B or e.Pmax < P:
+            self._engine = DecodeEngine(self.policy_model, B, P, C)
+        return self._engine
+
+    # ------------------------------------------------------------------ rollout (ppo_trainer.py:362-535)
+    @torch.no_grad()
+    def _no_grad_hidden(self, model: CausalLM, query_responses: torch.Tensor) -> torch.Tensor:
+        saved, model.grad = model.grad, None
+        try:
+            ids, mask, pos = _forward_inputs(query_responses, self.pad_token_id)
+            return model.hidden_states(ids, positions=pos, key_mask=mask)
+        finally:
+            model.grad = saved
+
+    @torch.no_grad()
+    def generate(self, queries: torch.Tensor):
+        """batch_generation (utils.py:1059-1128): sampled responses and the
+        log-probs of the drawn tokens under the processed (T + 1e-7) scores.
+        Generation ends when every row has stopped (transformers stops the
+        batch there), so the response width is the longest row."""
+        a = self.args
+        B, P = queries.shape
+        eng = self._engine_for(B, P)
+        attention_mask = (queries != self.pad_token_id).to(torch.int32)
+        input_ids = torch.masked_fill(queries, attention_mask == 0, 0)
+        seed = a.seed * 1_000_003 + self.rank
+        resp, logp = eng.generate(input_ids, attention_mask, a.response_length, temperature=a.temperature + 1e-7,
+                                  top_p=1.0, top_k=None, eos_token_id=self.stop_token_id,
+                                  pad_token_id=self.pad_token_id, seed=seed,
+                                  offset=self._gen_count * (a.response_length + 1), return_logp=True,
+                                  check_every=a.decode_check_every)
+        self._gen_count += 1
+        T = resp.shape[1]
+        if self.stop_token_id is not None:
+            stopped = first_true_indices(resp == self.stop_token_id)  # T where none
+            T = int(torch.clamp(stopped + 1, max=resp.shape[1]).max())
+        return resp[:, :T].contiguous(), logp[:, :T].contiguous()
+
+    @torch.no_grad()
+    def rollout_from(self, queries: torch.Tensor, responses: torch.Tensor, logprobs: torch.Tensor) -> dict:
+        """Everything after generation (ppo_trainer.py:389-535) for given
+        queries [B, P], responses [B, T] and their generation log-probs."""
+        a = self.args
+        pad = self.pad_token_id
+        P = queries.shape[1]
+        T = responses.shape[1]
+        temp = a.temperature + 1e-7
+        query_responses = torch.cat([queries, responses], 1)
+        # ref log-probs: forward, logits[:, P-1:-1] / (T + 1e-7), selective_log_softmax
+        h = self._no_grad_hidden(self.ref_model, query_responses)
+        ref_logprobs, _ = self.ref_model.logp_entropy(h[:, P - 1:P + T - 1], responses, temp, False)
+        # response processing 1: truncate after the first stop token
+        post = responses
+        if self.stop_token_id is not None:
+            post = truncate_response(self.stop_token_id, pad, responses)
+        sequence_lengths = first_true_indices(post == pad) - 1
+        # values: value model over the raw query_responses, positions P-1 .. P+T-2 (bf16 like the score Linear)
+        hv = self._no_grad_hidden(self.value_model, query_responses)
+        values = self.value_model.scores(hv[:, P - 1:P + T - 1])
+        # response processing 2: reward model score at the last non-pad token of query + truncated response
+        pqr = torch.cat([queries, post], 1)
+        hr = self._no_grad_hidden(self.reward_model, pqr)
+        rm_seq = first_true_indices(pqr[:, P:] == pad) - 1 + P
+        scores = self.reward_model.scores(hr[torch.arange(hr.shape[0], device=hr.device), rm_seq])  # bf16
+        rm_scores = scores.clone()
+        # response processing 3: missing-stop penalty
+        contain_eos = torch.any(post == self.eos_token_id, dim=-1) if self.eos_token_id is not None else \
+            torch.zeros(post.shape[0], dtype=torch.bool, device=post.device)
+        if a.missing_eos_penalty is not None:
+            scores[~contain_eos] -= a.missing_eos_penalty
+        response_idxs = torch.arange(T, device=responses.device).repeat(responses.shape[0], 1)
+        padding_mask = response_idxs > sequence_lengths.unsqueeze(1)
+        logprobs = torch.masked_fill(logprobs.float(), padding_mask, INVALID_LOGPROB)
+        ref_logprobs = torch.masked_fill(ref_logprobs, padding_mask, INVALID_LOGPROB)
+        sequence_lengths_p1 = sequence_lengths + 1
+        padding_mask_p1 = response_idxs > sequence_lengths_p1.unsqueeze(1)
+        values = torch.masked_fill(values, padding_mask_p1, 0)
+        # 4. rewards: -kl_coef * KL (k1 / k3), score added at min(seq_len + 1, T - 1)
+        logr = ref_logprobs - logprobs
+        kl = -logr if a.kl_estimator == "k1" else (logr.exp() - 1) - logr
+        non_score_reward = -a.kl_coef * kl
+        rewards = non_score_reward.clone()
+        actual_start = torch.arange(rewards.size(0), device=rewards.device)
+        actual_end = torch.where(sequence_lengths_p1 < rewards.size(1), sequence_lengths_p1, sequence_lengths)
+        rewards[actual_start, actual_end] += scores
+        # 5. whiten rewards
+        if a.whiten_rewards:
+            rewards = ops.masked_whiten_checked(rewards, ~padding_mask_p1, shift_mean=False)
+            rewards = torch.masked_fill(rewards, padding_mask_p1, 0)
+        # 6. advantages and returns (reverse GAE scan), whitened advantages
+        advantages, returns = ops.gae(rewards, values.float(), a.gamma, a.lam)
+        advantages = ops.masked_whiten_checked(advantages, ~padding_mask)
+        advantages = torch.masked_fill(advantages, padding_mask, 0)
+        return {"queries": queries, "responses": responses, "query_responses": query_responses,
+                "logprobs": logprobs, "ref_logprobs": ref_logprobs, "values": values, "scores": scores, "rm_scores": rm_scores,
+                "rewards": rewards, "advantages": advantages, "returns": returns, "kl": kl,
+                "non_score_reward": non_score_reward, "padding_mask": padding_mask,
+                "padding_mask_p1": padding_mask_p1, "sequence_lengths": sequence_lengths,
+                "postprocessed_responses": post}
+
+    # ------------------------------------------------------------------ PPO update (ppo_trainer.py:537-617)
+    def _micro_step(self, ro: dict, inds: torch.Tensor) -> torch.Tensor:
+        """One micro-batch: policy + value forwards, fused loss fwd/bwd, backward
+        scaled by 1/GA (accelerate's accumulate); returns stats f32[8] + entropy."""
+        a = self.args
+        P = ro["queries"].shape[1]
+        T = ro["responses"].shape[1]
+        temp = a.temperature + 1e-7
+        mb_qr = ro["query_responses"][inds]
+        mb_resp = ro["responses"][inds]
+        pm, pm1 = ro["padding_mask"][inds], ro["padding_mask_p1"][inds]
+        ids, mask, pos = _forward_inputs(mb_qr, self.pad_token_id)
+        hp = self.policy_model.hidden_states(ids, positions=pos, key_mask=mask)
+        new_logprobs, entropy = self.policy_model.logp_entropy(hp[:, P - 1:P + T - 1], mb_resp, temp, True)
+        hv = self.value_model.hidden_states(ids, positions=pos, key_mask=mask)
+        vpred = self.value_model.scores(hv[:, P - 1:P + T - 1])
+        nl = torch.masked_fill(new_logprobs.detach(), pm, INVALID_LOGPROB)
+        vp = torch.masked_fill(vpred.detach().float(), pm1, 0)
+        loss, dnl, dvp, stats = ops.ppo_loss_fwd_bwd(nl, ro["logprobs"][inds], ro["advantages"][inds], vp,
+                                                     ro["values"][inds].float(), ro["returns"][inds], pm, pm1,
+                                                     a.cliprange, a.cliprange_value, a.vf_coef)
+        ga = a.gradient_accumulation_steps
+        # masked_fill blocks the gradient at padded positions (the kernel's d is 0 there too)
+        dnl = torch.masked_fill(dnl, pm, 0.0) / ga
+        dvp = torch.masked_fill(dvp, pm1, 0.0) / ga
+        torch.autograd.backward([new_logprobs, vpred], [dnl.to(new_logprobs.dtype), dvp.to(vpred.dtype)])
+        out = torch.empty(9, device=self.device, dtype=torch.float32)
+        out[:8] = stats
+        out[8] = entropy.float().mean()
+        return out
+
+    def _optimizer_step(self, lr: float):
+        if self.world > 1:
+            swh_dist.allreduce_mean_(self.policy_model.grad)
+            swh_dist.allreduce_mean_(self.value_model.grad)
+        self.opt_policy.step(self.policy_model.grad, model_out=self.policy_model.flat, lr=lr)
+        self.opt_value.step(self.value_model.grad, model_out=self.value_model.flat, lr=lr)
+        self.policy_model.zero_grad()
+        self.value_model.zero_grad()
+
+    def ppo_update(self, ro: dict, lr: float, permutations=None) -> torch.Tensor:
+        """num_ppo_epochs x mini-batches x GA micro-batches (ppo_trainer.py:537-617).
+        `permutations` (tests): one index array per epoch instead of the RNG."""
+        a = self.args
+        stats = torch.zeros(a.num_ppo_epochs, a.num_mini_batches, a.gradient_accumulation_steps, 9,
+                            device=self.device)
+        self.policy_model.zero_grad()
+        self.value_model.zero_grad()
+        for ep in range(a.num_ppo_epochs):
+            b_inds = permutations[ep] if permutations is not None else self._np_rng.permutation(a.local_batch_size)
+            b_inds = torch.as_tensor(np.asarray(b_inds), device=self.device, dtype=torch.long)
+            for mi, mb0 in enumerate(range(0, a.local_batch_size, a.local_mini_batch_size)):
+                mini = b_inds[mb0:mb0 + a.local_mini_batch_size]
+                for gi, u0 in enumerate(range(0, a.local_mini_batch_size, a.per_device_train_batch_size)):
+                    stats[ep, mi, gi] = self._micro_step(ro, mini[u0:u0 + a.per_device_train_batch_size])
+                self._optimizer_step(lr)
+        return stats
+
+    # ------------------------------------------------------------------ the loop
+    def training_step(self, examples=None) -> dict:
+        """One PPO update: rollout of local_batch_size queries, rewards, GAE,
+        then the PPO epochs (ppo_trainer.py:356-617)."""
+        a = self.args
+        if examples is None:
+            if getattr(self, "_iter", None) is None:
+                self._iter = self._batches()
+            examples = next(self._iter)
+        self.state.episode += a.batch_size
+        queries = self._queries(examples)
+        _trace(f"queries {tuple(queries.shape)}")
+        responses, logprobs = self.generate(queries)
+        _trace("generated")
+        ro = self.rollout_from(queries, responses, logprobs)
+        _trace("rollout scored")
+        total = max(1, a.num_total_batches)
+        warm = a.warmup_steps or int(math.ceil(a.warmup_ratio * total))
+        lr = linear_lr(self.state.global_step, total, a.learning_rate, warm) \
+            if a.lr_scheduler_type == "linear" else a.learning_rate
+        stats = self.ppo_update(ro, lr)
+        _trace("ppo epochs")
+        self.state.global_step += 1
+        m = self._metrics
+        m["kl"].append(ro["kl"].sum(1).mean())
+        m["entropy"].append((-ro["logprobs"]).sum(1).mean())
+        m["non_score_reward"].append(ro["non_score_reward"].sum(1).mean())
+        m["scores"].append(ro["scores"].mean())
+        m["stats"].append(stats)
+        m["num_eos"].append((ro["responses"] == self.eos_token_id).sum() if self.eos_token_id is not None
+                            else torch.zeros((), device=self.device))
+        m["lr"].append(lr)
+        return ro
+
+    def _flush_logs(self) -> dict:
+        """ppo_trainer.py:619-646 metric names (one host sync per log)."""
+        m = self._metrics
+        if not m.get("stats"):
+            return {}
+        st = torch.stack(m["stats"]).float()  # [n, epochs, mini, ga, 9]
+        flat = st.reshape(-1, 9)
+        kl = float(torch.stack(m["kl"]).mean())
+        nsr = float(torch.stack(m["non_score_reward"]).mean())
+        sc = float(torch.stack(m["scores"]).mean())
+        log = {
+            "objective/kl": kl,
+            "objective/entropy": float(torch.stack(m["entropy"]).mean()),
+            "objective/non_score_reward": nsr,
+            "objective/rlhf_reward": nsr + sc,
+            "objective/scores": sc,
+            "policy/approxkl_avg": float(flat[:, 4].mean()),
+            "policy/clipfrac_avg": float(flat[:, 2].mean()),
+            "loss/policy_avg": float(flat[:, 0].mean()),
+            "loss/value_avg": float(flat[:, 1].mean()),
+            "val/clipfrac_avg": float(flat[:, 3].mean()),
+            "policy/entropy_avg": float(flat[:, 8].mean()),
+            "val/ratio": float(flat[:, 5].mean()),
+            "val/ratio_var": float(flat[:, 5].var()) if flat.shape[0] > 1 else 0.0,
+            "val/num_eos_tokens": float(torch.stack(m["num_eos"]).float().mean()),
+            "lr": m["lr"][-1],
+            "episode": self.state.episode,
+            "step": self.state.global_step,
+        }
+        m.clear()
+        self.state.log_history.append(log)
+        return log
+
+    def train(self):
+        a = self.args
+        self.state.global_step = 0
+        self.state.episode = 0
+        self.state.max_steps = a.num_total_batches
+        log_every = int(a.logging_steps) if a.logging_steps >= 1 else \
+            max(1, math.ceil(a.num_total_batches * a.logging_steps))
+        t0 = time.time()
+        for _ in range(a.num_total_batches):
+            self.training_step()
+            if self.state.global_step % log_every == 0 or self.state.global_step == a.num_total_batches:
+                log = self._flush_logs()
+                log["eps"] = int(self.state.episode / max(time.time() - t0, 1e-9))
+                if self.rank == 0:
+                    print(log, flush=True)
+        return self.state

@@ -60,6 +60,34 @@ def test_grpo_config_bookkeeping():
     assert c.extra == {"some_unknown_field": 1}
 
 
+def test_ppo_config_bookkeeping():
+    """ppo_trainer.py:224-250 derived batch sizes and their errors."""
+    from swh_trl_amd.trainer import PPOConfig
+    from swh_trl_amd.trainer.ppo_trainer import fill_batch_sizes
+    c = fill_batch_sizes(PPOConfig(per_device_train_batch_size=4, gradient_accumulation_steps=2,
+                                   num_mini_batches=2, num_train_epochs=2), dataset_len=50, world_size=4)
+    assert (c.local_batch_size, c.micro_batch_size, c.batch_size) == (8, 16, 32)
+    assert (c.mini_batch_size, c.local_mini_batch_size) == (16, 4)
+    assert c.total_episodes == 100 and c.num_total_batches == 4  # ceil(100 / 32)
+    assert c.kl_estimator == "k1" and c.response_length == 53 and c.temperature == 0.7 and c.bf16
+    with pytest.raises(ValueError):
+        fill_batch_sizes(PPOConfig(per_device_train_batch_size=3, num_mini_batches=2), 10, 1)
+    with pytest.raises(ValueError):  # whitening needs >= 8 rows per rank mini-batch
+        fill_batch_sizes(PPOConfig(per_device_train_batch_size=4, whiten_rewards=True), 10, 1)
+
+
+def test_ppo_response_helpers_match_oracle():
+    """first_true_indices / truncate_response (utils.py:877-897, :1036-1056)."""
+    from swh_trl_amd.trainer.ppo_trainer import first_true_indices, truncate_response
+    g = torch.Generator().manual_seed(0)
+    r = torch.randint(0, 6, (9, 13), generator=g)
+    r[0] = 5  # no stop token at all
+    for stop in (0, 1, 3):
+        assert torch.equal(first_true_indices(r == stop), trl_ref.first_true_indices(r == stop))
+        assert torch.equal(truncate_response(stop, 4, r), trl_ref.truncate_response(stop, 4, r))
+    assert first_true_indices(torch.zeros(2, 7, dtype=torch.bool)).tolist() == [7, 7]
+
+
 def test_split_and_shuffle_dicts():
     d = {"x": torch.arange(12).reshape(6, 2), "y": torch.arange(6), "z": None}
     parts = U.split_tensor_dict(d, 3)

@@ -1,0 +1,202 @@
+"""PPOTrainer parity on the GPU (-m gpu): the rollout scoring, the PPO
+micro-batch loss/gradients and the update loop against the CPU restatement in
+oracle/ppo_step.py (transformers Qwen2 models in fp32 on the host, loaded
+with the engine's bf16 weights).  Parity for this path is unpinned by the
+reference's own tests; tolerances below are the bf16
+engine against an fp32 restatement."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+PAD, EOS = 0, 1
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available()
+    return torch.device("cuda:0")
+
+
+def _hf(m, seqcls: bool):
+    from transformers import Qwen2Config, Qwen2ForCausalLM, Qwen2ForSequenceClassification
+    c = m.cfg
+    hc = Qwen2Config(vocab_size=c.vocab_size, hidden_size=c.hidden_size, intermediate_size=c.intermediate_size,
+                     num_hidden_layers=c.num_hidden_layers, num_attention_heads=c.num_attention_heads,
+                     num_key_value_heads=c.num_key_value_heads, rope_theta=c.rope_theta, rms_norm_eps=c.rms_norm_eps,
+                     tie_word_embeddings=c.tie_word_embeddings, max_position_embeddings=c.max_position_embeddings,
+                     num_labels=1, pad_token_id=PAD)
+    hc._attn_implementation = "eager"
+    hf = (Qwen2ForSequenceClassification if seqcls else Qwen2ForCausalLM)(hc)
+    sd = {k: v.detach().float().cpu() for k, v in m.hf_state_dict().items()}
+    missing, _ = hf.load_state_dict(sd, strict=False)
+    assert not [k for k in missing if "rotary" not in k and k != "lm_head.weight"], missing
+    return hf.float().eval()
+
+
+def _trainer(dev, **kw):
+    from swh_trl_amd.engine import CausalLM, tiny_qwen2
+    from swh_trl_amd.trainer import PPOConfig, PPOTrainer
+    cfg = tiny_qwen2(512, 2)
+    policy = CausalLM(cfg, dev, seed=11, init_std=0.05)
+    with torch.no_grad():  # make the stop token likely, so rows end at different lengths
+        policy.p["embed"][EOS].mul_(6.0)
+    value = CausalLM(cfg, dev, head="score", seed=12, init_std=0.05)
+    reward = CausalLM(tiny_qwen2(512, 1), dev, head="score", seed=13, init_std=0.05)
+    g = torch.Generator().manual_seed(3)
+    ds = []
+    for i in range(16):
+        n = 6 + i % 5  # ragged prompts -> left padding
+        ds.append({"input_ids": torch.randint(2, 512, (n,), generator=g).tolist()})
+    a = dict(per_device_train_batch_size=4, gradient_accumulation_steps=2, num_mini_batches=2, num_ppo_epochs=2,
+             response_length=12, stop_token_id=EOS, temperature=0.7, learning_rate=1e-3, total_episodes=16,
+             pad_token_id=PAD, eos_token_id=EOS, seed=5)
+    a.update(kw)
+    return PPOTrainer(PPOConfig(**a), None, policy, None, reward, ds, value), ds
+
+
+def _cpu(d):
+    return {k: (v.detach().cpu() if torch.is_tensor(v) else v) for k, v in d.items()}
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(kl_estimator="k3", whiten_rewards=True, missing_eos_penalty=1.0,
+                                               gradient_accumulation_steps=4, num_mini_batches=1),
+                                dict(stop_token_id=None)])
+def test_ppo_rollout_matches_oracle(dev, kw):
+    from oracle import ppo_step
+    tr, ds = _trainer(dev, **kw)
+    a = tr.args
+    queries = tr._queries(ds[:a.local_batch_size])
+    responses, logprobs = tr.generate(queries)
+    assert responses.shape[1] <= a.response_length
+    ro = tr.rollout_from(queries, responses, logprobs)
+    pol, ref = _hf(tr.policy_model, False), _hf(tr.ref_model, False)
+    val, rm = _hf(tr.value_model, True), _hf(tr.reward_model, True)
+    q, r = queries.cpu(), responses.cpu()
+    o = ppo_step.rollout_scores(pol, ref, val, rm, q, r, logprobs.cpu().float(), pad_token_id=PAD,
+                                stop_token_id=tr.stop_token_id, eos_token_id=EOS, temperature=a.temperature,
+                                kl_coef=a.kl_coef, kl_estimator=a.kl_estimator, whiten_rewards=a.whiten_rewards,
+                                missing_eos_penalty=a.missing_eos_penalty, gamma=a.gamma, lam=a.lam)
+    mine = _cpu(ro)
+    if tr.stop_token_id is not None:  # ragged ends exercised: some rows stopped early
+        assert (mine["sequence_lengths"] < responses.shape[1] - 1).any()
+    for k in ("padding_mask", "padding_mask_p1", "sequence_lengths", "postprocessed_responses"):
+        assert torch.equal(mine[k], o[k]), k
+    keep = ~o["padding_mask"]
+    # generation log-probs (decode kernels, bf16) vs the fp32 processed scores
+    gl = ppo_step.generation_logprobs(pol, q, r, PAD, a.temperature)
+    assert (logprobs.cpu()[keep] - gl[keep]).abs().max() < 6e-2
+    # model forwards: bf16 engine vs fp32 transformers
+    assert (mine["ref_logprobs"][keep] - o["ref_logprobs"][keep]).abs().max() < 6e-2
+    keep1 = ~o["padding_mask_p1"]
+    assert (mine["values"].float()[keep1] - o["values"][keep1]).abs().max() < 3e-2
+    assert (mine["rm_scores"].float() - (o["scores"] + (0 if a.missing_eos_penalty is None else
+            a.missing_eos_penalty * ~torch.any(o["postprocessed_responses"] == EOS, -1)))).abs().max() < 3e-2
+    # the arithmetic after the forwards, on the engine's own forward outputs: fp32-tight
+    oa = ppo_step.rollout_arith(logprobs.cpu().float(), mine["ref_logprobs"], mine["values"], mine["rm_scores"],
+                                mine["postprocessed_responses"], pad_token_id=PAD, eos_token_id=EOS,
+                                kl_coef=a.kl_coef, kl_estimator=a.kl_estimator, whiten_rewards=a.whiten_rewards,
+                                missing_eos_penalty=a.missing_eos_penalty, gamma=a.gamma, lam=a.lam)
+    for k in ("logprobs", "scores", "kl", "non_score_reward", "rewards", "returns", "advantages"):
+        torch.testing.assert_close(mine[k].float(), oa[k].float(), rtol=1e-4, atol=1e-4, msg=k)
+
+
+def test_ppo_micro_batch_gradients_match_oracle(dev):
+    from oracle import ppo_step
+    tr, ds = _trainer(dev, gradient_accumulation_steps=1, num_mini_batches=1, per_device_train_batch_size=8)
+    a = tr.args
+    queries = tr._queries(ds[:a.local_batch_size])
+    responses, logprobs = tr.generate(queries)
+    ro = tr.rollout_from(queries, responses, logprobs)
+    pol, val = _hf(tr.policy_model, False), _hf(tr.value_model, True)
+    inds = torch.tensor([5, 0, 3, 6, 1, 2, 7, 4])
+    tr.policy_model.zero_grad()
+    tr.value_model.zero_grad()
+    st = tr._micro_step(ro, inds.to(dev)).cpu()
+    oro = _cpu(ro)
+    oro["values"] = oro["values"].float()
+    loss, ost = ppo_step.micro_batch_loss(pol, val, oro, inds, context_length=queries.shape[1], pad_token_id=PAD,
+                                          temperature=a.temperature, cliprange=a.cliprange,
+                                          cliprange_value=a.cliprange_value, vf_coef=a.vf_coef)
+    loss.backward()
+    for i, k in ((0, "pg_loss"), (1, "vf_loss"), (4, "approxkl"), (5, "ratio")):
+        assert abs(float(st[i]) - ost[k]) < 2e-2 + 2e-2 * abs(ost[k]), (k, float(st[i]), ost[k])
+    assert abs(float(st[8]) - ost["entropy"]) < 2e-2 * max(1.0, abs(ost["entropy"]))
+
+    def grads(m):
+        saved = m.flat.clone()
+        m.flat.copy_(m.grad)
+        g = {k: v.float().cpu().clone() for k, v in m.hf_state_dict().items()}
+        m.flat.copy_(saved)
+        return g
+
+    gp, gv = grads(tr.policy_model), grads(tr.value_model)
+    rp, rv = dict(pol.named_parameters()), dict(val.named_parameters())
+    for name in ("model.layers.0.self_attn.q_proj.weight", "model.layers.1.mlp.down_proj.weight",
+                 "model.embed_tokens.weight", "model.norm.weight"):
+        rel = (gp[name] - rp[name].grad).norm() / rp[name].grad.norm().clamp_min(1e-12)
+        assert rel < 0.06, (name, float(rel))
+    for name in ("score.weight", "model.layers.1.self_attn.o_proj.weight", "model.layers.0.mlp.gate_proj.weight"):
+        rel = (gv[name] - rv[name].grad).norm() / rv[name].grad.norm().clamp_min(1e-12)
+        assert rel < 0.06, (name, float(rel))
+
+
+def test_ppo_update_schedule_matches_oracle(dev):
+    """Epochs x mini-batches x GA with one AdamW step per mini-batch: the engine's
+    fp32 master weights after a full update track the fp32 oracle's (the first
+    Adam steps move every weight by ~lr * sign(g): compare update directions)."""
+    from oracle import ppo_step
+    tr, ds = _trainer(dev, learning_rate=1e-4)
+    a = tr.args
+    queries = tr._queries(ds[:a.local_batch_size])
+    responses, logprobs = tr.generate(queries)
+    ro = tr.rollout_from(queries, responses, logprobs)
+    pol, val = _hf(tr.policy_model, False), _hf(tr.value_model, True)
+    p0 = {k: v.detach().clone() for k, v in pol.named_parameters()}
+    v0 = {k: v.detach().clone() for k, v in val.named_parameters()}
+    perms = [torch.randperm(a.local_batch_size, generator=torch.Generator().manual_seed(e)).tolist()
+             for e in range(a.num_ppo_epochs)]
+    mp0, mv0 = tr.opt_policy.master.clone(), tr.opt_value.master.clone()
+    tr.ppo_update(ro, a.learning_rate, permutations=perms)
+    oro = _cpu(ro)
+    oro["values"] = oro["values"].float()
+    opt = torch.optim.AdamW(list(pol.parameters()) + list(val.parameters()), lr=a.learning_rate, betas=(0.9, 0.999),
+                            eps=1e-8, weight_decay=0.0)
+    ppo_step.ppo_update(pol, val, opt, oro, perms, local_mini_batch_size=a.local_mini_batch_size,
+                        per_device_train_batch_size=a.per_device_train_batch_size,
+                        gradient_accumulation_steps=a.gradient_accumulation_steps, context_length=queries.shape[1],
+                        pad_token_id=PAD, temperature=a.temperature, cliprange=a.cliprange,
+                        cliprange_value=a.cliprange_value, vf_coef=a.vf_coef)
+
+    def mine(m, master, master0, name):
+        off, shape = m.layout[name]
+        n = 1
+        for d in shape:
+            n *= d
+        return (master[off:off + n] - master0[off:off + n]).view(shape).cpu()
+
+    rp, rv = dict(pol.named_parameters()), dict(val.named_parameters())
+    pairs = [
+        (mine(tr.policy_model, tr.opt_policy.master, mp0, "l0.qkv_w"),
+         torch.cat([rp[f"model.layers.0.self_attn.{n}_proj.weight"].detach() -
+                    p0[f"model.layers.0.self_attn.{n}_proj.weight"] for n in "qkv"])),
+        (mine(tr.policy_model, tr.opt_policy.master, mp0, "l1.down_w"),
+         rp["model.layers.1.mlp.down_proj.weight"].detach() - p0["model.layers.1.mlp.down_proj.weight"]),
+        (mine(tr.value_model, tr.opt_value.master, mv0, "score"), rv["score.weight"].detach() - v0["score.weight"]),
+    ]
+    for dm, dr in pairs:
+        cos = torch.nn.functional.cosine_similarity(dm.flatten(), dr.flatten(), 0)
+        assert cos > 0.9, float(cos)
+
+
+def test_ppo_trainer_train_runs(dev):
+    tr, _ = _trainer(dev)
+    before = tr.policy_model.flat.clone()
+    vbefore = tr.value_model.flat.clone()
+    state = tr.train()
+    assert state.global_step == tr.args.num_total_batches == 2
+    assert not torch.equal(before, tr.policy_model.flat)
+    assert not torch.equal(vbefore, tr.value_model.flat)
+    log = state.log_history[-1]
+    for k in ("objective/kl", "loss/policy_avg", "loss/value_avg", "policy/approxkl_avg", "val/ratio"):
+        assert log[k] == log[k], k  # finite
