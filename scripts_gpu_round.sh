@@ -22,6 +22,7 @@ for step in "$@"; do
     lat) run lat 120 python tools/latency_probe.py && HIP_FORCE_DEV_KERNARG=1 run lat1 120 python tools/latency_probe.py && HIP_FORCE_DEV_KERNARG=0 run lat0 120 python tools/latency_probe.py ;;
     profdec) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null && run profdec 400 rocprofv3 --kernel-trace --stats -d gpurun_out/profdec -o run --output-format csv -- python3 tools/bench_decode.py ;;
     ppo) run ppo 600 python -m pytest tests/test_ppo_gpu.py -q -m gpu -x ;;
+    ppob) run ppob 600 python tools/bench_ppo.py ;;
     engine) run engine 600 python -m pytest tests/test_engine_gpu.py -q -m gpu -x ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py --steps 3 --warmup 2 ;;

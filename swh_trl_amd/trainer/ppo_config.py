@@ -72,6 +72,8 @@ class PPOConfig:
     ds3_gather_for_generation: bool = True
     # engine knobs (not in the reference)
     decode_check_every: int = 8            # host check of "all finished" every k decode steps (0 = never)
+    fuse_micro_batches: bool = True        # a mini-batch's GA micro-batches as one forward/backward
+    fuse_token_budget: int = 1 << 16       # max rows * (query + response) tokens per fused pass
     extra: dict = field(default_factory=dict)
 
     def __init__(self, **kwargs):

@@ -285,9 +285,14 @@ class PPOTrainer:
                 "postprocessed_responses": post}
 
     # ------------------------------------------------------------------ PPO update (ppo_trainer.py:537-617)
-    def _micro_step(self, ro: dict, inds: torch.Tensor) -> torch.Tensor:
-        """One micro-batch: policy + value forwards, fused loss fwd/bwd, backward
-        scaled by 1/GA (accelerate's accumulate); returns stats f32[8] + entropy."""
+    def _micro_step(self, ro: dict, inds: torch.Tensor, n_micro: int = 1) -> torch.Tensor:
+        """`n_micro` micro-batches of equal size (rows `inds`, micro j = the j-th
+        slice) in ONE policy + value forward/backward: the fused loss kernel runs
+        per micro-batch slice (each keeps its own masked means, as the
+        reference's separate passes), every micro's gradient is scaled by 1/GA
+        (accelerate's accumulate) — the summed gradient equals GA separate
+        backward passes.  Returns stats [n_micro, 9] = kernel stats f32[8] +
+        mean entropy."""
         a = self.args
         P = ro["queries"].shape[1]
         T = ro["responses"].shape[1]
@@ -302,17 +307,23 @@ class PPOTrainer:
         vpred = self.value_model.scores(hv[:, P - 1:P + T - 1])
         nl = torch.masked_fill(new_logprobs.detach(), pm, INVALID_LOGPROB)
         vp = torch.masked_fill(vpred.detach().float(), pm1, 0)
-        loss, dnl, dvp, stats = ops.ppo_loss_fwd_bwd(nl, ro["logprobs"][inds], ro["advantages"][inds], vp,
-                                                     ro["values"][inds].float(), ro["returns"][inds], pm, pm1,
-                                                     a.cliprange, a.cliprange_value, a.vf_coef)
+        old_lp, adv = ro["logprobs"][inds], ro["advantages"][inds]
+        old_v, ret = ro["values"][inds].float(), ro["returns"][inds]
         ga = a.gradient_accumulation_steps
+        R = inds.numel() // n_micro
+        dnl, dvp = torch.empty_like(nl), torch.empty_like(vp)
+        out = torch.empty(n_micro, 9, device=self.device, dtype=torch.float32)
+        for j in range(n_micro):
+            sl = slice(j * R, (j + 1) * R)
+            _, d1, d2, stats = ops.ppo_loss_fwd_bwd(nl[sl], old_lp[sl], adv[sl], vp[sl], old_v[sl], ret[sl], pm[sl],
+                                                    pm1[sl], a.cliprange, a.cliprange_value, a.vf_coef)
+            dnl[sl], dvp[sl] = d1, d2
+            out[j, :8] = stats
+            out[j, 8] = entropy[sl].detach().float().mean()
         # masked_fill blocks the gradient at padded positions (the kernel's d is 0 there too)
         dnl = torch.masked_fill(dnl, pm, 0.0) / ga
         dvp = torch.masked_fill(dvp, pm1, 0.0) / ga
         torch.autograd.backward([new_logprobs, vpred], [dnl.to(new_logprobs.dtype), dvp.to(vpred.dtype)])
-        out = torch.empty(9, device=self.device, dtype=torch.float32)
-        out[:8] = stats
-        out[8] = entropy.float().mean()
         return out
 
     def _optimizer_step(self, lr: float):
@@ -337,8 +348,13 @@ class PPOTrainer:
             b_inds = torch.as_tensor(np.asarray(b_inds), device=self.device, dtype=torch.long)
             for mi, mb0 in enumerate(range(0, a.local_batch_size, a.local_mini_batch_size)):
                 mini = b_inds[mb0:mb0 + a.local_mini_batch_size]
-                for gi, u0 in enumerate(range(0, a.local_mini_batch_size, a.per_device_train_batch_size)):
-                    stats[ep, mi, gi] = self._micro_step(ro, mini[u0:u0 + a.per_device_train_batch_size])
+                mbs = a.per_device_train_batch_size
+                n_micro = a.local_mini_batch_size // mbs
+                if a.fuse_micro_batches and mini.numel() * ro["query_responses"].shape[1] <= a.fuse_token_budget:
+                    stats[ep, mi, :n_micro] = self._micro_step(ro, mini[:n_micro * mbs], n_micro)
+                else:  # the reference schedule, one pass per micro-batch
+                    for gi in range(n_micro):
+                        stats[ep, mi, gi] = self._micro_step(ro, mini[gi * mbs:(gi + 1) * mbs])[0]
                 self._optimizer_step(lr)
         return stats
 

@@ -112,7 +112,7 @@ def test_ppo_micro_batch_gradients_match_oracle(dev):
     inds = torch.tensor([5, 0, 3, 6, 1, 2, 7, 4])
     tr.policy_model.zero_grad()
     tr.value_model.zero_grad()
-    st = tr._micro_step(ro, inds.to(dev)).cpu()
+    st = tr._micro_step(ro, inds.to(dev))[0].cpu()
     oro = _cpu(ro)
     oro["values"] = oro["values"].float()
     loss, ost = ppo_step.micro_batch_loss(pol, val, oro, inds, context_length=queries.shape[1], pad_token_id=PAD,
@@ -200,3 +200,25 @@ def test_ppo_trainer_train_runs(dev):
     log = state.log_history[-1]
     for k in ("objective/kl", "loss/policy_avg", "loss/value_avg", "policy/approxkl_avg", "val/ratio"):
         assert log[k] == log[k], k  # finite
+
+
+def test_ppo_fused_micro_batches_equal_separate(dev):
+    """A mini-batch's GA micro-batches in one fused pass give the gradient of GA
+    separate passes (each micro keeps its own masked means)."""
+    tr, ds = _trainer(dev, gradient_accumulation_steps=2, num_mini_batches=1)
+    a = tr.args
+    queries = tr._queries(ds[:a.local_batch_size])
+    responses, logprobs = tr.generate(queries)
+    ro = tr.rollout_from(queries, responses, logprobs)
+    inds = torch.tensor([6, 2, 7, 1, 0, 4, 3, 5], device=dev)
+    tr.policy_model.zero_grad()
+    tr.value_model.zero_grad()
+    st_f = tr._micro_step(ro, inds, 2)
+    gp_f, gv_f = tr.policy_model.grad.float().clone(), tr.value_model.grad.float().clone()
+    tr.policy_model.zero_grad()
+    tr.value_model.zero_grad()
+    st_s = torch.cat([tr._micro_step(ro, inds[:4]), tr._micro_step(ro, inds[4:])])
+    gp_s, gv_s = tr.policy_model.grad.float(), tr.value_model.grad.float()
+    torch.testing.assert_close(st_f, st_s, rtol=2e-3, atol=2e-4)
+    assert float((gp_f - gp_s).norm() / gp_s.norm()) < 2e-2
+    assert float((gv_f - gv_s).norm() / gv_s.norm()) < 2e-2
