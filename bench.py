@@ -82,6 +82,21 @@ def cpu_baseline(steps_note: str) -> dict:
                        f"{G} samples; {steps_note}")}
 
 
+PMC_FILE = os.path.join(ROOT, "profiles", "r1_v2_pmc_decode.json")
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed PMC passes
+    (tools/pmc_summary.py: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE over
+    tools/bench_decode.py, MI355X_MICROARCH.md §HBM corrections), or None."""
+    try:
+        with open(PMC_FILE) as f:
+            k = json.load(f)["kernels"].get(kernel)
+        return None if k is None else k["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -155,7 +170,9 @@ def main():
     achieved = dom["bytes_per_launch"] / (dom["avg_us"] * 1e-6) / 1e9
     roof = {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "avg_us": round(dom["avg_us"], 2), "bytes_per_launch": dom["bytes_per_launch"], "traffic": None,
+            "avg_us": round(dom["avg_us"], 2), "bytes_per_launch": dom["bytes_per_launch"],
+            "traffic": pmc_traffic(dom_name), "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)",
+            "traffic_source": os.path.relpath(PMC_FILE, ROOT),
             "all_kernels": {k: {"avg_us": round(v["avg_us"], 2), "launches_per_step": v["per_step"],
                                 "ms_per_step": round(v["avg_us"] * v["per_step"] / 1000.0, 2),
                                 "GB/s": round(v["bytes_per_launch"] / (v["avg_us"] * 1e-6) / 1e9, 1)}
