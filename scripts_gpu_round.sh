@@ -16,6 +16,8 @@ for step in "$@"; do
     kern) run kern 600 python -m pytest tests/test_kernels_gpu.py -q -m gpu ;;
     kernx) run kernx 600 python -m pytest tests/test_kernels_gpu.py -q -m gpu -x ;;
     dec) run dec 300 python tools/bench_decode.py ;;
+    ku) run ku 400 python tools/bench_decode.py --ku ;;
+    dual) run dual 300 python tools/bench_decode.py --dual ;;
     sweep) run sweep 300 python tools/bench_decode.py --sweep ;;
     probe) run probe 300 python tools/gemm_probe.py ;;
     btrain) run btrain 600 python tools/bench_train.py ;;

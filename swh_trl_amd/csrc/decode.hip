@@ -118,8 +118,8 @@ __host__ __device__ inline GemmLds gemm_lds(int cb, int mr, int nw, int krmax, i
 // last arriver sums the S slabs in fixed order (deterministic, placement-
 // independent — MI355X_MICROARCH.md §Workgroup dispatch) and runs the epilogue.
 
-template <int CB, int MS, int NM, int EPI, bool BIAS>
-__global__ __launch_bounds__(512) void decode_gemm_kernel(
+template <int CB, int MS, int NM, int EPI, bool BIAS, int MAXT>
+__global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
     const uint16_t *__restrict__ x, const uint16_t *__restrict__ w, int M, int N, int K,
     const uint16_t *__restrict__ norm_w, float eps, const float *__restrict__ ss_in,
     const uint16_t *__restrict__ bias, uint16_t *__restrict__ res, float *__restrict__ ss_out,
@@ -1031,7 +1031,9 @@ int cu_count() {
     return n;
 }
 
-inline int gemm_waves(int ms) { return ms == 4 ? 8 : 4; }
+// 8 waves in every geometry: more k-steps in flight per CU (down 14.9 -> 11.5 us,
+// qkv 7.0 -> 6.3 us against 4 waves for 16- and 32-row tiles; tools/bench_decode.py --ku)
+inline int gemm_waves(int) { return 8; }
 
 // Modelled launch time (us) of one geometry — measured shape of the cost on
 // MI355X (tools/gemm_probe.py, tools/bench_decode.py --sweep): a fixed
@@ -1096,6 +1098,12 @@ GemmCfg pick_cfg(int64_t M, int64_t wcols, int64_t K, bool silu, int nm) {
         }
     }
     if (!best.persist) best.gx = (int)(8 * ((M + 16 * best.ms - 1) / (16 * best.ms)) * ((wcols / (16 * best.cb) + 7) / 8));
+    if (const char *e = getenv("SWH_GEMM_NW")) {  // tuning override: waves per workgroup (16: cb == 1 only)
+        const int v = atoi(e);
+        if ((v == 4 || v == 8 || (v == 16 && best.cb == 1)) && gemm_cost(GemmCfg{best.ms, best.cb, v, best.s, best.gx, best.persist}, M, wcols, K,
+                                            nm) < 1e29)
+            best.nw = v;
+    }
     return best;
 }
 
@@ -1105,18 +1113,18 @@ int64_t slab_bytes(const GemmCfg &c, int64_t M, int64_t wcols) {
     return nmt * wcols * c.s * MR * (int64_t)sizeof(float);  // tiles * NB == nmt * wcols
 }
 
-template <int CB, int MS, int NM, int EPI, bool BIAS>
+template <int CB, int MS, int NM, int EPI, bool BIAS, int MAXT>
 int launch_gemm(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W, int m,
                 int n, int k, const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs, uint16_t *R,
                 float *ss_out, uint16_t *Y, int ld, float *slab, int *ctr) {
     static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in once per kernel
     if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&decode_gemm_kernel<CB, MS, NM, EPI, BIAS>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&decode_gemm_kernel<CB, MS, NM, EPI, BIAS, MAXT>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
             return SWH_E_LAUNCH;
         attr = true;
     }
-    decode_gemm_kernel<CB, MS, NM, EPI, BIAS><<<grid, 64u * c.nw, lds, s>>>(
+    decode_gemm_kernel<CB, MS, NM, EPI, BIAS, MAXT><<<grid, 64u * c.nw, lds, s>>>(
         X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr, c.persist ? 1 : 0);
     return launch_status();
 }
@@ -1126,9 +1134,12 @@ int launch_gemm_cb(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const
                    int m, int n, int k, const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs,
                    uint16_t *R, float *ss_out, uint16_t *Y, int ld, float *slab, int *ctr) {
     switch (c.cb) {
-    case 1: return launch_gemm<1, MS, NM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
-    case 2: return launch_gemm<2, MS, NM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
-    default: return launch_gemm<4, MS, NM, EPI, BIAS>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
+    case 1:
+        if (c.nw > 8)  // 16 waves: one-column-block tiles over long K
+            return launch_gemm<1, MS, NM, EPI, BIAS, 1024>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
+        return launch_gemm<1, MS, NM, EPI, BIAS, 512>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
+    case 2: return launch_gemm<2, MS, NM, EPI, BIAS, 512>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
+    default: return launch_gemm<4, MS, NM, EPI, BIAS, 512>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
     }
 }
 

@@ -674,13 +674,18 @@ def test_rmsnorm_statistic_handoff(ops, dev):
     assert (y1 != y0).float().mean().item() < 0.01
 
 
-@pytest.mark.parametrize("cfg", ["1,1,1", "2,1,1", "4,1,1", "1,2,2", "2,4,1", "4,4,3", "1,1,3", "2,2,2", "4,2,1,1",
-                                 "4,4,1,1"])
-def test_decode_gemm_launch_configs(ops, dev, cfg, monkeypatch):
-    """Every (row blocks, column blocks, K split[, persistent]) geometry
-    computes the same GEMM: normed + bias, residual + statistic, SiLU gate."""
+@pytest.mark.parametrize("cfg,nw", [("1,1,1", None), ("2,1,1", None), ("4,1,1", None), ("1,2,2", None),
+                                    ("2,4,1", None), ("4,4,3", None), ("1,1,3", None), ("2,2,2", None),
+                                    ("4,2,1,1", None), ("4,4,1,1", None), ("1,1,1", "16"), ("2,1,2", "16"),
+                                    ("1,1,1", "4"), ("2,2,1", "4"), ("4,1,3", "16")])
+def test_decode_gemm_launch_configs(ops, dev, cfg, nw, monkeypatch):
+    """Every (row blocks, column blocks, K split[, persistent]) geometry and
+    wave count computes the same GEMM: normed + bias, residual + statistic,
+    SiLU gate."""
     from swh_trl_amd import nn_ops
     monkeypatch.setenv("SWH_GEMM_CFG", cfg)
+    if nw is not None:
+        monkeypatch.setenv("SWH_GEMM_NW", nw)
     g = _gen(34)
     M, H, I = 40, 896, 1024
     s = torch.randn(M, H, generator=g).to(torch.bfloat16).to(dev)

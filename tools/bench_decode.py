@@ -69,12 +69,110 @@ def sweep(eng, m):
     os.environ.pop("SWH_GEMM_CFG", None)
 
 
+def ku_sweep(eng, m):
+    """o / down / qkv under waves per workgroup (SWH_GEMM_NW) x geometry."""
+    from swh_trl_amd import nn_ops
+    c, p = eng.cfg, m.p
+    ss, L = eng.ss, c.num_hidden_layers
+    shapes = {
+        "o": lambda i: nn_ops.decode_gemm(eng.att, p[f"l{i}.o_w"], residual=eng.s, ss_out=ss),
+        "down": lambda i: nn_ops.decode_gemm(eng.act, p[f"l{i}.down_w"], residual=eng.s, ss_out=ss),
+        "qkv": lambda i: nn_ops.decode_gemm(eng.s, eng._normed(f"l{i}.qkv_w", f"l{i}.ln_in")[0],
+                                            bias=p.get(f"l{i}.qkv_b"), y=eng.qkv, ss_in=ss),
+    }
+
+    def t(fn):
+        fn(0)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for i in range(L):
+                fn(i)
+        g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(3):
+            g.replay()
+        e1.record()
+        e1.synchronize()
+        return 1000.0 * e0.elapsed_time(e1) / (3 * L)
+
+    print("cfg          nw " + " ".join(f"{k:>9s}" for k in shapes), flush=True)
+    for cf in (None, "1,1,1", "1,1,2", "2,1,1", "2,1,2", "4,1,2", "4,1,4"):
+        for ku in ("",):
+            for nw in ("4", "8", "16"):
+                for k, v in (("SWH_GEMM_CFG", cf), ("SWH_GEMM_NW", nw)):
+                    if v is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
+                row = []
+                for name, fn in shapes.items():
+                    try:
+                        row.append(t(fn))
+                    except Exception:
+                        row.append(float("nan"))
+                print(f"{str(cf):12s} {nw:>2s} " + " ".join(f"{v:9.2f}" for v in row), flush=True)
+    for k in ("SWH_GEMM_CFG", "SWH_GEMM_NW"):
+        os.environ.pop(k, None)
+
+
+def dual(eng, m):
+    """Two half-batch chains on two streams of one graph vs one full-batch chain:
+    does running independent decode kernels concurrently hide their latency?"""
+    from swh_trl_amd import nn_ops
+    c, p = eng.cfg, m.p
+    eps, ss, B = c.rms_norm_eps, eng.ss, eng.B
+    L, h = c.num_hidden_layers, eng.B // 2
+
+    def gu(i, r0, r1):
+        w = eng._normed(f"l{i}.gu_w", f"l{i}.ln_post")[0]
+        nn_ops.decode_gemm(eng.s[r0:r1], w, silu=True, y=eng.act[r0:r1], ss_in=ss[r0:r1])
+
+    def dn(i, r0, r1):
+        nn_ops.decode_gemm(eng.act[r0:r1], p[f"l{i}.down_w"], residual=eng.s[r0:r1], ss_out=ss[r0:r1])
+
+    def chain(r0, r1):
+        for i in range(L):
+            gu(i, r0, r1)
+            dn(i, r0, r1)
+
+    side = torch.cuda.Stream()
+
+    def both():
+        main = torch.cuda.current_stream()
+        side.wait_stream(main)
+        chain(0, h)
+        with torch.cuda.stream(side):
+            chain(h, B)
+        main.wait_stream(side)
+
+    for name, fn in (("full chain  (M=64)", lambda: chain(0, B)), ("half chain  (M=32)", lambda: chain(0, h)),
+                     ("two halves (2 streams)", both)):
+        fn()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            fn()
+        g.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            g.replay()
+        e1.record()
+        e1.synchronize()
+        print(f"{name:24s} {1000 * e0.elapsed_time(e1) / 5 / L:8.2f} us per layer (gate_up + down)", flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--step", type=int, default=128)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--gemm-cfg", default=None)
     ap.add_argument("--sweep", action="store_true", help="time the GEMM shapes under several launch geometries")
+    ap.add_argument("--dual", action="store_true", help="two half-batch chains on two streams vs one chain")
+    ap.add_argument("--ku", action="store_true", help="weight-round depth x waves x geometry sweep (o, down, qkv)")
     args = ap.parse_args()
     if args.gemm_cfg:
         os.environ["SWH_GEMM_CFG"] = args.gemm_cfg
@@ -95,6 +193,12 @@ def main():
     print(f"[bench_decode] setup {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
     if args.sweep:
         sweep(eng, m)
+        return
+    if args.dual:
+        dual(eng, m)
+        return
+    if args.ku:
+        ku_sweep(eng, m)
         return
     res = eng.kernel_timings(args.step)
     tot = 0.0
