@@ -191,9 +191,20 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
     issue(ksw0);
     // ---- (b) RMSNorm partial sums and the norm-weight slice (L2)
     const int nc = K / 64;
-    const bool use_ss = NM && ss_in && MR * nc <= 4 * NT;
+    // folded norm, one column block: the row statistic only scales the epilogue;
+    // 8 lanes per row sum the row's chunk partials in registers (no LDS pass)
+    const bool late_rstd = NM == 2 && !persist && ss_in && MR * 8 <= NT && nc <= 64;
+    const bool use_ss = NM && ss_in && MR * nc <= 4 * NT && !late_rstd;
     float4 ssv[4];
+    float4 ss8[8];
     uint4 nwv[2];
+    if (late_rstd) {
+        const int r = min(m0 + (tid >> 3), M - 1), sub = tid & 7;
+        const float4 *row = reinterpret_cast<const float4 *>(ss_in + (int64_t)r * (K / 16));
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (sub + 8 * j < nc) ss8[j] = row[sub + 8 * j];
+    }
     if constexpr (NM != 0) {
         if (use_ss) {
 #pragma unroll
@@ -243,7 +254,17 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
     SWH_GEMM_TRACE(1);
 
     // ---- (d) row statistic and norm weights into LDS
-    if constexpr (NM != 0) {
+    if (late_rstd) {  // read by the epilogue only, behind the merge barriers
+        const int r = tid >> 3, sub = tid & 7;
+        float v = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (sub + 8 * j < nc) v += ((ss8[j].x + ss8[j].y) + ss8[j].z) + ss8[j].w;
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        if (r < MR && sub == 0) rstd_s[r] = rsqrtf(v / (float)K + eps);
+    } else if constexpr (NM != 0) {
         if (use_ss) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
