@@ -94,10 +94,11 @@ def load() -> C.CDLL:
         return _lib
     with _lock:
         if _lib is None:
-            if not os.path.exists(LIB_PATH):
-                raise RuntimeError(f"{LIB_PATH} is missing: build it with `python swh_trl_amd/build.py` "
+            path = os.environ.get("SWH_LIB_PATH", LIB_PATH)  # A/B timing of two builds (tools only)
+            if not os.path.exists(path):
+                raise RuntimeError(f"{path} is missing: build it with `python swh_trl_amd/build.py` "
                                    "(the swh_trl_amd ops have no CPU fallback)")
-            lib = C.CDLL(LIB_PATH)
+            lib = C.CDLL(path)
             for name, (res, args) in SIGNATURES.items():
                 fn = getattr(lib, name)
                 fn.restype = res

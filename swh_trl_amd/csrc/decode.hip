@@ -89,13 +89,16 @@ struct GemmLds {
     int64_t nw_off, ss_off, body_off, xs_bytes, slots_off, total;
 };
 // nm: 0 = plain X, 1 = RMSNorm applied to the X image, 2 = rstd row scale in the epilogue
-__host__ __device__ inline GemmLds gemm_lds(int cb, int mr, int nw, int krmax, int K, int nm, bool persist) {
+// cb: the tile's 16-column blocks; wn: column groups of waves (nw / wn waves split K in each)
+__host__ __device__ inline GemmLds gemm_lds(int cb, int mr, int nw, int krmax, int K, int nm, bool persist,
+                                            int wn = 1) {
     GemmLds L;
     L.nw_off = 512;
     L.ss_off = L.nw_off + (nm == 1 ? (int64_t)krmax * 4 : 0);  // norm weights as f32
     L.body_off = L.ss_off + (nm ? ((int64_t)mr * (K / 64) * 4 + 15) / 16 * 16 : 0);  // partials beside the DMA'd image
     L.xs_bytes = (int64_t)mr * (krmax * 2 + 16);
-    const int64_t slots = (int64_t)(nw > 1 ? nw / 2 : 1) * 16 * cb * (mr + 4) * 4;  // [NW/2][NB][MR+4]
+    const int wk = nw / wn;
+    const int64_t slots = (int64_t)(wk > 1 ? wk / 2 : 1) * 16 * cb * (mr + 4) * 4;  // [WK/2][NB][MR+4]
     L.slots_off = L.body_off + (persist ? L.xs_bytes : 0);
     int64_t end = L.body_off + L.xs_bytes;
     if (L.slots_off + slots > end) end = L.slots_off + slots;
@@ -123,14 +126,18 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
     const uint16_t *__restrict__ x, const uint16_t *__restrict__ w, int M, int N, int K,
     const uint16_t *__restrict__ norm_w, float eps, const float *__restrict__ ss_in,
     const uint16_t *__restrict__ bias, uint16_t *__restrict__ res, float *__restrict__ ss_out,
-    uint16_t *__restrict__ y, int ldy, float *__restrict__ slabs, int *__restrict__ counters, int persist) {
+    uint16_t *__restrict__ y, int ldy, float *__restrict__ slabs, int *__restrict__ counters, int persist,
+    int wn) {
+    // a wave computes NB = 16 CB columns; the WN column groups of NW / WN waves each
+    // make a tile of NBT = WN NB columns (the waves of a group split K)
     constexpr int NB = 16 * CB, MR = 16 * MS, LDR = MR + 4;  // merge slots column-major: b128 parks
     constexpr int kU = 4;                                     // k-steps whose loads are issued together
-    constexpr int G8 = (EPI == EPI_SILU) ? CB : NB / 8;  // 8-column output groups per row
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, NT = blockDim.x, NW = NT >> 6;
+    const int WN = wn, NBT = NB * WN, WK = NW / WN, cg = wid / WK, kw = wid - cg * WK;
+    const int G8 = (EPI == EPI_SILU) ? CB * WN : NBT / 8;  // 8-column output groups per row
     const int S = gridDim.z, sidx = blockIdx.z;
-    const int ncb = (EPI == EPI_SILU) ? N / (NB / 2) : N / NB;
+    const int ncb = (EPI == EPI_SILU) ? N / (NBT / 2) : N / NBT;
     const int nmt = (M + MR - 1) / MR;
     // ---- tile of this workgroup
     int cb_first, cb_step, mt;
@@ -149,7 +156,7 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
     const int m0 = mt * MR;
     const int KS = K / 32, kb0 = (int)((int64_t)KS * sidx / S), kb1 = (int)((int64_t)KS * (sidx + 1) / S);
     const int Kr = (kb1 - kb0) * 32, k0 = kb0 * 32, RS = Kr * 2 + 16;
-    const GemmLds L = gemm_lds(CB, MR, NW, (KS + S - 1) / S * 32, K, NM, persist != 0);
+    const GemmLds L = gemm_lds(CB * WN, MR, NW, (KS + S - 1) / S * 32, K, NM, persist != 0, WN);
     float *rstd_s = reinterpret_cast<float *>(lds);
     int *flag_s = reinterpret_cast<int *>(lds + 256);
     float *nw_s = reinterpret_cast<float *>(lds + L.nw_off);
@@ -160,17 +167,17 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
     SWH_GEMM_TRACE(0);
 
     // ---- (a) this wave's weights for the first column block (HBM, the long pole: first in the queue)
-    const int ksw0 = kb0 + (kb1 - kb0) * wid / NW, ksw1 = kb0 + (kb1 - kb0) * (wid + 1) / NW;
+    const int ksw0 = kb0 + (kb1 - kb0) * kw / WK, ksw1 = kb0 + (kb1 - kb0) * (kw + 1) / WK;
     const uint16_t *wrow[CB];
     auto set_rows = [&](int n0) {
 #pragma unroll
         for (int j = 0; j < CB; ++j) {
             int n;
             if constexpr (EPI == EPI_SILU) {
-                const int c = j * 8 + (rl & 7);
+                const int c = (cg * CB + j) * 8 + (rl & 7);
                 n = (rl < 8) ? n0 + c : N + n0 + c;  // gate rows, then the matching up rows
             } else {
-                n = n0 + j * 16 + rl;
+                n = n0 + (cg * CB + j) * 16 + rl;
             }
             wrow[j] = w + (int64_t)n * K + kq;
         }
@@ -186,7 +193,7 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
             }
         }
     };
-    auto col0 = [&](int cbk) { return cbk * (EPI == EPI_SILU ? NB / 2 : NB); };
+    auto col0 = [&](int cbk) { return cbk * (EPI == EPI_SILU ? NBT / 2 : NBT); };
     set_rows(col0(cb_first));
     issue(ksw0);
     // ---- (b) RMSNorm partial sums and the norm-weight slice (L2)
@@ -327,7 +334,7 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
     SWH_GEMM_TRACE(3);
 
     // ---- (f) column blocks
-    auto slot = [&](int s, int r, int c) -> float & { return part[(s * NB + c) * LDR + r]; };
+    auto slot = [&](int s, int r, int c) -> float & { return part[(s * NBT + c) * LDR + r]; };
     for (int cbk = cb_first; cbk < ncb; cbk += cb_step) {
         const int n0 = col0(cbk);
         f32x4 acc[MS][CB];
@@ -367,30 +374,31 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
             for (int i = 0; i < MS; ++i)
 #pragma unroll
                 for (int j = 0; j < CB; ++j)
-                    *reinterpret_cast<f32x4 *>(&slot(s, i * 16 + (lane >> 4) * 4, j * 16 + rl)) = acc[i][j];
+                    *reinterpret_cast<f32x4 *>(&slot(s, i * 16 + (lane >> 4) * 4, (cg * CB + j) * 16 + rl)) = acc[i][j];
         };
-        for (int h = NW >> 1; h >= 1; h >>= 1) {
-            if (wid >= h && wid < 2 * h) park(wid - h);
+        for (int h = WK >> 1; h >= 1; h >>= 1) {
+            if (kw >= h && kw < 2 * h) park(kw - h);
             lds_barrier();
-            if (wid < h) {
+            if (kw < h) {
 #pragma unroll
                 for (int i = 0; i < MS; ++i)
 #pragma unroll
                     for (int j = 0; j < CB; ++j)
-                        acc[i][j] += *reinterpret_cast<const f32x4 *>(&slot(wid, i * 16 + (lane >> 4) * 4, j * 16 + rl));
+                        acc[i][j] += *reinterpret_cast<const f32x4 *>(
+                            &slot(kw, i * 16 + (lane >> 4) * 4, (cg * CB + j) * 16 + rl));
             }
             lds_barrier();
         }
-        if (wid == 0) park(0);
+        if (kw == 0) park(0);
         lds_barrier();
         SWH_GEMM_TRACE(5);
 
         // ---- cross-workgroup split-K: publish, ticket, last arriver reduces
         if (S > 1) {
             const int blk = mt * ncb + cbk;
-            float *my = slabs + ((int64_t)blk * S + sidx) * (MR * NB);
-            for (int idx = tid; idx < MR * NB; idx += NT)
-                __hip_atomic_store(my + idx, slot(0, idx / NB, idx % NB), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            float *my = slabs + ((int64_t)blk * S + sidx) * (MR * NBT);
+            for (int idx = tid; idx < MR * NBT; idx += NT)
+                __hip_atomic_store(my + idx, slot(0, idx / NBT, idx % NBT), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (tid == 0) {
@@ -399,13 +407,13 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
             }
             __syncthreads();
             if (!flag_s[0]) return;  // S > 1 never loops over column blocks
-            const float *base = slabs + (int64_t)blk * S * (MR * NB);
-            for (int idx = tid; idx < MR * NB; idx += NT) {
+            const float *base = slabs + (int64_t)blk * S * (MR * NBT);
+            for (int idx = tid; idx < MR * NBT; idx += NT) {
                 float v = 0.f;
                 for (int q = 0; q < S; ++q)
-                    v += __hip_atomic_load(base + (int64_t)q * MR * NB + idx, __ATOMIC_RELAXED,
+                    v += __hip_atomic_load(base + (int64_t)q * MR * NBT + idx, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
-                slot(0, idx / NB, idx % NB) = v;
+                slot(0, idx / NBT, idx % NBT) = v;
             }
             if (tid == 0) __hip_atomic_store(counters + blk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __syncthreads();
@@ -462,8 +470,8 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
             if constexpr (EPI == EPI_RESIDUAL) {
                 if (ss_out) {  // partial sums of squares of the new rows, per 16-column chunk
                     __syncthreads();
-                    for (int idx = tid; idx < MR * CB; idx += NT) {
-                        const int r = idx / CB, j = idx - r * CB;
+                    for (int idx = tid; idx < MR * CB * WN; idx += NT) {
+                        const int r = idx / (CB * WN), j = idx - r * (CB * WN);
                         if (m0 + r >= M) continue;
                         float ss = 0.f;
 #pragma unroll
@@ -1037,8 +1045,9 @@ int attn_dispatch_gq(int gq, const uint16_t *q, uint16_t *kc, uint16_t *vc, cons
 
 // ---- GEMM launch configuration -------------------------------------------
 struct GemmCfg {
-    int ms, cb, nw, s, gx;  // 16-row blocks, 16-col blocks, waves, K split, grid.x
+    int ms, cb, nw, s, gx;  // 16-row blocks, 16-col blocks (tile), waves, K split, grid.x
     bool persist;
+    int wn = 1;             // column groups: a wave computes cb / wn column blocks over K / (nw / wn)
 };
 
 int cu_count() {
@@ -1064,8 +1073,9 @@ inline int gemm_waves(int) { return 8; }
 double gemm_cost(const GemmCfg &c, int64_t M, int64_t wcols, int64_t K, int nm) {
     const int64_t MR = 16 * c.ms, KS = K / 32, ncu = cu_count();
     const int64_t krmax = (KS + c.s - 1) / c.s * 32;
-    const GemmLds L = gemm_lds(c.cb, (int)MR, c.nw, (int)krmax, (int)K, nm, c.persist);
+    const GemmLds L = gemm_lds(c.cb, (int)MR, c.nw, (int)krmax, (int)K, nm, c.persist, c.wn);
     if (L.total > 160 * 1024) return 1e30;
+    if (c.cb % c.wn || c.nw % c.wn || MR * c.cb * 2 > 2 * 64 * c.nw) return 1e30;  // epilogue: <= 2 groups / thread
     const int64_t ncb = wcols / (16 * c.cb), nmt = (M + MR - 1) / MR;
     const int64_t xbytes = MR * krmax * 2, wbytes = 2 * 16 * c.cb * krmax * 2;
     if (c.persist) {
@@ -1104,13 +1114,13 @@ GemmCfg pick_cfg(int64_t M, int64_t wcols, int64_t K, bool silu, int nm) {
         if (c.gx > wcols / 32 * nmt64) c.gx = (int)(wcols / 32 * nmt64);
         if (gemm_cost(c, M, wcols, K, nm) < best_cost) best = c;
     }
-    if (const char *e = getenv("SWH_GEMM_CFG")) {  // tuning override "ms,cb,s[,p]"
-        int a = 0, b = 0, d = 0, pz = 0;
-        const int got = sscanf(e, "%d,%d,%d,%d", &a, &b, &d, &pz);
+    if (const char *e = getenv("SWH_GEMM_CFG")) {  // tuning override "ms,cb,s[,p[,wn]]"
+        int a = 0, b = 0, d = 0, pz = 0, wn = 1;
+        const int got = sscanf(e, "%d,%d,%d,%d,%d", &a, &b, &d, &pz, &wn);
         if (got >= 3 && (a == 1 || a == 2 || a == 4) && (b == 1 || b == 2 || b == 4) && d >= 1 && d <= KS &&
-            wcols % (16 * b * align) == 0 && !(pz && d != 1)) {
+            wcols % (16 * b * align) == 0 && !(pz && d != 1) && (wn == 1 || wn == 2 || wn == 4)) {
             const int64_t nmt = (M + 16 * a - 1) / (16 * a);
-            GemmCfg c{a, b, gemm_waves(a), d, 0, pz != 0};
+            GemmCfg c{a, b, gemm_waves(a), d, 0, pz != 0, wn};
             if (c.persist) {
                 const int64_t per = ncu / nmt > 0 ? ncu / nmt : 1, ncb = wcols / (16 * b);
                 c.gx = (int)((per < ncb ? per : ncb) * nmt);
@@ -1119,10 +1129,15 @@ GemmCfg pick_cfg(int64_t M, int64_t wcols, int64_t K, bool silu, int nm) {
         }
     }
     if (!best.persist) best.gx = (int)(8 * ((M + 16 * best.ms - 1) / (16 * best.ms)) * ((wcols / (16 * best.cb) + 7) / 8));
+    // one column block per wave (column groups split the waves, each group splits K):
+    // a 4x smaller LDS merge; gate/up 14.7 -> 12.3 us (tools/bench_decode.py --ku)
+    if (!getenv("SWH_GEMM_CFG") && !best.persist && best.cb > 1 && best.nw % best.cb == 0 &&
+        gemm_cost(GemmCfg{best.ms, best.cb, best.nw, best.s, best.gx, false, best.cb}, M, wcols, K, nm) < 1e29)
+        best.wn = best.cb;
     if (const char *e = getenv("SWH_GEMM_NW")) {  // tuning override: waves per workgroup (16: cb == 1 only)
         const int v = atoi(e);
-        if ((v == 4 || v == 8 || (v == 16 && best.cb == 1)) && gemm_cost(GemmCfg{best.ms, best.cb, v, best.s, best.gx, best.persist}, M, wcols, K,
-                                            nm) < 1e29)
+        if ((v == 4 || v == 8 || (v == 16 && best.cb == best.wn)) &&
+            gemm_cost(GemmCfg{best.ms, best.cb, v, best.s, best.gx, best.persist, best.wn}, M, wcols, K, nm) < 1e29)
             best.nw = v;
     }
     return best;
@@ -1146,7 +1161,7 @@ int launch_gemm(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const ui
         attr = true;
     }
     decode_gemm_kernel<CB, MS, NM, EPI, BIAS, MAXT><<<grid, 64u * c.nw, lds, s>>>(
-        X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr, c.persist ? 1 : 0);
+        X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr, c.persist ? 1 : 0, c.wn);
     return launch_status();
 }
 
@@ -1154,7 +1169,7 @@ template <int MS, int NM, int EPI, bool BIAS>
 int launch_gemm_cb(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W,
                    int m, int n, int k, const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs,
                    uint16_t *R, float *ss_out, uint16_t *Y, int ld, float *slab, int *ctr) {
-    switch (c.cb) {
+    switch (c.cb / c.wn) {  // column blocks per wave
     case 1:
         if (c.nw > 8)  // 16 waves: one-column-block tiles over long K
             return launch_gemm<1, MS, NM, EPI, BIAS, 1024>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr);
@@ -1294,7 +1309,8 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
     auto *R = static_cast<uint16_t *>(residual);
     auto *Y = static_cast<uint16_t *>(y);
     const int m = (int)M, n = (int)N, k = (int)K, ld = (int)ldy;
-    const GemmLds L = gemm_lds(c.cb, (int)MR, c.nw, (int)((K / 32 + c.s - 1) / c.s * 32), (int)K, nm, c.persist);
+    const GemmLds L = gemm_lds(c.cb, (int)MR, c.nw, (int)((K / 32 + c.s - 1) / c.s * 32), (int)K, nm, c.persist,
+                               c.wn);
     if (L.total > 160 * 1024 || c.gx <= 0) return SWH_E_ARG;
     const dim3 grid((unsigned)c.gx, 1u, (unsigned)c.s);
     const size_t lds = (size_t)L.total;

@@ -677,7 +677,9 @@ def test_rmsnorm_statistic_handoff(ops, dev):
 @pytest.mark.parametrize("cfg,nw", [("1,1,1", None), ("2,1,1", None), ("4,1,1", None), ("1,2,2", None),
                                     ("2,4,1", None), ("4,4,3", None), ("1,1,3", None), ("2,2,2", None),
                                     ("4,2,1,1", None), ("4,4,1,1", None), ("1,1,1", "16"), ("2,1,2", "16"),
-                                    ("1,1,1", "4"), ("2,2,1", "4"), ("4,1,3", "16")])
+                                    ("1,1,1", "4"), ("2,2,1", "4"), ("4,1,3", "16"), ("4,4,1,0,4", None),
+                                    ("4,4,1,0,2", None), ("2,2,2,0,2", None), ("4,2,1,1,2", None),
+                                    ("4,4,1,0,4", "4"), ("1,4,3,0,4", None)])
 def test_decode_gemm_launch_configs(ops, dev, cfg, nw, monkeypatch):
     """Every (row blocks, column blocks, K split[, persistent]) geometry and
     wave count computes the same GEMM: normed + bias, residual + statistic,

@@ -79,6 +79,8 @@ def ku_sweep(eng, m):
         "down": lambda i: nn_ops.decode_gemm(eng.act, p[f"l{i}.down_w"], residual=eng.s, ss_out=ss),
         "qkv": lambda i: nn_ops.decode_gemm(eng.s, eng._normed(f"l{i}.qkv_w", f"l{i}.ln_in")[0],
                                             bias=p.get(f"l{i}.qkv_b"), y=eng.qkv, ss_in=ss),
+        "gate_up": lambda i: nn_ops.decode_gemm(eng.s, eng._normed(f"l{i}.gu_w", f"l{i}.ln_post")[0], silu=True,
+                                                y=eng.act, ss_in=ss),
     }
 
     def t(fn):
@@ -98,9 +100,10 @@ def ku_sweep(eng, m):
         return 1000.0 * e0.elapsed_time(e1) / (3 * L)
 
     print("cfg          nw " + " ".join(f"{k:>9s}" for k in shapes), flush=True)
-    for cf in (None, "1,1,1", "1,1,2", "2,1,1", "2,1,2", "4,1,2", "4,1,4"):
+    for cf in (None, "1,1,1", "2,1,1", "2,1,2", "4,4,1,0,2", "4,4,1,0,4", "2,4,1,0,4", "2,2,1,0,2", "4,2,1,0,2",
+               "1,2,1,0,2", "1,4,1,0,4", "2,2,2,0,2", "4,4,2,0,4", "4,2,1,1,2", "4,4,1,1,4"):
         for ku in ("",):
-            for nw in ("4", "8", "16"):
+            for nw in ("8",):
                 for k, v in (("SWH_GEMM_CFG", cf), ("SWH_GEMM_NW", nw)):
                     if v is None:
                         os.environ.pop(k, None)
