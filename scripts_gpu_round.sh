@@ -13,6 +13,9 @@ run() {  # name timeout cmd...
 }
 for step in "$@"; do
   case $step in
+    gpu) run gpu 1100 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
+    tune) SWH_GEMM_TUNING=tune SWH_GEMM_TABLE=gpurun_out/gemm_tuned.csv run tune 900 python bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
+    benchtuned) SWH_GEMM_TABLE=gpurun_out/gemm_tuned.csv run benchtuned 600 python bench.py --steps 3 --warmup 2 --no-cpu-baseline ;;
     kern) run kern 600 python -m pytest tests/test_kernels_gpu.py -q -m gpu ;;
     kernx) run kernx 600 python -m pytest tests/test_kernels_gpu.py -q -m gpu -x ;;
     dec) run dec 300 python tools/bench_decode.py ;;

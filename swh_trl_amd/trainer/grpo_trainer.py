@@ -27,6 +27,7 @@ from typing import Any, Callable, Optional, Union
 import torch
 
 from .. import dist as swh_dist
+from .. import gemm_tuning
 from .. import ops
 from ..engine.config import DecoderConfig, PRESETS, from_hf_config
 from ..engine.decode import DecodeEngine
@@ -114,6 +115,7 @@ class GRPOTrainer:
             raise RuntimeError("GRPOTrainer runs the MI355X engine and needs a ROCm device (no CPU fallback)")
         self.device = torch.device("cuda", self.local_rank)
         torch.cuda.set_device(self.device)
+        gemm_tuning.enable()
         torch.manual_seed(a.seed)
         self.model = load_model(model, self.device, trainable=True, seed=a.seed)
         self.processing_class = processing_class

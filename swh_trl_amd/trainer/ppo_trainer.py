@@ -30,6 +30,7 @@ import numpy as np
 import torch
 
 from .. import dist as swh_dist
+from .. import gemm_tuning
 from .. import ops
 from ..engine.decode import DecodeEngine
 from ..engine.model import CausalLM
@@ -132,6 +133,7 @@ class PPOTrainer:
             raise RuntimeError("PPOTrainer runs the MI355X engine and needs a ROCm device (no CPU fallback)")
         self.device = torch.device("cuda", self.local_rank)
         torch.cuda.set_device(self.device)
+        gemm_tuning.enable()
         # models: policy (lm head), frozen ref copy, value model + reward model (score heads)
         self.policy_model = load_model(model, self.device, trainable=True, seed=args.seed)
         if ref_model is not None:
