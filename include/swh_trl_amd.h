@@ -307,6 +307,20 @@ int swh_lm_head_sample(const void *x, const void *w, int64_t M, int64_t V, int64
                        int32_t *finished, int64_t *out_tokens, int64_t out_ld, int64_t *cur_tokens, void *workspace,
                        int64_t workspace_bytes, void *stream);
 
+/* swh_lm_head_sample plus the next decode step's input in the same launches:
+ * x_next[b] = embed[token drawn for row b] and ss_next its RMSNorm partial
+ * sums (as swh_embed_gather), and *step advanced by one once every row has
+ * read it (as swh_step_advance).  One replayable decode step ends here; the
+ * workspace (>= swh_lm_head_sample_workspace_bytes) must be ZEROED once at
+ * allocation (a self-resetting ticket lives at its end).  Replaces the
+ * per-token `input_ids = cat(input_ids, next_tokens)` / embedding lookup /
+ * cache_position advance of transformers `_sample` (grpo_trainer.py:1804). */
+int swh_lm_head_sample_step(const void *x, const void *w, int64_t M, int64_t V, int64_t K, const void *norm_w,
+                            float eps, const float *ss_in, const swh_sample_params *params, const uint64_t *rng,
+                            int32_t *step, int32_t *finished, int64_t *out_tokens, int64_t out_ld,
+                            int64_t *cur_tokens, const void *embed, void *x_next, float *ss_next, void *workspace,
+                            int64_t workspace_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -79,6 +79,8 @@ SIGNATURES = {
     "swh_lm_head_sample_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "swh_lm_head_sample": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_f32, c_vp, C.POINTER(SampleParams),
                                    c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
+    "swh_lm_head_sample_step": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_f32, c_vp, C.POINTER(SampleParams),
+                                        c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "swh_decode_gemm": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_f32, c_vp, c_vp, c_i32, c_vp, c_i64,
                                 c_vp, c_vp, c_vp, c_i64, c_vp]),
 }

@@ -121,6 +121,10 @@ __host__ __device__ inline GemmLds gemm_lds(int cb, int mr, int nw, int krmax, i
 // last arriver sums the S slabs in fixed order (deterministic, placement-
 // independent — MI355X_MICROARCH.md §Workgroup dispatch) and runs the epilogue.
 
+#ifndef SWH_KU
+#define SWH_KU 4  // weight-load round depth (k-steps per wave issued together)
+#endif
+
 template <int CB, int MS, int NM, int EPI, bool BIAS, int MAXT>
 __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
     const uint16_t *__restrict__ x, const uint16_t *__restrict__ w, int M, int N, int K,
@@ -131,7 +135,7 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
     // a wave computes NB = 16 CB columns; the WN column groups of NW / WN waves each
     // make a tile of NBT = WN NB columns (the waves of a group split K)
     constexpr int NB = 16 * CB, MR = 16 * MS, LDR = MR + 4;  // merge slots column-major: b128 parks
-    constexpr int kU = 4;                                     // k-steps whose loads are issued together
+    constexpr int kU = SWH_KU;                                // k-steps whose loads are issued together
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, NT = blockDim.x, NW = NT >> 6;
     const int WN = wn, NBT = NB * WN, WK = NW / WN, cg = wid / WK, kw = wid - cg * WK;
@@ -514,7 +518,11 @@ struct LmSample {
     int pstride;
 };
 
-template <int NM, int EPI, bool BIAS, bool SAMPLE>
+// KSC: K / 32 at compile time (0 = read from K): with a constant trip count the
+// compiler pipelines the A-fragment LDS reads across k-steps and waits on each
+// weight load in turn (vmcnt(k)), instead of one LDS round trip per MFMA
+// behind a wait for the whole tile (the lm head ran 5.6 us of MFMA per tile).
+template <int NM, int EPI, bool BIAS, bool SAMPLE, int KSC>
 __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict__ x, const uint16_t *__restrict__ w,
                                                       int M, int N, int K, const uint16_t *__restrict__ norm_w,
                                                       float eps, const float *__restrict__ ss_in,
@@ -525,7 +533,8 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
     const int rl = lane & 15, kq = (lane >> 4) * 8, g = lane >> 4;
     const int nmt = (M + 63) / 64, mt = blockIdx.x % nmt, m0 = mt * 64;
     const int wgs = gridDim.x / nmt, wg = blockIdx.x / nmt;
-    const int ntile = (EPI == EPI_SILU) ? N / 8 : N / 16, KS = K / 32, RS = K * 2 + 16;
+    constexpr int KSA = KSC ? KSC : kLmMaxKS;  // register array extent
+    const int ntile = (EPI == EPI_SILU) ? N / 8 : N / 16, KS = KSC ? KSC : K / 32, RS = K * 2 + 16;
     const GemmLds L = gemm_lds(1, 64, NW, K, K, NM, false);
     float *rstd_s = reinterpret_cast<float *>(lds);
     float *nw_s = reinterpret_cast<float *>(lds + L.nw_off);
@@ -535,7 +544,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
     int t = wg + wgs * wid;  // tile t -> workgroup t % wgs
     SWH_GEMM_TRACE(0);
 
-    uint4 bv[kLmMaxKS];
+    uint4 bv[KSA];
     auto wrow_of = [&](int tile) -> int64_t {
         if constexpr (EPI == EPI_SILU) return (rl < 8) ? tile * 8 + rl : N + tile * 8 + rl - 8;  // gate, then up
         return (int64_t)tile * 16 + rl;
@@ -543,8 +552,8 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
     auto issue = [&](int tile) {
         const uint16_t *wr = w + wrow_of(tile) * K + kq;
 #pragma unroll
-        for (int ks = 0; ks < kLmMaxKS; ++ks)
-            if (ks < KS) bv[ks] = *reinterpret_cast<const uint4 *>(wr + ks * 32);
+        for (int ks = 0; ks < KSA; ++ks)
+            if (KSC || ks < KS) bv[ks] = *reinterpret_cast<const uint4 *>(wr + ks * 32);
     };
     if (t < ntile) issue(t);  // the weight stream first
     // RMSNorm partials and norm weights (L2), then the X image by LDS-DMA
@@ -664,13 +673,35 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
         f32x4 acc[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const unsigned char *xrow = xs + rl * RS + kq * 2;
+        if constexpr (KSC != 0) {
+            // A fragments double-buffered one k-step ahead; the scheduling barrier
+            // keeps the compiler from hoisting every read (register pressure)
+            uint4 a[2][4];
 #pragma unroll
-        for (int ks = 0; ks < kLmMaxKS; ++ks) {
-            if (ks < KS) {
+            for (int i = 0; i < 4; ++i) a[0][i] = *reinterpret_cast<const uint4 *>(xrow + i * 16 * RS);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const uint4 a = *reinterpret_cast<const uint4 *>(xs + (i * 16 + rl) * RS + (ks * 32 + kq) * 2);
-                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(bv[ks]), acc[i], 0, 0, 0);
+            for (int ks = 0; ks < KSC; ++ks) {
+                if (ks + 1 < KSC) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        a[(ks + 1) & 1][i] = *reinterpret_cast<const uint4 *>(xrow + i * 16 * RS + (ks + 1) * 64);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[ks & 1][i]), as_bf16x8(bv[ks]),
+                                                                    acc[i], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+#pragma unroll
+            for (int ks = 0; ks < KSA; ++ks) {
+                if (ks < KS) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const uint4 a = *reinterpret_cast<const uint4 *>(xrow + i * 16 * RS + ks * 64);
+                        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(bv[ks]), acc[i], 0, 0, 0);
+                    }
                 }
             }
         }
@@ -751,15 +782,29 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
     SWH_GEMM_TRACE(6);
 }
 
+// The next step's input, produced by the finalize (swh_lm_head_sample_step):
+// the drawn token's embedding row and its RMSNorm partial sums, and the step
+// counter advanced by the last row to finish (ticket) — the three small
+// launches embed_gather / step_advance / finalize become one.
+struct LmNext {
+    const uint16_t *embed;  // [V, H] (null: no gather, no advance)
+    uint16_t *x;            // [M, H]
+    float *ss;              // [M, H / 16] (nullable)
+    int32_t *step;          // advanced once every row has read it
+    int32_t *ticket;        // zero at allocation, self-resetting
+    int H, M;
+};
+
 // Merge the per-wave partials of a row; EOS / pad bookkeeping as
 // swh_sample_step's finalize (csrc/sampler.hip).
 __global__ __launch_bounds__(256) void lm_sample_finalize_kernel(const LmPart *__restrict__ part, int P,
                                                                  swh_sample_params p, const int32_t *__restrict__ step_p,
                                                                  int32_t *__restrict__ finished,
                                                                  int64_t *__restrict__ out_tokens, int64_t out_ld,
-                                                                 int64_t *__restrict__ cur_tokens, int V) {
+                                                                 int64_t *__restrict__ cur_tokens, int V, LmNext nx) {
     __shared__ float kk[4];
     __shared__ int32_t ii[4];
+    __shared__ int64_t tok_s;
     const int64_t b = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     float k = kNegInf;
@@ -785,21 +830,53 @@ __global__ __launch_bounds__(256) void lm_sample_finalize_kernel(const LmPart *_
         ii[wid] = c;
     }
     __syncthreads();
-    if (tid != 0) return;
-    for (int q = 1; q < 4; ++q)
-        if (kk[q] > k || (kk[q] == k && (uint32_t)ii[q] < (uint32_t)c)) {
-            k = kk[q];
-            c = ii[q];
+    if (tid == 0) {
+        for (int q = 1; q < 4; ++q)
+            if (kk[q] > k || (kk[q] == k && (uint32_t)ii[q] < (uint32_t)c)) {
+                k = kk[q];
+                c = ii[q];
+            }
+        if (c < 0 || c >= V) c = 0;  // fully masked row (cannot happen with min_tokens_to_keep=1)
+        const int32_t step = *step_p;
+        int64_t tok = c;
+        if (p.pad_token_id >= 0 && finished[b] != 0) tok = p.pad_token_id;
+        bool is_eos = false;
+        for (int e = 0; e < p.n_eos && e < 4; ++e) is_eos |= (tok == p.eos_ids[e]);
+        if (is_eos) finished[b] = 1;
+        out_tokens[b * out_ld + step] = tok;
+        if (cur_tokens) cur_tokens[b] = tok;
+        tok_s = tok;
+    }
+    if (!nx.embed) return;
+    __syncthreads();
+    // the next step's input row: embedding of the drawn token + its RMSNorm partials
+    const int64_t id = tok_s;
+    const int nch = nx.H / 16;
+    for (int ch = tid; ch < nch; ch += 256) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(nx.embed + id * nx.H) + 2 * ch;
+        const uint4 lo = src[0], hi = src[1];
+        uint4 *dst = reinterpret_cast<uint4 *>(nx.x + b * nx.H) + 2 * ch;
+        dst[0] = lo;
+        dst[1] = hi;
+        if (nx.ss) {
+            float a[8], e[8];
+            unpack16<SWH_BF16>(lo, a);
+            unpack16<SWH_BF16>(hi, e);
+            float ss = 0.f;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) ss = fmaf(a[q], a[q], ss);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) ss = fmaf(e[q], e[q], ss);
+            nx.ss[b * nch + ch] = ss;
         }
-    if (c < 0 || c >= V) c = 0;  // fully masked row (cannot happen with min_tokens_to_keep=1)
-    const int32_t step = *step_p;
-    int64_t tok = c;
-    if (p.pad_token_id >= 0 && finished[b] != 0) tok = p.pad_token_id;
-    bool is_eos = false;
-    for (int e = 0; e < p.n_eos && e < 4; ++e) is_eos |= (tok == p.eos_ids[e]);
-    if (is_eos) finished[b] = 1;
-    out_tokens[b * out_ld + step] = tok;
-    if (cur_tokens) cur_tokens[b] = tok;
+    }
+    if (tid == 0) {  // every row has read *step before its ticket: the last one advances it
+        const int t = __hip_atomic_fetch_add(nx.ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == nx.M - 1) {
+            __hip_atomic_store(nx.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(nx.step, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1190,19 +1267,31 @@ int launch_gemm_ms(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const
     }
 }
 
-template <int NM, int EPI, bool BIAS, bool SAMPLE>
-int launch_lm(dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W, int M, int N, int K,
-              const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs, uint16_t *Y, int ldy,
-              const LmSample &smp) {
+template <int NM, int EPI, bool BIAS, bool SAMPLE, int KSC>
+int launch_lm_ks(dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W, int M, int N, int K,
+                 const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs, uint16_t *Y, int ldy,
+                 const LmSample &smp) {
     static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in once per kernel
     if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&lm_head_kernel<NM, EPI, BIAS, SAMPLE>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&lm_head_kernel<NM, EPI, BIAS, SAMPLE, KSC>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
             return SWH_E_LAUNCH;
         attr = true;
     }
-    lm_head_kernel<NM, EPI, BIAS, SAMPLE><<<grid, 512, lds, s>>>(X, W, M, N, K, NWt, eps, ss_in, Bs, Y, ldy, smp);
+    lm_head_kernel<NM, EPI, BIAS, SAMPLE, KSC><<<grid, 512, lds, s>>>(X, W, M, N, K, NWt, eps, ss_in, Bs, Y, ldy, smp);
     return launch_status();
+}
+
+// compile-time k-step counts for the model widths in use (Qwen2.5-0.5B: H = 896)
+template <int NM, int EPI, bool BIAS, bool SAMPLE>
+int launch_lm(dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W, int M, int N, int K,
+              const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs, uint16_t *Y, int ldy,
+              const LmSample &smp) {
+    switch (K / 32) {
+    case 28: return launch_lm_ks<NM, EPI, BIAS, SAMPLE, 28>(grid, lds, s, X, W, M, N, K, NWt, eps, ss_in, Bs, Y, ldy, smp);
+    case 32: return launch_lm_ks<NM, EPI, BIAS, SAMPLE, 32>(grid, lds, s, X, W, M, N, K, NWt, eps, ss_in, Bs, Y, ldy, smp);
+    default: return launch_lm_ks<NM, EPI, BIAS, SAMPLE, 0>(grid, lds, s, X, W, M, N, K, NWt, eps, ss_in, Bs, Y, ldy, smp);
+    }
 }
 
 // the tile kernel for plain / bias / SiLU epilogues
@@ -1336,17 +1425,22 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
 #undef SWH_GEMM
 }
 
+// [partials (M x per x 8 LmPart) | 256 B: the finalize ticket (zero at allocation)]
+static int64_t lm_part_bytes(int64_t M) {
+    const int64_t nmt = (M + 63) / 64, per = cu_count() / nmt > 0 ? cu_count() / nmt : 1;
+    return (M * per * 8 * (int64_t)sizeof(LmPart) + 255) / 256 * 256;
+}
+
 extern "C" int64_t swh_lm_head_sample_workspace_bytes(int64_t M, int64_t V, int64_t K) {
     (void)V;
     (void)K;
-    const int64_t nmt = (M + 63) / 64, per = cu_count() / nmt > 0 ? cu_count() / nmt : 1;
-    return M * per * 8 * (int64_t)sizeof(LmPart);
+    return lm_part_bytes(M) + 256;
 }
 
-extern "C" int swh_lm_head_sample(const void *x, const void *w, int64_t M, int64_t V, int64_t K, const void *norm_w,
-                                  float eps, const float *ss_in, const swh_sample_params *params, const uint64_t *rng,
-                                  const int32_t *step, int32_t *finished, int64_t *out_tokens, int64_t out_ld,
-                                  int64_t *cur_tokens, void *workspace, int64_t workspace_bytes, void *stream) {
+static int lm_head_sample_impl(const void *x, const void *w, int64_t M, int64_t V, int64_t K, const void *norm_w,
+                               float eps, const float *ss_in, const swh_sample_params *params, const uint64_t *rng,
+                               const int32_t *step, int32_t *finished, int64_t *out_tokens, int64_t out_ld,
+                               int64_t *cur_tokens, void *workspace, int64_t workspace_bytes, LmNext nx, void *stream) {
     if (!x || !w || !params || !rng || !step || !finished || !out_tokens || !workspace || M <= 0 || V <= 0 ||
         K <= 0 || K % 64 || K > 32 * kLmMaxKS || V % 16 || V >= ((int64_t)1 << 31) || M > (1 << 20))
         return SWH_E_ARG;
@@ -1375,6 +1469,29 @@ extern "C" int swh_lm_head_sample(const void *x, const void *w, int64_t M, int64
                                                                    nullptr, eps, nullptr, nullptr, nullptr, 0, smp);
     if (rc != SWH_OK) return rc;
     lm_sample_finalize_kernel<<<dim3((unsigned)M), 256, 0, s>>>(smp.part, smp.pstride, p, step, finished, out_tokens,
-                                                               out_ld, cur_tokens, (int)V);
+                                                               out_ld, cur_tokens, (int)V, nx);
     return launch_status();
+}
+
+extern "C" int swh_lm_head_sample(const void *x, const void *w, int64_t M, int64_t V, int64_t K, const void *norm_w,
+                                  float eps, const float *ss_in, const swh_sample_params *params, const uint64_t *rng,
+                                  const int32_t *step, int32_t *finished, int64_t *out_tokens, int64_t out_ld,
+                                  int64_t *cur_tokens, void *workspace, int64_t workspace_bytes, void *stream) {
+    return lm_head_sample_impl(x, w, M, V, K, norm_w, eps, ss_in, params, rng, step, finished, out_tokens, out_ld,
+                               cur_tokens, workspace, workspace_bytes, LmNext{}, stream);
+}
+
+extern "C" int swh_lm_head_sample_step(const void *x, const void *w, int64_t M, int64_t V, int64_t K,
+                                       const void *norm_w, float eps, const float *ss_in,
+                                       const swh_sample_params *params, const uint64_t *rng, int32_t *step,
+                                       int32_t *finished, int64_t *out_tokens, int64_t out_ld, int64_t *cur_tokens,
+                                       const void *embed, void *x_next, float *ss_next, void *workspace,
+                                       int64_t workspace_bytes, void *stream) {
+    if (!embed || !x_next || !cur_tokens || K % 16) return SWH_E_ARG;
+    if ((reinterpret_cast<uintptr_t>(embed) | reinterpret_cast<uintptr_t>(x_next)) & 15) return SWH_E_ARG;
+    if (workspace_bytes < swh_lm_head_sample_workspace_bytes(M, V, K)) return SWH_E_ARG;
+    LmNext nx{static_cast<const uint16_t *>(embed), static_cast<uint16_t *>(x_next), ss_next, step,
+              reinterpret_cast<int32_t *>(static_cast<char *>(workspace) + lm_part_bytes(M)), (int)K, (int)M};
+    return lm_head_sample_impl(x, w, M, V, K, norm_w, eps, ss_in, params, rng, step, finished, out_tokens, out_ld,
+                               cur_tokens, workspace, workspace_bytes, nx, stream);
 }

@@ -50,7 +50,8 @@ class DecodeEngine:
         self.d = torch.empty(B, H, **bf)
         self.logits_buf = torch.empty(B, c.vocab_size, **bf)
         self.ss = torch.empty(B, H // 16, device=dev, dtype=torch.float32)  # RMSNorm partial sums of s
-        self.sample_ws = torch.empty(ops._lib.load().swh_lm_head_sample_workspace_bytes(B, c.vocab_size, H),
+        # zeroed once: the fused finalize keeps a self-resetting ticket at its end
+        self.sample_ws = torch.zeros(ops._lib.load().swh_lm_head_sample_workspace_bytes(B, c.vocab_size, H),
                                      device=dev, dtype=torch.uint8)
         self.state = torch.zeros(2, device=dev, dtype=torch.int32)   # {step, P}
         self.rng = torch.zeros(2, device=dev, dtype=torch.int64)     # {seed, counter base}
@@ -88,14 +89,22 @@ class DecodeEngine:
     def _step(self):
         """One decode step: 5 fused kernels per layer when K % 128 == 0
         (norm+QKV+bias, RoPE+append+attention, O+residual, norm+gate/up+SiLU,
-        down+residual), then norm+lm head, sampler, step advance."""
+        down+residual), then norm+lm head, sampler, step advance.  With the
+        fused sampler the step ends in the lm-head finalize, which also
+        gathers the next input embedding and advances the step (the step
+        then starts at layer 0: `_chained` steps)."""
         if self.fused:
             self._step_fused()
         else:
             self._step_unfused()
         if not self._fused_sample():
             self._sample()
-        ops.step_advance(self.state[0:1])
+            ops.step_advance(self.state[0:1])
+
+    def _chained(self) -> bool:
+        """Steps chained through the fused finalize: the step's input row
+        (embedding + RMSNorm partials) was written by the previous step."""
+        return self._fused_sample()
 
     def _fused_sample(self) -> bool:
         """lm head + sampler in one kernel (no logits): unfiltered sampling
@@ -128,7 +137,8 @@ class DecodeEngine:
         p = m.p
         eps = c.rms_norm_eps
         ss = self.ss  # every producer of s writes its RMSNorm partial sums, every normed GEMM reads them
-        nn_ops.embed_gather(p["embed"], self.cur, self.s, ss_out=ss)
+        if not self._chained():
+            nn_ops.embed_gather(p["embed"], self.cur, self.s, ss_out=ss)
         for i in range(c.num_hidden_layers):
             w, nw = self._normed(f"l{i}.qkv_w", f"l{i}.ln_in")
             nn_ops.decode_gemm(self.s, w, norm_w=nw, eps=eps, bias=p.get(f"l{i}.qkv_b"), y=self.qkv, ss_in=ss)
@@ -141,8 +151,9 @@ class DecodeEngine:
             nn_ops.decode_gemm(self.act, p[f"l{i}.down_w"], residual=self.s, ss_out=ss)
         w, nw = self._normed("lm", "norm")
         if self._fused_sample():
-            nn_ops.lm_head_sample(self.s, w, self.params, self.rng, self.state[0:1], self.finished,
-                                  self.out, self.cur, norm_w=nw, eps=eps, ss_in=ss, workspace=self.sample_ws)
+            nn_ops.lm_head_sample_step(self.s, w, self.params, self.rng, self.state[0:1], self.finished,
+                                       self.out, self.cur, p["embed"], self.s, ss, norm_w=nw, eps=eps, ss_in=ss,
+                                       workspace=self.sample_ws)
         else:
             nn_ops.decode_gemm(self.s, w, norm_w=nw, eps=eps, y=self.logits_buf, ss_in=ss)
 
@@ -351,6 +362,8 @@ class DecodeEngine:
         self._prefill(prompt_ids, prompt_mask)
         self._sample()                      # token 0 from the prefill logits
         ops.step_advance(self.state[0:1])
+        if self.fused and self._chained():  # the first chained step's input row
+            nn_ops.embed_gather(self.model.p["embed"], self.cur, self.s, ss_out=self.ss)
         for s in range(1, max_new_tokens):
             if self.use_graph:
                 self.graph.replay()

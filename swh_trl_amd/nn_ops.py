@@ -177,6 +177,28 @@ def lm_head_sample(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Tensor, 
     return out_tokens
 
 
+def lm_head_sample_step(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Tensor, step: torch.Tensor,
+                        finished: torch.Tensor, out_tokens: torch.Tensor, cur_tokens: torch.Tensor,
+                        embed: torch.Tensor, x_next: torch.Tensor, ss_next: Optional[torch.Tensor], *,
+                        norm_w: Optional[torch.Tensor] = None, eps: float = 1e-6, ss_in: Optional[torch.Tensor] = None,
+                        workspace: torch.Tensor) -> torch.Tensor:
+    """lm_head_sample + the next step's input: x_next = embed[drawn token]
+    (+ RMSNorm partials ss_next) and *step += 1 once every row has read it
+    (include/swh_trl_amd.h swh_lm_head_sample_step).  `workspace` must have
+    been zeroed once at allocation."""
+    import ctypes
+    _dev(x, "lm_head_sample_step")
+    M, K = x.shape
+    V = w.shape[0]
+    if workspace.numel() < _lib.load().swh_lm_head_sample_workspace_bytes(M, V, K):
+        raise ValueError("lm_head_sample_step: workspace too small")
+    call("swh_lm_head_sample_step", x.data_ptr(), w.data_ptr(), M, V, K, _p(norm_w), float(eps), _p(ss_in),
+         ctypes.byref(params), rng.data_ptr(), step.data_ptr(), finished.data_ptr(), out_tokens.data_ptr(),
+         out_tokens.stride(0), cur_tokens.data_ptr(), embed.data_ptr(), x_next.data_ptr(), _p(ss_next),
+         workspace.data_ptr(), workspace.numel(), _stream())
+    return out_tokens
+
+
 class QKVRopeFn(torch.autograd.Function):
     """qkv [B, L, (Hq+2Hkv) D] -> q, k (rotated), v as contiguous [B, H, L, D]
     (include/swh_trl_amd.h swh_qkv_rope); backward writes d qkv in one pass."""
