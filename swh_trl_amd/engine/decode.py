@@ -311,14 +311,40 @@ class DecodeEngine:
         return out
 
     # ------------------------------------------------------------------ prefill
+    @staticmethod
+    def _unique_prompts(prompt_ids: torch.Tensor, prompt_mask: torch.Tensor):
+        """(representative row per distinct prompt, inverse map row -> distinct
+        prompt), or None when every row differs.  GRPO rolls out G copies of
+        each prompt (RepeatSampler, grpo_trainer.py:97-192): the prefill runs
+        once per distinct prompt and its K/V and last-position logits are
+        broadcast to the copies (row-independent arithmetic, same values)."""
+        if os.environ.get("SWH_PREFILL_DEDUP", "1") == "0":
+            return None
+        key = torch.cat([prompt_ids.to(torch.int64), prompt_mask.to(torch.int64)], 1)
+        uniq, inv = torch.unique(key, dim=0, return_inverse=True)
+        U, B = uniq.shape[0], key.shape[0]
+        if U == B:
+            return None
+        rep = torch.empty(U, dtype=torch.int64, device=key.device)
+        rep.scatter_(0, inv, torch.arange(B, device=key.device))
+        return rep, inv
+
     def _prefill(self, prompt_ids: torch.Tensor, prompt_mask: torch.Tensor):
         """Full forward over the prompt, K/V into cache slots [0, P), logits of the
-        last position.  Positions follow generate(): cumsum(mask) - 1."""
+        last position.  Positions follow generate(): cumsum(mask) - 1.  Copies
+        of one prompt are prefilled once (`_unique_prompts`)."""
         m = self.model
         P = prompt_ids.shape[1]
+        dedup = self._unique_prompts(prompt_ids, prompt_mask)
+        inv = None
+        if dedup is not None:
+            rep, inv = dedup
+            prompt_ids, prompt_mask = prompt_ids[rep], prompt_mask[rep]
         pos = (prompt_mask.long().cumsum(-1) - 1).clamp(min=0)
 
         def kv_out(i, k, v):
+            if inv is not None:
+                k, v = k.index_select(0, inv), v.index_select(0, inv)
             self.kv[i, 0, :, :, :P].copy_(k)
             self.kv[i, 1, :, :, :P].copy_(v)
 
@@ -327,7 +353,10 @@ class DecodeEngine:
             m.grad = None  # no grad accumulation in prefill
             try:
                 h = m.hidden_states(prompt_ids, positions=pos, key_mask=prompt_mask, kv_out=kv_out)
-                torch.mm(h[:, -1], m.lm_weight().t(), out=self.logits_buf)
+                if inv is None:
+                    torch.mm(h[:, -1], m.lm_weight().t(), out=self.logits_buf)
+                else:
+                    torch.index_select(h[:, -1] @ m.lm_weight().t(), 0, inv, out=self.logits_buf)
             finally:
                 m.grad = saved
 

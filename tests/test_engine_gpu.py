@@ -265,3 +265,37 @@ def test_grpo_trainer_smoke_and_oracle_step(dev):
     assert not torch.equal(before, tr.model.flat)
     log = state.log_history[-1]
     assert all(v == v for v in (log["loss"], log["grad_norm"]))  # finite
+
+
+@pytest.mark.parametrize("left_pad", [False, True])
+def test_prefill_dedup_matches_full_prefill(dev, monkeypatch, left_pad):
+    """GRPO groups: G copies of each prompt are prefilled once and broadcast.
+    The K/V cache and first-token logits equal the row-by-row prefill within
+    bf16 GEMM-order tolerance, and greedy rollouts agree token for token."""
+    from swh_trl_amd.engine import DecodeEngine
+    m = _tiny(dev, seed=7)
+    G, n, P, C = 4, 3, 12, 16
+    g = torch.Generator().manual_seed(7)
+    base = torch.randint(0, m.cfg.vocab_size, (n, P), generator=g)
+    bmask = torch.ones(n, P, dtype=torch.int32)
+    if left_pad:
+        bmask[1, :5] = 0
+        base[1, :5] = 0
+    ids = base.repeat_interleave(G, 0).to(dev)
+    mask = bmask.repeat_interleave(G, 0).to(dev)
+    assert DecodeEngine._unique_prompts(ids, mask) is not None
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SWH_PREFILL_DEDUP", flag)
+        eng = DecodeEngine(m, n * G, P, C)
+        eng.state[0], eng.state[1] = 0, P
+        eng._prefill(ids, mask)
+        kv, lg = eng.kv[:, :, :, :, :P].clone(), eng.logits_buf.clone()
+        comp, _ = eng.generate(ids, mask, C, greedy=True)
+        outs[flag] = (kv, lg, comp)
+    torch.testing.assert_close(outs["1"][0].float(), outs["0"][0].float(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(outs["1"][1].float(), outs["0"][1].float(), rtol=2e-2, atol=2e-2)
+    assert torch.equal(outs["1"][2], outs["0"][2])
+    # the copies of a prompt produce identical greedy continuations
+    comp = outs["1"][2].view(n, G, C)
+    assert (comp == comp[:, :1]).all()
