@@ -98,7 +98,7 @@ __host__ __device__ inline GemmLds gemm_lds(int cb, int mr, int nw, int krmax, i
     L.body_off = L.ss_off + (nm ? ((int64_t)mr * (K / 64) * 4 + 15) / 16 * 16 : 0);  // partials beside the DMA'd image
     L.xs_bytes = (int64_t)mr * (krmax * 2 + 16);
     const int wk = nw / wn;
-    const int64_t slots = (int64_t)(wk > 1 ? wk / 2 : 1) * 16 * cb * (mr + 4) * 4;  // [WK/2][NB][MR+4]
+    const int64_t slots = (int64_t)(wk + 1) * 16 * cb * (mr + 4) * 4;  // [WK + 1][NB][MR+4]
     L.slots_off = L.body_off + (persist ? L.xs_bytes : 0);
     int64_t end = L.body_off + L.xs_bytes;
     if (L.slots_off + slots > end) end = L.slots_off + slots;
@@ -123,6 +123,12 @@ __host__ __device__ inline GemmLds gemm_lds(int cb, int mr, int nw, int krmax, i
 
 #ifndef SWH_KU
 #define SWH_KU 4  // weight-load round depth (k-steps per wave issued together)
+#endif
+#ifndef SWH_ROUND_PREFETCH
+#define SWH_ROUND_PREFETCH 0  // all A reads of a full round before its MFMAs (A/B: tools/build_variant.py)
+#endif
+#ifndef SWH_FLAT_MERGE
+#define SWH_FLAT_MERGE 0  // one-barrier flat wave merge instead of the tree (A/B)
 #endif
 
 template <int CB, int MS, int NM, int EPI, bool BIAS, int MAXT>
@@ -339,6 +345,7 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
 
     // ---- (f) column blocks
     auto slot = [&](int s, int r, int c) -> float & { return part[(s * NBT + c) * LDR + r]; };
+    const int F = WK;  // the merged slot
     for (int cbk = cb_first; cbk < ncb; cbk += cb_step) {
         const int n0 = col0(cbk);
         f32x4 acc[MS][CB];
@@ -346,21 +353,38 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
         for (int i = 0; i < MS; ++i)
 #pragma unroll
             for (int j = 0; j < CB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const unsigned char *xrow = xs + rl * RS + kq * 2;
         for (int ks = ksw0; ks < ksw1; ks += kU) {
             if (ks != ksw0) issue(ks);
+            const unsigned char *xk = xrow + (ks - kb0) * 64;
+            if (SWH_ROUND_PREFETCH && ks + kU <= ksw1) {  // a full round: every A fragment read in flight first
+                uint4 a[kU][MS];
 #pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                if (ks + u >= ksw1) break;
-                const int kl = ((ks + u - kb0) * 32 + kq) * 2;
-                uint4 a[MS];
+                for (int u = 0; u < kU; ++u)
 #pragma unroll
-                for (int i = 0; i < MS; ++i) a[i] = *reinterpret_cast<const uint4 *>(xs + (i * 16 + rl) * RS + kl);
+                    for (int i = 0; i < MS; ++i) a[u][i] = *reinterpret_cast<const uint4 *>(xk + i * 16 * RS + u * 64);
 #pragma unroll
-                for (int i = 0; i < MS; ++i)
+                for (int u = 0; u < kU; ++u)
 #pragma unroll
-                    for (int j = 0; j < CB; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[i]), as_bf16x8(bv[u][j]),
-                                                                            acc[i][j], 0, 0, 0);
+                    for (int i = 0; i < MS; ++i)
+#pragma unroll
+                        for (int j = 0; j < CB; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[u][i]), as_bf16x8(bv[u][j]),
+                                                                                acc[i][j], 0, 0, 0);
+            } else {
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    if (ks + u >= ksw1) break;
+                    uint4 a[MS];
+#pragma unroll
+                    for (int i = 0; i < MS; ++i) a[i] = *reinterpret_cast<const uint4 *>(xk + i * 16 * RS + u * 64);
+#pragma unroll
+                    for (int i = 0; i < MS; ++i)
+#pragma unroll
+                        for (int j = 0; j < CB; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[i]), as_bf16x8(bv[u][j]),
+                                                                                acc[i][j], 0, 0, 0);
+                }
             }
         }
         // the next column block's first weight round overlaps this block's merge
@@ -370,9 +394,28 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
         }
         SWH_GEMM_TRACE(4);
 
-        // ---- merge the NW waves: fixed-order tree through NW/2 LDS slots -> slot 0
+#if SWH_FLAT_MERGE
+        // ---- merge the K-splitting waves: every wave parks its partial in its own slot,
+        // one barrier, then each output element sums the WK slots in fixed order into
+        // slot F = WK (two barriers instead of a log2(WK)-level tree)
         if (!persist) lds_barrier();  // the slots reuse the X image
         // C layout: lane holds rows 16 i + 4 g .. +3 of column 16 j + rl -> one 16-B store each
+#pragma unroll
+        for (int i = 0; i < MS; ++i)
+#pragma unroll
+            for (int j = 0; j < CB; ++j)
+                *reinterpret_cast<f32x4 *>(&slot(kw, i * 16 + (lane >> 4) * 4, (cg * CB + j) * 16 + rl)) = acc[i][j];
+        lds_barrier();
+        for (int idx = tid; idx < MR * NBT; idx += NT) {
+            const int c = idx / MR, r = idx - c * MR;  // r fastest: consecutive banks
+            float v = part[c * LDR + r];
+            for (int q = 1; q < WK; ++q) v += part[(q * NBT + c) * LDR + r];
+            part[(F * NBT + c) * LDR + r] = v;
+        }
+        lds_barrier();
+#else
+        // ---- merge the NW waves: fixed-order tree through the LDS slots -> slot F
+        if (!persist) lds_barrier();  // the slots reuse the X image
         auto park = [&](int s) {
 #pragma unroll
             for (int i = 0; i < MS; ++i)
@@ -393,8 +436,9 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
             }
             lds_barrier();
         }
-        if (kw == 0) park(0);
+        if (kw == 0) park(F);
         lds_barrier();
+#endif
         SWH_GEMM_TRACE(5);
 
         // ---- cross-workgroup split-K: publish, ticket, last arriver reduces
@@ -402,7 +446,7 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
             const int blk = mt * ncb + cbk;
             float *my = slabs + ((int64_t)blk * S + sidx) * (MR * NBT);
             for (int idx = tid; idx < MR * NBT; idx += NT)
-                __hip_atomic_store(my + idx, slot(0, idx / NBT, idx % NBT), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(my + idx, slot(F, idx / NBT, idx % NBT), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (tid == 0) {
@@ -417,7 +461,7 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
                 for (int q = 0; q < S; ++q)
                     v += __hip_atomic_load(base + (int64_t)q * MR * NBT + idx, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
-                slot(0, idx / NBT, idx % NBT) = v;
+                slot(F, idx / NBT, idx % NBT) = v;
             }
             if (tid == 0) __hip_atomic_store(counters + blk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __syncthreads();
@@ -433,8 +477,8 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
                 const float sc = (NM == 2) ? rstd_s[r] : 1.f;  // folded RMSNorm: y = rstd * (x W'^T)
 #pragma unroll
                 for (int cc = 0; cc < 8; ++cc) {
-                    const float g = round_bf16(slot(0, r, jb * 16 + cc) * sc);
-                    const float u = round_bf16(slot(0, r, jb * 16 + 8 + cc) * sc);
+                    const float g = round_bf16(slot(F, r, jb * 16 + cc) * sc);
+                    const float u = round_bf16(slot(F, r, jb * 16 + 8 + cc) * sc);
                     o[cc] = round_bf16(g / (1.f + expf(-g))) * u;
                 }
                 *reinterpret_cast<uint4 *>(y + (int64_t)gr * ldy + n0 + jb * 8) = pack8(o);
@@ -450,7 +494,7 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
                 float v[8];
                 const float sc = (NM == 2) ? rstd_s[r] : 1.f;  // folded RMSNorm: y = rstd * (x W'^T)
 #pragma unroll
-                for (int cc = 0; cc < 8; ++cc) v[cc] = slot(0, r, c8 + cc) * sc;
+                for (int cc = 0; cc < 8; ++cc) v[cc] = slot(F, r, c8 + cc) * sc;
                 if constexpr (BIAS) {
                     float b[8];
                     unpack16<SWH_BF16>(persist ? *reinterpret_cast<const uint4 *>(bias + gc) : pre_bias[q], b);
@@ -464,7 +508,7 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
 #pragma unroll
                     for (int cc = 0; cc < 8; ++cc) {
                         sres[cc] = round_bf16(sres[cc] + round_bf16(v[cc]));
-                        slot(0, r, c8 + cc) = sres[cc];
+                        slot(F, r, c8 + cc) = sres[cc];
                     }
                     *sp = pack8(sres);
                 } else {
@@ -479,7 +523,7 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
                         if (m0 + r >= M) continue;
                         float ss = 0.f;
 #pragma unroll
-                        for (int cc = 0; cc < 16; ++cc) ss = fmaf(slot(0, r, j * 16 + cc), slot(0, r, j * 16 + cc), ss);
+                        for (int cc = 0; cc < 16; ++cc) ss = fmaf(slot(F, r, j * 16 + cc), slot(F, r, j * 16 + cc), ss);
                         ss_out[(int64_t)(m0 + r) * (N / 16) + n0 / 16 + j] = ss;
                     }
                 }
