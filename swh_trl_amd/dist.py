@@ -58,6 +58,62 @@ def allreduce_mean_(flat: torch.Tensor, bucket_elems: int = 1 << 27):
         flat.div_(world)
 
 
+class OverlappedAllReduce:
+    """Gradient mean over ranks, launched DURING the backward pass: the caller
+    releases contiguous ranges of the flat gradient buffer as they become
+    final (the decoder layers in reverse order, from autograd hooks at each
+    layer input, engine/model.py `CausalLM.on_layer_grads`), each range is
+    all-reduced on a side stream behind an event of the compute stream, and
+    `finish()` reduces what is left (embedding / final norm / heads) and makes
+    the compute stream wait for every collective.  Replaces the reference's
+    DDP bucket hooks (accelerate -> torch DDP, 25 MB buckets): ranges here
+    are ~100 MB (a few whole layers), sized for per-link xGMI bandwidth.
+
+    With one process this is a no-op; on gloo (CPU tests) it sums and divides."""
+
+    def __init__(self, flat: torch.Tensor):
+        self.flat = flat
+        self.active = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        self.world = dist.get_world_size() if self.active else 1
+        self.nccl = self.active and dist.get_backend() == "nccl"
+        self.stream = torch.cuda.Stream(device=flat.device) if (self.nccl and flat.is_cuda) else None
+        self.works = []
+        self.done = []  # released [start, end) ranges
+
+    def release(self, start: int, end: int):
+        if not self.active or end <= start:
+            return
+        chunk = self.flat[start:end]
+        if self.stream is not None:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.flat.device))
+            self.stream.wait_event(ev)
+            with torch.cuda.stream(self.stream):
+                w = dist.all_reduce(chunk, op=dist.ReduceOp.AVG, async_op=True)
+        else:
+            w = dist.all_reduce(chunk, op=dist.ReduceOp.AVG if self.nccl else dist.ReduceOp.SUM, async_op=True)
+        self.works.append((w, chunk))
+        self.done.append((start, end))
+
+    def finish(self):
+        """Reduce every range not released yet, then wait for all of them."""
+        if not self.active:
+            return
+        n = self.flat.numel()
+        cur = 0
+        for s, e in sorted(self.done):
+            if s > cur:
+                self.release(cur, s)
+            cur = max(cur, e)
+        if cur < n:
+            self.release(cur, n)
+        for w, chunk in self.works:
+            w.wait()
+            if not self.nccl:
+                chunk.div_(self.world)
+        self.works, self.done = [], []
+
+
 def barrier():
     if dist.is_available() and dist.is_initialized():
         if dist.get_backend() == "nccl":

@@ -161,6 +161,22 @@ class _LMHeadLogp(torch.autograd.Function):
         return (dh.view(ctx.hshape) if dh is not None else None), None, None, None, None, None, None
 
 
+class _GradReady(torch.autograd.Function):
+    """Identity whose backward reports that the gradient has flowed past a
+    layer input: every weight gradient of that layer is final by then (they
+    are accumulated inside the layer's own backward nodes)."""
+
+    @staticmethod
+    def forward(ctx, x, layer, cb):
+        ctx.layer, ctx.cb = layer, cb
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        ctx.cb(ctx.layer)
+        return dy, None, None
+
+
 def rope_tables(cfg: DecoderConfig, max_pos: int, device) -> tuple[torch.Tensor, torch.Tensor]:
     """fp32 [max_pos, D/2] cos/sin holding bf16-rounded values (transformers computes
     them in fp32 and casts to the activation dtype before the multiply)."""
@@ -224,6 +240,14 @@ class CausalLM:
         if trainable:
             self.enable_grad_buffer()
         self._rope = None
+        # backward hook: called with layer index i once layer i's weight gradients are final
+        self.on_layer_grads = None
+
+    def layer_range(self, i: int) -> tuple[int, int]:
+        """[start, end) of layer i's parameters (and gradients) in the flat buffers."""
+        start = self.layout[f"l{i}.ln_in"][0]
+        end = self.layout[f"l{i + 1}.ln_in"][0] if i + 1 < self.cfg.num_hidden_layers else self.layout["norm"][0]
+        return start, end
 
     # ------------------------------------------------------------------ weights
     def init_weights(self, seed: int, std: float = 0.02):
@@ -370,6 +394,8 @@ class CausalLM:
             mask = causal & (km[:, None, None, :] | (eye & no_key[:, None, :, None]))
         x = _Embedding.apply(ids, self.p["embed"], self._gv("embed"), self._anchor)
         for i in range(c.num_hidden_layers):
+            if self.on_layer_grads is not None and torch.is_grad_enabled():
+                x = _GradReady.apply(x, i, self.on_layer_grads)
             x = self._layer(i, x, positions, cos_t, sin_t, mask, kv_out)
         return _RMSNorm.apply(x, self.p["norm"], self._gv("norm"), c.rms_norm_eps)
 

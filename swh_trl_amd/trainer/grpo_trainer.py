@@ -370,6 +370,22 @@ class GRPOTrainer:
         self._step += 1
         return inputs
 
+    def _bucket_release(self, ar, bucket_bytes: int = 100 << 20):
+        """Layer-completion callback for OverlappedAllReduce: layers finish in
+        reverse order; a bucket of consecutive layers (>= bucket_bytes) is
+        released when its lowest layer is done, the last at layer 0."""
+        m = self.model
+        state = {"hi": None}
+
+        def cb(i: int):
+            s, e = m.layer_range(i)
+            if state["hi"] is None:
+                state["hi"] = e
+            if (state["hi"] - s) * m.flat.element_size() >= bucket_bytes or i == 0:
+                ar.release(s, state["hi"])
+                state["hi"] = None
+        return cb
+
     def training_step_group(self) -> dict:
         """One optimizer step: GA micro-batches (fused), DP all-reduce, clip, AdamW."""
         a = self.args
@@ -379,14 +395,19 @@ class GRPOTrainer:
         outs = []
         tokens = sum(m["completion_ids"].shape[0] * (m["prompt_ids"].shape[1] + m["completion_ids"].shape[1])
                      for m in micro)
-        if a.fuse_micro_batches and tokens <= a.fuse_token_budget:
-            outs.append(self._loss_backward(micro))
-        else:
-            for m in micro:  # the reference schedule, one pass per micro-batch
-                o = self._loss_backward([m])
-                outs.append(o)
-        if self.world > 1:
-            swh_dist.allreduce_mean_(self.model.grad)
+        # DP: each layer's gradient all-reduce starts as soon as the (last) backward
+        # pass has finished that layer, overlapped with the rest of the backward
+        ar = swh_dist.OverlappedAllReduce(self.model.grad) if self.world > 1 else None
+        groups = [micro] if (a.fuse_micro_batches and tokens <= a.fuse_token_budget) else [[m] for m in micro]
+        for gi, grp in enumerate(groups):
+            if ar is not None and gi == len(groups) - 1:
+                self.model.on_layer_grads = self._bucket_release(ar)
+            try:
+                outs.append(self._loss_backward(grp))
+            finally:
+                self.model.on_layer_grads = None
+        if ar is not None:
+            ar.finish()
         total = max(1, self.state.max_steps)
         lr = linear_lr(self.state.global_step, total, a.learning_rate, a.warmup_steps) \
             if a.lr_scheduler_type == "linear" else a.learning_rate

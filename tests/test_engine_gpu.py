@@ -299,3 +299,31 @@ def test_prefill_dedup_matches_full_prefill(dev, monkeypatch, left_pad):
     # the copies of a prompt produce identical greedy continuations
     comp = outs["1"][2].view(n, G, C)
     assert (comp == comp[:, :1]).all()
+
+
+def test_layer_grad_hooks_fire_when_layer_grads_are_final(dev):
+    """DP overlap contract (dist.OverlappedAllReduce): the layer-input hook of
+    layer i fires in reverse layer order, after which layer i's slice of the
+    flat gradient buffer no longer changes during the rest of the backward."""
+    m = _tiny(dev, seed=9, layers=3)
+    g = torch.Generator().manual_seed(9)
+    ids = torch.randint(0, m.cfg.vocab_size, (2, 12), generator=g).to(dev)
+    snaps, order = {}, []
+
+    def cb(i):
+        order.append(i)
+        s, e = m.layer_range(i)
+        snaps[i] = m.grad[s:e].clone()
+
+    m.zero_grad()
+    m.on_layer_grads = cb
+    try:
+        lp, _ = m.logp_entropy(m.hidden_states(ids)[:, :-1], ids[:, 1:], 1.0, False)
+        lp.sum().backward()
+    finally:
+        m.on_layer_grads = None
+    torch.cuda.synchronize()
+    assert order == [2, 1, 0]
+    for i in range(3):
+        s, e = m.layer_range(i)
+        assert torch.equal(snaps[i], m.grad[s:e]) and snaps[i].abs().sum() > 0

@@ -132,3 +132,67 @@ def test_dp_exchange_and_sharding_gloo():
         assert b0[k] + b1[k] == glob[k * 16:(k + 1) * 16]          # contiguous rank slices
         for lb in (b0[k], b1[k]):
             assert all(len(set(lb[i:i + 4])) == 1 for i in range(0, 8, 4))  # whole groups per rank
+
+
+def _overlap_worker(rank, world, port, q):
+    """A 4-'layer' chain whose weight gradients live in one flat buffer, with the
+    layer-input hooks of engine/model.py releasing buckets during backward."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from swh_trl_amd import dist
+    from swh_trl_amd.engine.model import _GradReady
+    dist.init_from_env(backend="gloo")
+    L, H = 4, 8
+    flat_g = torch.zeros(3 + L * H * H + 5)        # [head | layers | tail], tail/head released by finish()
+    g = torch.Generator().manual_seed(11)
+    ws = [torch.randn(H, H, generator=g) for _ in range(L)]
+    x = (torch.randn(6, H, generator=g) * (rank + 1)).requires_grad_(True)  # rank-dependent grads
+    ar = dist.OverlappedAllReduce(flat_g)
+    order = []
+
+    def cb(i):
+        order.append(i)
+        s = 3 + i * H * H
+        ar.release(s, s + H * H)
+
+    h = x
+    params = []
+    for i in range(L):
+        h = _GradReady.apply(h, i, cb)
+        w = ws[i].clone().requires_grad_(True)
+        params.append(w)
+        h = torch.tanh(h @ w)
+    h.sum().backward()
+    ar.finish()  # drain pass 1 (its buffer held zeros)
+
+
+    # the hook fired in reverse layer order; copy grads then (this test's stand-in for in-backward accumulation)
+    local = torch.cat([torch.zeros(3)] + [w.grad.reshape(-1) for w in params] + [torch.full((5,), float(rank))])
+    q.put((rank, order, local))
+    # second pass: write grads first, then release in the hooks' order and finish
+    flat_g.copy_(local)
+    ar2 = dist.OverlappedAllReduce(flat_g)
+    for i in reversed(range(L)):
+        s = 3 + i * H * H
+        ar2.release(s, s + H * H)
+    ar2.finish()
+    q.put((rank, "reduced", flat_g.clone()))
+    torch.distributed.destroy_process_group()
+
+
+def test_overlapped_allreduce_hooks_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30500 + (os.getpid() % 1000)
+    ps = [ctx.Process(target=_overlap_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(4)]
+    for p in ps:
+        p.join(timeout=60)
+    firsts = {r: (o, loc) for r, o, loc in got if not isinstance(o, str)}
+    reduced = {r: t for r, o, t in got if isinstance(o, str)}
+    assert firsts[0][0] == [3, 2, 1, 0] and firsts[1][0] == [3, 2, 1, 0]   # reverse layer order during backward
+    mean = (firsts[0][1] + firsts[1][1]) / 2
+    for r in (0, 1):
+        torch.testing.assert_close(reduced[r], mean)                       # released ranges + finish() remainder
