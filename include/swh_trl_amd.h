@@ -250,6 +250,14 @@ int swh_silu_mul_bwd(const void *gu, const void *dout, int64_t rows, int64_t I, 
 int swh_qkv_rope(void *qkv, const int64_t *positions, const float *rope_cos, const float *rope_sin, int64_t B,
                  int64_t L, int32_t Hq, int32_t Hkv, int32_t D, void *q, void *k, void *v, int32_t backward,
                  void *stream);
+/* Folded RMSNorm weights for the decode GEMMs in ONE launch: for every job j of
+ * the device-resident table jobs[njobs] = {W [rows, cols] bf16, w [cols] bf16,
+ * out [rows, cols] bf16, rows, cols, row0 (prefix sum of rows)},
+ * out[n][k] = bf16(W[n][k] * w[k]); cols % 8 == 0, 16-B aligned rows.
+ * total_rows = sum of rows.  Run once per generate(): the policy update changes
+ * W and w (transformers applies w inside Qwen2RMSNorm every token). */
+int swh_fold_norm(const void *jobs, int32_t njobs, int64_t total_rows, void *stream);
+
 /* x[b, :] = table[ids[b], :] (bf16 rows of width H, H % 16 == 0); ss_out f32
  * [B, H/16] nullable: per 16-column chunk sums of squares of each row (the
  * RMSNorm statistic swh_decode_gemm takes as ss_in). */

@@ -219,6 +219,42 @@ __global__ __launch_bounds__(256) void silu_mul_bwd_kernel(const uint16_t *__res
     }
 }
 
+// Folded RMSNorm weights for the decode GEMMs, all matrices in one launch:
+// out_j[n][k] = bf16(W_j[n][k] * w_j[k]) (the product torch's bf16 mul forms).
+// Job table in device memory: {W, w, out, N, K} per matrix; the grid strides
+// over the concatenated rows.
+struct FoldJob {
+    const uint16_t *w;
+    const uint16_t *nw;
+    uint16_t *out;
+    int64_t rows, cols;
+    int64_t row0;  // first global row of this job
+};
+
+__global__ __launch_bounds__(256) void fold_norm_kernel(const FoldJob *__restrict__ jobs, int njobs,
+                                                        int64_t total_rows) {
+    for (int64_t gr = blockIdx.x; gr < total_rows; gr += gridDim.x) {
+        int j = 0;
+        while (j + 1 < njobs && jobs[j + 1].row0 <= gr) ++j;
+        const FoldJob jb = jobs[j];
+        const int64_t r = gr - jb.row0;
+        const uint4 *src = reinterpret_cast<const uint4 *>(jb.w + r * jb.cols);
+        const uint4 *nv = reinterpret_cast<const uint4 *>(jb.nw);
+        uint4 *dst = reinterpret_cast<uint4 *>(jb.out + r * jb.cols);
+        for (int64_t c = threadIdx.x; c < jb.cols / 8; c += blockDim.x) {
+            float a[8], b[8];
+            unpack16<SWH_BF16>(src[c], a);
+            unpack16<SWH_BF16>(nv[c], b);
+            uint32_t o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                o[q] = (uint32_t)f32_to_bf16_bits(a[2 * q] * b[2 * q]) |
+                       ((uint32_t)f32_to_bf16_bits(a[2 * q + 1] * b[2 * q + 1]) << 16);
+            dst[c] = uint4{o[0], o[1], o[2], o[3]};
+        }
+    }
+}
+
 // ss_out (nullable): per 16-column chunk sums of squares of the gathered row,
 // the RMSNorm statistic the decode GEMM prologue consumes (swh_decode_gemm ss_in)
 __global__ __launch_bounds__(256) void embed_gather_kernel(const uint16_t *__restrict__ table,
@@ -368,6 +404,14 @@ extern "C" int swh_silu_mul_bwd(const void *gu, const void *dout, int64_t rows, 
     if (rows == 0) return SWH_OK;
     silu_mul_bwd_kernel<<<ew_grid(rows * I / 8), 256, 0, static_cast<hipStream_t>(stream)>>>(
         static_cast<const uint16_t *>(gu), static_cast<const uint16_t *>(dout), rows, I, static_cast<uint16_t *>(dgu));
+    return launch_status();
+}
+
+extern "C" int swh_fold_norm(const void *jobs, int32_t njobs, int64_t total_rows, void *stream) {
+    if (!jobs || njobs <= 0 || total_rows <= 0) return SWH_E_ARG;
+    const int64_t grid = total_rows < 8192 ? total_rows : 8192;
+    fold_norm_kernel<<<dim3((unsigned)grid), 256, 0, static_cast<hipStream_t>(stream)>>>(
+        static_cast<const FoldJob *>(jobs), njobs, total_rows);
     return launch_status();
 }
 

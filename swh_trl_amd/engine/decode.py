@@ -23,6 +23,8 @@ from typing import Optional
 import torch
 
 from .. import nn_ops, ops
+from ..profiling import trace as _trace
+from .._lib import call
 from .model import CausalLM
 
 
@@ -81,6 +83,9 @@ class DecodeEngine:
                 self.fw[f"l{i}.gu_w"] = torch.empty_like(model.p[f"l{i}.gu_w"])
             self.fw["lm"] = torch.empty_like(model.lm_weight())
         self.graph = None
+        self.graph_k = None
+        self._prefill_graphs = {}
+        self.steps_per_graph = max(1, int(os.environ.get("SWH_DECODE_GRAPH_STEPS", "8")))
         self._graph_params = None
         self.params = ops.make_sample_params()
         self.want_logp = False
@@ -112,17 +117,32 @@ class DecodeEngine:
         return (self.fused and not self.want_logp and os.environ.get("SWH_FUSED_SAMPLE", "1") != "0" and
                 nn_ops.lm_head_sample_supported(self.params, self.cfg.vocab_size, self.cfg.hidden_size))
 
+    def _fold_jobs(self):
+        """Device table of (W, w_norm, W') jobs for swh_fold_norm (built once)."""
+        p = self.model.p
+        trip = []
+        for i in range(self.cfg.num_hidden_layers):
+            trip.append((p[f"l{i}.qkv_w"], p[f"l{i}.ln_in"], self.fw[f"l{i}.qkv_w"]))
+            trip.append((p[f"l{i}.gu_w"], p[f"l{i}.ln_post"], self.fw[f"l{i}.gu_w"]))
+        trip.append((self.model.lm_weight(), p["norm"], self.fw["lm"]))
+        rows, tab = 0, []
+        for w, nw, out in trip:
+            tab += [w.data_ptr(), nw.data_ptr(), out.data_ptr(), w.shape[0], w.shape[1], rows]
+            rows += w.shape[0]
+        self._fold_tab = torch.tensor(tab, dtype=torch.int64).to(self.dev)
+        self._fold_rows = rows
+        self._fold_n = len(trip)
+
     @torch.no_grad()
     def refresh_folded(self):
         """Re-derive the folded weights from the current parameters (once per
-        generate(): the optimizer changes both W and the norm weights)."""
+        generate(): the optimizer changes both W and the norm weights) — one
+        launch for all 2L + 1 matrices (swh_fold_norm)."""
         if not self.fold:
             return
-        p = self.model.p
-        for i in range(self.cfg.num_hidden_layers):
-            torch.mul(p[f"l{i}.qkv_w"], p[f"l{i}.ln_in"], out=self.fw[f"l{i}.qkv_w"])
-            torch.mul(p[f"l{i}.gu_w"], p[f"l{i}.ln_post"], out=self.fw[f"l{i}.gu_w"])
-        torch.mul(self.model.lm_weight(), p["norm"], out=self.fw["lm"])
+        if getattr(self, "_fold_tab", None) is None:
+            self._fold_jobs()
+        call("swh_fold_norm", self._fold_tab.data_ptr(), self._fold_n, self._fold_rows, ops._stream())
 
     def _normed(self, name: str, norm: str):
         """(weight, norm_w) of a normed projection: folded weight + row scale,
@@ -208,6 +228,13 @@ class DecodeEngine:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self._step()
+        # K steps per replay: one graph launch (~9 us of replay boundary) per K tokens
+        self.graph_k = None
+        if self.steps_per_graph > 1:
+            self.graph_k = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph_k):
+                for _ in range(self.steps_per_graph):
+                    self._step()
         self._graph_params = key
         for t, v in zip((self.state, self.finished, self.cur, self.out, self.out_logp, self.seen), saved):
             t.copy_(v)
@@ -312,7 +339,7 @@ class DecodeEngine:
 
     # ------------------------------------------------------------------ prefill
     @staticmethod
-    def _unique_prompts(prompt_ids: torch.Tensor, prompt_mask: torch.Tensor):
+    def _unique_prompts(prompt_ids: torch.Tensor, prompt_mask: torch.Tensor, group_size: int = 0):
         """(representative row per distinct prompt, inverse map row -> distinct
         prompt), or None when every row differs.  GRPO rolls out G copies of
         each prompt (RepeatSampler, grpo_trainer.py:97-192): the prefill runs
@@ -320,6 +347,14 @@ class DecodeEngine:
         broadcast to the copies (row-independent arithmetic, same values)."""
         if os.environ.get("SWH_PREFILL_DEDUP", "1") == "0":
             return None
+        B = prompt_ids.shape[0]
+        if group_size > 1 and B % group_size == 0:  # the caller's layout: G consecutive copies (checked)
+            ids3 = prompt_ids.view(B // group_size, group_size, -1)
+            m3 = prompt_mask.view(B // group_size, group_size, -1)
+            if bool(((ids3 == ids3[:, :1]) & (m3 == m3[:, :1])).all()):
+                rep = torch.arange(0, B, group_size, device=prompt_ids.device)
+                inv = torch.arange(B, device=prompt_ids.device) // group_size
+                return rep, inv
         key = torch.cat([prompt_ids.to(torch.int64), prompt_mask.to(torch.int64)], 1)
         uniq, inv = torch.unique(key, dim=0, return_inverse=True)
         U, B = uniq.shape[0], key.shape[0]
@@ -329,18 +364,13 @@ class DecodeEngine:
         rep.scatter_(0, inv, torch.arange(B, device=key.device))
         return rep, inv
 
-    def _prefill(self, prompt_ids: torch.Tensor, prompt_mask: torch.Tensor):
-        """Full forward over the prompt, K/V into cache slots [0, P), logits of the
-        last position.  Positions follow generate(): cumsum(mask) - 1.  Copies
-        of one prompt are prefilled once (`_unique_prompts`)."""
+    def _prefill_body(self, ids, mask, inv, padded: bool):
+        """The prefill forward on (distinct) prompt rows, K/V broadcast through
+        `inv` into the cache, last-position logits into logits_buf.  No host
+        sync inside (graph-capturable)."""
         m = self.model
-        P = prompt_ids.shape[1]
-        dedup = self._unique_prompts(prompt_ids, prompt_mask)
-        inv = None
-        if dedup is not None:
-            rep, inv = dedup
-            prompt_ids, prompt_mask = prompt_ids[rep], prompt_mask[rep]
-        pos = (prompt_mask.long().cumsum(-1) - 1).clamp(min=0)
+        P = ids.shape[1]
+        pos = (mask.long().cumsum(-1) - 1).clamp(min=0)
 
         def kv_out(i, k, v):
             if inv is not None:
@@ -348,15 +378,52 @@ class DecodeEngine:
             self.kv[i, 0, :, :, :P].copy_(k)
             self.kv[i, 1, :, :, :P].copy_(v)
 
+        h = m.hidden_states(ids, positions=pos, key_mask=mask, kv_out=kv_out, max_pos=P - 1, padded=padded)
+        if inv is None:
+            torch.mm(h[:, -1], m.lm_weight().t(), out=self.logits_buf)
+        else:
+            torch.index_select(h[:, -1] @ m.lm_weight().t(), 0, inv, out=self.logits_buf)
+
+    def _prefill(self, prompt_ids: torch.Tensor, prompt_mask: torch.Tensor, group_size: int = 0):
+        """Full forward over the prompt, K/V into cache slots [0, P), logits of the
+        last position.  Positions follow generate(): cumsum(mask) - 1.  Copies
+        of one prompt are prefilled once (`_unique_prompts`).  The forward is
+        captured into a HIP graph per (rows, P, padded) and replayed from
+        static input buffers (SWH_PREFILL_GRAPH=0: eager)."""
+        m = self.model
+        dedup = self._unique_prompts(prompt_ids, prompt_mask, group_size)
+        inv = None
+        if dedup is not None:
+            rep, inv = dedup
+            prompt_ids, prompt_mask = prompt_ids[rep], prompt_mask[rep]
+        padded = not bool(prompt_mask.bool().all())
         with torch.no_grad():
             saved = m.grad
             m.grad = None  # no grad accumulation in prefill
             try:
-                h = m.hidden_states(prompt_ids, positions=pos, key_mask=prompt_mask, kv_out=kv_out)
-                if inv is None:
-                    torch.mm(h[:, -1], m.lm_weight().t(), out=self.logits_buf)
-                else:
-                    torch.index_select(h[:, -1] @ m.lm_weight().t(), 0, inv, out=self.logits_buf)
+                if not (self.use_graph and os.environ.get("SWH_PREFILL_GRAPH", "1") != "0"):
+                    self._prefill_body(prompt_ids, prompt_mask, inv, padded)
+                    return
+                key = (tuple(prompt_ids.shape), inv is None, padded)
+                gp = self._prefill_graphs.get(key)
+                if gp is None:
+                    st = {"ids": prompt_ids.clone(), "mask": prompt_mask.clone(),
+                          "inv": None if inv is None else inv.clone()}
+                    side = torch.cuda.Stream()
+                    side.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(side):  # warm-up (library workspaces) outside capture
+                        self._prefill_body(st["ids"], st["mask"], st["inv"], padded)
+                    torch.cuda.current_stream().wait_stream(side)
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        self._prefill_body(st["ids"], st["mask"], st["inv"], padded)
+                    gp = self._prefill_graphs[key] = (g, st)
+                g, st = gp
+                st["ids"].copy_(prompt_ids)
+                st["mask"].copy_(prompt_mask)
+                if inv is not None:
+                    st["inv"].copy_(inv)
+                g.replay()
             finally:
                 m.grad = saved
 
@@ -365,7 +432,7 @@ class DecodeEngine:
     def generate(self, prompt_ids: torch.Tensor, prompt_mask: torch.Tensor, max_new_tokens: int, *,
                  temperature=1.0, top_p=1.0, top_k=None, min_p=None, repetition_penalty=1.0, greedy=False,
                  min_new_tokens=0, eos_token_id=None, pad_token_id=None, seed: int = 0, offset: int = 0,
-                 return_logp: bool = False, check_every: int = 0):
+                 return_logp: bool = False, check_every: int = 0, group_size: int = 0):
         """prompt_ids [B, P] left-padded (B == engine batch).  Returns completion ids
         [B, max_new_tokens] (pad after EOS, like `_sample`) and optional per-token
         log-probs of the drawn tokens under the processed distribution."""
@@ -384,21 +451,31 @@ class DecodeEngine:
         self.rng[0], self.rng[1] = int(seed) & ((1 << 63) - 1), int(offset)
         if repetition_penalty != 1.0:
             ops.seen_init(prompt_ids.to(torch.int64), prompt_mask, self.cfg.vocab_size, self.seen)
+        _trace("generate: setup")
         self.refresh_folded()
         if self.use_graph:
             self._ensure_graph()
+        _trace("generate: folded weights + graph")
         self.state[0], self.state[1] = 0, P
-        self._prefill(prompt_ids, prompt_mask)
+        self._prefill(prompt_ids, prompt_mask, group_size)
+        _trace("generate: prefill")
         self._sample()                      # token 0 from the prefill logits
         ops.step_advance(self.state[0:1])
         if self.fused and self._chained():  # the first chained step's input row
             nn_ops.embed_gather(self.model.p["embed"], self.cur, self.s, ss_out=self.ss)
-        for s in range(1, max_new_tokens):
+        s = 1
+        K = self.steps_per_graph
+        while s < max_new_tokens:
+            if self.use_graph and self.graph_k is not None and not check_every and s + K <= max_new_tokens:
+                self.graph_k.replay()
+                s += K
+                continue
             if self.use_graph:
                 self.graph.replay()
             else:
                 self._step()
             if check_every and s % check_every == 0 and bool(self.finished.all()):
                 break
+            s += 1
         comp = self.out[:, :max_new_tokens]
         return comp.clone(), (self.out_logp[:, :max_new_tokens].clone() if return_logp else None)

@@ -370,20 +370,27 @@ class CausalLM:
         return x + d
 
     def hidden_states(self, ids: torch.Tensor, positions: Optional[torch.Tensor] = None,
-                      key_mask: Optional[torch.Tensor] = None, kv_out=None) -> torch.Tensor:
+                      key_mask: Optional[torch.Tensor] = None, kv_out=None, max_pos: Optional[int] = None,
+                      padded: Optional[bool] = None) -> torch.Tensor:
         """Final-normed hidden states [B, L, H].
 
         positions: [B, L] (default arange, the transformers training forward);
         key_mask: [B, L] bool/int, 0 = padding key (left-padded prompts).
+        max_pos / padded: host-known bounds on positions and whether key_mask
+        has zeros — given both, the forward makes no host sync (graph capture).
         """
         c = self.cfg
         B, L = ids.shape
         if positions is None:
             positions = torch.arange(L, device=ids.device).expand(B, L)
-        cos_t, sin_t = self.rope(int(positions.max().item()) + 1 if positions.numel() else 1)
+        if max_pos is None:
+            max_pos = int(positions.max().item()) if positions.numel() else 0
+        cos_t, sin_t = self.rope(max_pos + 1)
         positions = positions.to(torch.int64).contiguous()
         mask = None
-        if key_mask is not None and not bool(key_mask.bool().all()):
+        if padded is None:
+            padded = key_mask is not None and not bool(key_mask.bool().all())
+        if key_mask is not None and padded:
             km = key_mask.bool()
             causal = torch.ones(L, L, device=ids.device, dtype=torch.bool).tril()
             # a query with no valid key at all (left padding) sees itself, so no

@@ -4,6 +4,9 @@ switches it on for the timed region.  Replaces the reference's wall-clock
 `profiling_context` (trl/extras/profiling.py:31-100) for device work."""
 from __future__ import annotations
 
+import os
+import sys
+import time
 from collections import defaultdict
 from contextlib import contextmanager
 
@@ -46,3 +49,16 @@ def summary() -> dict:
         out[k] = {"launches": len(ev), "total_ms": tot, "avg_us": 1000.0 * tot / max(1, len(ev)),
                   "bytes_per_launch": _bytes[k] / max(1, len(ev))}
     return out
+
+
+_TRACE = os.environ.get("SWH_TRACE", "0") == "1"
+_T0 = [time.time()]
+
+
+def trace(msg: str):
+    """SWH_TRACE=1: synchronised phase timings on stderr (diagnostics only)."""
+    if _TRACE:
+        import torch
+        torch.cuda.synchronize()
+        now = time.time()
+        print(f"[swh {now - _T0[0]:8.3f}s] {msg}", file=sys.stderr, flush=True)

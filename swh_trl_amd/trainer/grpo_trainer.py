@@ -229,7 +229,8 @@ class GRPOTrainer:
         completion_ids, _ = eng.generate(prompt_ids, prompt_mask, self.max_completion_length,
                                          eos_token_id=self.eos_token_id, pad_token_id=self.pad_token_id,
                                          seed=seed, offset=self._gen_count * (self.max_completion_length + 1),
-                                         check_every=a.decode_check_every, **self.gen_kwargs)
+                                         check_every=a.decode_check_every, group_size=self.num_generations,
+                                         **self.gen_kwargs)
         self._gen_count += 1
         _trace("generated")
         eos = [] if self.eos_token_id is None else self.eos_token_id

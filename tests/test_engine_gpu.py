@@ -327,3 +327,26 @@ def test_layer_grad_hooks_fire_when_layer_grads_are_final(dev):
     for i in range(3):
         s, e = m.layer_range(i)
         assert torch.equal(snaps[i], m.grad[s:e]) and snaps[i].abs().sum() > 0
+
+
+def test_fold_kernel_equals_torch_mul_and_group_dedup(dev):
+    """swh_fold_norm (all folded decode weights in one launch) is bit-identical
+    to torch's bf16 W * w; the group-size hint gives the same prefill plan as
+    the generic unique() path."""
+    from swh_trl_amd.engine import DecodeEngine
+    m = _tiny(dev, seed=10, layers=2)
+    with torch.no_grad():
+        for k in ("l0.ln_in", "l1.ln_post", "norm"):
+            m.p[k].copy_(1 + 0.1 * torch.randn_like(m.p[k].float()).to(m.p[k].dtype))
+    eng = DecodeEngine(m, 8, 6, 4)
+    eng.refresh_folded()
+    p = m.p
+    assert torch.equal(eng.fw["l0.qkv_w"], p["l0.qkv_w"] * p["l0.ln_in"])
+    assert torch.equal(eng.fw["l1.gu_w"], p["l1.gu_w"] * p["l1.ln_post"])
+    assert torch.equal(eng.fw["lm"], m.lm_weight() * p["norm"])
+    ids = torch.randint(0, m.cfg.vocab_size, (2, 6), device=dev).repeat_interleave(4, 0)
+    mask = torch.ones_like(ids, dtype=torch.int32)
+    rep, inv = DecodeEngine._unique_prompts(ids, mask, 4)
+    assert rep.tolist() == [0, 4] and inv.tolist() == [0, 0, 0, 0, 1, 1, 1, 1]
+    rep2, inv2 = DecodeEngine._unique_prompts(ids, mask)
+    assert torch.equal(ids[rep2][inv2], ids)
