@@ -100,8 +100,11 @@ def ku_sweep(eng, m):
         return 1000.0 * e0.elapsed_time(e1) / (3 * L)
 
     print("cfg          nw " + " ".join(f"{k:>9s}" for k in shapes), flush=True)
-    for cf in (None, "1,1,1", "2,1,1", "2,1,2", "4,4,1,0,2", "4,4,1,0,4", "2,4,1,0,4", "2,2,1,0,2", "4,2,1,0,2",
-               "1,2,1,0,2", "1,4,1,0,4", "2,2,2,0,2", "4,4,2,0,4", "4,2,1,1,2", "4,4,1,1,4"):
+    cfgs = os.environ.get("SWH_SWEEP_CFGS")
+    cfgs = [None if c == "None" else c for c in cfgs.split(";")] if cfgs else \
+        (None, "1,1,1", "2,1,1", "2,1,2", "4,4,1,0,2", "4,4,1,0,4", "2,4,1,0,4", "2,2,1,0,2", "4,2,1,0,2",
+         "1,2,1,0,2", "1,4,1,0,4", "2,2,2,0,2", "4,4,2,0,4", "4,2,1,1,2", "4,4,1,1,4")
+    for cf in cfgs:
         for ku in ("",):
             for nw in ("8",):
                 for k, v in (("SWH_GEMM_CFG", cf), ("SWH_GEMM_NW", nw)):
