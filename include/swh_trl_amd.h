@@ -250,6 +250,24 @@ int swh_silu_mul_bwd(const void *gu, const void *dout, int64_t rows, int64_t I, 
 int swh_qkv_rope(void *qkv, const int64_t *positions, const float *rope_cos, const float *rope_sin, int64_t B,
                  int64_t L, int32_t Hq, int32_t Hkv, int32_t D, void *q, void *k, void *v, int32_t backward,
                  void *stream);
+/* Causal GQA attention over full sequences (training / scoring / prefill),
+ * bf16 [B, H, L, D] tensors (D = 64 or 128), fp32 softmax statistics.
+ * Forward writes out and lse [B, Hq, L] (natural log of the row sum of
+ * exp(scale * q k), the backward's statistic).  Backward takes dout and
+ * writes dq, dk, dv (dk/dv summed over the Hq/Hkv query heads of each KV
+ * head); delta [B, Hq, L] fp32 is workspace.  key_mask int32 [B, L] (0 = pad)
+ * and first_valid int32 [B] are both null (pure causal) or both given: key k
+ * is seen by query q iff k <= q and (key_mask[k] or (k == q and
+ * q < first_valid)).  Replaces torch SDPA in the transformers Qwen2/Llama
+ * attention of the reference's scoring and training forwards
+ * (grpo_trainer.py:1249, ppo_trainer.py:86-96). */
+int swh_attn_fwd(const void *q, const void *k, const void *v, int64_t B, int32_t Hq, int32_t Hkv, int64_t L,
+                 int32_t D, float scale, const int32_t *key_mask, const int32_t *first_valid, void *out, float *lse,
+                 void *stream);
+int swh_attn_bwd(const void *q, const void *k, const void *v, const void *out, const void *dout, const float *lse,
+                 int64_t B, int32_t Hq, int32_t Hkv, int64_t L, int32_t D, float scale, const int32_t *key_mask,
+                 const int32_t *first_valid, float *delta, void *dq, void *dk, void *dv, void *stream);
+
 /* Folded RMSNorm weights for the decode GEMMs in ONE launch: for every job j of
  * the device-resident table jobs[njobs] = {W [rows, cols] bf16, w [cols] bf16,
  * out [rows, cols] bf16, rows, cols, row0 (prefix sum of rows)},

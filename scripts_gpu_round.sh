@@ -18,6 +18,8 @@ for step in "$@"; do
     benchtuned) SWH_GEMM_TABLE=gpurun_out/gemm_tuned.csv run benchtuned 600 python bench.py --steps 3 --warmup 2 --no-cpu-baseline ;;
     lmk) run lmk 300 python -u -m pytest tests/test_kernels_gpu.py -x -v -m gpu -k "lm_head or decode_gemm or sampler" --timeout 120 --timeout-method thread ;;
     decab) run dec0 300 python tools/bench_decode.py && for v in vA vB; do SWH_LIB_PATH=tools/_build/$v.so run dec_$v 300 python tools/bench_decode.py || exit 1; done ;;
+    attn) run attn 300 python -u -m pytest tests/test_kernels_gpu.py -x -v -m gpu -k attention --timeout 120 --timeout-method thread ;;
+    benchab) SWH_ATTN=torch run bench_torchattn 600 python bench.py --steps 2 --warmup 1 --no-cpu-baseline && run bench_hipattn 600 python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     kern) run kern 600 python -m pytest tests/test_kernels_gpu.py -q -m gpu ;;
     kernx) run kernx 600 python -m pytest tests/test_kernels_gpu.py -q -m gpu -x ;;
     dec) run dec 300 python tools/bench_decode.py ;;

@@ -70,6 +70,9 @@ SIGNATURES = {
     "swh_rmsnorm_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "swh_silu_mul_fwd": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp]),
     "swh_silu_mul_bwd": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "swh_attn_fwd": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "swh_attn_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i64, c_i32, c_f32, c_vp, c_vp,
+                             c_vp, c_vp, c_vp, c_vp, c_vp]),
     "swh_fold_norm": (c_i32, [c_vp, c_i32, c_i64, c_vp]),
     "swh_embed_gather": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "swh_qkv_rope": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i32,

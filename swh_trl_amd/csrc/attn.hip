@@ -1,0 +1,477 @@
+// Causal GQA attention for the full-sequence (training / scoring / prefill)
+// forward and backward, bf16 in / out, fp32 softmax statistics.
+//
+// Replaces torch SDPA in the transformers Qwen2 attention the reference runs
+// for every scoring and training forward (grpo_trainer.py:1249 ->
+// _get_per_token_logps_and_entropies; the PPO forwards ppo_trainer.py:
+// 86-96): at the GRPO shape (64 sequences x 14/2 heads x 384 positions x 64)
+// aotriton's flash kernels run ~150 us forward / ~430 us backward per layer.
+//
+// Orientation (the decode kernel's, csrc/decode.hip attn_decode_kernel): one
+// WAVE owns 16 queries and walks the keys in blocks of 32.  S^T = K Q^T on
+// v_mfma_f32_16x16x32_bf16 with the 16 queries as the MFMA columns, so each
+// lane holds one query and 8 keys: the softmax statistics need two lane
+// shuffles, and P^T, packed to bf16 pairs, is the B operand of O^T = V^T P^T
+// as it stands; V^T comes from the wave's own LDS tile through
+// ds_read_b64_tr_b16 (4 keys x 1 dim per lane).  No workgroup barriers: the
+// 4 waves of a workgroup are independent (their K/V reads share the CU's L1).
+//
+// Backward (FA2 split): delta = rowsum(dO * O); the dQ kernel repeats the
+// forward walk (S^T, dP^T = V dO^T, dS^T = P^T (dP^T - delta), dQ^T += K^T dS^T);
+// the dK/dV kernel gives a wave 16 KEYS and walks the queries of all the
+// heads of its KV group (GQA sum): S = Q K^T with keys as the columns,
+// dV^T += dO^T P, dK^T += Q^T dS.
+//
+// Visibility (transformers' 4-D mask as built in engine/model.py): key k is
+// seen by query q iff k <= q and (key_mask[k] or (k == q and q has no valid
+// key at or before it)); first_valid[b] = index of the row's first valid key.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "common.hpp"
+
+namespace swh {
+namespace {
+
+typedef __bf16 bf16x8a __attribute__((ext_vector_type(8)));
+typedef float f32x4a __attribute__((ext_vector_type(4)));
+typedef float f32x2a __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2a __attribute__((ext_vector_type(2)));
+typedef short bf16x4sa __attribute__((ext_vector_type(4)));
+
+constexpr int kFaWaves = 4;
+constexpr int kFaThreads = 64 * kFaWaves;
+
+__device__ __forceinline__ bf16x4sa fa_tr16(const uint16_t *p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) bf16x4sa *)(const_cast<uint16_t *>(p)));
+}
+
+struct FaArgs {
+    const uint16_t *q, *k, *v, *o, *dout;  // [B, H, L, D]
+    const int32_t *key_mask;               // [B, L] or null (no padding)
+    const int32_t *first_valid;            // [B] or null
+    float *lse, *delta;                    // [B, Hq, L]
+    uint16_t *out, *dq, *dk, *dv;
+    int B, Hq, Hkv, L;
+    float scale;
+};
+
+// the 8 keys a lane holds in a 32-key block: k0 + 16 t + 4 g + r, t = 0, 1, r = 0..3
+struct FaKeyMask {
+    int32_t v[8];  // key_mask of those keys (1 when unpadded)
+};
+__device__ __forceinline__ FaKeyMask fa_key_mask(const FaArgs &a, int b, int k0, int g) {
+    FaKeyMask m;
+    if (!a.key_mask) {  // uniform branch: the unpadded causal case reads nothing
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m.v[j] = 1;
+        return m;
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int k = k0 + 16 * t + 4 * g;  // 4 consecutive keys, 16-B aligned (k % 4 == 0, L % 4 not required:
+#pragma unroll                              // clamp each)
+        for (int r = 0; r < 4; ++r) m.v[4 * t + r] = a.key_mask[(int64_t)b * a.L + min(k + r, a.L - 1)];
+    }
+    return m;
+}
+// branch-free visibility of key k for query q (q < L): causal, padding, self when q has no valid key
+__device__ __forceinline__ bool fa_vis(int q, int k, int L, int km, int fv) {
+    return (k <= q) & (k < L) & ((km != 0) | ((k == q) & (q < fv)));
+}
+
+// rows [r0, r0 + 32) of a [L, D] slab (clamped) as the two 16-row A fragments of
+// one 32-row block: lane (g, c16) <- row r0 + 16 t + c16, dims 32 c + 8 g
+template <int D>
+__device__ __forceinline__ void fa_load_rows(u32x4 (&r)[2][D / 32], const uint16_t *base, int r0, int L, int c16,
+                                             int g) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int row = min(r0 + 16 * t + c16, L - 1);
+#pragma unroll
+        for (int c = 0; c < D / 32; ++c) r[t][c] = *reinterpret_cast<const u32x4 *>(base + (int64_t)row * D + c * 32 + g * 8);
+    }
+}
+
+// O^T[d][n] += X^T[d][rows of the block] Y^T[rows][n] where the block's 32 rows
+// X [32][D] are parked in the wave's LDS tile and Y^T comes as 8 fp32 values per
+// lane (rows 4g..4g+3 of the block's first 16, then of its second 16, column c16):
+// the decode kernel's P V step (csrc/decode.hip)
+template <int D, int VS>
+__device__ __forceinline__ void fa_xty(f32x4a (&o)[D / 16], uint16_t *tile, const u32x4 (&x)[2][D / 32],
+                                       const float (&y)[8], int c16, int g) {
+#pragma unroll
+    for (int c = 0; c < D / 32; ++c) {
+        *reinterpret_cast<u32x4 *>(tile + c16 * VS + c * 32 + g * 8) = x[0][c];
+        *reinterpret_cast<u32x4 *>(tile + (16 + c16) * VS + c * 32 + g * 8) = x[1][c];
+    }
+    uint32_t pb[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+        pb[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2a{y[2 * h], y[2 * h + 1]}, bf16x2a));
+    const bf16x8a yb = __builtin_bit_cast(bf16x8a, u32x4{pb[0], pb[1], pb[2], pb[3]});
+    const int qq = c16 >> 2, pq = c16 & 3;
+#pragma unroll
+    for (int d = 0; d < D / 16; ++d) {
+        const bf16x4sa lo = fa_tr16(tile + (4 * g + qq) * VS + d * 16 + 4 * pq);
+        const bf16x4sa hi = fa_tr16(tile + (16 + 4 * g + qq) * VS + d * 16 + 4 * pq);
+        const bf16x8a xa = __builtin_bit_cast(
+            bf16x8a, u32x4{__builtin_bit_cast(uint2, lo).x, __builtin_bit_cast(uint2, lo).y,
+                           __builtin_bit_cast(uint2, hi).x, __builtin_bit_cast(uint2, hi).y});
+        o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, yb, o[d], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the tile is rewritten by the next block
+}
+
+template <int D>
+__device__ __forceinline__ void fa_copy(u32x4 (&dst)[2][D / 32], const u32x4 (&src)[2][D / 32]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int c = 0; c < D / 32; ++c) dst[t][c] = src[t][c];
+}
+
+// S^T-like product: out[t][r] = sum_d A[row 16 t + 4 g + r][d] B[col c16][d]
+template <int D>
+__device__ __forceinline__ void fa_abt(f32x4a (&s)[2], const u32x4 (&a)[2][D / 32], const u32x4 (&bq)[D / 32]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        f32x4a acc = f32x4a{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < D / 32; ++c)
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8a, a[t][c]),
+                                                          __builtin_bit_cast(bf16x8a, bq[c]), acc, 0, 0, 0);
+        s[t] = acc;
+    }
+}
+
+template <int D>
+constexpr int fa_vs() { return D + (D == 64 ? 8 : 16); }
+
+// ---- forward: grid (ceil(L / 64), Hq, B), 4 waves x 16 queries
+template <int D>
+__global__ __launch_bounds__(kFaThreads) void fa_fwd_kernel(FaArgs a) {
+    constexpr int DC = D / 32, DB = D / 16, VS = fa_vs<D>();
+    __shared__ __attribute__((aligned(16))) uint16_t tiles[kFaWaves][32 * VS];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
+    const int b = blockIdx.z, h = blockIdx.y, kvh = h / (a.Hq / a.Hkv), L = a.L;
+    const int q0 = blockIdx.x * 64 + wid * 16;
+    if (q0 >= L) return;
+    const int qc = min(q0 + c16, L - 1);  // this lane's query column
+    const int fv = a.first_valid ? a.first_valid[b] : 0;
+    const uint16_t *qb_ = a.q + ((int64_t)b * a.Hq + h) * L * D;
+    const uint16_t *kb_ = a.k + ((int64_t)b * a.Hkv + kvh) * L * D;
+    const uint16_t *vb_ = a.v + ((int64_t)b * a.Hkv + kvh) * L * D;
+    u32x4 qf[DC];
+#pragma unroll
+    for (int c = 0; c < DC; ++c) qf[c] = *reinterpret_cast<const u32x4 *>(qb_ + (int64_t)qc * D + c * 32 + g * 8);
+    float m = kNegInf, l = 0.f;
+    f32x4a o[DB];
+#pragma unroll
+    for (int d = 0; d < DB; ++d) o[d] = f32x4a{0.f, 0.f, 0.f, 0.f};
+    uint16_t *tile = tiles[wid];
+    const int kend = min(q0 + 16, L);  // causal: keys < kend
+    u32x4 kr[2][DC], vr[2][DC], kn[2][DC], vn[2][DC];
+    fa_load_rows<D>(kn, kb_, 0, L, c16, g);
+    fa_load_rows<D>(vn, vb_, 0, L, c16, g);
+    for (int k0 = 0; k0 < kend; k0 += 32) {
+        fa_copy<D>(kr, kn);
+        fa_copy<D>(vr, vn);
+        if (k0 + 32 < kend) {  // the next block streams while this one computes
+            fa_load_rows<D>(kn, kb_, k0 + 32, L, c16, g);
+            fa_load_rows<D>(vn, vb_, k0 + 32, L, c16, g);
+        }
+        f32x4a s[2];
+        fa_abt<D>(s, kr, qf);
+        const FaKeyMask km = fa_key_mask(a, b, k0, g);
+        float sv[8], mx = m;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int key = k0 + 16 * t + 4 * g + r;
+                const float v = fa_vis(q0 + c16, key, L, km.v[4 * t + r], fv) ? s[t][r] * a.scale : kNegInf;
+                sv[4 * t + r] = v;
+                mx = fmaxf(mx, v);
+            }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+        const float corr = (mx == kNegInf) ? 1.f : __expf(m - mx);
+        l *= corr;
+#pragma unroll
+        for (int d = 0; d < DB; ++d) o[d] *= corr;
+        m = mx;
+        float p[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            p[j] = (mx == kNegInf) ? 0.f : __expf(sv[j] - mx);
+            l += p[j];
+        }
+        fa_xty<D, VS>(o, tile, vr, p, c16, g);
+    }
+    l += __shfl_xor(l, 16, kWave);
+    l += __shfl_xor(l, 32, kWave);
+    if (q0 + c16 < L) {
+        uint16_t *ob = a.out + (((int64_t)b * a.Hq + h) * L + q0 + c16) * D;
+        const float inv = 1.f / l;
+#pragma unroll
+        for (int d = 0; d < DB; ++d) {
+            const uint32_t lo = (uint32_t)f32_to_bf16_bits(o[d][0] * inv) | ((uint32_t)f32_to_bf16_bits(o[d][1] * inv) << 16);
+            const uint32_t hi = (uint32_t)f32_to_bf16_bits(o[d][2] * inv) | ((uint32_t)f32_to_bf16_bits(o[d][3] * inv) << 16);
+            *reinterpret_cast<uint2 *>(ob + d * 16 + 4 * g) = uint2{lo, hi};
+        }
+        if (g == 0) a.lse[((int64_t)b * a.Hq + h) * L + q0 + c16] = m + logf(l);
+    }
+}
+
+// ---- backward preprocess: delta[q] = sum_d dO[q][d] O[q][d] (one wave per 4 queries... one thread per query)
+template <int D>
+__global__ __launch_bounds__(256) void fa_delta_kernel(FaArgs a, int64_t rows) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= rows) return;
+    const uint4 *o = reinterpret_cast<const uint4 *>(a.o + r * D);
+    const uint4 *d = reinterpret_cast<const uint4 *>(a.dout + r * D);
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < D / 8; ++c) {
+        float x[8], y[8];
+        unpack16<SWH_BF16>(o[c], x);
+        unpack16<SWH_BF16>(d[c], y);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s = fmaf(x[j], y[j], s);
+    }
+    a.delta[r] = s;
+}
+
+// ---- dQ: the forward walk with dP^T = V dO^T and dQ^T += K^T dS^T
+template <int D>
+__global__ __launch_bounds__(kFaThreads) void fa_dq_kernel(FaArgs a) {
+    constexpr int DC = D / 32, DB = D / 16, VS = fa_vs<D>();
+    __shared__ __attribute__((aligned(16))) uint16_t tiles[kFaWaves][32 * VS];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
+    const int b = blockIdx.z, h = blockIdx.y, kvh = h / (a.Hq / a.Hkv), L = a.L;
+    const int q0 = blockIdx.x * 64 + wid * 16;
+    if (q0 >= L) return;
+    const int qc = min(q0 + c16, L - 1);
+    const int fv = a.first_valid ? a.first_valid[b] : 0;
+    const int64_t qrow = ((int64_t)b * a.Hq + h) * L;
+    const uint16_t *kb_ = a.k + ((int64_t)b * a.Hkv + kvh) * L * D;
+    const uint16_t *vb_ = a.v + ((int64_t)b * a.Hkv + kvh) * L * D;
+    u32x4 qf[DC], df[DC];
+#pragma unroll
+    for (int c = 0; c < DC; ++c) {
+        qf[c] = *reinterpret_cast<const u32x4 *>(a.q + (qrow + qc) * D + c * 32 + g * 8);
+        df[c] = *reinterpret_cast<const u32x4 *>(a.dout + (qrow + qc) * D + c * 32 + g * 8);
+    }
+    const float lse = a.lse[qrow + qc], dl = a.delta[qrow + qc];
+    f32x4a acc[DB];
+#pragma unroll
+    for (int d = 0; d < DB; ++d) acc[d] = f32x4a{0.f, 0.f, 0.f, 0.f};
+    uint16_t *tile = tiles[wid];
+    const int kend = min(q0 + 16, L);
+    u32x4 kr[2][DC], vr[2][DC], kn[2][DC], vn[2][DC];
+    fa_load_rows<D>(kn, kb_, 0, L, c16, g);
+    fa_load_rows<D>(vn, vb_, 0, L, c16, g);
+    for (int k0 = 0; k0 < kend; k0 += 32) {
+        fa_copy<D>(kr, kn);
+        fa_copy<D>(vr, vn);
+        if (k0 + 32 < kend) {
+            fa_load_rows<D>(kn, kb_, k0 + 32, L, c16, g);
+            fa_load_rows<D>(vn, vb_, k0 + 32, L, c16, g);
+        }
+        f32x4a s[2], dp[2];
+        fa_abt<D>(s, kr, qf);
+        fa_abt<D>(dp, vr, df);
+        const FaKeyMask km = fa_key_mask(a, b, k0, g);
+        float ds[8];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int key = k0 + 16 * t + 4 * g + r;
+                const float p = fa_vis(q0 + c16, key, L, km.v[4 * t + r], fv) ? __expf(s[t][r] * a.scale - lse) : 0.f;
+                ds[4 * t + r] = p * (dp[t][r] - dl);
+            }
+        fa_xty<D, VS>(acc, tile, kr, ds, c16, g);
+    }
+    if (q0 + c16 < L) {
+        uint16_t *qb = a.dq + (qrow + q0 + c16) * D;
+#pragma unroll
+        for (int d = 0; d < DB; ++d) {
+            const uint32_t lo = (uint32_t)f32_to_bf16_bits(acc[d][0] * a.scale) |
+                                ((uint32_t)f32_to_bf16_bits(acc[d][1] * a.scale) << 16);
+            const uint32_t hi = (uint32_t)f32_to_bf16_bits(acc[d][2] * a.scale) |
+                                ((uint32_t)f32_to_bf16_bits(acc[d][3] * a.scale) << 16);
+            *reinterpret_cast<uint2 *>(qb + d * 16 + 4 * g) = uint2{lo, hi};
+        }
+    }
+}
+
+// ---- dK / dV: a wave owns 16 keys, walks the queries of every head of its group
+template <int D>
+__global__ __launch_bounds__(kFaThreads) void fa_dkdv_kernel(FaArgs a) {
+    constexpr int DC = D / 32, DB = D / 16, VS = fa_vs<D>();
+    __shared__ __attribute__((aligned(16))) uint16_t tiles[kFaWaves][32 * VS];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
+    const int b = blockIdx.z, kvh = blockIdx.y, L = a.L, G = a.Hq / a.Hkv;
+    const int k0w = blockIdx.x * 64 + wid * 16;
+    if (k0w >= L) return;
+    const int kc = min(k0w + c16, L - 1);  // this lane's key column
+    const int fv = a.first_valid ? a.first_valid[b] : 0;
+    const int kmv = a.key_mask ? a.key_mask[(int64_t)b * L + kc] : 1;
+    const int64_t kvrow = ((int64_t)b * a.Hkv + kvh) * L;
+    u32x4 kf[DC], vf[DC];
+#pragma unroll
+    for (int c = 0; c < DC; ++c) {
+        kf[c] = *reinterpret_cast<const u32x4 *>(a.k + (kvrow + kc) * D + c * 32 + g * 8);
+        vf[c] = *reinterpret_cast<const u32x4 *>(a.v + (kvrow + kc) * D + c * 32 + g * 8);
+    }
+    f32x4a dk[DB], dv[DB];
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+        dk[d] = f32x4a{0.f, 0.f, 0.f, 0.f};
+        dv[d] = f32x4a{0.f, 0.f, 0.f, 0.f};
+    }
+    uint16_t *tile = tiles[wid];
+    const int qstart = k0w & ~31;  // causal: queries >= the wave's first key (32-aligned blocks)
+    const int nb = (L - qstart + 31) / 32, nit = G * nb;  // (head, query block) rounds
+    // round it: head kvh * G + it / nb, query rows r0 = qstart + 32 (it % nb); the next round's
+    // Q / dO rows and softmax statistics stream while this one computes
+    u32x4 qr[2][DC], dr[2][DC], qn[2][DC], dn[2][DC];
+    float ls[8], dl[8], lsn[8], dln[8];
+    auto fetch = [&](int it, u32x4(&q_)[2][DC], u32x4(&d_)[2][DC], float(&l_)[8], float(&e_)[8]) {
+        const int h = kvh * G + it / nb, r0 = qstart + 32 * (it % nb);
+        const int64_t qrow = ((int64_t)b * a.Hq + h) * L;
+        fa_load_rows<D>(q_, a.q + qrow * D, r0, L, c16, g);
+        fa_load_rows<D>(d_, a.dout + qrow * D, r0, L, c16, g);
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int qq = min(r0 + 16 * t + 4 * g + r, L - 1);
+                l_[4 * t + r] = a.lse[qrow + qq];
+                e_[4 * t + r] = a.delta[qrow + qq];
+            }
+    };
+    fetch(0, qn, dn, lsn, dln);
+    for (int it = 0; it < nit; ++it) {
+        fa_copy<D>(qr, qn);
+        fa_copy<D>(dr, dn);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            ls[j] = lsn[j];
+            dl[j] = dln[j];
+        }
+        if (it + 1 < nit) fetch(it + 1, qn, dn, lsn, dln);
+        const int r0 = qstart + 32 * (it % nb);
+        f32x4a s[2], dp[2];
+        fa_abt<D>(s, qr, kf);   // S[q = r0 + 16 t + 4 g + r][key c16]
+        fa_abt<D>(dp, dr, vf);  // dP likewise
+        float p[8], ds[8];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int q = r0 + 16 * t + 4 * g + r;
+                const bool vis = (q < L) & fa_vis(q, k0w + c16, L, kmv, fv);
+                const float pv = vis ? __expf(s[t][r] * a.scale - ls[4 * t + r]) : 0.f;
+                p[4 * t + r] = pv;
+                ds[4 * t + r] = vis ? pv * (dp[t][r] - dl[4 * t + r]) : 0.f;
+            }
+        fa_xty<D, VS>(dv, tile, dr, p, c16, g);
+        fa_xty<D, VS>(dk, tile, qr, ds, c16, g);
+    }
+    if (k0w + c16 < L) {
+        uint16_t *kb = a.dk + (kvrow + k0w + c16) * D;
+        uint16_t *vb = a.dv + (kvrow + k0w + c16) * D;
+#pragma unroll
+        for (int d = 0; d < DB; ++d) {
+            const uint32_t klo = (uint32_t)f32_to_bf16_bits(dk[d][0] * a.scale) |
+                                 ((uint32_t)f32_to_bf16_bits(dk[d][1] * a.scale) << 16);
+            const uint32_t khi = (uint32_t)f32_to_bf16_bits(dk[d][2] * a.scale) |
+                                 ((uint32_t)f32_to_bf16_bits(dk[d][3] * a.scale) << 16);
+            *reinterpret_cast<uint2 *>(kb + d * 16 + 4 * g) = uint2{klo, khi};
+            const uint32_t vlo = (uint32_t)f32_to_bf16_bits(dv[d][0]) | ((uint32_t)f32_to_bf16_bits(dv[d][1]) << 16);
+            const uint32_t vhi = (uint32_t)f32_to_bf16_bits(dv[d][2]) | ((uint32_t)f32_to_bf16_bits(dv[d][3]) << 16);
+            *reinterpret_cast<uint2 *>(vb + d * 16 + 4 * g) = uint2{vlo, vhi};
+        }
+    }
+}
+
+bool fa_args_ok(const void *q, const void *k, const void *v, int64_t B, int32_t Hq, int32_t Hkv, int64_t L,
+                int32_t D) {
+    return q && k && v && B > 0 && Hq > 0 && Hkv > 0 && Hq % Hkv == 0 && L > 0 && L <= (1 << 20) &&
+           B <= 65535 && Hq <= 65535 && (D == 64 || D == 128);
+}
+
+}  // namespace
+}  // namespace swh
+
+using namespace swh;
+
+extern "C" int swh_attn_fwd(const void *q, const void *k, const void *v, int64_t B, int32_t Hq, int32_t Hkv,
+                            int64_t L, int32_t D, float scale, const int32_t *key_mask, const int32_t *first_valid,
+                            void *out, float *lse, void *stream) {
+    if (!fa_args_ok(q, k, v, B, Hq, Hkv, L, D) || !out || !lse || (!key_mask != !first_valid)) return SWH_E_ARG;
+    FaArgs a{};
+    a.q = static_cast<const uint16_t *>(q);
+    a.k = static_cast<const uint16_t *>(k);
+    a.v = static_cast<const uint16_t *>(v);
+    a.key_mask = key_mask;
+    a.first_valid = first_valid;
+    a.lse = lse;
+    a.out = static_cast<uint16_t *>(out);
+    a.B = (int)B;
+    a.Hq = Hq;
+    a.Hkv = Hkv;
+    a.L = (int)L;
+    a.scale = scale;
+    const dim3 grid((unsigned)((L + 63) / 64), (unsigned)Hq, (unsigned)B);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (D == 64) fa_fwd_kernel<64><<<grid, kFaThreads, 0, s>>>(a);
+    else fa_fwd_kernel<128><<<grid, kFaThreads, 0, s>>>(a);
+    return launch_status();
+}
+
+extern "C" int swh_attn_bwd(const void *q, const void *k, const void *v, const void *out, const void *dout,
+                            const float *lse, int64_t B, int32_t Hq, int32_t Hkv, int64_t L, int32_t D, float scale,
+                            const int32_t *key_mask, const int32_t *first_valid, float *delta, void *dq, void *dk,
+                            void *dv, void *stream) {
+    if (!fa_args_ok(q, k, v, B, Hq, Hkv, L, D) || !out || !dout || !lse || !delta || !dq || !dk || !dv ||
+        (!key_mask != !first_valid))
+        return SWH_E_ARG;
+    FaArgs a{};
+    a.q = static_cast<const uint16_t *>(q);
+    a.k = static_cast<const uint16_t *>(k);
+    a.v = static_cast<const uint16_t *>(v);
+    a.o = static_cast<const uint16_t *>(out);
+    a.dout = static_cast<const uint16_t *>(dout);
+    a.key_mask = key_mask;
+    a.first_valid = first_valid;
+    a.lse = const_cast<float *>(lse);
+    a.delta = delta;
+    a.dq = static_cast<uint16_t *>(dq);
+    a.dk = static_cast<uint16_t *>(dk);
+    a.dv = static_cast<uint16_t *>(dv);
+    a.B = (int)B;
+    a.Hq = Hq;
+    a.Hkv = Hkv;
+    a.L = (int)L;
+    a.scale = scale;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int64_t rows = B * Hq * L;
+    const dim3 gq((unsigned)((L + 63) / 64), (unsigned)Hq, (unsigned)B);
+    const dim3 gk((unsigned)((L + 63) / 64), (unsigned)Hkv, (unsigned)B);
+    if (D == 64) {
+        fa_delta_kernel<64><<<dim3((unsigned)((rows + 255) / 256)), 256, 0, s>>>(a, rows);
+        fa_dq_kernel<64><<<gq, kFaThreads, 0, s>>>(a);
+        fa_dkdv_kernel<64><<<gk, kFaThreads, 0, s>>>(a);
+    } else {
+        fa_delta_kernel<128><<<dim3((unsigned)((rows + 255) / 256)), 256, 0, s>>>(a, rows);
+        fa_dq_kernel<128><<<gq, kFaThreads, 0, s>>>(a);
+        fa_dkdv_kernel<128><<<gk, kFaThreads, 0, s>>>(a);
+    }
+    return launch_status();
+}

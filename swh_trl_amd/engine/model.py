@@ -16,6 +16,7 @@ MLP, rotate-half RoPE with bf16 cos/sin, GQA attention scaled by D^-0.5.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -242,6 +243,10 @@ class CausalLM:
         self._rope = None
         # backward hook: called with layer index i once layer i's weight gradients are final
         self.on_layer_grads = None
+        # full-sequence attention: torch SDPA (aotriton) by default — at the GRPO shape it
+        # is still 10 % faster per step than csrc/attn.hip (fwd 169 + bwd 457 us vs
+        # 150 + 430 us per layer, tools/bench_attn.py); SWH_ATTN=hip selects the HIP kernels
+        self._hip_attn = nn_ops.attention_supported(cfg.head_dim) and os.environ.get("SWH_ATTN", "torch") == "hip"
 
     def layer_range(self, i: int) -> tuple[int, int]:
         """[start, end) of layer i's parameters (and gradients) in the flat buffers."""
@@ -353,13 +358,15 @@ class CausalLM:
         q, k, v = nn_ops.QKVRopeFn.apply(qkv, positions, cos_t, sin_t, Hq, Hkv, D)
         if kv_out is not None:
             kv_out(i, k, v)
-        # GQA inside the attention kernel: materialising repeat_interleave'd K/V
-        # (and summing its gradient back) costs 5x the attention itself
-        gqa = Hq != Hkv
-        if mask is None:
-            o = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=D ** -0.5, enable_gqa=gqa)
-        else:
-            o = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, scale=D ** -0.5, enable_gqa=gqa)
+        if self._hip_attn:  # csrc/attn.hip: causal GQA flash attention, padding as transformers
+            km, fv = (None, None) if mask is None else mask
+            o = nn_ops.AttentionFn.apply(q, k, v, D ** -0.5, km, fv)
+        else:  # torch SDPA (aotriton), GQA inside the kernel
+            gqa = Hq != Hkv
+            if mask is None:
+                o = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=D ** -0.5, enable_gqa=gqa)
+            else:
+                o = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, scale=D ** -0.5, enable_gqa=gqa)
         o = o.transpose(1, 2).reshape(B, L, c.q_dim)
         o = _Linear.apply(o, self.p[f"l{i}.o_w"], None, self._gv(f"l{i}.o_w"), None)
         x = x + o
@@ -390,7 +397,11 @@ class CausalLM:
         mask = None
         if padded is None:
             padded = key_mask is not None and not bool(key_mask.bool().all())
-        if key_mask is not None and padded:
+        if key_mask is not None and padded and self._hip_attn:
+            # (key_mask, index of the first valid key): the kernel's visibility rule
+            km = key_mask.to(torch.int32).contiguous()
+            mask = (km, (km.cumsum(-1) == 0).sum(-1).to(torch.int32))
+        elif key_mask is not None and padded:
             km = key_mask.bool()
             causal = torch.ones(L, L, device=ids.device, dtype=torch.bool).tril()
             # a query with no valid key at all (left padding) sees itself, so no

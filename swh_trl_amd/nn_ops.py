@@ -199,6 +199,45 @@ def lm_head_sample_step(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Ten
     return out_tokens
 
 
+class AttentionFn(torch.autograd.Function):
+    """Causal GQA attention, q [B, Hq, L, D], k/v [B, Hkv, L, D] bf16 -> o
+    [B, Hq, L, D] (include/swh_trl_amd.h swh_attn_fwd / swh_attn_bwd).
+    key_mask int32 [B, L] (0 = padding) with first_valid int32 [B] (index of
+    the first valid key), or both None: transformers' padded causal mask as
+    engine/model.py builds it (a query with no valid key sees itself)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, scale: float, key_mask=None, first_valid=None):
+        _dev(q, "attention")
+        B, Hq, L, D = q.shape
+        Hkv = k.shape[1]
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        out = torch.empty_like(q)
+        lse = torch.empty(B, Hq, L, device=q.device, dtype=torch.float32)
+        call("swh_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), B, Hq, Hkv, L, D, float(scale),
+             _p(key_mask), _p(first_valid), out.data_ptr(), lse.data_ptr(), _stream())
+        ctx.save_for_backward(q, k, v, out, lse)
+        ctx.km, ctx.fv, ctx.scale = key_mask, first_valid, float(scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, out, lse = ctx.saved_tensors
+        B, Hq, L, D = q.shape
+        Hkv = k.shape[1]
+        dout = dout.contiguous()
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        delta = torch.empty(B, Hq, L, device=q.device, dtype=torch.float32)
+        call("swh_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), dout.data_ptr(),
+             lse.data_ptr(), B, Hq, Hkv, L, D, ctx.scale, _p(ctx.km), _p(ctx.fv), delta.data_ptr(), dq.data_ptr(),
+             dk.data_ptr(), dv.data_ptr(), _stream())
+        return dq, dk, dv, None, None, None
+
+
+def attention_supported(D: int) -> bool:
+    return D in (64, 128)
+
+
 class QKVRopeFn(torch.autograd.Function):
     """qkv [B, L, (Hq+2Hkv) D] -> q, k (rotated), v as contiguous [B, H, L, D]
     (include/swh_trl_amd.h swh_qkv_rope); backward writes d qkv in one pass."""

@@ -350,3 +350,26 @@ def test_fold_kernel_equals_torch_mul_and_group_dedup(dev):
     assert rep.tolist() == [0, 4] and inv.tolist() == [0, 0, 0, 0, 1, 1, 1, 1]
     rep2, inv2 = DecodeEngine._unique_prompts(ids, mask)
     assert torch.equal(ids[rep2][inv2], ids)
+
+
+def test_hip_attention_path_matches_sdpa_path(dev, monkeypatch):
+    """The model with csrc/attn.hip attention (SWH_ATTN=hip) against the SDPA
+    path: hidden states with left padding and weight gradients agree within
+    bf16 tolerance."""
+    from swh_trl_amd.engine import CausalLM, tiny_qwen2
+    g = torch.Generator().manual_seed(12)
+    ids = torch.randint(0, 1024, (3, 40), generator=g).to(dev)
+    km = torch.ones(3, 40, dtype=torch.int32, device=dev)
+    km[1, :9] = 0
+    outs = {}
+    for mode in ("torch", "hip"):
+        monkeypatch.setenv("SWH_ATTN", mode)
+        m = CausalLM(tiny_qwen2(1024, 2), dev, seed=12, init_std=0.05)
+        assert m._hip_attn == (mode == "hip")
+        m.zero_grad()
+        h = m.hidden_states(ids, key_mask=km)
+        (h.float() * torch.linspace(-1, 1, h.shape[-1], device=dev)).sum().backward()
+        outs[mode] = (h.detach().float(), m.grad.float().clone())
+    torch.testing.assert_close(outs["hip"][0], outs["torch"][0], rtol=3e-2, atol=3e-2)
+    gt, gh = outs["torch"][1], outs["hip"][1]
+    assert (gh - gt).norm() <= 0.05 * gt.norm()

@@ -811,3 +811,55 @@ def test_decode_gemm_folded_norm(ops, dev, M, N, K, silu):
         gu = ref.to(torch.bfloat16)
         ref = (torch.nn.functional.silu(gu[:, :N]) * gu[:, N:]).float()
     torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=3e-2)  # rounding of the fold, then SiLU's
+
+
+# --------------------------------------------------------------------------- training attention (csrc/attn.hip)
+def _ref_attention(q, k, v, scale, km=None):
+    """fp32 reference: transformers' padded causal mask (a query with no valid
+    key sees itself), GQA by head repetition."""
+    B, Hq, L, D = q.shape
+    G = Hq // k.shape[1]
+    kf, vf = k.float().repeat_interleave(G, 1), v.float().repeat_interleave(G, 1)
+    causal = torch.ones(L, L, dtype=torch.bool, device=q.device).tril()
+    if km is None:
+        mask = causal[None, None]
+    else:
+        kb = km.bool()
+        no_key = kb.cumsum(-1) == 0
+        eye = torch.eye(L, dtype=torch.bool, device=q.device)
+        mask = causal & (kb[:, None, None, :] | (eye & no_key[:, None, :, None]))
+    s = (q.float() @ kf.transpose(-1, -2)) * scale
+    s = s.masked_fill(~mask, float("-inf"))
+    return torch.softmax(s, -1) @ vf
+
+
+@pytest.mark.parametrize("B,Hq,Hkv,L,D,pad", [(2, 14, 2, 384, 64, False), (3, 14, 2, 100, 64, True),
+                                              (2, 4, 4, 77, 64, True), (1, 8, 2, 96, 128, False)])
+def test_attention_fwd_bwd_matches_reference(ops, dev, B, Hq, Hkv, L, D, pad):
+    """swh_attn_fwd/bwd vs an fp32 autograd reference of the same mask: output
+    and dq/dk/dv within bf16 tolerance (bf16 P in the P V and dS products)."""
+    from swh_trl_amd import nn_ops
+    g = _gen(60 + L)
+    q = torch.randn(B, Hq, L, D, generator=g).to(torch.bfloat16).to(dev)
+    k = torch.randn(B, Hkv, L, D, generator=g).to(torch.bfloat16).to(dev)
+    v = torch.randn(B, Hkv, L, D, generator=g).to(torch.bfloat16).to(dev)
+    do = torch.randn(B, Hq, L, D, generator=g).to(torch.bfloat16).to(dev)
+    km = fv = None
+    if pad:
+        km = torch.ones(B, L, dtype=torch.int32)
+        for b in range(B):
+            km[b, : (7 * b + 3) % (L // 2)] = 0  # left padding of different lengths
+        km[0, L - 5:] = 0                       # and right padding on one row
+        km = km.to(dev)
+        fv = (km.cumsum(-1) == 0).sum(-1).to(torch.int32)
+    scale = D ** -0.5
+    qa, ka, va = (t.clone().requires_grad_(True) for t in (q, k, v))
+    o = nn_ops.AttentionFn.apply(qa, ka, va, scale, km, fv)
+    o.backward(do)
+    qr, kr, vr = (t.float().clone().requires_grad_(True) for t in (q, k, v))
+    ref = _ref_attention(qr, kr, vr, scale, km)
+    ref.backward(do.float())
+    torch.testing.assert_close(o.float(), ref, rtol=2e-2, atol=2e-2)
+    for mine, r in ((qa.grad, qr.grad), (ka.grad, kr.grad), (va.grad, vr.grad)):
+        err = (mine.float() - r).abs().max().item()
+        assert err <= 3e-2 * max(1.0, r.abs().max().item()), err
