@@ -82,16 +82,17 @@ def cpu_baseline(steps_note: str) -> dict:
                        f"{G} samples; {steps_note}")}
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r1_v2_pmc_decode.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r1_v4_pmc_decode.json")
 
 
 def pmc_traffic(kernel: str):
     """HBM bytes per launch of `kernel` from the committed PMC passes
     (tools/pmc_summary.py: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE over
     tools/bench_decode.py, MI355X_MICROARCH.md §HBM corrections), or None."""
+    key = "decode_gemm.o+down" if kernel in ("decode_gemm.o", "decode_gemm.down") else kernel  # one template
     try:
         with open(PMC_FILE) as f:
-            k = json.load(f)["kernels"].get(kernel)
+            k = json.load(f)["kernels"].get(key)
         return None if k is None else k["hbm_bytes_per_launch"]
     except (OSError, ValueError, KeyError):
         return None

@@ -5,7 +5,7 @@ FETCH_SIZE counts half the bytes of wide streaming reads on gfx950 (x2);
 both counters are KiB.  Writes profiles/<name>.json, which bench.py reads
 for `roofline.traffic`.
 
-    python tools/pmc_summary.py gpurun_out/pmcf gpurun_out/pmcw profiles/r1_v2_pmc_decode.json
+    python tools/pmc_summary.py gpurun_out/pmcf gpurun_out/pmcw profiles/r1_v4_pmc_decode.json
 """
 import collections
 import csv
@@ -13,12 +13,12 @@ import json
 import re
 import sys
 
-NAMES = {  # kernel template (+ grid) -> the bench's kernel name
-    ("decode_gemm_kernel<4, 4, 2, 2, false>", None): "decode_gemm.gate_up",
-    ("decode_gemm_kernel<1, 2, 2, 0, true>", None): "decode_gemm.qkv",
-    ("decode_gemm_kernel<1, 1, 0, 1, false>", None): "decode_gemm.o+down",
-    ("attn_decode_kernel<64, 7>", None): "attn_decode",
-    ("lm_head_kernel<2, 0, false, true>", None): "lm_head_sample",
+NAMES = {  # kernel template prefix -> the bench's kernel name
+    "lm_head_kernel<2, 2, false, false": "decode_gemm.gate_up",   # tile kernel, folded norm, SiLU epilogue
+    "decode_gemm_kernel<1, 2, 2, 0, true": "decode_gemm.qkv",
+    "decode_gemm_kernel<1, 1, 0, 1, false": "decode_gemm.o+down",
+    "attn_decode_kernel<64, 7>": "attn_decode",
+    "lm_head_kernel<2, 0, false, true": "lm_head_sample",
 }
 
 
@@ -38,10 +38,13 @@ def main():
     fetch, write = per_kernel(fdir, "FETCH_SIZE"), per_kernel(wdir, "WRITE_SIZE")
     res = {"source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE -- python3 tools/bench_decode.py",
            "correction": "FETCH_SIZE x2 (gfx950 wide-read tally), KiB -> bytes", "kernels": {}}
-    for (tmpl, _), name in NAMES.items():
-        if tmpl in fetch and tmpl in write:
+    for prefix, name in NAMES.items():
+        tf = [k for k in fetch if k.startswith(prefix)]
+        tw = [k for k in write if k.startswith(prefix)]
+        if tf and tw:
+            tmpl = tf[0]
             rd = fetch[tmpl][1] * 2 * 1024
-            wr = write[tmpl][1] * 1024
+            wr = write[tw[0]][1] * 1024
             res["kernels"][name] = {"template": tmpl, "dispatches": fetch[tmpl][0], "hbm_read_bytes": round(rd),
                                     "hbm_write_bytes": round(wr), "hbm_bytes_per_launch": round(rd + wr)}
     with open(out, "w") as f:
