@@ -150,20 +150,92 @@ __device__ __forceinline__ void fa_abt(f32x4a (&s)[2], const u32x4 (&a)[2][D / 3
 template <int D>
 constexpr int fa_vs() { return D + (D == 64 ? 8 : 16); }
 
-// ---- forward: grid (ceil(L / 64), Hq, B), 4 waves x 16 queries
+// X^T Y with the 32-row block X already in a (shared) LDS tile: read-only variant of fa_xty
+template <int D, int VS>
+__device__ __forceinline__ void fa_xty_shared(f32x4a (&o)[D / 16], const uint16_t *tile, const float (&y)[8],
+                                              int c16, int g) {
+    uint32_t pb[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+        pb[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2a{y[2 * h], y[2 * h + 1]}, bf16x2a));
+    const bf16x8a yb = __builtin_bit_cast(bf16x8a, u32x4{pb[0], pb[1], pb[2], pb[3]});
+    const int qq = c16 >> 2, pq = c16 & 3;
+#pragma unroll
+    for (int d = 0; d < D / 16; ++d) {
+        const bf16x4sa lo = fa_tr16(tile + (4 * g + qq) * VS + d * 16 + 4 * pq);
+        const bf16x4sa hi = fa_tr16(tile + (16 + 4 * g + qq) * VS + d * 16 + 4 * pq);
+        const bf16x8a xa = __builtin_bit_cast(
+            bf16x8a, u32x4{__builtin_bit_cast(uint2, lo).x, __builtin_bit_cast(uint2, lo).y,
+                           __builtin_bit_cast(uint2, hi).x, __builtin_bit_cast(uint2, hi).y});
+        o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, yb, o[d], 0, 0, 0);
+    }
+}
+
+// the A fragments of a 32-row block from a shared LDS tile: lane (g, c16) <- row 16 t + c16, dims 32 c + 8 g
+template <int D, int VS>
+__device__ __forceinline__ void fa_rows_lds(u32x4 (&r)[2][D / 32], const uint16_t *tile, int c16, int g) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int c = 0; c < D / 32; ++c)
+            r[t][c] = *reinterpret_cast<const u32x4 *>(tile + (16 * t + c16) * VS + c * 32 + g * 8);
+}
+
+// cooperative staging of a 32-row block of two [L, D] slabs (K and V) by the whole workgroup:
+// global -> registers (issued early) -> LDS (written late)
 template <int D>
-__global__ __launch_bounds__(kFaThreads) void fa_fwd_kernel(FaArgs a) {
+struct FaStage {
+    static constexpr int kPieces = 2 * 32 * D / 8;  // 16-B pieces of the two blocks
+    static constexpr int kPer = kPieces / 256;        // per thread (blocks have >= 256 threads)
+    u32x4 v[kPer];
+};
+template <int D>
+__device__ __forceinline__ void fa_stage_load(FaStage<D> &st, const uint16_t *kbase, const uint16_t *vbase, int r0,
+                                              int L, int tid, int nthr) {
+#pragma unroll
+    for (int j = 0; j < FaStage<D>::kPer; ++j) {
+        const int pc = tid + j * nthr;
+        if (pc < FaStage<D>::kPieces) {
+            const int which = pc / (32 * D / 8), rem = pc - which * (32 * D / 8);
+            const int row = rem / (D / 8), col = rem - row * (D / 8);
+            const uint16_t *src = (which ? vbase : kbase) + (int64_t)min(r0 + row, L - 1) * D + col * 8;
+            st.v[j] = *reinterpret_cast<const u32x4 *>(src);
+        }
+    }
+}
+template <int D, int VS>
+__device__ __forceinline__ void fa_stage_store(const FaStage<D> &st, uint16_t *ktile, uint16_t *vtile, int tid,
+                                               int nthr) {
+#pragma unroll
+    for (int j = 0; j < FaStage<D>::kPer; ++j) {
+        const int pc = tid + j * nthr;
+        if (pc < FaStage<D>::kPieces) {
+            const int which = pc / (32 * D / 8), rem = pc - which * (32 * D / 8);
+            const int row = rem / (D / 8), col = rem - row * (D / 8);
+            *reinterpret_cast<u32x4 *>((which ? vtile : ktile) + row * VS + col * 8) = st.v[j];
+        }
+    }
+}
+
+
+// ---- forward: grid (ceil(L / 16), Hkv, B); a workgroup = the G = Hq / Hkv query
+// heads of one KV head (one wave each) over the same 16 queries, so every K/V block
+// is staged into LDS once (double-buffered, one barrier per block) for all G heads
+template <int D>
+__global__ __launch_bounds__(512) void fa_fwd_kernel(FaArgs a) {
     constexpr int DC = D / 32, DB = D / 16, VS = fa_vs<D>();
-    __shared__ __attribute__((aligned(16))) uint16_t tiles[kFaWaves][32 * VS];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
-    const int b = blockIdx.z, h = blockIdx.y, kvh = h / (a.Hq / a.Hkv), L = a.L;
-    const int q0 = blockIdx.x * 64 + wid * 16;
-    if (q0 >= L) return;
+    __shared__ __attribute__((aligned(16))) uint16_t kt[2][32 * VS], vt[2][32 * VS];
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const int lane = tid & 63, wid = tid >> 6, g = lane >> 4, c16 = lane & 15;
+    const int b = blockIdx.z, kvh = blockIdx.y, G = a.Hq / a.Hkv, L = a.L;
+    const bool active = wid < G;  // waves past the group's heads only help staging (blocks >= 4 waves)
+    const int h = kvh * G + min(wid, G - 1);
+    const int q0 = blockIdx.x * 16;
     const int qc = min(q0 + c16, L - 1);  // this lane's query column
     const int fv = a.first_valid ? a.first_valid[b] : 0;
-    const uint16_t *qb_ = a.q + ((int64_t)b * a.Hq + h) * L * D;
     const uint16_t *kb_ = a.k + ((int64_t)b * a.Hkv + kvh) * L * D;
     const uint16_t *vb_ = a.v + ((int64_t)b * a.Hkv + kvh) * L * D;
+    const uint16_t *qb_ = a.q + ((int64_t)b * a.Hq + h) * L * D;
     u32x4 qf[DC];
 #pragma unroll
     for (int c = 0; c < DC; ++c) qf[c] = *reinterpret_cast<const u32x4 *>(qb_ + (int64_t)qc * D + c * 32 + g * 8);
@@ -171,18 +243,17 @@ __global__ __launch_bounds__(kFaThreads) void fa_fwd_kernel(FaArgs a) {
     f32x4a o[DB];
 #pragma unroll
     for (int d = 0; d < DB; ++d) o[d] = f32x4a{0.f, 0.f, 0.f, 0.f};
-    uint16_t *tile = tiles[wid];
     const int kend = min(q0 + 16, L);  // causal: keys < kend
-    u32x4 kr[2][DC], vr[2][DC], kn[2][DC], vn[2][DC];
-    fa_load_rows<D>(kn, kb_, 0, L, c16, g);
-    fa_load_rows<D>(vn, vb_, 0, L, c16, g);
-    for (int k0 = 0; k0 < kend; k0 += 32) {
-        fa_copy<D>(kr, kn);
-        fa_copy<D>(vr, vn);
-        if (k0 + 32 < kend) {  // the next block streams while this one computes
-            fa_load_rows<D>(kn, kb_, k0 + 32, L, c16, g);
-            fa_load_rows<D>(vn, vb_, k0 + 32, L, c16, g);
-        }
+    FaStage<D> st;
+    fa_stage_load<D>(st, kb_, vb_, 0, L, tid, nthr);
+    fa_stage_store<D, VS>(st, kt[0], vt[0], tid, nthr);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = 0; k0 < kend; k0 += 32, buf ^= 1) {
+        const bool more = k0 + 32 < kend;
+        if (more) fa_stage_load<D>(st, kb_, vb_, k0 + 32, L, tid, nthr);  // next block streams meanwhile
+        u32x4 kr[2][DC];
+        fa_rows_lds<D, VS>(kr, kt[buf], c16, g);
         f32x4a s[2];
         fa_abt<D>(s, kr, qf);
         const FaKeyMask km = fa_key_mask(a, b, k0, g);
@@ -209,11 +280,13 @@ __global__ __launch_bounds__(kFaThreads) void fa_fwd_kernel(FaArgs a) {
             p[j] = (mx == kNegInf) ? 0.f : __expf(sv[j] - mx);
             l += p[j];
         }
-        fa_xty<D, VS>(o, tile, vr, p, c16, g);
+        fa_xty_shared<D, VS>(o, vt[buf], p, c16, g);
+        if (more) fa_stage_store<D, VS>(st, kt[buf ^ 1], vt[buf ^ 1], tid, nthr);
+        __syncthreads();
     }
     l += __shfl_xor(l, 16, kWave);
     l += __shfl_xor(l, 32, kWave);
-    if (q0 + c16 < L) {
+    if (active && q0 + c16 < L) {
         uint16_t *ob = a.out + (((int64_t)b * a.Hq + h) * L + q0 + c16) * D;
         const float inv = 1.f / l;
 #pragma unroll
@@ -245,15 +318,18 @@ __global__ __launch_bounds__(256) void fa_delta_kernel(FaArgs a, int64_t rows) {
     a.delta[r] = s;
 }
 
-// ---- dQ: the forward walk with dP^T = V dO^T and dQ^T += K^T dS^T
+// ---- dQ: the forward walk (K / V blocks shared through LDS by the G query heads)
+// with dP^T = V dO^T and dQ^T += K^T dS^T
 template <int D>
-__global__ __launch_bounds__(kFaThreads) void fa_dq_kernel(FaArgs a) {
+__global__ __launch_bounds__(512) void fa_dq_kernel(FaArgs a) {
     constexpr int DC = D / 32, DB = D / 16, VS = fa_vs<D>();
-    __shared__ __attribute__((aligned(16))) uint16_t tiles[kFaWaves][32 * VS];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
-    const int b = blockIdx.z, h = blockIdx.y, kvh = h / (a.Hq / a.Hkv), L = a.L;
-    const int q0 = blockIdx.x * 64 + wid * 16;
-    if (q0 >= L) return;
+    __shared__ __attribute__((aligned(16))) uint16_t kt[2][32 * VS], vt[2][32 * VS];
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const int lane = tid & 63, wid = tid >> 6, g = lane >> 4, c16 = lane & 15;
+    const int b = blockIdx.z, kvh = blockIdx.y, G = a.Hq / a.Hkv, L = a.L;
+    const bool active = wid < G;
+    const int h = kvh * G + min(wid, G - 1);
+    const int q0 = blockIdx.x * 16;
     const int qc = min(q0 + c16, L - 1);
     const int fv = a.first_valid ? a.first_valid[b] : 0;
     const int64_t qrow = ((int64_t)b * a.Hq + h) * L;
@@ -269,18 +345,18 @@ __global__ __launch_bounds__(kFaThreads) void fa_dq_kernel(FaArgs a) {
     f32x4a acc[DB];
 #pragma unroll
     for (int d = 0; d < DB; ++d) acc[d] = f32x4a{0.f, 0.f, 0.f, 0.f};
-    uint16_t *tile = tiles[wid];
     const int kend = min(q0 + 16, L);
-    u32x4 kr[2][DC], vr[2][DC], kn[2][DC], vn[2][DC];
-    fa_load_rows<D>(kn, kb_, 0, L, c16, g);
-    fa_load_rows<D>(vn, vb_, 0, L, c16, g);
-    for (int k0 = 0; k0 < kend; k0 += 32) {
-        fa_copy<D>(kr, kn);
-        fa_copy<D>(vr, vn);
-        if (k0 + 32 < kend) {
-            fa_load_rows<D>(kn, kb_, k0 + 32, L, c16, g);
-            fa_load_rows<D>(vn, vb_, k0 + 32, L, c16, g);
-        }
+    FaStage<D> st;
+    fa_stage_load<D>(st, kb_, vb_, 0, L, tid, nthr);
+    fa_stage_store<D, VS>(st, kt[0], vt[0], tid, nthr);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = 0; k0 < kend; k0 += 32, buf ^= 1) {
+        const bool more = k0 + 32 < kend;
+        if (more) fa_stage_load<D>(st, kb_, vb_, k0 + 32, L, tid, nthr);
+        u32x4 kr[2][DC], vr[2][DC];
+        fa_rows_lds<D, VS>(kr, kt[buf], c16, g);
+        fa_rows_lds<D, VS>(vr, vt[buf], c16, g);
         f32x4a s[2], dp[2];
         fa_abt<D>(s, kr, qf);
         fa_abt<D>(dp, vr, df);
@@ -294,9 +370,11 @@ __global__ __launch_bounds__(kFaThreads) void fa_dq_kernel(FaArgs a) {
                 const float p = fa_vis(q0 + c16, key, L, km.v[4 * t + r], fv) ? __expf(s[t][r] * a.scale - lse) : 0.f;
                 ds[4 * t + r] = p * (dp[t][r] - dl);
             }
-        fa_xty<D, VS>(acc, tile, kr, ds, c16, g);
+        fa_xty_shared<D, VS>(acc, kt[buf], ds, c16, g);
+        if (more) fa_stage_store<D, VS>(st, kt[buf ^ 1], vt[buf ^ 1], tid, nthr);
+        __syncthreads();
     }
-    if (q0 + c16 < L) {
+    if (active && q0 + c16 < L) {
         uint16_t *qb = a.dq + (qrow + q0 + c16) * D;
 #pragma unroll
         for (int d = 0; d < DB; ++d) {
@@ -309,15 +387,17 @@ __global__ __launch_bounds__(kFaThreads) void fa_dq_kernel(FaArgs a) {
     }
 }
 
-// ---- dK / dV: a wave owns 16 keys, walks the queries of every head of its group
+// ---- dK / dV: a workgroup owns 16 keys of one KV head; wave w walks the queries of
+// head kvh * G + w (its own LDS tile for the transposed reads), then the G partial
+// dK / dV are summed in fixed order through LDS
 template <int D>
-__global__ __launch_bounds__(kFaThreads) void fa_dkdv_kernel(FaArgs a) {
+__global__ __launch_bounds__(512) void fa_dkdv_kernel(FaArgs a) {
     constexpr int DC = D / 32, DB = D / 16, VS = fa_vs<D>();
-    __shared__ __attribute__((aligned(16))) uint16_t tiles[kFaWaves][32 * VS];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
+    __shared__ __attribute__((aligned(16))) uint16_t tiles[8][32 * VS];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wid = tid >> 6, g = lane >> 4, c16 = lane & 15;
     const int b = blockIdx.z, kvh = blockIdx.y, L = a.L, G = a.Hq / a.Hkv;
-    const int k0w = blockIdx.x * 64 + wid * 16;
-    if (k0w >= L) return;
+    const int k0w = blockIdx.x * 16;
     const int kc = min(k0w + c16, L - 1);  // this lane's key column
     const int fv = a.first_valid ? a.first_valid[b] : 0;
     const int kmv = a.key_mask ? a.key_mask[(int64_t)b * L + kc] : 1;
@@ -335,15 +415,15 @@ __global__ __launch_bounds__(kFaThreads) void fa_dkdv_kernel(FaArgs a) {
         dv[d] = f32x4a{0.f, 0.f, 0.f, 0.f};
     }
     uint16_t *tile = tiles[wid];
-    const int qstart = k0w & ~31;  // causal: queries >= the wave's first key (32-aligned blocks)
-    const int nb = (L - qstart + 31) / 32, nit = G * nb;  // (head, query block) rounds
-    // round it: head kvh * G + it / nb, query rows r0 = qstart + 32 (it % nb); the next round's
-    // Q / dO rows and softmax statistics stream while this one computes
+    const int h = kvh * G + min(wid, G - 1);
+    const int64_t qrow = ((int64_t)b * a.Hq + h) * L;
+    const int qstart = k0w & ~31;  // causal: queries >= the workgroup's first key (32-aligned blocks)
+    const int nit = wid < G ? (L - qstart + 31) / 32 : 0;  // waves past the group's heads: no walk
+    // the next query block's Q / dO rows and softmax statistics stream while this one computes
     u32x4 qr[2][DC], dr[2][DC], qn[2][DC], dn[2][DC];
     float ls[8], dl[8], lsn[8], dln[8];
     auto fetch = [&](int it, u32x4(&q_)[2][DC], u32x4(&d_)[2][DC], float(&l_)[8], float(&e_)[8]) {
-        const int h = kvh * G + it / nb, r0 = qstart + 32 * (it % nb);
-        const int64_t qrow = ((int64_t)b * a.Hq + h) * L;
+        const int r0 = qstart + 32 * it;
         fa_load_rows<D>(q_, a.q + qrow * D, r0, L, c16, g);
         fa_load_rows<D>(d_, a.dout + qrow * D, r0, L, c16, g);
 #pragma unroll
@@ -355,7 +435,7 @@ __global__ __launch_bounds__(kFaThreads) void fa_dkdv_kernel(FaArgs a) {
                 e_[4 * t + r] = a.delta[qrow + qq];
             }
     };
-    fetch(0, qn, dn, lsn, dln);
+    if (nit > 0) fetch(0, qn, dn, lsn, dln);
     for (int it = 0; it < nit; ++it) {
         fa_copy<D>(qr, qn);
         fa_copy<D>(dr, dn);
@@ -365,7 +445,7 @@ __global__ __launch_bounds__(kFaThreads) void fa_dkdv_kernel(FaArgs a) {
             dl[j] = dln[j];
         }
         if (it + 1 < nit) fetch(it + 1, qn, dn, lsn, dln);
-        const int r0 = qstart + 32 * (it % nb);
+        const int r0 = qstart + 32 * it;
         f32x4a s[2], dp[2];
         fa_abt<D>(s, qr, kf);   // S[q = r0 + 16 t + 4 g + r][key c16]
         fa_abt<D>(dp, dr, vf);  // dP likewise
@@ -383,27 +463,37 @@ __global__ __launch_bounds__(kFaThreads) void fa_dkdv_kernel(FaArgs a) {
         fa_xty<D, VS>(dv, tile, dr, p, c16, g);
         fa_xty<D, VS>(dk, tile, qr, ds, c16, g);
     }
-    if (k0w + c16 < L) {
-        uint16_t *kb = a.dk + (kvrow + k0w + c16) * D;
-        uint16_t *vb = a.dv + (kvrow + k0w + c16) * D;
+    // sum the G heads' partials in fixed order: park all, then wave 0 adds them up
+    __syncthreads();
+    float *red = reinterpret_cast<float *>(tiles);  // [G][DB][64 lanes][4] f32 (one of dk / dv at a time)
+    const bool store = k0w + c16 < L;
+    uint16_t *kb = a.dk + (kvrow + k0w + c16) * D;
+    uint16_t *vb = a.dv + (kvrow + k0w + c16) * D;
 #pragma unroll
-        for (int d = 0; d < DB; ++d) {
-            const uint32_t klo = (uint32_t)f32_to_bf16_bits(dk[d][0] * a.scale) |
-                                 ((uint32_t)f32_to_bf16_bits(dk[d][1] * a.scale) << 16);
-            const uint32_t khi = (uint32_t)f32_to_bf16_bits(dk[d][2] * a.scale) |
-                                 ((uint32_t)f32_to_bf16_bits(dk[d][3] * a.scale) << 16);
-            *reinterpret_cast<uint2 *>(kb + d * 16 + 4 * g) = uint2{klo, khi};
-            const uint32_t vlo = (uint32_t)f32_to_bf16_bits(dv[d][0]) | ((uint32_t)f32_to_bf16_bits(dv[d][1]) << 16);
-            const uint32_t vhi = (uint32_t)f32_to_bf16_bits(dv[d][2]) | ((uint32_t)f32_to_bf16_bits(dv[d][3]) << 16);
-            *reinterpret_cast<uint2 *>(vb + d * 16 + 4 * g) = uint2{vlo, vhi};
+    for (int pass = 0; pass < 2; ++pass) {
+        f32x4a(&x)[DB] = pass == 0 ? dk : dv;
+#pragma unroll
+        for (int d = 0; d < DB; ++d) *reinterpret_cast<f32x4a *>(red + ((wid * DB + d) * 64 + lane) * 4) = x[d];
+        __syncthreads();
+        if (wid == 0) {
+#pragma unroll
+            for (int d = 0; d < DB; ++d) {
+                f32x4a sum = x[d];
+                for (int w = 1; w < G; ++w) sum += *reinterpret_cast<const f32x4a *>(red + ((w * DB + d) * 64 + lane) * 4);
+                const float sc = pass == 0 ? a.scale : 1.f;
+                const uint32_t lo = (uint32_t)f32_to_bf16_bits(sum[0] * sc) | ((uint32_t)f32_to_bf16_bits(sum[1] * sc) << 16);
+                const uint32_t hi = (uint32_t)f32_to_bf16_bits(sum[2] * sc) | ((uint32_t)f32_to_bf16_bits(sum[3] * sc) << 16);
+                if (store) *reinterpret_cast<uint2 *>((pass == 0 ? kb : vb) + d * 16 + 4 * g) = uint2{lo, hi};
+            }
         }
+        __syncthreads();
     }
 }
 
 bool fa_args_ok(const void *q, const void *k, const void *v, int64_t B, int32_t Hq, int32_t Hkv, int64_t L,
                 int32_t D) {
     return q && k && v && B > 0 && Hq > 0 && Hkv > 0 && Hq % Hkv == 0 && L > 0 && L <= (1 << 20) &&
-           B <= 65535 && Hq <= 65535 && (D == 64 || D == 128);
+           B <= 65535 && Hq / Hkv <= 8 && (D == 64 || D == 128);  // a workgroup = the query heads of one KV head
 }
 
 }  // namespace
@@ -428,10 +518,11 @@ extern "C" int swh_attn_fwd(const void *q, const void *k, const void *v, int64_t
     a.Hkv = Hkv;
     a.L = (int)L;
     a.scale = scale;
-    const dim3 grid((unsigned)((L + 63) / 64), (unsigned)Hq, (unsigned)B);
+    const dim3 grid((unsigned)((L + 15) / 16), (unsigned)Hkv, (unsigned)B);
+    const unsigned thr = 64u * (unsigned)(Hq / Hkv < 4 ? 4 : Hq / Hkv);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (D == 64) fa_fwd_kernel<64><<<grid, kFaThreads, 0, s>>>(a);
-    else fa_fwd_kernel<128><<<grid, kFaThreads, 0, s>>>(a);
+    if (D == 64) fa_fwd_kernel<64><<<grid, thr, 0, s>>>(a);
+    else fa_fwd_kernel<128><<<grid, thr, 0, s>>>(a);
     return launch_status();
 }
 
@@ -462,16 +553,16 @@ extern "C" int swh_attn_bwd(const void *q, const void *k, const void *v, const v
     a.scale = scale;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int64_t rows = B * Hq * L;
-    const dim3 gq((unsigned)((L + 63) / 64), (unsigned)Hq, (unsigned)B);
-    const dim3 gk((unsigned)((L + 63) / 64), (unsigned)Hkv, (unsigned)B);
+    const dim3 grid((unsigned)((L + 15) / 16), (unsigned)Hkv, (unsigned)B);
+    const unsigned thr = 64u * (unsigned)(Hq / Hkv < 4 ? 4 : Hq / Hkv);
     if (D == 64) {
         fa_delta_kernel<64><<<dim3((unsigned)((rows + 255) / 256)), 256, 0, s>>>(a, rows);
-        fa_dq_kernel<64><<<gq, kFaThreads, 0, s>>>(a);
-        fa_dkdv_kernel<64><<<gk, kFaThreads, 0, s>>>(a);
+        fa_dq_kernel<64><<<grid, thr, 0, s>>>(a);
+        fa_dkdv_kernel<64><<<grid, thr, 0, s>>>(a);
     } else {
         fa_delta_kernel<128><<<dim3((unsigned)((rows + 255) / 256)), 256, 0, s>>>(a, rows);
-        fa_dq_kernel<128><<<gq, kFaThreads, 0, s>>>(a);
-        fa_dkdv_kernel<128><<<gk, kFaThreads, 0, s>>>(a);
+        fa_dq_kernel<128><<<grid, thr, 0, s>>>(a);
+        fa_dkdv_kernel<128><<<grid, thr, 0, s>>>(a);
     }
     return launch_status();
 }

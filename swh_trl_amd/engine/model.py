@@ -243,10 +243,10 @@ class CausalLM:
         self._rope = None
         # backward hook: called with layer index i once layer i's weight gradients are final
         self.on_layer_grads = None
-        # full-sequence attention: torch SDPA (aotriton) by default — at the GRPO shape it
-        # is still 10 % faster per step than csrc/attn.hip (fwd 169 + bwd 457 us vs
-        # 150 + 430 us per layer, tools/bench_attn.py); SWH_ATTN=hip selects the HIP kernels
-        self._hip_attn = nn_ops.attention_supported(cfg.head_dim) and os.environ.get("SWH_ATTN", "torch") == "hip"
+        # full-sequence attention on csrc/attn.hip (fwd 95 + bwd 395 us per layer at the GRPO
+        # shape against aotriton's 150 + 430, rocprofv3 of tools/bench_attn.py); SWH_ATTN=torch
+        # selects torch SDPA for A/B
+        self._hip_attn = nn_ops.attention_supported(cfg.head_dim) and os.environ.get("SWH_ATTN", "hip") != "torch"
 
     def layer_range(self, i: int) -> tuple[int, int]:
         """[start, end) of layer i's parameters (and gradients) in the flat buffers."""
