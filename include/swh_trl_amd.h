@@ -234,8 +234,14 @@ int swh_rmsnorm_fwd(const void *x, const void *residual, void *residual_out, con
                     int64_t rows, int64_t H, float eps, void *y, float *rstd, void *stream);
 /* Backward: dx = rstd*(w*dy - n*mean(w*dy*n)), n = x*rstd; dw partial sums
  * f32 [ceil(rows/rows_per_block) x H] reduced by the caller. */
-int swh_rmsnorm_bwd(const void *x, const void *weight, const float *rstd, const void *dy, int64_t rows,
-                    int64_t H, void *dx, float *dw_partial, int64_t rows_per_block, void *stream);
+int swh_rmsnorm_bwd(const void *x, const void *weight, const float *rstd, const void *dy, int64_t rows, int64_t H,
+                    void *dx, float *dw_partial, int64_t rows_per_block, const void *dres, void *stream);
+/* dres (nullable, bf16 [rows, H]): the gradient arriving through the residual
+ * branch; dx = bf16(bf16(norm backward) + dres), the sum autograd forms where
+ * the residual stream forks into the next RMSNorm.  swh_rmsnorm_dw_accum folds
+ * the partial weight-gradient column sums into the bf16 gradient view:
+ * grad_w = bf16(grad_w + bf16(sum over blocks)). */
+int swh_rmsnorm_dw_accum(const float *dw_partial, int64_t nblocks, int64_t H, void *grad_w, void *stream);
 /* out[r, i] = bf16(bf16(silu(gu[r, i])) * gu[r, I + i]) — gate/up packed. */
 int swh_silu_mul_fwd(const void *gu, int64_t rows, int64_t I, void *out, void *stream);
 int swh_silu_mul_bwd(const void *gu, const void *dout, int64_t rows, int64_t I, void *dgu, void *stream);

@@ -83,7 +83,7 @@ template <int VEC>
 __global__ __launch_bounds__(kNormBwdThreads) void rmsnorm_bwd_kernel(
     const uint16_t *__restrict__ x, const uint16_t *__restrict__ w, const float *__restrict__ rstd,
     const uint16_t *__restrict__ dy, int64_t rows, int64_t H, uint16_t *__restrict__ dx,
-    float *__restrict__ dw_part, int64_t rpb) {
+    float *__restrict__ dw_part, int64_t rpb, const uint16_t *__restrict__ dres) {
     extern __shared__ float dws[];  // [waves][H]
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     constexpr int NWV = kNormBwdThreads / 64;
@@ -135,6 +135,12 @@ __global__ __launch_bounds__(kNormBwdThreads) void rmsnorm_bwd_kernel(
                     const float n = a[k] * rs;
                     dwa[j][k] = fmaf(g[k], round_bf16(n), dwa[j][k]);
                     a[k] = rs * (g[k] * wv[j][k] - n * c);
+                }
+                if (dres) {  // + the residual branch's gradient: bf16(bf16(dx_norm) + dres), as autograd adds them
+                    float d[8];
+                    unpack16<SWH_BF16>(reinterpret_cast<const uint4 *>(dres + r * H)[lane + 64 * j], d);
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) a[k] = round_bf16(a[k]) + d[k];
                 }
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
@@ -364,8 +370,27 @@ extern "C" int swh_rmsnorm_fwd(const void *x, const void *residual, void *residu
     return launch_status();
 }
 
+// d weight: gw[h] = bf16(gw[h] + bf16(sum_b part[b][h])) — the partial column sums of
+// swh_rmsnorm_bwd folded into the bf16 gradient view in one launch
+__global__ __launch_bounds__(256) void rmsnorm_dw_accum_kernel(const float *__restrict__ part, int64_t nb, int64_t H,
+                                                              uint16_t *__restrict__ gw) {
+    const int64_t h = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (h >= H) return;
+    float t = 0.f;
+    for (int64_t b = 0; b < nb; ++b) t += part[b * H + h];
+    gw[h] = f32_to_bf16_bits(bf16_bits_to_f32(gw[h]) + round_bf16(t));
+}
+
+extern "C" int swh_rmsnorm_dw_accum(const float *dw_partial, int64_t nblocks, int64_t H, void *grad_w, void *stream) {
+    if (!dw_partial || !grad_w || nblocks <= 0 || H <= 0) return SWH_E_ARG;
+    rmsnorm_dw_accum_kernel<<<dim3((unsigned)((H + 255) / 256)), 256, 0, static_cast<hipStream_t>(stream)>>>(
+        dw_partial, nblocks, H, static_cast<uint16_t *>(grad_w));
+    return launch_status();
+}
+
 extern "C" int swh_rmsnorm_bwd(const void *x, const void *weight, const float *rstd, const void *dy, int64_t rows,
-                               int64_t H, void *dx, float *dw_partial, int64_t rows_per_block, void *stream) {
+                               int64_t H, void *dx, float *dw_partial, int64_t rows_per_block, const void *dres,
+                               void *stream) {
     if (!x || !weight || !rstd || !dy || !dx || !dw_partial || rows < 0 || H <= 0 || H % 8 ||
         H > 64 * 8 * kNormBwdVec || rows_per_block <= 0 || rows_per_block > 4096)
         return SWH_E_ARG;
@@ -377,7 +402,8 @@ extern "C" int swh_rmsnorm_bwd(const void *x, const void *weight, const float *r
     const auto *DY = static_cast<const uint16_t *>(dy);
     auto *DX = static_cast<uint16_t *>(dx);
 #define SWH_NORM_BWD(V) \
-    rmsnorm_bwd_kernel<V><<<dim3(nb), dim3(kNormBwdThreads), lds, st>>>(X, Wt, rstd, DY, rows, H, DX, dw_partial, rows_per_block)
+    rmsnorm_bwd_kernel<V><<<dim3(nb), dim3(kNormBwdThreads), lds, st>>>(X, Wt, rstd, DY, rows, H, DX, dw_partial, \
+                                                                        rows_per_block, static_cast<const uint16_t *>(dres))
     if (H <= 64 * 8 * 2) SWH_NORM_BWD(2);
     else if (H <= 64 * 8 * 4) SWH_NORM_BWD(4);
     else SWH_NORM_BWD(8);

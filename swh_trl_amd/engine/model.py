@@ -90,17 +90,50 @@ class _RMSNorm(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w, rstd = ctx.saved_tensors
-        H = x.shape[-1]
-        rows = x.numel() // H
-        rpb = 64
-        part = torch.empty((rows + rpb - 1) // rpb, H, device=x.device, dtype=torch.float32)
-        dx = torch.empty_like(x)
-        dyc = dy.contiguous()
-        call("swh_rmsnorm_bwd", x.data_ptr(), w.data_ptr(), rstd.data_ptr(), dyc.data_ptr(), rows, H, dx.data_ptr(),
-             part.data_ptr(), rpb, _stream())
-        if ctx.gw is not None:
-            ctx.gw.add_(part.sum(0).to(ctx.gw.dtype))
-        return dx, None, None, None
+        return _norm_backward(x, w, rstd, dy, None, ctx.gw), None, None, None
+
+
+def _norm_backward(x, w, rstd, dy, dres, gw):
+    """dx of the RMSNorm (+ dres, the residual branch's gradient, in the same
+    pass) and the weight gradient folded into its bf16 view in one launch."""
+    H = x.shape[-1]
+    rows = x.numel() // H
+    rpb = 64
+    nb = (rows + rpb - 1) // rpb
+    part = torch.empty(nb, H, device=x.device, dtype=torch.float32)
+    dx = torch.empty_like(x)
+    dyc = dy.contiguous()
+    dr = dres.contiguous() if dres is not None else None
+    call("swh_rmsnorm_bwd", x.data_ptr(), w.data_ptr(), rstd.data_ptr(), dyc.data_ptr(), rows, H, dx.data_ptr(),
+         part.data_ptr(), rpb, None if dr is None else dr.data_ptr(), _stream())
+    if gw is not None:
+        call("swh_rmsnorm_dw_accum", part.data_ptr(), nb, H, gw.data_ptr(), _stream())
+    return dx
+
+
+class _AddRMSNorm(torch.autograd.Function):
+    """s = bf16(x + r) (the residual add), h = RMSNorm(s) in one kernel; the
+    backward forms ds + d(norm)/ds in one pass and returns it for x and r."""
+
+    @staticmethod
+    def forward(ctx, x, r, w, gw, eps):
+        xc, rc = x.contiguous(), r.contiguous()
+        H = xc.shape[-1]
+        rows = xc.numel() // H
+        rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+        h, s = nn_ops.rmsnorm_residual(xc, rc, w, eps, rstd=rstd)
+        ctx.save_for_backward(s, w, rstd)
+        ctx.gw = gw
+        return s, h
+
+    @staticmethod
+    def backward(ctx, ds, dh):
+        s, w, rstd = ctx.saved_tensors
+        if dh is None:
+            g = ds
+        else:
+            g = _norm_backward(s, w, rstd, dh, ds, ctx.gw)
+        return g, g, None, None, None
 
 
 class _LMHeadLogp(torch.autograd.Function):
@@ -347,11 +380,13 @@ class CausalLM:
     def _gv(self, name):
         return self.g.get(name) if self.grad is not None else None
 
-    def _layer(self, i: int, x: torch.Tensor, positions, cos_t, sin_t, mask, kv_out=None):
+    def _layer(self, i: int, x: torch.Tensor, h: torch.Tensor, positions, cos_t, sin_t, mask, kv_out=None):
+        """Layer i on the residual stream x with h = RMSNorm_in(x) already formed;
+        returns (x + attention, the MLP output d): the caller folds x + d into
+        the next RMSNorm (`_AddRMSNorm`)."""
         c = self.cfg
         B, L, _ = x.shape
         Hq, Hkv, D = c.num_attention_heads, c.num_key_value_heads, c.head_dim
-        h = _RMSNorm.apply(x, self.p[f"l{i}.ln_in"], self._gv(f"l{i}.ln_in"), c.rms_norm_eps)
         qkv = _Linear.apply(h, self.p[f"l{i}.qkv_w"], self.p.get(f"l{i}.qkv_b"), self._gv(f"l{i}.qkv_w"),
                             self._gv(f"l{i}.qkv_b"))
         # split + rotate-half RoPE + [B, H, L, D] layout in one kernel each way
@@ -369,12 +404,11 @@ class CausalLM:
                 o = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, scale=D ** -0.5, enable_gqa=gqa)
         o = o.transpose(1, 2).reshape(B, L, c.q_dim)
         o = _Linear.apply(o, self.p[f"l{i}.o_w"], None, self._gv(f"l{i}.o_w"), None)
-        x = x + o
-        h = _RMSNorm.apply(x, self.p[f"l{i}.ln_post"], self._gv(f"l{i}.ln_post"), c.rms_norm_eps)
+        x, h = _AddRMSNorm.apply(x, o, self.p[f"l{i}.ln_post"], self._gv(f"l{i}.ln_post"), c.rms_norm_eps)
         gu = _Linear.apply(h, self.p[f"l{i}.gu_w"], None, self._gv(f"l{i}.gu_w"), None)
         a = nn_ops.SiluMulFn.apply(gu)
         d = _Linear.apply(a, self.p[f"l{i}.down_w"], None, self._gv(f"l{i}.down_w"), None)
-        return x + d
+        return x, d
 
     def hidden_states(self, ids: torch.Tensor, positions: Optional[torch.Tensor] = None,
                       key_mask: Optional[torch.Tensor] = None, kv_out=None, max_pos: Optional[int] = None,
@@ -411,11 +445,20 @@ class CausalLM:
             eye = torch.eye(L, device=ids.device, dtype=torch.bool)
             mask = causal & (km[:, None, None, :] | (eye & no_key[:, None, :, None]))
         x = _Embedding.apply(ids, self.p["embed"], self._gv("embed"), self._anchor)
+        d = None
+        eps = c.rms_norm_eps
         for i in range(c.num_hidden_layers):
+            # hook on the residual stream entering layer i's input norm: its gradient is
+            # formed by that norm's backward, the last of layer i's backward nodes
             if self.on_layer_grads is not None and torch.is_grad_enabled():
                 x = _GradReady.apply(x, i, self.on_layer_grads)
-            x = self._layer(i, x, positions, cos_t, sin_t, mask, kv_out)
-        return _RMSNorm.apply(x, self.p["norm"], self._gv("norm"), c.rms_norm_eps)
+            if d is None:
+                h = _RMSNorm.apply(x, self.p[f"l{i}.ln_in"], self._gv(f"l{i}.ln_in"), eps)
+            else:  # previous layer's residual add + this layer's input norm, one kernel
+                x, h = _AddRMSNorm.apply(x, d, self.p[f"l{i}.ln_in"], self._gv(f"l{i}.ln_in"), eps)
+            x, d = self._layer(i, x, h, positions, cos_t, sin_t, mask, kv_out)
+        _, h = _AddRMSNorm.apply(x, d, self.p["norm"], self._gv("norm"), eps)
+        return h
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """lm head (bf16 logits) on selected hidden states [.., H]."""

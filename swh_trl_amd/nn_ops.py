@@ -56,7 +56,7 @@ class RMSNormFn(torch.autograd.Function):
         part = torch.empty(nb, H, device=x.device, dtype=torch.float32)
         dyc = dy.contiguous()
         call("swh_rmsnorm_bwd", x.data_ptr(), w.data_ptr(), rstd.data_ptr(), dyc.data_ptr(), rows, H, dx.data_ptr(),
-             part.data_ptr(), rpb, _stream())
+             part.data_ptr(), rpb, None, _stream())
         return dx, part.sum(0).to(w.dtype), None
 
 
