@@ -20,6 +20,7 @@ for step in "$@"; do
     decab) run dec0 300 python tools/bench_decode.py && for v in vA vB; do SWH_LIB_PATH=tools/_build/$v.so run dec_$v 300 python tools/bench_decode.py || exit 1; done ;;
     attn) run attn 300 python -u -m pytest tests/test_kernels_gpu.py -x -v -m gpu -k attention --timeout 120 --timeout-method thread ;;
     benchab) SWH_ATTN=torch run bench_torchattn 600 python bench.py --steps 2 --warmup 1 --no-cpu-baseline && SWH_ATTN=hip run bench_hipattn 600 python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    dwab) SWH_DW_SPLIT=0 run b_nosplit 600 python bench.py --steps 4 --warmup 2 --no-cpu-baseline && run b_split 600 python bench.py --steps 4 --warmup 2 --no-cpu-baseline ;;
     kern) run kern 600 python -m pytest tests/test_kernels_gpu.py -q -m gpu ;;
     kernx) run kernx 600 python -m pytest tests/test_kernels_gpu.py -q -m gpu -x ;;
     dec) run dec 300 python tools/bench_decode.py ;;

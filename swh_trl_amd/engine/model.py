@@ -47,10 +47,36 @@ class _Linear(torch.autograd.Function):
         if ctx.gw is not None:
             dy2 = dy.reshape(-1, dy.shape[-1])
             x2 = x.reshape(-1, x.shape[-1])
-            ctx.gw.addmm_(dy2.t(), x2)
+            S = _dw_split(dy2.shape[0], dy2.shape[1] * x2.shape[1])
+            if S > 1:
+                # few output tiles over a long token dimension: split the tokens into S
+                # batched GEMMs (S x the workgroups), sum the partials into the gradient
+                Kc = dy2.shape[0] // S
+                parts = torch.bmm(dy2[:S * Kc].view(S, Kc, -1).transpose(1, 2), x2[:S * Kc].view(S, Kc, -1))
+                acc = parts.sum(0, dtype=torch.float32)
+                if S * Kc < dy2.shape[0]:
+                    acc.addmm_(dy2[S * Kc:].t().float(), x2[S * Kc:].float())
+                ctx.gw.add_(acc)
+            else:
+                ctx.gw.addmm_(dy2.t(), x2)
             if ctx.gb is not None:
                 ctx.gb.add_(dy2.sum(0, dtype=torch.float32).to(ctx.gb.dtype))
         return dx, None, None, None, None
+
+
+def _dw_split(tokens: int, outputs: int) -> int:
+    """K split of a weight-gradient GEMM dW[N, M] = dY^T X over `tokens`: the
+    small-output projections (o, qkv: <= 1.2M outputs = < 20 output tiles of
+    256 x 256) leave most CUs idle at any token count (0.33-0.4 PFLOP/s at
+    24576 tokens); splitting the tokens gives S x the tiles.  SWH_DW_SPLIT=0
+    keeps the single GEMM."""
+    if os.environ.get("SWH_DW_SPLIT", "1") == "0" or tokens < 8192:
+        return 1
+    if outputs <= 1_500_000:
+        return 8
+    if outputs <= 5_000_000:
+        return 4
+    return 1
 
 
 class _Embedding(torch.autograd.Function):
