@@ -387,17 +387,21 @@ __global__ __launch_bounds__(512) void fa_dq_kernel(FaArgs a) {
     }
 }
 
-// ---- dK / dV: a workgroup owns 16 keys of one KV head; wave w walks the queries of
-// head kvh * G + w (its own LDS tile for the transposed reads), then the G partial
-// dK / dV are summed in fixed order through LDS
+// ---- dK / dV: a workgroup owns 64 keys of one KV head (a wave per 16 keys) and walks
+// (query head of the group, 32-query block) rounds; each round's Q and dO blocks and
+// their softmax statistics are staged into LDS once (double-buffered, one barrier per
+// round) for the 4 key tiles, whose waves read Q / dO fragments and the transposed
+// tiles from there.  The GQA head sum stays inside each wave's accumulators.
 template <int D>
-__global__ __launch_bounds__(512) void fa_dkdv_kernel(FaArgs a) {
+__global__ __launch_bounds__(256) void fa_dkdv_kernel(FaArgs a) {
     constexpr int DC = D / 32, DB = D / 16, VS = fa_vs<D>();
-    __shared__ __attribute__((aligned(16))) uint16_t tiles[8][32 * VS];
-    const int tid = threadIdx.x;
+    constexpr int R = 2;  // 32-query sub-blocks per round: more work per barrier / prefetch
+    __shared__ __attribute__((aligned(16))) uint16_t qt[2][R][32 * VS], dt[2][R][32 * VS];
+    __shared__ float lse_s[2][32 * R], del_s[2][32 * R];
+    const int tid = threadIdx.x, nthr = blockDim.x;
     const int lane = tid & 63, wid = tid >> 6, g = lane >> 4, c16 = lane & 15;
     const int b = blockIdx.z, kvh = blockIdx.y, L = a.L, G = a.Hq / a.Hkv;
-    const int k0w = blockIdx.x * 16;
+    const int kb0 = blockIdx.x * 64, k0w = kb0 + wid * 16;
     const int kc = min(k0w + c16, L - 1);  // this lane's key column
     const int fv = a.first_valid ? a.first_valid[b] : 0;
     const int kmv = a.key_mask ? a.key_mask[(int64_t)b * L + kc] : 1;
@@ -414,79 +418,80 @@ __global__ __launch_bounds__(512) void fa_dkdv_kernel(FaArgs a) {
         dk[d] = f32x4a{0.f, 0.f, 0.f, 0.f};
         dv[d] = f32x4a{0.f, 0.f, 0.f, 0.f};
     }
-    uint16_t *tile = tiles[wid];
-    const int h = kvh * G + min(wid, G - 1);
-    const int64_t qrow = ((int64_t)b * a.Hq + h) * L;
-    const int qstart = k0w & ~31;  // causal: queries >= the workgroup's first key (32-aligned blocks)
-    const int nit = wid < G ? (L - qstart + 31) / 32 : 0;  // waves past the group's heads: no walk
-    // the next query block's Q / dO rows and softmax statistics stream while this one computes
-    u32x4 qr[2][DC], dr[2][DC], qn[2][DC], dn[2][DC];
-    float ls[8], dl[8], lsn[8], dln[8];
-    auto fetch = [&](int it, u32x4(&q_)[2][DC], u32x4(&d_)[2][DC], float(&l_)[8], float(&e_)[8]) {
-        const int r0 = qstart + 32 * it;
-        fa_load_rows<D>(q_, a.q + qrow * D, r0, L, c16, g);
-        fa_load_rows<D>(d_, a.dout + qrow * D, r0, L, c16, g);
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int qq = min(r0 + 16 * t + 4 * g + r, L - 1);
-                l_[4 * t + r] = a.lse[qrow + qq];
-                e_[4 * t + r] = a.delta[qrow + qq];
-            }
+    const int qstart = kb0;  // causal: queries >= the workgroup's first key
+    const int nb = (L - qstart + 32 * R - 1) / (32 * R), nit = G * nb;
+    auto rows_of = [&](int it, int64_t &qrow, int &r0) {
+        r0 = qstart + 32 * R * (it % nb);
+        qrow = ((int64_t)b * a.Hq + kvh * G + it / nb) * L;
     };
-    if (nit > 0) fetch(0, qn, dn, lsn, dln);
-    for (int it = 0; it < nit; ++it) {
-        fa_copy<D>(qr, qn);
-        fa_copy<D>(dr, dn);
+    FaStage<D> st[R];
+    auto load = [&](int it) {
+        int64_t qrow;
+        int r0;
+        rows_of(it, qrow, r0);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            ls[j] = lsn[j];
-            dl[j] = dln[j];
-        }
-        if (it + 1 < nit) fetch(it + 1, qn, dn, lsn, dln);
-        const int r0 = qstart + 32 * it;
-        f32x4a s[2], dp[2];
-        fa_abt<D>(s, qr, kf);   // S[q = r0 + 16 t + 4 g + r][key c16]
-        fa_abt<D>(dp, dr, vf);  // dP likewise
-        float p[8], ds[8];
+        for (int h = 0; h < R; ++h)
+            fa_stage_load<D>(st[h], a.q + qrow * D, a.dout + qrow * D, r0 + 32 * h, L, tid, nthr);
+    };
+    auto store = [&](int it, int buf) {  // staged blocks + the rows' lse / delta into LDS
+        int64_t qrow;
+        int r0;
+        rows_of(it, qrow, r0);
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int q = r0 + 16 * t + 4 * g + r;
-                const bool vis = (q < L) & fa_vis(q, k0w + c16, L, kmv, fv);
-                const float pv = vis ? __expf(s[t][r] * a.scale - ls[4 * t + r]) : 0.f;
-                p[4 * t + r] = pv;
-                ds[4 * t + r] = vis ? pv * (dp[t][r] - dl[4 * t + r]) : 0.f;
-            }
-        fa_xty<D, VS>(dv, tile, dr, p, c16, g);
-        fa_xty<D, VS>(dk, tile, qr, ds, c16, g);
-    }
-    // sum the G heads' partials in fixed order: park all, then wave 0 adds them up
+        for (int h = 0; h < R; ++h) fa_stage_store<D, VS>(st[h], qt[buf][h], dt[buf][h], tid, nthr);
+        if (tid < 32 * R) lse_s[buf][tid] = a.lse[qrow + min(r0 + tid, L - 1)];
+        else if (tid < 64 * R) del_s[buf][tid - 32 * R] = a.delta[qrow + min(r0 + tid - 32 * R, L - 1)];
+    };
+    load(0);
+    store(0, 0);
     __syncthreads();
-    float *red = reinterpret_cast<float *>(tiles);  // [G][DB][64 lanes][4] f32 (one of dk / dv at a time)
-    const bool store = k0w + c16 < L;
-    uint16_t *kb = a.dk + (kvrow + k0w + c16) * D;
-    uint16_t *vb = a.dv + (kvrow + k0w + c16) * D;
+    int buf = 0;
+    for (int it = 0; it < nit; ++it, buf ^= 1) {
+        const bool more = it + 1 < nit;
+        if (more) load(it + 1);  // the next round's Q / dO blocks stream while this one computes
+        const int r0 = qstart + 32 * R * (it % nb);
 #pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-        f32x4a(&x)[DB] = pass == 0 ? dk : dv;
+        for (int h = 0; h < R; ++h) {
+            const int rh = r0 + 32 * h;
+            if (rh + 31 >= k0w && rh < L && k0w < L) {  // some query of the block sees some key of this wave
+                u32x4 qr[2][DC], dr[2][DC];
+                fa_rows_lds<D, VS>(qr, qt[buf][h], c16, g);
+                fa_rows_lds<D, VS>(dr, dt[buf][h], c16, g);
+                f32x4a s[2], dp[2];
+                fa_abt<D>(s, qr, kf);   // S[q = rh + 16 t + 4 g + r][key c16]
+                fa_abt<D>(dp, dr, vf);  // dP likewise
+                float p[8], ds[8];
 #pragma unroll
-        for (int d = 0; d < DB; ++d) *reinterpret_cast<f32x4a *>(red + ((wid * DB + d) * 64 + lane) * 4) = x[d];
-        __syncthreads();
-        if (wid == 0) {
+                for (int t = 0; t < 2; ++t)
 #pragma unroll
-            for (int d = 0; d < DB; ++d) {
-                f32x4a sum = x[d];
-                for (int w = 1; w < G; ++w) sum += *reinterpret_cast<const f32x4a *>(red + ((w * DB + d) * 64 + lane) * 4);
-                const float sc = pass == 0 ? a.scale : 1.f;
-                const uint32_t lo = (uint32_t)f32_to_bf16_bits(sum[0] * sc) | ((uint32_t)f32_to_bf16_bits(sum[1] * sc) << 16);
-                const uint32_t hi = (uint32_t)f32_to_bf16_bits(sum[2] * sc) | ((uint32_t)f32_to_bf16_bits(sum[3] * sc) << 16);
-                if (store) *reinterpret_cast<uint2 *>((pass == 0 ? kb : vb) + d * 16 + 4 * g) = uint2{lo, hi};
+                    for (int r = 0; r < 4; ++r) {
+                        const int qi = 32 * h + 16 * t + 4 * g + r, q = r0 + qi;
+                        const bool vis = (q < L) & fa_vis(q, k0w + c16, L, kmv, fv);
+                        const float pv = vis ? __expf(s[t][r] * a.scale - lse_s[buf][qi]) : 0.f;
+                        p[4 * t + r] = pv;
+                        ds[4 * t + r] = vis ? pv * (dp[t][r] - del_s[buf][qi]) : 0.f;
+                    }
+                fa_xty_shared<D, VS>(dv, dt[buf][h], p, c16, g);
+                fa_xty_shared<D, VS>(dk, qt[buf][h], ds, c16, g);
             }
         }
+        if (more) store(it + 1, buf ^ 1);
         __syncthreads();
+    }
+    if (k0w + c16 < L) {
+        uint16_t *kb = a.dk + (kvrow + k0w + c16) * D;
+        uint16_t *vb = a.dv + (kvrow + k0w + c16) * D;
+#pragma unroll
+        for (int d = 0; d < DB; ++d) {
+            const uint32_t klo = (uint32_t)f32_to_bf16_bits(dk[d][0] * a.scale) |
+                                 ((uint32_t)f32_to_bf16_bits(dk[d][1] * a.scale) << 16);
+            const uint32_t khi = (uint32_t)f32_to_bf16_bits(dk[d][2] * a.scale) |
+                                 ((uint32_t)f32_to_bf16_bits(dk[d][3] * a.scale) << 16);
+            *reinterpret_cast<uint2 *>(kb + d * 16 + 4 * g) = uint2{klo, khi};
+            const uint32_t vlo = (uint32_t)f32_to_bf16_bits(dv[d][0]) | ((uint32_t)f32_to_bf16_bits(dv[d][1]) << 16);
+            const uint32_t vhi = (uint32_t)f32_to_bf16_bits(dv[d][2]) | ((uint32_t)f32_to_bf16_bits(dv[d][3]) << 16);
+            *reinterpret_cast<uint2 *>(vb + d * 16 + 4 * g) = uint2{vlo, vhi};
+        }
     }
 }
 
@@ -555,14 +560,15 @@ extern "C" int swh_attn_bwd(const void *q, const void *k, const void *v, const v
     const int64_t rows = B * Hq * L;
     const dim3 grid((unsigned)((L + 15) / 16), (unsigned)Hkv, (unsigned)B);
     const unsigned thr = 64u * (unsigned)(Hq / Hkv < 4 ? 4 : Hq / Hkv);
+    const dim3 gk((unsigned)((L + 63) / 64), (unsigned)Hkv, (unsigned)B);
     if (D == 64) {
         fa_delta_kernel<64><<<dim3((unsigned)((rows + 255) / 256)), 256, 0, s>>>(a, rows);
         fa_dq_kernel<64><<<grid, thr, 0, s>>>(a);
-        fa_dkdv_kernel<64><<<grid, thr, 0, s>>>(a);
+        fa_dkdv_kernel<64><<<gk, 256, 0, s>>>(a);
     } else {
         fa_delta_kernel<128><<<dim3((unsigned)((rows + 255) / 256)), 256, 0, s>>>(a, rows);
         fa_dq_kernel<128><<<grid, thr, 0, s>>>(a);
-        fa_dkdv_kernel<128><<<grid, thr, 0, s>>>(a);
+        fa_dkdv_kernel<128><<<gk, 256, 0, s>>>(a);
     }
     return launch_status();
 }

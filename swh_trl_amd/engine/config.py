@@ -63,6 +63,15 @@ def tiny_qwen2(vocab_size: int = 1024, layers: int = 2) -> DecoderConfig:
                          max_position_embeddings=4096)
 
 
+def tiny_llama(vocab_size: int = 2048, layers: int = 2) -> DecoderConfig:
+    """Small Llama-3-shaped model for parity tests: head_dim 128, GQA 4:1,
+    no attention bias, untied lm head (the config-5 code paths at test size)."""
+    return DecoderConfig(vocab_size=vocab_size, hidden_size=1024, intermediate_size=2048, num_hidden_layers=layers,
+                         num_attention_heads=8, num_key_value_heads=2, head_dim=128, rope_theta=500000.0,
+                         rms_norm_eps=1e-5, tie_word_embeddings=False, attention_bias=False,
+                         max_position_embeddings=4096, model_type="llama")
+
+
 def from_hf_config(cfg) -> DecoderConfig:
     """Build from a transformers Qwen2Config / LlamaConfig (object or dict)."""
     g = (lambda k, d=None: cfg.get(k, d)) if isinstance(cfg, dict) else (lambda k, d=None: getattr(cfg, k, d))
@@ -79,4 +88,4 @@ def from_hf_config(cfg) -> DecoderConfig:
                          max_position_embeddings=int(g("max_position_embeddings", 32768)), model_type=mt)
 
 
-PRESETS = {"qwen2.5-0.5b": qwen2_5_0_5b, "llama-3-8b": llama3_8b, "tiny": tiny_qwen2}
+PRESETS = {"qwen2.5-0.5b": qwen2_5_0_5b, "llama-3-8b": llama3_8b, "tiny": tiny_qwen2, "tiny-llama": tiny_llama}

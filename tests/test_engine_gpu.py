@@ -373,3 +373,103 @@ def test_hip_attention_path_matches_sdpa_path(dev, monkeypatch):
     torch.testing.assert_close(outs["hip"][0], outs["torch"][0], rtol=3e-2, atol=3e-2)
     gt, gh = outs["torch"][1], outs["hip"][1]
     assert (gh - gt).norm() <= 0.05 * gt.norm()
+
+
+# ---- Llama-3 architecture (BASELINE config 5 code paths at test size): head_dim 128,
+# GQA 4:1, no qkv bias, untied lm head; oracle = transformers LlamaForCausalLM
+def _tiny_llama(dev, seed=0, layers=2):
+    from swh_trl_amd.engine import CausalLM, tiny_llama
+    return CausalLM(tiny_llama(2048, layers), dev, seed=seed, init_std=0.05)
+
+
+def _hf_llama_from(m, dtype):
+    from transformers import LlamaConfig, LlamaForCausalLM
+    c = m.cfg
+    hc = LlamaConfig(vocab_size=c.vocab_size, hidden_size=c.hidden_size, intermediate_size=c.intermediate_size,
+                     num_hidden_layers=c.num_hidden_layers, num_attention_heads=c.num_attention_heads,
+                     num_key_value_heads=c.num_key_value_heads, head_dim=c.head_dim, rope_theta=c.rope_theta,
+                     rms_norm_eps=c.rms_norm_eps, tie_word_embeddings=False, attention_bias=False, mlp_bias=False,
+                     max_position_embeddings=c.max_position_embeddings)
+    hc._attn_implementation = "sdpa"
+    hf = LlamaForCausalLM(hc)
+    sd = {k: v.detach().float().cpu() for k, v in m.hf_state_dict().items()}
+    missing, unexpected = hf.load_state_dict(sd, strict=False)
+    assert not [k for k in missing if "rotary" not in k], missing
+    assert not unexpected, unexpected
+    return hf.to(dtype).to(m.device).eval()
+
+
+def test_llama_forward_matches_transformers(dev):
+    m = _tiny_llama(dev)
+    assert "lm_head" in m.p  # untied
+    hf = _hf_llama_from(m, torch.float32)
+    g = torch.Generator().manual_seed(0)
+    ids = torch.randint(0, m.cfg.vocab_size, (3, 40), generator=g).to(dev)
+    mask = torch.ones_like(ids)
+    mask[2, :9] = 0
+    with torch.no_grad():
+        pos = (mask.cumsum(-1) - 1).clamp(min=0)
+        lg = m.logits(m.hidden_states(ids, positions=pos, key_mask=mask)).float()
+        ref = hf(input_ids=ids, attention_mask=mask, position_ids=pos).logits.float()
+    keep = mask.bool()
+    err = (lg - ref)[keep].abs().max().item()
+    scale = ref[keep].abs().max().item()
+    assert err <= 0.03 * scale + 0.03, (err, scale)
+
+
+def test_llama_greedy_matches_transformers_generate(dev):
+    """Fused decode path at head_dim 128 / GQA 4 / untied head vs transformers generate."""
+    from swh_trl_amd.engine import DecodeEngine
+    m = _tiny_llama(dev, seed=3)
+    hf = _hf_llama_from(m, torch.bfloat16)
+    g = torch.Generator().manual_seed(3)
+    B, P, C = 4, 10, 32
+    ids = torch.randint(0, m.cfg.vocab_size, (B, P), generator=g).to(dev)
+    mask = torch.ones(B, P, dtype=torch.int64, device=dev)
+    eng = DecodeEngine(m, B, P, C)
+    assert eng.fused
+    mine, _ = eng.generate(ids, mask, C, greedy=True)
+    with torch.no_grad():
+        ref = hf.generate(input_ids=ids, attention_mask=mask, max_new_tokens=C, do_sample=False,
+                          pad_token_id=0, eos_token_id=None)[:, P:]
+    for b in range(B):
+        neq = (mine[b] != ref[b]).nonzero()
+        if neq.numel() == 0:
+            continue
+        t = int(neq[0])
+        seq = torch.cat([ids[b], ref[b, :t]]).unsqueeze(0)
+        with torch.no_grad():
+            lg = hf(input_ids=seq).logits[0, -1].float()
+        top2 = lg.topk(2).values
+        # a near-tie within the forward-parity tolerance (3% of the logit scale at
+        # hidden 1024: test_llama_forward_matches_transformers)
+        assert (top2[0] - top2[1]).item() <= 0.03 * lg.abs().max().item() + 1e-3, (b, t, top2)
+
+
+def test_llama_grpo_step_with_frozen_ref_kl(dev):
+    """Config-5 shape of the loop at test size: beta > 0 keeps a frozen reference
+    copy whose per-token log-probs enter the k3 KL; the first step's KL is 0
+    (policy == reference) and the reference stays frozen while the policy moves."""
+    from swh_trl_amd.engine import tiny_llama
+    from swh_trl_amd.trainer import GRPOConfig, GRPOTrainer
+    cfg = tiny_llama(2048, 2)
+    ds = [{"prompt": None, "prompt_ids": list(range(5 + i, 21 + i))} for i in range(8)]
+
+    def rew(prompts=None, completions=None, completion_ids=None, **kw):
+        return [float(len(set(c)) % 5) for c in completion_ids]
+
+    args = GRPOConfig(per_device_train_batch_size=8, gradient_accumulation_steps=1, num_generations=4,
+                      max_prompt_length=16, max_completion_length=24, max_steps=2, learning_rate=1e-3, beta=0.04,
+                      generation_kwargs={"eos_token_id": 1, "pad_token_id": 0, "min_new_tokens": 24},
+                      logging_steps=1)
+    tr = GRPOTrainer(model=cfg, reward_funcs=rew, args=args, train_dataset=ds)
+    assert tr.ref_model is not None
+    ref0 = tr.ref_model.flat.clone()
+    before = tr.model.flat.clone()
+    state = tr.train()
+    assert state.global_step == 2
+    assert torch.equal(ref0, tr.ref_model.flat)
+    assert not torch.equal(before, tr.model.flat)
+    first, last = state.log_history[0], state.log_history[-1]
+    assert abs(first["kl"]) < 1e-3, first  # scoring vs training forward: bf16-level differences only
+    assert last["kl"] >= 0 and all(v == v for v in (last["loss"], last["grad_norm"], last["kl"]))

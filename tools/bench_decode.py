@@ -169,6 +169,30 @@ def dual(eng, m):
         e1.record()
         e1.synchronize()
         print(f"{name:24s} {1000 * e0.elapsed_time(e1) / 5 / L:8.2f} us per layer (gate_up + down)", flush=True)
+    # two separately captured half-batch graphs replayed on two streams
+    gs = []
+    for r0, r1 in ((0, h), (h, B)):
+        chain(r0, r1)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            chain(r0, r1)
+        gs.append(g)
+    s2 = [torch.cuda.Stream(), torch.cuda.Stream()]
+    main = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        for g, st in zip(gs, s2):
+            st.wait_stream(main)
+            with torch.cuda.stream(st):
+                g.replay()
+        for st in s2:
+            main.wait_stream(st)
+    e1.record()
+    e1.synchronize()
+    print(f"{'two graphs 2 streams':24s} {1000 * e0.elapsed_time(e1) / 5 / L:8.2f} us per layer (gate_up + down)",
+          flush=True)
 
 
 def main():
