@@ -278,7 +278,7 @@ int swh_attn_bwd(const void *q, const void *k, const void *v, const void *out, c
  * the device-resident table jobs[njobs] = {W [rows, cols] bf16, w [cols] bf16,
  * out [rows, cols] bf16, rows, cols, row0 (prefix sum of rows)},
  * out[n][k] = bf16(W[n][k] * w[k]); cols % 8 == 0, 16-B aligned rows.
- * total_rows = sum of rows.  Run once per generate(): the policy update changes
+ * total_rows = sum of rows, njobs <= 256.  Run once per generate(): the policy update changes
  * W and w (transformers applies w inside Qwen2RMSNorm every token). */
 int swh_fold_norm(const void *jobs, int32_t njobs, int64_t total_rows, void *stream);
 

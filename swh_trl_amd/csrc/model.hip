@@ -237,26 +237,71 @@ struct FoldJob {
     int64_t row0;  // first global row of this job
 };
 
+constexpr int kFoldMaxJobs = 256, kFoldRows = 8;
+// a workgroup folds chunks of kFoldRows rows; the job table is read into LDS once
+// and a chunk finds its job by binary search there.  A chunk inside one job is one
+// flat run of 16-B pieces (every thread's loads issued together); a chunk that
+// straddles jobs goes row by row.
 __global__ __launch_bounds__(256) void fold_norm_kernel(const FoldJob *__restrict__ jobs, int njobs,
                                                         int64_t total_rows) {
-    for (int64_t gr = blockIdx.x; gr < total_rows; gr += gridDim.x) {
-        int j = 0;
-        while (j + 1 < njobs && jobs[j + 1].row0 <= gr) ++j;
-        const FoldJob jb = jobs[j];
-        const int64_t r = gr - jb.row0;
-        const uint4 *src = reinterpret_cast<const uint4 *>(jb.w + r * jb.cols);
-        const uint4 *nv = reinterpret_cast<const uint4 *>(jb.nw);
-        uint4 *dst = reinterpret_cast<uint4 *>(jb.out + r * jb.cols);
-        for (int64_t c = threadIdx.x; c < jb.cols / 8; c += blockDim.x) {
-            float a[8], b[8];
-            unpack16<SWH_BF16>(src[c], a);
-            unpack16<SWH_BF16>(nv[c], b);
-            uint32_t o[4];
+    __shared__ FoldJob tab[kFoldMaxJobs];
+    for (int j = threadIdx.x; j < njobs; j += blockDim.x) tab[j] = jobs[j];
+    __syncthreads();
+    auto find = [&](int64_t gr) {
+        int lo = 0, hi = njobs - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (tab[mid].row0 <= gr) lo = mid;
+            else hi = mid - 1;
+        }
+        return lo;
+    };
+    auto fold8 = [](const uint4 &x, const uint4 &w) {
+        float a[8], b[8];
+        unpack16<SWH_BF16>(x, a);
+        unpack16<SWH_BF16>(w, b);
+        uint32_t o[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                o[q] = (uint32_t)f32_to_bf16_bits(a[2 * q] * b[2 * q]) |
-                       ((uint32_t)f32_to_bf16_bits(a[2 * q + 1] * b[2 * q + 1]) << 16);
-            dst[c] = uint4{o[0], o[1], o[2], o[3]};
+        for (int q = 0; q < 4; ++q)
+            o[q] = (uint32_t)f32_to_bf16_bits(a[2 * q] * b[2 * q]) |
+                   ((uint32_t)f32_to_bf16_bits(a[2 * q + 1] * b[2 * q + 1]) << 16);
+        return uint4{o[0], o[1], o[2], o[3]};
+    };
+    const int64_t nchunk = (total_rows + kFoldRows - 1) / kFoldRows;
+    for (int64_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
+        const int64_t g0 = ch * kFoldRows, g1 = min(g0 + kFoldRows, total_rows);
+        const int j = find(g0);
+        const FoldJob &jb = tab[j];
+        if (g1 <= jb.row0 + jb.rows) {  // one job: a flat run of (g1 - g0) * cols / 8 pieces
+            const int64_t cpr = jb.cols / 8, np = (g1 - g0) * cpr;
+            const uint4 *src = reinterpret_cast<const uint4 *>(jb.w + (g0 - jb.row0) * jb.cols);
+            const uint4 *nv = reinterpret_cast<const uint4 *>(jb.nw);
+            uint4 *dst = reinterpret_cast<uint4 *>(jb.out + (g0 - jb.row0) * jb.cols);
+            for (int64_t p0 = threadIdx.x; p0 < np; p0 += 4 * blockDim.x) {
+                uint4 x[4], w[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int64_t p = p0 + u * blockDim.x;
+                    if (p < np) {
+                        x[u] = src[p];
+                        w[u] = nv[p % cpr];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int64_t p = p0 + u * blockDim.x;
+                    if (p < np) dst[p] = fold8(x[u], w[u]);
+                }
+            }
+        } else {
+            for (int64_t gr = g0; gr < g1; ++gr) {
+                const FoldJob &jr = tab[find(gr)];
+                const int64_t r = gr - jr.row0;
+                const uint4 *src = reinterpret_cast<const uint4 *>(jr.w + r * jr.cols);
+                const uint4 *nv = reinterpret_cast<const uint4 *>(jr.nw);
+                uint4 *dst = reinterpret_cast<uint4 *>(jr.out + r * jr.cols);
+                for (int64_t c = threadIdx.x; c < jr.cols / 8; c += blockDim.x) dst[c] = fold8(src[c], nv[c]);
+            }
         }
     }
 }
@@ -372,18 +417,39 @@ extern "C" int swh_rmsnorm_fwd(const void *x, const void *residual, void *residu
 
 // d weight: gw[h] = bf16(gw[h] + bf16(sum_b part[b][h])) — the partial column sums of
 // swh_rmsnorm_bwd folded into the bf16 gradient view in one launch
-__global__ __launch_bounds__(256) void rmsnorm_dw_accum_kernel(const float *__restrict__ part, int64_t nb, int64_t H,
-                                                              uint16_t *__restrict__ gw) {
-    const int64_t h = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (h >= H) return;
+// a workgroup = 64 columns x 16 row slices: slice s sums partial rows s, s + 16, ...
+// (loads issued 8 at a time), then the 16 slice sums add in fixed order through LDS
+constexpr int kDwSlices = 16;
+__global__ __launch_bounds__(64 * kDwSlices) void rmsnorm_dw_accum_kernel(const float *__restrict__ part, int64_t nb,
+                                                                         int64_t H, uint16_t *__restrict__ gw) {
+    __shared__ float red[kDwSlices][64];
+    const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
+    const int64_t h = (int64_t)blockIdx.x * 64 + c;
     float t = 0.f;
-    for (int64_t b = 0; b < nb; ++b) t += part[b * H + h];
-    gw[h] = f32_to_bf16_bits(bf16_bits_to_f32(gw[h]) + round_bf16(t));
+    if (h < H) {
+        int64_t b = sl;
+        for (; b + 7 * kDwSlices < nb; b += 8 * kDwSlices) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = part[(b + j * kDwSlices) * H + h];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) t += v[j];
+        }
+        for (; b < nb; b += kDwSlices) t += part[b * H + h];
+    }
+    red[sl][c] = t;
+    __syncthreads();
+    if (sl == 0 && h < H) {
+        float u = 0.f;
+#pragma unroll
+        for (int q = 0; q < kDwSlices; ++q) u += red[q][c];
+        gw[h] = f32_to_bf16_bits(bf16_bits_to_f32(gw[h]) + round_bf16(u));
+    }
 }
 
 extern "C" int swh_rmsnorm_dw_accum(const float *dw_partial, int64_t nblocks, int64_t H, void *grad_w, void *stream) {
     if (!dw_partial || !grad_w || nblocks <= 0 || H <= 0) return SWH_E_ARG;
-    rmsnorm_dw_accum_kernel<<<dim3((unsigned)((H + 255) / 256)), 256, 0, static_cast<hipStream_t>(stream)>>>(
+    rmsnorm_dw_accum_kernel<<<dim3((unsigned)((H + 63) / 64)), 64 * kDwSlices, 0, static_cast<hipStream_t>(stream)>>>(
         dw_partial, nblocks, H, static_cast<uint16_t *>(grad_w));
     return launch_status();
 }
@@ -434,8 +500,9 @@ extern "C" int swh_silu_mul_bwd(const void *gu, const void *dout, int64_t rows, 
 }
 
 extern "C" int swh_fold_norm(const void *jobs, int32_t njobs, int64_t total_rows, void *stream) {
-    if (!jobs || njobs <= 0 || total_rows <= 0) return SWH_E_ARG;
-    const int64_t grid = total_rows < 8192 ? total_rows : 8192;
+    if (!jobs || njobs <= 0 || njobs > kFoldMaxJobs || total_rows <= 0) return SWH_E_ARG;
+    const int64_t nchunk = (total_rows + kFoldRows - 1) / kFoldRows;
+    const int64_t grid = nchunk < 4096 ? nchunk : 4096;
     fold_norm_kernel<<<dim3((unsigned)grid), 256, 0, static_cast<hipStream_t>(stream)>>>(
         static_cast<const FoldJob *>(jobs), njobs, total_rows);
     return launch_status();

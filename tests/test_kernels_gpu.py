@@ -472,6 +472,58 @@ def test_rmsnorm_backward(ops, dev):
     torch.testing.assert_close(wd.grad.cpu().double(), wr.grad, rtol=2e-2, atol=5e-2)
 
 
+@pytest.mark.parametrize("rows", [6144, 77])
+def test_rmsnorm_backward_dres_and_dw_accumulation(ops, dev, rows):
+    """engine/model.py _norm_backward: dx + the residual branch's gradient in one
+    pass, the weight gradient summed from the per-block partials (swh_rmsnorm_dw_accum)
+    and added to an existing bf16 gradient; rows = one training micro-batch and a ragged count."""
+    from swh_trl_amd.engine.model import _norm_backward
+    g = _gen(21)
+    H = 896
+    x = torch.randn(rows, H, generator=g).to(torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(H, generator=g)).to(torch.bfloat16)
+    dy = torch.randn(rows, H, generator=g).to(torch.bfloat16)
+    dres = torch.randn(rows, H, generator=g).to(torch.bfloat16)
+    gw0 = torch.randn(H, generator=g).to(torch.bfloat16)
+    xf = x.float()
+    rstd = torch.rsqrt(xf.pow(2).mean(-1) + 1e-6)
+    gw = gw0.to(dev)
+    dx = _norm_backward(x.to(dev), w.to(dev), rstd.to(dev), dy.to(dev), dres.to(dev), gw)
+    xr, wr = x.double().requires_grad_(True), w.double().requires_grad_(True)
+    yr = wr * (xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6))
+    yr.backward(dy.double())
+    torch.testing.assert_close(dx.cpu().double(), xr.grad + dres.double(), rtol=2e-2, atol=3e-2)
+    # dW = sum over rows of dy * bf16(x * rstd) (Qwen2RMSNorm's rounding point, as the
+    # forward computes it), then two bf16 roundings (the summed partial, the accumulated view)
+    xhat = (xf * rstd[:, None]).to(torch.bfloat16).double()
+    dw = (dy.double() * xhat).sum(0)
+    ref_gw = gw0.double() + dw
+    err = (gw.cpu().double() - ref_gw).abs()
+    bound = 2.0 ** -7 * (dw.abs() + gw0.double().abs()) + 1e-2
+    assert (err <= bound).all(), (err.max().item(), (err / bound).max().item())
+
+
+def test_fold_norm_ragged_jobs(ops, dev):
+    """swh_fold_norm over jobs whose row counts are not multiples of the kernel's
+    8-row chunks (chunks straddle jobs) and of different widths: bit-identical to
+    torch's bf16 W * w for every job."""
+    from swh_trl_amd._lib import call
+    g = _gen(31)
+    shapes = [(5, 16), (13, 896), (3, 24), (1, 8), (40, 64)]
+    ws = [torch.randn(r, c, generator=g).to(torch.bfloat16).to(dev) for r, c in shapes]
+    nws = [(1 + 0.2 * torch.randn(c, generator=g)).to(torch.bfloat16).to(dev) for _, c in shapes]
+    outs = [torch.zeros_like(w) for w in ws]
+    tab, row0 = [], 0
+    for w, nw, o in zip(ws, nws, outs):
+        tab += [w.data_ptr(), nw.data_ptr(), o.data_ptr(), w.shape[0], w.shape[1], row0]
+        row0 += w.shape[0]
+    t = torch.tensor(tab, dtype=torch.int64).to(dev)
+    call("swh_fold_norm", t.data_ptr(), len(shapes), row0, ops._stream())
+    torch.cuda.synchronize()
+    for w, nw, o in zip(ws, nws, outs):
+        assert torch.equal(o, w * nw)
+
+
 def test_silu_mul(ops, dev):
     from swh_trl_amd import nn_ops
     g = _gen(19)
