@@ -127,6 +127,9 @@ __host__ __device__ inline GemmLds gemm_lds(int cb, int mr, int nw, int krmax, i
 #ifndef SWH_ROUND_PREFETCH
 #define SWH_ROUND_PREFETCH 0  // all A reads of a full round before its MFMAs (A/B: tools/build_variant.py)
 #endif
+#ifndef SWH_LM_RING
+#define SWH_LM_RING 1  // lm-head tile loop: refill each weight register right after its MFMA (A/B)
+#endif
 #ifndef SWH_FLAT_MERGE
 #define SWH_FLAT_MERGE 0  // one-barrier flat wave merge instead of the tree (A/B)
 #endif
@@ -718,6 +721,10 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
         const unsigned char *xrow = xs + rl * RS + kq * 2;
+        // ring refill: k-step ks's weight register takes the next tile's fragment as
+        // soon as its MFMA has read it, so a wave always has KS loads in flight
+        const bool ring = SWH_LM_RING && KSC != 0 && t + tstep < ntile;
+        const uint16_t *wnext = w + wrow_of(ring ? t + tstep : t) * K + kq;
         if constexpr (KSC != 0) {
             // A fragments double-buffered one k-step ahead; the scheduling barrier
             // keeps the compiler from hoisting every read (register pressure)
@@ -735,6 +742,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
                 for (int i = 0; i < 4; ++i)
                     acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[ks & 1][i]), as_bf16x8(bv[ks]),
                                                                     acc[i], 0, 0, 0);
+                if (ring) bv[ks] = *reinterpret_cast<const uint4 *>(wnext + ks * 32);
                 __builtin_amdgcn_sched_barrier(0);
             }
         } else {
@@ -749,7 +757,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
                 }
             }
         }
-        if (t + tstep < ntile) issue(t + tstep);
+        if (!ring && t + tstep < ntile) issue(t + tstep);
         SWH_GEMM_TRACE(4);
         if constexpr (SAMPLE) {
             const int col = t * 16 + rl;

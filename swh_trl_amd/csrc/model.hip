@@ -97,19 +97,33 @@ __global__ __launch_bounds__(kNormBwdThreads) void rmsnorm_bwd_kernel(
 #pragma unroll
         for (int k = 0; k < 8; ++k) dwa[j][k] = 0.f;
     }
-    for (int64_t r = r0 + wid; r < r1; r += NWV) {
-        const uint4 *xr = reinterpret_cast<const uint4 *>(x + r * H);
-        const uint4 *gr = reinterpret_cast<const uint4 *>(dy + r * H);
-        uint4 xv[VEC], gv[VEC];
+    // a row's x / dy / dres (and rstd) are loaded one row ahead: the next row's loads
+    // are in flight while this row reduces and stores
+    uint4 nx[VEC], ng[VEC], nd[VEC];
+    float nrs = 0.f;
+    auto load_row = [&](int64_t r) {
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
             const int v = lane + 64 * j;
             if (v < nv) {
-                xv[j] = xr[v];
-                gv[j] = gr[v];
+                nx[j] = reinterpret_cast<const uint4 *>(x + r * H)[v];
+                ng[j] = reinterpret_cast<const uint4 *>(dy + r * H)[v];
+                if (dres) nd[j] = reinterpret_cast<const uint4 *>(dres + r * H)[v];
             }
         }
-        const float rs = rstd[r];
+        nrs = rstd[r];
+    };
+    if (r0 + wid < r1) load_row(r0 + wid);
+    for (int64_t r = r0 + wid; r < r1; r += NWV) {
+        uint4 xv[VEC], gv[VEC], dv[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            xv[j] = nx[j];
+            gv[j] = ng[j];
+            dv[j] = nd[j];
+        }
+        const float rs = nrs;
+        if (r + NWV < r1) load_row(r + NWV);
         float c = 0.f;
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
@@ -138,7 +152,7 @@ __global__ __launch_bounds__(kNormBwdThreads) void rmsnorm_bwd_kernel(
                 }
                 if (dres) {  // + the residual branch's gradient: bf16(bf16(dx_norm) + dres), as autograd adds them
                     float d[8];
-                    unpack16<SWH_BF16>(reinterpret_cast<const uint4 *>(dres + r * H)[lane + 64 * j], d);
+                    unpack16<SWH_BF16>(dv[j], d);
 #pragma unroll
                     for (int k = 0; k < 8; ++k) a[k] = round_bf16(a[k]) + d[k];
                 }

@@ -62,32 +62,46 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float *__restrict__ p, 
         const float denom = sqrtf(vv) / bc2_sqrt + eps;
         pp = pp - step_size * (mm / denom);
     };
-    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n4; i += stride) {
-        float4 pp = reinterpret_cast<float4 *>(p)[i];
-        float4 mm = reinterpret_cast<float4 *>(m)[i];
-        float4 vv = reinterpret_cast<float4 *>(v)[i];
-        float gg[4];
-        if constexpr (GDT == SWH_F32) {
-            const float4 t = reinterpret_cast<const float4 *>(g)[i];
-            gg[0] = t.x; gg[1] = t.y; gg[2] = t.z; gg[3] = t.w;
-        } else {
-            const uint2 t = reinterpret_cast<const uint2 *>(g)[i];
-            gg[0] = Elem<GDT>::load(reinterpret_cast<const uint16_t *>(&t.x));
-            gg[1] = Elem<GDT>::load(reinterpret_cast<const uint16_t *>(&t.x) + 1);
-            gg[2] = Elem<GDT>::load(reinterpret_cast<const uint16_t *>(&t.y));
-            gg[3] = Elem<GDT>::load(reinterpret_cast<const uint16_t *>(&t.y) + 1);
+    // U grid-strided float4 groups per trip, every load of the trip issued before any math
+    constexpr int U = 2;
+    for (int64_t i0 = (int64_t)blockIdx.x * kThreads + threadIdx.x; i0 < n4; i0 += U * stride) {
+        float4 pp[U], mm[U], vv[U];
+        float gg[U][4];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * stride;
+            if (i < n4) {
+                pp[u] = reinterpret_cast<float4 *>(p)[i];
+                mm[u] = reinterpret_cast<float4 *>(m)[i];
+                vv[u] = reinterpret_cast<float4 *>(v)[i];
+                if constexpr (GDT == SWH_F32) {
+                    const float4 t = reinterpret_cast<const float4 *>(g)[i];
+                    gg[u][0] = t.x; gg[u][1] = t.y; gg[u][2] = t.z; gg[u][3] = t.w;
+                } else {
+                    const uint2 t = reinterpret_cast<const uint2 *>(g)[i];
+                    gg[u][0] = Elem<GDT>::load(reinterpret_cast<const uint16_t *>(&t.x));
+                    gg[u][1] = Elem<GDT>::load(reinterpret_cast<const uint16_t *>(&t.x) + 1);
+                    gg[u][2] = Elem<GDT>::load(reinterpret_cast<const uint16_t *>(&t.y));
+                    gg[u][3] = Elem<GDT>::load(reinterpret_cast<const uint16_t *>(&t.y) + 1);
+                }
+            }
         }
-        upd(pp.x, mm.x, vv.x, gg[0]);
-        upd(pp.y, mm.y, vv.y, gg[1]);
-        upd(pp.z, mm.z, vv.z, gg[2]);
-        upd(pp.w, mm.w, vv.w, gg[3]);
-        reinterpret_cast<float4 *>(p)[i] = pp;
-        reinterpret_cast<float4 *>(m)[i] = mm;
-        reinterpret_cast<float4 *>(v)[i] = vv;
-        if constexpr (WRITE_MODEL) {
-            const uint32_t lo = (uint32_t)f32_to_bf16_bits(pp.x) | ((uint32_t)f32_to_bf16_bits(pp.y) << 16);
-            const uint32_t hi = (uint32_t)f32_to_bf16_bits(pp.z) | ((uint32_t)f32_to_bf16_bits(pp.w) << 16);
-            reinterpret_cast<uint2 *>(model)[i] = uint2{lo, hi};
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * stride;
+            if (i >= n4) break;
+            upd(pp[u].x, mm[u].x, vv[u].x, gg[u][0]);
+            upd(pp[u].y, mm[u].y, vv[u].y, gg[u][1]);
+            upd(pp[u].z, mm[u].z, vv[u].z, gg[u][2]);
+            upd(pp[u].w, mm[u].w, vv[u].w, gg[u][3]);
+            reinterpret_cast<float4 *>(p)[i] = pp[u];
+            reinterpret_cast<float4 *>(m)[i] = mm[u];
+            reinterpret_cast<float4 *>(v)[i] = vv[u];
+            if constexpr (WRITE_MODEL) {
+                const uint32_t lo = (uint32_t)f32_to_bf16_bits(pp[u].x) | ((uint32_t)f32_to_bf16_bits(pp[u].y) << 16);
+                const uint32_t hi = (uint32_t)f32_to_bf16_bits(pp[u].z) | ((uint32_t)f32_to_bf16_bits(pp[u].w) << 16);
+                reinterpret_cast<uint2 *>(model)[i] = uint2{lo, hi};
+            }
         }
     }
     for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * kThreads + threadIdx.x; i < N; i += stride) {

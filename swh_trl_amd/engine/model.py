@@ -119,12 +119,15 @@ class _RMSNorm(torch.autograd.Function):
         return _norm_backward(x, w, rstd, dy, None, ctx.gw), None, None, None
 
 
+_NORM_RPB = int(os.environ.get("SWH_NORM_RPB", "32"))
+
+
 def _norm_backward(x, w, rstd, dy, dres, gw):
     """dx of the RMSNorm (+ dres, the residual branch's gradient, in the same
     pass) and the weight gradient folded into its bf16 view in one launch."""
     H = x.shape[-1]
     rows = x.numel() // H
-    rpb = 64
+    rpb = _NORM_RPB  # rows per workgroup: 8 per wave, >= 3 workgroups per CU at 24576 rows
     nb = (rows + rpb - 1) // rpb
     part = torch.empty(nb, H, device=x.device, dtype=torch.float32)
     dx = torch.empty_like(x)
