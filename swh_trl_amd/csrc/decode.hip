@@ -605,9 +605,20 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
     if (t < ntile) issue(t);  // the weight stream first
     // RMSNorm partials and norm weights (L2), then the X image by LDS-DMA
     const int nc = K / 64;
-    const bool use_ss = NM && ss_in && 64 * nc <= 4 * NT;
+    // folded norm: 8 lanes per row sum the row's chunk partials in registers and the
+    // row statistic is in LDS by the image barrier (no LDS pass, no extra barrier)
+    const bool reg_rstd = NM == 2 && ss_in && 64 * 8 <= NT && nc <= 64;
+    const bool use_ss = NM && ss_in && 64 * nc <= 4 * NT && !reg_rstd;
     float4 ssv[4];
+    float4 ss8[8];
     uint4 nwv[2];
+    if (reg_rstd) {
+        const int r = min(m0 + (tid >> 3), M - 1), sub = tid & 7;
+        const float4 *row = reinterpret_cast<const float4 *>(ss_in + (int64_t)r * (K / 16));
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (sub + 8 * j < nc) ss8[j] = row[sub + 8 * j];
+    }
     if constexpr (NM != 0) {
         if (use_ss) {
 #pragma unroll
@@ -652,9 +663,20 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
     }
     SWH_GEMM_TRACE(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // image (and this wave's first tile) landed
+    if (reg_rstd) {
+        const int r = tid >> 3, sub = tid & 7;
+        float v = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (sub + 8 * j < nc) v += ((ss8[j].x + ss8[j].y) + ss8[j].z) + ss8[j].w;
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        if (r < 64 && sub == 0) rstd_s[r] = rsqrtf(v / (float)K + eps);
+    }
     lds_barrier();
     SWH_GEMM_TRACE(2);
-    if constexpr (NM != 0) {
+    if (NM != 0 && !reg_rstd) {
         if (tid < 64) {
             float ssum = 0.f;
             if (use_ss) {

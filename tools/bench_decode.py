@@ -43,6 +43,8 @@ def sweep(eng, m):
         "gate_up": lambda: nn_ops.decode_gemm(eng.s, p["l0.gu_w"], norm_w=p["l0.ln_post"], eps=eps, silu=True,
                                               y=eng.act, ss_in=ss),
         "gate_up_nonorm": lambda: nn_ops.decode_gemm(eng.s, p["l0.gu_w"], silu=True, y=eng.act),
+        "gate_up_folded": lambda: nn_ops.decode_gemm(eng.s, eng._normed("l0.gu_w", "l0.ln_post")[0], silu=True,
+                                                     y=eng.act, ss_in=ss),
         "down": lambda: nn_ops.decode_gemm(eng.act, p["l0.down_w"], residual=eng.s, ss_out=ss),
         "lm": lambda: nn_ops.decode_gemm(eng.s, m.lm_weight(), norm_w=p["norm"], eps=eps, y=eng.logits_buf,
                                          ss_in=ss),
