@@ -301,6 +301,16 @@ int swh_embed_gather(const void *table, const int64_t *ids, int64_t B, int64_t H
 int swh_attn_decode(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
                     const float *rope_sin, const int32_t *prompt_len, const int32_t *state, int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax, float scale, void *out,
                     void *stream);
+/* swh_attn_decode plus cache warming for the next weight-bound launch: extra
+ * workgroup rows (about as many as the attention's Hkv x B) read the gate/up
+ * weights pf_w bf16 [2 pf_n, pf_k] (SiLU pair layout: gate rows, then up rows)
+ * tile by tile into the L2 of the XCD whose swh_decode_gemm(silu) workgroups
+ * consume that tile.  Results are those of swh_attn_decode; pf_w == NULL is
+ * swh_attn_decode.  pf_n % 8 == 0, pf_k % 8 == 0, pf_w 16-B aligned. */
+int swh_attn_decode_prefetch(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
+                             const float *rope_sin, const int32_t *prompt_len, const int32_t *state, int64_t B,
+                             int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax, float scale, void *out,
+                             const void *pf_w, int64_t pf_n, int64_t pf_k, void *stream);
 
 /* Weight-streaming decode GEMM Y[M,N] = X[M,K] W[N,K]^T (bf16, fp32 MFMA
  * accumulation, K % 64 == 0, 16-B aligned operands, ldy % 8 == 0) with the

@@ -973,11 +973,24 @@ __device__ __forceinline__ bf16x4s lds_read_tr16(const uint16_t *p) {
         (__attribute__((address_space(3))) bf16x4s *)(const_cast<uint16_t *>(p)));
 }
 
+// Cache warming riding on the attention launch: the attention grid covers only
+// Hkv x B workgroups (128 of 256 CUs at the bench shape), so extra workgroup rows
+// read the SAME layer's gate/up weight tiles (SiLU tile layout: tile t = gate rows
+// 8t.. and up rows N + 8t..) into the L2 of the XCD whose gate/up workgroups will
+// consume them (tile t runs on XCD t mod 8 there, workgroup id mod 8 here), by
+// LDS-DMA into a scratch tile (no registers, nothing consumed).
+struct AttnPrefetch {
+    const uint16_t *w;  // [2N, K] gate/up weights, or null
+    int n, k;           // N (SiLU pairs), K
+    int rows;           // attention rows (B): grid rows past it prefetch
+};
+
 template <int D, int GQ>
 __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
     const uint16_t *__restrict__ qkv, uint16_t *__restrict__ kc, uint16_t *__restrict__ vc,
     const float *__restrict__ rcos, const float *__restrict__ rsin, const int32_t *__restrict__ plen,
-    const int32_t *__restrict__ state, int Hq, int Hkv, int Tmax, float scale, uint16_t *__restrict__ out) {
+    const int32_t *__restrict__ state, int Hq, int Hkv, int Tmax, float scale, uint16_t *__restrict__ out,
+    AttnPrefetch pf) {
     static_assert(GQ <= 16, "a kv head serves at most 16 query heads");
     constexpr int DC = D / 32;                 // 32-dim chunks: k-steps of K Q^T
     constexpr int DB = D / 16;                 // 16-dim blocks of O^T
@@ -995,6 +1008,24 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
     const int64_t b = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int g = lane >> 4, c16 = lane & 15;
+    if ((int)blockIdx.y >= pf.rows) {  // a prefetch workgroup
+        const int lin = blockIdx.y * gridDim.x + blockIdx.x, p = lin - pf.rows * gridDim.x;
+        const int npf = (gridDim.y - pf.rows) * gridDim.x / 8 * 8;  // whole groups of 8: every XCD covered
+        if (p >= npf) return;
+        const int xcd = lin & 7, j = p >> 3, per = npf >> 3;
+        const int ppr = pf.k / 8, ntile = pf.n / 8;
+        unsigned char *scratch = reinterpret_cast<unsigned char *>(vt_s[wid]);
+        for (int t = xcd + 8 * j; t < ntile; t += 8 * per) {
+            for (int pc = tid; pc < 16 * ppr; pc += kAttnThreads) {
+                const int r = pc / ppr, c = pc - r * ppr;
+                const int64_t row = (r < 8) ? (int64_t)t * 8 + r : (int64_t)pf.n + (int64_t)t * 8 + r - 8;
+                __builtin_amdgcn_global_load_lds(pf.w + row * pf.k + c * 8,
+                                                 (__attribute__((address_space(3))) void *)scratch, 16, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        return;
+    }
     // state[0] = index of the token sampled this step; the input token is state[0] - 1
     const int step = state[0] - 1, P = state[1];
     const int pl = plen[b];
@@ -1171,25 +1202,34 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
 
 template <int D, int GQ>
 int launch_attn(const uint16_t *q, uint16_t *kc, uint16_t *vc, const float *rc, const float *rs, const int32_t *pl,
-                const int32_t *st, int64_t B, int Hq, int Hkv, int Tmax, float scale, uint16_t *o, hipStream_t s) {
-    attn_decode_kernel<D, GQ><<<dim3((unsigned)Hkv, (unsigned)B), kAttnThreads, 0, s>>>(q, kc, vc, rc, rs, pl, st, Hq,
-                                                                                      Hkv, Tmax, scale, o);
+                const int32_t *st, int64_t B, int Hq, int Hkv, int Tmax, float scale, uint16_t *o, hipStream_t s,
+                const AttnPrefetch &pf) {
+    // prefetch rows: about as many workgroups as the attention itself has, in groups of 8
+    int64_t extra = 0;
+    if (pf.w) {
+        static const int mult = getenv("SWH_PF_MULT") ? atoi(getenv("SWH_PF_MULT")) : 2;  // 1-3 measured
+        const int64_t want = (mult * B * Hkv + 7) / 8 * 8;
+        extra = (want + Hkv - 1) / Hkv;
+        if (B + extra > 65535) extra = 0;
+    }
+    attn_decode_kernel<D, GQ><<<dim3((unsigned)Hkv, (unsigned)(B + extra)), kAttnThreads, 0, s>>>(
+        q, kc, vc, rc, rs, pl, st, Hq, Hkv, Tmax, scale, o, pf);
     return launch_status();
 }
 
 template <int D>
 int attn_dispatch_gq(int gq, const uint16_t *q, uint16_t *kc, uint16_t *vc, const float *rc, const float *rs,
                      const int32_t *pl, const int32_t *st, int64_t B, int Hq, int Hkv, int Tmax, float scale,
-                     uint16_t *o, hipStream_t s) {
+                     uint16_t *o, hipStream_t s, const AttnPrefetch &pf) {
     switch (gq) {
-    case 1: return launch_attn<D, 1>(q, kc, vc, rc, rs, pl, st, B, Hq, Hkv, Tmax, scale, o, s);
-    case 2: return launch_attn<D, 2>(q, kc, vc, rc, rs, pl, st, B, Hq, Hkv, Tmax, scale, o, s);
-    case 3: return launch_attn<D, 3>(q, kc, vc, rc, rs, pl, st, B, Hq, Hkv, Tmax, scale, o, s);
-    case 4: return launch_attn<D, 4>(q, kc, vc, rc, rs, pl, st, B, Hq, Hkv, Tmax, scale, o, s);
-    case 5: return launch_attn<D, 5>(q, kc, vc, rc, rs, pl, st, B, Hq, Hkv, Tmax, scale, o, s);
-    case 6: return launch_attn<D, 6>(q, kc, vc, rc, rs, pl, st, B, Hq, Hkv, Tmax, scale, o, s);
-    case 7: return launch_attn<D, 7>(q, kc, vc, rc, rs, pl, st, B, Hq, Hkv, Tmax, scale, o, s);
-    case 8: return launch_attn<D, 8>(q, kc, vc, rc, rs, pl, st, B, Hq, Hkv, Tmax, scale, o, s);
+    case 1: return launch_attn<D, 1>(q, kc, vc, rc, rs, pl, st, B, Hq, Hkv, Tmax, scale, o, s, pf);
+    case 2: return launch_attn<D, 2>(q, kc, vc, rc, rs, pl, st, B, Hq, Hkv, Tmax, scale, o, s, pf);
+    case 3: return launch_attn<D, 3>(q, kc, vc, rc, rs, pl, st, B, Hq, Hkv, Tmax, scale, o, s, pf);
+    case 4: return launch_attn<D, 4>(q, kc, vc, rc, rs, pl, st, B, Hq, Hkv, Tmax, scale, o, s, pf);
+    case 5: return launch_attn<D, 5>(q, kc, vc, rc, rs, pl, st, B, Hq, Hkv, Tmax, scale, o, s, pf);
+    case 6: return launch_attn<D, 6>(q, kc, vc, rc, rs, pl, st, B, Hq, Hkv, Tmax, scale, o, s, pf);
+    case 7: return launch_attn<D, 7>(q, kc, vc, rc, rs, pl, st, B, Hq, Hkv, Tmax, scale, o, s, pf);
+    case 8: return launch_attn<D, 8>(q, kc, vc, rc, rs, pl, st, B, Hq, Hkv, Tmax, scale, o, s, pf);
     default: return SWH_E_ARG;
     }
 }
@@ -1383,12 +1423,15 @@ int launch_tiles(int nm, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X
 
 using namespace swh;
 
-extern "C" int swh_attn_decode(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
-                               const float *rope_sin, const int32_t *prompt_len, const int32_t *state, int64_t B,
-                               int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax, float scale, void *out,
-                               void *stream) {
+extern "C" int swh_attn_decode_prefetch(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
+                                        const float *rope_sin, const int32_t *prompt_len, const int32_t *state,
+                                        int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax, float scale,
+                                        void *out, const void *pf_w, int64_t pf_n, int64_t pf_k, void *stream) {
     if (!qkv || !k_cache || !v_cache || !rope_cos || !rope_sin || !prompt_len || !state || !out || B < 0 || Hkv <= 0 ||
         Hq % Hkv || Tmax <= 0 || B > 65535)
+        return SWH_E_ARG;
+    if (pf_w && (pf_n <= 0 || pf_n % 8 || pf_k <= 0 || pf_k % 8 || pf_n >= (1 << 28) || pf_k >= (1 << 20) ||
+                 (reinterpret_cast<uintptr_t>(pf_w) & 15)))
         return SWH_E_ARG;
     if (B == 0) return SWH_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1396,9 +1439,18 @@ extern "C" int swh_attn_decode(const void *qkv, void *k_cache, void *v_cache, co
     auto *kc = static_cast<uint16_t *>(k_cache), *vc = static_cast<uint16_t *>(v_cache);
     auto *o = static_cast<uint16_t *>(out);
     const int gq = Hq / Hkv;
-    if (D == 64) return attn_dispatch_gq<64>(gq, q, kc, vc, rope_cos, rope_sin, prompt_len, state, B, Hq, Hkv, Tmax, scale, o, s);
-    if (D == 128) return attn_dispatch_gq<128>(gq, q, kc, vc, rope_cos, rope_sin, prompt_len, state, B, Hq, Hkv, Tmax, scale, o, s);
+    const AttnPrefetch pf{static_cast<const uint16_t *>(pf_w), (int)pf_n, (int)pf_k, (int)B};
+    if (D == 64) return attn_dispatch_gq<64>(gq, q, kc, vc, rope_cos, rope_sin, prompt_len, state, B, Hq, Hkv, Tmax, scale, o, s, pf);
+    if (D == 128) return attn_dispatch_gq<128>(gq, q, kc, vc, rope_cos, rope_sin, prompt_len, state, B, Hq, Hkv, Tmax, scale, o, s, pf);
     return SWH_E_ARG;
+}
+
+extern "C" int swh_attn_decode(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
+                               const float *rope_sin, const int32_t *prompt_len, const int32_t *state, int64_t B,
+                               int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax, float scale, void *out,
+                               void *stream) {
+    return swh_attn_decode_prefetch(qkv, k_cache, v_cache, rope_cos, rope_sin, prompt_len, state, B, Hq, Hkv, D, Tmax,
+                                    scale, out, nullptr, 0, 0, stream);
 }
 
 extern "C" int64_t swh_decode_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K) {

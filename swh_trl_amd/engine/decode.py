@@ -89,6 +89,9 @@ class DecodeEngine:
         self._graph_params = None
         self.params = ops.make_sample_params()
         self.want_logp = False
+        # the attention launch warms the gate/up weights into the consuming XCDs' L2:
+        # gate/up gains what the longer attention launch loses, off
+        self.prefetch = os.environ.get("SWH_DECODE_PREFETCH", "0") != "0"
 
     # ------------------------------------------------------------------ one decode step (capturable)
     def _step(self):
@@ -162,11 +165,11 @@ class DecodeEngine:
         for i in range(c.num_hidden_layers):
             w, nw = self._normed(f"l{i}.qkv_w", f"l{i}.ln_in")
             nn_ops.decode_gemm(self.s, w, norm_w=nw, eps=eps, bias=p.get(f"l{i}.qkv_b"), y=self.qkv, ss_in=ss)
+            w, nw = self._normed(f"l{i}.gu_w", f"l{i}.ln_post")
             nn_ops.attn_decode(self.qkv, self.kv[i, 0], self.kv[i, 1], self.cos, self.sin, self.plen, self.state,
                                c.num_attention_heads, c.num_key_value_heads, c.head_dim, c.head_dim ** -0.5,
-                               out=self.att)
+                               out=self.att, prefetch_gate_up=w if self.prefetch else None)
             nn_ops.decode_gemm(self.att, p[f"l{i}.o_w"], residual=self.s, ss_out=ss)
-            w, nw = self._normed(f"l{i}.gu_w", f"l{i}.ln_post")
             nn_ops.decode_gemm(self.s, w, norm_w=nw, eps=eps, silu=True, y=self.act, ss_in=ss)
             nn_ops.decode_gemm(self.act, p[f"l{i}.down_w"], residual=self.s, ss_out=ss)
         w, nw = self._normed("lm", "norm")
@@ -283,7 +286,9 @@ class DecodeEngine:
             "attn_decode": (lambda i: nn_ops.attn_decode(self.qkv, self.kv[i, 0], self.kv[i, 1], self.cos, self.sin,
                                                          self.plen, self.state, c.num_attention_heads,
                                                          c.num_key_value_heads, c.head_dim, c.head_dim ** -0.5,
-                                                         out=self.att),
+                                                         out=self.att,
+                                                         prefetch_gate_up=self._normed(f"l{i}.gu_w", "")[0]
+                                                         if self.prefetch else None),
                             att_bytes, L),
             "decode_gemm.o": (lambda i: nn_ops.decode_gemm(self.att, p[f"l{i}.o_w"], residual=self.s, ss_out=ss),
                               gemm_bytes(H, c.q_dim), L),

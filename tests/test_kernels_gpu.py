@@ -635,6 +635,26 @@ def test_attn_decode(ops, dev, D, Hq, Hkv, Tmax, step):
     assert torch.isnan(out2.float()).all() and torch.equal(before, kcd)
 
 
+@pytest.mark.parametrize("B,Hkv,I", [(64, 2, 4864), (5, 8, 1024), (3, 1, 24)])
+def test_attn_decode_prefetch_is_result_neutral(ops, dev, B, Hkv, I):
+    """swh_attn_decode_prefetch (extra workgroup rows warming the gate/up weights)
+    writes exactly what swh_attn_decode writes, output and cache, at any grid shape."""
+    from swh_trl_amd import nn_ops
+    g = _gen(22)
+    D, Hq, Tmax, P, step = 64, 4 * Hkv, 96, 40, 17
+    plen = torch.randint(1, P + 1, (B,), generator=g).to(torch.int32).to(dev)
+    kc = torch.randn(B, Hkv, Tmax, D, generator=g).to(torch.bfloat16).to(dev)
+    vc = torch.randn(B, Hkv, Tmax, D, generator=g).to(torch.bfloat16).to(dev)
+    qkv = torch.randn(B, (Hq + 2 * Hkv) * D, generator=g).to(torch.bfloat16).to(dev)
+    gu = torch.randn(2 * I, 896, generator=g).to(torch.bfloat16).to(dev)
+    cos, sin = _rope_tables(D, 2048, 1e6, dev)
+    state = torch.tensor([step + 1, P], dtype=torch.int32, device=dev)
+    k1, v1, k2, v2 = kc.clone(), vc.clone(), kc.clone(), vc.clone()
+    a = nn_ops.attn_decode(qkv, k1, v1, cos, sin, plen, state, Hq, Hkv, D, D ** -0.5)
+    b = nn_ops.attn_decode(qkv, k2, v2, cos, sin, plen, state, Hq, Hkv, D, D ** -0.5, prefetch_gate_up=gu)
+    assert torch.equal(a, b) and torch.equal(k1, k2) and torch.equal(v1, v2)
+
+
 # --------------------------------------------------------------------------- fused decode GEMM
 def _ref_norm(x, w, eps):
     xf = x.float()
