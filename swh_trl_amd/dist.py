@@ -71,8 +71,9 @@ class OverlappedAllReduce:
 
     With one process this is a no-op; on gloo (CPU tests) it sums and divides."""
 
-    def __init__(self, flat: torch.Tensor):
+    def __init__(self, flat: torch.Tensor, wait_streams=()):
         self.flat = flat
+        self.wait_streams = list(wait_streams)  # producers of gradients beside the compute stream
         self.active = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
         self.world = dist.get_world_size() if self.active else 1
         self.nccl = self.active and dist.get_backend() == "nccl"
@@ -88,6 +89,8 @@ class OverlappedAllReduce:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.flat.device))
             self.stream.wait_event(ev)
+            for st in self.wait_streams:
+                self.stream.wait_stream(st)
             with torch.cuda.stream(self.stream):
                 w = dist.all_reduce(chunk, op=dist.ReduceOp.AVG, async_op=True)
         else:

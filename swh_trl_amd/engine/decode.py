@@ -17,6 +17,8 @@ post-RoPE keys/values into the cache.
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 import os
 from typing import Optional
 
@@ -26,6 +28,21 @@ from .. import nn_ops, ops
 from ..profiling import trace as _trace
 from .._lib import call
 from .model import CausalLM
+
+
+@contextlib.contextmanager
+def _capture(graph: "torch.cuda.CUDAGraph"):
+    """torch.cuda.graph with the Python GC held off for the capture: the graph
+    context collects once on entry; a collection INSIDE the capture could destroy
+    an unreachable engine's graphs or events mid-capture, which aborts."""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        with torch.cuda.graph(graph):
+            yield
+    finally:
+        if was:
+            gc.enable()
 
 
 class DecodeEngine:
@@ -229,13 +246,13 @@ class DecodeEngine:
             self._step()
         torch.cuda.current_stream().wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with _capture(self.graph):
             self._step()
         # K steps per replay: one graph launch (~9 us of replay boundary) per K tokens
         self.graph_k = None
         if self.steps_per_graph > 1:
             self.graph_k = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph_k):
+            with _capture(self.graph_k):
                 for _ in range(self.steps_per_graph):
                     self._step()
         self._graph_params = key
@@ -321,7 +338,7 @@ class DecodeEngine:
             fn(0)
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with _capture(g):
                 for r in range(n):
                     fn(r % cycle)
             g.replay()
@@ -420,7 +437,7 @@ class DecodeEngine:
                         self._prefill_body(st["ids"], st["mask"], st["inv"], padded)
                     torch.cuda.current_stream().wait_stream(side)
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g):
+                    with _capture(g):
                         self._prefill_body(st["ids"], st["mask"], st["inv"], padded)
                     gp = self._prefill_graphs[key] = (g, st)
                 g, st = gp

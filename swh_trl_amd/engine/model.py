@@ -30,9 +30,72 @@ from .config import DecoderConfig
 _ALIGN = 64  # elements; keeps every view 128-byte aligned
 
 
+_DW_STREAMS: dict = {}
+
+
+def _dw_stream(dev: torch.device):
+    """Side stream for the weight-gradient launches (SWH_DW_STREAM=0: inline).
+    The backward's critical path is dX -> next layer; dW of a layer is a leaf, so
+    it runs beside the chain (each launch waits for the compute stream's
+    progress so far) and the compute stream joins it once, after backward
+    (`dw_sync`).  Accumulation order into the gradient views is unchanged."""
+    if dev.type != "cuda" or os.environ.get("SWH_DW_STREAM", "1") == "0":
+        return None
+    st = _DW_STREAMS.get(dev.index)
+    if st is None:
+        st = _DW_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+    return st
+
+
+def dw_streams(dev: torch.device) -> list:
+    """The weight-gradient side streams in use on `dev` (for collectives that
+    must wait for the final gradients)."""
+    st = _DW_STREAMS.get(dev.index) if dev.type == "cuda" else None
+    return [] if st is None else [st]
+
+
+_DW_KEEP: list = []  # tensors the side stream reads, alive until the compute stream has joined it
+
+
+def dw_sync(dev: torch.device):
+    """The current stream waits for every weight-gradient launch issued so far
+    (called at the end of every backward by the embedding node, which runs last)."""
+    for st in dw_streams(dev):
+        torch.cuda.current_stream(dev).wait_stream(st)
+    _DW_KEEP.clear()
+
+
+class _OnStream:
+    """`with _OnStream(st):` — run on side stream `st` after the current stream's
+    work so far (no-op for st None); `keep(t...)` marks tensors the side stream reads."""
+
+    def __init__(self, st):
+        self.st = st
+        self.ctx = None
+
+    def __enter__(self):
+        if self.st is not None:
+            self.st.wait_stream(torch.cuda.current_stream(self.st.device))
+            self.ctx = torch.cuda.stream(self.st)
+            self.ctx.__enter__()
+        return self
+
+    def keep(self, *ts):
+        # references instead of record_stream: freeing a record_stream'd block
+        # records an event on the side stream, which a later graph capture forbids
+        if self.st is not None:
+            _DW_KEEP.extend(t for t in ts if t is not None)
+
+    def __exit__(self, *exc):
+        if self.ctx is not None:
+            self.ctx.__exit__(*exc)
+        return False
+
+
 class _Linear(torch.autograd.Function):
     """y = x W^T (+ b); backward returns dx and ACCUMULATES dW (and db) into the
-    flat-gradient views (hipBLASLt addmm with beta = 1)."""
+    flat-gradient views (hipBLASLt addmm with beta = 1), on the weight-gradient
+    side stream."""
 
     @staticmethod
     def forward(ctx, x, w, b, gw, gb):
@@ -45,22 +108,24 @@ class _Linear(torch.autograd.Function):
         x, w = ctx.saved_tensors
         dx = dy @ w if ctx.needs_input_grad[0] else None
         if ctx.gw is not None:
-            dy2 = dy.reshape(-1, dy.shape[-1])
-            x2 = x.reshape(-1, x.shape[-1])
-            S = _dw_split(dy2.shape[0], dy2.shape[1] * x2.shape[1])
-            if S > 1:
-                # few output tiles over a long token dimension: split the tokens into S
-                # batched GEMMs (S x the workgroups), sum the partials into the gradient
-                Kc = dy2.shape[0] // S
-                parts = torch.bmm(dy2[:S * Kc].view(S, Kc, -1).transpose(1, 2), x2[:S * Kc].view(S, Kc, -1))
-                acc = parts.sum(0, dtype=torch.float32)
-                if S * Kc < dy2.shape[0]:
-                    acc.addmm_(dy2[S * Kc:].t().float(), x2[S * Kc:].float())
-                ctx.gw.add_(acc)
-            else:
-                ctx.gw.addmm_(dy2.t(), x2)
-            if ctx.gb is not None:
-                ctx.gb.add_(dy2.sum(0, dtype=torch.float32).to(ctx.gb.dtype))
+            with _OnStream(_dw_stream(dy.device)) as side:
+                side.keep(dy, x)
+                dy2 = dy.reshape(-1, dy.shape[-1])
+                x2 = x.reshape(-1, x.shape[-1])
+                S = _dw_split(dy2.shape[0], dy2.shape[1] * x2.shape[1])
+                if S > 1:
+                    # few output tiles over a long token dimension: split the tokens into S
+                    # batched GEMMs (S x the workgroups), sum the partials into the gradient
+                    Kc = dy2.shape[0] // S
+                    parts = torch.bmm(dy2[:S * Kc].view(S, Kc, -1).transpose(1, 2), x2[:S * Kc].view(S, Kc, -1))
+                    acc = parts.sum(0, dtype=torch.float32)
+                    if S * Kc < dy2.shape[0]:
+                        acc.addmm_(dy2[S * Kc:].t().float(), x2[S * Kc:].float())
+                    ctx.gw.add_(acc)
+                else:
+                    ctx.gw.addmm_(dy2.t(), x2)
+                if ctx.gb is not None:
+                    ctx.gb.add_(dy2.sum(0, dtype=torch.float32).to(ctx.gb.dtype))
         return dx, None, None, None, None
 
 
@@ -96,6 +161,7 @@ class _Embedding(torch.autograd.Function):
         (ids,) = ctx.saved_tensors
         if ctx.gtable is not None:
             ctx.gtable.index_add_(0, ids.reshape(-1), dy.reshape(-1, dy.shape[-1]))
+        dw_sync(dy.device)  # the first op of the forward: every weight gradient is issued
         return None, None, None, None
 
 
@@ -136,7 +202,9 @@ def _norm_backward(x, w, rstd, dy, dres, gw):
     call("swh_rmsnorm_bwd", x.data_ptr(), w.data_ptr(), rstd.data_ptr(), dyc.data_ptr(), rows, H, dx.data_ptr(),
          part.data_ptr(), rpb, None if dr is None else dr.data_ptr(), _stream())
     if gw is not None:
-        call("swh_rmsnorm_dw_accum", part.data_ptr(), nb, H, gw.data_ptr(), _stream())
+        with _OnStream(_dw_stream(x.device)) as side:
+            side.keep(part)
+            call("swh_rmsnorm_dw_accum", part.data_ptr(), nb, H, gw.data_ptr(), _stream())
     return dx
 
 

@@ -31,7 +31,7 @@ from .. import gemm_tuning
 from .. import ops
 from ..engine.config import DecoderConfig, PRESETS, from_hf_config
 from ..engine.decode import DecodeEngine
-from ..engine.model import CausalLM
+from ..engine.model import CausalLM, dw_streams, dw_sync
 from ..optim import FlatAdamW
 from .grpo_config import GRPOConfig
 from .utils import generation_batch_indices, left_pad, linear_lr, pad_left_cat, split_tensor_dict, \
@@ -351,6 +351,7 @@ class GRPOTrainer:
             max_completion_length=self.max_completion_length)
         _trace("loss")
         loss.backward()
+        dw_sync(self.device)  # the weight-gradient side stream joins the compute stream
         _trace("backward")
         return {"loss": loss.detach(), "metrics": metrics}
 
@@ -398,7 +399,7 @@ class GRPOTrainer:
                      for m in micro)
         # DP: each layer's gradient all-reduce starts as soon as the (last) backward
         # pass has finished that layer, overlapped with the rest of the backward
-        ar = swh_dist.OverlappedAllReduce(self.model.grad) if self.world > 1 else None
+        ar = swh_dist.OverlappedAllReduce(self.model.grad, dw_streams(self.device)) if self.world > 1 else None
         groups = [micro] if (a.fuse_micro_batches and tokens <= a.fuse_token_budget) else [[m] for m in micro]
         for gi, grp in enumerate(groups):
             if ar is not None and gi == len(groups) - 1:

@@ -33,7 +33,7 @@ from .. import dist as swh_dist
 from .. import gemm_tuning
 from .. import ops
 from ..engine.decode import DecodeEngine
-from ..engine.model import CausalLM
+from ..engine.model import CausalLM, dw_sync
 from ..optim import FlatAdamW
 from .grpo_trainer import TrainerState, _trace, load_model
 from .ppo_config import PPOConfig
@@ -326,6 +326,7 @@ class PPOTrainer:
         dnl = torch.masked_fill(dnl, pm, 0.0) / ga
         dvp = torch.masked_fill(dvp, pm1, 0.0) / ga
         torch.autograd.backward([new_logprobs, vpred], [dnl.to(new_logprobs.dtype), dvp.to(vpred.dtype)])
+        dw_sync(self.device)
         return out
 
     def _optimizer_step(self, lr: float):
