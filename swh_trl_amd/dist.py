@@ -22,8 +22,8 @@ def init_from_env(backend: str | None = None):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not dist.is_initialized():
-        if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend is None:  # SWH_DIST_BACKEND: tests run gloo ranks that share one GPU
+            backend = os.environ.get("SWH_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
             torch.cuda.set_device(local)
@@ -94,6 +94,9 @@ class OverlappedAllReduce:
             with torch.cuda.stream(self.stream):
                 w = dist.all_reduce(chunk, op=dist.ReduceOp.AVG, async_op=True)
         else:
+            if chunk.is_cuda:  # gloo on device buffers orders after the current stream only
+                for st in self.wait_streams:
+                    torch.cuda.current_stream(chunk.device).wait_stream(st)
             w = dist.all_reduce(chunk, op=dist.ReduceOp.AVG if self.nccl else dist.ReduceOp.SUM, async_op=True)
         self.works.append((w, chunk))
         self.done.append((start, end))

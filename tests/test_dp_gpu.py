@@ -1,0 +1,69 @@
+"""Data-parallel GRPO step on the GPU with two ranks (-m gpu).
+
+Both ranks share cuda:0 and talk over gloo (SWH_DIST_BACKEND=gloo): the
+collective differs from the RCCL runs of bench.py, but the trainer's DP data
+path is the one under test — per-layer gradient ranges released from the
+backward hooks (OverlappedAllReduce) while the weight-gradient side stream is
+still producing, the remainder in finish(), then AdamW on each replica.  The
+replicas must stay bit-identical, and differ from a single-rank run on the
+same rank-0 prompts (the other rank's gradients were averaged in).
+"""
+import hashlib
+import multiprocessing as mp
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _worker(rank, world, port, q, steps):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), SWH_DIST_BACKEND="gloo")
+    try:
+        from swh_trl_amd.engine import tiny_qwen2
+        from swh_trl_amd.trainer import GRPOConfig, GRPOTrainer
+        cfg = tiny_qwen2(512, 4)
+        ds = [{"prompt": None, "prompt_ids": list(range(3 + i, 11 + i))} for i in range(32)]
+
+        def rew(prompts=None, completions=None, completion_ids=None, **kw):
+            return [float(len(set(c)) % 5) for c in completion_ids]
+
+        args = GRPOConfig(per_device_train_batch_size=8, gradient_accumulation_steps=2, num_generations=4,
+                          max_prompt_length=8, max_completion_length=16, max_steps=steps, learning_rate=1e-3,
+                          generation_kwargs={"eos_token_id": 1, "pad_token_id": 0, "min_new_tokens": 16},
+                          logging_steps=1, seed=7)
+        tr = GRPOTrainer(model=cfg, reward_funcs=rew, args=args, train_dataset=ds)
+        tr.train()
+        torch.cuda.synchronize()
+        flat = tr.model.flat.float().cpu().numpy()
+        q.put((rank, (hashlib.sha256(flat.tobytes()).hexdigest(), float(flat.astype("float64").sum()))))
+    except Exception as e:  # surface the failure to the parent
+        q.put((rank, repr(e)))
+    finally:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _run(world, steps):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31500 + (os.getpid() % 1000) + world
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, steps)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    for r, v in got.items():
+        assert isinstance(v, tuple), (r, v)
+    return got
+
+
+def test_dp_two_ranks_keep_replicas_identical():
+    got = _run(2, 2)  # (sha256 of the fp32 weights, their sum) per rank
+    assert got[0][0] == got[1][0]
+    single = _run(1, 2)
+    assert single[0][0] != got[0][0]
