@@ -127,6 +127,10 @@ __host__ __device__ inline GemmLds gemm_lds(int cb, int mr, int nw, int krmax, i
 #ifndef SWH_ROUND_PREFETCH
 #define SWH_ROUND_PREFETCH 0  // all A reads of a full round before its MFMAs (A/B: tools/build_variant.py)
 #endif
+#ifndef SWH_GEMM_RING
+#define SWH_GEMM_RING 0  // decode_gemm k-loop: refill each k-step's weight registers right after its MFMAs (A/B)
+#endif
+static_assert(!(SWH_GEMM_RING && SWH_ROUND_PREFETCH), "the ring refill lives in the per-k-step loop");
 #ifndef SWH_LM_RING
 #define SWH_LM_RING 1  // lm-head tile loop: refill each weight register right after its MFMA (A/B)
 #endif
@@ -358,7 +362,7 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
             for (int j = 0; j < CB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         const unsigned char *xrow = xs + rl * RS + kq * 2;
         for (int ks = ksw0; ks < ksw1; ks += kU) {
-            if (ks != ksw0) issue(ks);
+            if (!SWH_GEMM_RING && ks != ksw0) issue(ks);
             const unsigned char *xk = xrow + (ks - kb0) * 64;
             if (SWH_ROUND_PREFETCH && ks + kU <= ksw1) {  // a full round: every A fragment read in flight first
                 uint4 a[kU][MS];
@@ -387,6 +391,13 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
                         for (int j = 0; j < CB; ++j)
                             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[i]), as_bf16x8(bv[u][j]),
                                                                                 acc[i][j], 0, 0, 0);
+                    if (SWH_GEMM_RING && ks + kU + u < ksw1) {
+                        // ring refill: k-step ks + u's registers take k-step ks + kU + u as soon as
+                        // its MFMAs have read them, so kU k-steps stay in flight per wave
+#pragma unroll
+                        for (int j = 0; j < CB; ++j)
+                            bv[u][j] = *reinterpret_cast<const uint4 *>(wrow[j] + (ks + kU + u) * 32);
+                    }
                 }
             }
         }
