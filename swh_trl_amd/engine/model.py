@@ -159,9 +159,12 @@ class _Embedding(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         (ids,) = ctx.saved_tensors
+        # the first op of the forward: every weight gradient is issued by now.  Join
+        # the side stream BEFORE the add: with tied embeddings the lm-head dW (side
+        # stream) accumulates into this same view
+        dw_sync(dy.device)
         if ctx.gtable is not None:
             ctx.gtable.index_add_(0, ids.reshape(-1), dy.reshape(-1, dy.shape[-1]))
-        dw_sync(dy.device)  # the first op of the forward: every weight gradient is issued
         return None, None, None, None
 
 
@@ -286,8 +289,10 @@ class _LMHeadLogp(torch.autograd.Function):
             ops.logp_backward(lg, idx[r0:r1], lse[r0:r1], g[r0:r1], ctx.temperature, out=lg)  # in place
             if dh is not None:
                 torch.mm(lg, w, out=dh[r0:r1])
-            if ctx.gw is not None:
-                ctx.gw.addmm_(lg.t(), h2[r0:r1])
+            if ctx.gw is not None:  # beside the next chunk's (HBM-bound) logp backward
+                with _OnStream(_dw_stream(lg.device)) as side:
+                    side.keep(lg, h2)
+                    ctx.gw.addmm_(lg.t(), h2[r0:r1])
         ctx.chunks = None
         return (dh.view(ctx.hshape) if dh is not None else None), None, None, None, None, None, None
 
