@@ -259,15 +259,21 @@ class _LMHeadLogp(torch.autograd.Function):
         ent = torch.empty(R, device=h.device, dtype=torch.float32) if compute_entropy else None
         lse = torch.empty(R, device=h.device, dtype=torch.float32)
         chunks = []
+        # chunk k's (HBM-bound) log-prob pass runs on the side stream beside chunk
+        # k+1's GEMM; the outputs are joined once after the loop
+        side = _dw_stream(h.device) if R > chunk_rows else None
         for r0 in range(0, R, chunk_rows):
             r1 = min(R, r0 + chunk_rows)
             lg = h2[r0:r1] @ w.t()
-            lp_c, en_c, ls_c = ops.logp_entropy(lg, idx[r0:r1], temperature, compute_entropy)
-            logp[r0:r1] = lp_c
-            lse[r0:r1] = ls_c
-            if compute_entropy:
-                ent[r0:r1] = en_c
+            with _OnStream(side):
+                lp_c, en_c, ls_c = ops.logp_entropy(lg, idx[r0:r1], temperature, compute_entropy)
+                logp[r0:r1] = lp_c
+                lse[r0:r1] = ls_c
+                if compute_entropy:
+                    ent[r0:r1] = en_c
             chunks.append(lg)
+        if side is not None:
+            torch.cuda.current_stream(h.device).wait_stream(side)
         ctx.chunks, ctx.gw, ctx.temperature, ctx.chunk_rows = chunks, gw, temperature, chunk_rows
         ctx.hshape = h.shape
         ctx.save_for_backward(h2, w, idx, lse)
