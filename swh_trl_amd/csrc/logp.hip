@@ -174,10 +174,10 @@ extern "C" int swh_logp_entropy_fwd(const void *logits, int dtype, int64_t rows_
                                     int64_t stride_outer, int64_t stride_inner, int64_t V, const int64_t *ids,
                                     float temperature, int flags, float *logp, float *entropy, float *lse,
                                     void *stream) {
-    if (!logits || !rows_ok(rows_outer, rows_inner, V) || !(temperature > 0.f)) return SWH_E_ARG;
-    if (logp && !ids) return SWH_E_ARG;
+    if (!rows_ok(rows_outer, rows_inner, V) || !(temperature > 0.f)) return SWH_E_ARG;
     const int64_t R = rows_outer * rows_inner;
-    if (R == 0) return SWH_OK;
+    if (R == 0) return SWH_OK;  // empty batch: nothing to read (buffers may be null)
+    if (!logits || (logp && !ids)) return SWH_E_ARG;
     RowAddr ra{rows_outer, rows_inner, stride_outer, stride_inner};
     hipStream_t s = static_cast<hipStream_t>(stream);
     dim3 grid((unsigned)R), block(kThreads);
@@ -204,11 +204,10 @@ extern "C" int swh_logp_bwd(const void *logits, int dtype, int64_t rows_outer, i
                             int64_t stride_outer, int64_t stride_inner, int64_t V, const int64_t *ids,
                             float temperature, int flags, const float *lse, const float *dlogp, void *dlogits,
                             int64_t dstride_outer, int64_t dstride_inner, void *stream) {
-    if (!logits || !ids || !lse || !dlogp || !dlogits || !rows_ok(rows_outer, rows_inner, V) ||
-        !(temperature > 0.f))
-        return SWH_E_ARG;
+    if (!rows_ok(rows_outer, rows_inner, V) || !(temperature > 0.f)) return SWH_E_ARG;
     const int64_t R = rows_outer * rows_inner;
-    if (R == 0) return SWH_OK;
+    if (R == 0) return SWH_OK;  // empty batch (buffers may be null)
+    if (!logits || !ids || !lse || !dlogp || !dlogits) return SWH_E_ARG;
     RowAddr ra{rows_outer, rows_inner, stride_outer, stride_inner};
     RowAddr rd{rows_outer, rows_inner, dstride_outer, dstride_inner};
     hipStream_t s = static_cast<hipStream_t>(stream);

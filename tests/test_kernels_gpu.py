@@ -524,6 +524,33 @@ def test_fold_norm_ragged_jobs(ops, dev):
         assert torch.equal(o, w * nw)
 
 
+def test_degenerate_inputs(ops, dev):
+    """Edge cases the reference defines: zero rows (empty batches from a
+    completion-less rank), an all-zero mask (core.py:59 raises), groups with
+    identical rewards (std 0: advantage 0 and is_std_zero, grpo_trainer.py:1921-1930),
+    and an all-masked completion in the loss (bnpo clamps the token count at 1)."""
+    V = 1000
+    lg = torch.empty(0, 7, V, device=dev, dtype=torch.bfloat16)
+    ix = torch.empty(0, 7, device=dev, dtype=torch.int64)
+    assert ops.selective_log_softmax(lg, ix).shape == (0, 7)
+    assert ops.entropy_from_logits(torch.empty(0, V, device=dev)).shape == (0,)
+    with pytest.raises(ValueError):
+        ops.masked_whiten_checked(torch.randn(4, 3, device=dev), torch.zeros(4, 3, device=dev))
+    # constant rewards within each group of 4: mean = the constant, std 0, advantage 0
+    rpf = torch.tensor([[2.0], [2.0], [2.0], [2.0], [1.0], [3.0], [1.0], [3.0]], device=dev)
+    adv, rew, gm, gs, zs = ops.group_advantages(rpf, torch.ones(1, device=dev), 4, True)
+    assert zs.tolist() == [True, False]
+    assert torch.equal(adv[:4].cpu(), torch.zeros(4))
+    ref = (rpf[4:, 0] - rpf[4:, 0].mean()) / (rpf[4:, 0].std() + 1e-4)
+    torch.testing.assert_close(adv[4:], ref, rtol=1e-6, atol=1e-6)
+    # every completion token masked: bnpo loss = 0 / clamp(0, 1) = 0 and a zero gradient
+    lp = torch.randn(2, 5, device=dev)
+    loss, dlp, _ = ops.grpo_loss_fwd_bwd(lp, torch.tensor([1.0, -1.0], device=dev),
+                                         torch.zeros(2, 5, device=dev, dtype=torch.int32), loss_type="bnpo",
+                                         max_completion_length=5)
+    assert float(loss.reshape(-1)[0]) == 0.0 and torch.count_nonzero(dlp) == 0
+
+
 def test_silu_mul(ops, dev):
     from swh_trl_amd import nn_ops
     g = _gen(19)
