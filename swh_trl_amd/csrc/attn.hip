@@ -218,10 +218,15 @@ __device__ __forceinline__ void fa_stage_store(const FaStage<D> &st, uint16_t *k
 }
 
 
-// ---- forward: grid (ceil(L / 16), Hkv, B); a workgroup = the G = Hq / Hkv query
-// heads of one KV head (one wave each) over the same 16 queries, so every K/V block
-// is staged into LDS once (double-buffered, one barrier per block) for all G heads
-template <int D>
+#ifndef SWH_FA_FWD_QT
+#define SWH_FA_FWD_QT 1  // query tiles per wave in the forward (2: 125 vs 102 us at the bench shape)
+#endif
+
+// ---- forward: grid (ceil(L / (16 QT)), Hkv, B); a workgroup = the G = Hq / Hkv query
+// heads of one KV head (one wave each) over the same 16 QT queries, so every K/V block
+// is staged into LDS once (double-buffered, one barrier per block) for all G heads, and
+// each wave's K fragments of a block serve its QT query tiles
+template <int D, int QT>
 __global__ __launch_bounds__(512) void fa_fwd_kernel(FaArgs a) {
     constexpr int DC = D / 32, DB = D / 16, VS = fa_vs<D>();
     __shared__ __attribute__((aligned(16))) uint16_t kt[2][32 * VS], vt[2][32 * VS];
@@ -230,20 +235,29 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(FaArgs a) {
     const int b = blockIdx.z, kvh = blockIdx.y, G = a.Hq / a.Hkv, L = a.L;
     const bool active = wid < G;  // waves past the group's heads only help staging (blocks >= 4 waves)
     const int h = kvh * G + min(wid, G - 1);
-    const int q0 = blockIdx.x * 16;
-    const int qc = min(q0 + c16, L - 1);  // this lane's query column
+    const int q0 = blockIdx.x * 16 * QT;
     const int fv = a.first_valid ? a.first_valid[b] : 0;
     const uint16_t *kb_ = a.k + ((int64_t)b * a.Hkv + kvh) * L * D;
     const uint16_t *vb_ = a.v + ((int64_t)b * a.Hkv + kvh) * L * D;
     const uint16_t *qb_ = a.q + ((int64_t)b * a.Hq + h) * L * D;
-    u32x4 qf[DC];
+    u32x4 qf[QT][DC];
 #pragma unroll
-    for (int c = 0; c < DC; ++c) qf[c] = *reinterpret_cast<const u32x4 *>(qb_ + (int64_t)qc * D + c * 32 + g * 8);
-    float m = kNegInf, l = 0.f;
-    f32x4a o[DB];
+    for (int t = 0; t < QT; ++t) {
+        const int qc = min(q0 + 16 * t + c16, L - 1);  // this lane's query column of tile t
 #pragma unroll
-    for (int d = 0; d < DB; ++d) o[d] = f32x4a{0.f, 0.f, 0.f, 0.f};
-    const int kend = min(q0 + 16, L);  // causal: keys < kend
+        for (int c = 0; c < DC; ++c)
+            qf[t][c] = *reinterpret_cast<const u32x4 *>(qb_ + (int64_t)qc * D + c * 32 + g * 8);
+    }
+    float m[QT], l[QT];
+    f32x4a o[QT][DB];
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+        m[t] = kNegInf;
+        l[t] = 0.f;
+#pragma unroll
+        for (int d = 0; d < DB; ++d) o[t][d] = f32x4a{0.f, 0.f, 0.f, 0.f};
+    }
+    const int kend = min(q0 + 16 * QT, L);  // causal: keys < kend
     FaStage<D> st;
     fa_stage_load<D>(st, kb_, vb_, 0, L, tid, nthr);
     fa_stage_store<D, VS>(st, kt[0], vt[0], tid, nthr);
@@ -254,48 +268,60 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(FaArgs a) {
         if (more) fa_stage_load<D>(st, kb_, vb_, k0 + 32, L, tid, nthr);  // next block streams meanwhile
         u32x4 kr[2][DC];
         fa_rows_lds<D, VS>(kr, kt[buf], c16, g);
-        f32x4a s[2];
-        fa_abt<D>(s, kr, qf);
         const FaKeyMask km = fa_key_mask(a, b, k0, g);
-        float sv[8], mx = m;
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < QT; ++t) {
+            const int qt0 = q0 + 16 * t;
+            if (k0 >= qt0 + 16) continue;  // wave-uniform: the whole block is in this tile's future
+            f32x4a sc[2];
+            fa_abt<D>(sc, kr, qf[t]);
+            float sv[8], mx = m[t];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int key = k0 + 16 * t + 4 * g + r;
-                const float v = fa_vis(q0 + c16, key, L, km.v[4 * t + r], fv) ? s[t][r] * a.scale : kNegInf;
-                sv[4 * t + r] = v;
-                mx = fmaxf(mx, v);
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int key = k0 + 16 * u + 4 * g + r;
+                    const float v = fa_vis(qt0 + c16, key, L, km.v[4 * u + r], fv) ? sc[u][r] * a.scale : kNegInf;
+                    sv[4 * u + r] = v;
+                    mx = fmaxf(mx, v);
+                }
+            mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
+            mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+            const float corr = (mx == kNegInf) ? 1.f : __expf(m[t] - mx);
+            l[t] *= corr;
+#pragma unroll
+            for (int d = 0; d < DB; ++d) o[t][d] *= corr;
+            m[t] = mx;
+            float p[8];
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+                p[jj] = (mx == kNegInf) ? 0.f : __expf(sv[jj] - mx);
+                l[t] += p[jj];
             }
-        mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
-        const float corr = (mx == kNegInf) ? 1.f : __expf(m - mx);
-        l *= corr;
-#pragma unroll
-        for (int d = 0; d < DB; ++d) o[d] *= corr;
-        m = mx;
-        float p[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            p[j] = (mx == kNegInf) ? 0.f : __expf(sv[j] - mx);
-            l += p[j];
+            fa_xty_shared<D, VS>(o[t], vt[buf], p, c16, g);
         }
-        fa_xty_shared<D, VS>(o, vt[buf], p, c16, g);
         if (more) fa_stage_store<D, VS>(st, kt[buf ^ 1], vt[buf ^ 1], tid, nthr);
         __syncthreads();
     }
-    l += __shfl_xor(l, 16, kWave);
-    l += __shfl_xor(l, 32, kWave);
-    if (active && q0 + c16 < L) {
-        uint16_t *ob = a.out + (((int64_t)b * a.Hq + h) * L + q0 + c16) * D;
-        const float inv = 1.f / l;
 #pragma unroll
-        for (int d = 0; d < DB; ++d) {
-            const uint32_t lo = (uint32_t)f32_to_bf16_bits(o[d][0] * inv) | ((uint32_t)f32_to_bf16_bits(o[d][1] * inv) << 16);
-            const uint32_t hi = (uint32_t)f32_to_bf16_bits(o[d][2] * inv) | ((uint32_t)f32_to_bf16_bits(o[d][3] * inv) << 16);
-            *reinterpret_cast<uint2 *>(ob + d * 16 + 4 * g) = uint2{lo, hi};
+    for (int t = 0; t < QT; ++t) {
+        float lt = l[t];
+        lt += __shfl_xor(lt, 16, kWave);
+        lt += __shfl_xor(lt, 32, kWave);
+        const int q = q0 + 16 * t + c16;
+        if (active && q < L) {
+            uint16_t *ob = a.out + (((int64_t)b * a.Hq + h) * L + q) * D;
+            const float inv = 1.f / lt;
+#pragma unroll
+            for (int d = 0; d < DB; ++d) {
+                const uint32_t lo = (uint32_t)f32_to_bf16_bits(o[t][d][0] * inv) |
+                                    ((uint32_t)f32_to_bf16_bits(o[t][d][1] * inv) << 16);
+                const uint32_t hi = (uint32_t)f32_to_bf16_bits(o[t][d][2] * inv) |
+                                    ((uint32_t)f32_to_bf16_bits(o[t][d][3] * inv) << 16);
+                *reinterpret_cast<uint2 *>(ob + d * 16 + 4 * g) = uint2{lo, hi};
+            }
+            if (g == 0) a.lse[((int64_t)b * a.Hq + h) * L + q] = m[t] + logf(lt);
         }
-        if (g == 0) a.lse[((int64_t)b * a.Hq + h) * L + q0 + c16] = m + logf(l);
     }
 }
 
@@ -526,8 +552,11 @@ extern "C" int swh_attn_fwd(const void *q, const void *k, const void *v, int64_t
     const dim3 grid((unsigned)((L + 15) / 16), (unsigned)Hkv, (unsigned)B);
     const unsigned thr = 64u * (unsigned)(Hq / Hkv < 4 ? 4 : Hq / Hkv);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (D == 64) fa_fwd_kernel<64><<<grid, thr, 0, s>>>(a);
-    else fa_fwd_kernel<128><<<grid, thr, 0, s>>>(a);
+    // SWH_FA_FWD_QT 16-query tiles per wave (the K fragments of a block serve them all)
+    constexpr int QT = SWH_FA_FWD_QT;
+    const dim3 gq((unsigned)((L + 16 * QT - 1) / (16 * QT)), (unsigned)Hkv, (unsigned)B);
+    if (D == 64) fa_fwd_kernel<64, QT><<<gq, thr, 0, s>>>(a);
+    else fa_fwd_kernel<128, QT><<<gq, thr, 0, s>>>(a);
     return launch_status();
 }
 
