@@ -127,6 +127,14 @@ __host__ __device__ inline GemmLds gemm_lds(int cb, int mr, int nw, int krmax, i
 #ifndef SWH_ROUND_PREFETCH
 #define SWH_ROUND_PREFETCH 0  // all A reads of a full round before its MFMAs (A/B: tools/build_variant.py)
 #endif
+#ifndef SWH_W_NT
+#define SWH_W_NT 0  // weight-stream loads with the non-temporal policy (A/B)
+#endif
+// one 16-B weight fragment (read once per launch)
+__device__ __forceinline__ uint4 ld_w(const uint16_t *p) {
+    if constexpr (SWH_W_NT) return ld_nt(reinterpret_cast<const uint4 *>(p));
+    return *reinterpret_cast<const uint4 *>(p);
+}
 #ifndef SWH_GEMM_RING
 #define SWH_GEMM_RING 0  // decode_gemm k-loop: refill each k-step's weight registers right after its MFMAs (A/B)
 #endif
@@ -206,7 +214,7 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
             if (ks + u < ksw1) {
 #pragma unroll
                 for (int j = 0; j < CB; ++j)  // plain loads: the line's other half is the next k-step's load
-                    bv[u][j] = *reinterpret_cast<const uint4 *>(wrow[j] + (ks + u) * 32);
+                    bv[u][j] = ld_w(wrow[j] + (ks + u) * 32);
             }
         }
     };
@@ -396,7 +404,7 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
                         // its MFMAs have read them, so kU k-steps stay in flight per wave
 #pragma unroll
                         for (int j = 0; j < CB; ++j)
-                            bv[u][j] = *reinterpret_cast<const uint4 *>(wrow[j] + (ks + kU + u) * 32);
+                            bv[u][j] = ld_w(wrow[j] + (ks + kU + u) * 32);
                     }
                 }
             }
@@ -611,7 +619,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
         const uint16_t *wr = w + wrow_of(tile) * K + kq;
 #pragma unroll
         for (int ks = 0; ks < KSA; ++ks)
-            if (KSC || ks < KS) bv[ks] = *reinterpret_cast<const uint4 *>(wr + ks * 32);
+            if (KSC || ks < KS) bv[ks] = ld_w(wr + ks * 32);
     };
     if (t < ntile) issue(t);  // the weight stream first
     // RMSNorm partials and norm weights (L2), then the X image by LDS-DMA
@@ -775,7 +783,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
                 for (int i = 0; i < 4; ++i)
                     acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[ks & 1][i]), as_bf16x8(bv[ks]),
                                                                     acc[i], 0, 0, 0);
-                if (ring) bv[ks] = *reinterpret_cast<const uint4 *>(wnext + ks * 32);
+                if (ring) bv[ks] = ld_w(wnext + ks * 32);
                 __builtin_amdgcn_sched_barrier(0);
             }
         } else {
