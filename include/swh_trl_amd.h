@@ -273,6 +273,14 @@ int swh_attn_fwd(const void *q, const void *k, const void *v, int64_t B, int32_t
 int swh_attn_bwd(const void *q, const void *k, const void *v, const void *out, const void *dout, const float *lse,
                  int64_t B, int32_t Hq, int32_t Hkv, int64_t L, int32_t D, float scale, const int32_t *key_mask,
                  const int32_t *first_valid, float *delta, void *dq, void *dk, void *dv, void *stream);
+/* swh_attn_bwd in parts, for callers that overlap them on two streams: bit 1
+ * delta = rowsum(dO * O) (the other two read it), bit 2 dQ, bit 4 dK/dV.  dQ and
+ * dK/dV are independent once delta is written.  parts = 7 is swh_attn_bwd. */
+enum { SWH_ATTN_BWD_DELTA = 1, SWH_ATTN_BWD_DQ = 2, SWH_ATTN_BWD_DKDV = 4 };
+int swh_attn_bwd_parts(const void *q, const void *k, const void *v, const void *out, const void *dout,
+                       const float *lse, int64_t B, int32_t Hq, int32_t Hkv, int64_t L, int32_t D, float scale,
+                       const int32_t *key_mask, const int32_t *first_valid, float *delta, void *dq, void *dk,
+                       void *dv, int32_t parts, void *stream);
 
 /* Folded RMSNorm weights for the decode GEMMs in ONE launch: for every job j of
  * the device-resident table jobs[njobs] = {W [rows, cols] bf16, w [cols] bf16,

@@ -74,6 +74,8 @@ SIGNATURES = {
     "swh_attn_fwd": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "swh_attn_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i64, c_i32, c_f32, c_vp, c_vp,
                              c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "swh_attn_bwd_parts": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i64, c_i32, c_f32, c_vp,
+                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp]),
     "swh_fold_norm": (c_i32, [c_vp, c_i32, c_i64, c_vp]),
     "swh_embed_gather": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "swh_qkv_rope": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i32,

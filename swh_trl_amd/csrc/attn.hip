@@ -560,12 +560,12 @@ extern "C" int swh_attn_fwd(const void *q, const void *k, const void *v, int64_t
     return launch_status();
 }
 
-extern "C" int swh_attn_bwd(const void *q, const void *k, const void *v, const void *out, const void *dout,
-                            const float *lse, int64_t B, int32_t Hq, int32_t Hkv, int64_t L, int32_t D, float scale,
-                            const int32_t *key_mask, const int32_t *first_valid, float *delta, void *dq, void *dk,
-                            void *dv, void *stream) {
+extern "C" int swh_attn_bwd_parts(const void *q, const void *k, const void *v, const void *out, const void *dout,
+                                  const float *lse, int64_t B, int32_t Hq, int32_t Hkv, int64_t L, int32_t D,
+                                  float scale, const int32_t *key_mask, const int32_t *first_valid, float *delta,
+                                  void *dq, void *dk, void *dv, int32_t parts, void *stream) {
     if (!fa_args_ok(q, k, v, B, Hq, Hkv, L, D) || !out || !dout || !lse || !delta || !dq || !dk || !dv ||
-        (!key_mask != !first_valid))
+        (!key_mask != !first_valid) || parts <= 0 || parts > 7)
         return SWH_E_ARG;
     FaArgs a{};
     a.q = static_cast<const uint16_t *>(q);
@@ -590,14 +590,23 @@ extern "C" int swh_attn_bwd(const void *q, const void *k, const void *v, const v
     const dim3 grid((unsigned)((L + 15) / 16), (unsigned)Hkv, (unsigned)B);
     const unsigned thr = 64u * (unsigned)(Hq / Hkv < 4 ? 4 : Hq / Hkv);
     const dim3 gk((unsigned)((L + 63) / 64), (unsigned)Hkv, (unsigned)B);
+    const dim3 gd((unsigned)((rows + 255) / 256));
     if (D == 64) {
-        fa_delta_kernel<64><<<dim3((unsigned)((rows + 255) / 256)), 256, 0, s>>>(a, rows);
-        fa_dq_kernel<64><<<grid, thr, 0, s>>>(a);
-        fa_dkdv_kernel<64><<<gk, 256, 0, s>>>(a);
+        if (parts & SWH_ATTN_BWD_DELTA) fa_delta_kernel<64><<<gd, 256, 0, s>>>(a, rows);
+        if (parts & SWH_ATTN_BWD_DQ) fa_dq_kernel<64><<<grid, thr, 0, s>>>(a);
+        if (parts & SWH_ATTN_BWD_DKDV) fa_dkdv_kernel<64><<<gk, 256, 0, s>>>(a);
     } else {
-        fa_delta_kernel<128><<<dim3((unsigned)((rows + 255) / 256)), 256, 0, s>>>(a, rows);
-        fa_dq_kernel<128><<<grid, thr, 0, s>>>(a);
-        fa_dkdv_kernel<128><<<gk, 256, 0, s>>>(a);
+        if (parts & SWH_ATTN_BWD_DELTA) fa_delta_kernel<128><<<gd, 256, 0, s>>>(a, rows);
+        if (parts & SWH_ATTN_BWD_DQ) fa_dq_kernel<128><<<grid, thr, 0, s>>>(a);
+        if (parts & SWH_ATTN_BWD_DKDV) fa_dkdv_kernel<128><<<gk, 256, 0, s>>>(a);
     }
     return launch_status();
+}
+
+extern "C" int swh_attn_bwd(const void *q, const void *k, const void *v, const void *out, const void *dout,
+                            const float *lse, int64_t B, int32_t Hq, int32_t Hkv, int64_t L, int32_t D, float scale,
+                            const int32_t *key_mask, const int32_t *first_valid, float *delta, void *dq, void *dk,
+                            void *dv, void *stream) {
+    return swh_attn_bwd_parts(q, k, v, out, dout, lse, B, Hq, Hkv, L, D, scale, key_mask, first_valid, delta, dq, dk,
+                              dv, SWH_ATTN_BWD_DELTA | SWH_ATTN_BWD_DQ | SWH_ATTN_BWD_DKDV, stream);
 }

@@ -6,6 +6,7 @@ runs (third-party code reached from grpo_trainer.py:1804 and :1249).
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -232,10 +233,38 @@ class AttentionFn(torch.autograd.Function):
         dout = dout.contiguous()
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         delta = torch.empty(B, Hq, L, device=q.device, dtype=torch.float32)
-        call("swh_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), dout.data_ptr(),
-             lse.data_ptr(), B, Hq, Hkv, L, D, ctx.scale, _p(ctx.km), _p(ctx.fv), delta.data_ptr(), dq.data_ptr(),
-             dk.data_ptr(), dv.data_ptr(), _stream())
+        args = (q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), B, Hq,
+                Hkv, L, D, ctx.scale, _p(ctx.km), _p(ctx.fv), delta.data_ptr(), dq.data_ptr(), dk.data_ptr(),
+                dv.data_ptr())
+        aux = _aux_stream(q.device)
+        if aux is None:
+            call("swh_attn_bwd_parts", *args, 7, _stream())
+            return dq, dk, dv, None, None, None
+        # dK/dV on the auxiliary stream beside dQ (both read delta only): the key
+        # tiles' uneven causal work leaves CUs the dQ blocks fill
+        main = torch.cuda.current_stream(q.device)
+        call("swh_attn_bwd_parts", *args, 1, _stream())
+        aux.wait_stream(main)
+        with torch.cuda.stream(aux):
+            call("swh_attn_bwd_parts", *args, 4, _stream())
+        call("swh_attn_bwd_parts", *args, 2, _stream())
+        main.wait_stream(aux)
         return dq, dk, dv, None, None, None
+
+
+_AUX_STREAMS: dict = {}
+
+
+def _aux_stream(dev: torch.device):
+    """Second stream for the dK/dV half of the attention backward (SWH_ATTN_SPLIT=0:
+    one stream).  Every tensor it touches was allocated on, and is joined back to,
+    the calling stream before the backward returns."""
+    if dev.type != "cuda" or os.environ.get("SWH_ATTN_SPLIT", "1") == "0":
+        return None
+    st = _AUX_STREAMS.get(dev.index)
+    if st is None:
+        st = _AUX_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+    return st
 
 
 def attention_supported(D: int) -> bool:
