@@ -108,25 +108,30 @@ class _Linear(torch.autograd.Function):
         x, w = ctx.saved_tensors
         dx = dy @ w if ctx.needs_input_grad[0] else None
         if ctx.gw is not None:
-            with _OnStream(_dw_stream(dy.device)) as side:
-                side.keep(dy, x)
-                dy2 = dy.reshape(-1, dy.shape[-1])
-                x2 = x.reshape(-1, x.shape[-1])
-                S = _dw_split(dy2.shape[0], dy2.shape[1] * x2.shape[1])
-                if S > 1:
-                    # few output tiles over a long token dimension: split the tokens into S
-                    # batched GEMMs (S x the workgroups), sum the partials into the gradient
-                    Kc = dy2.shape[0] // S
-                    parts = torch.bmm(dy2[:S * Kc].view(S, Kc, -1).transpose(1, 2), x2[:S * Kc].view(S, Kc, -1))
-                    acc = parts.sum(0, dtype=torch.float32)
-                    if S * Kc < dy2.shape[0]:
-                        acc.addmm_(dy2[S * Kc:].t().float(), x2[S * Kc:].float())
-                    ctx.gw.add_(acc)
-                else:
-                    ctx.gw.addmm_(dy2.t(), x2)
-                if ctx.gb is not None:
-                    ctx.gb.add_(dy2.sum(0, dtype=torch.float32).to(ctx.gb.dtype))
+            _accumulate_dw(ctx.gw, ctx.gb, dy, x)
         return dx, None, None, None, None
+
+
+def _accumulate_dw(gw, gb, dy, x):
+    """gw += dy^T x (and gb += column sums of dy) on the weight-gradient stream."""
+    with _OnStream(_dw_stream(dy.device)) as side:
+        side.keep(dy, x)
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        x2 = x.reshape(-1, x.shape[-1])
+        S = _dw_split(dy2.shape[0], dy2.shape[1] * x2.shape[1])
+        if S > 1:
+            # few output tiles over a long token dimension: split the tokens into S
+            # batched GEMMs (S x the workgroups), sum the partials into the gradient
+            Kc = dy2.shape[0] // S
+            parts = torch.bmm(dy2[:S * Kc].view(S, Kc, -1).transpose(1, 2), x2[:S * Kc].view(S, Kc, -1))
+            acc = parts.sum(0, dtype=torch.float32)
+            if S * Kc < dy2.shape[0]:
+                acc.addmm_(dy2[S * Kc:].t().float(), x2[S * Kc:].float())
+            gw.add_(acc)
+        else:
+            gw.addmm_(dy2.t(), x2)
+        if gb is not None:
+            gb.add_(dy2.sum(0, dtype=torch.float32).to(gb.dtype))
 
 
 def _dw_split(tokens: int, outputs: int) -> int:

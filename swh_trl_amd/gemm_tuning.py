@@ -39,6 +39,8 @@ def enable(mode: str | None = None) -> str:
         tun.tuning_enable(True)
         tun.set_max_tuning_duration(30)
         tun.set_filename(path, False)
+        if os.path.exists(path):  # extend an existing table: only new shapes are tuned
+            tun.read_file(path)
     elif mode == "use":
         if not os.path.exists(path):
             return "off"
