@@ -105,6 +105,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--layers", type=int, default=None, help="debug only: shrink the model (invalid for reporting)")
+    ap.add_argument("--variant", choices=("default", "top_p", "greedy"), default="default",
+                    help="SURVEY.md §8d cfg2 sampling variants: top_p 0.9, or greedy decoding")
     args = ap.parse_args()
 
     from swh_trl_amd import dist as sd
@@ -120,11 +122,14 @@ def main():
     steps, warm = args.steps, args.warmup
     n_prompts = PROMPTS_PER_GPU * world * (steps + warm + 1)
     ds = make_dataset(n_prompts, cfg.vocab_size)
+    gen_kw = {"min_new_tokens": C, "eos_token_id": EOS, "pad_token_id": PAD}
+    if args.variant == "greedy":
+        gen_kw["do_sample"] = False
     gc = GRPOConfig(output_dir="/tmp/grpo-bench", per_device_train_batch_size=MB, gradient_accumulation_steps=GA,
                     num_generations=G, max_prompt_length=P, max_completion_length=C, learning_rate=1e-6,
-                    beta=0.0, temperature=1.0, top_p=1.0, max_steps=steps + warm, logging_steps=10 ** 9, seed=0,
-                    shuffle_dataset=True,
-                    generation_kwargs={"min_new_tokens": C, "eos_token_id": EOS, "pad_token_id": PAD})
+                    beta=0.0, temperature=1.0, top_p=0.9 if args.variant == "top_p" else 1.0,
+                    max_steps=steps + warm, logging_steps=10 ** 9, seed=0, shuffle_dataset=True,
+                    generation_kwargs=gen_kw)
     tr = GRPOTrainer(model=cfg, reward_funcs=dummy_reward, args=gc, train_dataset=ds)
     tr.state.max_steps = steps + warm
     tb = time.perf_counter()
@@ -184,7 +189,8 @@ def main():
             "warmup": warm, "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (uniform prompt ids seed 1234, random-init weights, dummy reward)",
-            "config": {"workload": "configs[1]: Qwen2.5-0.5B GRPO bf16, group_size=8, 256-tok completions",
+            "config": {"workload": "configs[1]: Qwen2.5-0.5B GRPO bf16, group_size=8, 256-tok completions" +
+                       ("" if args.variant == "default" else f" ({args.variant} sampling variant)"),
                        "model": "Qwen2.5-0.5B (random init)", "global_batch": world * PROMPTS_PER_GPU * G,
                        "prompts_per_gpu": PROMPTS_PER_GPU, "num_generations": G, "prompt_len": P,
                        "completion_len": C, "seq_len": P + C, "micro_batch": MB, "grad_accum": GA, "beta": 0.0,

@@ -103,7 +103,27 @@ __device__ __forceinline__ void row_foreach(const typename Elem<DT>::T *row, int
     const int64_t b0 = begin + head;
     const int64_t nvec = (end - b0) / PV;
     const uint4 *vp = reinterpret_cast<const uint4 *>(row + b0);
-    for (int64_t v = tid; v < nvec; v += nthreads) {
+    // four grid-strided vectors per trip, all loads issued before any use: a
+    // workgroup walking a long row alone keeps 4 loads in flight per thread
+    constexpr int U = 4;
+    int64_t v = tid;
+    for (; v + (U - 1) * (int64_t)nthreads < nvec; v += U * (int64_t)nthreads) {
+        uint4 raw[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if constexpr (NT) raw[u] = ld_nt(vp + v + u * nthreads);
+            else raw[u] = vp[v + u * nthreads];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float x[PV];
+            unpack16<DT>(raw[u], x);
+            const int64_t j0 = b0 + (v + u * nthreads) * PV;
+#pragma unroll
+            for (int k = 0; k < PV; ++k) f(j0 + k, x[k]);
+        }
+    }
+    for (; v < nvec; v += nthreads) {
         float x[PV];
         uint4 raw;
         if constexpr (NT) raw = ld_nt(vp + v);

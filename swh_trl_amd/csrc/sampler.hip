@@ -14,11 +14,13 @@
 //  * unfiltered rows (no top-k/top-p/min-p): the row is split over S
 //    workgroups (B*S >= ~512 WGs fill the chip), each folding its chunk into
 //    (max, sum e^{z-m}, best key, best index); `finalize` merges the S partials.
-//  * filtered rows: one 1024-thread workgroup per row; thresholds for top-k
-//    (count) and top-p (mass) by an 11/11/10-bit radix select in LDS over the
-//    order-preserving integer image of z; min-p is the closed form
-//    z >= max + ln(min_p).  All three filters keep {z >= tau}, so their
-//    composition is the largest tau.
+//  * filtered rows: the same split over workgroups for every pass; thresholds
+//    for top-k (count) and top-p (mass) by an 11/11/10-bit radix select over
+//    the order-preserving integer image of z (per-split digit histograms, one
+//    select launch per digit); min-p is the closed form z >= max + ln(min_p).
+//    All three filters keep {z >= tau}, so their composition is the largest tau.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace swh {
@@ -168,138 +170,234 @@ __device__ __forceinline__ float key_to_float(uint32_t k) {
 
 constexpr int kBins = 2048;
 
-// Block-wide: find the key tau with W(key > tau) < target <= W(key >= tau),
-// where W sums weight(z) over elements with z >= lo (the current kept set).
-// The bin at each level is the HIGHEST bin whose inclusive suffix weight
-// reaches target (a max-reduction, robust to float reassociation).  Returns
-// false if the total weight stays below target (keep everything).
-template <int DT, typename WF>
-__device__ bool radix_select(const typename Elem<DT>::T *row, int64_t V, const Proc &pr, float lo, WF weight,
-                             float target, float *hist, float *scan, int *sel, uint32_t &tau_key) {
-    uint32_t prefix = 0, pmask = 0;
-    float above = 0.f;
-    const int t = threadIdx.x;
-    const int lane = t & 63, wid = t >> 6, nw = blockDim.x >> 6;
-#pragma unroll 1
-    for (int lvl = 0; lvl < 3; ++lvl) {
-        const int sh = lvl == 0 ? 21 : (lvl == 1 ? 10 : 0);
-        const uint32_t dmask = lvl == 2 ? 0x3ffu : 0x7ffu;
-        for (int i = t; i < kBins; i += blockDim.x) hist[i] = 0.f;
-        if (t == 0) {
-            sel[0] = -1;
-            sel[1] = kBins;
-        }
-        __syncthreads();
-        row_foreach<DT, false>(row, 0, V, t, blockDim.x, [&](int64_t j, float x) {
-            const float z = pr(j, x);
-            if (!(z >= lo) || z == kNegInf) return;
-            const uint32_t k = ord_key(z);
-            if ((k & pmask) != prefix) return;
-            atomicAdd(&hist[(k >> sh) & dmask], weight(z));
-        });
-        __syncthreads();
-        const float h0 = hist[2 * t], h1 = hist[2 * t + 1];
-        const float tsum = h0 + h1;
-        float v = tsum;  // inclusive suffix scan over lanes (higher lanes = higher bins)
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const float u = __shfl_down(v, o, kWave);
-            if (lane + o < 64) v += u;
-        }
-        if (lane == 0) scan[wid] = v;
-        __syncthreads();
-        float after = 0.f;
-        for (int w = wid + 1; w < nw; ++w) after += scan[w];
-        const float a1 = above + (v - tsum) + after;  // weight strictly above bin 2t+1
-        const float a0 = a1 + h1;                     // weight strictly above bin 2t
-        int cand = -1;
-        if (h1 > 0.f && a1 + h1 >= target) cand = 2 * t + 1;
-        else if (h0 > 0.f && a0 + h0 >= target) cand = 2 * t;
-        if (cand >= 0) atomicMax(&sel[0], cand);
-        if (h0 > 0.f) atomicMin(&sel[1], 2 * t);
-        else if (h1 > 0.f) atomicMin(&sel[1], 2 * t + 1);
-        __syncthreads();
-        int bin = sel[0];
-        if (bin < 0) {
-            if (lvl == 0) return false;
-            bin = sel[1] < kBins ? sel[1] : 0;
-        }
-        if (bin == 2 * t + 1) scan[nw] = a1;
-        if (bin == 2 * t) scan[nw] = a0;
-        __syncthreads();
-        above = scan[nw];
-        __syncthreads();
-        prefix |= (uint32_t)bin << sh;
-        pmask |= dmask << sh;
-    }
-    tau_key = prefix;
-    return true;
+constexpr int kFiltSplit = 32;  // workgroups per filtered row (at most)
+
+// Filtered rows over S workgroups each.  Every pass is split like the
+// unfiltered path (one workgroup per row ran 64 rows on 64 CUs, and its LDS
+// histogram atomics piled onto the few exponent bins most scores share: 549 us
+// at 64 x 151936, top-p 0.9).  A threshold is an 11/11/10-bit radix select over
+// the order-preserving key of z: each split writes its own 2048-bin partial
+// histogram of the next digit, and a per-row select launch sums the S partials
+// in fixed order, takes the HIGHEST bin whose inclusive suffix weight reaches
+// the target (a max-reduction, robust to float reassociation) and advances the
+// row's state in the workspace.  A filter whose total weight stays below its
+// target keeps everything.
+struct FiltRow {
+    float M, lse, lo, above;  // row max, log-normaliser of the weights, threshold, weight above the bin
+    uint32_t prefix, pmask;   // key bits resolved so far
+    int32_t active, pad;      // 0: the current filter keeps everything
+};
+
+struct FiltWs {
+    FiltRow *row;  // [B]
+    float2 *soft;  // [B][S] (max, sum e^(z - max)) partials
+    float *hist;   // [B][S][kBins]
+};
+
+inline FiltWs filt_ws(void *ws, int64_t B) {
+    char *base = static_cast<char *>(ws) + B * kMaxSplit * (int64_t)sizeof(Partial);
+    FiltWs w;
+    w.row = reinterpret_cast<FiltRow *>(base);
+    base += B * (int64_t)sizeof(FiltRow);
+    w.soft = reinterpret_cast<float2 *>(base);
+    base += B * kFiltSplit * (int64_t)sizeof(float2);
+    w.hist = reinterpret_cast<float *>(base);
+    return w;
 }
 
+__device__ __forceinline__ void split_range(int64_t V, int64_t chunk, int64_t &beg, int64_t &end) {
+    beg = (int64_t)blockIdx.x * chunk;
+    end = beg + chunk < V ? beg + chunk : V;
+}
+
+// (max, sum) of the processed scores >= the row threshold (st null: all) over split blockIdx.x
 template <int DT>
-__global__ __launch_bounds__(kFiltThreads) void sample_filtered_kernel(
+__global__ __launch_bounds__(kSplitThreads) void filt_soft_kernel(
     const typename Elem<DT>::T *__restrict__ logits, int64_t V, int64_t ld, swh_sample_params p,
-    const uint64_t *__restrict__ rng, const int32_t *__restrict__ step_p, const uint32_t *__restrict__ seen,
-    int64_t words, Partial *__restrict__ part, float *__restrict__ scores_out) {
+    const int32_t *__restrict__ step_p, const uint32_t *__restrict__ seen, int64_t words, int64_t chunk,
+    const FiltRow *__restrict__ st, float2 *__restrict__ psoft) {
+    __shared__ float red[5 * (kSplitThreads / kWave)];
+    const int64_t b = blockIdx.y;
+    const Proc pr = make_proc(p, *step_p, seen ? seen + b * words : nullptr);
+    const float lo = st ? st[b].lo : kNegInf;
+    int64_t beg, end;
+    split_range(V, chunk, beg, end);
+    SoftState sf = soft_init();
+    row_foreach<DT, false>(logits + b * ld, beg, end, threadIdx.x, kSplitThreads, [&](int64_t j, float x) {
+        float z = pr(j, x);
+        if (!(z >= lo)) z = kNegInf;
+        soft_fold<1>(sf, &z);
+    });
+    sf = block_soft(sf, red);
+    if (threadIdx.x == 0) psoft[b * gridDim.x + blockIdx.x] = float2{sf.m, sf.s1};
+}
+
+// Opens a filter: mode 0 also records the row max and sets the threshold to -inf
+// (the log-normaliser of all scores); mode 1 takes the log-normaliser of the
+// survivors of the previous filter.
+__global__ __launch_bounds__(64) void filt_row_kernel(FiltRow *__restrict__ st, const float2 *__restrict__ psoft,
+                                                      int S, int mode) {
+    const int64_t b = blockIdx.x;
+    const int lane = threadIdx.x;
+    SoftState a = soft_init();
+    for (int q = lane; q < S; q += 64) a = soft_merge(a, SoftState{psoft[b * S + q].x, psoft[b * S + q].y, 0.f});
+    a = wave_soft(a);
+    if (lane != 0) return;
+    FiltRow r = st[b];
+    if (mode == 0) {
+        r.M = a.m;
+        r.lo = kNegInf;
+    }
+    r.lse = a.m + fast_log(a.s1);
+    r.above = 0.f;
+    r.prefix = 0u;
+    r.pmask = 0u;
+    r.active = 1;
+    st[b] = r;
+}
+
+// Partial histogram of digit `lvl` over split blockIdx.x: scores >= lo whose
+// resolved key bits match, weighted 1 (top-k) or e^(z - lse) (top-p).  Runs of
+// equal bins within a thread's elements are summed in registers first (scores
+// mostly share a few exponent bins), one LDS atomic per run.
+template <int DT, bool EXPW>
+__global__ __launch_bounds__(kSplitThreads) void filt_hist_kernel(
+    const typename Elem<DT>::T *__restrict__ logits, int64_t V, int64_t ld, swh_sample_params p,
+    const int32_t *__restrict__ step_p, const uint32_t *__restrict__ seen, int64_t words, int64_t chunk,
+    const FiltRow *__restrict__ st, int lvl, float *__restrict__ phist) {
     __shared__ float hist[kBins];
+    const int64_t b = blockIdx.y;
+    const int t = threadIdx.x;
+    const FiltRow r = st[b];
+    if (!r.active) return;
+    const int sh = lvl == 0 ? 21 : (lvl == 1 ? 10 : 0);
+    const uint32_t dmask = lvl == 2 ? 0x3ffu : 0x7ffu;
+    for (int i = t; i < kBins; i += kSplitThreads) hist[i] = 0.f;
+    __syncthreads();
+    const Proc pr = make_proc(p, *step_p, seen ? seen + b * words : nullptr);
+    int64_t beg, end;
+    split_range(V, chunk, beg, end);
+    int run_bin = -1;
+    float run_w = 0.f;
+    row_foreach<DT, false>(logits + b * ld, beg, end, t, kSplitThreads, [&](int64_t j, float x) {
+        const float z = pr(j, x);
+        if (!(z >= r.lo) || z == kNegInf) return;
+        const uint32_t k = ord_key(z);
+        if ((k & r.pmask) != r.prefix) return;
+        const int bin = (int)((k >> sh) & dmask);
+        const float w = EXPW ? fast_exp(z - r.lse) : 1.0f;
+        if (bin == run_bin) {
+            run_w += w;
+        } else {
+            if (run_bin >= 0) atomicAdd(&hist[run_bin], run_w);
+            run_bin = bin;
+            run_w = w;
+        }
+    });
+    if (run_bin >= 0) atomicAdd(&hist[run_bin], run_w);
+    __syncthreads();
+    float *dst = phist + (b * gridDim.x + blockIdx.x) * (int64_t)kBins;
+    for (int i = t; i < kBins; i += kSplitThreads) dst[i] = hist[i];
+}
+
+// One radix level per row: the bin of digit `lvl` where the weight from the top
+// reaches `target`; the last level turns the resolved key into the threshold.
+__global__ __launch_bounds__(kFiltThreads) void filt_select_kernel(FiltRow *__restrict__ st,
+                                                                    const float *__restrict__ phist, int S, int lvl,
+                                                                    float target) {
     __shared__ float scan[64];
     __shared__ int sel[2];
-    __shared__ float red[5 * (kFiltThreads / kWave)];
     const int64_t b = blockIdx.x;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6, nw = kFiltThreads >> 6;
+    const FiltRow r = st[b];
+    if (!r.active) return;
+    const int sh = lvl == 0 ? 21 : (lvl == 1 ? 10 : 0);
+    const uint32_t dmask = lvl == 2 ? 0x3ffu : 0x7ffu;
+    float h0 = 0.f, h1 = 0.f;
+    for (int q = 0; q < S; ++q) {  // splits in fixed order
+        const float *h = phist + (b * S + q) * (int64_t)kBins;
+        h0 += h[2 * t];
+        h1 += h[2 * t + 1];
+    }
+    if (t == 0) {
+        sel[0] = -1;
+        sel[1] = kBins;
+    }
+    __syncthreads();
+    const float tsum = h0 + h1;
+    float v = tsum;  // inclusive suffix scan over lanes (higher lanes = higher bins)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const float u = __shfl_down(v, o, kWave);
+        if (lane + o < 64) v += u;
+    }
+    if (lane == 0) scan[wid] = v;
+    __syncthreads();
+    float after = 0.f;
+    for (int w = wid + 1; w < nw; ++w) after += scan[w];
+    const float a1 = r.above + (v - tsum) + after;  // weight strictly above bin 2t+1
+    const float a0 = a1 + h1;                       // weight strictly above bin 2t
+    int cand = -1;
+    if (h1 > 0.f && a1 + h1 >= target) cand = 2 * t + 1;
+    else if (h0 > 0.f && a0 + h0 >= target) cand = 2 * t;
+    if (cand >= 0) atomicMax(&sel[0], cand);
+    if (h0 > 0.f) atomicMin(&sel[1], 2 * t);
+    else if (h1 > 0.f) atomicMin(&sel[1], 2 * t + 1);
+    __syncthreads();
+    int bin = sel[0];
+    if (bin < 0) {
+        if (lvl == 0) {  // the filter's total weight stays below its target: keep everything
+            if (t == 0) st[b].active = 0;
+            return;
+        }
+        bin = sel[1] < kBins ? sel[1] : 0;
+    }
+    if (bin == 2 * t + 1) scan[nw] = a1;
+    if (bin == 2 * t) scan[nw] = a0;
+    __syncthreads();
+    if (t == 0) {
+        FiltRow w = r;
+        w.above = scan[nw];
+        w.prefix |= (uint32_t)bin << sh;
+        w.pmask |= dmask << sh;
+        if (lvl == 2) w.lo = fmaxf(w.lo, key_to_float(w.prefix));
+        st[b] = w;
+    }
+}
+
+// Final pass over split blockIdx.x: min-p, then the Gumbel-max draw among the survivors
+template <int DT>
+__global__ __launch_bounds__(kSplitThreads) void filt_draw_kernel(
+    const typename Elem<DT>::T *__restrict__ logits, int64_t V, int64_t ld, swh_sample_params p,
+    const uint64_t *__restrict__ rng, const int32_t *__restrict__ step_p, const uint32_t *__restrict__ seen,
+    int64_t words, int64_t chunk, const FiltRow *__restrict__ st, Partial *__restrict__ part,
+    float *__restrict__ scores_out) {
+    __shared__ float red[5 * (kSplitThreads / kWave)];
+    const int64_t b = blockIdx.y;
     const int32_t step = *step_p;
     const Proc pr = make_proc(p, step, seen ? seen + b * words : nullptr);
-    const auto *row = logits + b * ld;
-
-    // pass 1: max / lse of the processed scores
-    SoftState st = soft_init();
-    row_foreach<DT, false>(row, 0, V, threadIdx.x, kFiltThreads, [&](int64_t j, float x) {
-        const float z = pr(j, x);
-        soft_fold<1>(st, &z);
-    });
-    st = block_soft(st, red);
-    const float M = st.m;
-    float lo = kNegInf;
-    // top-k (count threshold)
-    if (p.top_k > 0 && p.top_k < V) {
-        uint32_t tk;
-        if (radix_select<DT>(row, V, pr, kNegInf, [](float) { return 1.0f; }, (float)p.top_k, hist, scan, sel, tk))
-            lo = key_to_float(tk);
-    }
-    // top-p (mass threshold, renormalised over the top-k survivors)
-    if (p.top_p < 1.0f) {
-        SoftState sk = soft_init();
-        row_foreach<DT, false>(row, 0, V, threadIdx.x, kFiltThreads, [&](int64_t j, float x) {
-            float z = pr(j, x);
-            if (!(z >= lo)) z = kNegInf;
-            soft_fold<1>(sk, &z);
-        });
-        sk = block_soft(sk, red);
-        const float lse_k = sk.m + fast_log(sk.s1);
-        uint32_t tp;
-        if (radix_select<DT>(row, V, pr, lo, [&](float z) { return fast_exp(z - lse_k); }, p.top_p, hist, scan, sel, tp))
-            lo = fmaxf(lo, key_to_float(tp));
-    }
+    const FiltRow r = st[b];
+    float lo = r.lo;
     // min-p: p_j < min_p * p_max  <=>  z_j < M + ln(min_p)
-    if (p.min_p > 0.f) lo = fmaxf(lo, M + logf(p.min_p));
-
-    // final pass: draw among survivors
+    if (p.min_p > 0.f) lo = fmaxf(lo, r.M + logf(p.min_p));
     const uint64_t seed = rng[0], ctr = rng[1] + (uint64_t)step;
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    int64_t beg, end;
+    split_range(V, chunk, beg, end);
     SoftState sf = soft_init();
     float bk = kNegInf;
     int32_t bi = 0x7fffffff;
     float *srow = scores_out ? scores_out + b * V : nullptr;
-    row_foreach<DT, false>(row, 0, V, threadIdx.x, kFiltThreads, [&](int64_t j, float x) {
+    row_foreach<DT, false>(logits + b * ld, beg, end, threadIdx.x, kSplitThreads, [&](int64_t j, float x) {
         float z = pr(j, x);
         if (!(z >= lo)) z = kNegInf;
         if (srow) srow[j] = z;
         if (z == kNegInf) return;
         soft_fold<1>(sf, &z);
-        const float key = z + gumbel_at(k0, k1, j, b, ctr);
-        best_merge(bk, bi, key, (int32_t)j);
+        best_merge(bk, bi, z + gumbel_at(k0, k1, j, b, ctr), (int32_t)j);
     });
     block_partial(sf, bk, bi, red);
-    if (threadIdx.x == 0) part[b] = Partial{sf.m, sf.s1, bk, bi};
+    if (threadIdx.x == 0) part[b * gridDim.x + blockIdx.x] = Partial{sf.m, sf.s1, bk, bi};
 }
 
 // ---------------------------------------------------------------------------
@@ -363,14 +461,55 @@ int choose_split(int64_t B, int64_t V) {
     return S;
 }
 
+template <int DT>
+int launch_filtered(const typename Elem<DT>::T *lg, int64_t B, int64_t V, int64_t ld, const swh_sample_params &p,
+                    const uint64_t *rng, const int32_t *step, const uint32_t *seen, int64_t words, void *workspace,
+                    float *scores_out, hipStream_t s) {
+    // more splits than the unfiltered path: each digit pass is bound by its
+    // workgroups' LDS histogram atomics, so spread a row over up to SWH_FILT_WGS
+    static const int target = getenv("SWH_FILT_WGS") ? atoi(getenv("SWH_FILT_WGS")) : 1024;
+    int S = 1;
+    while (S < kFiltSplit && B * S < target && V / (S * 2) >= 2048) S *= 2;
+    int64_t chunk = (V + S - 1) / S;
+    chunk = (chunk + 7) / 8 * 8;
+    const FiltWs w = filt_ws(workspace, B);
+    Partial *part = static_cast<Partial *>(workspace);
+    const dim3 gs((unsigned)S, (unsigned)B), gr((unsigned)B);
+    filt_soft_kernel<DT><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, seen, words, chunk, nullptr, w.soft);
+    filt_row_kernel<<<gr, 64, 0, s>>>(w.row, w.soft, S, 0);
+    const bool topk = p.top_k > 0 && p.top_k < V;
+    if (topk) {  // count threshold
+        for (int lvl = 0; lvl < 3; ++lvl) {
+            filt_hist_kernel<DT, false><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, seen, words, chunk, w.row,
+                                                                     lvl, w.hist);
+            filt_select_kernel<<<gr, kFiltThreads, 0, s>>>(w.row, w.hist, S, lvl, (float)p.top_k);
+        }
+    }
+    if (p.top_p < 1.0f) {  // mass threshold, renormalised over the top-k survivors
+        if (topk) {
+            filt_soft_kernel<DT><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, seen, words, chunk, w.row, w.soft);
+            filt_row_kernel<<<gr, 64, 0, s>>>(w.row, w.soft, S, 1);
+        }
+        for (int lvl = 0; lvl < 3; ++lvl) {
+            filt_hist_kernel<DT, true><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, seen, words, chunk, w.row,
+                                                                    lvl, w.hist);
+            filt_select_kernel<<<gr, kFiltThreads, 0, s>>>(w.row, w.hist, S, lvl, p.top_p);
+        }
+    }
+    filt_draw_kernel<DT><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, rng, step, seen, words, chunk, w.row, part,
+                                                      scores_out);
+    return S;
+}
+
 }  // namespace
 }  // namespace swh
 
 using namespace swh;
 
 extern "C" int64_t swh_sample_workspace_bytes(int64_t B, int64_t V) {
-    (void)V;
-    return B * kMaxSplit * (int64_t)sizeof(Partial);
+    (void)V;  // [split partials | filtered rows: state, (max, sum) partials, digit histograms]
+    return B * kMaxSplit * (int64_t)sizeof(Partial) + B * (int64_t)sizeof(FiltRow) +
+           B * kFiltSplit * (int64_t)sizeof(float2) + B * kFiltSplit * kBins * (int64_t)sizeof(float);
 }
 
 extern "C" int swh_sample_step(const void *logits, int dtype, int64_t B, int64_t V, int64_t ld,
@@ -393,9 +532,7 @@ extern "C" int swh_sample_step(const void *logits, int dtype, int64_t B, int64_t
     do {                                                                                                        \
         const TY *lg = static_cast<const TY *>(logits);                                                         \
         if (filtered) {                                                                                         \
-            sample_filtered_kernel<DTC><<<dim3((unsigned)B), dim3(kFiltThreads), 0, s>>>(lg, V, ld, p, rng, step, \
-                                                                                        seen, words, part,       \
-                                                                                        scores_out);            \
+            S = launch_filtered<DTC>(lg, B, V, ld, p, rng, step, seen, words, workspace, scores_out, s);         \
         } else {                                                                                                \
             S = choose_split(B, V);                                                                             \
             int64_t chunk = (V + S - 1) / S;                                                                    \
