@@ -86,7 +86,9 @@ int swh_logp_bwd(const void *logits, int dtype, int64_t rows_outer, int64_t rows
  *   out_logp    f32 [B, out_ld] or NULL: log-prob of the drawn token under the
  *               processed distribution (the PPO rollout log-prob, utils.py:1094)
  *   scores_out  f32 [B, V] or NULL: processed scores (HF output_scores)
- *   workspace   >= swh_sample_workspace_bytes(B, V) bytes                   */
+ *   workspace   >= swh_sample_workspace_bytes(B, V) bytes: split partials, and
+ *               for filtered rows their threshold state and per-split digit
+ *               histograms (the filtered path is several launches on `stream`) */
 typedef struct {
     float temperature;        /* 1.0 = off */
     float top_p;              /* 1.0 = off */
