@@ -851,8 +851,12 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
         }
     }
     SWH_GEMM_TRACE(5);
-    if constexpr (SAMPLE) {  // best over the 16 column lanes, one partial per (row, wave)
-        const int pq = wg * NW + wid;
+    if constexpr (SAMPLE) {
+        // best over the 16 column lanes per wave, then over the workgroup's waves
+        // through LDS (the X image is free once every wave is past its tiles):
+        // one partial per (row, workgroup) for the finalize
+        LmPart *wpart = reinterpret_cast<LmPart *>(xs);  // [NW][64]
+        __syncthreads();
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -868,9 +872,17 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
                         c = c2;
                     }
                 }
-                const int row = m0 + i * 16 + 4 * g + e;
-                if (rl == 0 && row < M) smp.part[(int64_t)row * smp.pstride + pq] = LmPart{k, c};
+                if (rl == 0) wpart[wid * 64 + i * 16 + 4 * g + e] = LmPart{k, c};
             }
+        __syncthreads();
+        if (tid < 64 && m0 + tid < M) {
+            LmPart bpart = wpart[tid];
+            for (int q = 1; q < NW; ++q) {
+                const LmPart o = wpart[q * 64 + tid];
+                if (o.key > bpart.key || (o.key == bpart.key && (uint32_t)o.idx < (uint32_t)bpart.idx)) bpart = o;
+            }
+            smp.part[(int64_t)(m0 + tid) * smp.pstride + wg] = bpart;
+        }
     }
     SWH_GEMM_TRACE(6);
 }
@@ -1604,7 +1616,7 @@ static int lm_head_sample_impl(const void *x, const void *w, int64_t M, int64_t 
     const int nm = norm_w ? 1 : (ss_in ? 2 : 0);
     const GemmLds L = gemm_lds(1, 64, 8, (int)K, (int)K, nm, false);
     const dim3 grid((unsigned)(per * nmt));
-    LmSample smp{p, rng, step, static_cast<LmPart *>(workspace), (int)(per * 8)};
+    LmSample smp{p, rng, step, static_cast<LmPart *>(workspace), (int)per};  // one partial per (row, workgroup)
     const auto *X = static_cast<const uint16_t *>(x);
     const auto *W = static_cast<const uint16_t *>(w);
     const auto *NWt = static_cast<const uint16_t *>(norm_w);
