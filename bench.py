@@ -82,7 +82,7 @@ def cpu_baseline(steps_note: str) -> dict:
                        f"{G} samples; {steps_note}")}
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r1_v5_pmc_decode.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r1_v7_pmc_decode.json")
 
 
 def pmc_traffic(kernel: str):
