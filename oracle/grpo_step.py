@@ -101,7 +101,7 @@ def grpo_step(model, optimizer, prompt_ids, prompt_mask, reward_fn: Callable, *,
                                     epsilon_low=epsilon, epsilon_high=epsilon_high or epsilon, loss_type=loss_type,
                                     importance_sampling_level=importance_sampling_level, max_completion_length=C)
         (loss / GA).backward()
-        losses.append(float(loss) / GA)
+        losses.append(float(loss.detach()) / GA)
         grads_of_logps.append(lp.grad)
     total = torch.nn.utils.clip_grad_norm_(model.parameters(), max_grad_norm)
     optimizer.step()
