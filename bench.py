@@ -14,12 +14,19 @@ grad-norm clip and AdamW.  Weak scaling: per-GPU work is fixed as N grows.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+`--gpus N` without torchrun's environment: this process never touches the
+GPU; it starts `torch.distributed.run` with N ranks (one per GPU, RCCL) as a
+child and exits with its status.  Under torchrun, N must equal WORLD_SIZE.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -47,10 +54,21 @@ def make_dataset(n: int, V: int):
     return [{"prompt": None, "prompt_ids": ids[i].tolist()} for i in range(n)]
 
 
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
 def cpu_baseline(steps_note: str) -> dict:
-    """The oracle's CPU restatement of the reference GRPO step, on a bounded
-    sample of the same workload (1 prompt x G=8, P=128, C=32 instead of 256),
-    timed on the host cores; scaled to the full sample per token."""
+    """The oracle's CPU restatement of the reference GRPO step (SURVEY.md §8d:
+    reduced cfg2 = 1 prompt x G=8, P=128, C=256 at full length), timed on the
+    host cores and reported per sample; nothing is extrapolated."""
     from oracle import grpo_step as og
     from swh_trl_amd.engine.config import qwen2_5_0_5b
     threads = min(16, len(os.sched_getaffinity(0)))
@@ -65,21 +83,17 @@ def cpu_baseline(steps_note: str) -> dict:
     def reward(cids, cmask):
         return [len(set(r[m.bool()].tolist())) % 7 for r, m in zip(cids, cmask)]
 
-    cs = 32
     kw = dict(num_generations=G, per_device_train_batch_size=G, gradient_accumulation_steps=1, eos_token_id=EOS,
-              pad_token_id=PAD, min_new_tokens=cs)
-    og.grpo_step(model, opt, prompt[:, :16], pm[:, :16], reward, C=4, **dict(kw, min_new_tokens=4))  # warm-up
+              pad_token_id=PAD)
+    og.grpo_step(model, opt, prompt[:, :16], pm[:, :16], reward, C=4, min_new_tokens=4, **kw)  # warm-up
     tm = {}
     t0 = time.perf_counter()
-    og.grpo_step(model, opt, prompt, pm, reward, C=cs, timings=tm, **kw)
+    og.grpo_step(model, opt, prompt, pm, reward, C=C, min_new_tokens=C, timings=tm, **kw)
     wall = time.perf_counter() - t0
-    # scale: decode time ~ linear in generated tokens; update ~ linear in P + C tokens
-    full_s = tm["generate_s"] * (C / cs) + tm["update_s"] * ((P + C) / (P + cs))
-    return {"value": G / full_s, "unit": "samples/s", "cores": threads, "kind": "port",
+    return {"value": G / wall, "unit": "samples/s", "cores": threads, "kind": "port", "cpu": _cpu_model(),
             "sample": (f"oracle/grpo_step.py (CPU restatement, transformers Qwen2 bf16, torch {torch.__version__}) on "
-                       f"1 prompt x G={G}, P={P}, C={cs}: generate {tm['generate_s']:.2f}s + update "
-                       f"{tm['update_s']:.2f}s = {wall:.2f}s wall; scaled per token to C={C}: {full_s:.1f}s per "
-                       f"{G} samples; {steps_note}")}
+                       f"1 prompt x G={G}, P={P}, C={C} (full length): generate {tm['generate_s']:.2f}s + update "
+                       f"{tm['update_s']:.2f}s = {wall:.2f}s wall for {G} samples, {threads} threads; {steps_note}")}
 
 
 PMC_FILE = os.path.join(ROOT, "profiles", "r1_v7_pmc_decode.json")
@@ -98,6 +112,17 @@ def pmc_traffic(kernel: str):
         return None
 
 
+def _launch_ranks(n: int, argv: list) -> int:
+    """Start N ranks under torch.distributed.run (127.0.0.1 rendezvous) as a
+    child process; this parent has not initialised the GPU and never does."""
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -108,6 +133,8 @@ def main():
     ap.add_argument("--variant", choices=("default", "top_p", "greedy"), default="default",
                     help="SURVEY.md §8d cfg2 sampling variants: top_p 0.9, or greedy decoding")
     args = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_launch_ranks(args.gpus, sys.argv[1:]))
 
     from swh_trl_amd import dist as sd
     from swh_trl_amd import profiling
@@ -115,7 +142,10 @@ def main():
     from swh_trl_amd.trainer import GRPOConfig, GRPOTrainer
 
     rank, world, local = sd.init_from_env()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
+    ranks_seen = sd.world_info()[1]
     cfg = qwen2_5_0_5b()
     if args.layers:
         cfg.num_hidden_layers = args.layers
@@ -187,6 +217,7 @@ def main():
     t_roof_ms = 70.5
     line = {"metric": METRIC, "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": steps,
             "warmup": warm, "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak",
+            "ranks_seen": ranks_seen, "backend": sd.backend_name(),
             "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (uniform prompt ids seed 1234, random-init weights, dummy reward)",
             "config": {"workload": "configs[1]: Qwen2.5-0.5B GRPO bf16, group_size=8, 256-tok completions" +

@@ -216,11 +216,16 @@ int swh_finalize_clip(const float *partials, int64_t n_partials, float max_norm,
  *   g = grad * clip[1] (clip NULL => 1) ; p *= 1 - lr*wd ;
  *   m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2 ;
  *   p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
- * master/m/v f32 [N]; grad bf16/f32 [N]; model_out bf16 [N] or NULL
- * (refreshed low-precision weights); step_count >= 1. */
+ * master/m/v f32 [N]; grad bf16/f32 [N]; model_out [N] of model_dtype (bf16:
+ * the refreshed low-precision weights; f32: an fp32 model's own weights) or
+ * NULL; step_count >= 1.  no_decay int64 [2 n_no_decay] = sorted, disjoint
+ * [start, end) element ranges updated with weight_decay 0 (transformers
+ * Trainer.get_decay_parameter_names: biases and norm weights), each start/end
+ * a multiple of 4; NULL / 0 = decay everywhere. */
 int swh_adamw(float *master, float *exp_avg, float *exp_avg_sq, const void *grad, int grad_dtype,
-              void *model_out, int64_t N, float lr, float beta1, float beta2, float eps,
-              float weight_decay, int64_t step_count, const float *clip, void *stream);
+              void *model_out, int model_dtype, int64_t N, float lr, float beta1, float beta2, float eps,
+              float weight_decay, int64_t step_count, const float *clip, const int64_t *no_decay,
+              int32_t n_no_decay, void *stream);
 /* dst_f32[i] += src[i] (bf16/f32) — accumulate micro-batch grads in fp32. */
 int swh_accumulate(float *dst, const void *src, int dtype, int64_t N, float scale, void *stream);
 
@@ -228,25 +233,31 @@ int swh_accumulate(float *dst, const void *src, int dtype, int64_t N, float scal
  * The transformer the reference runs through transformers' Qwen2/Llama
  * modeling code (third-party); GEMMs stay on hipBLASLt (MFMA), everything
  * between GEMMs is here.  bf16 in/out, fp32 math, rounding points as the
- * transformers bf16 modules (RMSNorm casts before the weight multiply).   */
+ * transformers bf16 modules (RMSNorm casts before the weight multiply).
+ * The full-sequence kernels below that take `dtype` also run an fp32 model
+ * (dtype SWH_F32: every tensor argument f32, no intermediate rounding — the
+ * transformers fp32 modules); the decode kernels are bf16 only.            */
 /* y = bf16(w * bf16(s * rsqrt(mean(s^2) + eps))), s = x (+ residual), the sum
  * s also written to residual_out when residual is given; rstd f32 [rows]
  * nullable (saved for the backward). */
 int swh_rmsnorm_fwd(const void *x, const void *residual, void *residual_out, const void *weight,
-                    int64_t rows, int64_t H, float eps, void *y, float *rstd, void *stream);
+                    int64_t rows, int64_t H, float eps, void *y, float *rstd, int32_t dtype, void *stream);
 /* Backward: dx = rstd*(w*dy - n*mean(w*dy*n)), n = x*rstd; dw partial sums
  * f32 [ceil(rows/rows_per_block) x H] reduced by the caller. */
 int swh_rmsnorm_bwd(const void *x, const void *weight, const float *rstd, const void *dy, int64_t rows, int64_t H,
-                    void *dx, float *dw_partial, int64_t rows_per_block, const void *dres, void *stream);
+                    void *dx, float *dw_partial, int64_t rows_per_block, const void *dres, int32_t dtype,
+                    void *stream);
 /* dres (nullable, bf16 [rows, H]): the gradient arriving through the residual
  * branch; dx = bf16(bf16(norm backward) + dres), the sum autograd forms where
  * the residual stream forks into the next RMSNorm.  swh_rmsnorm_dw_accum folds
  * the partial weight-gradient column sums into the bf16 gradient view:
- * grad_w = bf16(grad_w + bf16(sum over blocks)). */
-int swh_rmsnorm_dw_accum(const float *dw_partial, int64_t nblocks, int64_t H, void *grad_w, void *stream);
+ * grad_w = bf16(grad_w + bf16(sum over blocks)) (f32: grad_w += sum). */
+int swh_rmsnorm_dw_accum(const float *dw_partial, int64_t nblocks, int64_t H, void *grad_w, int32_t dtype,
+                         void *stream);
 /* out[r, i] = bf16(bf16(silu(gu[r, i])) * gu[r, I + i]) — gate/up packed. */
-int swh_silu_mul_fwd(const void *gu, int64_t rows, int64_t I, void *out, void *stream);
-int swh_silu_mul_bwd(const void *gu, const void *dout, int64_t rows, int64_t I, void *dgu, void *stream);
+int swh_silu_mul_fwd(const void *gu, int64_t rows, int64_t I, void *out, int32_t dtype, void *stream);
+int swh_silu_mul_bwd(const void *gu, const void *dout, int64_t rows, int64_t I, void *dgu, int32_t dtype,
+                     void *stream);
 /* QKV split + rotate-half RoPE of the full-sequence forward (transformers
  * apply_rotary_pos_emb in bf16, with bf16-rounded cos/sin; the reference's
  * training / scoring forward, grpo_trainer.py:1249):
@@ -257,7 +268,7 @@ int swh_silu_mul_bwd(const void *gu, const void *dout, int64_t rows, int64_t I, 
  *            dx2 = bf16(bf16(dy2 c) - bf16(dy1 s))).  D % 16 == 0. */
 int swh_qkv_rope(void *qkv, const int64_t *positions, const float *rope_cos, const float *rope_sin, int64_t B,
                  int64_t L, int32_t Hq, int32_t Hkv, int32_t D, void *q, void *k, void *v, int32_t backward,
-                 void *stream);
+                 int32_t dtype, void *stream);
 /* Causal GQA attention over full sequences (training / scoring / prefill),
  * bf16 [B, H, L, D] tensors (D = 64 or 128), fp32 softmax statistics.
  * Forward writes out and lse [B, Hq, L] (natural log of the row sum of

@@ -73,8 +73,14 @@ def grpo_step(model, optimizer, prompt_ids, prompt_mask, reward_fn: Callable, *,
               per_device_train_batch_size: int, gradient_accumulation_steps: int, temperature=1.0,
               eos_token_id=None, pad_token_id=0, beta=0.0, epsilon=0.2, epsilon_high=None, loss_type="bnpo",
               importance_sampling_level="token", scale_rewards=True, max_grad_norm=1.0, do_sample=True,
-              min_new_tokens=0, perm: Optional[torch.Tensor] = None, completion_ids=None, timings=None):
-    """One optimizer step; returns (mean loss, dict of intermediates)."""
+              min_new_tokens=0, perm: Optional[torch.Tensor] = None, completion_ids=None, timings=None,
+              ref_model=None, capture: bool = False):
+    """One optimizer step; returns (mean loss, dict of intermediates).
+
+    ref_model (beta != 0): the frozen reference scored on the whole batch
+    before the shuffle (grpo_trainer.py:1871-1899).  capture=True adds the
+    per-token log-probs of every micro-batch ("logps", permuted row order),
+    the pre-clip gradients ("grads", name -> tensor) and the per-micro losses."""
     t0 = time.perf_counter()
     if completion_ids is None:
         completion_ids = generate(model, prompt_ids, prompt_mask, C, do_sample=do_sample, temperature=temperature,
@@ -86,9 +92,16 @@ def grpo_step(model, optimizer, prompt_ids, prompt_mask, reward_fn: Callable, *,
     rewards = torch.tensor([float(x) for x in reward_fn(completion_ids, mask)], dtype=torch.float32).view(-1, 1)
     adv, _, _, _, _ = trl_ref.group_advantages(rewards, torch.ones(1), num_generations, scale_rewards)
     B = completion_ids.shape[0]
+    ref_lp = None
+    if beta != 0.0:
+        if ref_model is None:
+            raise ValueError("beta != 0 needs ref_model")
+        with torch.no_grad():
+            ref_lp, _ = per_token_logps(ref_model, prompt_ids, prompt_mask, completion_ids, mask, temperature,
+                                        compute_entropy=False)
     perm = torch.arange(B) if perm is None else perm
     data = {"p": prompt_ids[perm], "pm": prompt_mask[perm], "c": completion_ids[perm], "cm": mask[perm],
-            "a": adv[perm]}
+            "a": adv[perm], "r": None if ref_lp is None else ref_lp[perm]}
     spg = B // per_device_train_batch_size
     GA = gradient_accumulation_steps
     losses = []
@@ -97,12 +110,16 @@ def grpo_step(model, optimizer, prompt_ids, prompt_mask, reward_fn: Callable, *,
         sl = slice(j * per_device_train_batch_size, (j + 1) * per_device_train_batch_size)
         lp, ent = per_token_logps(model, data["p"][sl], data["pm"][sl], data["c"][sl], data["cm"][sl], temperature)
         lp.retain_grad()
-        loss, _ = trl_ref.grpo_loss(lp, data["a"][sl], data["cm"][sl], entropies=ent, beta=beta,
+        loss, _ = trl_ref.grpo_loss(lp, data["a"][sl], data["cm"][sl],
+                                    ref_per_token_logps=None if data["r"] is None else data["r"][sl],
+                                    entropies=ent, beta=beta,
                                     epsilon_low=epsilon, epsilon_high=epsilon_high or epsilon, loss_type=loss_type,
                                     importance_sampling_level=importance_sampling_level, max_completion_length=C)
         (loss / GA).backward()
         losses.append(float(loss.detach()) / GA)
-        grads_of_logps.append(lp.grad)
+        grads_of_logps.append(lp.detach())
+    grads = ({n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
+             if capture else None)
     total = torch.nn.utils.clip_grad_norm_(model.parameters(), max_grad_norm)
     optimizer.step()
     optimizer.zero_grad()
@@ -110,5 +127,8 @@ def grpo_step(model, optimizer, prompt_ids, prompt_mask, reward_fn: Callable, *,
     if timings is not None:
         timings["generate_s"] = t1 - t0
         timings["update_s"] = t2 - t1
-    return sum(losses), {"completion_ids": completion_ids, "completion_mask": mask, "advantages": adv,
-                         "grad_norm": float(total), "perm": perm}
+    out = {"completion_ids": completion_ids, "completion_mask": mask, "advantages": adv, "rewards": rewards,
+           "grad_norm": float(total), "perm": perm}
+    if capture:
+        out.update(logps=torch.cat(grads_of_logps), grads=grads, losses=losses)
+    return sum(losses), out

@@ -94,17 +94,24 @@ def truncate_response(stop_token_id: int, pad_token_id: int, responses: torch.Te
     return responses.masked_fill(pos > first, pad_token_id)
 
 
-def pad(tensors: Sequence[torch.Tensor], padding_value: int = 0, padding_side: str = "right") -> torch.Tensor:
-    """trl/trainer/utils.py:245-308 — stack ragged tensors into one padded tensor."""
-    shape = [len(tensors)] + [max(t.shape[d] for t in tensors) for d in range(tensors[0].dim())]
-    out = torch.full(shape, padding_value, dtype=tensors[0].dtype)
+def pad(tensors: Sequence[torch.Tensor], padding_value: int = 0, padding_side: str = "right",
+        pad_to_multiple_of: Optional[int] = None) -> torch.Tensor:
+    """trl/trainer/utils.py:245-308 — stack ragged tensors into one padded tensor:
+    the output shape is the per-dim max (:284), the first dim rounded up to
+    pad_to_multiple_of (:287-290); `padding_side` places each tensor along the
+    FIRST dim only, the trailing dims always start at 0 (:296-305)."""
+    shape = [max(t.shape[d] for t in tensors) for d in range(tensors[0].dim())]
+    if pad_to_multiple_of is not None and shape[0] % pad_to_multiple_of:
+        shape[0] += pad_to_multiple_of - shape[0] % pad_to_multiple_of
+    out = torch.full([len(tensors)] + shape, padding_value, dtype=tensors[0].dtype)
     for i, t in enumerate(tensors):
         if padding_side == "left":
-            sl = tuple(slice(s - t.shape[d], s) for d, s in enumerate(shape[1:]))
+            start = shape[0] - t.shape[0]
         elif padding_side == "right":
-            sl = tuple(slice(0, t.shape[d]) for d in range(t.dim()))
+            start = 0
         else:
             raise ValueError("padding_side must be 'left' or 'right'")
+        sl = (slice(start, start + t.shape[0]),) + tuple(slice(0, s) for s in t.shape[1:])
         out[(i,) + sl] = t
     return out
 

@@ -14,6 +14,8 @@ run() {  # name timeout cmd...
 for step in "$@"; do
   case $step in
     gpu) run gpu 1100 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
+    gpuall) run gpuall 1100 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread ;;
+    newt) run newt 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread -k "step_parity or adamw or bench_launches or masked_whiten" ;;
     tune) SWH_GEMM_TUNING=tune SWH_GEMM_TABLE=gpurun_out/gemm_tuned.csv run tune 900 python bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
     benchtuned) SWH_GEMM_TABLE=gpurun_out/gemm_tuned.csv run benchtuned 600 python bench.py --steps 3 --warmup 2 --no-cpu-baseline ;;
     lmk) run lmk 300 python -u -m pytest tests/test_kernels_gpu.py -x -v -m gpu -k "lm_head or decode_gemm or sampler" --timeout 120 --timeout-method thread ;;

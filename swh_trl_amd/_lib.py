@@ -63,14 +63,14 @@ SIGNATURES = {
     "swh_sqnorm_partials": (c_i64, [c_i64]),
     "swh_grad_sqnorm": (c_i32, [c_vp, c_i32, c_i64, c_vp, c_vp]),
     "swh_finalize_clip": (c_i32, [c_vp, c_i64, c_f32, c_vp, c_vp]),
-    "swh_adamw": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32,
-                          c_i64, c_vp, c_vp]),
+    "swh_adamw": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32,
+                          c_i64, c_vp, c_vp, c_i32, c_vp]),
     "swh_accumulate": (c_i32, [c_vp, c_vp, c_i32, c_i64, c_f32, c_vp]),
-    "swh_rmsnorm_fwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_vp, c_vp, c_vp]),
-    "swh_rmsnorm_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
-    "swh_rmsnorm_dw_accum": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp]),
-    "swh_silu_mul_fwd": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp]),
-    "swh_silu_mul_bwd": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "swh_rmsnorm_fwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_vp, c_vp, c_i32, c_vp]),
+    "swh_rmsnorm_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp]),
+    "swh_rmsnorm_dw_accum": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_vp]),
+    "swh_silu_mul_fwd": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_vp]),
+    "swh_silu_mul_bwd": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i32, c_vp]),
     "swh_attn_fwd": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "swh_attn_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i64, c_i32, c_f32, c_vp, c_vp,
                              c_vp, c_vp, c_vp, c_vp, c_vp]),
@@ -79,7 +79,7 @@ SIGNATURES = {
     "swh_fold_norm": (c_i32, [c_vp, c_i32, c_i64, c_vp]),
     "swh_embed_gather": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "swh_qkv_rope": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i32,
-                             c_vp]),
+                             c_i32, c_vp]),
     "swh_attn_decode": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32,
                                 c_f32, c_vp, c_vp]),
     "swh_attn_decode_prefetch": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32,

@@ -414,15 +414,141 @@ __global__ __launch_bounds__(256) void qkv_rope_kernel(uint16_t *__restrict__ qk
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// fp32 variants (reference-precision mode: an fp32 model, as transformers runs
+// one loaded with torch_dtype=float32).  No intermediate rounding; the
+// formulas are the fp32 modules': y = w * (s * rsqrt(mean(s^2) + eps)),
+// silu(g) * u, x*cos + rotate_half(x)*sin.  One element per lane, one wave
+// per row for the norms (16-B vectors are not needed at these sizes).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rmsnorm_fwd_f32_kernel(const float *__restrict__ x, const float *__restrict__ res,
+                                                              float *__restrict__ res_out, const float *__restrict__ w,
+                                                              int64_t rows, int64_t H, float eps, float *__restrict__ y,
+                                                              float *__restrict__ rstd_out) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= rows) return;
+    float ss = 0.f;
+    for (int64_t h = lane; h < H; h += 64) {
+        float a = x[r * H + h];
+        if (res) {
+            a += res[r * H + h];
+            if (res_out) res_out[r * H + h] = a;
+        }
+        ss = fmaf(a, a, ss);
+    }
+    ss = wave_sum(ss);
+    const float rs = rsqrtf(ss / (float)H + eps);
+    if (lane == 0 && rstd_out) rstd_out[r] = rs;
+    for (int64_t h = lane; h < H; h += 64) {
+        const float a = res ? x[r * H + h] + res[r * H + h] : x[r * H + h];
+        y[r * H + h] = w[h] * (a * rs);
+    }
+}
+
+// a workgroup = 4 waves over rows r0 .. r0 + rpb (a wave per row at a time);
+// each wave keeps its dw column sums in its own LDS row, summed per block at the end
+__global__ __launch_bounds__(256) void rmsnorm_bwd_f32_kernel(const float *__restrict__ x, const float *__restrict__ w,
+                                                              const float *__restrict__ rstd, const float *__restrict__ dy,
+                                                              int64_t rows, int64_t H, float *__restrict__ dx,
+                                                              float *__restrict__ dw_part, int64_t rpb,
+                                                              const float *__restrict__ dres) {
+    extern __shared__ float dws[];  // [4][H]
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int64_t h = lane; h < H; h += 64) dws[wid * H + h] = 0.f;
+    const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+    for (int64_t r = r0 + wid; r < r1; r += 4) {
+        const float rs = rstd[r];
+        float c = 0.f;
+        for (int64_t h = lane; h < H; h += 64) c = fmaf(dy[r * H + h] * w[h], x[r * H + h] * rs, c);
+        c = wave_sum(c) / (float)H;
+        for (int64_t h = lane; h < H; h += 64) {
+            const float n = x[r * H + h] * rs, g = dy[r * H + h];
+            dws[wid * H + h] = fmaf(g, n, dws[wid * H + h]);
+            float d = rs * (g * w[h] - n * c);
+            if (dres) d += dres[r * H + h];
+            dx[r * H + h] = d;
+        }
+    }
+    __syncthreads();
+    for (int64_t h = threadIdx.x; h < H; h += 256)
+        dw_part[(int64_t)blockIdx.x * H + h] = ((dws[h] + dws[H + h]) + dws[2 * H + h]) + dws[3 * H + h];
+}
+
+__global__ __launch_bounds__(256) void silu_mul_f32_kernel(const float *__restrict__ gu, const float *__restrict__ dout,
+                                                           int64_t rows, int64_t I, float *__restrict__ out) {
+    const int64_t total = rows * I;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = idx / I, i = idx - r * I;
+        const float g = gu[r * 2 * I + i], u = gu[r * 2 * I + I + i];
+        const float sg = 1.f / (1.f + expf(-g));
+        if (!dout) {
+            out[idx] = (g * sg) * u;
+        } else {  // out = d gu [rows, 2I]
+            const float d = dout[idx];
+            out[r * 2 * I + i] = (d * u) * (sg * (1.f + g * (1.f - sg)));
+            out[r * 2 * I + I + i] = d * (g * sg);
+        }
+    }
+}
+
+template <bool BWD>
+__global__ __launch_bounds__(256) void qkv_rope_f32_kernel(float *__restrict__ qkv, const int64_t *__restrict__ pos,
+                                                           const float *__restrict__ rc, const float *__restrict__ rsn,
+                                                           int64_t R, int L, int Hq, int Hkv, int D,
+                                                           float *__restrict__ q, float *__restrict__ k,
+                                                           float *__restrict__ v) {
+    const int HD = D / 2, H3 = Hq + 2 * Hkv;
+    const int64_t total = R * H3 * HD;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int i = (int)(idx % HD);
+        const int h = (int)((idx / HD) % H3);
+        const int64_t r = idx / ((int64_t)HD * H3);
+        const int64_t b = r / L, l = r - b * L;
+        float *src = qkv + r * (int64_t)H3 * D + (int64_t)h * D;
+        float *dst;
+        if (h < Hq) dst = q + ((b * Hq + h) * (int64_t)L + l) * D;
+        else if (h < Hq + Hkv) dst = k + ((b * Hkv + (h - Hq)) * (int64_t)L + l) * D;
+        else dst = v + ((b * Hkv + (h - Hq - Hkv)) * (int64_t)L + l) * D;
+        float *o = BWD ? src : dst;
+        const float *in = BWD ? dst : src;
+        const float x1 = in[i], x2 = in[i + HD];
+        if (h >= Hq + Hkv) {
+            o[i] = x1;
+            o[i + HD] = x2;
+            continue;
+        }
+        const int64_t p = pos[r] < 0 ? 0 : pos[r];
+        const float c = rc[p * HD + i], s = rsn[p * HD + i];
+        if (!BWD) {
+            o[i] = x1 * c + (-x2) * s;
+            o[i + HD] = x2 * c + x1 * s;
+        } else {
+            o[i] = x1 * c + x2 * s;
+            o[i + HD] = x2 * c - x1 * s;
+        }
+    }
+}
+
 }  // namespace
 }  // namespace swh
 
 using namespace swh;
 
 extern "C" int swh_rmsnorm_fwd(const void *x, const void *residual, void *residual_out, const void *weight,
-                               int64_t rows, int64_t H, float eps, void *y, float *rstd, void *stream) {
+                               int64_t rows, int64_t H, float eps, void *y, float *rstd, int32_t dtype, void *stream) {
     if (!x || !weight || !y || rows < 0 || H <= 0 || H % 8) return SWH_E_ARG;
+    if (dtype != SWH_BF16 && dtype != SWH_F32) return SWH_E_DTYPE;
     if (rows == 0) return SWH_OK;
+    if (dtype == SWH_F32) {
+        rmsnorm_fwd_f32_kernel<<<dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, static_cast<hipStream_t>(stream)>>>(
+            static_cast<const float *>(x), static_cast<const float *>(residual), static_cast<float *>(residual_out),
+            static_cast<const float *>(weight), rows, H, eps, static_cast<float *>(y), rstd);
+        return launch_status();
+    }
     rmsnorm_fwd_kernel<<<dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, static_cast<hipStream_t>(stream)>>>(
         static_cast<const uint16_t *>(x), static_cast<const uint16_t *>(residual), static_cast<uint16_t *>(residual_out),
         static_cast<const uint16_t *>(weight), rows, H, eps, static_cast<uint16_t *>(y), rstd);
@@ -434,8 +560,9 @@ extern "C" int swh_rmsnorm_fwd(const void *x, const void *residual, void *residu
 // a workgroup = 64 columns x 16 row slices: slice s sums partial rows s, s + 16, ...
 // (loads issued 8 at a time), then the 16 slice sums add in fixed order through LDS
 constexpr int kDwSlices = 16;
+template <int DT>
 __global__ __launch_bounds__(64 * kDwSlices) void rmsnorm_dw_accum_kernel(const float *__restrict__ part, int64_t nb,
-                                                                         int64_t H, uint16_t *__restrict__ gw) {
+                                                                         int64_t H, typename Elem<DT>::T *__restrict__ gw) {
     __shared__ float red[kDwSlices][64];
     const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
     const int64_t h = (int64_t)blockIdx.x * 64 + c;
@@ -457,25 +584,42 @@ __global__ __launch_bounds__(64 * kDwSlices) void rmsnorm_dw_accum_kernel(const 
         float u = 0.f;
 #pragma unroll
         for (int q = 0; q < kDwSlices; ++q) u += red[q][c];
-        gw[h] = f32_to_bf16_bits(bf16_bits_to_f32(gw[h]) + round_bf16(u));
+        if constexpr (DT == SWH_F32) gw[h] += u;
+        else gw[h] = f32_to_bf16_bits(bf16_bits_to_f32(gw[h]) + round_bf16(u));
     }
 }
 
-extern "C" int swh_rmsnorm_dw_accum(const float *dw_partial, int64_t nblocks, int64_t H, void *grad_w, void *stream) {
+extern "C" int swh_rmsnorm_dw_accum(const float *dw_partial, int64_t nblocks, int64_t H, void *grad_w, int32_t dtype,
+                                    void *stream) {
     if (!dw_partial || !grad_w || nblocks <= 0 || H <= 0) return SWH_E_ARG;
-    rmsnorm_dw_accum_kernel<<<dim3((unsigned)((H + 63) / 64)), 64 * kDwSlices, 0, static_cast<hipStream_t>(stream)>>>(
-        dw_partial, nblocks, H, static_cast<uint16_t *>(grad_w));
+    const dim3 grid((unsigned)((H + 63) / 64));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (dtype == SWH_BF16)
+        rmsnorm_dw_accum_kernel<SWH_BF16><<<grid, 64 * kDwSlices, 0, st>>>(dw_partial, nblocks, H,
+                                                                         static_cast<uint16_t *>(grad_w));
+    else if (dtype == SWH_F32)
+        rmsnorm_dw_accum_kernel<SWH_F32><<<grid, 64 * kDwSlices, 0, st>>>(dw_partial, nblocks, H,
+                                                                        static_cast<float *>(grad_w));
+    else
+        return SWH_E_DTYPE;
     return launch_status();
 }
 
 extern "C" int swh_rmsnorm_bwd(const void *x, const void *weight, const float *rstd, const void *dy, int64_t rows,
                                int64_t H, void *dx, float *dw_partial, int64_t rows_per_block, const void *dres,
-                               void *stream) {
+                               int32_t dtype, void *stream) {
     if (!x || !weight || !rstd || !dy || !dx || !dw_partial || rows < 0 || H <= 0 || H % 8 ||
         H > 64 * 8 * kNormBwdVec || rows_per_block <= 0 || rows_per_block > 4096)
         return SWH_E_ARG;
+    if (dtype != SWH_BF16 && dtype != SWH_F32) return SWH_E_DTYPE;
     if (rows == 0) return SWH_OK;
     const unsigned nb = (unsigned)((rows + rows_per_block - 1) / rows_per_block);
+    if (dtype == SWH_F32) {
+        rmsnorm_bwd_f32_kernel<<<dim3(nb), dim3(256), 4 * H * sizeof(float), static_cast<hipStream_t>(stream)>>>(
+            static_cast<const float *>(x), static_cast<const float *>(weight), rstd, static_cast<const float *>(dy),
+            rows, H, static_cast<float *>(dx), dw_partial, rows_per_block, static_cast<const float *>(dres));
+        return launch_status();
+    }
     const size_t lds = (kNormBwdThreads / 64) * H * sizeof(float);
     hipStream_t st = static_cast<hipStream_t>(stream);
     const auto *X = static_cast<const uint16_t *>(x), *Wt = static_cast<const uint16_t *>(weight);
@@ -497,17 +641,30 @@ static unsigned ew_grid(int64_t work) {
     return (unsigned)(g < 1 ? 1 : g);
 }
 
-extern "C" int swh_silu_mul_fwd(const void *gu, int64_t rows, int64_t I, void *out, void *stream) {
+extern "C" int swh_silu_mul_fwd(const void *gu, int64_t rows, int64_t I, void *out, int32_t dtype, void *stream) {
     if (!gu || !out || rows < 0 || I <= 0 || I % 8) return SWH_E_ARG;
+    if (dtype != SWH_BF16 && dtype != SWH_F32) return SWH_E_DTYPE;
     if (rows == 0) return SWH_OK;
+    if (dtype == SWH_F32) {
+        silu_mul_f32_kernel<<<ew_grid(rows * I), 256, 0, static_cast<hipStream_t>(stream)>>>(
+            static_cast<const float *>(gu), nullptr, rows, I, static_cast<float *>(out));
+        return launch_status();
+    }
     silu_mul_fwd_kernel<<<ew_grid(rows * I / 8), 256, 0, static_cast<hipStream_t>(stream)>>>(
         static_cast<const uint16_t *>(gu), rows, I, static_cast<uint16_t *>(out));
     return launch_status();
 }
 
-extern "C" int swh_silu_mul_bwd(const void *gu, const void *dout, int64_t rows, int64_t I, void *dgu, void *stream) {
+extern "C" int swh_silu_mul_bwd(const void *gu, const void *dout, int64_t rows, int64_t I, void *dgu, int32_t dtype,
+                                void *stream) {
     if (!gu || !dout || !dgu || rows < 0 || I <= 0 || I % 8) return SWH_E_ARG;
+    if (dtype != SWH_BF16 && dtype != SWH_F32) return SWH_E_DTYPE;
     if (rows == 0) return SWH_OK;
+    if (dtype == SWH_F32) {
+        silu_mul_f32_kernel<<<ew_grid(rows * I), 256, 0, static_cast<hipStream_t>(stream)>>>(
+            static_cast<const float *>(gu), static_cast<const float *>(dout), rows, I, static_cast<float *>(dgu));
+        return launch_status();
+    }
     silu_mul_bwd_kernel<<<ew_grid(rows * I / 8), 256, 0, static_cast<hipStream_t>(stream)>>>(
         static_cast<const uint16_t *>(gu), static_cast<const uint16_t *>(dout), rows, I, static_cast<uint16_t *>(dgu));
     return launch_status();
@@ -533,12 +690,26 @@ extern "C" int swh_embed_gather(const void *table, const int64_t *ids, int64_t B
 
 extern "C" int swh_qkv_rope(void *qkv, const int64_t *positions, const float *rope_cos, const float *rope_sin,
                             int64_t B, int64_t L, int32_t Hq, int32_t Hkv, int32_t D, void *q, void *k, void *v,
-                            int32_t backward, void *stream) {
+                            int32_t backward, int32_t dtype, void *stream) {
     if (!qkv || !positions || !rope_cos || !rope_sin || !q || !k || !v || B < 0 || L < 0 || Hq <= 0 || Hkv <= 0 ||
         D <= 0 || D % 16)
         return SWH_E_ARG;
+    if (dtype != SWH_BF16 && dtype != SWH_F32) return SWH_E_DTYPE;
     const int64_t R = B * L;
     if (R == 0) return SWH_OK;
+    if (dtype == SWH_F32) {
+        int64_t g = (R * (Hq + 2 * Hkv) * (D / 2) + 255) / 256;
+        if (g > 256 * 32) g = 256 * 32;
+        auto *Qf = static_cast<float *>(q), *Kf = static_cast<float *>(k), *Vf = static_cast<float *>(v);
+        auto *X = static_cast<float *>(qkv);
+        if (backward)
+            qkv_rope_f32_kernel<true><<<dim3((unsigned)g), 256, 0, static_cast<hipStream_t>(stream)>>>(
+                X, positions, rope_cos, rope_sin, R, (int)L, Hq, Hkv, D, Qf, Kf, Vf);
+        else
+            qkv_rope_f32_kernel<false><<<dim3((unsigned)g), 256, 0, static_cast<hipStream_t>(stream)>>>(
+                X, positions, rope_cos, rope_sin, R, (int)L, Hq, Hkv, D, Qf, Kf, Vf);
+        return launch_status();
+    }
     const int64_t work = R * (Hq + 2 * Hkv) * (D / 16);
     int64_t grid = (work + 255) / 256;
     if (grid > 256 * 32) grid = 256 * 32;

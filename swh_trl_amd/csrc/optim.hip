@@ -43,17 +43,45 @@ __global__ __launch_bounds__(kThreads) void finalize_clip_kernel(const float *__
     }
 }
 
-template <int GDT, bool WRITE_MODEL>
+constexpr int kMaxNoDecay = 1024;  // no-decay ranges held in LDS
+
+// WM: 0 = no model copy, SWH_BF16 = bf16 copy, SWH_F32 = fp32 copy.  NR: the
+// no-decay range table is consulted (binary search in LDS per float4 group;
+// ranges are 4-aligned so a group never straddles one).
+template <int GDT, int WM, bool NR>
 __global__ __launch_bounds__(kThreads) void adamw_kernel(float *__restrict__ p, float *__restrict__ m,
                                                          float *__restrict__ v,
                                                          const typename Elem<GDT>::T *__restrict__ g,
-                                                         uint16_t *__restrict__ model, int64_t N, float lr,
+                                                         void *__restrict__ model_v, int64_t N, float lr,
                                                          float b1, float b2, float eps, float wd, float step_size,
-                                                         float bc2_sqrt, const float *__restrict__ clip) {
+                                                         float bc2_sqrt, const float *__restrict__ clip,
+                                                         const int64_t *__restrict__ nd, int nnd) {
+    __shared__ int64_t tab[NR ? 2 * kMaxNoDecay : 1];
+    if constexpr (NR) {
+        for (int i = threadIdx.x; i < 2 * nnd; i += kThreads) tab[i] = nd[i];
+        __syncthreads();
+    }
     const float cf = clip ? clip[1] : 1.f;
-    const float decay = 1.f - lr * wd;
+    const float decay_on = 1.f - lr * wd;
+    // 1 - lr*wd, or 1 inside a no-decay range
+    auto decay_at = [&](int64_t e) {
+        if constexpr (!NR) {
+            return decay_on;
+        } else {
+            int lo = 0, hi = nnd - 1, hit = -1;
+            while (lo <= hi) {
+                const int mid = (lo + hi) >> 1;
+                if (tab[2 * mid] <= e) { hit = mid; lo = mid + 1; }
+                else hi = mid - 1;
+            }
+            return (hit >= 0 && e < tab[2 * hit + 1]) ? 1.f : decay_on;
+        }
+    };
+    uint16_t *model = static_cast<uint16_t *>(model_v);
+    float *model32 = static_cast<float *>(model_v);
     const int64_t n4 = N / 4;
     const int64_t stride = (int64_t)gridDim.x * kThreads;
+    float decay = decay_on;
     auto upd = [&](float &pp, float &mm, float &vv, float gg) {
         gg *= cf;
         pp *= decay;
@@ -90,6 +118,7 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float *__restrict__ p, 
         for (int u = 0; u < U; ++u) {
             const int64_t i = i0 + u * stride;
             if (i >= n4) break;
+            decay = decay_at(4 * i);
             upd(pp[u].x, mm[u].x, vv[u].x, gg[u][0]);
             upd(pp[u].y, mm[u].y, vv[u].y, gg[u][1]);
             upd(pp[u].z, mm[u].z, vv[u].z, gg[u][2]);
@@ -97,7 +126,8 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float *__restrict__ p, 
             reinterpret_cast<float4 *>(p)[i] = pp[u];
             reinterpret_cast<float4 *>(m)[i] = mm[u];
             reinterpret_cast<float4 *>(v)[i] = vv[u];
-            if constexpr (WRITE_MODEL) {
+            if constexpr (WM == SWH_F32) reinterpret_cast<float4 *>(model32)[i] = pp[u];
+            if constexpr (WM == SWH_BF16) {
                 const uint32_t lo = (uint32_t)f32_to_bf16_bits(pp[u].x) | ((uint32_t)f32_to_bf16_bits(pp[u].y) << 16);
                 const uint32_t hi = (uint32_t)f32_to_bf16_bits(pp[u].z) | ((uint32_t)f32_to_bf16_bits(pp[u].w) << 16);
                 reinterpret_cast<uint2 *>(model)[i] = uint2{lo, hi};
@@ -106,11 +136,13 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float *__restrict__ p, 
     }
     for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * kThreads + threadIdx.x; i < N; i += stride) {
         float pp = p[i], mm = m[i], vv = v[i];
+        decay = decay_at(i);
         upd(pp, mm, vv, Elem<GDT>::load(g + i));
         p[i] = pp;
         m[i] = mm;
         v[i] = vv;
-        if constexpr (WRITE_MODEL) model[i] = f32_to_bf16_bits(pp);
+        if constexpr (WM == SWH_BF16) model[i] = f32_to_bf16_bits(pp);
+        if constexpr (WM == SWH_F32) model32[i] = pp;
     }
 }
 
@@ -162,31 +194,44 @@ extern "C" int swh_finalize_clip(const float *partials, int64_t n_partials, floa
 }
 
 extern "C" int swh_adamw(float *master, float *exp_avg, float *exp_avg_sq, const void *grad, int grad_dtype,
-                         void *model_out, int64_t N, float lr, float beta1, float beta2, float eps,
-                         float weight_decay, int64_t step_count, const float *clip, void *stream) {
+                         void *model_out, int model_dtype, int64_t N, float lr, float beta1, float beta2, float eps,
+                         float weight_decay, int64_t step_count, const float *clip, const int64_t *no_decay,
+                         int32_t n_no_decay, void *stream) {
     if (!master || !exp_avg || !exp_avg_sq || !grad || N < 0 || step_count < 1) return SWH_E_ARG;
     if (((uintptr_t)master | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) & 15) return SWH_E_ARG;
+    if (n_no_decay < 0 || n_no_decay > kMaxNoDecay || (n_no_decay > 0 && !no_decay)) return SWH_E_ARG;
+    if (model_out && model_dtype != SWH_BF16 && model_dtype != SWH_F32) return SWH_E_DTYPE;
+    if (grad_dtype != SWH_BF16 && grad_dtype != SWH_F32) return SWH_E_DTYPE;
     if (N == 0) return SWH_OK;
+    if ((uintptr_t)grad & (grad_dtype == SWH_BF16 ? 7 : 15)) return SWH_E_ARG;
+    if (model_out && ((uintptr_t)model_out & (model_dtype == SWH_BF16 ? 7 : 15))) return SWH_E_ARG;
     const double bc1 = 1.0 - pow((double)beta1, (double)step_count);
     const double bc2 = 1.0 - pow((double)beta2, (double)step_count);
     const float step_size = (float)(lr / bc1);
     const float bc2_sqrt = (float)sqrt(bc2);
     hipStream_t s = static_cast<hipStream_t>(stream);
     const unsigned nb = grid_for((N + 3) / 4);
-    uint16_t *mo = static_cast<uint16_t *>(model_out);
-    if (mo && ((uintptr_t)mo & 7)) return SWH_E_ARG;
-#define SWH_ADAM(GDT, TY, WM)                                                                                     \
-    adamw_kernel<GDT, WM><<<nb, kThreads, 0, s>>>(master, exp_avg, exp_avg_sq, static_cast<const TY *>(grad), mo, N, \
-                                                  lr, beta1, beta2, eps, weight_decay, step_size, bc2_sqrt, clip)
-    if (grad_dtype == SWH_BF16) {
-        if ((uintptr_t)grad & 7) return SWH_E_ARG;
-        if (mo) SWH_ADAM(SWH_BF16, uint16_t, true); else SWH_ADAM(SWH_BF16, uint16_t, false);
-    } else if (grad_dtype == SWH_F32) {
-        if ((uintptr_t)grad & 15) return SWH_E_ARG;
-        if (mo) SWH_ADAM(SWH_F32, float, true); else SWH_ADAM(SWH_F32, float, false);
-    } else {
-        return SWH_E_DTYPE;
+    const bool nr = n_no_decay > 0 && weight_decay != 0.f;
+    const int wm = model_out ? model_dtype : -1;
+#define SWH_ADAM(GDT, WM, NR)                                                                                       \
+    adamw_kernel<GDT, WM, NR><<<nb, kThreads, 0, s>>>(master, exp_avg, exp_avg_sq,                                 \
+                                                      static_cast<const typename Elem<GDT>::T *>(grad), model_out, N, \
+                                                      lr, beta1, beta2, eps, weight_decay, step_size, bc2_sqrt, clip, \
+                                                      no_decay, n_no_decay)
+#define SWH_ADAM_G(GDT)                                     \
+    if (wm == SWH_BF16) {                                   \
+        if (nr) SWH_ADAM(GDT, SWH_BF16, true); else SWH_ADAM(GDT, SWH_BF16, false); \
+    } else if (wm == SWH_F32) {                             \
+        if (nr) SWH_ADAM(GDT, SWH_F32, true); else SWH_ADAM(GDT, SWH_F32, false);   \
+    } else {                                                \
+        if (nr) SWH_ADAM(GDT, -1, true); else SWH_ADAM(GDT, -1, false);             \
     }
+    if (grad_dtype == SWH_BF16) {
+        SWH_ADAM_G(SWH_BF16)
+    } else {
+        SWH_ADAM_G(SWH_F32)
+    }
+#undef SWH_ADAM_G
 #undef SWH_ADAM
     return launch_status();
 }

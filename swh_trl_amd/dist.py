@@ -17,13 +17,22 @@ import torch.distributed as dist
 
 def init_from_env(backend: str | None = None):
     """Initialise torch.distributed from RANK/WORLD_SIZE/MASTER_* (torchrun).
-    Returns (rank, world_size, local_rank).  No-op for a single process."""
+    Returns (rank, world_size, device_index).  No-op for a single process.
+
+    device_index is LOCAL_RANK (one process per GPU).  On gloo with more ranks
+    than visible devices (tests rehearsing N ranks on one GPU) ranks share
+    devices round-robin; RCCL refuses that, so the nccl backend raises."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend is None:  # SWH_DIST_BACKEND: tests run gloo ranks that share one GPU
+        backend = os.environ.get("SWH_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+    ndev = torch.cuda.device_count()
+    if ndev and local >= ndev:
+        if backend == "nccl":
+            raise RuntimeError(f"LOCAL_RANK {local} but only {ndev} visible GPU(s): RCCL needs one GPU per rank")
+        local = local % ndev
     if world > 1 and not dist.is_initialized():
-        if backend is None:  # SWH_DIST_BACKEND: tests run gloo ranks that share one GPU
-            backend = os.environ.get("SWH_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
             torch.cuda.set_device(local)
@@ -35,6 +44,13 @@ def world_info():
     if dist.is_available() and dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
     return 0, 1
+
+
+def backend_name() -> str:
+    """The collective backend in use ("nccl" is RCCL on ROCm), or "none"."""
+    if dist.is_available() and dist.is_initialized():
+        return str(dist.get_backend())
+    return "none"
 
 
 def allreduce_mean_(flat: torch.Tensor, bucket_elems: int = 1 << 27):

@@ -72,16 +72,34 @@ def tiny_llama(vocab_size: int = 2048, layers: int = 2) -> DecoderConfig:
                          max_position_embeddings=4096, model_type="llama")
 
 
+SUPPORTED_MODEL_TYPES = ("qwen2", "llama")
+
+
 def from_hf_config(cfg) -> DecoderConfig:
-    """Build from a transformers Qwen2Config / LlamaConfig (object or dict)."""
+    """Build from a transformers Qwen2Config / LlamaConfig (object or dict).
+
+    Other architectures (GPT-2's learned positions / LayerNorm / GELU MLP, MoE,
+    ...) have no kernels in this engine and are refused here with a clear error
+    rather than failing later.  RoPE theta is read from `rope_parameters`
+    (transformers >= 5) or the older top-level `rope_theta`; only the default
+    (unscaled) RoPE is implemented."""
     g = (lambda k, d=None: cfg.get(k, d)) if isinstance(cfg, dict) else (lambda k, d=None: getattr(cfg, k, d))
     mt = g("model_type", "qwen2")
+    if mt not in SUPPORTED_MODEL_TYPES:
+        raise ValueError(f"model_type {mt!r} is not supported by the MI355X engine (supported: "
+                         f"{', '.join(SUPPORTED_MODEL_TYPES)}: Llama-style decoders with RMSNorm, RoPE and a SiLU "
+                         "gated MLP)")
+    rp = g("rope_parameters") or g("rope_scaling") or {}
+    rtype = rp.get("rope_type", rp.get("type", "default")) if isinstance(rp, dict) else "default"
+    if rtype not in ("default", None):
+        raise ValueError(f"rope_type {rtype!r} is not supported (default RoPE only)")
+    theta = (rp.get("rope_theta") if isinstance(rp, dict) else None) or g("rope_theta") or 10000.0
     heads = g("num_attention_heads")
     hd = g("head_dim") or g("hidden_size") // heads
     return DecoderConfig(vocab_size=g("vocab_size"), hidden_size=g("hidden_size"),
                          intermediate_size=g("intermediate_size"), num_hidden_layers=g("num_hidden_layers"),
                          num_attention_heads=heads, num_key_value_heads=g("num_key_value_heads", heads), head_dim=hd,
-                         rope_theta=float(g("rope_theta", 10000.0) or 10000.0),
+                         rope_theta=float(theta),
                          rms_norm_eps=float(g("rms_norm_eps", 1e-6)),
                          tie_word_embeddings=bool(g("tie_word_embeddings", False)),
                          attention_bias=bool(g("attention_bias", mt == "qwen2")),

@@ -49,6 +49,8 @@ class DecodeEngine:
     def __init__(self, model: CausalLM, batch_size: int, max_prompt_len: int, max_new_tokens: int,
                  use_graph: bool = True, fused: Optional[bool] = None):
         c = model.cfg
+        if model.dtype != torch.bfloat16:
+            raise ValueError("DecodeEngine: the decode kernels read bf16 weights (pass a bf16 copy of an fp32 model)")
         self.model, self.cfg = model, c
         self.B, self.Pmax, self.Cmax = batch_size, max_prompt_len, max_new_tokens
         self.Tmax = max_prompt_len + max_new_tokens
@@ -472,7 +474,9 @@ class DecodeEngine:
         self.out.fill_(pad_token_id if pad_token_id is not None else 0)
         self.rng[0], self.rng[1] = int(seed) & ((1 << 63) - 1), int(offset)
         if repetition_penalty != 1.0:
-            ops.seen_init(prompt_ids.to(torch.int64), prompt_mask, self.cfg.vocab_size, self.seen)
+            # every prompt position, left pads included: transformers'
+            # RepetitionPenaltyLogitsProcessor gathers over the whole input_ids
+            ops.seen_init(prompt_ids.to(torch.int64), None, self.cfg.vocab_size, self.seen)
         _trace("generate: setup")
         self.refresh_folded()
         if self.use_graph:

@@ -24,7 +24,7 @@ import torch.nn.functional as F
 
 from .. import nn_ops
 from .._lib import call
-from ..ops import _stream
+from ..ops import _dtype_code, _stream
 from .config import DecoderConfig
 
 _ALIGN = 64  # elements; keeps every view 128-byte aligned
@@ -207,12 +207,13 @@ def _norm_backward(x, w, rstd, dy, dres, gw):
     dx = torch.empty_like(x)
     dyc = dy.contiguous()
     dr = dres.contiguous() if dres is not None else None
+    dt = _dtype_code(x, "rmsnorm")
     call("swh_rmsnorm_bwd", x.data_ptr(), w.data_ptr(), rstd.data_ptr(), dyc.data_ptr(), rows, H, dx.data_ptr(),
-         part.data_ptr(), rpb, None if dr is None else dr.data_ptr(), _stream())
+         part.data_ptr(), rpb, None if dr is None else dr.data_ptr(), dt, _stream())
     if gw is not None:
         with _OnStream(_dw_stream(x.device)) as side:
             side.keep(part)
-            call("swh_rmsnorm_dw_accum", part.data_ptr(), nb, H, gw.data_ptr(), _stream())
+            call("swh_rmsnorm_dw_accum", part.data_ptr(), nb, H, gw.data_ptr(), dt, _stream())
     return dx
 
 
@@ -324,15 +325,16 @@ class _GradReady(torch.autograd.Function):
         return dy, None, None
 
 
-def rope_tables(cfg: DecoderConfig, max_pos: int, device) -> tuple[torch.Tensor, torch.Tensor]:
-    """fp32 [max_pos, D/2] cos/sin holding bf16-rounded values (transformers computes
-    them in fp32 and casts to the activation dtype before the multiply)."""
+def rope_tables(cfg: DecoderConfig, max_pos: int, device, dtype=torch.bfloat16) -> tuple[torch.Tensor, torch.Tensor]:
+    """fp32 [max_pos, D/2] cos/sin holding values of the activation dtype
+    (transformers computes them in fp32 and casts to the activation dtype
+    before the multiply: bf16-rounded for a bf16 model, exact for fp32)."""
     D = cfg.head_dim
     inv = 1.0 / (cfg.rope_theta ** (torch.arange(0, D, 2, dtype=torch.int64).float() / D))
     pos = torch.arange(max_pos, dtype=torch.float32)
     fr = torch.outer(pos, inv)
-    return (fr.cos().to(torch.bfloat16).float().to(device).contiguous(),
-            fr.sin().to(torch.bfloat16).float().to(device).contiguous())
+    return (fr.cos().to(dtype).float().to(device).contiguous(),
+            fr.sin().to(dtype).float().to(device).contiguous())
 
 
 def _apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
@@ -391,8 +393,12 @@ class CausalLM:
         self.on_layer_grads = None
         # full-sequence attention on csrc/attn.hip (fwd 95 + bwd 395 us per layer at the GRPO
         # shape against aotriton's 150 + 430, rocprofv3 of tools/bench_attn.py); SWH_ATTN=torch
-        # selects torch SDPA for A/B
-        self._hip_attn = nn_ops.attention_supported(cfg.head_dim) and os.environ.get("SWH_ATTN", "hip") != "torch"
+        # selects torch SDPA for A/B.  The MFMA kernel is bf16: an fp32 model (the
+        # reference-precision mode) runs SDPA
+        if dtype not in (torch.bfloat16, torch.float32):
+            raise ValueError(f"CausalLM dtype {dtype}: bf16 (the product path) or float32 (reference precision)")
+        self._hip_attn = (nn_ops.attention_supported(cfg.head_dim) and dtype == torch.bfloat16
+                          and os.environ.get("SWH_ATTN", "hip") != "torch")
 
     def layer_range(self, i: int) -> tuple[int, int]:
         """[start, end) of layer i's parameters (and gradients) in the flat buffers."""
@@ -420,6 +426,16 @@ class CausalLM:
         if self.grad is not None:
             self.grad.zero_()
 
+    def no_decay_ranges(self) -> list[tuple[int, int]]:
+        """[start, end) ranges of the flat buffer excluded from weight decay, as
+        transformers' Trainer.get_decay_parameter_names excludes biases and
+        norm weights (ALL_LAYERNORM_LAYERS / names with "bias", "norm")."""
+        out = []
+        for k, (o, s) in sorted(self.layout.items(), key=lambda kv: kv[1][0]):
+            if k.endswith(("ln_in", "ln_post", "qkv_b")) or k == "norm":
+                out.append((o, o + math.prod(s)))
+        return out
+
     def lm_weight(self) -> torch.Tensor:
         return self.p["embed"] if (self.cfg.tie_word_embeddings and self.head == "lm") else self.p.get("lm_head")
 
@@ -431,7 +447,7 @@ class CausalLM:
     def rope(self, max_pos: int):
         if self._rope is None or self._rope[0].shape[0] < max_pos:
             n = max(max_pos, 4096)
-            self._rope = rope_tables(self.cfg, n, self.device)
+            self._rope = rope_tables(self.cfg, n, self.device, self.dtype)
         return self._rope
 
     # ------------------------------------------------------------------ HF interop

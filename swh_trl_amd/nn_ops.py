@@ -13,7 +13,7 @@ import torch
 
 from . import _lib
 from ._lib import call
-from .ops import _dev, _p, _stream
+from .ops import _dev, _dtype_code, _p, _stream
 
 
 def rmsnorm_residual(x: torch.Tensor, residual: Optional[torch.Tensor], weight: torch.Tensor, eps: float,
@@ -29,7 +29,7 @@ def rmsnorm_residual(x: torch.Tensor, residual: Optional[torch.Tensor], weight: 
     if residual is not None and s_out is None:
         s_out = torch.empty_like(x)
     call("swh_rmsnorm_fwd", x.data_ptr(), _p(residual), _p(s_out), weight.data_ptr(), rows, H, float(eps),
-         y.data_ptr(), _p(rstd), _stream())
+         y.data_ptr(), _p(rstd), _dtype_code(x, "rmsnorm"), _stream())
     return y, (s_out if residual is not None else x)
 
 
@@ -57,7 +57,7 @@ class RMSNormFn(torch.autograd.Function):
         part = torch.empty(nb, H, device=x.device, dtype=torch.float32)
         dyc = dy.contiguous()
         call("swh_rmsnorm_bwd", x.data_ptr(), w.data_ptr(), rstd.data_ptr(), dyc.data_ptr(), rows, H, dx.data_ptr(),
-             part.data_ptr(), rpb, None, _stream())
+             part.data_ptr(), rpb, None, _dtype_code(x, "rmsnorm"), _stream())
         return dx, part.sum(0).to(w.dtype), None
 
 
@@ -70,7 +70,8 @@ class SiluMulFn(torch.autograd.Function):
         I2 = guc.shape[-1]
         rows = guc.numel() // I2
         out = torch.empty(*guc.shape[:-1], I2 // 2, device=gu.device, dtype=gu.dtype)
-        call("swh_silu_mul_fwd", guc.data_ptr(), rows, I2 // 2, out.data_ptr(), _stream())
+        call("swh_silu_mul_fwd", guc.data_ptr(), rows, I2 // 2, out.data_ptr(), _dtype_code(guc, "silu_mul"),
+             _stream())
         ctx.save_for_backward(guc)
         return out
 
@@ -81,7 +82,8 @@ class SiluMulFn(torch.autograd.Function):
         rows = gu.numel() // I2
         dgu = torch.empty_like(gu)
         d = dout.contiguous()
-        call("swh_silu_mul_bwd", gu.data_ptr(), d.data_ptr(), rows, I2 // 2, dgu.data_ptr(), _stream())
+        call("swh_silu_mul_bwd", gu.data_ptr(), d.data_ptr(), rows, I2 // 2, dgu.data_ptr(),
+             _dtype_code(gu, "silu_mul"), _stream())
         return dgu
 
 
@@ -90,7 +92,7 @@ def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tens
     rows = gu.numel() // I2
     if out is None:
         out = torch.empty(*gu.shape[:-1], I2 // 2, device=gu.device, dtype=gu.dtype)
-    call("swh_silu_mul_fwd", gu.data_ptr(), rows, I2 // 2, out.data_ptr(), _stream())
+    call("swh_silu_mul_fwd", gu.data_ptr(), rows, I2 // 2, out.data_ptr(), _dtype_code(gu, "silu_mul"), _stream())
     return out
 
 
@@ -285,19 +287,21 @@ class QKVRopeFn(torch.autograd.Function):
         k = torch.empty(B, Hkv, L, D, device=qkv.device, dtype=qkv.dtype)
         v = torch.empty(B, Hkv, L, D, device=qkv.device, dtype=qkv.dtype)
         call("swh_qkv_rope", qkv_c.data_ptr(), pos.data_ptr(), cos.data_ptr(), sin.data_ptr(), B, L, Hq, Hkv, D,
-             q.data_ptr(), k.data_ptr(), v.data_ptr(), 0, _stream())
+             q.data_ptr(), k.data_ptr(), v.data_ptr(), 0, _dtype_code(qkv_c, "qkv_rope"), _stream())
         ctx.save_for_backward(pos, cos, sin)
         ctx.dims = (B, L, Hq, Hkv, D)
+        ctx.dtype = qkv.dtype
         return q, k, v
 
     @staticmethod
     def backward(ctx, dq, dk, dv):
         pos, cos, sin = ctx.saved_tensors
         B, L, Hq, Hkv, D = ctx.dims
-        dq = torch.zeros(B, Hq, L, D, device=pos.device, dtype=torch.bfloat16) if dq is None else dq.contiguous()
-        dk = torch.zeros(B, Hkv, L, D, device=pos.device, dtype=torch.bfloat16) if dk is None else dk.contiguous()
-        dv = torch.zeros(B, Hkv, L, D, device=pos.device, dtype=torch.bfloat16) if dv is None else dv.contiguous()
-        dqkv = torch.empty(B, L, (Hq + 2 * Hkv) * D, device=pos.device, dtype=dq.dtype)
+        dt = ctx.dtype
+        dq = torch.zeros(B, Hq, L, D, device=pos.device, dtype=dt) if dq is None else dq.contiguous()
+        dk = torch.zeros(B, Hkv, L, D, device=pos.device, dtype=dt) if dk is None else dk.contiguous()
+        dv = torch.zeros(B, Hkv, L, D, device=pos.device, dtype=dt) if dv is None else dv.contiguous()
+        dqkv = torch.empty(B, L, (Hq + 2 * Hkv) * D, device=pos.device, dtype=dt)
         call("swh_qkv_rope", dqkv.data_ptr(), pos.data_ptr(), cos.data_ptr(), sin.data_ptr(), B, L, Hq, Hkv, D,
-             dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), 1, _stream())
+             dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), 1, _dtype_code(dq, "qkv_rope"), _stream())
         return dqkv, None, None, None, None, None, None

@@ -144,8 +144,14 @@ def entropy_from_logits(logits: torch.Tensor, chunk_size: int = 1) -> torch.Tens
 # trl/core.py
 # ---------------------------------------------------------------------------
 
-def masked_whiten(values: torch.Tensor, mask: torch.Tensor, shift_mean: bool = True):
-    """trl/core.py:70-76 on device; raises ValueError on an all-zero mask (core.py:59)."""
+_ZERO_MASK_MSG = ("The sum of the mask is zero, which can happen when `mini_batch_size=1`;"
+                  "try increase the `mini_batch_size` or `gradient_accumulation_steps`")
+
+
+def masked_whiten_stats(values: torch.Tensor, mask: torch.Tensor, shift_mean: bool = True):
+    """Hot-path form of trl/core.py:70-76 with no host sync: returns (whitened,
+    stats f32[3] = masked mean, unbiased masked variance, mask sum).  A zero
+    mask yields NaNs here; `masked_whiten` raises for it as the reference."""
     _dev(values, "masked_whiten")
     v = values.reshape(-1).to(torch.float32).contiguous()
     m = mask.reshape(-1).to(torch.int32).contiguous()
@@ -156,25 +162,32 @@ def masked_whiten(values: torch.Tensor, mask: torch.Tensor, shift_mean: bool = T
     return out.view(values.shape).to(values.dtype), stats
 
 
-def masked_whiten_checked(values, mask, shift_mean: bool = True):
-    out, stats = masked_whiten(values, mask, shift_mean)
-    if float(stats[2]) == 0:  # host sync only on this checked variant
-        raise ValueError("The sum of the mask is zero, which can happen when `mini_batch_size=1`;"
-                         "try increase the `mini_batch_size` or `gradient_accumulation_steps`")
+def masked_whiten(values: torch.Tensor, mask: torch.Tensor, shift_mean: bool = True) -> torch.Tensor:
+    """trl/core.py:70-76: `(values - mean) * rsqrt(var + 1e-8)` (+ mean back when
+    shift_mean=False) over the masked entries, one device kernel.  Raises
+    ValueError on an all-zero mask like the reference's `masked_var`
+    (core.py:57-62), which checks `mask.sum() == 0` on the host too."""
+    out, stats = masked_whiten_stats(values, mask, shift_mean)
+    if float(stats[2]) == 0:
+        raise ValueError(_ZERO_MASK_MSG)
     return out
 
 
-def masked_mean(values, mask, axis=None):
+def masked_mean(values: torch.Tensor, mask: torch.Tensor, axis=None) -> torch.Tensor:
     """trl/core.py:43-48 (reduction is tiny; kept in torch on the device)."""
     if axis is not None:
         return (values * mask).sum(axis=axis) / mask.sum(axis=axis)
     return (values * mask).sum() / mask.sum()
 
 
-def masked_var(values, mask, unbiased: bool = True):
-    """trl/core.py:51-67 via the whitening kernel's stats."""
-    _, stats = masked_whiten(values, mask)
+def masked_var(values: torch.Tensor, mask: torch.Tensor, unbiased: bool = True) -> torch.Tensor:
+    """trl/core.py:51-67 via the whitening kernel's statistics: the masked
+    variance, Bessel-corrected when `unbiased`; raises ValueError on an
+    all-zero mask when `unbiased` (core.py:57-62), NaN otherwise."""
+    _, stats = masked_whiten_stats(values, mask)
     if unbiased:
+        if float(stats[2]) == 0:
+            raise ValueError(_ZERO_MASK_MSG)
         return stats[1]
     n = stats[2]
     return stats[1] * (n - 1) / n

@@ -19,7 +19,7 @@ from .ops import _dtype_code, _p, _stream
 
 class FlatAdamW:
     def __init__(self, numel: int, device, lr: float = 1e-6, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0, max_grad_norm: Optional[float] = 1.0):
+                 weight_decay: float = 0.0, max_grad_norm: Optional[float] = 1.0, no_decay_ranges=()):
         self.numel = int(numel)
         self.lr = float(lr)
         self.betas = (float(betas[0]), float(betas[1]))
@@ -33,6 +33,18 @@ class FlatAdamW:
         self._partials = torch.empty(_lib.load().swh_sqnorm_partials(self.numel), device=device,
                                      dtype=torch.float32)
         self.clip_out = torch.empty(2, device=device, dtype=torch.float32)  # {total_norm, coef}
+        # [start, end) element ranges without weight decay (biases / norm weights), merged,
+        # each start/end a multiple of 4 (the model layout aligns every view to 64)
+        merged = []
+        for s, e in sorted(no_decay_ranges):
+            if merged and s <= merged[-1][1]:
+                merged[-1][1] = max(merged[-1][1], e)
+            else:
+                merged.append([s, e])
+        if any(s % 4 or (e % 4 and e != self.numel) for s, e in merged):
+            raise ValueError("no_decay_ranges must start and end on multiples of 4 elements")
+        self.no_decay = (torch.tensor(merged, dtype=torch.int64, device=device).reshape(-1)
+                         if merged else None)
 
     def grad_norm(self, grad: torch.Tensor) -> torch.Tensor:
         call("swh_grad_sqnorm", grad.data_ptr(), _dtype_code(grad, "grad_norm"), self.numel, self._partials.data_ptr(),
@@ -51,10 +63,13 @@ class FlatAdamW:
         lr = self.lr if lr is None else float(lr)
         clip = self.clip_out if self.max_grad_norm else None
         nbytes = self.numel * (24 + grad.element_size() + (model_out.element_size() if model_out is not None else 0))
+        nd = self.no_decay
         with profiling.kernel("adamw", nbytes):
             call("swh_adamw", self.master.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
-                 grad.data_ptr(), _dtype_code(grad, "adamw"), _p(model_out), self.numel, lr, self.betas[0],
-                 self.betas[1], self.eps, self.weight_decay, self.step_count, _p(clip), _stream())
+                 grad.data_ptr(), _dtype_code(grad, "adamw"), _p(model_out),
+                 _dtype_code(model_out, "adamw") if model_out is not None else 0, self.numel, lr, self.betas[0],
+                 self.betas[1], self.eps, self.weight_decay, self.step_count, _p(clip), _p(nd),
+                 0 if nd is None else nd.numel() // 2, _stream())
         return norm
 
     def state_dict(self):

@@ -62,28 +62,43 @@ class TrainerState:
         self.log_history: list[dict] = []
 
 
-def load_model(model, device, trainable=True, seed=0, head: str = "lm") -> CausalLM:
+def model_dtype(model_init_kwargs: Optional[dict]) -> torch.dtype:
+    """The model's parameter dtype from GRPOConfig/PPOConfig.model_init_kwargs
+    (`torch_dtype` / `dtype`, as the reference passes them to from_pretrained,
+    grpo_trainer.py:611-627): "float32" selects the fp32 reference-precision
+    mode; anything else (default, "auto", "bfloat16") the bf16 engine."""
+    kw = model_init_kwargs or {}
+    d = kw.get("torch_dtype", kw.get("dtype"))
+    if d in (torch.float32, "float32", "fp32"):
+        return torch.float32
+    if d in (None, "auto", torch.bfloat16, "bfloat16", "bf16"):
+        return torch.bfloat16
+    raise ValueError(f"model dtype {d!r}: the MI355X engine trains bfloat16 or float32 models")
+
+
+def load_model(model, device, trainable=True, seed=0, head: str = "lm", dtype=torch.bfloat16) -> CausalLM:
     """`model` may be a CausalLM, a preset name ("qwen2.5-0.5b", "llama-3-8b",
     "tiny"), a DecoderConfig (random init), a local directory holding a
     transformers config.json + safetensors, or a transformers PreTrainedModel.
     head="score": a sequence-classification model (value / reward model, one
-    output), as transformers' *ForSequenceClassification."""
+    output), as transformers' *ForSequenceClassification.  `dtype`: parameter
+    dtype of a newly built model (a CausalLM passed in keeps its own)."""
     if isinstance(model, CausalLM):
         if model.head != head:
             raise ValueError(f"expected a model with a {head!r} head, got {model.head!r}")
         return model
     if isinstance(model, DecoderConfig):
-        return CausalLM(model, device, head=head, seed=seed, trainable=trainable)
+        return CausalLM(model, device, head=head, seed=seed, trainable=trainable, dtype=dtype)
     if isinstance(model, str):
         if model in PRESETS:
-            return CausalLM(PRESETS[model](), device, head=head, seed=seed, trainable=trainable)
+            return CausalLM(PRESETS[model](), device, head=head, seed=seed, trainable=trainable, dtype=dtype)
         if os.path.isdir(model):
             import json
 
             from safetensors.torch import load_file
             with open(os.path.join(model, "config.json")) as f:
                 cfg = from_hf_config(json.load(f))
-            m = CausalLM(cfg, device, head=head, seed=None, trainable=trainable)
+            m = CausalLM(cfg, device, head=head, seed=None, trainable=trainable, dtype=dtype)
             sd = {}
             for fn in sorted(os.listdir(model)):
                 if fn.endswith(".safetensors"):
@@ -94,7 +109,7 @@ def load_model(model, device, trainable=True, seed=0, head: str = "lm") -> Causa
                          "model object")
     if hasattr(model, "config") and hasattr(model, "state_dict"):
         cfg = from_hf_config(model.config)
-        m = CausalLM(cfg, device, head=head, seed=None, trainable=trainable)
+        m = CausalLM(cfg, device, head=head, seed=None, trainable=trainable, dtype=dtype)
         m.load_hf_state_dict({k: v.to(device) for k, v in model.state_dict().items()})
         return m
     raise TypeError(f"unsupported model type {type(model)}")
@@ -117,7 +132,11 @@ class GRPOTrainer:
         torch.cuda.set_device(self.device)
         gemm_tuning.enable()
         torch.manual_seed(a.seed)
-        self.model = load_model(model, self.device, trainable=True, seed=a.seed)
+        self.model = load_model(model, self.device, trainable=True, seed=a.seed,
+                                dtype=model_dtype(a.model_init_kwargs))
+        # the decode engine's kernels are bf16: an fp32 model rolls out from a bf16
+        # copy of its weights, refreshed before every generation
+        self._rollout_model: Optional[CausalLM] = None
         self.processing_class = processing_class
         if not isinstance(reward_funcs, list):
             reward_funcs = [reward_funcs]
@@ -160,11 +179,12 @@ class GRPOTrainer:
                                min_new_tokens=int(gk.get("min_new_tokens", 0) or 0))
         self.ref_model = None
         if self.beta != 0.0:
-            self.ref_model = CausalLM(self.model.cfg, self.device, seed=None, trainable=False)
+            self.ref_model = CausalLM(self.model.cfg, self.device, seed=None, trainable=False, dtype=self.model.dtype)
             self.ref_model.copy_from(self.model)
         self.optimizer = FlatAdamW(self.model.numel, self.device, lr=a.learning_rate,
                                    betas=(a.adam_beta1, a.adam_beta2), eps=a.adam_epsilon,
-                                   weight_decay=a.weight_decay, max_grad_norm=a.max_grad_norm)
+                                   weight_decay=a.weight_decay, max_grad_norm=a.max_grad_norm,
+                                   no_decay_ranges=self.model.no_decay_ranges())
         self.optimizer.master.copy_(self.model.flat.float())
         self.state = TrainerState()
         self._step = 0
@@ -209,12 +229,24 @@ class GRPOTrainer:
             ids, mask = truncate_with_protected_tokens(ids, mask, self.max_prompt_length, [])
         return ids, mask, texts
 
+    def _generation_model(self) -> CausalLM:
+        """The bf16 weights the decode engine reads: the policy itself, or for an
+        fp32 policy a bf16 copy refreshed now (one cast of the flat buffer)."""
+        m = self.model
+        if m.dtype == torch.bfloat16:
+            return m
+        if self._rollout_model is None:
+            self._rollout_model = CausalLM(m.cfg, self.device, seed=None, trainable=False, dtype=torch.bfloat16)
+        self._rollout_model.flat.copy_(m.flat)
+        return self._rollout_model
+
     def _engine_for(self, B: int, P: int) -> DecodeEngine:
         C = self.max_completion_length
+        gm = self._generation_model()
         e = self._engine
-        if e is None or e.B != B or e.Pmax < P:
+        if e is None or e.B != B or e.Pmax < P or e.model is not gm:
             Pmax = max(P, self.max_prompt_length or P) if (self.max_prompt_length or 0) <= 4096 else P
-            self._engine = DecodeEngine(self.model, B, Pmax, C)
+            self._engine = DecodeEngine(gm, B, Pmax, C)
         return self._engine
 
     # ------------------------------------------------------------------ rollout + scoring

@@ -151,7 +151,8 @@ class PPOTrainer:
         # gradient clipping in the reference loop: two flat buffers, same update
         mk = lambda m: FlatAdamW(m.numel, self.device, lr=args.learning_rate,  # noqa: E731
                                  betas=(args.adam_beta1, args.adam_beta2), eps=args.adam_epsilon,
-                                 weight_decay=args.weight_decay, max_grad_norm=None)
+                                 weight_decay=args.weight_decay, max_grad_norm=None,
+                                 no_decay_ranges=m.no_decay_ranges())
         self.opt_policy, self.opt_value = mk(self.policy_model), mk(self.value_model)
         self.opt_policy.master.copy_(self.policy_model.flat.float())
         self.opt_value.master.copy_(self.value_model.flat.float())
@@ -273,11 +274,11 @@ class PPOTrainer:
         rewards[actual_start, actual_end] += scores
         # 5. whiten rewards
         if a.whiten_rewards:
-            rewards = ops.masked_whiten_checked(rewards, ~padding_mask_p1, shift_mean=False)
+            rewards = ops.masked_whiten(rewards, ~padding_mask_p1, shift_mean=False)
             rewards = torch.masked_fill(rewards, padding_mask_p1, 0)
         # 6. advantages and returns (reverse GAE scan), whitened advantages
         advantages, returns = ops.gae(rewards, values.float(), a.gamma, a.lam)
-        advantages = ops.masked_whiten_checked(advantages, ~padding_mask)
+        advantages = ops.masked_whiten(advantages, ~padding_mask)
         advantages = torch.masked_fill(advantages, padding_mask, 0)
         return {"queries": queries, "responses": responses, "query_responses": query_responses,
                 "logprobs": logprobs, "ref_logprobs": ref_logprobs, "values": values, "scores": scores, "rm_scores": rm_scores,

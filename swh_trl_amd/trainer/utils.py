@@ -48,12 +48,15 @@ def generation_batch_indices(n: int, num_generations: int, generation_batch_size
     contiguous local chunk of each global generation batch, and the repeats are
     consumed without regenerating (`_prepare_inputs` :1411-1444).  Here the
     repeats are collapsed and each yielded list is one local generation batch
-    (whole groups of G: local_batch_size is a multiple of G)."""
+    (whole groups of G: local_batch_size is a multiple of G).  One sampler (one
+    generator) serves every epoch, as the reference's dataloader re-iterates
+    the same RepeatSampler: each epoch draws a fresh permutation."""
+    sampler = RepeatSampler(range(n), mini_repeat_count=num_generations,
+                            batch_size=generation_batch_size // num_generations, repeat_count=1,
+                            shuffle=shuffle, seed=seed)
     ep = 0
     while epochs is None or ep < epochs:
-        idx = list(RepeatSampler(range(n), mini_repeat_count=num_generations,
-                                 batch_size=generation_batch_size // num_generations, repeat_count=1,
-                                 shuffle=shuffle, seed=seed))
+        idx = list(sampler)
         for s in range(0, len(idx) - generation_batch_size + 1, generation_batch_size):
             yield idx[s + rank * local_batch_size:s + (rank + 1) * local_batch_size]
         ep += 1
@@ -84,6 +87,24 @@ def truncate_with_protected_tokens(ids: torch.Tensor, mask: torch.Tensor, target
         raise ValueError("rows shorter than target_length cannot be truncated to a common width")
     w = int(counts[0])
     return ids[keep].view(B, w), mask[keep].view(B, w)
+
+
+def pad(tensors: Sequence[torch.Tensor], padding_value: int = 0, padding_side: str = "right",
+        pad_to_multiple_of: Optional[int] = None) -> torch.Tensor:
+    """trl/trainer/utils.py:245-308: one [n, *max_shape] tensor holding the
+    ragged inputs; the leading (sequence) dim is padded on `padding_side` and
+    rounded up to `pad_to_multiple_of`, trailing dims are filled from 0."""
+    if padding_side not in ("left", "right"):
+        raise ValueError("padding_side must be 'left' or 'right'")
+    nd = tensors[0].dim()
+    size = [max(int(t.shape[d]) for t in tensors) for d in range(nd)]
+    if pad_to_multiple_of:
+        size[0] = -(-size[0] // pad_to_multiple_of) * pad_to_multiple_of
+    out = tensors[0].new_full([len(tensors), *size], padding_value)
+    for i, t in enumerate(tensors):
+        lead = size[0] - t.shape[0] if padding_side == "left" else 0
+        out[(i, slice(lead, lead + t.shape[0])) + tuple(slice(0, s) for s in t.shape[1:])] = t
+    return out
 
 
 def left_pad(seqs: Sequence[Sequence[int]], pad_id: int, device=None):

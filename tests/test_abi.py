@@ -52,7 +52,10 @@ def test_host_only_calls(lib):
     with pytest.raises(ValueError):
         _lib.call("swh_logp_entropy_fwd", None, 1, 1, 1, 0, 0, 10, None, 1.0, 0, None, None, None, None)
     with pytest.raises(ValueError):
-        _lib.call("swh_adamw", None, None, None, None, 1, None, 10, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1, None, None)
+        _lib.call("swh_adamw", None, None, None, None, 1, None, 1, 10, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1, None, None,
+                  0, None)
+    with pytest.raises(ValueError):  # dtype code outside {f32, bf16} for an fp32-model op
+        _lib.call("swh_silu_mul_fwd", 8, 1, 8, 8, 7, None)
 
 
 def test_struct_layouts_match_c(tmp_path):

@@ -9,8 +9,11 @@ replicas must stay bit-identical, and differ from a single-rank run on the
 same rank-0 prompts (the other rank's gradients were averaged in).
 """
 import hashlib
+import json
 import multiprocessing as mp
 import os
+import subprocess
+import sys
 
 import pytest
 import torch
@@ -67,3 +70,21 @@ def test_dp_two_ranks_keep_replicas_identical():
     assert got[0][0] == got[1][0]
     single = _run(1, 2)
     assert single[0][0] != got[0][0]
+
+
+def test_bench_launches_n_ranks_itself():
+    """`python bench.py --gpus 2` (no torchrun environment) starts two ranks
+    itself; rank 0 prints one line with n_gpus 2 and the world size the process
+    group reports.  gloo here: RCCL needs one GPU per rank and this box has one."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SWH_DIST_BACKEND="gloo")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--layers", "2", "--steps", "1", "--warmup", "1",
+                        "--no-cpu-baseline"], cwd=root, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["ranks_seen"] == 2 and line["backend"] == "gloo"
+    assert line["config"]["global_batch"] == 128 and line["value"] > 0

@@ -244,9 +244,10 @@ def test_chunked_lm_head_logp_matches_unchunked(dev):
     assert rel < 0.02, float(rel)
 
 
-def test_grpo_trainer_smoke_and_oracle_step(dev):
-    """A full GRPOTrainer step on a tiny model runs, changes the weights, and its
-    loss equals the CPU oracle step's loss on the same completions."""
+def test_grpo_trainer_smoke(dev):
+    """GRPOTrainer.train() runs two steps on a tiny bf16 model, changes the
+    weights and logs finite loss / grad norm.  Step-level parity against the
+    CPU oracle step is tests/test_step_parity_gpu.py."""
     from swh_trl_amd.trainer import GRPOConfig, GRPOTrainer
     from swh_trl_amd.engine import tiny_qwen2
     cfg = tiny_qwen2(512, 2)

@@ -248,11 +248,20 @@ def test_masked_whiten(ops, dev):
     v = torch.randn(8, 53, generator=g)
     m = torch.rand(8, 53, generator=g) > 0.3
     for shift in (True, False):
-        out, stats = ops.masked_whiten(v.to(dev), m.to(dev), shift_mean=shift)
+        out = ops.masked_whiten(v.to(dev), m.to(dev), shift_mean=shift)
+        assert isinstance(out, torch.Tensor) and out.shape == v.shape
         exp = trl_ref.masked_whiten(v.double(), m.double(), shift_mean=shift)
         torch.testing.assert_close(out.cpu().double(), exp, rtol=1e-5, atol=1e-5)
-    with pytest.raises(ValueError):
-        ops.masked_whiten_checked(v.to(dev), torch.zeros_like(m).to(dev))
+    for unbiased in (True, False):
+        torch.testing.assert_close(ops.masked_var(v.to(dev), m.to(dev), unbiased).cpu().double(),
+                                   trl_ref.masked_var(v.double(), m.double(), unbiased), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(ops.masked_mean(v.to(dev), m.to(dev)).cpu().double(),
+                               trl_ref.masked_mean(v.double(), m.double()), rtol=1e-5, atol=1e-6)
+    # core.py:57-62: an all-zero mask raises in masked_var(unbiased) and so in masked_whiten
+    with pytest.raises(ValueError, match="sum of the mask is zero"):
+        ops.masked_whiten(v.to(dev), torch.zeros_like(m).to(dev))
+    with pytest.raises(ValueError, match="sum of the mask is zero"):
+        ops.masked_var(v.to(dev), torch.zeros_like(m).to(dev))
 
 
 def test_gae(ops, dev):
@@ -320,6 +329,39 @@ def test_adamw_and_clip(dev):
         q, m, v = trl_ref.adamw_step(q, gr.double() * coef, m, v, step, 1e-3, weight_decay=0.01)
     torch.testing.assert_close(st.master.cpu().double(), q, rtol=1e-5, atol=1e-6)
     assert torch.equal(model.cpu(), st.master.cpu().to(torch.bfloat16))
+
+
+def test_adamw_no_decay_ranges_and_fp32_model(dev):
+    """weight_decay > 0 with the transformers Trainer grouping (no decay on
+    biases / norm weights: CausalLM.no_decay_ranges) against torch AdamW with
+    two param groups; the fp32 model copy is the master itself."""
+    from swh_trl_amd import optim
+    from swh_trl_amd.engine import CausalLM, tiny_qwen2
+    m = CausalLM(tiny_qwen2(512, 2), "cpu", seed=1, dtype=torch.float32, trainable=False)
+    N = m.numel
+    nd = m.no_decay_ranges()
+    assert len(nd) == 2 * 3 + 1  # per layer: ln_in, qkv_b, ln_post; the final norm
+    decay = torch.ones(N, dtype=torch.bool)
+    for s, e in nd:
+        decay[s:e] = False
+    g = _gen(15)
+    p0 = torch.randn(N, generator=g)
+    st = optim.FlatAdamW(N, dev, lr=1e-2, weight_decay=0.1, max_grad_norm=None, no_decay_ranges=nd)
+    st.master.copy_(p0.to(dev))
+    model = torch.empty(N, dtype=torch.float32, device=dev)
+    pd = torch.nn.Parameter(p0[decay].double().clone())
+    pn = torch.nn.Parameter(p0[~decay].double().clone())
+    opt = torch.optim.AdamW([{"params": [pd], "weight_decay": 0.1}, {"params": [pn], "weight_decay": 0.0}],
+                            lr=1e-2, foreach=False)
+    for _ in range(3):
+        gr = torch.randn(N, generator=g) * 0.1
+        st.step(gr.to(dev), model_out=model)
+        pd.grad, pn.grad = gr[decay].double(), gr[~decay].double()
+        opt.step()
+    out = st.master.cpu().double()
+    torch.testing.assert_close(out[decay], pd.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(out[~decay], pn.detach(), rtol=1e-5, atol=1e-6)
+    assert torch.equal(model.cpu(), st.master.cpu())
 
 
 # --------------------------------------------------------------------------- sampler
@@ -535,7 +577,7 @@ def test_degenerate_inputs(ops, dev):
     assert ops.selective_log_softmax(lg, ix).shape == (0, 7)
     assert ops.entropy_from_logits(torch.empty(0, V, device=dev)).shape == (0,)
     with pytest.raises(ValueError):
-        ops.masked_whiten_checked(torch.randn(4, 3, device=dev), torch.zeros(4, 3, device=dev))
+        ops.masked_whiten(torch.randn(4, 3, device=dev), torch.zeros(4, 3, device=dev))
     # constant rewards within each group of 4: mean = the constant, std 0, advantage 0
     rpf = torch.tensor([[2.0], [2.0], [2.0], [2.0], [1.0], [3.0], [1.0], [3.0]], device=dev)
     adv, rew, gm, gs, zs = ops.group_advantages(rpf, torch.ones(1, device=dev), 4, True)
