@@ -226,6 +226,12 @@ int swh_adamw(float *master, float *exp_avg, float *exp_avg_sq, const void *grad
               void *model_out, int model_dtype, int64_t N, float lr, float beta1, float beta2, float eps,
               float weight_decay, int64_t step_count, const float *clip, const int64_t *no_decay,
               int32_t n_no_decay, void *stream);
+/* TR-DPO reference-model sync (trl/trainer/callbacks.py:106-131, SyncRefModelCallback
+ * ._sync_target_model, run every ref_model_sync_steps by grpo_trainer.py:1032-1033):
+ * target = target * (1 - alpha) + alpha * src over a flat parameter buffer,
+ * rounded to the parameter dtype after the multiply and after the add as torch's
+ * mul_ / add_(alpha=) do.  dtype bf16 or f32. */
+int swh_ema_mix(void *target, const void *src, int dtype, int64_t N, float alpha, void *stream);
 /* dst_f32[i] += src[i] (bf16/f32) — accumulate micro-batch grads in fp32. */
 int swh_accumulate(float *dst, const void *src, int dtype, int64_t N, float scale, void *stream);
 

@@ -136,6 +136,25 @@ class OverlappedAllReduce:
         self.works, self.done = [], []
 
 
+def all_gather_rows(t: torch.Tensor) -> torch.Tensor:
+    """Concatenate every rank's [n, ...] tensor along dim 0 in rank order (the
+    reference's accelerate `gather(rewards_per_func)`, grpo_trainer.py:1497).
+    Equal n on every rank; RCCL gathers in place on the device, gloo through
+    host copies.  One process: returns t."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return t
+    world = dist.get_world_size()
+    tc = t.contiguous()
+    if dist.get_backend() == "nccl":
+        out = torch.empty((world * tc.shape[0],) + tuple(tc.shape[1:]), dtype=tc.dtype, device=tc.device)
+        dist.all_gather_into_tensor(out, tc)
+        return out
+    host = tc.cpu()
+    parts = [torch.empty_like(host) for _ in range(world)]
+    dist.all_gather(parts, host)
+    return torch.cat(parts).to(t.device)
+
+
 def barrier():
     if dist.is_available() and dist.is_initialized():
         if dist.get_backend() == "nccl":

@@ -82,3 +82,12 @@ class FlatAdamW:
         self.exp_avg_sq.copy_(sd["exp_avg_sq"])
         self.step_count = int(sd["step"])
         self.lr = float(sd.get("lr", self.lr))
+
+
+def sync_ref_model(ref_flat: torch.Tensor, policy_flat: torch.Tensor, alpha: float) -> None:
+    """TR-DPO mixup (callbacks.py:106-131): ref = ref * (1 - alpha) + alpha * policy,
+    one streaming kernel over the flat parameter buffers."""
+    if ref_flat.shape != policy_flat.shape or ref_flat.dtype != policy_flat.dtype:
+        raise ValueError("sync_ref_model: reference and policy buffers must match in size and dtype")
+    call("swh_ema_mix", ref_flat.data_ptr(), policy_flat.data_ptr(), _dtype_code(ref_flat, "sync_ref_model"),
+         ref_flat.numel(), float(alpha), _stream())

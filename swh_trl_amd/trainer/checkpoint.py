@@ -143,17 +143,25 @@ def _flat_views(model: CausalLM, flat: torch.Tensor) -> dict:
         model.p = saved
 
 
-def optimizer_state_dict(model: CausalLM, opt, weight_decay: float) -> dict:
+def optimizer_state_dict(model: CausalLM, opt, weight_decay: float, parts=None) -> dict:
     """The flat AdamW state as torch.optim.AdamW.state_dict() of the Trainer's
-    two param groups (decay, no decay) over the transformers parameters."""
-    names = hf_param_order(model)
+    two param groups (decay, no decay) over the transformers parameters.
+    parts: [(name prefix, model, flat optimizer), ...] for a module holding
+    several models (PPO's PolicyAndValueWrapper: "policy.", "value_model.")."""
+    parts = parts or [("", model, opt)]
+    names, moments, steps = [], {}, {}
+    for pre, mdl, o in parts:
+        m, v = _flat_views(mdl, o.exp_avg), _flat_views(mdl, o.exp_avg_sq)
+        for n in hf_param_order(mdl):
+            names.append(pre + n)
+            moments[pre + n] = (m[n], v[n])
+            steps[pre + n] = o.step_count
     groups = [[n for n in names if not _no_decay_name(n)], [n for n in names if _no_decay_name(n)]]
     order = groups[0] + groups[1]
-    m, v = _flat_views(model, opt.exp_avg), _flat_views(model, opt.exp_avg_sq)
     state = {}
     for i, n in enumerate(order):
-        state[i] = {"step": torch.tensor(float(opt.step_count)), "exp_avg": m[n].detach().cpu().clone(),
-                    "exp_avg_sq": v[n].detach().cpu().clone()}
+        state[i] = {"step": torch.tensor(float(steps[n])), "exp_avg": moments[n][0].detach().cpu().clone(),
+                    "exp_avg_sq": moments[n][1].detach().cpu().clone()}
     base = {"lr": opt.lr, "betas": opt.betas, "eps": opt.eps, "amsgrad": False, "foreach": None, "maximize": False,
             "capturable": False, "differentiable": False, "fused": None, "initial_lr": opt.lr}
     pg = [dict(base, weight_decay=weight_decay, params=list(range(len(groups[0])))),

@@ -32,7 +32,11 @@ class GRPOConfig:
     warmup_steps: int = 0
     warmup_ratio: float = 0.0
     logging_steps: float = 10
+    save_strategy: str = "steps"           # "steps" | "no" (TrainingArguments)
     save_steps: float = 500
+    save_total_limit: Optional[int] = None
+    save_only_model: bool = False
+    hub_model_id: Optional[str] = None
     seed: int = 42
     bf16: Optional[bool] = None
     fp16: bool = False

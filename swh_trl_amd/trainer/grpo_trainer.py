@@ -32,7 +32,7 @@ from .. import ops
 from ..engine.config import DecoderConfig, PRESETS, from_hf_config
 from ..engine.decode import DecodeEngine
 from ..engine.model import CausalLM, dw_streams, dw_sync
-from ..optim import FlatAdamW
+from ..optim import FlatAdamW, sync_ref_model
 from .grpo_config import GRPOConfig
 from .utils import generation_batch_indices, left_pad, linear_lr, pad_left_cat, split_tensor_dict, \
     truncate_with_protected_tokens
@@ -191,7 +191,7 @@ class GRPOTrainer:
         self._buffered_inputs = None
         self._metrics = {"train": defaultdict(list), "eval": defaultdict(list)}
         self._engine: Optional[DecodeEngine] = None
-        self._gen_count = 0
+        self._gen_count = 0      # generation batches drawn so far (data-stream position, rollout RNG offset)
         self._shuffle_gen = torch.Generator().manual_seed(a.seed + 17 * self.rank)
         self._batches = None
         self.callbacks = callbacks or []
@@ -209,6 +209,13 @@ class GRPOTrainer:
                                              bool(a.shuffle_dataset)):
             yield [self.train_dataset[i] for i in mine]
 
+    @staticmethod
+    def _is_conversational(example: dict) -> bool:
+        """trl/data_utils.py:31-69 (prompt-only datasets): the prompt is a list of
+        {"role", "content"} messages."""
+        p = example.get("prompt")
+        return isinstance(p, list) and len(p) > 0 and isinstance(p[0], dict) and "role" in p[0] and "content" in p[0]
+
     def _tokenize_prompts(self, examples):
         if "prompt_ids" in examples[0]:
             ids, mask = left_pad([list(x["prompt_ids"]) for x in examples], self.pad_token_id, self.device)
@@ -220,8 +227,14 @@ class GRPOTrainer:
             texts = []
             for x in examples:
                 p = x["prompt"]
-                if isinstance(p, list) and hasattr(tok, "apply_chat_template"):
-                    p = tok.apply_chat_template(p, tokenize=False, add_generation_prompt=True)
+                if self._is_conversational(x):
+                    # data_utils.py:100-116: a trailing assistant turn is continued,
+                    # otherwise the generation prompt is added
+                    last = p[-1]["role"]
+                    if last not in ("user", "assistant"):
+                        raise ValueError(f"Invalid role in the last message: {last}")
+                    p = tok.apply_chat_template(p, continue_final_message=last == "assistant", tokenize=False,
+                                                add_generation_prompt=last == "user")
                 texts.append(p)
             enc = tok(text=texts, return_tensors="pt", padding=True, padding_side="left", add_special_tokens=False)
             ids, mask = enc["input_ids"].to(self.device), enc["attention_mask"].to(self.device).int()
@@ -271,8 +284,14 @@ class GRPOTrainer:
         rewards_per_func = self._calculate_rewards(examples, prompts_text, prompt_ids, prompt_mask, completion_ids,
                                                    completion_mask)
         _trace("rewards")
+        # grpo_trainer.py:1494-1497 / :1933-1938: the rewards of every rank are gathered
+        # (a group of G completions may straddle ranks), the advantages are formed on
+        # the global batch and this rank keeps its own rows
+        rewards_per_func = swh_dist.all_gather_rows(rewards_per_func)
         adv, rewards, gmean, gstd, zstd = ops.group_advantages(rewards_per_func, self.reward_weights,
                                                                self.num_generations, self.scale_rewards)
+        if self.world > 1:
+            adv = adv[self.rank * B:(self.rank + 1) * B]
         out = {"prompt_ids": prompt_ids, "prompt_mask": prompt_mask, "completion_ids": completion_ids,
                "completion_mask": completion_mask, "advantages": adv}
         generate_every = a.steps_per_generation * self.num_iterations
@@ -289,35 +308,59 @@ class GRPOTrainer:
         self.state.num_input_tokens_seen += int(B * P + B * self.max_completion_length) * self.world
         return out
 
+    def _completions_for_rewards(self, examples, ids_h, completion_ids_list):
+        """grpo_trainer.py:1901-1908: decoded completions; for conversational
+        prompts each becomes [{"role": "assistant", "content": bootstrap + text}]
+        where bootstrap is the content of a trailing assistant prompt turn."""
+        tok = self.processing_class
+        if tok is None or not hasattr(tok, "batch_decode"):
+            return completion_ids_list
+        texts = tok.batch_decode(ids_h, skip_special_tokens=True)
+        if not self._is_conversational(examples[0]):
+            return texts
+        out = []
+        for x, t in zip(examples, texts):
+            last = x["prompt"][-1]
+            boot = last["content"] if last["role"] == "assistant" else ""
+            out.append([{"role": "assistant", "content": boot + t}])
+        return out
+
     def _calculate_rewards(self, examples, prompts_text, prompt_ids, prompt_mask, completion_ids, completion_mask):
-        """grpo_trainer.py:1446-1498: reward callables on host (None -> NaN)."""
+        """grpo_trainer.py:1446-1498: reward callables on host (None -> NaN);
+        reward models (nn.Module) score the prompt + completion text, chat-
+        templated for conversational data (:1462-1473)."""
+        import copy
         B = completion_ids.shape[0]
         F = len(self.reward_funcs)
         rpf = torch.zeros(B, F, dtype=torch.float32)
         ids_h = completion_ids.cpu()
         mask_h = completion_mask.cpu().bool()
         completion_ids_list = [row[m].tolist() for row, m in zip(ids_h, mask_h)]
-        tok = self.processing_class
-        if tok is not None and hasattr(tok, "batch_decode"):
-            completions = tok.batch_decode(ids_h, skip_special_tokens=True)
-        else:
-            completions = completion_ids_list
-        prompts = [x.get("prompt") for x in examples]
+        completions = self._completions_for_rewards(examples, ids_h, completion_ids_list)
+        prompts = [copy.deepcopy(x.get("prompt")) for x in examples]  # original_prompts (:1508-1511)
         keys = [k for k in examples[0] if k not in ("prompt", "completion", "completion_ids")]
         kw = {k: [x[k] for x in examples] for k in keys}
         kw["trainer_state"] = self.state
+        conversational = self._is_conversational(examples[0])
         for i, (fn, rtok) in enumerate(zip(self.reward_funcs, self.reward_processing_classes)):
             if isinstance(fn, torch.nn.Module):
-                texts = [str(p) + str(c) for p, c in zip(prompts, completions)]
+                if rtok is None:
+                    raise ValueError("a reward model needs its reward_processing_class (tokenizer)")
+                if conversational:
+                    texts = [rtok.apply_chat_template(p + c, tokenize=False) for p, c in zip(prompts, completions)]
+                else:
+                    texts = [p + c for p, c in zip(prompts, completions)]
                 enc = rtok(text=texts, return_tensors="pt", padding=True, padding_side="right",
                            add_special_tokens=False)
-                enc = {k: v.to(self.device) for k, v in enc.items()}
+                dev = next(fn.parameters()).device
+                enc = {k: v.to(dev) for k, v in enc.items()}
                 with torch.inference_mode():
                     rpf[:, i] = fn(**enc).logits[:, 0].float().cpu()
             else:
                 vals = fn(prompts=prompts, completions=completions, completion_ids=completion_ids_list, **kw)
                 rpf[:, i] = torch.tensor([float("nan") if v is None else float(v) for v in vals],
                                          dtype=torch.float32)
+        self._last_reward_inputs = {"prompts": prompts, "completions": completions}
         return rpf.to(self.device)
 
     # ------------------------------------------------------------------ scoring forward
@@ -395,6 +438,8 @@ class GRPOTrainer:
         if self._step % generate_every == 0 or self._buffered_inputs is None:
             if self._batches is None:
                 self._batches = self._generation_batches()
+                for _ in range(self._gen_count):  # resumed: skip the batches already trained on
+                    next(self._batches)
             gen = self._generate_and_score_completions(next(self._batches))
             n = gen["completion_ids"].shape[0]
             perm = torch.randperm(n, generator=self._shuffle_gen).to(self.device)
@@ -442,15 +487,13 @@ class GRPOTrainer:
                 self.model.on_layer_grads = None
         if ar is not None:
             ar.finish()
-        total = max(1, self.state.max_steps)
-        lr = linear_lr(self.state.global_step, total, a.learning_rate, a.warmup_steps) \
-            if a.lr_scheduler_type == "linear" else a.learning_rate
+        lr = self._current_lr()
         norm = self.optimizer.step(self.model.grad, model_out=self.model.flat, lr=lr)
         self.state.global_step += 1
         _trace(f"optimizer step {self.state.global_step}")
         if self.ref_model is not None and a.sync_ref_model and self.state.global_step % a.ref_model_sync_steps == 0:
             # TR-DPO mixup (callbacks.py:106-131): ref = alpha * policy + (1 - alpha) * ref
-            self.ref_model.flat.mul_(1 - a.ref_model_mixup_alpha).add_(self.model.flat, alpha=a.ref_model_mixup_alpha)
+            sync_ref_model(self.ref_model.flat, self.model.flat, a.ref_model_mixup_alpha)
         loss = sum(o["loss"] for o in outs) if len(outs) > 1 else outs[0]["loss"]
         if len(outs) > 1:
             loss = loss  # per-micro losses already carry the 1/GA row scale
@@ -497,10 +540,131 @@ class GRPOTrainer:
         self.state.log_history.append(log)
         return log
 
+    # ------------------------------------------------------------------ checkpoints
+    def save_model(self, output_dir: Optional[str] = None, _internal_call: bool = False):
+        """Trainer.save_model: the policy in transformers layout (config.json +
+        safetensors) and the tokenizer, on the main process."""
+        from . import checkpoint as ck
+        out = output_dir or self.args.output_dir
+        if out is None:
+            raise ValueError("save_model needs an output_dir")
+        if self.rank == 0:
+            ck.save_pretrained(self.model, out, eos_token_id=self.eos_token_id, pad_token_id=self.pad_token_id)
+            if self.processing_class is not None and hasattr(self.processing_class, "save_pretrained"):
+                self.processing_class.save_pretrained(out)
+        swh_dist.barrier()
+
+    def create_model_card(self, model_name: Optional[str] = None, dataset_name: Optional[str] = None, tags=None):
+        """grpo_trainer.py:2243-2306: README.md model card in output_dir."""
+        from . import checkpoint as ck
+        if self.rank != 0 or not self.args.output_dir:
+            return
+        tags = set([tags] if isinstance(tags, str) else (tags or []))
+        tags.update(self._tag_names)
+        os.makedirs(self.args.output_dir, exist_ok=True)
+        with open(os.path.join(self.args.output_dir, "README.md"), "w") as f:
+            f.write(ck.model_card("GRPO", model_name or os.path.basename(os.path.normpath(self.args.output_dir)),
+                                  "DeepSeekMath, arXiv:2402.03300", ck.GRPO_CITATION, tags))
+
+    def _save_checkpoint(self, model=None, trial=None):
+        """grpo_trainer.py:2234-2241 + transformers Trainer._save_checkpoint:
+        output_dir/checkpoint-<global_step>/ with model, optimizer, scheduler,
+        trainer state and RNG/data-stream state (exact resume)."""
+        import json
+
+        from . import checkpoint as ck
+        a = self.args
+        name = a.hub_model_id.split("/")[-1] if a.hub_model_id else os.path.basename(os.path.normpath(a.output_dir))
+        self.create_model_card(model_name=name)
+        d = os.path.join(a.output_dir, f"checkpoint-{self.state.global_step}")
+        self.save_model(d)
+        if self.rank == 0:
+            if not a.save_only_model:
+                torch.save(ck.optimizer_state_dict(self.model, self.optimizer, a.weight_decay),
+                           os.path.join(d, "optimizer.pt"))
+                torch.save({"last_epoch": self.state.global_step, "_step_count": self.state.global_step + 1,
+                            "base_lrs": [a.learning_rate, a.learning_rate], "_last_lr": [self._current_lr()] * 2},
+                           os.path.join(d, "scheduler.pt"))
+                ck.save_master(self.optimizer, d)
+                if self.ref_model is not None and a.sync_ref_model:  # the mixed reference is trainer state
+                    from safetensors.torch import save_file
+                    save_file({"ref": self.ref_model.flat.detach().cpu()}, os.path.join(d, "swh_ref.safetensors"))
+                torch.save(self._resume_state(), os.path.join(d, "swh_trainer_state.pt"))
+            with open(os.path.join(d, "trainer_state.json"), "w") as f:
+                json.dump(ck.trainer_state_json(self.state, a, a.per_device_train_batch_size), f, indent=2)
+            ck.rotate_checkpoints(a.output_dir, a.save_total_limit)
+        swh_dist.barrier()
+        return d
+
+    def _current_lr(self) -> float:
+        a = self.args
+        return linear_lr(self.state.global_step, max(1, self.state.max_steps), a.learning_rate, a.warmup_steps) \
+            if a.lr_scheduler_type == "linear" else a.learning_rate
+
+    def _resume_state(self) -> dict:
+        """Tensors only (loaded with weights_only=True): the data-stream position,
+        the shuffle generator, the rollouts still buffered for the next steps."""
+        st = {"gen_count": torch.tensor(self._gen_count), "micro_step": torch.tensor(self._step),
+              "shuffle_gen": self._shuffle_gen.get_state(), "global_step": torch.tensor(self.state.global_step),
+              "tokens_seen": torch.tensor(self.state.num_input_tokens_seen)}
+        if self._buffered_inputs is not None:
+            for i, mb in enumerate(self._buffered_inputs):
+                for k, v in mb.items():
+                    if v is not None:
+                        st[f"buf.{i}.{k}"] = v.detach().cpu()
+        return st
+
+    def _load_checkpoint(self, d: str):
+        import json
+
+        from . import checkpoint as ck
+        if os.path.exists(os.path.join(d, "swh_master.safetensors")):
+            from safetensors.torch import load_file
+            self.optimizer.master.copy_(load_file(os.path.join(d, "swh_master.safetensors"))["master"])
+            self.model.flat.copy_(self.optimizer.master)
+        else:  # a transformers checkpoint: the saved weights are the master
+            ck.load_weights_into(self.model, d)
+            self.optimizer.master.copy_(self.model.flat.float())
+        ref_path = os.path.join(d, "swh_ref.safetensors")
+        if self.ref_model is not None and self.args.sync_ref_model and os.path.exists(ref_path):
+            from safetensors.torch import load_file
+            self.ref_model.flat.copy_(load_file(ref_path)["ref"])
+        opt_path = os.path.join(d, "optimizer.pt")
+        if os.path.exists(opt_path):
+            ck.load_optimizer_state_dict(self.model, self.optimizer, torch.load(opt_path, weights_only=True))
+        with open(os.path.join(d, "trainer_state.json")) as f:
+            js = json.load(f)
+        self.state.global_step = int(js["global_step"])
+        self.state.log_history = list(js.get("log_history", []))
+        self.state.num_input_tokens_seen = int(js.get("num_input_tokens_seen", 0))
+        sp = os.path.join(d, "swh_trainer_state.pt")
+        if os.path.exists(sp):
+            st = torch.load(sp, weights_only=True)
+            self._gen_count = int(st["gen_count"])
+            self._step = int(st["micro_step"])
+            self._shuffle_gen.set_state(st["shuffle_gen"])
+            bufs = {}
+            for k, v in st.items():
+                if k.startswith("buf."):
+                    _, i, name = k.split(".", 2)
+                    bufs.setdefault(int(i), {})[name] = v.to(self.device)
+            self._buffered_inputs = [bufs[i] for i in sorted(bufs)] if bufs else None
+        else:  # transformers checkpoint: position from the step count
+            self._gen_count = self.state.global_step * self.args.gradient_accumulation_steps // (
+                self.args.steps_per_generation * self.num_iterations)
+            self._step = self.state.global_step * self.args.gradient_accumulation_steps
+        self._batches = None
+
     def train(self, resume_from_checkpoint=None):
         a = self.args
         if self.train_dataset is None:
             raise ValueError("train_dataset is required")
+        if resume_from_checkpoint:
+            from . import checkpoint as ck
+            d = ck.latest_checkpoint(a.output_dir) if resume_from_checkpoint is True else resume_from_checkpoint
+            if d is None:
+                raise ValueError(f"No valid checkpoint found in output directory ({a.output_dir})")
+            self._load_checkpoint(d)
         if a.max_steps and a.max_steps > 0:
             total = a.max_steps
         else:
@@ -509,12 +673,15 @@ class GRPOTrainer:
                                          / a.gradient_accumulation_steps * a.num_train_epochs)))
         self.state.max_steps = total
         log_every = int(a.logging_steps) if a.logging_steps >= 1 else max(1, int(total * a.logging_steps))
+        save_every = int(a.save_steps) if a.save_steps >= 1 else max(1, int(total * a.save_steps))
         t0 = time.time()
-        for _ in range(total):
+        while self.state.global_step < total:
             self.training_step_group()
             if self.state.global_step % log_every == 0 or self.state.global_step == total:
                 log = self._flush_logs()
                 log["train_runtime"] = time.time() - t0
                 if self.rank == 0:
                     print(log, flush=True)
+            if a.save_strategy == "steps" and a.output_dir and self.state.global_step % save_every == 0:
+                self._save_checkpoint()
         return self.state

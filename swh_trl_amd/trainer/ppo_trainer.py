@@ -22,6 +22,7 @@ tables, hub pushes, checkpoints.
 from __future__ import annotations
 
 import math
+import os
 import time
 from collections import defaultdict
 from typing import Optional
@@ -429,6 +430,52 @@ class PPOTrainer:
         self.state.log_history.append(log)
         return log
 
+    # ------------------------------------------------------------------ checkpoints
+    def save_model(self, output_dir: Optional[str] = None, _internal_call: bool = False):
+        """ppo_trainer.py:332-346: only the policy is saved (transformers layout)."""
+        from . import checkpoint as ck
+        out = output_dir or self.args.output_dir
+        if self.rank == 0:
+            ck.save_pretrained(self.policy_model, out, eos_token_id=self.eos_token_id, pad_token_id=self.pad_token_id)
+            if self.processing_class is not None and hasattr(self.processing_class, "save_pretrained"):
+                self.processing_class.save_pretrained(out)
+        swh_dist.barrier()
+
+    def create_model_card(self, model_name: Optional[str] = None, dataset_name: Optional[str] = None, tags=None):
+        """ppo_trainer.py:760-: README.md model card in output_dir."""
+        from . import checkpoint as ck
+        if self.rank != 0 or not self.args.output_dir:
+            return
+        tags = set([tags] if isinstance(tags, str) else (tags or []))
+        tags.update(self._tag_names)
+        os.makedirs(self.args.output_dir, exist_ok=True)
+        with open(os.path.join(self.args.output_dir, "README.md"), "w") as f:
+            f.write(ck.model_card("PPO", model_name or os.path.basename(os.path.normpath(self.args.output_dir)),
+                                  "Fine-Tuning Language Models from Human Preferences, arXiv:1909.08593",
+                                  ck.PPO_CITATION, tags))
+
+    def _save_checkpoint(self, model=None, trial=None):
+        """ppo_trainer.py:752-758 + transformers Trainer._save_checkpoint: the
+        policy weights, the AdamW state of the policy + value wrapper
+        (PolicyAndValueWrapper parameter names), trainer state, model card."""
+        import json
+
+        from . import checkpoint as ck
+        a = self.args
+        self.create_model_card(model_name=os.path.basename(os.path.normpath(a.output_dir)))
+        d = os.path.join(a.output_dir, f"checkpoint-{self.state.global_step}")
+        self.save_model(d)
+        if self.rank == 0:
+            parts = [("policy.", self.policy_model, self.opt_policy), ("value_model.", self.value_model, self.opt_value)]
+            torch.save(ck.optimizer_state_dict(self.policy_model, self.opt_policy, a.weight_decay, parts=parts),
+                       os.path.join(d, "optimizer.pt"))
+            with open(os.path.join(d, "trainer_state.json"), "w") as f:
+                js = ck.trainer_state_json(self.state, a, a.per_device_train_batch_size)
+                js["episode"] = self.state.episode
+                json.dump(js, f, indent=2)
+        swh_dist.barrier()
+        return d
+
     def train(self):
         a = self.args
         self.state.global_step = 0
@@ -444,4 +491,8 @@ class PPOTrainer:
                 log["eps"] = int(self.state.episode / max(time.time() - t0, 1e-9))
                 if self.rank == 0:
                     print(log, flush=True)
+            save_every = int(a.save_steps) if a.save_steps >= 1 else max(1, math.ceil(a.num_total_batches * a.save_steps))
+            if getattr(a, "save_strategy", "steps") == "steps" and a.output_dir and \
+                    self.state.global_step % save_every == 0:
+                self._save_checkpoint()
         return self.state

@@ -1,0 +1,101 @@
+"""Checkpoint format on the host: the saved directory is what
+transformers' from_pretrained reads (config + safetensors, tied head dropped),
+and optimizer.pt is a torch AdamW state_dict over the transformers parameters
+in the Trainer's decay / no-decay grouping (transformers Trainer.create_optimizer,
+get_decay_parameter_names), loadable by torch.optim.AdamW."""
+import os
+
+import pytest
+import torch
+
+from swh_trl_amd.engine import CausalLM
+from swh_trl_amd.engine.config import tiny_llama, tiny_qwen2
+from swh_trl_amd.trainer import checkpoint as ck
+
+
+def _cpu_model(cfg, dtype=torch.bfloat16, head="lm"):
+    return CausalLM(cfg, "cpu", seed=2, dtype=dtype, trainable=False, head=head)
+
+
+@pytest.mark.parametrize("cfg_fn,dtype", [(tiny_qwen2, torch.bfloat16), (tiny_llama, torch.bfloat16),
+                                          (tiny_qwen2, torch.float32)])
+def test_save_pretrained_loads_in_transformers(tmp_path, cfg_fn, dtype):
+    from transformers import AutoModelForCausalLM
+    m = _cpu_model(cfg_fn(512, 2), dtype)
+    ck.save_pretrained(m, str(tmp_path), eos_token_id=1, pad_token_id=0)
+    assert os.path.exists(tmp_path / "config.json") and os.path.exists(tmp_path / "model.safetensors")
+    hf = AutoModelForCausalLM.from_pretrained(str(tmp_path), dtype=dtype)
+    assert hf.config.model_type == m.cfg.model_type
+    ref = hf.state_dict()
+    for k, v in m.hf_state_dict().items():
+        assert torch.equal(ref[k], v), k
+    # and back into the engine's layout
+    from swh_trl_amd.trainer.grpo_trainer import load_model
+    m2 = load_model(str(tmp_path), "cpu", trainable=False, dtype=dtype)
+    assert m2.cfg == m.cfg and torch.equal(m2.flat, m.flat)
+
+
+def test_score_head_saves_as_sequence_classifier(tmp_path):
+    from transformers import AutoModelForSequenceClassification
+    m = _cpu_model(tiny_qwen2(512, 2), head="score")
+    ck.save_pretrained(m, str(tmp_path))
+    hf = AutoModelForSequenceClassification.from_pretrained(str(tmp_path), dtype=torch.bfloat16)
+    assert hf.config.num_labels == 1 and torch.equal(hf.score.weight, m.p["score"])
+
+
+def test_sharded_save(tmp_path, monkeypatch):
+    from transformers import AutoModelForCausalLM
+    monkeypatch.setattr(ck, "SHARD_BYTES", 1 << 20)
+    m = _cpu_model(tiny_qwen2(512, 2))
+    ck.save_pretrained(m, str(tmp_path))
+    assert os.path.exists(tmp_path / "model.safetensors.index.json")
+    hf = AutoModelForCausalLM.from_pretrained(str(tmp_path), dtype=torch.bfloat16)
+    assert torch.equal(hf.model.embed_tokens.weight, m.p["embed"])
+
+
+def test_optimizer_state_is_a_torch_adamw_state_dict(tmp_path):
+    from transformers import Qwen2Config, Qwen2ForCausalLM
+
+    from swh_trl_amd.optim import FlatAdamW
+    m = _cpu_model(tiny_qwen2(512, 2), torch.float32)
+    opt = FlatAdamW(m.numel, "cpu", lr=3e-4, weight_decay=0.1, no_decay_ranges=m.no_decay_ranges())
+    g = torch.Generator().manual_seed(0)
+    opt.exp_avg.copy_(torch.randn(m.numel, generator=g))
+    opt.exp_avg_sq.copy_(torch.rand(m.numel, generator=g))
+    opt.step_count = 7
+    sd = ck.optimizer_state_dict(m, opt, 0.1)
+    torch.save(sd, tmp_path / "optimizer.pt")
+    sd = torch.load(tmp_path / "optimizer.pt", weights_only=True)
+    c = m.cfg
+    hf = Qwen2ForCausalLM(Qwen2Config(vocab_size=c.vocab_size, hidden_size=c.hidden_size,
+                                      intermediate_size=c.intermediate_size, num_hidden_layers=c.num_hidden_layers,
+                                      num_attention_heads=c.num_attention_heads,
+                                      num_key_value_heads=c.num_key_value_heads, tie_word_embeddings=True))
+    names = [n for n, _ in hf.named_parameters()]
+    assert names == ck.hf_param_order(m)
+    # the Trainer's grouping, built from transformers' own decay-name rule
+    from transformers import Trainer
+    decay = Trainer.get_decay_parameter_names(Trainer.__new__(Trainer), hf)
+    params = dict(hf.named_parameters())
+    groups = [{"params": [params[n] for n in names if n in decay], "weight_decay": 0.1},
+              {"params": [params[n] for n in names if n not in decay], "weight_decay": 0.0}]
+    topt = torch.optim.AdamW(groups, lr=3e-4)
+    topt.load_state_dict(sd)
+    exp_m, exp_v = ck._flat_views(m, opt.exp_avg), ck._flat_views(m, opt.exp_avg_sq)
+    for n in names:
+        st = topt.state[params[n]]
+        assert int(st["step"]) == 7
+        assert torch.equal(st["exp_avg"], exp_m[n]) and torch.equal(st["exp_avg_sq"], exp_v[n]), n
+    # and back into a fresh flat optimizer
+    opt2 = FlatAdamW(m.numel, "cpu", lr=1.0, weight_decay=0.1)
+    ck.load_optimizer_state_dict(m, opt2, sd)
+    assert opt2.step_count == 7 and opt2.lr == pytest.approx(3e-4)
+    assert torch.equal(opt2.exp_avg, opt.exp_avg) and torch.equal(opt2.exp_avg_sq, opt.exp_avg_sq)
+
+
+def test_checkpoint_rotation(tmp_path):
+    for s in (1, 2, 3, 10):
+        os.makedirs(tmp_path / f"checkpoint-{s}")
+    assert ck.latest_checkpoint(str(tmp_path)).endswith("checkpoint-10")
+    ck.rotate_checkpoints(str(tmp_path), 2)
+    assert sorted(os.listdir(tmp_path)) == ["checkpoint-10", "checkpoint-3"]

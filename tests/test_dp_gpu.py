@@ -21,7 +21,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, q, steps):
+def _worker(rank, world, port, q, steps, pdb=8, ga=2):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port), SWH_DIST_BACKEND="gloo")
     try:
@@ -33,7 +33,7 @@ def _worker(rank, world, port, q, steps):
         def rew(prompts=None, completions=None, completion_ids=None, **kw):
             return [float(len(set(c)) % 5) for c in completion_ids]
 
-        args = GRPOConfig(per_device_train_batch_size=8, gradient_accumulation_steps=2, num_generations=4,
+        args = GRPOConfig(per_device_train_batch_size=pdb, gradient_accumulation_steps=ga, num_generations=4,
                           max_prompt_length=8, max_completion_length=16, max_steps=steps, learning_rate=1e-3,
                           generation_kwargs={"eos_token_id": 1, "pad_token_id": 0, "min_new_tokens": 16},
                           logging_steps=1, seed=7)
@@ -41,7 +41,9 @@ def _worker(rank, world, port, q, steps):
         tr.train()
         torch.cuda.synchronize()
         flat = tr.model.flat.float().cpu().numpy()
-        q.put((rank, (hashlib.sha256(flat.tobytes()).hexdigest(), float(flat.astype("float64").sum()))))
+        log = tr.state.log_history[-1]
+        q.put((rank, (hashlib.sha256(flat.tobytes()).hexdigest(), float(flat.astype("float64").sum()),
+                      log["reward"], log["loss"])))
     except Exception as e:  # surface the failure to the parent
         q.put((rank, repr(e)))
     finally:
@@ -50,11 +52,11 @@ def _worker(rank, world, port, q, steps):
             dist.destroy_process_group()
 
 
-def _run(world, steps):
+def _run(world, steps, pdb=8, ga=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 31500 + (os.getpid() % 1000) + world
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q, steps)) for r in range(world)]
+    port = 31500 + (os.getpid() % 1000) + world + 7 * pdb
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, steps, pdb, ga)) for r in range(world)]
     for p in ps:
         p.start()
     got = dict(q.get(timeout=240) for _ in range(world))
@@ -70,6 +72,17 @@ def test_dp_two_ranks_keep_replicas_identical():
     assert got[0][0] == got[1][0]
     single = _run(1, 2)
     assert single[0][0] != got[0][0]
+
+
+def test_dp_groups_straddling_ranks():
+    """per_device_train_batch_size 2 with G = 4 on two ranks: every group of 4
+    completions is split over both ranks.  The reference gathers the rewards
+    (grpo_trainer.py:1497), forms advantages on the global batch and keeps each
+    rank's slice (:1933-1938); the replicas stay identical and both ranks log
+    the same (global) mean reward."""
+    got = _run(2, 2, pdb=2, ga=1)
+    assert got[0][0] == got[1][0]
+    assert got[0][2] == got[1][2]
 
 
 def test_bench_launches_n_ranks_itself():

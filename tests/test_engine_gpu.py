@@ -474,3 +474,52 @@ def test_llama_grpo_step_with_frozen_ref_kl(dev):
     first, last = state.log_history[0], state.log_history[-1]
     assert abs(first["kl"]) < 1e-3, first  # scoring vs training forward: bf16-level differences only
     assert last["kl"] >= 0 and all(v == v for v in (last["loss"], last["grad_norm"], last["kl"]))
+
+
+def test_checkpoint_resume_is_bit_identical_and_loads_in_transformers(dev, tmp_path):
+    """a run checkpointed after step 1 and resumed from that
+    checkpoint ends with the same weights, bit for bit, as the run that never
+    stopped (master weights, AdamW moments, data stream, shuffle and rollout RNG
+    all restored); the checkpoint loads in transformers and its logits match the
+    engine's (bf16 tolerance)."""
+    from transformers import AutoModelForCausalLM
+
+    from swh_trl_amd.engine import CausalLM, tiny_qwen2
+    from swh_trl_amd.trainer import GRPOConfig, GRPOTrainer
+    cfg = tiny_qwen2(512, 2)
+    ds = [{"prompt": None, "prompt_ids": list(range(3 + i, 11 + i))} for i in range(16)]
+
+    def rew(prompts=None, completions=None, completion_ids=None, **kw):
+        return [float(len(set(c)) % 5) for c in completion_ids]
+
+    def trainer(out, steps):
+        args = GRPOConfig(output_dir=str(out), per_device_train_batch_size=8, gradient_accumulation_steps=2,
+                          num_generations=4, max_prompt_length=8, max_completion_length=16, max_steps=steps,
+                          learning_rate=1e-3, save_steps=1, logging_steps=1, seed=3, weight_decay=0.01,
+                          generation_kwargs={"eos_token_id": 1, "pad_token_id": 0})
+        return GRPOTrainer(model=CausalLM(cfg, dev, seed=4, init_std=0.05), reward_funcs=rew, args=args,
+                           train_dataset=ds)
+
+    full = trainer(tmp_path / "a", 3)
+    full.train()
+    ref_flat, ref_master = full.model.flat.clone(), full.optimizer.master.clone()
+    resumed = trainer(tmp_path / "b", 3)
+    resumed.args.save_steps = 10 ** 9
+    resumed.train(resume_from_checkpoint=str(tmp_path / "a" / "checkpoint-1"))
+    assert resumed.state.global_step == 3
+    assert torch.equal(resumed.optimizer.master, ref_master)
+    assert torch.equal(resumed.model.flat, ref_flat)
+    # the latest checkpoint, read by transformers
+    d = tmp_path / "a" / "checkpoint-3"
+    for f in ("config.json", "model.safetensors", "optimizer.pt", "scheduler.pt", "trainer_state.json",
+              "swh_master.safetensors", "swh_trainer_state.pt"):
+        assert (d / f).exists(), f
+    assert (tmp_path / "a" / "README.md").exists()
+    hf = AutoModelForCausalLM.from_pretrained(str(d), dtype=torch.float32).to(dev).eval()
+    g = torch.Generator().manual_seed(9)
+    ids = torch.randint(0, cfg.vocab_size, (2, 20), generator=g).to(dev)
+    with torch.no_grad():
+        mine = full.model.logits(full.model.hidden_states(ids)).float()
+        theirs = hf(input_ids=ids).logits.float()
+    err = (mine - theirs).abs().max().item()
+    assert err <= 0.03 * theirs.abs().max().item() + 0.03, err

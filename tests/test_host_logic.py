@@ -96,6 +96,17 @@ def test_split_and_shuffle_dicts():
     assert [("abcdef"[int(i)]) for i in s["x"]] == s["y"]
 
 
+def test_generation_batches_reshuffle_every_epoch():
+    """One RepeatSampler (one generator) across epochs, as the reference's
+    dataloader re-iterates it: epoch 2 draws a fresh permutation, equal to the
+    sampler's second pass."""
+    two = list(U.generation_batch_indices(12, 2, 6, 6, 0, seed=4, shuffle=True, epochs=2))
+    s = U.RepeatSampler(range(12), 2, 3, 1, shuffle=True, seed=4)
+    ref = list(s) + list(s)
+    assert [i for b in two for i in b] == ref
+    assert two[:4] != two[4:]
+
+
 def test_linear_lr():
     assert U.linear_lr(0, 10, 1.0) == 1.0 and U.linear_lr(5, 10, 1.0) == 0.5 and U.linear_lr(10, 10, 1.0) == 0.0
     assert U.linear_lr(1, 10, 1.0, warmup=2) == 0.5
@@ -109,7 +120,8 @@ def _worker(rank, world, port, q):
     buf = torch.full((1000,), float(r + 1), dtype=torch.bfloat16)
     dist.allreduce_mean_(buf, bucket_elems=300)
     gens = U.generation_batch_indices(40, 4, 16, 8, r, seed=7, shuffle=True, epochs=1)
-    q.put((r, buf.float().mean().item(), [list(b) for b in gens], dist.all_max(float(r))))
+    rows = dist.all_gather_rows(torch.full((3, 2), float(r)) + torch.arange(3.0).view(3, 1))
+    q.put((r, buf.float().mean().item(), [list(b) for b in gens], dist.all_max(float(r)), rows.tolist()))
     torch.distributed.destroy_process_group()
 
 
@@ -123,8 +135,11 @@ def test_dp_exchange_and_sharding_gloo():
     res = sorted([q.get(timeout=120) for _ in range(2)])
     for p in ps:
         p.join(timeout=60)
-    assert all(abs(m - 1.5) < 1e-6 for _, m, _, _ in res)
-    assert all(mx == 1.0 for _, _, _, mx in res)
+    assert all(abs(m - 1.5) < 1e-6 for _, m, _, _, _ in res)
+    assert all(mx == 1.0 for _, _, _, mx, _ in res)
+    # the reward gather (grpo_trainer.py:1497): rank-ordered rows, identical on every rank
+    exp = [[0.0, 0.0], [1.0, 1.0], [2.0, 2.0], [1.0, 1.0], [2.0, 2.0], [3.0, 3.0]]
+    assert res[0][4] == exp and res[1][4] == exp
     b0, b1 = res[0][2], res[1][2]
     assert len(b0) == len(b1) == 10  # 40 prompts / 4 unique prompts per global generation batch
     glob = list(U.RepeatSampler(range(40), 4, 4, 1, shuffle=True, seed=7))

@@ -1,0 +1,167 @@
+"""Reward paths and the TR-DPO reference sync of GRPOTrainer (-m gpu).
+
+* conversational prompts (grpo_trainer.py:1534, :1901-1908; data_utils.py
+  :100-116): the chat template continues a trailing assistant turn, and reward
+  callables receive completions as [{"role": "assistant", "content":
+  bootstrap + text}];
+* a reward model given as an nn.Module (a transformers sequence classifier,
+  :1462-1473): it scores the chat-templated prompt + completion messages
+  (plain prompt + completion text otherwise), padded right, logits[:, 0];
+* sync_ref_model (callbacks.py:106-131): every ref_model_sync_steps the
+  reference becomes ref * (1 - alpha) + alpha * policy, rounded as torch's
+  mul_ / add_ on the parameter dtype.
+"""
+import os
+import sys
+
+import pytest
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from fake_tokenizer import make_tokenizer  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+V = 512
+
+
+def _cfg():
+    from swh_trl_amd.engine import tiny_qwen2
+    return tiny_qwen2(V, 2)
+
+
+def _classifier(dev):
+    from transformers import Qwen2Config, Qwen2ForSequenceClassification
+    torch.manual_seed(0)
+    hc = Qwen2Config(vocab_size=V, hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=2,
+                     num_key_value_heads=1, num_labels=1, pad_token_id=0)
+    return Qwen2ForSequenceClassification(hc).to(dev).eval()
+
+
+@pytest.mark.parametrize("bootstrap", [False, True])
+def test_conversational_prompts_and_reward_model(bootstrap):
+    from swh_trl_amd.trainer import GRPOConfig, GRPOTrainer
+    dev = torch.device("cuda:0")
+    tok = make_tokenizer(V)
+    g = torch.Generator().manual_seed(1)
+
+    def conv(i):
+        words = " ".join(f"w{int(x)}" for x in torch.randint(5, V, (4 + i % 3,), generator=g))
+        p = [{"role": "system", "content": "w9 w10"}, {"role": "user", "content": words}]
+        if bootstrap:
+            p.append({"role": "assistant", "content": "w11 w12"})
+        return {"prompt": p, "tag": i}
+
+    ds = [conv(i) for i in range(8)]
+    seen = {}
+
+    def rew_fn(prompts=None, completions=None, completion_ids=None, tag=None, trainer_state=None, **kw):
+        seen.setdefault("calls", []).append((prompts, completions, completion_ids, tag))
+        return [float(len(c[0]["content"].split()) % 3) for c in completions]
+
+    rm = _classifier(dev)
+    args = GRPOConfig(per_device_train_batch_size=8, gradient_accumulation_steps=1, num_generations=4,
+                      max_prompt_length=32, max_completion_length=12, learning_rate=1e-4, max_steps=1, seed=2,
+                      shuffle_dataset=False, logging_steps=1, save_strategy="no")
+    tr = GRPOTrainer(model=_cfg(), reward_funcs=[rew_fn, rm], args=args, train_dataset=ds, processing_class=tok,
+                     reward_processing_classes=[None, tok])
+    got = {}
+    calc = tr._calculate_rewards
+
+    def capture(examples, *a):
+        out = calc(examples, *a)
+        got["rpf"], got["examples"] = out.detach().cpu().clone(), examples
+        got["ids"] = a[3].detach().cpu().clone()
+        got["mask"] = a[4].detach().cpu().clone()
+        return out
+
+    tr._calculate_rewards = capture
+    tr.train()
+    prompts, completions, cids, tags = seen["calls"][0]
+    examples = got["examples"]
+    assert tags == [x["tag"] for x in examples]
+    # the prompts the reward functions see are the originals, untouched
+    assert prompts == [x["prompt"] for x in examples]
+    texts = tok.batch_decode(got["ids"], skip_special_tokens=True)
+    boot = "w11 w12" if bootstrap else ""
+    assert completions == [[{"role": "assistant", "content": boot + t}] for t in texts]
+    assert cids == [r[m.bool()].tolist() for r, m in zip(got["ids"], got["mask"])]
+    # the prompt token ids: the chat template continues a trailing assistant turn
+    p0 = tok.apply_chat_template(examples[0]["prompt"], tokenize=False, continue_final_message=bootstrap,
+                                 add_generation_prompt=not bootstrap)
+    assert p0.endswith("w11 w12") if bootstrap else p0.endswith("<assistant> ")
+    # the reward model: logits[:, 0] on the chat-templated prompt + completion
+    msgs = [tok.apply_chat_template(x["prompt"] + c, tokenize=False) for x, c in zip(examples, completions)]
+    enc = tok(text=msgs, return_tensors="pt", padding=True, padding_side="right", add_special_tokens=False)
+    with torch.inference_mode():
+        exp = rm(**{k: v.to(dev) for k, v in enc.items()}).logits[:, 0].float().cpu()
+    torch.testing.assert_close(got["rpf"][:, 1], exp)
+    torch.testing.assert_close(got["rpf"][:, 0], torch.tensor([float(len(c[0]["content"].split()) % 3)
+                                                               for c in completions]))
+
+
+def test_reward_model_plain_text_prompts():
+    """Non-conversational text prompts: the reward model scores prompt + completion text."""
+    from swh_trl_amd.trainer import GRPOConfig, GRPOTrainer
+    dev = torch.device("cuda:0")
+    tok = make_tokenizer(V)
+    ds = [{"prompt": " ".join(f"w{5 + (7 * i + j) % 400}" for j in range(6)) + " "} for i in range(4)]
+    rm = _classifier(dev)
+    args = GRPOConfig(per_device_train_batch_size=8, gradient_accumulation_steps=1, num_generations=4,
+                      max_prompt_length=16, max_completion_length=8, max_steps=1, seed=3, shuffle_dataset=False,
+                      save_strategy="no")
+    tr = GRPOTrainer(model=_cfg(), reward_funcs=rm, args=args, train_dataset=ds, processing_class=tok,
+                     reward_processing_classes=[tok])
+    got = {}
+    calc = tr._calculate_rewards
+
+    def capture(examples, *a):
+        out = calc(examples, *a)
+        got["rpf"], got["examples"], got["ids"] = out.cpu().clone(), examples, a[3].cpu().clone()
+        return out
+
+    tr._calculate_rewards = capture
+    tr.train()
+    texts = [x["prompt"] + c for x, c in zip(got["examples"], tok.batch_decode(got["ids"], skip_special_tokens=True))]
+    enc = tok(text=texts, return_tensors="pt", padding=True, padding_side="right", add_special_tokens=False)
+    with torch.inference_mode():
+        exp = rm(**{k: v.to(dev) for k, v in enc.items()}).logits[:, 0].float().cpu()
+    torch.testing.assert_close(got["rpf"][:, 0], exp)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_sync_ref_model_kernel_matches_callback_formula(dtype):
+    """swh_ema_mix == SyncRefModelCallback._sync_target_model on the same dtype:
+    target.mul_(1 - alpha).add_(copy, alpha=alpha) (torch ops on the GPU)."""
+    from swh_trl_amd.optim import sync_ref_model
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(4)
+    ref = torch.randn(1_000_003, generator=g).to(dtype).to(dev)
+    pol = torch.randn(1_000_003, generator=g).to(dtype).to(dev)
+    for alpha in (0.6, 0.1, 0.9):
+        exp = ref.clone().mul_(1.0 - alpha).add_(pol, alpha=alpha)
+        got = ref.clone()
+        sync_ref_model(got, pol, alpha)
+        assert torch.equal(got, exp), (dtype, alpha, (got.float() - exp.float()).abs().max().item())
+
+
+def test_trainer_syncs_reference_every_n_steps():
+    from swh_trl_amd.engine import CausalLM
+    from swh_trl_amd.trainer import GRPOConfig, GRPOTrainer
+    dev = torch.device("cuda:0")
+    ds = [{"prompt": None, "prompt_ids": list(range(5 + i, 13 + i))} for i in range(16)]
+
+    def rew(completion_ids=None, **kw):
+        return [float(len(set(c)) % 5) for c in completion_ids]
+
+    args = GRPOConfig(per_device_train_batch_size=8, gradient_accumulation_steps=1, num_generations=4,
+                      max_prompt_length=8, max_completion_length=8, learning_rate=1e-3, beta=0.04, max_steps=3,
+                      sync_ref_model=True, ref_model_sync_steps=2, ref_model_mixup_alpha=0.6, seed=1,
+                      save_strategy="no", generation_kwargs={"eos_token_id": 1, "pad_token_id": 0})
+    tr = GRPOTrainer(model=CausalLM(_cfg(), dev, seed=5, init_std=0.05), reward_funcs=rew, args=args,
+                     train_dataset=ds)
+    ref0 = tr.ref_model.flat.clone()
+    tr.training_step_group()
+    assert torch.equal(tr.ref_model.flat, ref0)            # step 1: no sync
+    tr.training_step_group()                               # step 2: sync
+    exp = ref0.clone().mul_(1 - 0.6).add_(tr.model.flat, alpha=0.6)
+    assert torch.equal(tr.ref_model.flat, exp)
