@@ -228,10 +228,11 @@ int swh_adamw(float *master, float *exp_avg, float *exp_avg_sq, const void *grad
               int32_t n_no_decay, void *stream);
 /* TR-DPO reference-model sync (trl/trainer/callbacks.py:106-131, SyncRefModelCallback
  * ._sync_target_model, run every ref_model_sync_steps by grpo_trainer.py:1032-1033):
- * target = target * (1 - alpha) + alpha * src over a flat parameter buffer,
- * rounded to the parameter dtype after the multiply and after the add as torch's
- * mul_ / add_(alpha=) do.  dtype bf16 or f32. */
-int swh_ema_mix(void *target, const void *src, int dtype, int64_t N, float alpha, void *stream);
+ * target = target * keep + alpha * src over a flat parameter buffer, keep =
+ * float(1 - alpha) formed by the caller in double precision (torch casts the
+ * Python scalar 1 - alpha), rounded to the parameter dtype after the multiply and
+ * after the add as torch's mul_ / add_(alpha=) do.  dtype bf16 or f32. */
+int swh_ema_mix(void *target, const void *src, int dtype, int64_t N, float keep, float alpha, void *stream);
 /* dst_f32[i] += src[i] (bf16/f32) — accumulate micro-batch grads in fp32. */
 int swh_accumulate(float *dst, const void *src, int dtype, int64_t N, float scale, void *stream);
 
@@ -308,6 +309,18 @@ int swh_attn_bwd_parts(const void *q, const void *k, const void *v, const void *
  * total_rows = sum of rows, njobs <= 256.  Run once per generate(): the policy update changes
  * W and w (transformers applies w inside Qwen2RMSNorm every token). */
 int swh_fold_norm(const void *jobs, int32_t njobs, int64_t total_rows, void *stream);
+
+/* Embedding weight gradient, deterministic (no atomics): grad_table[id] +=
+ * sum of dy rows whose token is id, rows visited in the order given by a STABLE
+ * sort of the ids (sorted_ids int64 [N], order int64 [N] = the sort's
+ * permutation; ids outside [0, V) are skipped), summed in fp32 and folded in
+ * once: bf16: g = bf16(g + bf16(sum)), f32: g += sum.  dy [N, H] and
+ * grad_table [V, H] of `dtype`; workspace f32 >= swh_embedding_bwd_workspace_bytes.
+ * Replaces the embedding backward (torch index_add_ / embedding_dense_backward)
+ * of the reference's training forward (grpo_trainer.py:1249). */
+int64_t swh_embedding_bwd_workspace_bytes(int64_t N, int64_t H);
+int swh_embedding_bwd(const int64_t *sorted_ids, const int64_t *order, const void *dy, int64_t N, int64_t H, int64_t V,
+                      void *grad_table, int32_t dtype, float *workspace, void *stream);
 
 /* x[b, :] = table[ids[b], :] (bf16 rows of width H, H % 16 == 0); ss_out f32
  * [B, H/16] nullable: per 16-column chunk sums of squares of each row (the

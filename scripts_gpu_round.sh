@@ -15,6 +15,7 @@ for step in "$@"; do
   case $step in
     gpu) run gpu 1100 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
     gpuall) run gpuall 1100 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread ;;
+    new2) run new2 900 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -k "rewards or checkpoint or dp_ or step_parity" ;;
     newt) run newt 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread -k "step_parity or adamw or bench_launches or masked_whiten" ;;
     tune) SWH_GEMM_TUNING=tune SWH_GEMM_TABLE=gpurun_out/gemm_tuned.csv run tune 900 python bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
     benchtuned) SWH_GEMM_TABLE=gpurun_out/gemm_tuned.csv run benchtuned 600 python bench.py --steps 3 --warmup 2 --no-cpu-baseline ;;

@@ -66,7 +66,7 @@ SIGNATURES = {
     "swh_adamw": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32,
                           c_i64, c_vp, c_vp, c_i32, c_vp]),
     "swh_accumulate": (c_i32, [c_vp, c_vp, c_i32, c_i64, c_f32, c_vp]),
-    "swh_ema_mix": (c_i32, [c_vp, c_vp, c_i32, c_i64, c_f32, c_vp]),
+    "swh_ema_mix": (c_i32, [c_vp, c_vp, c_i32, c_i64, c_f32, c_f32, c_vp]),
     "swh_rmsnorm_fwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_vp, c_vp, c_i32, c_vp]),
     "swh_rmsnorm_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp]),
     "swh_rmsnorm_dw_accum": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_vp]),
@@ -78,6 +78,8 @@ SIGNATURES = {
     "swh_attn_bwd_parts": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i64, c_i32, c_f32, c_vp,
                                    c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp]),
     "swh_fold_norm": (c_i32, [c_vp, c_i32, c_i64, c_vp]),
+    "swh_embedding_bwd_workspace_bytes": (c_i64, [c_i64, c_i64]),
+    "swh_embedding_bwd": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp]),
     "swh_embed_gather": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "swh_qkv_rope": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i32,
                              c_i32, c_vp]),

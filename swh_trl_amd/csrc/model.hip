@@ -533,6 +533,87 @@ __global__ __launch_bounds__(256) void qkv_rope_f32_kernel(float *__restrict__ q
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Embedding weight gradient without atomics (deterministic): token rows are
+// visited in the order of the stably sorted ids.  Phase 1: each block of
+// kEmbPiece sorted positions sums its pieces of id-runs into fp32 rows of the
+// workspace (row = the piece's first sorted position).  Phase 2: the head of
+// each run adds its pieces in sorted order (a run continues at the next block
+// start) and folds the sum into the gradient row once:
+// g[id] = round(g[id] + round(sum)) — torch's fp32-accumulating embedding
+// backward followed by the AccumulateGrad add (tied lm-head gradient first).
+// ---------------------------------------------------------------------------
+constexpr int kEmbPiece = 32;
+
+template <int DT>
+__global__ __launch_bounds__(128) void embed_bwd_piece_kernel(const int64_t *__restrict__ sid,
+                                                              const int64_t *__restrict__ order,
+                                                              const typename Elem<DT>::T *__restrict__ dy, int64_t N,
+                                                              int64_t H, float *__restrict__ ws) {
+    constexpr int PV = kPerVec<DT>;
+    const int64_t c0 = ((int64_t)blockIdx.y * 128 + threadIdx.x) * PV;
+    if (c0 >= H) return;
+    const int64_t b0 = (int64_t)blockIdx.x * kEmbPiece, b1 = min(N, b0 + kEmbPiece);
+    float acc[PV];
+#pragma unroll
+    for (int k = 0; k < PV; ++k) acc[k] = 0.f;
+    int64_t start = b0, cur = sid[b0];
+    auto flush = [&](int64_t at) {
+        float4 *o = reinterpret_cast<float4 *>(ws + at * H + c0);
+#pragma unroll
+        for (int k = 0; k < PV / 4; ++k) o[k] = float4{acc[4 * k], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3]};
+    };
+    for (int64_t p = b0; p < b1; ++p) {
+        const int64_t id = sid[p];
+        if (id != cur) {
+            flush(start);
+#pragma unroll
+            for (int k = 0; k < PV; ++k) acc[k] = 0.f;
+            start = p;
+            cur = id;
+        }
+        float x[PV];
+        unpack16<DT>(*reinterpret_cast<const uint4 *>(dy + order[p] * H + c0), x);
+#pragma unroll
+        for (int k = 0; k < PV; ++k) acc[k] += x[k];
+    }
+    flush(start);
+}
+
+template <int DT>
+__global__ __launch_bounds__(128) void embed_bwd_sum_kernel(const int64_t *__restrict__ sid, int64_t N, int64_t H,
+                                                            int64_t V, const float *__restrict__ ws,
+                                                            typename Elem<DT>::T *__restrict__ g) {
+    constexpr int PV = kPerVec<DT>;
+    const int64_t p = blockIdx.x;
+    const int64_t id = sid[p];
+    if ((p > 0 && sid[p - 1] == id) || id < 0 || id >= V) return;  // not a run head
+    const int64_t c0 = ((int64_t)blockIdx.y * 128 + threadIdx.x) * PV;
+    if (c0 >= H) return;
+    float tot[PV];
+#pragma unroll
+    for (int k = 0; k < PV; ++k) tot[k] = ws[p * H + c0 + k];
+    for (int64_t q = (p / kEmbPiece + 1) * kEmbPiece; q < N && sid[q] == id; q += kEmbPiece) {
+#pragma unroll
+        for (int k = 0; k < PV; ++k) tot[k] += ws[q * H + c0 + k];
+    }
+    if constexpr (DT == SWH_F32) {
+#pragma unroll
+        for (int k = 0; k < PV; ++k) g[id * H + c0 + k] += tot[k];
+    } else {
+        float cur[PV];
+        uint4 *gp = reinterpret_cast<uint4 *>(g + id * H + c0);
+        unpack16<DT>(*gp, cur);
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            o[k] = (uint32_t)f32_to_bf16_bits(cur[2 * k] + round_bf16(tot[2 * k])) |
+                   ((uint32_t)f32_to_bf16_bits(cur[2 * k + 1] + round_bf16(tot[2 * k + 1])) << 16);
+        *gp = uint4{o[0], o[1], o[2], o[3]};
+    }
+}
+
 }  // namespace
 }  // namespace swh
 
@@ -721,5 +802,31 @@ extern "C" int swh_qkv_rope(void *qkv, const int64_t *positions, const float *ro
     else
         qkv_rope_kernel<false><<<dim3((unsigned)grid), 256, 0, s>>>(static_cast<uint16_t *>(qkv), positions, rope_cos,
                                                                    rope_sin, R, (int)L, Hq, Hkv, D, Q, K, V);
+    return launch_status();
+}
+
+extern "C" int64_t swh_embedding_bwd_workspace_bytes(int64_t N, int64_t H) { return N * H * (int64_t)sizeof(float); }
+
+extern "C" int swh_embedding_bwd(const int64_t *sorted_ids, const int64_t *order, const void *dy, int64_t N, int64_t H,
+                                 int64_t V, void *grad_table, int32_t dtype, float *workspace, void *stream) {
+    if (!sorted_ids || !order || !dy || !grad_table || !workspace || N < 0 || H <= 0 || V <= 0) return SWH_E_ARG;
+    if (dtype != SWH_BF16 && dtype != SWH_F32) return SWH_E_DTYPE;
+    const int pv = dtype == SWH_F32 ? 4 : 8;
+    if (H % pv) return SWH_E_ARG;
+    if (N == 0) return SWH_OK;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const unsigned gy = (unsigned)((H / pv + 127) / 128);
+    const dim3 g1((unsigned)((N + kEmbPiece - 1) / kEmbPiece), gy), g2((unsigned)N, gy);
+    if (dtype == SWH_BF16) {
+        embed_bwd_piece_kernel<SWH_BF16><<<g1, 128, 0, st>>>(sorted_ids, order, static_cast<const uint16_t *>(dy), N, H,
+                                                             workspace);
+        embed_bwd_sum_kernel<SWH_BF16><<<g2, 128, 0, st>>>(sorted_ids, N, H, V, workspace,
+                                                           static_cast<uint16_t *>(grad_table));
+    } else {
+        embed_bwd_piece_kernel<SWH_F32><<<g1, 128, 0, st>>>(sorted_ids, order, static_cast<const float *>(dy), N, H,
+                                                            workspace);
+        embed_bwd_sum_kernel<SWH_F32><<<g2, 128, 0, st>>>(sorted_ids, N, H, V, workspace,
+                                                          static_cast<float *>(grad_table));
+    }
     return launch_status();
 }

@@ -155,15 +155,15 @@ __global__ __launch_bounds__(kThreads) void accumulate_kernel(float *__restrict_
         dst[i] = fmaf(Elem<DT>::load(src + i), scale, dst[i]);
 }
 
-// TR-DPO reference sync: target = (target * (1 - alpha)) + alpha * src with the
+// TR-DPO reference sync: target = (target * keep) + alpha * src with the
 // rounding points of torch's `mul_(1 - alpha)` then `add_(src, alpha=alpha)` on
-// tensors of the parameter dtype (each op rounds once to that dtype).
+// tensors of the parameter dtype (each op rounds once to that dtype); keep is
+// the host's float(1 - alpha), as torch casts the Python scalar.
 template <int DT>
 __global__ __launch_bounds__(kThreads) void ema_mix_kernel(typename Elem<DT>::T *__restrict__ dst,
                                                            const typename Elem<DT>::T *__restrict__ src, int64_t N,
-                                                           float alpha) {
+                                                           float keep, float alpha) {
     const int64_t stride = (int64_t)gridDim.x * kThreads;
-    const float keep = 1.f - alpha;
     for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < N; i += stride) {
         const float t = Elem<DT>::round(Elem<DT>::load(dst + i) * keep);
         const float r = fmaf(alpha, Elem<DT>::load(src + i), t);
@@ -266,14 +266,15 @@ extern "C" int swh_accumulate(float *dst, const void *src, int dtype, int64_t N,
     return launch_status();
 }
 
-extern "C" int swh_ema_mix(void *target, const void *src, int dtype, int64_t N, float alpha, void *stream) {
+extern "C" int swh_ema_mix(void *target, const void *src, int dtype, int64_t N, float keep, float alpha,
+                           void *stream) {
     if (!target || !src || N < 0) return SWH_E_ARG;
     if (N == 0) return SWH_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const unsigned nb = grid_for(N);
     switch (dtype) {
-    case SWH_BF16: ema_mix_kernel<SWH_BF16><<<nb, kThreads, 0, s>>>(static_cast<uint16_t *>(target), static_cast<const uint16_t *>(src), N, alpha); break;
-    case SWH_F32: ema_mix_kernel<SWH_F32><<<nb, kThreads, 0, s>>>(static_cast<float *>(target), static_cast<const float *>(src), N, alpha); break;
+    case SWH_BF16: ema_mix_kernel<SWH_BF16><<<nb, kThreads, 0, s>>>(static_cast<uint16_t *>(target), static_cast<const uint16_t *>(src), N, keep, alpha); break;
+    case SWH_F32: ema_mix_kernel<SWH_F32><<<nb, kThreads, 0, s>>>(static_cast<float *>(target), static_cast<const float *>(src), N, keep, alpha); break;
     default: return SWH_E_DTYPE;
     }
     return launch_status();

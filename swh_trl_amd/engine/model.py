@@ -169,8 +169,25 @@ class _Embedding(torch.autograd.Function):
         # stream) accumulates into this same view
         dw_sync(dy.device)
         if ctx.gtable is not None:
-            ctx.gtable.index_add_(0, ids.reshape(-1), dy.reshape(-1, dy.shape[-1]))
+            embedding_backward(ids, dy, ctx.gtable)
         return None, None, None, None
+
+
+def embedding_backward(ids: torch.Tensor, dy: torch.Tensor, gtable: torch.Tensor) -> None:
+    """gtable[id] += sum of the dy rows of token id, deterministically: rows are
+    visited in stable-sorted id order and each id's sum is folded in once
+    (swh_embedding_bwd; torch's index_add_ accumulates with atomics, so its bf16
+    result depends on the arrival order of duplicate ids)."""
+    flat_ids = ids.reshape(-1)
+    H = dy.shape[-1]
+    d2 = dy.reshape(-1, H)
+    if not d2.is_contiguous():
+        d2 = d2.contiguous()
+    sid, order = torch.sort(flat_ids, stable=True)
+    N = flat_ids.numel()
+    ws = torch.empty(max(1, N * H), device=dy.device, dtype=torch.float32)
+    call("swh_embedding_bwd", sid.data_ptr(), order.data_ptr(), d2.data_ptr(), N, H, gtable.shape[0],
+         gtable.data_ptr(), _dtype_code(gtable, "embedding_backward"), ws.data_ptr(), _stream())
 
 
 class _RMSNorm(torch.autograd.Function):

@@ -90,4 +90,4 @@ def sync_ref_model(ref_flat: torch.Tensor, policy_flat: torch.Tensor, alpha: flo
     if ref_flat.shape != policy_flat.shape or ref_flat.dtype != policy_flat.dtype:
         raise ValueError("sync_ref_model: reference and policy buffers must match in size and dtype")
     call("swh_ema_mix", ref_flat.data_ptr(), policy_flat.data_ptr(), _dtype_code(ref_flat, "sync_ref_model"),
-         ref_flat.numel(), float(alpha), _stream())
+         ref_flat.numel(), 1.0 - float(alpha), float(alpha), _stream())

@@ -364,6 +364,31 @@ def test_adamw_no_decay_ranges_and_fp32_model(dev):
     assert torch.equal(model.cpu(), st.master.cpu())
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_embedding_backward_deterministic(dev, dtype):
+    """swh_embedding_bwd: the per-id sums of dy rows folded into the gradient
+    table (fp64 reference: g + sum), with long runs of one id (pads) across
+    many 32-row pieces, ids outside the table skipped, and bit-identical
+    results on every call (no atomics)."""
+    from swh_trl_amd.engine.model import embedding_backward
+    g = _gen(16)
+    V, H, N = 300, 896, 5000
+    ids = torch.randint(0, V, (N,), generator=g)
+    ids[1000:3000] = 7                      # a 2000-row run (pad tokens after EOS)
+    ids[::97] = 5
+    dy = (torch.randn(N, H, generator=g) * 0.1).to(dtype)
+    g0 = (torch.randn(V, H, generator=g) * 0.01).to(dtype)
+    exp = g0.double().index_add(0, ids, dy.double())
+    outs = []
+    for _ in range(3):
+        gt = g0.to(dev)
+        embedding_backward(ids.view(50, 100).to(dev), dy.view(50, 100, H).to(dev), gt)
+        outs.append(gt.cpu())
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    torch.testing.assert_close(outs[0].double(), exp, rtol=tol, atol=tol * 0.1)
+
+
 # --------------------------------------------------------------------------- sampler
 def _oracle_lib():
     so = os.path.join(ROOT, "oracle", "_build", "libswh_oracle.so")
