@@ -96,17 +96,17 @@ def cpu_baseline(steps_note: str) -> dict:
                        f"{tm['update_s']:.2f}s = {wall:.2f}s wall for {G} samples, {threads} threads; {steps_note}")}
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r1_v7_pmc_decode.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r2_pmc_decode.json")
 
 
 def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed PMC passes
+    """Per-launch memory-side traffic of `kernel` from the committed PMC passes
     (tools/pmc_summary.py: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE over
-    tools/bench_decode.py, MI355X_MICROARCH.md §HBM corrections), or None."""
-    key = "decode_gemm.o+down" if kernel in ("decode_gemm.o", "decode_gemm.down") else kernel  # one template
+    tools/bench_decode.py, MI355X_MICROARCH.md §HBM corrections; each kernel its
+    own instantiation, o and down included), or None."""
     try:
         with open(PMC_FILE) as f:
-            k = json.load(f)["kernels"].get(key)
+            k = json.load(f)["kernels"].get(kernel)
         return None if k is None else k["hbm_bytes_per_launch"]
     except (OSError, ValueError, KeyError):
         return None

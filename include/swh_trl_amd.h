@@ -233,6 +233,13 @@ int swh_adamw(float *master, float *exp_avg, float *exp_avg_sq, const void *grad
  * Python scalar 1 - alpha), rounded to the parameter dtype after the multiply and
  * after the add as torch's mul_ / add_(alpha=) do.  dtype bf16 or f32. */
 int swh_ema_mix(void *target, const void *src, int dtype, int64_t N, float keep, float alpha, void *stream);
+/* Token-split weight gradient fold (the training backward's dW = dY^T X split
+ * over S token ranges into a batched GEMM): grad[i] = round(grad[i] +
+ * sum_s parts[s][i]), the sum in fp32 in s order, rounded once to the grad
+ * dtype.  parts [S, n] and grad [n] of `dtype` (bf16 / f32), 16-B aligned, n a
+ * multiple of 8 (bf16) / 4 (f32).  Replaces the AccumulateGrad of the
+ * reference's weight gradients (one GEMM per weight). */
+int swh_dw_reduce(const void *parts, int32_t S, int64_t n, void *grad, int32_t dtype, void *stream);
 /* dst_f32[i] += src[i] (bf16/f32) — accumulate micro-batch grads in fp32. */
 int swh_accumulate(float *dst, const void *src, int dtype, int64_t N, float scale, void *stream);
 

@@ -45,6 +45,10 @@ for step in "$@"; do
     serial2) AMD_SERIALIZE_KERNEL=3 SWH_TRACE=1 run serial2 500 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --layers 2 ;;
     trace2) SWH_TRACE=1 run trace2 400 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --layers 2 ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null && run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
+    tk) run tk 600 python tools/train_kernels.py ;;
+    proftk) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null && run proftk 600 rocprofv3 --kernel-trace --stats -d gpurun_out/proftk -o run --output-format csv -- python3 tools/train_kernels.py ;;
+    pmcft) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null && run pmcft 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmcft -o run --output-format csv -- python3 tools/train_kernels.py --reps 1 ;;
+    pmcwt) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null && run pmcwt 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmcwt -o run --output-format csv -- python3 tools/train_kernels.py --reps 1 ;;
     pmcf) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null && run pmcf 400 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmcf -o run --output-format csv -- python3 tools/bench_decode.py ;;
     pmcw) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null && run pmcw 400 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmcw -o run --output-format csv -- python3 tools/bench_decode.py ;;
     trace) SWH_TRACE=1 run trace 600 python bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;

@@ -146,7 +146,9 @@ static_assert(!(SWH_GEMM_RING && SWH_ROUND_PREFETCH), "the ring refill lives in 
 #define SWH_FLAT_MERGE 0  // one-barrier flat wave merge instead of the tree (A/B)
 #endif
 
-template <int CB, int MS, int NM, int EPI, bool BIAS, int MAXT>
+// KL: a K-class tag (0: K <= 1024, 1: longer) that only separates the rocprof
+// names of otherwise identical instantiations (o_proj K 896 vs down_proj K 4864)
+template <int CB, int MS, int NM, int EPI, bool BIAS, int MAXT, int KL = 0>
 __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
     const uint16_t *__restrict__ x, const uint16_t *__restrict__ w, int M, int N, int K,
     const uint16_t *__restrict__ norm_w, float eps, const float *__restrict__ ss_in,
@@ -1371,20 +1373,32 @@ int64_t slab_bytes(const GemmCfg &c, int64_t M, int64_t wcols) {
     return nmt * wcols * c.s * MR * (int64_t)sizeof(float);  // tiles * NB == nmt * wcols
 }
 
-template <int CB, int MS, int NM, int EPI, bool BIAS, int MAXT>
-int launch_gemm(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W, int m,
-                int n, int k, const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs, uint16_t *R,
-                float *ss_out, uint16_t *Y, int ld, float *slab, int *ctr) {
+template <int CB, int MS, int NM, int EPI, bool BIAS, int MAXT, int KL>
+int launch_gemm_kl(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W,
+                   int m, int n, int k, const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs,
+                   uint16_t *R, float *ss_out, uint16_t *Y, int ld, float *slab, int *ctr) {
     static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in once per kernel
     if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&decode_gemm_kernel<CB, MS, NM, EPI, BIAS, MAXT>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&decode_gemm_kernel<CB, MS, NM, EPI, BIAS, MAXT, KL>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
             return SWH_E_LAUNCH;
         attr = true;
     }
-    decode_gemm_kernel<CB, MS, NM, EPI, BIAS, MAXT><<<grid, 64u * c.nw, lds, s>>>(
+    decode_gemm_kernel<CB, MS, NM, EPI, BIAS, MAXT, KL><<<grid, 64u * c.nw, lds, s>>>(
         X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr, c.persist ? 1 : 0, c.wn);
     return launch_status();
+}
+
+template <int CB, int MS, int NM, int EPI, bool BIAS, int MAXT>
+int launch_gemm(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W, int m,
+                int n, int k, const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs, uint16_t *R,
+                float *ss_out, uint16_t *Y, int ld, float *slab, int *ctr) {
+    // residual projections: o_proj (K = H) and down_proj (K = I) get distinct names
+    if (EPI == EPI_RESIDUAL && k > 1024)
+        return launch_gemm_kl<CB, MS, NM, EPI, BIAS, MAXT, 1>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R,
+                                                              ss_out, Y, ld, slab, ctr);
+    return launch_gemm_kl<CB, MS, NM, EPI, BIAS, MAXT, 0>(c, grid, lds, s, X, W, m, n, k, NWt, eps, ss_in, Bs, R,
+                                                          ss_out, Y, ld, slab, ctr);
 }
 
 template <int MS, int NM, int EPI, bool BIAS>

@@ -172,6 +172,41 @@ __global__ __launch_bounds__(kThreads) void ema_mix_kernel(typename Elem<DT>::T 
     }
 }
 
+// Split-K weight-gradient fold: grad = round(grad + sum_s parts[s]) with the S
+// partial products (parts dtype = grad dtype) summed in fp32 in s order — the
+// batched-GEMM partials of a token-split dW GEMM reduced and accumulated in ONE
+// pass (replaces a torch sum over S plus an add: two extra fp32 round trips).
+template <int DT>
+__global__ __launch_bounds__(kThreads) void dw_reduce_kernel(const typename Elem<DT>::T *__restrict__ parts, int S,
+                                                             int64_t n, typename Elem<DT>::T *__restrict__ g) {
+    using T = typename Elem<DT>::T;
+    constexpr int PV = kPerVec<DT>;
+    const int64_t nv = n / PV;
+    const int64_t stride = (int64_t)gridDim.x * kThreads;
+    for (int64_t v = (int64_t)blockIdx.x * kThreads + threadIdx.x; v < nv; v += stride) {
+        float acc[PV], x[PV];
+        unpack16<DT>(reinterpret_cast<const uint4 *>(g)[v], acc);
+        float s[PV];
+        unpack16<DT>(reinterpret_cast<const uint4 *>(parts)[v], s);
+        for (int q = 1; q < S; ++q) {
+            unpack16<DT>(reinterpret_cast<const uint4 *>(parts + (int64_t)q * n)[v], x);
+#pragma unroll
+            for (int k = 0; k < PV; ++k) s[k] += x[k];
+        }
+        if constexpr (DT == SWH_F32) {
+            reinterpret_cast<float4 *>(g)[v] = float4{acc[0] + s[0], acc[1] + s[1], acc[2] + s[2], acc[3] + s[3]};
+        } else {
+            uint32_t o[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                o[k] = (uint32_t)f32_to_bf16_bits(acc[2 * k] + s[2 * k]) |
+                       ((uint32_t)f32_to_bf16_bits(acc[2 * k + 1] + s[2 * k + 1]) << 16);
+            reinterpret_cast<uint4 *>(g)[v] = uint4{o[0], o[1], o[2], o[3]};
+        }
+    }
+    (void)sizeof(T);
+}
+
 unsigned grid_for(int64_t work_items) {
     int64_t g = (work_items + kThreads - 1) / kThreads;
     if (g > 256 * 16) g = 256 * 16;
@@ -277,5 +312,22 @@ extern "C" int swh_ema_mix(void *target, const void *src, int dtype, int64_t N, 
     case SWH_F32: ema_mix_kernel<SWH_F32><<<nb, kThreads, 0, s>>>(static_cast<float *>(target), static_cast<const float *>(src), N, keep, alpha); break;
     default: return SWH_E_DTYPE;
     }
+    return launch_status();
+}
+
+extern "C" int swh_dw_reduce(const void *parts, int32_t S, int64_t n, void *grad, int32_t dtype, void *stream) {
+    if (!parts || !grad || S < 1 || n < 0) return SWH_E_ARG;
+    if (dtype != SWH_BF16 && dtype != SWH_F32) return SWH_E_DTYPE;
+    const int pv = dtype == SWH_F32 ? 4 : 8;
+    if (n % pv || ((reinterpret_cast<uintptr_t>(parts) | reinterpret_cast<uintptr_t>(grad)) & 15)) return SWH_E_ARG;
+    if (n == 0) return SWH_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const unsigned nb = grid_for(n / pv);
+    if (dtype == SWH_BF16)
+        dw_reduce_kernel<SWH_BF16><<<nb, kThreads, 0, s>>>(static_cast<const uint16_t *>(parts), S, n,
+                                                           static_cast<uint16_t *>(grad));
+    else
+        dw_reduce_kernel<SWH_F32><<<nb, kThreads, 0, s>>>(static_cast<const float *>(parts), S, n,
+                                                          static_cast<float *>(grad));
     return launch_status();
 }

@@ -124,10 +124,12 @@ def _accumulate_dw(gw, gb, dy, x):
             # batched GEMMs (S x the workgroups), sum the partials into the gradient
             Kc = dy2.shape[0] // S
             parts = torch.bmm(dy2[:S * Kc].view(S, Kc, -1).transpose(1, 2), x2[:S * Kc].view(S, Kc, -1))
-            acc = parts.sum(0, dtype=torch.float32)
+            side.keep(parts)
+            # the S partials summed and folded into the gradient view in one pass
+            call("swh_dw_reduce", parts.data_ptr(), S, gw.numel(), gw.data_ptr(), _dtype_code(gw, "dw_reduce"),
+                 _stream())
             if S * Kc < dy2.shape[0]:
-                acc.addmm_(dy2[S * Kc:].t().float(), x2[S * Kc:].float())
-            gw.add_(acc)
+                gw.addmm_(dy2[S * Kc:].t(), x2[S * Kc:])
         else:
             gw.addmm_(dy2.t(), x2)
         if gb is not None:

@@ -389,6 +389,34 @@ def test_embedding_backward_deterministic(dev, dtype):
     torch.testing.assert_close(outs[0].double(), exp, rtol=tol, atol=tol * 0.1)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_token_split_weight_gradient_fold(dev, dtype):
+    """engine/model.py _accumulate_dw at a token count that takes the split
+    path (S token ranges as one batched GEMM, swh_dw_reduce folding the S
+    partials into the gradient view): gw + dy^T x against fp64, plus the bias
+    column sums; the result is identical on every call."""
+    from swh_trl_amd.engine.model import _accumulate_dw, _dw_split, dw_sync
+    g = _gen(17)
+    T, N, K = 16384 + 40, 896, 1152
+    assert _dw_split(T, N * K) > 1
+    dy = (torch.randn(T, N, generator=g) * 0.05).to(dtype)
+    x = (torch.randn(T, K, generator=g) * 0.05).to(dtype)
+    g0 = (torch.randn(N, K, generator=g) * 0.01).to(dtype)
+    b0 = torch.zeros(N, dtype=dtype)
+    exp = g0.double() + dy.double().t() @ x.double()
+    outs = []
+    for _ in range(2):
+        gw, gb = g0.to(dev), b0.to(dev)
+        _accumulate_dw(gw, gb, dy.to(dev), x.to(dev))
+        dw_sync(dev)
+        torch.cuda.synchronize()
+        outs.append(gw.cpu())
+    assert torch.equal(outs[0], outs[1])
+    rel = ((outs[0].double() - exp).norm() / exp.norm()).item()
+    assert rel < (3e-3 if dtype == torch.bfloat16 else 1e-5), rel
+    torch.testing.assert_close(gb.cpu().double(), dy.double().sum(0), rtol=2e-2, atol=2e-2)
+
+
 # --------------------------------------------------------------------------- sampler
 def _oracle_lib():
     so = os.path.join(ROOT, "oracle", "_build", "libswh_oracle.so")

@@ -5,7 +5,7 @@ FETCH_SIZE counts half the bytes of wide streaming reads on gfx950 (x2);
 both counters are KiB.  Writes profiles/<name>.json, which bench.py reads
 for `roofline.traffic`.
 
-    python tools/pmc_summary.py gpurun_out/pmcf gpurun_out/pmcw profiles/r1_v4_pmc_decode.json
+    python tools/pmc_summary.py gpurun_out/pmcf gpurun_out/pmcw profiles/r2_pmc_decode.json [source script]
 """
 import collections
 import csv
@@ -16,9 +16,20 @@ import sys
 NAMES = {  # kernel template prefix -> the bench's kernel name
     "lm_head_kernel<2, 2, false, false": "decode_gemm.gate_up",   # tile kernel, folded norm, SiLU epilogue
     "decode_gemm_kernel<1, 2, 2, 0, true": "decode_gemm.qkv",
-    "decode_gemm_kernel<1, 1, 0, 1, false": "decode_gemm.o+down",
+    "decode_gemm_kernel<1, 1, 0, 1, false, 512, 0>": "decode_gemm.o",     # K-class tag 0: K <= 1024
+    "decode_gemm_kernel<1, 1, 0, 1, false, 512, 1>": "decode_gemm.down",  # K-class tag 1
     "attn_decode_kernel<64, 7>": "attn_decode",
     "lm_head_kernel<2, 0, false, true": "lm_head_sample",
+    # training kernels (tools/train_kernels.py)
+    "logp_entropy_fwd_kernel": "logp_entropy_fwd",
+    "logp_bwd_kernel": "logp_bwd",
+    "adamw_kernel": "adamw",
+    "fa_fwd_kernel": "attn_fwd",
+    "fa_dq_kernel": "attn_bwd.dq",
+    "fa_dkdv_kernel": "attn_bwd.dkdv",
+    "dw_reduce_kernel": "dw_reduce",
+    "rmsnorm_bwd_kernel": "rmsnorm_bwd",
+    "silu_mul_bwd_kernel": "silu_mul_bwd",
 }
 
 
@@ -36,7 +47,8 @@ def per_kernel(path: str, counter: str) -> dict:
 def main():
     fdir, wdir, out = sys.argv[1:4]
     fetch, write = per_kernel(fdir, "FETCH_SIZE"), per_kernel(wdir, "WRITE_SIZE")
-    res = {"source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE -- python3 tools/bench_decode.py",
+    src = sys.argv[4] if len(sys.argv) > 4 else "tools/bench_decode.py"
+    res = {"source": f"rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE -- python3 {src}",
            "correction": "FETCH_SIZE x2 (gfx950 wide-read tally), KiB -> bytes", "kernels": {}}
     for prefix, name in NAMES.items():
         tf = [k for k in fetch if k.startswith(prefix)]
