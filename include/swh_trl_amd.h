@@ -268,6 +268,13 @@ int swh_rmsnorm_bwd(const void *x, const void *weight, const float *rstd, const 
  * grad_w = bf16(grad_w + bf16(sum over blocks)) (f32: grad_w += sum). */
 int swh_rmsnorm_dw_accum(const float *dw_partial, int64_t nblocks, int64_t H, void *grad_w, int32_t dtype,
                          void *stream);
+/* Column sums of x [rows, cols] (`dtype` bf16/f32, cols % 8 (bf16) / 4 (f32) == 0)
+ * into fp32 partial rows part [ceil(rows / rows_per_chunk), cols], fixed order
+ * (no atomics); swh_rmsnorm_dw_accum then folds them into a gradient view.  The
+ * bias gradient of the q/k/v projection (the autograd of transformers'
+ * nn.Linear bias in the reference's training forward). */
+int swh_colsum_partials(const void *x, int64_t rows, int64_t cols, int64_t rows_per_chunk, float *part,
+                        int32_t dtype, void *stream);
 /* out[r, i] = bf16(bf16(silu(gu[r, i])) * gu[r, I + i]) — gate/up packed. */
 int swh_silu_mul_fwd(const void *gu, int64_t rows, int64_t I, void *out, int32_t dtype, void *stream);
 int swh_silu_mul_bwd(const void *gu, const void *dout, int64_t rows, int64_t I, void *dgu, int32_t dtype,

@@ -614,6 +614,55 @@ __global__ __launch_bounds__(128) void embed_bwd_sum_kernel(const int64_t *__res
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Column sums of a tall [rows, cols] matrix (the bias gradient: sum over tokens
+// of dy), deterministic: a workgroup sums one chunk of rows for 512 (bf16) /
+// 256 (f32) columns, its 4 waves taking every 4th row, then adds the waves in
+// fixed order into one fp32 partial row per chunk; swh_rmsnorm_dw_accum folds
+// the partial rows into the gradient view.
+// ---------------------------------------------------------------------------
+template <int DT>
+__global__ __launch_bounds__(256) void colsum_partials_kernel(const typename Elem<DT>::T *__restrict__ x, int64_t rows,
+                                                              int64_t cols, int64_t rpc, float *__restrict__ part) {
+    constexpr int PV = kPerVec<DT>;
+    __shared__ float red[4][64 * PV];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int64_t c0 = ((int64_t)blockIdx.x * 64 + lane) * PV;
+    const int64_t r0 = (int64_t)blockIdx.y * rpc, r1 = min(rows, r0 + rpc);
+    float acc[PV];
+#pragma unroll
+    for (int k = 0; k < PV; ++k) acc[k] = 0.f;
+    if (c0 < cols) {
+        int64_t r = r0 + wid;
+        for (; r + 12 < r1; r += 16) {  // four rows' loads in flight
+            uint4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4 *>(x + (r + 4 * u) * cols + c0);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                float f[PV];
+                unpack16<DT>(v[u], f);
+#pragma unroll
+                for (int k = 0; k < PV; ++k) acc[k] += f[k];
+            }
+        }
+        for (; r < r1; r += 4) {
+            float f[PV];
+            unpack16<DT>(*reinterpret_cast<const uint4 *>(x + r * cols + c0), f);
+#pragma unroll
+            for (int k = 0; k < PV; ++k) acc[k] += f[k];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < PV; ++k) red[wid][lane * PV + k] = acc[k];
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * PV; i += 256) {
+        const int64_t c = (int64_t)blockIdx.x * 64 * PV + i;
+        if (c < cols) part[(int64_t)blockIdx.y * cols + c] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+    }
+}
+
 }  // namespace
 }  // namespace swh
 
@@ -828,5 +877,23 @@ extern "C" int swh_embedding_bwd(const int64_t *sorted_ids, const int64_t *order
         embed_bwd_sum_kernel<SWH_F32><<<g2, 128, 0, st>>>(sorted_ids, N, H, V, workspace,
                                                           static_cast<float *>(grad_table));
     }
+    return launch_status();
+}
+
+extern "C" int swh_colsum_partials(const void *x, int64_t rows, int64_t cols, int64_t rows_per_chunk, float *part,
+                                   int32_t dtype, void *stream) {
+    if (!x || !part || rows < 0 || cols <= 0 || rows_per_chunk <= 0) return SWH_E_ARG;
+    if (dtype != SWH_BF16 && dtype != SWH_F32) return SWH_E_DTYPE;
+    const int pv = dtype == SWH_F32 ? 4 : 8;
+    if (cols % pv || (reinterpret_cast<uintptr_t>(x) & 15)) return SWH_E_ARG;
+    if (rows == 0) return SWH_OK;
+    const dim3 grid((unsigned)((cols / pv + 63) / 64), (unsigned)((rows + rows_per_chunk - 1) / rows_per_chunk));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (dtype == SWH_BF16)
+        colsum_partials_kernel<SWH_BF16><<<grid, 256, 0, st>>>(static_cast<const uint16_t *>(x), rows, cols,
+                                                               rows_per_chunk, part);
+    else
+        colsum_partials_kernel<SWH_F32><<<grid, 256, 0, st>>>(static_cast<const float *>(x), rows, cols,
+                                                              rows_per_chunk, part);
     return launch_status();
 }

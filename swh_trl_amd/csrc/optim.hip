@@ -52,7 +52,8 @@ template <int GDT, int WM, bool NR>
 __global__ __launch_bounds__(kThreads) void adamw_kernel(float *__restrict__ p, float *__restrict__ m,
                                                          float *__restrict__ v,
                                                          const typename Elem<GDT>::T *__restrict__ g,
-                                                         void *__restrict__ model_v, int64_t N, float lr,
+                                                         uint16_t *__restrict__ model,
+                                                         float *__restrict__ model32, int64_t N, float lr,
                                                          float b1, float b2, float eps, float wd, float step_size,
                                                          float bc2_sqrt, const float *__restrict__ clip,
                                                          const int64_t *__restrict__ nd, int nnd) {
@@ -77,12 +78,9 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float *__restrict__ p, 
             return (hit >= 0 && e < tab[2 * hit + 1]) ? 1.f : decay_on;
         }
     };
-    uint16_t *model = static_cast<uint16_t *>(model_v);
-    float *model32 = static_cast<float *>(model_v);
     const int64_t n4 = N / 4;
     const int64_t stride = (int64_t)gridDim.x * kThreads;
-    float decay = decay_on;
-    auto upd = [&](float &pp, float &mm, float &vv, float gg) {
+    auto upd = [&](float &pp, float &mm, float &vv, float gg, float decay) {
         gg *= cf;
         pp *= decay;
         mm = fmaf(1.f - b1, gg - mm, mm);       // exp_avg.lerp_(grad, 1 - beta1)
@@ -118,11 +116,11 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float *__restrict__ p, 
         for (int u = 0; u < U; ++u) {
             const int64_t i = i0 + u * stride;
             if (i >= n4) break;
-            decay = decay_at(4 * i);
-            upd(pp[u].x, mm[u].x, vv[u].x, gg[u][0]);
-            upd(pp[u].y, mm[u].y, vv[u].y, gg[u][1]);
-            upd(pp[u].z, mm[u].z, vv[u].z, gg[u][2]);
-            upd(pp[u].w, mm[u].w, vv[u].w, gg[u][3]);
+            const float dc = decay_at(4 * i);
+            upd(pp[u].x, mm[u].x, vv[u].x, gg[u][0], dc);
+            upd(pp[u].y, mm[u].y, vv[u].y, gg[u][1], dc);
+            upd(pp[u].z, mm[u].z, vv[u].z, gg[u][2], dc);
+            upd(pp[u].w, mm[u].w, vv[u].w, gg[u][3], dc);
             reinterpret_cast<float4 *>(p)[i] = pp[u];
             reinterpret_cast<float4 *>(m)[i] = mm[u];
             reinterpret_cast<float4 *>(v)[i] = vv[u];
@@ -136,8 +134,7 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float *__restrict__ p, 
     }
     for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * kThreads + threadIdx.x; i < N; i += stride) {
         float pp = p[i], mm = m[i], vv = v[i];
-        decay = decay_at(i);
-        upd(pp, mm, vv, Elem<GDT>::load(g + i));
+        upd(pp, mm, vv, Elem<GDT>::load(g + i), decay_at(i));
         p[i] = pp;
         m[i] = mm;
         v[i] = vv;
@@ -267,7 +264,8 @@ extern "C" int swh_adamw(float *master, float *exp_avg, float *exp_avg_sq, const
     const int wm = model_out ? model_dtype : -1;
 #define SWH_ADAM(GDT, WM, NR)                                                                                       \
     adamw_kernel<GDT, WM, NR><<<nb, kThreads, 0, s>>>(master, exp_avg, exp_avg_sq,                                 \
-                                                      static_cast<const typename Elem<GDT>::T *>(grad), model_out, N, \
+                                                      static_cast<const typename Elem<GDT>::T *>(grad),              \
+                                                      static_cast<uint16_t *>(model_out), static_cast<float *>(model_out), N, \
                                                       lr, beta1, beta2, eps, weight_decay, step_size, bc2_sqrt, clip, \
                                                       no_decay, n_no_decay)
 #define SWH_ADAM_G(GDT)                                     \

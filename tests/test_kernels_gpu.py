@@ -415,6 +415,10 @@ def test_token_split_weight_gradient_fold(dev, dtype):
     rel = ((outs[0].double() - exp).norm() / exp.norm()).item()
     assert rel < (3e-3 if dtype == torch.bfloat16 else 1e-5), rel
     torch.testing.assert_close(gb.cpu().double(), dy.double().sum(0), rtol=2e-2, atol=2e-2)
+    gb2 = b0.to(dev)
+    _accumulate_dw(g0.to(dev), gb2, dy.to(dev), x.to(dev))
+    dw_sync(dev)
+    assert torch.equal(gb2.cpu(), gb.cpu())  # the bias column sums are deterministic too
 
 
 # --------------------------------------------------------------------------- sampler

@@ -51,7 +51,8 @@ def sweep(eng, m):
         "lm_nonorm": lambda: nn_ops.decode_gemm(eng.s, m.lm_weight(), y=eng.logits_buf),
     }
     cfgs = [None, "1,1,1", "2,1,1", "4,1,1", "1,2,1", "2,2,1", "4,2,1", "4,4,1", "2,4,1", "1,1,2", "2,1,2",
-            "4,1,4", "4,2,5", "1,1,4", "4,2,1,1", "4,4,1,1"]
+            "4,1,4", "4,2,5", "1,1,4", "4,2,1,1", "4,4,1,1", "4,1,2", "2,1,4", "4,1,8", "4,2,4", "4,2,8", "2,2,2",
+            "2,2,4", "1,2,2", "4,4,4"]
     print("cfg      " + " ".join(f"{k:>14s}" for k in shapes), flush=True)
     for cf in cfgs:
         if cf is None:
