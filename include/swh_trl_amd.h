@@ -196,6 +196,26 @@ int swh_ppo_loss_fwd_bwd(const float *new_logp, const float *old_logp, const flo
                          float cliprange, float cliprange_value, float vf_coef, float *loss,
                          float *dnew_logp, float *dvpred, float *stats, void *workspace, void *stream);
 
+/* ---- a16: PPO rollout post-processing (ppo_trainer.py:478-516) --------------
+ * swh_ppo_truncate: post = truncate_response(stop, pad, responses) (utils.py
+ * :1036-1056: tokens after the first stop token become pad; stop < 0 = none),
+ * seq_len[b] = first_true_indices(post == pad) - 1 (utils.py:877-897).
+ * responses / post int64 [B, T]; seq_len int64 [B]. */
+int swh_ppo_truncate(const int64_t *responses, int64_t B, int64_t T, int64_t stop_token_id, int64_t pad_token_id,
+                     int64_t *post, int64_t *seq_len, void *stream);
+/* swh_ppo_rewards, per row after the value / reward-model forwards:
+ * padding_mask = t > seq_len, padding_mask_p1 = t > seq_len + 1 (uint8 [B, T]);
+ * logprobs / ref_logprobs f32 [B, T] set to INVALID_LOGPROB (1.0) under the
+ * mask (in place); values bf16 [B, T] zeroed under mask_p1 (in place); scores
+ * bf16 [B] minus missing_eos_penalty where no eos token is in post (has_penalty,
+ * eos < 0 = none; in place); kl = -logr (k1) or (exp(logr) - 1) - logr (k3),
+ * logr = ref - logp; non_score_reward = -kl_coef * kl; rewards = non_score_reward
+ * + score at min(seq_len + 1, T - 1) (all f32 [B, T]). */
+int swh_ppo_rewards(const int64_t *post, const int64_t *seq_len, int64_t B, int64_t T, int64_t eos_token_id,
+                    float missing_eos_penalty, int32_t has_penalty, float kl_coef, int32_t kl_k3, float *logprobs,
+                    float *ref_logprobs, void *values_bf16, void *scores_bf16, uint8_t *padding_mask,
+                    uint8_t *padding_mask_p1, float *kl, float *non_score_reward, float *rewards, void *stream);
+
 /* ---- a20: value head (modeling_value_head.py:50-59; PPO score head
  * ppo_trainer.py:95, utils.py:937): out[r] = sum_h hidden[r,h]*w[h] (+ bias).
  * hidden bf16/f32 [R, H] row stride ld; w f32 [H]; bias nullable f32[1]. */

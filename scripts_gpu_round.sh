@@ -45,6 +45,8 @@ for step in "$@"; do
     serial2) AMD_SERIALIZE_KERNEL=3 SWH_TRACE=1 run serial2 500 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --layers 2 ;;
     trace2) SWH_TRACE=1 run trace2 400 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --layers 2 ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null && run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
+    l8) run l8 1000 python tools/bench_llama8b.py --prompts 8 --P 256 --C 1024 --steps 1 --warmup 1 --fuse-budget 16384 ;;
+    l8k) run l8k 600 python -u -m pytest tests/test_kernels_gpu.py -v -m gpu -k "llama3_8b" --timeout 200 --timeout-method thread ;;
     tk) run tk 600 python tools/train_kernels.py ;;
     proftk) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null && run proftk 600 rocprofv3 --kernel-trace --stats -d gpurun_out/proftk -o run --output-format csv -- python3 tools/train_kernels.py ;;
     pmcft) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null && run pmcft 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmcft -o run --output-format csv -- python3 tools/train_kernels.py --reps 1 ;;

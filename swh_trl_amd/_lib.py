@@ -59,6 +59,9 @@ SIGNATURES = {
     "swh_ppo_loss_workspace_bytes": (c_i64, [c_i64]),
     "swh_ppo_loss_fwd_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32,
                                      c_f32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "swh_ppo_truncate": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "swh_ppo_rewards": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_f32, c_i32, c_f32, c_i32, c_vp, c_vp, c_vp, c_vp,
+                                c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "swh_value_head_fwd": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "swh_sqnorm_partials": (c_i64, [c_i64]),
     "swh_grad_sqnorm": (c_i32, [c_vp, c_i32, c_i64, c_vp, c_vp]),

@@ -402,6 +402,83 @@ __global__ __launch_bounds__(256) void value_head_kernel(const typename Elem<DT>
     if (lane == 0) out[r] = s + (bias ? bias[0] : 0.f);
 }
 
+
+// ---------------------------------------------------------------------------
+// a16 — PPO rollout post-processing (ppo_trainer.py:478-516), one workgroup
+// per row: (1) truncate_response after the first stop token and the sequence
+// length (first pad of the truncated row, minus one: utils.py:1036-1056,
+// :877-897); (2) the masks, INVALID_LOGPROB fill, value masking, missing-EOS
+// penalty, k1/k3 KL, KL-shaped rewards and the score scatter at
+// min(seq_len + 1, T - 1).  Replaces ~15 torch launches of host glue.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int block_min_i32(int v, int *red) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, kWave));
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    int r = red[0];
+    for (int w = 1; w < nw; ++w) r = min(r, red[w]);
+    __syncthreads();
+    return r;
+}
+
+__global__ __launch_bounds__(256) void ppo_truncate_kernel(const int64_t *__restrict__ resp, int64_t T,
+                                                           int64_t stop, int64_t pad, int64_t *__restrict__ post,
+                                                           int64_t *__restrict__ seq_len) {
+    __shared__ int red[4];
+    const int64_t b = blockIdx.x;
+    const int64_t *r = resp + b * T;
+    int first = (int)T;
+    if (stop >= 0)
+        for (int64_t t = threadIdx.x; t < T; t += blockDim.x)
+            if (r[t] == stop) { first = (int)t; break; }
+    first = block_min_i32(first, red);
+    int fpad = (int)T;
+    for (int64_t t = threadIdx.x; t < T; t += blockDim.x) {
+        const int64_t v = (t > first) ? pad : r[t];
+        post[b * T + t] = v;
+        if (v == pad && (int)t < fpad) fpad = (int)t;
+    }
+    fpad = block_min_i32(fpad, red);
+    if (threadIdx.x == 0) seq_len[b] = (int64_t)fpad - 1;
+}
+
+__global__ __launch_bounds__(256) void ppo_rewards_kernel(
+    const int64_t *__restrict__ post, const int64_t *__restrict__ seq_len, int64_t T, int64_t eos, float penalty,
+    int32_t has_penalty, float kl_coef, int32_t k3, float *__restrict__ logp, float *__restrict__ ref,
+    uint16_t *__restrict__ values, uint16_t *__restrict__ scores, uint8_t *__restrict__ pmask,
+    uint8_t *__restrict__ pmask1, float *__restrict__ kl, float *__restrict__ nsr, float *__restrict__ rewards) {
+    __shared__ int red[4];
+    const int64_t b = blockIdx.x;
+    const int64_t sl = seq_len[b];
+    int has = 0;
+    if (eos >= 0)
+        for (int64_t t = threadIdx.x; t < T; t += blockDim.x) has |= (post[b * T + t] == eos);
+    has = -block_min_i32(-has, red);  // any
+    float score = bf16_bits_to_f32(scores[b]);
+    if (has_penalty && !has) score = round_bf16(score - penalty);  // bf16 tensor minus a Python float
+    const int64_t end = (sl + 1 < T) ? sl + 1 : sl;                  // ppo_trainer.py:513-515
+    for (int64_t t = threadIdx.x; t < T; t += blockDim.x) {
+        const int64_t i = b * T + t;
+        const bool pm = t > sl, pm1 = t > sl + 1;
+        pmask[i] = pm;
+        pmask1[i] = pm1;
+        const float lp = pm ? 1.0f : logp[i];  // INVALID_LOGPROB (ppo_trainer.py:81)
+        const float rf = pm ? 1.0f : ref[i];
+        logp[i] = lp;
+        ref[i] = rf;
+        if (pm1) values[i] = 0;
+        const float logr = rf - lp;
+        const float k = k3 ? (expf(logr) - 1.f) - logr : -logr;
+        const float n = -kl_coef * k;
+        kl[i] = k;
+        nsr[i] = n;
+        rewards[i] = (t == end) ? n + score : n;
+    }
+    if (threadIdx.x == 0) scores[b] = f32_to_bf16_bits(score);
+}
+
 }  // namespace
 }  // namespace swh
 
@@ -508,5 +585,30 @@ extern "C" int swh_value_head_fwd(const void *hidden, int dtype, int64_t R, int6
     default:
         return SWH_E_DTYPE;
     }
+    return launch_status();
+}
+
+extern "C" int swh_ppo_truncate(const int64_t *responses, int64_t B, int64_t T, int64_t stop_token_id,
+                                int64_t pad_token_id, int64_t *post, int64_t *seq_len, void *stream) {
+    if (!responses || !post || !seq_len || B < 0 || T <= 0 || T > (1 << 30)) return SWH_E_ARG;
+    if (B == 0) return SWH_OK;
+    ppo_truncate_kernel<<<dim3((unsigned)B), 256, 0, static_cast<hipStream_t>(stream)>>>(responses, T, stop_token_id,
+                                                                                          pad_token_id, post, seq_len);
+    return launch_status();
+}
+
+extern "C" int swh_ppo_rewards(const int64_t *post, const int64_t *seq_len, int64_t B, int64_t T, int64_t eos_token_id,
+                               float missing_eos_penalty, int32_t has_penalty, float kl_coef, int32_t kl_k3,
+                               float *logprobs, float *ref_logprobs, void *values_bf16, void *scores_bf16,
+                               uint8_t *padding_mask, uint8_t *padding_mask_p1, float *kl, float *non_score_reward,
+                               float *rewards, void *stream) {
+    if (!post || !seq_len || !logprobs || !ref_logprobs || !values_bf16 || !scores_bf16 || !padding_mask ||
+        !padding_mask_p1 || !kl || !non_score_reward || !rewards || B < 0 || T <= 0 || T > (1 << 30))
+        return SWH_E_ARG;
+    if (B == 0) return SWH_OK;
+    ppo_rewards_kernel<<<dim3((unsigned)B), 256, 0, static_cast<hipStream_t>(stream)>>>(
+        post, seq_len, T, eos_token_id, missing_eos_penalty, has_penalty, kl_coef, kl_k3, logprobs, ref_logprobs,
+        static_cast<uint16_t *>(values_bf16), static_cast<uint16_t *>(scores_bf16), padding_mask, padding_mask_p1,
+        kl, non_score_reward, rewards);
     return launch_status();
 }

@@ -330,6 +330,48 @@ def ppo_loss_fwd_bwd(new_logprobs, mb_logprobs, mb_advantage, vpred, mb_values, 
     return loss, dnl, dvp, stats
 
 
+def ppo_truncate(responses: torch.Tensor, stop_token_id, pad_token_id: int):
+    """utils.py:1036-1056 truncate_response + :877-897 first_true_indices in one
+    launch: (postprocessed responses int64 [B, T], sequence_lengths int64 [B])."""
+    _dev(responses, "ppo_truncate")
+    r = responses.to(torch.int64).contiguous()
+    B, T = r.shape
+    post = torch.empty_like(r)
+    seq = torch.empty(B, dtype=torch.int64, device=r.device)
+    call("swh_ppo_truncate", r.data_ptr(), B, T, -1 if stop_token_id is None else int(stop_token_id), int(pad_token_id),
+         post.data_ptr(), seq.data_ptr(), _stream())
+    return post, seq
+
+
+def ppo_rewards(post: torch.Tensor, sequence_lengths: torch.Tensor, logprobs: torch.Tensor,
+                ref_logprobs: torch.Tensor, values: torch.Tensor, scores: torch.Tensor, *, eos_token_id,
+                missing_eos_penalty, kl_coef: float, kl_estimator: str = "k1") -> dict:
+    """ppo_trainer.py:490-516 in one launch: masks, INVALID_LOGPROB fill, value
+    masking, missing-EOS penalty, KL (k1 / k3) and KL-shaped rewards with the
+    score scattered at min(seq_len + 1, T - 1).  values / scores are the bf16
+    outputs of the score heads (modified like the reference's tensors)."""
+    _dev(post, "ppo_rewards")
+    if kl_estimator not in ("k1", "k3"):
+        raise ValueError(f"kl_estimator must be 'k1' or 'k3', got {kl_estimator!r}")
+    if values.dtype != torch.bfloat16 or scores.dtype != torch.bfloat16:
+        raise ValueError("ppo_rewards: values and scores are the bf16 score-head outputs")
+    B, T = post.shape
+    lp = logprobs.to(torch.float32).contiguous().clone()
+    rf = ref_logprobs.to(torch.float32).contiguous().clone()
+    v = values.contiguous().clone()
+    s = scores.contiguous().clone()
+    pm = torch.empty(B, T, dtype=torch.bool, device=post.device)
+    pm1 = torch.empty_like(pm)
+    kl, nsr, rew = torch.empty_like(lp), torch.empty_like(lp), torch.empty_like(lp)
+    call("swh_ppo_rewards", post.contiguous().data_ptr(), sequence_lengths.to(torch.int64).contiguous().data_ptr(), B,
+         T, -1 if eos_token_id is None else int(eos_token_id),
+         0.0 if missing_eos_penalty is None else float(missing_eos_penalty), int(missing_eos_penalty is not None),
+         float(kl_coef), int(kl_estimator == "k3"), lp.data_ptr(), rf.data_ptr(), v.data_ptr(), s.data_ptr(),
+         pm.data_ptr(), pm1.data_ptr(), kl.data_ptr(), nsr.data_ptr(), rew.data_ptr(), _stream())
+    return {"logprobs": lp, "ref_logprobs": rf, "values": v, "scores": s, "padding_mask": pm,
+            "padding_mask_p1": pm1, "kl": kl, "non_score_reward": nsr, "rewards": rew}
+
+
 def value_head(hidden: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None):
     """modeling_value_head.py:50-59 (eval) → fp32 [*hidden.shape[:-1]]."""
     _dev(hidden, "value_head")

@@ -70,17 +70,21 @@ def fill_batch_sizes(args: PPOConfig, dataset_len: int, world_size: int) -> PPOC
 
 
 def first_true_indices(bools: torch.Tensor, dtype=torch.long) -> torch.Tensor:
-    """utils.py:877-897: index of the first True per row, the row length if none."""
-    row_len = bools.size(-1)
-    zero_or_index = row_len * (~bools).type(dtype) + torch.arange(row_len, dtype=dtype, device=bools.device)
-    return torch.min(zero_or_index, dim=-1).values
+    """utils.py:877-897: per row, the index of the first True, or the row
+    length when there is none (argmax returns the first maximum)."""
+    first = bools.to(torch.uint8).argmax(-1)
+    return torch.where(bools.any(-1), first, bools.size(-1)).to(dtype)
 
 
 def truncate_response(stop_token_id: int, pad_token_id: int, responses: torch.Tensor) -> torch.Tensor:
-    """utils.py:1036-1056: pad everything after the first stop token."""
-    trunc_idxs = first_true_indices(responses == stop_token_id).unsqueeze(-1)
-    idxs = torch.arange(responses.shape[1], device=responses.device).view(1, -1)
-    return torch.masked_fill(responses, idxs > trunc_idxs, pad_token_id)
+    """utils.py:1036-1056: every token after the first stop token becomes pad.
+    Device tensors: one kernel (ops.ppo_truncate); host tensors (tests, data
+    prep): the same rule in torch."""
+    if responses.is_cuda:
+        return ops.ppo_truncate(responses, stop_token_id, pad_token_id)[0]
+    cut = first_true_indices(responses == stop_token_id)
+    after = torch.arange(responses.shape[1], device=responses.device) > cut.unsqueeze(1)
+    return torch.where(after, torch.full_like(responses, pad_token_id), responses)
 
 
 def _forward_inputs(query_responses: torch.Tensor, pad_token_id: int):
@@ -239,40 +243,23 @@ class PPOTrainer:
         # ref log-probs: forward, logits[:, P-1:-1] / (T + 1e-7), selective_log_softmax
         h = self._no_grad_hidden(self.ref_model, query_responses)
         ref_logprobs, _ = self.ref_model.logp_entropy(h[:, P - 1:P + T - 1], responses, temp, False)
-        # response processing 1: truncate after the first stop token
-        post = responses
-        if self.stop_token_id is not None:
-            post = truncate_response(self.stop_token_id, pad, responses)
-        sequence_lengths = first_true_indices(post == pad) - 1
+        # response processing 1: truncate after the first stop token, sequence lengths (one launch)
+        post, sequence_lengths = ops.ppo_truncate(responses, self.stop_token_id, pad)
         # values: value model over the raw query_responses, positions P-1 .. P+T-2 (bf16 like the score Linear)
         hv = self._no_grad_hidden(self.value_model, query_responses)
         values = self.value_model.scores(hv[:, P - 1:P + T - 1])
         # response processing 2: reward model score at the last non-pad token of query + truncated response
         pqr = torch.cat([queries, post], 1)
         hr = self._no_grad_hidden(self.reward_model, pqr)
-        rm_seq = first_true_indices(pqr[:, P:] == pad) - 1 + P
-        scores = self.reward_model.scores(hr[torch.arange(hr.shape[0], device=hr.device), rm_seq])  # bf16
+        scores = self.reward_model.scores(hr[torch.arange(hr.shape[0], device=hr.device), sequence_lengths + P])
         rm_scores = scores.clone()
-        # response processing 3: missing-stop penalty
-        contain_eos = torch.any(post == self.eos_token_id, dim=-1) if self.eos_token_id is not None else \
-            torch.zeros(post.shape[0], dtype=torch.bool, device=post.device)
-        if a.missing_eos_penalty is not None:
-            scores[~contain_eos] -= a.missing_eos_penalty
-        response_idxs = torch.arange(T, device=responses.device).repeat(responses.shape[0], 1)
-        padding_mask = response_idxs > sequence_lengths.unsqueeze(1)
-        logprobs = torch.masked_fill(logprobs.float(), padding_mask, INVALID_LOGPROB)
-        ref_logprobs = torch.masked_fill(ref_logprobs, padding_mask, INVALID_LOGPROB)
-        sequence_lengths_p1 = sequence_lengths + 1
-        padding_mask_p1 = response_idxs > sequence_lengths_p1.unsqueeze(1)
-        values = torch.masked_fill(values, padding_mask_p1, 0)
-        # 4. rewards: -kl_coef * KL (k1 / k3), score added at min(seq_len + 1, T - 1)
-        logr = ref_logprobs - logprobs
-        kl = -logr if a.kl_estimator == "k1" else (logr.exp() - 1) - logr
-        non_score_reward = -a.kl_coef * kl
-        rewards = non_score_reward.clone()
-        actual_start = torch.arange(rewards.size(0), device=rewards.device)
-        actual_end = torch.where(sequence_lengths_p1 < rewards.size(1), sequence_lengths_p1, sequence_lengths)
-        rewards[actual_start, actual_end] += scores
+        # 3.-4. missing-stop penalty, masks, INVALID_LOGPROB, KL and KL-shaped rewards (one launch)
+        r = ops.ppo_rewards(post, sequence_lengths, logprobs, ref_logprobs, values, scores,
+                            eos_token_id=self.eos_token_id, missing_eos_penalty=a.missing_eos_penalty,
+                            kl_coef=a.kl_coef, kl_estimator=a.kl_estimator)
+        logprobs, ref_logprobs, values, scores = r["logprobs"], r["ref_logprobs"], r["values"], r["scores"]
+        padding_mask, padding_mask_p1, rewards = r["padding_mask"], r["padding_mask_p1"], r["rewards"]
+        kl, non_score_reward = r["kl"], r["non_score_reward"]
         # 5. whiten rewards
         if a.whiten_rewards:
             rewards = ops.masked_whiten(rewards, ~padding_mask_p1, shift_mean=False)

@@ -264,6 +264,47 @@ def test_masked_whiten(ops, dev):
         ops.masked_var(v.to(dev), torch.zeros_like(m).to(dev))
 
 
+@pytest.mark.parametrize("stop,est,pen", [(3, "k1", None), (3, "k3", 1.0), (None, "k1", 0.5)])
+def test_ppo_rollout_postprocess_matches_oracle(ops, dev, stop, est, pen):
+    """swh_ppo_truncate + swh_ppo_rewards against the oracle's restatement of
+    ppo_trainer.py:478-516 (truncate_response, first_true_indices, masks,
+    INVALID_LOGPROB, value masking, missing-EOS penalty, k1/k3 KL, the score
+    scatter): stop at t = 0, no stop token, a row already full of pads."""
+    g = _gen(40)
+    B, T, PAD, EOS = 9, 23, 0, 3
+    resp = torch.randint(4, 50, (B, T), generator=g)
+    resp[0, 0] = 3
+    resp[1, 7] = 3
+    resp[2, 22] = 3
+    resp[3, 5] = 3
+    resp[3, 9] = 3
+    resp[4, :] = PAD
+    resp[5, 11] = PAD  # a pad token generated before any stop
+    lp = -torch.rand(B, T, generator=g) * 3
+    ref = lp + 0.1 * torch.randn(B, T, generator=g)
+    vals = torch.randn(B, T, generator=g).to(torch.bfloat16)
+    sc = torch.randn(B, generator=g).to(torch.bfloat16)
+    post, seq = ops.ppo_truncate(resp.to(dev), stop, PAD)
+    exp_post = trl_ref.truncate_response(stop, PAD, resp) if stop is not None else resp
+    exp_seq = trl_ref.first_true_indices(exp_post == PAD) - 1
+    assert torch.equal(post.cpu(), exp_post) and torch.equal(seq.cpu(), exp_seq)
+    r = ops.ppo_rewards(post, seq, lp.to(dev), ref.to(dev), vals.to(dev), sc.to(dev), eos_token_id=EOS,
+                        missing_eos_penalty=pen, kl_coef=0.05, kl_estimator=est)
+    idx = torch.arange(T).repeat(B, 1)
+    pm, pm1 = idx > exp_seq[:, None], idx > (exp_seq + 1)[:, None]
+    assert torch.equal(r["padding_mask"].cpu(), pm) and torch.equal(r["padding_mask_p1"].cpu(), pm1)
+    elp = lp.masked_fill(pm, trl_ref.INVALID_LOGPROB)
+    eref = ref.masked_fill(pm, trl_ref.INVALID_LOGPROB)
+    esc = sc.clone()
+    if pen is not None:
+        esc[~torch.any(exp_post == EOS, -1)] -= pen
+    rew, kl, nsr = trl_ref.ppo_rewards(elp, eref, esc, exp_seq, 0.05, est)
+    assert torch.equal(r["logprobs"].cpu(), elp) and torch.equal(r["ref_logprobs"].cpu(), eref)
+    assert torch.equal(r["values"].cpu(), vals.masked_fill(pm1, 0)) and torch.equal(r["scores"].cpu(), esc)
+    for k, e in (("kl", kl), ("non_score_reward", nsr), ("rewards", rew)):
+        torch.testing.assert_close(r[k].cpu(), e, rtol=1e-6, atol=1e-6, msg=k)
+
+
 def test_gae(ops, dev):
     g = _gen(11)
     r = torch.randn(64, 53, generator=g)
@@ -804,6 +845,43 @@ def test_decode_gemm_plain(ops, dev, M, N, K, norm):
     if b is not None:
         ref = ref + b.float()
     torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("name,M,N,K", [("qkv", 64, 6144, 4096), ("o", 64, 4096, 4096), ("lm_head", 64, 128256, 4096),
+                                        ("down", 64, 4096, 14336)])
+def test_decode_gemm_llama3_8b_shapes(ops, dev, name, M, N, K):
+    """BASELINE config 5 decode projections (Llama-3-8B: H 4096, I 14336, V
+    128256, GQA 32:8 x 128, untied head) at 64 rows: plain / folded-norm /
+    residual epilogues against an fp32 reference."""
+    from swh_trl_amd import nn_ops
+    g = _gen(33)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(dev)
+    if name == "down":
+        s = torch.randn(M, N, generator=g).to(torch.bfloat16).to(dev)
+        s0 = s.clone()
+        nn_ops.decode_gemm(x, w, residual=s)
+        ref = s0 + (x.float() @ w.float().t()).to(torch.bfloat16)
+        torch.testing.assert_close(s.float(), ref.float(), rtol=1e-2, atol=2e-2)
+        return
+    nw = (1 + 0.1 * torch.randn(K, generator=g)).to(torch.bfloat16).to(dev)
+    y = nn_ops.decode_gemm(x, w, norm_w=nw, eps=1e-5)
+    ref = _ref_norm(x, nw, 1e-5).float() @ w.float().t()
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=2e-2)
+
+
+def test_decode_gemm_llama3_8b_gate_up(ops, dev):
+    """Config 5 gate/up (2 x 14336 rows over K 4096) with the SiLU epilogue."""
+    from swh_trl_amd import nn_ops
+    g = _gen(34)
+    M, H, I = 64, 4096, 14336
+    s = torch.randn(M, H, generator=g).to(torch.bfloat16).to(dev)
+    wgu = (torch.randn(2 * I, H, generator=g) * H ** -0.5).to(torch.bfloat16).to(dev)
+    nw = (1 + 0.1 * torch.randn(H, generator=g)).to(torch.bfloat16).to(dev)
+    act = nn_ops.decode_gemm(s, wgu, norm_w=nw, eps=1e-5, silu=True)
+    gu = (_ref_norm(s, nw, 1e-5).float() @ wgu.float().t()).to(torch.bfloat16)
+    ref = torch.nn.functional.silu(gu[:, :I]) * gu[:, I:]
+    torch.testing.assert_close(act.float(), ref.float(), rtol=2e-2, atol=2e-2)
 
 
 def test_decode_gemm_residual_and_silu(ops, dev):

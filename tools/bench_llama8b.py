@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--C", type=int, default=256)
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--fuse-budget", type=int, default=1 << 17,
+                    help="GA micro-batches run as one pass up to this many tokens (activation memory)")
     args = ap.parse_args()
     from swh_trl_amd.engine import llama3_8b
     from swh_trl_amd.trainer import GRPOConfig, GRPOTrainer
@@ -44,7 +46,8 @@ def main():
     mb = min(B, 8)
     gc = GRPOConfig(output_dir="/tmp/grpo-llama", per_device_train_batch_size=mb, gradient_accumulation_steps=B // mb,
                     num_generations=G, max_prompt_length=P, max_completion_length=C, learning_rate=1e-6, beta=0.04,
-                    max_steps=args.steps + args.warmup, logging_steps=10 ** 9, seed=0,
+                    max_steps=args.steps + args.warmup, logging_steps=10 ** 9, seed=0, save_strategy="no",
+                    fuse_token_budget=args.fuse_budget,
                     generation_kwargs={"min_new_tokens": C, "eos_token_id": 128001, "pad_token_id": 128002})
     t0 = time.perf_counter()
     tr = GRPOTrainer(model=cfg, reward_funcs=rew, args=gc, train_dataset=ds)
@@ -68,6 +71,7 @@ def main():
                       "decode_step_us": round(dec.get("decode_step", {}).get("avg_us", float("nan")), 1),
                       "decode_kernels_us": {k: round(v["avg_us"], 2) for k, v in dec.items()},
                       "peak_mem_GiB": round(torch.cuda.max_memory_allocated() / 2**30, 1),
+                      "fuse_token_budget": args.fuse_budget,
                       "loss": log.get("loss"), "kl": log.get("kl")}), flush=True)
 
 
