@@ -60,6 +60,14 @@ int swh_logp_entropy_fwd(const void *logits, int dtype, int64_t rows_outer, int6
  * of the temperature division): dlogits[r, j] = dlogp[r]/T * (1[j==ids[r]] - p_j).
  * dlogits has the logits dtype and its own (outer, inner) strides; row
  * stride between elements is 1. */
+/* selective_log_softmax for bf16/fp16 rows of V <= 1024 (trl/trainer/utils.py:1451-1459,
+ * the half-precision `log_softmax(row).gather` branch): the fp32 operations of
+ * torch's persistent warp softmax in its order, so out (logits dtype, [rows])
+ * equals torch.gather(logits.log_softmax(-1), -1, ids) bit for bit
+ * (tests/test_utils.py:540-558).  SWH_E_ARG for V > 1024, SWH_E_DTYPE for f32. */
+int swh_log_softmax_gather_exact(const void *logits, int dtype, int64_t rows_outer, int64_t rows_inner,
+                                 int64_t stride_outer, int64_t stride_inner, int64_t V, const int64_t *ids,
+                                 void *out, void *stream);
 int swh_logp_bwd(const void *logits, int dtype, int64_t rows_outer, int64_t rows_inner,
                  int64_t stride_outer, int64_t stride_inner, int64_t V, const int64_t *ids,
                  float temperature, int flags, const float *lse, const float *dlogp, void *dlogits,

@@ -16,6 +16,7 @@ for step in "$@"; do
     gpu) run gpu 1100 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
     gpuall) run gpuall 1100 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread ;;
     new2) run new2 900 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -k "rewards or checkpoint or dp_ or step_parity" ;;
+    newp) run newp 600 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -s -k "selective_log_softmax or greedy_matches" ;;
     newt) run newt 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread -k "step_parity or adamw or bench_launches or masked_whiten" ;;
     tune) SWH_GEMM_TUNING=tune SWH_GEMM_TABLE=gpurun_out/gemm_tuned.csv run tune 900 python bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
     benchtuned) SWH_GEMM_TABLE=gpurun_out/gemm_tuned.csv run benchtuned 600 python bench.py --steps 3 --warmup 2 --no-cpu-baseline ;;
@@ -45,7 +46,7 @@ for step in "$@"; do
     serial2) AMD_SERIALIZE_KERNEL=3 SWH_TRACE=1 run serial2 500 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --layers 2 ;;
     trace2) SWH_TRACE=1 run trace2 400 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --layers 2 ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null && run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
-    l8) run l8 1000 python tools/bench_llama8b.py --prompts 8 --P 256 --C 1024 --steps 1 --warmup 1 --fuse-budget 16384 ;;
+    l8) SWH_TRACE=1 run l8 1000 python tools/bench_llama8b.py --prompts 8 --P 256 --C 1024 --steps 1 --warmup 1 --fuse-budget 16384 ;;
     l8k) run l8k 600 python -u -m pytest tests/test_kernels_gpu.py -v -m gpu -k "llama3_8b" --timeout 200 --timeout-method thread ;;
     tk) run tk 600 python tools/train_kernels.py ;;
     proftk) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null && run proftk 600 rocprofv3 --kernel-trace --stats -d gpurun_out/proftk -o run --output-format csv -- python3 tools/train_kernels.py ;;

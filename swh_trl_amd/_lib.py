@@ -40,6 +40,7 @@ SIGNATURES = {
     "swh_status_string": (C.c_char_p, [c_i32]),
     "swh_logp_entropy_fwd": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_f32, c_i32,
                                      c_vp, c_vp, c_vp, c_vp]),
+    "swh_log_softmax_gather_exact": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "swh_logp_bwd": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_f32, c_i32, c_vp, c_vp,
                              c_vp, c_i64, c_i64, c_vp]),
     "swh_sample_workspace_bytes": (c_i64, [c_i64, c_i64]),

@@ -161,6 +161,54 @@ __global__ __launch_bounds__(kThreads) void logp_bwd_kernel(
     for (int64_t j = body_end + threadIdx.x; j < V; j += kThreads) store(j, grad(Elem<DT>::load(row + j), j));
 }
 
+// Half-precision rows of V <= 1024: the reference's bf16/fp16 branch
+// (utils.py:1451-1459) is `log_softmax(row)` then gather, and its own test
+// (test_utils.py:540-558) asks for bit equality with torch's log_softmax.  For
+// these widths torch's device kernel is the persistent warp softmax (ATen
+// PersistentSoftmax.cuh, softmax_warp_forward): WS = min(2^ceil(log2 V), 64)
+// lanes per row, lane l holds elements l + it*WS (it < 2^ceil(log2 V)/WS,
+// -inf past V), a sequential per-lane max / sum of exp(x - max) in it order,
+// then xor-butterfly merges (offsets WS/2 .. 1) with max(a, b) = a < b ? b : a
+// and a + b; out = (x - max) - log(sum) in fp32, rounded once (RNE).  This
+// kernel performs exactly those fp32 operations in that order, with the
+// accurate expf / logf (not the fast forms the fused kernel uses), so the
+// gathered value is the same bits.  One WS-lane group per row.
+template <int DT>
+__global__ __launch_bounds__(kThreads) void log_softmax_gather_exact_kernel(const uint16_t *__restrict__ logits,
+                                                                           RowAddr ra, int V, int ws, int iters,
+                                                                           const int64_t *__restrict__ ids,
+                                                                           int64_t R, uint16_t *__restrict__ out) {
+    const int lane = threadIdx.x & (ws - 1);
+    const int64_t r = ((int64_t)blockIdx.x * kThreads + threadIdx.x) / ws;
+    const bool live = r < R;  // dead groups still take part in the shuffles of their wave
+    const uint16_t *row = logits + ra.off(live ? r : 0);
+    float e[16];
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+        const int j = lane + it * ws;
+        e[it] = (it < iters && j < V) ? Elem<DT>::load(row + j) : kNegInf;
+    }
+    float mx = e[0];
+#pragma unroll
+    for (int it = 0; it < 16; ++it)
+        if (it < iters) mx = mx > e[it] ? mx : e[it];
+    for (int off = ws / 2; off > 0; off >>= 1) {
+        const float b = __shfl_xor(mx, off, ws);
+        mx = mx < b ? b : mx;
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int it = 0; it < 16; ++it)
+        if (it < iters) sum += expf(e[it] - mx);
+    for (int off = ws / 2; off > 0; off >>= 1) sum = sum + __shfl_xor(sum, off, ws);
+    if (!live || lane != 0) return;
+    const float ls = logf(sum);
+    const int64_t id = ids[r];
+    float v = __builtin_nanf("");
+    if (id >= 0 && id < V) v = (Elem<DT>::load(row + id) - mx) - ls;
+    out[r] = (DT == SWH_BF16) ? f32_to_bf16_bits(v) : f32_to_f16_bits(v);
+}
+
 bool rows_ok(int64_t outer, int64_t inner, int64_t V) {
     return outer >= 0 && inner >= 0 && V > 0 && outer * inner < (int64_t)1 << 31;
 }
@@ -197,6 +245,30 @@ extern "C" int swh_logp_entropy_fwd(const void *logits, int dtype, int64_t rows_
     default:
         return SWH_E_DTYPE;
     }
+    return launch_status();
+}
+
+extern "C" int swh_log_softmax_gather_exact(const void *logits, int dtype, int64_t rows_outer, int64_t rows_inner,
+                                            int64_t stride_outer, int64_t stride_inner, int64_t V,
+                                            const int64_t *ids, void *out, void *stream) {
+    if (!rows_ok(rows_outer, rows_inner, V) || V > 1024) return SWH_E_ARG;
+    if (dtype != SWH_BF16 && dtype != SWH_F16) return SWH_E_DTYPE;
+    const int64_t R = rows_outer * rows_inner;
+    if (R == 0) return SWH_OK;
+    if (!logits || !ids || !out) return SWH_E_ARG;
+    int p2 = 1;
+    while (p2 < V) p2 <<= 1;
+    const int ws = p2 < kWave ? p2 : kWave, iters = p2 / ws;
+    RowAddr ra{rows_outer, rows_inner, stride_outer, stride_inner};
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int64_t groups_per_block = kThreads / ws;
+    dim3 grid((unsigned)((R + groups_per_block - 1) / groups_per_block)), block(kThreads);
+    const uint16_t *lg = static_cast<const uint16_t *>(logits);
+    uint16_t *o = static_cast<uint16_t *>(out);
+    if (dtype == SWH_BF16)
+        log_softmax_gather_exact_kernel<SWH_BF16><<<grid, block, 0, s>>>(lg, ra, (int)V, ws, iters, ids, R, o);
+    else
+        log_softmax_gather_exact_kernel<SWH_F16><<<grid, block, 0, s>>>(lg, ra, (int)V, ws, iters, ids, R, o);
     return launch_status();
 }
 

@@ -127,7 +127,21 @@ def logp_entropy_autograd(logits, index, temperature: float = 1.0, compute_entro
 
 def selective_log_softmax(logits: torch.Tensor, index: torch.Tensor) -> torch.Tensor:
     """trl/trainer/utils.py:1430 — log_softmax(logits).gather(index); output in the
-    logits dtype like the reference (bf16/fp16 rounded once from fp32)."""
+    logits dtype like the reference.  bf16/fp16 rows of V <= 1024 take the
+    exact-order kernel (bit-equal to torch's log_softmax, as the reference's
+    test_utils.py:540-558 asks); wider half-precision rows and fp32/fp64 go
+    through the fused fp32 kernel (wider bf16 rows: see DESIGN.md §8)."""
+    _dev(logits, "selective_log_softmax")
+    if logits.dtype in (torch.bfloat16, torch.float16) and 0 < logits.shape[-1] <= 1024:
+        lg = logits.reshape(-1, logits.shape[-1]) if logits.dim() > 3 else logits
+        o, i, so, si, V = _rows_view(lg)
+        idx = index.reshape(-1).to(torch.int64).contiguous()
+        if idx.numel() != o * i:
+            raise ValueError("index shape must match logits.shape[:-1]")
+        out = torch.empty(o * i, device=logits.device, dtype=logits.dtype)
+        call("swh_log_softmax_gather_exact", lg.data_ptr(), _dtype_code(lg, "selective_log_softmax"), o, i, so, si,
+             V, idx.data_ptr(), out.data_ptr(), _stream())
+        return out.view(index.shape)
     logp, _, _ = logp_entropy(logits, index, 1.0, False)
     return logp.to(logits.dtype)
 

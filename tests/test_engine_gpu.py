@@ -132,13 +132,55 @@ def test_fused_sampler_generation_equals_logits_path(dev, monkeypatch, kw):
     assert torch.equal(outs[0], outs[1])
 
 
-def test_greedy_matches_transformers_generate(dev):
-    """First-divergence index vs transformers generate (bf16 both sides)."""
-    from swh_trl_amd.engine import DecodeEngine
-    m = _tiny(dev, seed=3)
+def _greedy_divergence_report(m, ids, mine, ref, max_ulps):
+    """Greedy ids of the engine vs transformers bf16 generate, row by row.
+
+    Both pick argmax over bf16 logits with the lowest index on ties
+    (torch.argmax), so two bf16 implementations can only part where the two
+    candidates' logits lie within bf16 rounding noise of each other.  For every
+    row that diverges, the cause is measured: the fp32 transformers model on
+    the common prefix gives the two candidates' logits, and their gap in units
+    of one bf16 ulp at the top logit must be <= max_ulps.  Returns
+    [(row, first divergence or None, gap in ulps)]."""
+    hf32 = _hf_from(m, torch.float32)
+    rep = []
+    for b in range(ids.shape[0]):
+        neq = (mine[b] != ref[b]).nonzero()
+        if neq.numel() == 0:
+            rep.append((b, None, 0.0))
+            continue
+        t = int(neq[0])
+        seq = torch.cat([ids[b], ref[b, :t]]).unsqueeze(0)
+        with torch.no_grad():
+            z = hf32(input_ids=seq).logits[0, -1].double()
+        top = z.max().abs().item()
+        ulp = 2.0 ** (torch.tensor(top).log2().floor().item() - 7)  # bf16: 8 significant bits
+        gap = abs(z[int(mine[b, t])] - z[int(ref[b, t])]).item() / ulp
+        rep.append((b, t, gap))
+    print("greedy first divergences (row, step, fp32 gap in bf16 ulps):", rep)
+    bad = [r for r in rep if r[1] is not None and r[2] > max_ulps]
+    assert not bad, bad
+    return rep
+
+
+@pytest.mark.parametrize("shape", ["tiny", "qwen2.5-0.5b-width"])
+@pytest.mark.parametrize("fold", ["1", "0"])
+def test_greedy_matches_transformers_generate(dev, monkeypatch, shape, fold):
+    """Greedy ids vs transformers bf16 generate: equal up to the first step
+    whose two candidate logits are a bf16 tie (<= 2 ulps apart in fp32), at the
+    tiny preset and at the real Qwen2.5-0.5B width (H 896, V 151936, 14:2
+    heads, 2 layers); folded decode RMSNorm (default) and the exact form."""
+    from swh_trl_amd.engine import CausalLM, DecodeEngine
+    from swh_trl_amd.engine.config import DecoderConfig
+    monkeypatch.setenv("SWH_DECODE_FOLD", fold)
+    if shape == "tiny":
+        m = _tiny(dev, seed=3)
+        B, P, C = 4, 10, 32
+    else:
+        m = CausalLM(DecoderConfig(num_hidden_layers=2), dev, seed=3, init_std=0.02)
+        B, P, C = 8, 16, 48
     hf = _hf_from(m, torch.bfloat16)
     g = torch.Generator().manual_seed(3)
-    B, P, C = 4, 10, 32
     ids = torch.randint(0, m.cfg.vocab_size, (B, P), generator=g).to(dev)
     mask = torch.ones(B, P, dtype=torch.int64, device=dev)
     eng = DecodeEngine(m, B, P, C)
@@ -146,18 +188,9 @@ def test_greedy_matches_transformers_generate(dev):
     with torch.no_grad():
         ref = hf.generate(input_ids=ids, attention_mask=mask, max_new_tokens=C, do_sample=False,
                           pad_token_id=0, eos_token_id=None)[:, P:]
-    # Every first divergence must sit at a bf16 near-tie of the transformers
-    # logits on the common prefix (top-2 gap below 1% of the logit scale).
-    for b in range(B):
-        neq = (mine[b] != ref[b]).nonzero()
-        if neq.numel() == 0:
-            continue
-        t = int(neq[0])
-        seq = torch.cat([ids[b], ref[b, :t]]).unsqueeze(0)
-        with torch.no_grad():
-            lg = hf(input_ids=seq).logits[0, -1].float()
-        top2 = lg.topk(2).values
-        assert (top2[0] - top2[1]).item() <= 0.01 * lg.abs().max().item() + 1e-3, (b, t, top2)
+    rep = _greedy_divergence_report(m, ids, mine, ref, max_ulps=2.0)
+    # most rows agree over the whole completion
+    assert sum(t is None for _, t, _ in rep) >= len(rep) // 4, rep
 
 
 def test_sampled_rollout_is_reproducible_and_respects_min_new_tokens(dev):

@@ -51,13 +51,32 @@ def test_logp_entropy_reference_shape(ops, dev, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-def test_selective_log_softmax_lowp_matches_torch(ops, dev, dtype):
-    """Reference test_utils.py:540-558 asks bf16/fp16 outputs to equal
-    gather(log_softmax) bit-for-bit.  The fused kernel reassociates the fp32
-    sum, so the bound here is: >= 99.9% bit-identical, the rest 1 ulp."""
+@pytest.mark.parametrize("V", [1024, 1000, 128, 100, 33, 7, 1])
+def test_selective_log_softmax_lowp_bit_exact(ops, dev, dtype, V):
+    """Reference test_utils.py:540-558: bf16/fp16 outputs equal
+    gather(log_softmax) bit for bit (its shape is 4 x 32 x 1024; narrower rows
+    exercise the sub-wave lane groups of torch's warp softmax)."""
     g = _gen(1)
-    logits = torch.randn(4, 32, 1024, generator=g).to(dtype).to(dev)
-    ids = torch.randint(0, 1024, (4, 32), generator=g).to(dev)
+    logits = (torch.randn(4, 32, V, generator=g) * 3).to(dtype).to(dev)
+    ids = torch.randint(0, V, (4, 32), generator=g).to(dev)
+    got = ops.selective_log_softmax(logits, ids)
+    exp = torch.gather(logits.log_softmax(-1), -1, ids.unsqueeze(-1)).squeeze(-1)
+    assert got.dtype == dtype
+    assert torch.equal(got, exp), (got != exp).sum().item()
+    # a strided [R, T, V] view (rows of a longer buffer) as the trainer slices logits
+    wide = torch.randn(4, 33, V, generator=g).to(dtype).to(dev)[:, 1:]
+    got = ops.selective_log_softmax(wide, ids)
+    assert torch.equal(got, torch.gather(wide.log_softmax(-1), -1, ids.unsqueeze(-1)).squeeze(-1))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_selective_log_softmax_lowp_wide_rows(ops, dev, dtype):
+    """Rows wider than 1024 (torch's block softmax, whose reduction order is not
+    restated): the fused fp32 kernel rounded once; >= 99.9% bit-identical, the
+    rest 1 ulp."""
+    g = _gen(1)
+    logits = torch.randn(4, 32, 4096, generator=g).to(dtype).to(dev)
+    ids = torch.randint(0, 4096, (4, 32), generator=g).to(dev)
     got = ops.selective_log_softmax(logits, ids)
     exp = torch.gather(logits.log_softmax(-1), -1, ids.unsqueeze(-1)).squeeze(-1)
     assert got.dtype == dtype
