@@ -46,6 +46,12 @@ for step in "$@"; do
     serial2) AMD_SERIALIZE_KERNEL=3 SWH_TRACE=1 run serial2 500 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --layers 2 ;;
     trace2) SWH_TRACE=1 run trace2 400 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --layers 2 ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null && run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
+    l8s) SWH_TRACE=1 run l8s 400 python tools/bench_llama8b.py --prompts 2 --P 256 --C 1024 --steps 1 --warmup 1 --fuse-budget 16384 ;;
+    hangp) run hangp 150 python tools/phase_probe.py --layers 2 --B 8 --L 512 && run hangp2 150 python tools/phase_probe.py --layers 2 --B 8 --L 1280 ;;
+    hangq) run hangq 120 python tools/phase_probe.py --layers 1 --B 8 --L 1280 --part lmhead && run hangq2 120 python tools/phase_probe.py --layers 1 --B 8 --L 1280 --part attn ;;
+    hangs) AMD_SERIALIZE_KERNEL=3 run hangs 100 python tools/phase_probe.py --layers 1 --B 8 --L 1280 ;;
+    hangt) SWH_DW_STREAM=0 SWH_ATTN_SPLIT=0 run hangt1 100 python tools/phase_probe.py --layers 2 --B 8 --L 1280 && SWH_GEMM_TUNING=off run hangt2 100 python tools/phase_probe.py --layers 2 --B 8 --L 1280 ;;
+    hangf) run hangf 100 python tools/phase_probe.py --layers 2 --B 8 --L 1280 --reps 3 ;;
     l8) SWH_TRACE=1 run l8 1000 python tools/bench_llama8b.py --prompts 8 --P 256 --C 1024 --steps 1 --warmup 1 --fuse-budget 16384 ;;
     l8k) run l8k 600 python -u -m pytest tests/test_kernels_gpu.py -v -m gpu -k "llama3_8b" --timeout 200 --timeout-method thread ;;
     tk) run tk 600 python tools/train_kernels.py ;;

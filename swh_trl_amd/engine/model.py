@@ -63,6 +63,35 @@ def dw_sync(dev: torch.device):
     for st in dw_streams(dev):
         torch.cuda.current_stream(dev).wait_stream(st)
     _DW_KEEP.clear()
+    _SIDE_GEMM.pop(dev.index, None)
+
+
+_GEMM_FENCE = os.environ.get("SWH_GEMM_FENCE", "1") != "0"  # A/B only: 0 can deadlock (below)
+_SIDE_GEMM: dict = {}  # device index -> event after the last library GEMM issued on the side stream
+
+
+def _side_gemm_issued(st) -> None:
+    """Mark that library GEMMs were just issued on side stream `st`."""
+    if st is not None:
+        ev = torch.cuda.Event()
+        ev.record(st)
+        _SIDE_GEMM[st.device.index] = ev
+
+
+def _main_gemm_fence(dev: torch.device) -> None:
+    """Before a library GEMM on the compute stream, wait for the side stream's
+    GEMMs issued so far.  hipBLASLt may pick persistent (stream-K style)
+    solutions whose workgroups wait on each other's partial tiles; two of them
+    running at once on two streams each hold part of the CUs while waiting for
+    workgroups that cannot be placed, and both spin forever (observed at the
+    Llama-3-8B shapes with 10240-token passes, tools/phase_probe.py; no hang
+    with the side stream off).  Each side GEMM already waits for the compute
+    stream's work issued before it, so with this fence no two library GEMMs
+    overlap; the side GEMMs still overlap the compute stream's HIP kernels
+    (norm / SiLU / attention / log-prob backward)."""
+    ev = _SIDE_GEMM.pop(dev.index, None) if dev.type == "cuda" else None
+    if ev is not None and _GEMM_FENCE:
+        torch.cuda.current_stream(dev).wait_event(ev)
 
 
 class _OnStream:
@@ -106,7 +135,10 @@ class _Linear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        dx = dy @ w if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            _main_gemm_fence(dy.device)
+            dx = dy @ w
         if ctx.gw is not None:
             _accumulate_dw(ctx.gw, ctx.gb, dy, x)
         return dx, None, None, None, None
@@ -132,6 +164,7 @@ def _accumulate_dw(gw, gb, dy, x):
                 gw.addmm_(dy2[S * Kc:].t(), x2[S * Kc:])
         else:
             gw.addmm_(dy2.t(), x2)
+        _side_gemm_issued(side.st)
         if gb is not None:  # bias: token sums of dy, fixed order, folded into the view once
             bias_grad_accumulate(dy2, gb)
 
@@ -333,11 +366,13 @@ class _LMHeadLogp(torch.autograd.Function):
             r1 = r0 + lg.shape[0]
             ops.logp_backward(lg, idx[r0:r1], lse[r0:r1], g[r0:r1], ctx.temperature, out=lg)  # in place
             if dh is not None:
+                _main_gemm_fence(lg.device)
                 torch.mm(lg, w, out=dh[r0:r1])
             if ctx.gw is not None:  # beside the next chunk's (HBM-bound) logp backward
                 with _OnStream(_dw_stream(lg.device)) as side:
                     side.keep(lg, h2)
                     ctx.gw.addmm_(lg.t(), h2[r0:r1])
+                    _side_gemm_issued(side.st)
         ctx.chunks = None
         return (dh.view(ctx.hshape) if dh is not None else None), None, None, None, None, None, None
 

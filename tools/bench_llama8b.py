@@ -50,6 +50,15 @@ def main():
                     fuse_token_budget=args.fuse_budget,
                     generation_kwargs={"min_new_tokens": C, "eos_token_id": 128001, "pad_token_id": 128002})
     t0 = time.perf_counter()
+
+    def heartbeat():  # long phases (backward of an 8B model) print nothing for minutes
+        while True:
+            time.sleep(20)
+            print(f"[llama8b] alive {time.perf_counter() - t0:.0f}s, "
+                  f"{torch.cuda.memory_allocated() / 2**30:.1f} GiB allocated", file=sys.stderr, flush=True)
+
+    import threading
+    threading.Thread(target=heartbeat, daemon=True).start()
     tr = GRPOTrainer(model=cfg, reward_funcs=rew, args=gc, train_dataset=ds)
     print(f"[llama8b] init {time.perf_counter() - t0:.1f}s, "
           f"{torch.cuda.memory_allocated() / 2**30:.1f} GiB allocated", file=sys.stderr, flush=True)
