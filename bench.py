@@ -91,9 +91,38 @@ def cpu_baseline(steps_note: str) -> dict:
     og.grpo_step(model, opt, prompt, pm, reward, C=C, min_new_tokens=C, timings=tm, **kw)
     wall = time.perf_counter() - t0
     return {"value": G / wall, "unit": "samples/s", "cores": threads, "kind": "port", "cpu": _cpu_model(),
+            "cfg1": cpu_cfg1(threads),
             "sample": (f"oracle/grpo_step.py (CPU restatement, transformers Qwen2 bf16, torch {torch.__version__}) on "
                        f"1 prompt x G={G}, P={P}, C={C} (full length): generate {tm['generate_s']:.2f}s + update "
                        f"{tm['update_s']:.2f}s = {wall:.2f}s wall for {G} samples, {threads} threads; {steps_note}")}
+
+
+def cpu_cfg1(threads: int, steps: int = 2) -> dict:
+    """BASELINE.json config 1 on the host (tiny random GPT-2, 4
+    prompts x G=2 x 16 tokens, P=8, fp32, 2 optimizer steps) through the same
+    oracle step; tools/bench_cfg1.py runs the product on the GPU beside it."""
+    from oracle import grpo_step as og
+    from swh_trl_amd.engine.gpt2 import gpt2_config
+    torch.set_num_threads(threads)
+    cfg = gpt2_config().to_dict()
+    model = og.hf_gpt2_from_config(cfg, seed=0)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-6)
+    g = torch.Generator().manual_seed(1234)
+    prompt = torch.randint(2, cfg["vocab_size"], (4, 8), generator=g).repeat_interleave(2, 0)
+
+    def reward(cids, cmask):
+        return [len(set(r[m.bool()].tolist())) % 7 for r, m in zip(cids, cmask)]
+
+    kw = dict(num_generations=2, per_device_train_batch_size=8, gradient_accumulation_steps=1, eos_token_id=EOS,
+              pad_token_id=PAD, C=16, min_new_tokens=16)
+    og.grpo_step(model, opt, prompt, torch.ones_like(prompt), reward, **kw)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        og.grpo_step(model, opt, prompt, torch.ones_like(prompt), reward, **kw)
+    wall = time.perf_counter() - t0
+    return {"value": 8 * steps / wall, "unit": "samples/s", "cores": threads,
+            "sample": f"configs[0]: GPT-2 (vocab 1024, n_embd 32, 2 layers) 4 prompts x G=2 x 16 tok, P=8, fp32, "
+                      f"{steps} steps in {wall:.3f}s"}
 
 
 PMC_FILE = os.path.join(ROOT, "profiles", "r2_pmc_decode.json")

@@ -60,6 +60,10 @@ int swh_logp_entropy_fwd(const void *logits, int dtype, int64_t rows_outer, int6
  * of the temperature division): dlogits[r, j] = dlogp[r]/T * (1[j==ids[r]] - p_j).
  * dlogits has the logits dtype and its own (outer, inner) strides; row
  * stride between elements is 1. */
+int swh_logp_bwd(const void *logits, int dtype, int64_t rows_outer, int64_t rows_inner,
+                 int64_t stride_outer, int64_t stride_inner, int64_t V, const int64_t *ids,
+                 float temperature, int flags, const float *lse, const float *dlogp, void *dlogits,
+                 int64_t dstride_outer, int64_t dstride_inner, void *stream);
 /* selective_log_softmax for bf16/fp16 rows of V <= 1024 (trl/trainer/utils.py:1451-1459,
  * the half-precision `log_softmax(row).gather` branch): the fp32 operations of
  * torch's persistent warp softmax in its order, so out (logits dtype, [rows])
@@ -68,10 +72,7 @@ int swh_logp_entropy_fwd(const void *logits, int dtype, int64_t rows_outer, int6
 int swh_log_softmax_gather_exact(const void *logits, int dtype, int64_t rows_outer, int64_t rows_inner,
                                  int64_t stride_outer, int64_t stride_inner, int64_t V, const int64_t *ids,
                                  void *out, void *stream);
-int swh_logp_bwd(const void *logits, int dtype, int64_t rows_outer, int64_t rows_inner,
-                 int64_t stride_outer, int64_t stride_inner, int64_t V, const int64_t *ids,
-                 float temperature, int flags, const float *lse, const float *dlogp, void *dlogits,
-                 int64_t dstride_outer, int64_t dstride_inner, void *stream);
+
 
 /* ---- a4: one rollout sampling step ----------------------------------------
  * Replaces the HF `_sample` body the reference reaches through
@@ -444,6 +445,31 @@ int swh_lm_head_sample_step(const void *x, const void *w, int64_t M, int64_t V, 
                             int32_t *step, int32_t *finished, int64_t *out_tokens, int64_t out_ld,
                             int64_t *cur_tokens, const void *embed, void *x_next, float *ss_next, void *workspace,
                             int64_t workspace_bytes, void *stream);
+
+/* ---- GPT-2 family (BASELINE.json config 1) --------------------------------
+ * transformers GPT2Block's LayerNorms and NewGELUActivation (the modeling code
+ * the reference's tiny-random-GPT2 tests run through grpo_trainer.py:1249 /
+ * :1804), bf16 or fp32.  dtype SWH_BF16 / SWH_F32; every tensor in it.
+ *
+ * swh_layernorm_fwd: s = residual ? dtype(x + residual) : x (written to s_out
+ * when residual is given), y = dtype((s - mean) * rstd * w + b) with fp32
+ * mean, biased variance and rstd = 1/sqrt(var + eps) per row (saved). */
+int swh_layernorm_fwd(const void *x, const void *residual, const void *w, const void *b, int64_t rows, int64_t H,
+                      float eps, void *y, void *s_out, float *mean, float *rstd, int32_t dtype, void *stream);
+/* Rows of partial sums the backward writes: ceil(rows / rows_per_block). */
+int64_t swh_layernorm_bwd_partial_rows(int64_t rows, int64_t rows_per_block);
+/* dx = rstd (g - mean(g) - xhat mean(g xhat)) + dres (nullable), g = dy w;
+ * part_w / part_b (nullable together) [partial_rows][H] fp32: per block of
+ * rows_per_block rows, sum dy * xhat and sum dy in fixed row order
+ * (fold them into the gradient views with swh_rmsnorm_dw_accum). */
+int swh_layernorm_bwd(const void *s, const void *w, const float *mean, const float *rstd, const void *dy,
+                      const void *dres, int64_t rows, int64_t H, int64_t rows_per_block, void *dx, float *part_w,
+                      float *part_b, int32_t dtype, void *stream);
+/* gelu_new: y = 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3))) over n
+ * elements, rounded to dtype after each torch op of the reference activation
+ * (exact fp32 for SWH_F32); the backward is the analytic derivative in fp32. */
+int swh_gelu_tanh_fwd(const void *x, int64_t n, void *y, int32_t dtype, void *stream);
+int swh_gelu_tanh_bwd(const void *x, const void *dy, int64_t n, void *dx, int32_t dtype, void *stream);
 
 #ifdef __cplusplus
 }

@@ -37,6 +37,30 @@ def hf_qwen2_from_config(cfg: dict, seed: int = 0, dtype=torch.float32):
     return m
 
 
+def hf_gpt2_from_config(cfg: dict, seed: int = 0, dtype=torch.float32):
+    """Random-init transformers GPT2LMHeadModel (BASELINE.json config 1), dropout
+    off (`disable_dropout=True` in GRPOConfig terms: the engine has none)."""
+    from transformers import GPT2Config, GPT2LMHeadModel
+    torch.manual_seed(seed)
+    H = cfg["hidden_size"]
+    hc = GPT2Config(vocab_size=cfg["vocab_size"], n_embd=H, n_layer=cfg["num_hidden_layers"],
+                    n_head=cfg["num_attention_heads"], n_positions=cfg["max_position_embeddings"],
+                    n_inner=None if cfg["intermediate_size"] == 4 * H else cfg["intermediate_size"],
+                    layer_norm_epsilon=cfg["rms_norm_eps"], resid_pdrop=0.0, embd_pdrop=0.0, attn_pdrop=0.0,
+                    bos_token_id=None, eos_token_id=None)
+    hc._attn_implementation = "sdpa"
+    m = GPT2LMHeadModel(hc).to(dtype)
+    m.eval()
+    return m
+
+
+def hf_from_config(cfg: dict, seed: int = 0, dtype=torch.float32):
+    """The transformers model of cfg["model_type"] (GPT-2, or Qwen2 / Llama-style)."""
+    if cfg.get("model_type") == "gpt2":
+        return hf_gpt2_from_config(cfg, seed, dtype)
+    return hf_qwen2_from_config(cfg, seed, dtype)
+
+
 def generate(model, prompt_ids, prompt_mask, C: int, *, do_sample=True, temperature=1.0, top_p=1.0, top_k=None,
              min_p=None, repetition_penalty=1.0, min_new_tokens=0, pad_token_id=0, eos_token_id=None):
     """transformers generate with the GenerationConfig of grpo_trainer.py:995-1014."""

@@ -17,6 +17,8 @@ for step in "$@"; do
     gpuall) run gpuall 1100 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread ;;
     new2) run new2 900 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -k "rewards or checkpoint or dp_ or step_parity" ;;
     newp) run newp 600 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -s -k "selective_log_softmax or greedy_matches" ;;
+    g2) run g2 600 python -u -m pytest tests/test_gpt2_gpu.py -v -m gpu --timeout 200 --timeout-method thread ;;
+    cfg1) run cfg1 300 python tools/bench_cfg1.py ;;
     newt) run newt 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread -k "step_parity or adamw or bench_launches or masked_whiten" ;;
     tune) SWH_GEMM_TUNING=tune SWH_GEMM_TABLE=gpurun_out/gemm_tuned.csv run tune 900 python bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
     benchtuned) SWH_GEMM_TABLE=gpurun_out/gemm_tuned.csv run benchtuned 600 python bench.py --steps 3 --warmup 2 --no-cpu-baseline ;;

@@ -76,6 +76,12 @@ SIGNATURES = {
     "swh_rmsnorm_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp]),
     "swh_rmsnorm_dw_accum": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_vp]),
     "swh_colsum_partials": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp]),
+    "swh_layernorm_fwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp]),
+    "swh_layernorm_bwd_partial_rows": (c_i64, [c_i64, c_i64]),
+    "swh_layernorm_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i32,
+                                  c_vp]),
+    "swh_gelu_tanh_fwd": (c_i32, [c_vp, c_i64, c_vp, c_i32, c_vp]),
+    "swh_gelu_tanh_bwd": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i32, c_vp]),
     "swh_silu_mul_fwd": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_vp]),
     "swh_silu_mul_bwd": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i32, c_vp]),
     "swh_attn_fwd": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -1,5 +1,5 @@
-"""Decoder configuration for the Llama-style families the benchmarks name
-(Qwen2.5-0.5B: BASELINE.json configs 2-4; Llama-3-8B: config 5)."""
+"""Decoder configuration for the families the benchmarks name (Qwen2.5-0.5B:
+BASELINE.json configs 2-4; Llama-3-8B: config 5; tiny GPT-2: config 1)."""
 from __future__ import annotations
 
 import dataclasses
@@ -72,7 +72,7 @@ def tiny_llama(vocab_size: int = 2048, layers: int = 2) -> DecoderConfig:
                          max_position_embeddings=4096, model_type="llama")
 
 
-SUPPORTED_MODEL_TYPES = ("qwen2", "llama")
+SUPPORTED_MODEL_TYPES = ("qwen2", "llama", "gpt2")
 
 
 def from_hf_config(cfg) -> DecoderConfig:
@@ -88,7 +88,20 @@ def from_hf_config(cfg) -> DecoderConfig:
     if mt not in SUPPORTED_MODEL_TYPES:
         raise ValueError(f"model_type {mt!r} is not supported by the MI355X engine (supported: "
                          f"{', '.join(SUPPORTED_MODEL_TYPES)}: Llama-style decoders with RMSNorm, RoPE and a SiLU "
-                         "gated MLP)")
+                         "gated MLP, and GPT-2)")
+    if mt == "gpt2":  # transformers GPT2Config (BASELINE.json config 1)
+        act = g("activation_function", "gelu_new")
+        if act not in ("gelu_new", "gelu_pytorch_tanh"):
+            raise ValueError(f"GPT-2 activation {act!r} is not supported (gelu_new only)")
+        if g("scale_attn_by_inverse_layer_idx", False) or g("reorder_and_upcast_attn", False) or \
+                not g("scale_attn_weights", True):
+            raise ValueError("GPT-2 attention variants other than the default head_dim^-0.5 scaling are not supported")
+        H, nh = g("n_embd"), g("n_head")
+        return DecoderConfig(vocab_size=g("vocab_size"), hidden_size=H, intermediate_size=g("n_inner") or 4 * H,
+                             num_hidden_layers=g("n_layer"), num_attention_heads=nh, num_key_value_heads=nh,
+                             head_dim=H // nh, rope_theta=0.0, rms_norm_eps=float(g("layer_norm_epsilon", 1e-5)),
+                             tie_word_embeddings=bool(g("tie_word_embeddings", True)), attention_bias=True,
+                             max_position_embeddings=int(g("n_positions", 1024)), model_type="gpt2")
     rp = g("rope_parameters") or g("rope_scaling") or {}
     rtype = rp.get("rope_type", rp.get("type", "default")) if isinstance(rp, dict) else "default"
     if rtype not in ("default", None):

@@ -430,22 +430,7 @@ class CausalLM:
             self.layout[name] = (off, tuple(shape))
             off += (n + _ALIGN - 1) // _ALIGN * _ALIGN
 
-        H, I, V = cfg.hidden_size, cfg.intermediate_size, cfg.vocab_size
-        add("embed", V, H)
-        for i in range(cfg.num_hidden_layers):
-            add(f"l{i}.ln_in", H)
-            add(f"l{i}.qkv_w", cfg.qkv_dim, H)
-            if cfg.attention_bias:
-                add(f"l{i}.qkv_b", cfg.qkv_dim)
-            add(f"l{i}.o_w", H, cfg.q_dim)
-            add(f"l{i}.ln_post", H)
-            add(f"l{i}.gu_w", 2 * I, H)
-            add(f"l{i}.down_w", H, I)
-        add("norm", H)
-        if head == "score":
-            add("score", 1, H)
-        elif not cfg.tie_word_embeddings:
-            add("lm_head", V, H)
+        self._build_layout(add)
         self.numel = off
         self.flat = torch.zeros(off, device=self.device, dtype=dtype)
         self.p = {k: self.flat[o:o + math.prod(s)].view(s) for k, (o, s) in self.layout.items()}
@@ -465,7 +450,30 @@ class CausalLM:
         # reference-precision mode) runs SDPA
         if dtype not in (torch.bfloat16, torch.float32):
             raise ValueError(f"CausalLM dtype {dtype}: bf16 (the product path) or float32 (reference precision)")
-        self._hip_attn = (nn_ops.attention_supported(cfg.head_dim) and dtype == torch.bfloat16
+        self._check_attention()
+
+    def _build_layout(self, add):
+        """Weights in flat-buffer order: add(name, *shape) per tensor."""
+        cfg = self.cfg
+        H, I, V = cfg.hidden_size, cfg.intermediate_size, cfg.vocab_size
+        add("embed", V, H)
+        for i in range(cfg.num_hidden_layers):
+            add(f"l{i}.ln_in", H)
+            add(f"l{i}.qkv_w", cfg.qkv_dim, H)
+            if cfg.attention_bias:
+                add(f"l{i}.qkv_b", cfg.qkv_dim)
+            add(f"l{i}.o_w", H, cfg.q_dim)
+            add(f"l{i}.ln_post", H)
+            add(f"l{i}.gu_w", 2 * I, H)
+            add(f"l{i}.down_w", H, I)
+        add("norm", H)
+        if self.head == "score":
+            add("score", 1, H)
+        elif not cfg.tie_word_embeddings:
+            add("lm_head", V, H)
+
+    def _check_attention(self):
+        self._hip_attn = (nn_ops.attention_supported(self.cfg.head_dim) and self.dtype == torch.bfloat16
                           and os.environ.get("SWH_ATTN", "hip") != "torch")
 
     def layer_range(self, i: int) -> tuple[int, int]:

@@ -42,8 +42,22 @@ SHARD_BYTES = 5 << 30  # transformers' default max_shard_size ("5GB")
 
 def hf_config_dict(cfg: DecoderConfig, head: str = "lm", dtype: torch.dtype = torch.bfloat16,
                    eos_token_id=None, pad_token_id=None) -> dict:
-    """transformers config.json for a Qwen2 / Llama decoder (or its
+    """transformers config.json for a Qwen2 / Llama / GPT-2 model (or its
     *ForSequenceClassification with one label for head="score")."""
+    tdt = "float32" if dtype == torch.float32 else "bfloat16"
+    if cfg.model_type == "gpt2":
+        H = cfg.hidden_size
+        d = {"architectures": ["GPT2LMHeadModel" if head == "lm" else "GPT2ForSequenceClassification"],
+             "model_type": "gpt2", "vocab_size": cfg.vocab_size, "n_embd": H, "n_layer": cfg.num_hidden_layers,
+             "n_head": cfg.num_attention_heads, "n_positions": cfg.max_position_embeddings,
+             "n_inner": None if cfg.intermediate_size == 4 * H else cfg.intermediate_size,
+             "layer_norm_epsilon": cfg.rms_norm_eps, "activation_function": "gelu_new", "resid_pdrop": 0.0,
+             "embd_pdrop": 0.0, "attn_pdrop": 0.0, "scale_attn_weights": True, "tie_word_embeddings": True,
+             "initializer_range": 0.02, "use_cache": True, "torch_dtype": tdt, "eos_token_id": eos_token_id,
+             "pad_token_id": pad_token_id, "bos_token_id": None}
+        if head == "score":
+            d.update(num_labels=1, id2label={"0": "LABEL_0"}, label2id={"LABEL_0": 0})
+        return d
     fam = "Qwen2" if cfg.model_type == "qwen2" else "Llama"
     arch = f"{fam}ForCausalLM" if head == "lm" else f"{fam}ForSequenceClassification"
     d = {
@@ -54,7 +68,7 @@ def hf_config_dict(cfg: DecoderConfig, head: str = "lm", dtype: torch.dtype = to
         "max_position_embeddings": cfg.max_position_embeddings, "rms_norm_eps": cfg.rms_norm_eps,
         "rope_theta": cfg.rope_theta, "rope_parameters": {"rope_theta": cfg.rope_theta, "rope_type": "default"},
         "tie_word_embeddings": cfg.tie_word_embeddings, "attention_dropout": 0.0, "initializer_range": 0.02,
-        "use_cache": True, "torch_dtype": "float32" if dtype == torch.float32 else "bfloat16",
+        "use_cache": True, "torch_dtype": tdt,
         "eos_token_id": eos_token_id, "pad_token_id": pad_token_id, "bos_token_id": None,
     }
     if cfg.model_type == "llama":
@@ -111,6 +125,17 @@ def hf_param_order(model: CausalLM) -> list[str]:
     """model.named_parameters() order of the transformers module (tied lm_head
     is the embedding parameter and appears once)."""
     c = model.cfg
+    if c.model_type == "gpt2":
+        names = ["transformer.wte.weight", "transformer.wpe.weight"]
+        for i in range(c.num_hidden_layers):
+            pre = f"transformer.h.{i}."
+            names += [pre + n for n in ("ln_1.weight", "ln_1.bias", "attn.c_attn.weight", "attn.c_attn.bias",
+                                        "attn.c_proj.weight", "attn.c_proj.bias", "ln_2.weight", "ln_2.bias",
+                                        "mlp.c_fc.weight", "mlp.c_fc.bias", "mlp.c_proj.weight", "mlp.c_proj.bias")]
+        names += ["transformer.ln_f.weight", "transformer.ln_f.bias"]
+        if model.head == "score":
+            names.append("score.weight")
+        return names
     names = ["model.embed_tokens.weight"]
     for i in range(c.num_hidden_layers):
         pre = f"model.layers.{i}."
@@ -129,8 +154,9 @@ def hf_param_order(model: CausalLM) -> list[str]:
 
 
 def _no_decay_name(n: str) -> bool:
-    """transformers Trainer.get_decay_parameter_names: biases and norm weights."""
-    return n.endswith(".bias") or "norm" in n
+    """transformers Trainer.get_decay_parameter_names: biases and norm weights
+    (GPT-2's LayerNorms are ln_1 / ln_2 / ln_f)."""
+    return n.endswith(".bias") or "norm" in n or ".ln_" in n
 
 
 def _flat_views(model: CausalLM, flat: torch.Tensor) -> dict:

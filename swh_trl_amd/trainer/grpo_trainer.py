@@ -30,6 +30,8 @@ from .. import dist as swh_dist
 from .. import gemm_tuning
 from .. import ops
 from ..engine.config import DecoderConfig, PRESETS, from_hf_config
+from ..engine import build_engine, build_model
+from ..engine.gpt2 import warn_dropout
 from ..engine.decode import DecodeEngine
 from ..engine.model import CausalLM, dw_streams, dw_sync
 from ..optim import FlatAdamW, sync_ref_model
@@ -88,17 +90,17 @@ def load_model(model, device, trainable=True, seed=0, head: str = "lm", dtype=to
             raise ValueError(f"expected a model with a {head!r} head, got {model.head!r}")
         return model
     if isinstance(model, DecoderConfig):
-        return CausalLM(model, device, head=head, seed=seed, trainable=trainable, dtype=dtype)
+        return build_model(model, device, head=head, seed=seed, trainable=trainable, dtype=dtype)
     if isinstance(model, str):
         if model in PRESETS:
-            return CausalLM(PRESETS[model](), device, head=head, seed=seed, trainable=trainable, dtype=dtype)
+            return build_model(PRESETS[model](), device, head=head, seed=seed, trainable=trainable, dtype=dtype)
         if os.path.isdir(model):
             import json
 
             from safetensors.torch import load_file
             with open(os.path.join(model, "config.json")) as f:
                 cfg = from_hf_config(json.load(f))
-            m = CausalLM(cfg, device, head=head, seed=None, trainable=trainable, dtype=dtype)
+            m = build_model(cfg, device, head=head, seed=None, trainable=trainable, dtype=dtype)
             sd = {}
             for fn in sorted(os.listdir(model)):
                 if fn.endswith(".safetensors"):
@@ -109,7 +111,9 @@ def load_model(model, device, trainable=True, seed=0, head: str = "lm", dtype=to
                          "model object")
     if hasattr(model, "config") and hasattr(model, "state_dict"):
         cfg = from_hf_config(model.config)
-        m = CausalLM(cfg, device, head=head, seed=None, trainable=trainable, dtype=dtype)
+        if cfg.model_type == "gpt2":
+            warn_dropout(model.config)
+        m = build_model(cfg, device, head=head, seed=None, trainable=trainable, dtype=dtype)
         m.load_hf_state_dict({k: v.to(device) for k, v in model.state_dict().items()})
         return m
     raise TypeError(f"unsupported model type {type(model)}")
@@ -179,7 +183,8 @@ class GRPOTrainer:
                                min_new_tokens=int(gk.get("min_new_tokens", 0) or 0))
         self.ref_model = None
         if self.beta != 0.0:
-            self.ref_model = CausalLM(self.model.cfg, self.device, seed=None, trainable=False, dtype=self.model.dtype)
+            self.ref_model = build_model(self.model.cfg, self.device, seed=None, trainable=False,
+                                         dtype=self.model.dtype)
             self.ref_model.copy_from(self.model)
         self.optimizer = FlatAdamW(self.model.numel, self.device, lr=a.learning_rate,
                                    betas=(a.adam_beta1, a.adam_beta2), eps=a.adam_epsilon,
@@ -246,10 +251,11 @@ class GRPOTrainer:
         """The bf16 weights the decode engine reads: the policy itself, or for an
         fp32 policy a bf16 copy refreshed now (one cast of the flat buffer)."""
         m = self.model
-        if m.dtype == torch.bfloat16:
+        if m.dtype == torch.bfloat16 or m.cfg.model_type == "gpt2":  # the GPT-2 step runs in the model dtype
             return m
         if self._rollout_model is None:
-            self._rollout_model = CausalLM(m.cfg, self.device, seed=None, trainable=False, dtype=torch.bfloat16)
+            self._rollout_model = build_model(m.cfg, self.device, seed=None, trainable=False,
+                                              dtype=torch.bfloat16)
         self._rollout_model.flat.copy_(m.flat)
         return self._rollout_model
 
@@ -259,7 +265,7 @@ class GRPOTrainer:
         e = self._engine
         if e is None or e.B != B or e.Pmax < P or e.model is not gm:
             Pmax = max(P, self.max_prompt_length or P) if (self.max_prompt_length or 0) <= 4096 else P
-            self._engine = DecodeEngine(gm, B, Pmax, C)
+            self._engine = build_engine(gm, B, Pmax, C)
         return self._engine
 
     # ------------------------------------------------------------------ rollout + scoring

@@ -33,6 +33,7 @@ import torch
 from .. import dist as swh_dist
 from .. import gemm_tuning
 from .. import ops
+from ..engine import build_engine, build_model
 from ..engine.decode import DecodeEngine
 from ..engine.model import CausalLM, dw_sync
 from ..optim import FlatAdamW
@@ -144,7 +145,8 @@ class PPOTrainer:
         if ref_model is not None:
             self.ref_model = load_model(ref_model, self.device, trainable=False, seed=args.seed)
         else:  # create_reference_model (modeling_base.py:592-664): a frozen deep copy
-            self.ref_model = CausalLM(self.policy_model.cfg, self.device, seed=None, trainable=False)
+            self.ref_model = build_model(self.policy_model.cfg, self.device, seed=None, trainable=False,
+                                         dtype=self.policy_model.dtype)
             self.ref_model.copy_from(self.policy_model)
         self.value_model = load_model(value_model, self.device, trainable=True, seed=args.seed + 1, head="score")
         self.reward_model = load_model(reward_model, self.device, trainable=False, seed=args.seed + 2, head="score")
@@ -193,7 +195,7 @@ class PPOTrainer:
         e = self._engine
         C = self.args.response_length
         if e is None or e.B != B or e.Pmax < P:
-            self._engine = DecodeEngine(self.policy_model, B, P, C)
+            self._engine = build_engine(self.policy_model, B, P, C)
         return self._engine
 
     # ------------------------------------------------------------------ rollout (ppo_trainer.py:362-535)

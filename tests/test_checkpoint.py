@@ -99,3 +99,31 @@ def test_checkpoint_rotation(tmp_path):
     assert ck.latest_checkpoint(str(tmp_path)).endswith("checkpoint-10")
     ck.rotate_checkpoints(str(tmp_path), 2)
     assert sorted(os.listdir(tmp_path)) == ["checkpoint-10", "checkpoint-3"]
+
+
+def test_gpt2_checkpoint_round_trip_and_param_order(tmp_path):
+    """BASELINE.json config 1 family: the GPT-2 layout saves as a transformers
+    GPT2LMHeadModel (Conv1D weights transposed back), loads back bit-equal,
+    its parameter order is GPT2LMHeadModel.named_parameters(), and the
+    Trainer's no-decay set (biases + LayerNorms) matches."""
+    from transformers import AutoModelForCausalLM, GPT2LMHeadModel
+    from swh_trl_amd.engine import GPT2LM, gpt2_config
+    from swh_trl_amd.engine.config import from_hf_config
+    from swh_trl_amd.trainer.grpo_trainer import load_model
+    m = GPT2LM(gpt2_config(), "cpu", seed=2, dtype=torch.float32, trainable=False)
+    ck.save_pretrained(m, str(tmp_path), eos_token_id=1, pad_token_id=0)
+    hf = AutoModelForCausalLM.from_pretrained(str(tmp_path), dtype=torch.float32)
+    assert isinstance(hf, GPT2LMHeadModel) and from_hf_config(hf.config) == m.cfg
+    ref = hf.state_dict()
+    for k, v in m.hf_state_dict().items():
+        assert torch.equal(ref[k], v), k
+    assert ck.hf_param_order(m) == [n for n, _ in hf.named_parameters()]
+    m2 = load_model(str(tmp_path), "cpu", trainable=False, dtype=torch.float32)
+    assert isinstance(m2, GPT2LM) and torch.equal(m2.flat, m.flat)
+    # no-decay ranges cover exactly the bias / LayerNorm parameters
+    nd = set()
+    for s, e in m.no_decay_ranges():
+        nd.update(range(s, e))
+    for name, (o, shape) in m.layout.items():
+        want = name.endswith("_b") or "ln_" in name
+        assert (o in nd) == want, name

@@ -1,0 +1,264 @@
+"""GPT-2 family (BASELINE.json config 1, the reference's tiny-random-GPT2
+plumbing config) on the GPU (-m gpu).
+
+Oracles: torch's LayerNorm / transformers NewGELUActivation for the kernels,
+transformers GPT2LMHeadModel (third-party modeling code the reference runs)
+for forward / gradients / greedy generation, and the CPU GRPO step
+restatement (oracle/grpo_step.py) for one whole GRPOTrainer step at config
+1's shape: GPT2Config(vocab 1024, n_positions 64, n_embd 32, n_layer 2,
+n_head 2), 4 prompts x G 2 x 16 tokens, fp32.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+EOS, PAD = 1, 0
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available()
+    return torch.device("cuda:0")
+
+
+def _gen(seed):
+    return torch.Generator().manual_seed(seed)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("H", [32, 768, 1000])
+def test_layernorm_residual_fwd_bwd(dev, dtype, H):
+    from swh_trl_amd.engine.gpt2 import _AddLayerNorm
+    g = _gen(H)
+    rows = 37
+    x = torch.randn(rows, H, generator=g).to(dtype).to(dev).requires_grad_(True)
+    r = torch.randn(rows, H, generator=g).to(dtype).to(dev).requires_grad_(True)
+    w = (1 + 0.1 * torch.randn(H, generator=g)).to(dtype).to(dev)
+    b = (0.1 * torch.randn(H, generator=g)).to(dtype).to(dev)
+    gw, gb = torch.zeros_like(w), torch.zeros_like(b)
+    s, h = _AddLayerNorm.apply(x, r, w, b, gw, gb, 1e-5)
+    cs, ch = torch.randn(rows, H, generator=g).to(dev), torch.randn(rows, H, generator=g).to(dev)
+    ((s.float() * cs).sum() + (h.float() * ch).sum()).backward()
+    torch.cuda.synchronize()
+    # reference: torch ops (fp32 math) with the same rounding of s
+    xr, rr = x.detach().float().requires_grad_(True), r.detach().float().requires_grad_(True)
+    wr, br = w.float().requires_grad_(True), b.float().requires_grad_(True)
+    sr = (xr + rr)
+    sq = sr.to(dtype).float() if dtype != torch.float32 else sr
+    hr = torch.nn.functional.layer_norm(sq, (H,), wr, br, 1e-5)
+    ((sr * cs).sum() + (hr * ch).sum()).backward()
+    tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(s.float(), sq.detach(), **tol)
+    torch.testing.assert_close(h.float(), hr.detach(), **tol)
+    torch.testing.assert_close(x.grad.float(), xr.grad, **(tol if dtype == torch.float32 else dict(rtol=3e-2, atol=5e-2)))
+    torch.testing.assert_close(r.grad, x.grad)
+    tolw = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=0.3)
+    torch.testing.assert_close(gw.float(), wr.grad, **tolw)
+    torch.testing.assert_close(gb.float(), br.grad, **tolw)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gelu_new_fwd_bwd(dev, dtype):
+    from transformers.activations import NewGELUActivation
+    from swh_trl_amd.engine.gpt2 import GeluNewFn
+    g = _gen(3)
+    x = (torch.randn(4099, generator=g) * 3).to(dtype).to(dev).requires_grad_(True)
+    y = GeluNewFn.apply(x)
+    dy = torch.randn(4099, generator=g).to(dtype).to(dev)
+    y.backward(dy)
+    xr = x.detach().clone().requires_grad_(True)
+    yr = NewGELUActivation()(xr)
+    yr.backward(dy)
+    if dtype == torch.float32:
+        torch.testing.assert_close(y, yr, rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(x.grad, xr.grad, rtol=1e-5, atol=1e-5)
+    else:  # one bf16 rounding per torch op, as NewGELUActivation: the same bits
+        assert torch.equal(y, yr), (y != yr).sum().item()
+        torch.testing.assert_close(x.grad.float(), xr.grad.float(), rtol=3e-2, atol=3e-2)
+
+
+def _pair(dev, dtype=torch.float32, seed=0, **kw):
+    from oracle.grpo_step import hf_gpt2_from_config
+    from swh_trl_amd.engine import GPT2LM, gpt2_config
+    cfg = gpt2_config(**kw)
+    hf = hf_gpt2_from_config(cfg.to_dict(), seed=seed).to(dev)
+    m = GPT2LM(cfg, dev, seed=None, dtype=dtype)
+    m.load_hf_state_dict({k: v.detach() for k, v in hf.state_dict().items()})
+    return m, hf
+
+
+def test_gpt2_forward_and_grads_match_transformers(dev):
+    from swh_trl_amd import ops
+    m, hf = _pair(dev, n_embd=64, n_head=4, n_layer=2, vocab_size=1024, n_positions=64)
+    g = _gen(1)
+    B, L, P = 3, 24, 8
+    ids = torch.randint(0, 1024, (B, L), generator=g).to(dev)
+    mask = torch.ones(B, L, dtype=torch.int64, device=dev)
+    mask[1, :5] = 0
+    w = torch.randn(B, L - P, generator=g).to(dev)
+    m.zero_grad()
+    h = m.hidden_states(ids, key_mask=mask)
+    lp, _ = m.logp_entropy(h[:, P - 1:-1], ids[:, P:], 0.9, False)
+    (lp * w).sum().backward()
+    torch.cuda.synchronize()
+    out = hf(input_ids=ids, attention_mask=mask).logits
+    lpr = torch.log_softmax(out[:, P - 1:-1].float() / 0.9, -1).gather(-1, ids[:, P:, None]).squeeze(-1)
+    (lpr * w).sum().backward()
+    keep = mask[:, P:].bool()
+    torch.testing.assert_close(lp[keep], lpr.detach()[keep], rtol=1e-4, atol=1e-4)
+    # hidden states of the valid positions
+    with torch.no_grad():
+        ref_h = hf.transformer(input_ids=ids, attention_mask=mask).last_hidden_state
+    torch.testing.assert_close(h.detach()[mask.bool()], ref_h[mask.bool()], rtol=1e-4, atol=1e-4)
+    saved = m.flat.clone()
+    m.flat.copy_(m.grad)
+    gm = {k: v.detach().float().clone() for k, v in m.hf_state_dict().items()}
+    m.flat.copy_(saved)
+    for k, p in hf.named_parameters():
+        if p.grad is None:
+            continue
+        rel = ((gm[k] - p.grad).norm() / p.grad.norm().clamp_min(1e-20)).item()
+        assert rel <= 1e-4, (k, rel)
+
+
+def test_gpt2_greedy_matches_transformers_generate(dev):
+    """fp32: greedy ids equal transformers generate exactly (left padding too)."""
+    from swh_trl_amd.engine import build_engine
+    m, hf = _pair(dev, seed=2)
+    g = _gen(2)
+    B, P, C = 4, 8, 16
+    ids = torch.randint(2, 1024, (B, P), generator=g).to(dev)
+    mask = torch.ones(B, P, dtype=torch.int64, device=dev)
+    mask[3, :3] = 0
+    ids[3, :3] = PAD
+    eng = build_engine(m, B, P, C)
+    mine, _ = eng.generate(ids, mask, C, greedy=True, pad_token_id=PAD)
+    with torch.no_grad():
+        ref = hf.generate(input_ids=ids, attention_mask=mask, max_new_tokens=C, do_sample=False, pad_token_id=PAD,
+                          eos_token_id=None)[:, P:]
+    assert torch.equal(mine, ref), (mine, ref)
+    # graph replay == eager steps
+    eng2 = build_engine(m, B, P, C, use_graph=False)
+    mine2, _ = eng2.generate(ids, mask, C, greedy=True, pad_token_id=PAD)
+    assert torch.equal(mine, mine2)
+
+
+def test_gpt2_sampled_rollout_reproducible(dev):
+    from swh_trl_amd.engine import build_engine
+    m, _ = _pair(dev, seed=4)
+    B, P, C = 8, 8, 16
+    ids = torch.randint(2, 1024, (B, P), generator=_gen(4)).to(dev)
+    mask = torch.ones(B, P, dtype=torch.int64, device=dev)
+    eng = build_engine(m, B, P, C)
+    a, lpa = eng.generate(ids, mask, C, seed=3, eos_token_id=EOS, pad_token_id=PAD, min_new_tokens=C,
+                          return_logp=True, temperature=0.9)
+    b, lpb = eng.generate(ids, mask, C, seed=3, eos_token_id=EOS, pad_token_id=PAD, min_new_tokens=C,
+                          return_logp=True, temperature=0.9)
+    assert torch.equal(a, b) and torch.equal(lpa, lpb)
+    assert not (a == EOS).any() and (lpa <= 0).all()
+
+
+def _reward_oracle(cids, cmask):
+    return [float(len(set(r[m.bool()].tolist())) % 5) for r, m in zip(cids, cmask)]
+
+
+def _reward_product(prompts=None, completions=None, completion_ids=None, **kw):
+    return [float(len(set(c)) % 5) for c in completion_ids]
+
+
+def test_cfg1_grpo_step_matches_oracle(dev):
+    """One GRPOTrainer step at config 1 (tiny GPT-2, 4 prompts x 2 generations
+    x 16 tokens, fp32) against the CPU restatement of the reference step on
+    the same weights / completions / shuffle: masks, advantages, log-probs and
+    the loss to 1e-5, gradients to 1e-4 relative."""
+    from oracle import grpo_step as og
+    from swh_trl_amd.engine import GPT2LM, gpt2_config
+    from swh_trl_amd.trainer import GRPOConfig, GRPOTrainer
+    cfg = gpt2_config()
+    G, P, C, MB, GA = 2, 8, 16, 8, 1
+    g = _gen(11)
+    ds = [{"prompt": None, "prompt_ids": torch.randint(2, cfg.vocab_size, (P,), generator=g).tolist()}
+          for _ in range(4)]
+    args = GRPOConfig(per_device_train_batch_size=MB, gradient_accumulation_steps=GA, num_generations=G,
+                      max_prompt_length=P, max_completion_length=C, learning_rate=1e-3, max_steps=1,
+                      lr_scheduler_type="constant", seed=5, shuffle_dataset=False,
+                      model_init_kwargs={"torch_dtype": "float32"},
+                      generation_kwargs={"eos_token_id": EOS, "pad_token_id": PAD})
+    model = GPT2LM(cfg, dev, seed=3, dtype=torch.float32)
+    tr = GRPOTrainer(model=model, reward_funcs=_reward_product, args=args, train_dataset=ds)
+    w0 = {k: v.detach().float().cpu().clone() for k, v in tr.model.hf_state_dict().items()}
+    captured = {}
+    gen_fn = tr._generate_and_score_completions
+
+    def gen_capture(examples):
+        out = gen_fn(examples)
+        captured["gen"] = {k: v.detach().clone() for k, v in out.items()}
+        captured["shuffle_state"] = tr._shuffle_gen.get_state()
+        return out
+
+    lp_fn = tr._completion_logps
+
+    def lp_capture(model_, batch, compute_entropy):
+        lp, ent = lp_fn(model_, batch, compute_entropy)
+        if compute_entropy:
+            captured["logps"] = lp.detach().float().cpu().clone()
+        return lp, ent
+
+    tr._generate_and_score_completions = gen_capture
+    tr._completion_logps = lp_capture
+    out = tr.training_step_group()
+    torch.cuda.synchronize()
+    loss = float(out["loss"])
+    saved = tr.model.flat.clone()
+    tr.model.flat.copy_(tr.model.grad)
+    grads = {k: v.detach().float().cpu().clone() for k, v in tr.model.hf_state_dict().items()}
+    tr.model.flat.copy_(saved)
+    gen = {k: v.cpu() for k, v in captured["gen"].items()}
+    n = gen["completion_ids"].shape[0]
+    perm = torch.randperm(n, generator=torch.Generator().set_state(captured["shuffle_state"]))
+    hf = og.hf_gpt2_from_config(cfg.to_dict())
+    hf.load_state_dict(w0, strict=False)
+    opt = torch.optim.AdamW(hf.parameters(), lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, foreach=False)
+    oloss, inter = og.grpo_step(hf, opt, gen["prompt_ids"], gen["prompt_mask"].long(), _reward_oracle,
+                                num_generations=G, C=C, per_device_train_batch_size=MB,
+                                gradient_accumulation_steps=GA, eos_token_id=EOS, pad_token_id=PAD,
+                                completion_ids=gen["completion_ids"], perm=perm, capture=True)
+    assert torch.equal(inter["completion_mask"].int(), gen["completion_mask"].int())
+    torch.testing.assert_close(gen["advantages"].float(), inter["advantages"].float(), rtol=0, atol=1e-6)
+    m = gen["completion_mask"][perm].bool()
+    d_lp = (captured["logps"] - inter["logps"].float()).abs()[m]
+    assert d_lp.max().item() <= 1e-5, d_lp.max().item()
+    assert abs(loss - oloss) <= 1e-5 * max(1.0, abs(oloss)), (loss, oloss)
+    for k, gr in inter["grads"].items():
+        rel = ((grads[k] - gr).norm() / gr.norm().clamp_min(1e-20)).item()
+        assert rel <= 1e-4, (k, rel)
+
+
+def test_cfg1_trainer_runs_saves_and_reloads(dev, tmp_path):
+    """config 1 through GRPOTrainer.train() from a transformers GPT2LMHeadModel:
+    two steps, then save_model loads back in transformers with equal logits."""
+    from transformers import GPT2LMHeadModel
+    from oracle.grpo_step import hf_gpt2_from_config
+    from swh_trl_amd.engine import gpt2_config
+    from swh_trl_amd.trainer import GRPOConfig, GRPOTrainer
+    hf = hf_gpt2_from_config(gpt2_config().to_dict(), seed=7)
+    ds = [{"prompt": None, "prompt_ids": list(range(3 + i, 11 + i))} for i in range(8)]
+    args = GRPOConfig(output_dir=str(tmp_path), per_device_train_batch_size=8, num_generations=2,
+                      max_prompt_length=8, max_completion_length=16, max_steps=2, learning_rate=1e-3,
+                      model_init_kwargs={"torch_dtype": "float32"}, save_strategy="no",
+                      generation_kwargs={"eos_token_id": EOS, "pad_token_id": PAD})
+    tr = GRPOTrainer(model=hf, reward_funcs=_reward_product, args=args, train_dataset=ds)
+    before = tr.model.flat.clone()
+    state = tr.train()
+    assert state.global_step == 2 and not torch.equal(before, tr.model.flat)
+    assert math.isfinite(state.log_history[-1]["loss"])
+    tr.save_model(str(tmp_path / "final"))
+    back = GPT2LMHeadModel.from_pretrained(str(tmp_path / "final"), torch_dtype=torch.float32).to(dev).eval()
+    ids = torch.randint(0, 1024, (2, 20), generator=_gen(0)).to(dev)
+    with torch.no_grad():
+        ref = back(input_ids=ids).logits
+        mine = tr.model.logits(tr.model.hidden_states(ids))
+    torch.testing.assert_close(mine, ref, rtol=1e-4, atol=1e-4)
