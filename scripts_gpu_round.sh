@@ -19,6 +19,7 @@ for step in "$@"; do
     newp) run newp 600 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -s -k "selective_log_softmax or greedy_matches" ;;
     g2) run g2 600 python -u -m pytest tests/test_gpt2_gpu.py -v -m gpu --timeout 200 --timeout-method thread ;;
     cfg1) run cfg1 300 python tools/bench_cfg1.py ;;
+    wide) run wide 600 python -u -m pytest tests -v -m gpu --timeout 200 --timeout-method thread -k "wide_gemm or llama" ;;
     newt) run newt 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread -k "step_parity or adamw or bench_launches or masked_whiten" ;;
     tune) SWH_GEMM_TUNING=tune SWH_GEMM_TABLE=gpurun_out/gemm_tuned.csv run tune 900 python bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
     benchtuned) SWH_GEMM_TABLE=gpurun_out/gemm_tuned.csv run benchtuned 600 python bench.py --steps 3 --warmup 2 --no-cpu-baseline ;;
@@ -54,6 +55,7 @@ for step in "$@"; do
     hangs) AMD_SERIALIZE_KERNEL=3 run hangs 100 python tools/phase_probe.py --layers 1 --B 8 --L 1280 ;;
     hangt) SWH_DW_STREAM=0 SWH_ATTN_SPLIT=0 run hangt1 100 python tools/phase_probe.py --layers 2 --B 8 --L 1280 && SWH_GEMM_TUNING=off run hangt2 100 python tools/phase_probe.py --layers 2 --B 8 --L 1280 ;;
     hangf) run hangf 100 python tools/phase_probe.py --layers 2 --B 8 --L 1280 --reps 3 ;;
+    l8w4) SWH_WIDE_SMAX=4 SWH_TRACE=1 run l8w4 1000 python tools/bench_llama8b.py --prompts 8 --P 256 --C 1024 --steps 1 --warmup 1 --fuse-budget 16384 ;;
     l8) SWH_TRACE=1 run l8 1000 python tools/bench_llama8b.py --prompts 8 --P 256 --C 1024 --steps 1 --warmup 1 --fuse-budget 16384 ;;
     l8k) run l8k 600 python -u -m pytest tests/test_kernels_gpu.py -v -m gpu -k "llama3_8b" --timeout 200 --timeout-method thread ;;
     tk) run tk 600 python tools/train_kernels.py ;;

@@ -28,6 +28,12 @@
 #include "common.hpp"
 
 namespace swh {
+// csrc/wide_gemm.hip: 1 = shape not eligible, else a SWH status
+int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, float eps, const float *ss_in,
+              const void *bias, void *residual, int32_t silu, void *y, int64_t ldy, float *ss_out, void *workspace,
+              int64_t workspace_bytes, int64_t counter_bytes, hipStream_t stream);
+int64_t wide_gemm_slab_bytes(int64_t M, int64_t N, int64_t K, int32_t silu);
+
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -1268,6 +1274,16 @@ int attn_dispatch_gq(int gq, const uint16_t *q, uint16_t *kc, uint16_t *vc, cons
 }
 
 // ---- GEMM launch configuration -------------------------------------------
+// SWH_WIDE_GEMM=0 keeps every shape on decode_gemm (A/B of csrc/wide_gemm.hip)
+bool wide_gemm_enabled() {
+    static int on = -1;
+    if (on < 0) {
+        const char *e = getenv("SWH_WIDE_GEMM");
+        on = !(e && e[0] == '0');
+    }
+    return on != 0;
+}
+
 struct GemmCfg {
     int ms, cb, nw, s, gx;  // 16-row blocks, 16-col blocks (tile), waves, K split, grid.x
     bool persist;
@@ -1500,7 +1516,7 @@ extern "C" int swh_attn_decode(const void *qkv, void *k_cache, void *v_cache, co
 
 extern "C" int64_t swh_decode_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K) {
     if (M <= 0 || N <= 0 || K <= 0) return kCounterBytes;
-    int64_t a = 0, b = 0;
+    int64_t a = wide_gemm_slab_bytes(M, N, K, 0), b = wide_gemm_slab_bytes(M, N, K, 1);
     for (int nrm : {0, 1, 2}) {
         const int64_t a1 = slab_bytes(pick_cfg(M, N, K, false, nrm), M, N);
         const int64_t b1 = slab_bytes(pick_cfg(M, 2 * N, K, true, nrm), M, 2 * N);
@@ -1529,6 +1545,11 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int64_t wcols = silu ? 2 * N : N;
     const int nm = norm_w ? 1 : (ss_in ? 2 : 0);
+    if (nm != 1 && K >= 2048 && wide_gemm_enabled()) {  // the bandwidth regime (8B decode): csrc/wide_gemm.hip
+        const int st = wide_gemm(x, w, M, N, K, eps, ss_in, bias, residual, silu, y, ldy, ss_out, workspace,
+                                 workspace_bytes, kCounterBytes, s);
+        if (st != 1) return st;
+    }
     {  // many 16-column tiles and a K that fits the X image: the tile kernel (lm head, gate/up)
         const int64_t ntile = silu ? N / 8 : N / 16;
         const char *e = getenv("SWH_GEMM_CFG");

@@ -1,0 +1,379 @@
+// Streamed decode GEMM for the bandwidth regime (Llama-3-8B decode at 64 rows,
+// BASELINE.json config 5): Y[M <= 64, N] = X[M, K] W[N, K]^T with K >= 2048.
+//
+// Why a second decode GEMM: decode_gemm stages a workgroup's whole X slice
+// [rows x K/S] in LDS, so at 64 rows and K = 4096 / 14336 it must tile the
+// rows by 16 (every weight byte then crosses the CU load path once per row
+// tile) or split K many ways; at 8B that ran the decode projections at
+// 1.6-2 TB/s.  Here a workgroup owns 128 weight rows (32 per wave) for ALL 64
+// rows over a K range, and both operands stream through a 3-slot LDS ring in
+// 128-k rounds by LDS-DMA (two rounds in flight while one is computed;
+// XOR-swizzled 16-B pieces so the 16 rows an MFMA fragment reads sit in
+// distinct banks): every weight byte is read from HBM once, X (L2-resident)
+// once per workgroup.  v_mfma_f32_16x16x32_bf16, A = X rows, B = weight rows.
+// K is split over S workgroups only as far as needed to fill the CUs; the S
+// fp32 tiles meet through write-through slabs and an agent-scope ticket (the
+// last arriver sums them in fixed order: deterministic), no spin-waits.
+// Epilogues as decode_gemm: plain (+ bias) with the folded-RMSNorm row scale
+// rstd from the producer's partial sums (ss_in), residual (+ the next norm's
+// partial sums ss_out), SiLU gate.
+#include <cstdlib>
+
+#include "common.hpp"
+
+namespace swh {
+
+int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, float eps, const float *ss_in,
+              const void *bias, void *residual, int32_t silu, void *y, int64_t ldy, float *ss_out, void *workspace,
+              int64_t workspace_bytes, int64_t counter_bytes, hipStream_t stream);
+int64_t wide_gemm_slab_bytes(int64_t M, int64_t N, int64_t K, int32_t silu);
+
+namespace {
+
+typedef __bf16 bf16x8w __attribute__((ext_vector_type(8)));
+typedef float f32x4w __attribute__((ext_vector_type(4)));
+
+constexpr int kWW = 8;                 // waves per workgroup
+constexpr int kWT = 64 * kWW;          // threads
+constexpr int kWCB = 1;                // 16-column blocks per wave
+constexpr int kWNB = 16 * kWCB * kWW;  // weight rows (tile columns) per workgroup: 128
+constexpr int kWKS = 4;                // k-steps (of 32) per round
+constexpr int kWKC = 32 * kWKS;        // k per round: 128 (256-B rows of 16 pieces)
+constexpr int kWD = 7;                 // rounds in flight (register ring depth: 24 VGPRs per round)
+constexpr int kWXB = 64 * kWKC * 2;    // X bytes of a round (16 KB)
+constexpr int kWXU = kWXB / 16 / kWT;  // X pieces per thread per round (2)
+constexpr int kWLdt = kWNB + 4;        // epilogue tile row stride (f32)
+constexpr int kWAux = 64 * kWLdt * 4;  // the epilogue tile (the two X slots live inside it), then rstd + flag
+constexpr int kWLds = kWAux + 64 * 4 + 16;
+static_assert(2 * kWXB <= kWAux, "the two X slots must fit under the epilogue tile");
+
+enum : int { WEPI_PLAIN = 0, WEPI_RESIDUAL = 1, WEPI_SILU = 2 };
+
+__device__ __forceinline__ bf16x8w as_bf8(const uint4 &v) { return __builtin_bit_cast(bf16x8w, v); }
+
+// barrier that waits for LDS traffic only: LDS-DMA still in flight stays in flight
+__device__ __forceinline__ void wide_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ uint4 pack8w(const float *v) {
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        o[k] = (uint32_t)f32_to_bf16_bits(v[2 * k]) | ((uint32_t)f32_to_bf16_bits(v[2 * k + 1]) << 16);
+    return uint4{o[0], o[1], o[2], o[3]};
+}
+
+// NM: 0 = plain X, 2 = folded RMSNorm (rstd row scale from ss_in in the epilogue).
+// Plain register loads only (no LDS-DMA: hipcc drains vmcnt(0) at the use of
+// any register load while an LDS-DMA is in flight — cdna_hip_programming.md,
+// LDS-DMA notes), so the compiler's counted waits keep kWD - 1 rounds in
+// flight; one LDS array (a second __shared__ object makes hipcc wait before
+// LDS reads).
+template <int EPI, int NM, bool BIAS>
+__global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restrict__ x, const uint16_t *__restrict__ w,
+                                                        int M, int N, int K, float eps, const float *__restrict__ ss_in,
+                                                        const uint16_t *__restrict__ bias, uint16_t *__restrict__ res,
+                                                        float *__restrict__ ss_out, uint16_t *__restrict__ y, int ldy,
+                                                        float *__restrict__ slabs, int *__restrict__ counters) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    float *rstd_s = reinterpret_cast<float *>(lds + kWAux);
+    int *flag_s = reinterpret_cast<int *>(lds + kWAux + 64 * 4);
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, rl = lane & 15, kg = lane >> 4;
+    const int S = gridDim.y, sidx = blockIdx.y, cb = blockIdx.x;
+    const int nr_all = K / kWKC;
+    const int r0 = (int)((int64_t)nr_all * sidx / S), r1 = (int)((int64_t)nr_all * (sidx + 1) / S), nr = r1 - r0;
+    const int kbase = r0 * kWKC;
+
+    // ---- the folded norm's row statistic (L2)
+    if constexpr (NM == 2) {
+        const int r = min(tid >> 2, M - 1), sub = tid & 3, nc = K / 16;
+        const float *row = ss_in + (int64_t)r * nc;
+        float v = 0.f;
+        for (int c = sub; c < nc; c += 4) v += row[c];
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        if (sub == 0) rstd_s[tid >> 2] = rsqrtf(v / (float)K + eps);
+    }
+
+    // ---- operands: a register ring kWD rounds deep per thread (X pieces + this wave's weight
+    // fragments; plain loads, so hipcc counts vmcnt per round), X then copied into one of two
+    // LDS slots per round.  LDS piece (row, p) holds X piece (row, p ^ (row & 15)): the 16 rows
+    // an MFMA fragment reads sit in distinct banks.  Tile row t -> weight row: wave t / 16,
+    // lane t % 16; SiLU tiles pair gate rows (lanes 0-7) with the matching up rows (lanes 8-15).
+    auto wrow_of = [&](int t) -> int {
+        if constexpr (EPI == WEPI_SILU) {
+            const int oc = cb * (kWNB / 2) + (t >> 4) * 8 + (t & 7);
+            return (t & 15) < 8 ? oc : N + oc;
+        } else {
+            return cb * kWNB + t;
+        }
+    };
+    const uint16_t *wp[kWCB];
+#pragma unroll
+    for (int j = 0; j < kWCB; ++j) wp[j] = w + (int64_t)wrow_of(wid * 16 * kWCB + 16 * j + rl) * K + kbase + 8 * kg;
+    const uint16_t *xp[kWXU];
+#pragma unroll
+    for (int u = 0; u < kWXU; ++u) {
+        const int id = tid + kWT * u, row = id >> 4;
+        xp[u] = x + (int64_t)min(row, M - 1) * K + kbase + (id & 15) * 8;
+    }
+    u32x4 xr[kWD][kWXU];  // vector type, not the uint4 struct: an aggregate copy kept the ring in scratch
+    uint4 wr[kWD][kWKS][kWCB];
+#define SWH_WIDE_ISSUE(q, D)                                                                                    \
+    do {                                                                                                        \
+        _Pragma("unroll") for (int u = 0; u < kWXU; ++u) xr[D][u] =                                            \
+            *reinterpret_cast<const u32x4 *>(xp[u] + (q) * kWKC);                                               \
+        _Pragma("unroll") for (int s = 0; s < kWKS; ++s) _Pragma("unroll") for (int j = 0; j < kWCB; ++j)       \
+            wr[D][s][j] = *reinterpret_cast<const uint4 *>(wp[j] + (q) * kWKC + 32 * s);                        \
+        __builtin_amdgcn_sched_barrier(0); /* rounds issue in order: the counted waits rely on it */            \
+    } while (0)
+    f32x4w acc[4][kWCB];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < kWCB; ++j) acc[i][j] = f32x4w{0.f, 0.f, 0.f, 0.f};
+    // one round: X(r) into LDS slot r & 1, barrier, 4 k-steps x 4 row blocks of MFMAs, refill
+    // the registers round r used with round r + kWD
+#define SWH_WIDE_ROUND(r, D, REFILL)                                                                            \
+    do {                                                                                                        \
+        unsigned char *xs = lds + ((r) & 1) * kWXB;                                                             \
+        _Pragma("unroll") for (int u = 0; u < kWXU; ++u) {                                                      \
+            const int id = tid + kWT * u, row = id >> 4;                                                        \
+            *reinterpret_cast<u32x4 *>(xs + row * (kWKC * 2) + (((id & 15) ^ (row & 15)) * 16)) = xr[D][u];    \
+        }                                                                                                       \
+        wide_lds_barrier(); /* X(r) visible; every wave has left round r - 2 (same slot) */                     \
+        _Pragma("unroll") for (int s = 0; s < kWKS; ++s) {                                                      \
+            uint4 a[4];                                                                                         \
+            _Pragma("unroll") for (int i = 0; i < 4; ++i) a[i] =                                                \
+                *reinterpret_cast<const uint4 *>(xs + (16 * i + rl) * (kWKC * 2) + (((4 * s + kg) ^ rl) * 16));  \
+            _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < kWCB; ++j)      \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf8(a[i]), as_bf8(wr[D][s][j]),          \
+                                                                    acc[i][j], 0, 0, 0);                         \
+        }                                                                                                       \
+        __builtin_amdgcn_sched_barrier(0);                                                                      \
+        if (REFILL) SWH_WIDE_ISSUE((r) + kWD, D);                                                               \
+    } while (0)
+    int rb = 0;
+    if (nr >= 2 * kWD) {
+        // unconditional prologue and steady state: every refill is in range, so hipcc's counted
+        // waits see one fixed pattern at the loop header (kWD - 1 rounds stay in flight)
+#pragma unroll
+        for (int d = 0; d < kWD; ++d) SWH_WIDE_ISSUE(d, d);
+        for (; rb + 2 * kWD <= nr; rb += kWD) {
+#pragma unroll
+            for (int d = 0; d < kWD; ++d) SWH_WIDE_ROUND(rb + d, d, true);
+        }
+    } else {
+#pragma unroll
+        for (int d = 0; d < kWD; ++d)
+            if (d < nr) SWH_WIDE_ISSUE(d, d);
+    }
+    // tail: the last kWD .. 2 kWD - 1 rounds (or all of them when nr < 2 kWD)
+#pragma unroll
+    for (int d = 0; d < 2 * kWD; ++d) {
+        const int r = rb + d;
+        if (r < nr) SWH_WIDE_ROUND(r, d % kWD, r + kWD < nr);
+    }
+#undef SWH_WIDE_ROUND
+    wide_lds_barrier();  // every wave is past its last X read: the slots become the epilogue tile
+#undef SWH_WIDE_ISSUE
+
+    // ---- this workgroup's 64 x 128 fp32 tile (C layout: lane holds rows 16 i + 4 kg + e, column rl)
+    float *tile = reinterpret_cast<float *>(lds);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < kWCB; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) tile[(16 * i + 4 * kg + e) * kWLdt + wid * 16 * kWCB + 16 * j + rl] = acc[i][j][e];
+    __syncthreads();
+
+    // ---- split K (the in-launch slab hand-off of cdna_hip_programming.md, projection GEMMs item 2):
+    // plain 16-B slab stores, one agent-scope release before the ticket; the last arriver acquires
+    // once and sums the S slabs with plain 16-B loads in fixed order (deterministic, placement-free)
+    if (S > 1) {
+        float4 *my = reinterpret_cast<float4 *>(slabs + ((int64_t)cb * S + sidx) * (64 * kWNB));
+        for (int idx = tid; idx < 64 * kWNB / 4; idx += kWT) {
+            const int r = idx / (kWNB / 4), c4 = idx % (kWNB / 4);
+            my[idx] = *reinterpret_cast<const float4 *>(tile + r * kWLdt + 4 * c4);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int t = __hip_atomic_fetch_add(counters + cb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *flag_s = (t == S - 1);
+            if (t == S - 1) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+        __syncthreads();
+        if (!*flag_s) return;
+        const float4 *base = reinterpret_cast<const float4 *>(slabs + (int64_t)cb * S * (64 * kWNB));
+        for (int idx = tid; idx < 64 * kWNB / 4; idx += kWT) {
+            float4 v[8];
+            float4 sum = float4{0.f, 0.f, 0.f, 0.f};
+            for (int q0 = 0; q0 < S; q0 += 8) {  // up to eight slab loads in flight per thread
+                const int nq = min(8, S - q0);
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    if (q < nq) v[q] = base[(int64_t)(q0 + q) * (64 * kWNB / 4) + idx];
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    if (q < nq) {
+                        sum.x += v[q].x;
+                        sum.y += v[q].y;
+                        sum.z += v[q].z;
+                        sum.w += v[q].w;
+                    }
+            }
+            const int r = idx / (kWNB / 4), c4 = idx % (kWNB / 4);
+            *reinterpret_cast<float4 *>(tile + r * kWLdt + 4 * c4) = sum;
+        }
+        if (tid == 0) __hip_atomic_store(counters + cb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+    }
+
+    // ---- epilogue
+    if constexpr (EPI == WEPI_SILU) {
+        // 64 rows x 8 groups of 8 output columns: tile columns 16 g + c (gate) and 16 g + 8 + c (up)
+        for (int idx = tid; idx < 64 * 8; idx += kWT) {
+            const int r = idx >> 3, g = idx & 7;
+            if (r >= M) continue;
+            const float sc = NM == 2 ? rstd_s[r] : 1.f;
+            float o[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const float gv = round_bf16(tile[r * kWLdt + 16 * g + c] * sc);
+                const float uv = round_bf16(tile[r * kWLdt + 16 * g + 8 + c] * sc);
+                o[c] = round_bf16(gv / (1.f + expf(-gv))) * uv;
+            }
+            *reinterpret_cast<uint4 *>(y + (int64_t)r * ldy + cb * (kWNB / 2) + 8 * g) = pack8w(o);
+        }
+    } else if constexpr (EPI == WEPI_RESIDUAL) {
+        // 64 rows x 8 chunks of 16 columns: s = bf16(s + bf16(acc)), chunk sum of squares of the new s
+        for (int idx = tid; idx < 64 * 8; idx += kWT) {
+            const int r = idx >> 3, j = idx & 7;
+            if (r >= M) continue;
+            uint4 *sp = reinterpret_cast<uint4 *>(res + (int64_t)r * ldy + cb * kWNB + 16 * j);
+            const uint4 s0 = sp[0], s1 = sp[1];
+            float a[16], nv[16];
+            unpack16<SWH_BF16>(s0, a);
+            unpack16<SWH_BF16>(s1, a + 8);
+            float ss = 0.f;
+#pragma unroll
+            for (int c = 0; c < 16; ++c) {
+                nv[c] = round_bf16(a[c] + round_bf16(tile[r * kWLdt + 16 * j + c]));
+                ss = fmaf(nv[c], nv[c], ss);
+            }
+            sp[0] = pack8w(nv);
+            sp[1] = pack8w(nv + 8);
+            if (ss_out) ss_out[(int64_t)r * (N / 16) + cb * (kWNB / 16) + j] = ss;
+        }
+    } else {
+        // 64 rows x 16 groups of 8 columns
+        for (int idx = tid; idx < 64 * 16; idx += kWT) {
+            const int r = idx >> 4, j = idx & 15;
+            if (r >= M) continue;
+            const float sc = NM == 2 ? rstd_s[r] : 1.f;
+            const int col = cb * kWNB + 8 * j;
+            float v[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) v[c] = tile[r * kWLdt + 8 * j + c] * sc;
+            if constexpr (BIAS) {
+                float b[8];
+                unpack16<SWH_BF16>(*reinterpret_cast<const uint4 *>(bias + col), b);
+#pragma unroll
+                for (int c = 0; c < 8; ++c) v[c] += b[c];
+            }
+            *reinterpret_cast<uint4 *>(y + (int64_t)r * ldy + col) = pack8w(v);
+        }
+    }
+}
+
+int wide_split(int64_t N, int64_t K, int32_t silu) {
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+    }
+    const int64_t ncb = (silu ? 2 * N : N) / kWNB, nr = K / kWKC;
+    int64_t s = (ncu + ncb / 2) / ncb;  // about one workgroup per CU
+    static int smax = 0;
+    if (!smax) {  // the last arriver reads S x 32 KB of slabs (SWH_WIDE_SMAX: A/B)
+        const char *e = getenv("SWH_WIDE_SMAX");
+        smax = e ? atoi(e) : 8;
+        if (smax < 1) smax = 1;
+    }
+    if (s > smax) s = smax;
+    if (s < 1) s = 1;
+    if (s > nr) s = nr;
+    return (int)s;
+}
+
+template <int EPI, int NM, bool BIAS>
+int launch_wide(dim3 grid, hipStream_t st, const uint16_t *x, const uint16_t *w, int M, int N, int K, float eps,
+                const float *ss_in, const uint16_t *bias, uint16_t *res, float *ss_out, uint16_t *y, int ldy,
+                float *slabs, int *counters) {
+    static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in once per kernel
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&wide_gemm_kernel<EPI, NM, BIAS>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kWLds) != hipSuccess)
+            return SWH_E_LAUNCH;
+        attr = true;
+    }
+    wide_gemm_kernel<EPI, NM, BIAS><<<grid, kWT, kWLds, st>>>(x, w, M, N, K, eps, ss_in, bias, res, ss_out, y, ldy,
+                                                              slabs, counters);
+    return launch_status();
+}
+
+}  // namespace
+
+// Bytes of fp32 slabs the split-K reduction needs (0 when the shape is not eligible or S == 1).
+int64_t wide_gemm_slab_bytes(int64_t M, int64_t N, int64_t K, int32_t silu) {
+    if (M <= 0 || M > 64 || K % kWKC || (silu ? 2 * N : N) % kWNB || (silu ? 2 * N : N) < 1024) return 0;
+    const int64_t ncb = (silu ? 2 * N : N) / kWNB;
+    const int s = wide_split(N, K, silu);
+    return s > 1 ? ncb * s * 64 * kWNB * (int64_t)sizeof(float) : 0;
+}
+
+// 1 = not eligible (the caller uses decode_gemm), else a SWH status.
+int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, float eps, const float *ss_in,
+              const void *bias, void *residual, int32_t silu, void *y, int64_t ldy, float *ss_out, void *workspace,
+              int64_t workspace_bytes, int64_t counter_bytes, hipStream_t st) {
+    const int64_t wcols = silu ? 2 * N : N;
+    // wide tiles only: a narrow output (Qwen2.5-0.5B down, N 896) stays on decode_gemm
+    if (M <= 0 || M > 64 || K % kWKC || K < kWKC || wcols % kWNB || wcols < 1024 || N % 16) return 1;
+    const int64_t ncb = wcols / kWNB;
+    const int s = wide_split(N, K, silu);
+    if (ncb > 65535 || ncb * (int64_t)sizeof(int) > counter_bytes) return 1;
+    float *slabs = nullptr;
+    if (s > 1) {
+        if (!workspace || workspace_bytes < counter_bytes + ncb * s * 64 * kWNB * (int64_t)sizeof(float)) return 1;
+        slabs = reinterpret_cast<float *>(static_cast<char *>(workspace) + counter_bytes);
+    }
+    int *ctr = static_cast<int *>(workspace);
+    const dim3 grid((unsigned)ncb, (unsigned)s);
+    const auto *X = static_cast<const uint16_t *>(x);
+    const auto *W = static_cast<const uint16_t *>(w);
+    const auto *B = static_cast<const uint16_t *>(bias);
+    auto *R = static_cast<uint16_t *>(residual);
+    auto *Y = static_cast<uint16_t *>(y);
+    const int m = (int)M, n = (int)N, k = (int)K, ld = (int)ldy;
+    if (silu) {
+        if (ss_in) return launch_wide<WEPI_SILU, 2, false>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
+        return launch_wide<WEPI_SILU, 0, false>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
+    }
+    if (residual) return launch_wide<WEPI_RESIDUAL, 0, false>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
+    if (B) {
+        if (ss_in) return launch_wide<WEPI_PLAIN, 2, true>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
+        return launch_wide<WEPI_PLAIN, 0, true>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
+    }
+    if (ss_in) return launch_wide<WEPI_PLAIN, 2, false>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
+    return launch_wide<WEPI_PLAIN, 0, false>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
+}
+
+}  // namespace swh

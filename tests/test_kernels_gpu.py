@@ -1158,3 +1158,46 @@ def test_attention_fwd_bwd_matches_reference(ops, dev, B, Hq, Hkv, L, D, pad):
     for mine, r in ((qa.grad, qr.grad), (ka.grad, kr.grad), (va.grad, vr.grad)):
         err = (mine.float() - r).abs().max().item()
         assert err <= 3e-2 * max(1.0, r.abs().max().item()), err
+
+
+@pytest.mark.parametrize("name,M,N,K", [("qkv_bias", 64, 6144, 4096), ("o_res", 8, 4096, 4096),
+                                        ("gate_up", 33, 14336, 4096), ("down", 64, 4096, 14336),
+                                        ("down_tiny_llama", 6, 1024, 2048), ("lm_head", 64, 128256, 4096)])
+def test_wide_gemm_bandwidth_regime(ops, dev, name, M, N, K):
+    """csrc/wide_gemm.hip (decode GEMMs with K >= 2048, the Llama-3-8B decode
+    shapes of config 5) through swh_decode_gemm, in the forms the decode step
+    uses: folded-RMSNorm row scale from the producer's partial sums (ss_in)
+    with / without bias, SiLU gate, residual + the next norm's partial sums;
+    64 rows and ragged row counts; split-K tiles bit-identical across launches."""
+    from swh_trl_amd import nn_ops
+    g = _gen(35)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
+    ss = x.float().view(M, K // 16, 16).pow(2).sum(-1).contiguous()
+    rstd = torch.rsqrt(ss.sum(-1, keepdim=True) / K + 1e-5)
+    if name.startswith(("o_", "down")):
+        w = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(dev)
+        s = torch.randn(M, N, generator=g).to(torch.bfloat16).to(dev)
+        s0 = s.clone()
+        sso = torch.empty(M, N // 16, device=dev)
+        nn_ops.decode_gemm(x, w, residual=s, ss_out=sso)
+        ref = (s0.float() + (x.float() @ w.float().t()).to(torch.bfloat16).float()).to(torch.bfloat16)
+        assert (s.float() - ref.float()).abs().max().item() <= 2e-2 * ref.float().abs().max().item() + 2e-2
+        torch.testing.assert_close(sso, s.float().view(M, N // 16, 16).pow(2).sum(-1), rtol=1e-5, atol=1e-4)
+        s2 = s0.clone()
+        nn_ops.decode_gemm(x, w, residual=s2, ss_out=sso)
+        assert torch.equal(s, s2)
+        return
+    if name == "gate_up":
+        w = (torch.randn(2 * N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(dev)
+        act = nn_ops.decode_gemm(x, w, silu=True, ss_in=ss, eps=1e-5)
+        gu = ((x.float() @ w.float().t()) * rstd).to(torch.bfloat16)
+        ref = (torch.nn.functional.silu(gu[:, :N].float()).to(torch.bfloat16).float() * gu[:, N:].float())
+        torch.testing.assert_close(act.float(), ref, rtol=2e-2, atol=2e-2)
+        assert torch.equal(act, nn_ops.decode_gemm(x, w, silu=True, ss_in=ss, eps=1e-5))
+        return
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(dev)
+    b = (0.1 * torch.randn(N, generator=g)).to(torch.bfloat16).to(dev) if name == "qkv_bias" else None
+    y = nn_ops.decode_gemm(x, w, ss_in=ss, eps=1e-5, bias=b)
+    ref = (x.float() @ w.float().t()) * rstd + (b.float() if b is not None else 0.0)
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=2e-2)
+    assert torch.equal(y, nn_ops.decode_gemm(x, w, ss_in=ss, eps=1e-5, bias=b))
