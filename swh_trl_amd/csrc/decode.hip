@@ -1274,6 +1274,15 @@ int attn_dispatch_gq(int gq, const uint16_t *q, uint16_t *kc, uint16_t *vc, cons
 }
 
 // ---- GEMM launch configuration -------------------------------------------
+// smallest K routed to csrc/wide_gemm.hip (SWH_WIDE_KMIN: A/B)
+int64_t wide_gemm_kmin() {
+    static int64_t k = -1;
+    if (k < 0) {
+        const char *e = getenv("SWH_WIDE_KMIN");
+        k = e ? atoll(e) : 2048;
+    }
+    return k;
+}
 // SWH_WIDE_GEMM=0 keeps every shape on decode_gemm (A/B of csrc/wide_gemm.hip)
 bool wide_gemm_enabled() {
     static int on = -1;
@@ -1545,7 +1554,7 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int64_t wcols = silu ? 2 * N : N;
     const int nm = norm_w ? 1 : (ss_in ? 2 : 0);
-    if (nm != 1 && K >= 2048 && wide_gemm_enabled()) {  // the bandwidth regime (8B decode): csrc/wide_gemm.hip
+    if (nm != 1 && K >= wide_gemm_kmin() && wide_gemm_enabled()) {  // the bandwidth regime (8B decode): csrc/wide_gemm.hip
         const int st = wide_gemm(x, w, M, N, K, eps, ss_in, bias, residual, silu, y, ldy, ss_out, workspace,
                                  workspace_bytes, kCounterBytes, s);
         if (st != 1) return st;

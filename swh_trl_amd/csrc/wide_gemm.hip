@@ -187,20 +187,23 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
             for (int e = 0; e < 4; ++e) tile[(16 * i + 4 * kg + e) * kWLdt + wid * 16 * kWCB + 16 * j + rl] = acc[i][j][e];
     __syncthreads();
 
-    // ---- split K (the in-launch slab hand-off of cdna_hip_programming.md, projection GEMMs item 2):
-    // plain 16-B slab stores, one agent-scope release before the ticket; the last arriver acquires
-    // once and sums the S slabs with plain 16-B loads in fixed order (deterministic, placement-free)
+    // ---- split K (the in-launch slab hand-off of cdna_hip_programming.md, projection GEMMs item 2,
+    // write-through form): sc1 16-B slab stores drained by every wave, one relaxed agent-scope
+    // ticket; the last arriver acquires once and sums the S slabs with plain 16-B loads in fixed
+    // order (deterministic for any placement of the S workgroups over the XCDs)
     if (S > 1) {
-        float4 *my = reinterpret_cast<float4 *>(slabs + ((int64_t)cb * S + sidx) * (64 * kWNB));
+        float *my = slabs + ((int64_t)cb * S + sidx) * (64 * kWNB);
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(my, 0, 64 * kWNB * 4, 0x00020000);
         for (int idx = tid; idx < 64 * kWNB / 4; idx += kWT) {
             const int r = idx / (kWNB / 4), c4 = idx % (kWNB / 4);
-            my[idx] = *reinterpret_cast<const float4 *>(tile + r * kWLdt + 4 * c4);
+            const float4 v = *reinterpret_cast<const float4 *>(tile + r * kWLdt + 4 * c4);
+            __builtin_amdgcn_raw_buffer_store_b128(
+                u32x4{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)}, rsrc,
+                idx * 16, 0, 16 /* sc1: write-through */);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const int t = __hip_atomic_fetch_add(counters + cb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             *flag_s = (t == S - 1);
             if (t == S - 1) {
