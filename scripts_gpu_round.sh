@@ -20,8 +20,9 @@ for step in "$@"; do
     g2) run g2 600 python -u -m pytest tests/test_gpt2_gpu.py -v -m gpu --timeout 200 --timeout-method thread ;;
     cfg1) run cfg1 300 python tools/bench_cfg1.py ;;
     wide) run wide 600 python -u -m pytest tests -v -m gpu --timeout 200 --timeout-method thread -k "wide_gemm or llama" ;;
+    shared) run shared 600 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -k "shared_prompt or step_parity or grpo_trainer_smoke or llama_grpo or rewards or checkpoint_resume" ;;
     newt) run newt 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread -k "step_parity or adamw or bench_launches or masked_whiten" ;;
-    tune) SWH_GEMM_TUNING=tune SWH_GEMM_TABLE=gpurun_out/gemm_tuned.csv run tune 900 python bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
+    tune) cp swh_trl_amd/tuning/gemm_mi355x.csv gpurun_out/gemm_tuned.csv && SWH_GEMM_TUNING=tune SWH_GEMM_TABLE=gpurun_out/gemm_tuned.csv run tune 900 python bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
     benchtuned) SWH_GEMM_TABLE=gpurun_out/gemm_tuned.csv run benchtuned 600 python bench.py --steps 3 --warmup 2 --no-cpu-baseline ;;
     lmk) run lmk 300 python -u -m pytest tests/test_kernels_gpu.py -x -v -m gpu -k "lm_head or decode_gemm or sampler" --timeout 120 --timeout-method thread ;;
     decab) run dec0 300 python tools/bench_decode.py && for v in vA vB; do SWH_LIB_PATH=tools/_build/$v.so run dec_$v 300 python tools/bench_decode.py || exit 1; done ;;
@@ -49,6 +50,8 @@ for step in "$@"; do
     dbg_graph) GRAPH=1 run dbg_graph 300 python tools/debug_decode.py ;;
     serial2) AMD_SERIALIZE_KERNEL=3 SWH_TRACE=1 run serial2 500 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --layers 2 ;;
     trace2) SWH_TRACE=1 run trace2 400 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --layers 2 ;;
+    ktrace) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null && run ktrace 900 rocprofv3 --kernel-trace -d gpurun_out/ktrace -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
+    fenceab) SWH_GEMM_FENCE=0 run b_nofence 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline && run b_fence 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline && SWH_GEMM_FENCE=0 run b_nofence2 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null && run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline ;;
     l8s) SWH_TRACE=1 run l8s 400 python tools/bench_llama8b.py --prompts 2 --P 256 --C 1024 --steps 1 --warmup 1 --fuse-budget 16384 ;;
     hangp) run hangp 150 python tools/phase_probe.py --layers 2 --B 8 --L 512 && run hangp2 150 python tools/phase_probe.py --layers 2 --B 8 --L 1280 ;;

@@ -169,6 +169,8 @@ class GPT2LM(CausalLM):
         if self.head == "score":
             add("score", 1, H)
 
+    supports_shared_prefix = False  # the grouped forward is the Qwen2 / Llama layer
+
     def _check_attention(self):
         self._hip_attn = False  # SDPA: head_dim 16 (config 1) is below the MFMA attention tile
 

@@ -598,22 +598,110 @@ class CausalLM:
         q, k, v = nn_ops.QKVRopeFn.apply(qkv, positions, cos_t, sin_t, Hq, Hkv, D)
         if kv_out is not None:
             kv_out(i, k, v)
+        o = self._attend(q, k, v, mask)
+        o = o.transpose(1, 2).reshape(B, L, c.q_dim)
+        return self._post_attention(i, x, o)
+
+    def _attend(self, q, k, v, mask):
+        """Causal GQA attention over [B, H, L, D] (padding mask as built by hidden_states)."""
+        c = self.cfg
+        D = c.head_dim
         if self._hip_attn:  # csrc/attn.hip: causal GQA flash attention, padding as transformers
             km, fv = (None, None) if mask is None else mask
-            o = nn_ops.AttentionFn.apply(q, k, v, D ** -0.5, km, fv)
-        else:  # torch SDPA (aotriton), GQA inside the kernel
-            gqa = Hq != Hkv
-            if mask is None:
-                o = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=D ** -0.5, enable_gqa=gqa)
-            else:
-                o = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, scale=D ** -0.5, enable_gqa=gqa)
-        o = o.transpose(1, 2).reshape(B, L, c.q_dim)
+            return nn_ops.AttentionFn.apply(q, k, v, D ** -0.5, km, fv)
+        gqa = c.num_attention_heads != c.num_key_value_heads  # torch SDPA (aotriton), GQA inside the kernel
+        if mask is None:
+            return F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=D ** -0.5, enable_gqa=gqa)
+        return F.scaled_dot_product_attention(q, k, v, attn_mask=mask, scale=D ** -0.5, enable_gqa=gqa)
+
+    def _post_attention(self, i, x, o):
+        """o-proj, residual + post-attention norm, the SiLU-gated MLP: (x + o, MLP output)."""
+        c = self.cfg
         o = _Linear.apply(o, self.p[f"l{i}.o_w"], None, self._gv(f"l{i}.o_w"), None)
         x, h = _AddRMSNorm.apply(x, o, self.p[f"l{i}.ln_post"], self._gv(f"l{i}.ln_post"), c.rms_norm_eps)
         gu = _Linear.apply(h, self.p[f"l{i}.gu_w"], None, self._gv(f"l{i}.gu_w"), None)
         a = nn_ops.SiluMulFn.apply(gu)
         d = _Linear.apply(a, self.p[f"l{i}.down_w"], None, self._gv(f"l{i}.down_w"), None)
         return x, d
+
+    def _mask(self, key_mask, L: int, padded: bool, device):
+        """The attention mask of a key-padding mask [B, L] (None: causal only)."""
+        if key_mask is None or not padded:
+            return None
+        if self._hip_attn:
+            # (key_mask, index of the first valid key): the kernel's visibility rule
+            km = key_mask.to(torch.int32).contiguous()
+            return km, (km.cumsum(-1) == 0).sum(-1).to(torch.int32)
+        km = key_mask.bool()
+        causal = torch.ones(L, L, device=device, dtype=torch.bool).tril()
+        # a query with no valid key at all (left padding) sees itself, so no
+        # softmax row is empty; any other padded query (right padding after
+        # a stop token) sees exactly the valid keys before it, as transformers
+        no_key = km.cumsum(-1) == 0
+        eye = torch.eye(L, device=device, dtype=torch.bool)
+        return causal & (km[:, None, None, :] | (eye & no_key[:, None, :, None]))
+
+    supports_shared_prefix = True
+
+    def hidden_states_grouped(self, prompt_ids: torch.Tensor, prompt_mask: torch.Tensor,
+                              completion_ids: torch.Tensor, G: int):
+        """The scoring / training forward of `hidden_states(cat(prompt, completion))`
+        for rows in groups of G consecutive rows that share one prompt (GRPO's
+        num_generations copies, grpo_trainer.py:97-192): every token-wise op
+        (projections, norms, MLP) runs on the prompt tokens ONCE per group
+        and on each row's completion tokens; attention sees, per row, the
+        group's prompt keys followed by its own completion (positions and
+        padding exactly as the per-row forward).  The prompt K/V/Q are
+        broadcast to the group's rows by expand (their gradients are the
+        fixed-order sums over the rows).  Returns (h_last [U, H]: the final
+        hidden state of the last prompt position of each group, h_comp
+        [R, C, H]: the completion positions)."""
+        c = self.cfg
+        R, C = completion_ids.shape
+        if G < 1 or R % G:
+            raise ValueError(f"{R} rows do not form groups of {G}")
+        U = R // G
+        dev = completion_ids.device
+        pid = prompt_ids[::G].contiguous()
+        pm = prompt_mask[::G]
+        P = pid.shape[1]
+        NP, H = U * P, c.hidden_size
+        Hq, Hkv, D = c.num_attention_heads, c.num_key_value_heads, c.head_dim
+        ids = torch.cat([pid.reshape(-1), completion_ids.reshape(-1)]).view(1, -1)
+        pos_p = torch.arange(P, device=dev).expand(U, P)
+        pos_c = torch.arange(P, P + C, device=dev).expand(R, C)
+        cos_t, sin_t = self.rope(P + C)
+        padded = not bool(pm.bool().all())
+        km = torch.cat([pm.to(torch.int32).repeat_interleave(G, 0), torch.ones(R, C, dtype=torch.int32, device=dev)], 1)
+        mask = self._mask(km, P + C, padded, dev)
+
+        def bcast(t):  # [U, ...] -> [R, ...], the group's tensor for each of its rows
+            return t[:, None].expand(U, G, *t.shape[1:]).reshape(R, *t.shape[1:])
+
+        x = _Embedding.apply(ids, self.p["embed"], self._gv("embed"), self._anchor).view(-1, H)
+        d = None
+        eps = c.rms_norm_eps
+        for i in range(c.num_hidden_layers):
+            if self.on_layer_grads is not None and torch.is_grad_enabled():
+                x = _GradReady.apply(x, i, self.on_layer_grads)
+            if d is None:
+                h = _RMSNorm.apply(x, self.p[f"l{i}.ln_in"], self._gv(f"l{i}.ln_in"), eps)
+            else:
+                x, h = _AddRMSNorm.apply(x, d, self.p[f"l{i}.ln_in"], self._gv(f"l{i}.ln_in"), eps)
+            qkv = _Linear.apply(h, self.p[f"l{i}.qkv_w"], self.p.get(f"l{i}.qkv_b"), self._gv(f"l{i}.qkv_w"),
+                                self._gv(f"l{i}.qkv_b"))
+            q_p, k_p, v_p = nn_ops.QKVRopeFn.apply(qkv[:NP].view(U, P, -1), pos_p, cos_t, sin_t, Hq, Hkv, D)
+            q_c, k_c, v_c = nn_ops.QKVRopeFn.apply(qkv[NP:].view(R, C, -1), pos_c, cos_t, sin_t, Hq, Hkv, D)
+            q = torch.cat([bcast(q_p), q_c], 2)
+            k = torch.cat([bcast(k_p), k_c], 2)
+            v = torch.cat([bcast(v_p), v_c], 2)
+            o = self._attend(q, k, v, mask)  # [R, Hq, P + C, D]
+            o_p = o.view(U, G, Hq, P + C, D)[:, 0, :, :P]  # the group's prompt rows, once
+            o_c = o[:, :, P:]
+            o = torch.cat([o_p.transpose(1, 2).reshape(NP, c.q_dim), o_c.transpose(1, 2).reshape(R * C, c.q_dim)])
+            x, d = self._post_attention(i, x, o)
+        _, h = _AddRMSNorm.apply(x, d, self.p["norm"], self._gv("norm"), eps)
+        return h[:NP].view(U, P, H)[:, P - 1], h[NP:].view(R, C, H)
 
     def hidden_states(self, ids: torch.Tensor, positions: Optional[torch.Tensor] = None,
                       key_mask: Optional[torch.Tensor] = None, kv_out=None, max_pos: Optional[int] = None,
@@ -633,22 +721,9 @@ class CausalLM:
             max_pos = int(positions.max().item()) if positions.numel() else 0
         cos_t, sin_t = self.rope(max_pos + 1)
         positions = positions.to(torch.int64).contiguous()
-        mask = None
         if padded is None:
             padded = key_mask is not None and not bool(key_mask.bool().all())
-        if key_mask is not None and padded and self._hip_attn:
-            # (key_mask, index of the first valid key): the kernel's visibility rule
-            km = key_mask.to(torch.int32).contiguous()
-            mask = (km, (km.cumsum(-1) == 0).sum(-1).to(torch.int32))
-        elif key_mask is not None and padded:
-            km = key_mask.bool()
-            causal = torch.ones(L, L, device=ids.device, dtype=torch.bool).tril()
-            # a query with no valid key at all (left padding) sees itself, so no
-            # softmax row is empty; any other padded query (right padding after
-            # a stop token) sees exactly the valid keys before it, as transformers
-            no_key = km.cumsum(-1) == 0
-            eye = torch.eye(L, device=ids.device, dtype=torch.bool)
-            mask = causal & (km[:, None, None, :] | (eye & no_key[:, None, :, None]))
+        mask = self._mask(key_mask, L, padded, ids.device)
         x = _Embedding.apply(ids, self.p["embed"], self._gv("embed"), self._anchor)
         d = None
         eps = c.rms_norm_eps

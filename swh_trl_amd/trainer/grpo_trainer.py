@@ -40,17 +40,7 @@ from .utils import generation_batch_indices, left_pad, linear_lr, pad_left_cat, 
     truncate_with_protected_tokens
 
 RewardFunc = Union[str, Callable, torch.nn.Module]
-_TRACE = os.environ.get("SWH_TRACE", "0") == "1"
-_T0 = [time.time()]
-
-
-def _trace(msg: str):
-    """SWH_TRACE=1: synchronised phase timings on stderr (diagnostics only)."""
-    if _TRACE:
-        torch.cuda.synchronize()
-        import sys
-        now = time.time()
-        print(f"[swh {now - _T0[0]:8.3f}s] {msg}", file=sys.stderr, flush=True)
+from ..profiling import trace as _trace  # noqa: E402  (one clock for every phase line)
 
 
 class TrainerState:
@@ -375,12 +365,42 @@ class GRPOTrainer:
         logits_to_keep=C+1, drop the last position, /T, selective_log_softmax
         and entropy_from_logits — lm head + log-prob + entropy fused and
         row-chunked (engine/model.py `_LMHeadLogp`)."""
+        grp = self._prompt_groups(batch) if getattr(model, "supports_shared_prefix", False) else None
+        if grp is not None:
+            # the G copies of each prompt share one prompt forward (CausalLM.hidden_states_grouped)
+            perm, G = grp
+            cid = batch["completion_ids"][perm]
+            h_last, h_comp = model.hidden_states_grouped(batch["prompt_ids"][perm], batch["prompt_mask"][perm], cid, G)
+            R, C = cid.shape
+            U, H = h_last.shape
+            first = h_last[:, None, None].expand(U, G, 1, H).reshape(R, 1, H)  # predicts completion token 0
+            lp, ent = model.logp_entropy(torch.cat([first, h_comp[:, :C - 1]], 1), cid, self.temperature,
+                                         compute_entropy)
+            inv = torch.empty_like(perm)
+            inv[perm] = torch.arange(R, device=perm.device)
+            return lp[inv], (ent[inv] if ent is not None else None)
         ids = torch.cat([batch["prompt_ids"], batch["completion_ids"]], 1)
         P = batch["prompt_ids"].shape[1]
         C = batch["completion_ids"].shape[1]
         key_mask = torch.cat([batch["prompt_mask"], torch.ones_like(batch["completion_ids"], dtype=torch.int32)], 1)
         h = model.hidden_states(ids, key_mask=key_mask)
         return model.logp_entropy(h[:, P - 1:P + C - 1], batch["completion_ids"], self.temperature, compute_entropy)
+
+    @staticmethod
+    def _prompt_groups(batch: dict):
+        """(row order putting each prompt's rows consecutively, G) when every
+        prompt of the batch appears exactly G >= 2 times (GRPO's generations of
+        one prompt, in any shuffled order); None otherwise.  SWH_SHARED_PREFIX=0
+        keeps the per-row forward."""
+        if os.environ.get("SWH_SHARED_PREFIX", "1") == "0":
+            return None
+        pid, pm = batch["prompt_ids"], batch["prompt_mask"]
+        key = torch.cat([pid.to(torch.int64), pm.to(torch.int64)], 1)
+        _, inv, counts = torch.unique(key, dim=0, return_inverse=True, return_counts=True)
+        G = int(counts[0])
+        if G < 2 or not bool((counts == G).all()):
+            return None
+        return torch.sort(inv, stable=True).indices, G
 
     @torch.no_grad()
     def _score_logps(self, model: CausalLM, batch: dict) -> torch.Tensor:

@@ -556,3 +556,46 @@ def test_checkpoint_resume_is_bit_identical_and_loads_in_transformers(dev, tmp_p
         theirs = hf(input_ids=ids).logits.float()
     err = (mine - theirs).abs().max().item()
     assert err <= 0.03 * theirs.abs().max().item() + 0.03, err
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("left_pad", [False, True])
+def test_shared_prompt_forward_matches_per_row(dev, dtype, left_pad):
+    """CausalLM.hidden_states_grouped (the G generations of a prompt share one
+    prompt forward) equals the per-row forward over cat(prompt, completion):
+    completion log-probs and every weight gradient (fp32: SDPA path, 1e-5;
+    bf16: HIP attention path, bf16 tolerance)."""
+    from swh_trl_amd.engine import CausalLM, tiny_qwen2
+    m = CausalLM(tiny_qwen2(1024, 2), dev, seed=9, init_std=0.05, dtype=dtype)
+    g = torch.Generator().manual_seed(9)
+    U, G, P, C = 3, 4, 12, 20
+    R = U * G
+    pid = torch.randint(2, 1024, (U, P), generator=g).repeat_interleave(G, 0).to(dev)
+    pm = torch.ones(R, P, dtype=torch.int32, device=dev)
+    if left_pad:
+        pm[G:2 * G, :5] = 0
+        pid[G:2 * G, :5] = 0
+    comp = torch.randint(2, 1024, (R, C), generator=g).to(dev)
+    w = torch.randn(R, C, generator=g).to(dev)
+    m.zero_grad()
+    km = torch.cat([pm, torch.ones(R, C, dtype=torch.int32, device=dev)], 1)
+    h = m.hidden_states(torch.cat([pid, comp], 1), key_mask=km)
+    lp1, _ = m.logp_entropy(h[:, P - 1:P + C - 1], comp, 0.9, False)
+    (lp1 * w).sum().backward()
+    torch.cuda.synchronize()
+    g1 = m.grad.float().clone()
+    m.zero_grad()
+    h_last, h_comp = m.hidden_states_grouped(pid, pm, comp, G)
+    first = h_last[:, None, None].expand(U, G, 1, h_last.shape[-1]).reshape(R, 1, -1)
+    lp2, _ = m.logp_entropy(torch.cat([first, h_comp[:, :C - 1]], 1), comp, 0.9, False)
+    (lp2 * w).sum().backward()
+    torch.cuda.synchronize()
+    g2 = m.grad.float().clone()
+    if dtype == torch.float32:
+        torch.testing.assert_close(lp2, lp1, rtol=1e-5, atol=1e-5)
+        tol = 1e-5
+    else:
+        torch.testing.assert_close(lp2, lp1, rtol=2e-2, atol=5e-2)
+        tol = 3e-2
+    rel = ((g2 - g1).norm() / g1.norm()).item()
+    assert rel <= tol, rel
