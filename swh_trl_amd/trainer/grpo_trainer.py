@@ -288,8 +288,12 @@ class GRPOTrainer:
                                                                self.num_generations, self.scale_rewards)
         if self.world > 1:
             adv = adv[self.rank * B:(self.rank + 1) * B]
+        # rows of one prompt are consecutive here (RepeatSampler): a group id per row lets the
+        # training forward share each prompt's tokens after the shuffle (_prompt_groups)
+        same = (prompt_ids[1:] == prompt_ids[:-1]).all(1) & (prompt_mask[1:] == prompt_mask[:-1]).all(1)
+        group = torch.cat([torch.zeros(1, dtype=torch.int64, device=self.device), (~same).long().cumsum(0)])
         out = {"prompt_ids": prompt_ids, "prompt_mask": prompt_mask, "completion_ids": completion_ids,
-               "completion_mask": completion_mask, "advantages": adv}
+               "completion_mask": completion_mask, "advantages": adv, "prompt_group": group + self._gen_count * B}
         generate_every = a.steps_per_generation * self.num_iterations
         if a.gradient_accumulation_steps % generate_every != 0:
             out["old_per_token_logps"] = self._score_logps(self.model, out)
@@ -392,15 +396,16 @@ class GRPOTrainer:
         prompt of the batch appears exactly G >= 2 times (GRPO's generations of
         one prompt, in any shuffled order); None otherwise.  SWH_SHARED_PREFIX=0
         keeps the per-row forward."""
-        if os.environ.get("SWH_SHARED_PREFIX", "1") == "0":
+        if os.environ.get("SWH_SHARED_PREFIX", "1") == "0" or "prompt_group" not in batch:
             return None
-        pid, pm = batch["prompt_ids"], batch["prompt_mask"]
-        key = torch.cat([pid.to(torch.int64), pm.to(torch.int64)], 1)
-        _, inv, counts = torch.unique(key, dim=0, return_inverse=True, return_counts=True)
-        G = int(counts[0])
-        if G < 2 or not bool((counts == G).all()):
+        rows: dict = {}
+        for r, gid in enumerate(batch["prompt_group"].tolist()):  # one small device -> host copy
+            rows.setdefault(gid, []).append(r)
+        sizes = {len(v) for v in rows.values()}
+        if len(sizes) != 1 or sizes.pop() < 2:
             return None
-        return torch.sort(inv, stable=True).indices, G
+        order = [r for v in rows.values() for r in v]
+        return torch.tensor(order, device=batch["prompt_ids"].device), len(order) // len(rows)
 
     @torch.no_grad()
     def _score_logps(self, model: CausalLM, batch: dict) -> torch.Tensor:
@@ -427,6 +432,8 @@ class GRPOTrainer:
             "completion_mask": torch.cat([m["completion_mask"] for m in micro]),
             "advantages": torch.cat([m["advantages"] for m in micro]),
         }
+        if all("prompt_group" in m for m in micro):
+            batch["prompt_group"] = torch.cat([m["prompt_group"] for m in micro])
         for k in ("old_per_token_logps", "ref_per_token_logps"):
             if k in micro[0]:
                 batch[k] = torch.cat([m[k] for m in micro])
