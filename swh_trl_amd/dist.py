@@ -87,10 +87,11 @@ class OverlappedAllReduce:
 
     With one process this is a no-op; on gloo (CPU tests) it sums and divides."""
 
-    def __init__(self, flat: torch.Tensor, wait_streams=()):
+    def __init__(self, flat: torch.Tensor, wait_streams=(), force: bool = False):
         self.flat = flat
         self.wait_streams = list(wait_streams)  # producers of gradients beside the compute stream
-        self.active = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        # force: run the collectives even in a one-rank group (tests exercising RCCL on one GPU)
+        self.active = dist.is_available() and dist.is_initialized() and (dist.get_world_size() > 1 or force)
         self.world = dist.get_world_size() if self.active else 1
         self.nccl = self.active and dist.get_backend() == "nccl"
         self.stream = torch.cuda.Stream(device=flat.device) if (self.nccl and flat.is_cuda) else None

@@ -101,3 +101,56 @@ def test_bench_launches_n_ranks_itself():
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["ranks_seen"] == 2 and line["backend"] == "gloo"
     assert line["config"]["global_batch"] == 128 and line["value"] > 0
+
+
+def _rccl_worker(port, q):
+    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        import torch.distributed as dist
+        from swh_trl_amd import dist as swh_dist
+        rank, world, local = swh_dist.init_from_env("nccl")
+        if not dist.is_initialized():  # init_from_env leaves a one-process run alone
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", rank=0, world_size=1)
+        dev = torch.device("cuda", local)
+        g = torch.Generator(device=dev).manual_seed(0)
+        flat = torch.randn(3 << 20, generator=g, device=dev).to(torch.bfloat16)
+        ref = flat.clone()
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):  # a producer beside the compute stream, as the dW stream
+            flat[1 << 20:2 << 20].mul_(2)
+            ref[1 << 20:2 << 20].mul_(2)
+        ar = swh_dist.OverlappedAllReduce(flat, [side], force=True)
+        assert ar.nccl and ar.stream is not None
+        ar.release(2 << 20, 3 << 20)
+        ar.release(1 << 20, 2 << 20)
+        ar.finish()  # the remainder [0, 1M), then every collective joins the compute stream
+        torch.cuda.synchronize()
+        ok = bool(torch.equal(flat, ref))
+        rows = torch.arange(12, device=dev, dtype=torch.float32).view(4, 3)
+        out = torch.empty_like(rows)
+        dist.all_gather_into_tensor(out, rows)
+        swh_dist.barrier()
+        q.put(("ok", ok and bool(torch.equal(out, rows)), dist.get_backend()))
+    except Exception as e:
+        q.put(("err", repr(e), None))
+    finally:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_rccl_one_rank_overlapped_allreduce():
+    """The RCCL branch of OverlappedAllReduce on real hardware: a one-rank
+    "nccl" (RCCL) group, ranges released out of order behind a producer side
+    stream, the remainder in finish(), AVG over one rank = identity; plus
+    all_gather_into_tensor and the device barrier the launcher uses."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(32700 + os.getpid() % 500, q))
+    p.start()
+    status, ok, backend = q.get(timeout=240)
+    p.join(timeout=60)
+    assert status == "ok", ok
+    assert ok and backend == "nccl"
