@@ -416,6 +416,21 @@ int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t 
                     const void *bias, void *residual, int32_t silu, void *y, int64_t ldy, const float *ss_in,
                     float *ss_out, void *workspace, int64_t workspace_bytes, void *stream);
 
+/* Bandwidth-regime decode GEMM over a PACKED weight (Llama-3-8B decode at 64
+ * rows; replaces the same reference call sites as swh_decode_gemm — the policy
+ * forward inside unwrapped_model.generate(), trl/trainer/grpo_trainer.py:1114-1130).
+ * swh_wide_pack writes W (or the folded-norm weight bf16(W * norm_w)) in the
+ * MFMA-fragment order: each 16-row group's 128-k rounds are contiguous 4 KB
+ * runs.  swh_wide_gemm_packed then computes what swh_decode_gemm computes on
+ * the row-major weight with norm_w == NULL (bit-identical), for shapes
+ * swh_wide_gemm_eligible accepts (M <= 64, K % 128 == 0, N (2N with silu)
+ * % 128 == 0 and >= 1024); anything else is SWH_E_ARG. */
+int swh_wide_gemm_eligible(int64_t M, int64_t N, int64_t K, int32_t silu);
+int swh_wide_pack(const void *w, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, void *stream);
+int swh_wide_gemm_packed(const void *x, const void *w, int64_t M, int64_t N, int64_t K, float eps, const void *bias,
+                         void *residual, int32_t silu, void *y, int64_t ldy, const float *ss_in, float *ss_out,
+                         void *workspace, int64_t workspace_bytes, void *stream);
+
 /* Decode lm head with the sampler fused into its epilogue: RMSNorm(X) W^T
  * (as swh_decode_gemm with norm_w / ss_in) and, per row, the token that
  * swh_sample_step would draw from those logits with the same rng / step

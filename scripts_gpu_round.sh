@@ -31,6 +31,7 @@ for step in "$@"; do
     dwab) SWH_DW_SPLIT=0 run b_nosplit 600 python bench.py --steps 4 --warmup 2 --no-cpu-baseline && run b_split 600 python bench.py --steps 4 --warmup 2 --no-cpu-baseline ;;
     kern) run kern 600 python -m pytest tests/test_kernels_gpu.py -q -m gpu ;;
     kernx) run kernx 600 python -m pytest tests/test_kernels_gpu.py -q -m gpu -x ;;
+    pack) run pack 400 python -u -m pytest tests -v -m gpu --timeout 200 --timeout-method thread -k "wide_gemm or packed_wide or llama or recapture" && run l8d1 300 python tools/bench_llama8b_decode.py && SWH_WIDE_PACK=0 run l8d0 300 python tools/bench_llama8b_decode.py ;;
     decw) SWH_WIDE_KMIN=512 run decw 300 python tools/bench_decode.py ;;
     dec) run dec 300 python tools/bench_decode.py ;;
     ku) run ku 400 python tools/bench_decode.py --ku ;;

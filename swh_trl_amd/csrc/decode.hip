@@ -31,8 +31,10 @@ namespace swh {
 // csrc/wide_gemm.hip: 1 = shape not eligible, else a SWH status
 int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, float eps, const float *ss_in,
               const void *bias, void *residual, int32_t silu, void *y, int64_t ldy, float *ss_out, void *workspace,
-              int64_t workspace_bytes, int64_t counter_bytes, hipStream_t stream);
+              int64_t workspace_bytes, int64_t counter_bytes, int32_t packed, hipStream_t stream);
 int64_t wide_gemm_slab_bytes(int64_t M, int64_t N, int64_t K, int32_t silu);
+bool wide_gemm_eligible(int64_t M, int64_t N, int64_t K, int32_t silu);
+int wide_pack(const void *src, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, hipStream_t stream);
 
 namespace {
 
@@ -1274,23 +1276,17 @@ int attn_dispatch_gq(int gq, const uint16_t *q, uint16_t *kc, uint16_t *vc, cons
 }
 
 // ---- GEMM launch configuration -------------------------------------------
-// smallest K routed to csrc/wide_gemm.hip (SWH_WIDE_KMIN: A/B)
+// smallest K routed to csrc/wide_gemm.hip (SWH_WIDE_KMIN: A/B).  Read per call (host
+// side only, at graph capture in the decode loop) so it tracks the DecodeEngine's
+// choice of packed projections, which reads the same variable.
 int64_t wide_gemm_kmin() {
-    static int64_t k = -1;
-    if (k < 0) {
-        const char *e = getenv("SWH_WIDE_KMIN");
-        k = e ? atoll(e) : 2048;
-    }
-    return k;
+    const char *e = getenv("SWH_WIDE_KMIN");
+    return e ? atoll(e) : 2048;
 }
 // SWH_WIDE_GEMM=0 keeps every shape on decode_gemm (A/B of csrc/wide_gemm.hip)
 bool wide_gemm_enabled() {
-    static int on = -1;
-    if (on < 0) {
-        const char *e = getenv("SWH_WIDE_GEMM");
-        on = !(e && e[0] == '0');
-    }
-    return on != 0;
+    const char *e = getenv("SWH_WIDE_GEMM");
+    return !(e && e[0] == '0');
 }
 
 struct GemmCfg {
@@ -1556,7 +1552,7 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
     const int nm = norm_w ? 1 : (ss_in ? 2 : 0);
     if (nm != 1 && K >= wide_gemm_kmin() && wide_gemm_enabled()) {  // the bandwidth regime (8B decode): csrc/wide_gemm.hip
         const int st = wide_gemm(x, w, M, N, K, eps, ss_in, bias, residual, silu, y, ldy, ss_out, workspace,
-                                 workspace_bytes, kCounterBytes, s);
+                                 workspace_bytes, kCounterBytes, 0, s);
         if (st != 1) return st;
     }
     {  // many 16-column tiles and a K that fits the X image: the tile kernel (lm head, gate/up)
@@ -1674,6 +1670,42 @@ static int lm_head_sample_impl(const void *x, const void *w, int64_t M, int64_t 
     lm_sample_finalize_kernel<<<dim3((unsigned)M), 256, 0, s>>>(smp.part, smp.pstride, p, step, finished, out_tokens,
                                                                out_ld, cur_tokens, (int)V, nx);
     return launch_status();
+}
+
+// Packed-weight form of the bandwidth-regime decode GEMM (csrc/wide_gemm.hip): w is the
+// fragment order swh_wide_pack writes.  Same arguments and epilogues as swh_decode_gemm
+// with a folded (or no) norm; shapes wide_gemm does not serve are SWH_E_ARG (no fallback:
+// the packed weight has no row-major reading).
+extern "C" int swh_wide_gemm_packed(const void *x, const void *w, int64_t M, int64_t N, int64_t K, float eps,
+                                    const void *bias, void *residual, int32_t silu, void *y, int64_t ldy,
+                                    const float *ss_in, float *ss_out, void *workspace, int64_t workspace_bytes,
+                                    void *stream) {
+    if (!x || !w || !wide_gemm_eligible(M, N, K, silu)) return SWH_E_ARG;
+    if (residual && (silu || bias || ss_in)) return SWH_E_ARG;
+    if (!residual && !y) return SWH_E_ARG;
+    if (ss_out && !residual) return SWH_E_ARG;
+    if (ldy % 8 || ldy < N) return SWH_E_ARG;
+    const uintptr_t out_ptr = reinterpret_cast<uintptr_t>(residual ? residual : y);
+    if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w) | out_ptr) & 15) return SWH_E_ARG;
+    if ((bias && (reinterpret_cast<uintptr_t>(bias) & 15)) || (ss_in && (reinterpret_cast<uintptr_t>(ss_in) & 15)))
+        return SWH_E_ARG;
+    const int st = wide_gemm(x, w, M, N, K, eps, ss_in, bias, residual, silu, y, ldy, ss_out, workspace,
+                             workspace_bytes, kCounterBytes, 1, static_cast<hipStream_t>(stream));
+    return st == 1 ? SWH_E_ARG : st;
+}
+
+// 1 when swh_wide_gemm_packed serves [M rows] x [N (x2 with silu), K].
+extern "C" int swh_wide_gemm_eligible(int64_t M, int64_t N, int64_t K, int32_t silu) {
+    return wide_gemm_eligible(M, N, K, silu) ? 1 : 0;
+}
+
+extern "C" int swh_wide_pack(const void *w, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst,
+                             void *stream) {
+    if (!w || !dst || w == dst) return SWH_E_ARG;
+    if ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(dst) |
+         reinterpret_cast<uintptr_t>(norm_w)) & 15)
+        return SWH_E_ARG;
+    return wide_pack(w, norm_w, N, K, silu, dst, static_cast<hipStream_t>(stream));
 }
 
 extern "C" int swh_lm_head_sample(const void *x, const void *w, int64_t M, int64_t V, int64_t K, const void *norm_w,

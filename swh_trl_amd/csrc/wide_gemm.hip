@@ -25,8 +25,10 @@ namespace swh {
 
 int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, float eps, const float *ss_in,
               const void *bias, void *residual, int32_t silu, void *y, int64_t ldy, float *ss_out, void *workspace,
-              int64_t workspace_bytes, int64_t counter_bytes, hipStream_t stream);
+              int64_t workspace_bytes, int64_t counter_bytes, int32_t packed, hipStream_t stream);
 int64_t wide_gemm_slab_bytes(int64_t M, int64_t N, int64_t K, int32_t silu);
+bool wide_gemm_eligible(int64_t M, int64_t N, int64_t K, int32_t silu);
+int wide_pack(const void *src, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, hipStream_t stream);
 
 namespace {
 
@@ -63,12 +65,16 @@ __device__ __forceinline__ uint4 pack8w(const float *v) {
 }
 
 // NM: 0 = plain X, 2 = folded RMSNorm (rstd row scale from ss_in in the epilogue).
+// PACKED: the weight is in the fragment order wide_pack writes (below): a wave's
+// 16 rows x 128 k of a round are one contiguous 4 KB run and each load
+// instruction of the wave reads 1 KB of it, instead of 16 rows x 64 B 8 KB
+// (K x 2 B) apart; same k-slot mapping, so the results are bit-identical.
 // Plain register loads only (no LDS-DMA: hipcc drains vmcnt(0) at the use of
 // any register load while an LDS-DMA is in flight — cdna_hip_programming.md,
 // LDS-DMA notes), so the compiler's counted waits keep kWD - 1 rounds in
 // flight; one LDS array (a second __shared__ object makes hipcc wait before
 // LDS reads).
-template <int EPI, int NM, bool BIAS>
+template <int EPI, int NM, bool BIAS, bool PACKED>
 __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restrict__ x, const uint16_t *__restrict__ w,
                                                         int M, int N, int K, float eps, const float *__restrict__ ss_in,
                                                         const uint16_t *__restrict__ bias, uint16_t *__restrict__ res,
@@ -107,9 +113,18 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
             return cb * kWNB + t;
         }
     };
+    // weight element strides of a round and of a k-step in the two layouts
+    constexpr int kRS = PACKED ? 16 * kWKC : kWKC, kSS = PACKED ? 16 * 32 : 32;
     const uint16_t *wp[kWCB];
 #pragma unroll
-    for (int j = 0; j < kWCB; ++j) wp[j] = w + (int64_t)wrow_of(wid * 16 * kWCB + 16 * j + rl) * K + kbase + 8 * kg;
+    for (int j = 0; j < kWCB; ++j) {
+        if constexpr (PACKED) {
+            const int64_t bw = (int64_t)cb * (kWNB / 16) + wid * kWCB + j;  // 16-row group in tile order
+            wp[j] = w + (bw * nr_all + r0) * (16 * kWKC) + (kg * 16 + rl) * 8;
+        } else {
+            wp[j] = w + (int64_t)wrow_of(wid * 16 * kWCB + 16 * j + rl) * K + kbase + 8 * kg;
+        }
+    }
     const uint16_t *xp[kWXU];
 #pragma unroll
     for (int u = 0; u < kWXU; ++u) {
@@ -123,7 +138,7 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
         _Pragma("unroll") for (int u = 0; u < kWXU; ++u) xr[D][u] =                                            \
             *reinterpret_cast<const u32x4 *>(xp[u] + (q) * kWKC);                                               \
         _Pragma("unroll") for (int s = 0; s < kWKS; ++s) _Pragma("unroll") for (int j = 0; j < kWCB; ++j)       \
-            wr[D][s][j] = *reinterpret_cast<const uint4 *>(wp[j] + (q) * kWKC + 32 * s);                        \
+            wr[D][s][j] = *reinterpret_cast<const uint4 *>(wp[j] + (q) * kRS + kSS * s);                         \
         __builtin_amdgcn_sched_barrier(0); /* rounds issue in order: the counted waits rely on it */            \
     } while (0)
     f32x4w acc[4][kWCB];
@@ -317,19 +332,19 @@ int wide_split(int64_t N, int64_t K, int32_t silu) {
     return (int)s;
 }
 
-template <int EPI, int NM, bool BIAS>
+template <int EPI, int NM, bool BIAS, bool PACKED>
 int launch_wide(dim3 grid, hipStream_t st, const uint16_t *x, const uint16_t *w, int M, int N, int K, float eps,
                 const float *ss_in, const uint16_t *bias, uint16_t *res, float *ss_out, uint16_t *y, int ldy,
                 float *slabs, int *counters) {
     static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in once per kernel
     if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&wide_gemm_kernel<EPI, NM, BIAS>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&wide_gemm_kernel<EPI, NM, BIAS, PACKED>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kWLds) != hipSuccess)
             return SWH_E_LAUNCH;
         attr = true;
     }
-    wide_gemm_kernel<EPI, NM, BIAS><<<grid, kWT, kWLds, st>>>(x, w, M, N, K, eps, ss_in, bias, res, ss_out, y, ldy,
-                                                              slabs, counters);
+    wide_gemm_kernel<EPI, NM, BIAS, PACKED><<<grid, kWT, kWLds, st>>>(x, w, M, N, K, eps, ss_in, bias, res, ss_out, y,
+                                                                      ldy, slabs, counters);
     return launch_status();
 }
 
@@ -337,22 +352,45 @@ int launch_wide(dim3 grid, hipStream_t st, const uint16_t *x, const uint16_t *w,
 
 // Bytes of fp32 slabs the split-K reduction needs (0 when the shape is not eligible or S == 1).
 int64_t wide_gemm_slab_bytes(int64_t M, int64_t N, int64_t K, int32_t silu) {
-    if (M <= 0 || M > 64 || K % kWKC || (silu ? 2 * N : N) % kWNB || (silu ? 2 * N : N) < 1024) return 0;
+    if (!wide_gemm_eligible(M, N, K, silu)) return 0;
     const int64_t ncb = (silu ? 2 * N : N) / kWNB;
     const int s = wide_split(N, K, silu);
     return s > 1 ? ncb * s * 64 * kWNB * (int64_t)sizeof(float) : 0;
 }
 
-// 1 = not eligible (the caller uses decode_gemm), else a SWH status.
+// wide tiles only: a narrow output (Qwen2.5-0.5B down, N 896) stays on decode_gemm
+bool wide_gemm_eligible(int64_t M, int64_t N, int64_t K, int32_t silu) {
+    const int64_t wcols = silu ? 2 * N : N;
+    return M > 0 && M <= 64 && K % kWKC == 0 && K >= kWKC && wcols % kWNB == 0 && wcols >= 1024 && N % 16 == 0 &&
+           wcols / kWNB <= 65535 && K < (1 << 29);
+}
+
+template <bool P>
+int dispatch_wide(dim3 grid, hipStream_t st, const uint16_t *X, const uint16_t *W, int m, int n, int k, float eps,
+                  const float *ss_in, const uint16_t *B, uint16_t *R, float *ss_out, uint16_t *Y, int ld, float *slabs,
+                  int *ctr, bool silu) {
+    if (silu) {
+        if (ss_in) return launch_wide<WEPI_SILU, 2, false, P>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
+        return launch_wide<WEPI_SILU, 0, false, P>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
+    }
+    if (R) return launch_wide<WEPI_RESIDUAL, 0, false, P>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
+    if (B) {
+        if (ss_in) return launch_wide<WEPI_PLAIN, 2, true, P>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
+        return launch_wide<WEPI_PLAIN, 0, true, P>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
+    }
+    if (ss_in) return launch_wide<WEPI_PLAIN, 2, false, P>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
+    return launch_wide<WEPI_PLAIN, 0, false, P>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
+}
+
+// 1 = not eligible (the caller uses decode_gemm), else a SWH status.  packed: w is in
+// wide_pack's fragment order.
 int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, float eps, const float *ss_in,
               const void *bias, void *residual, int32_t silu, void *y, int64_t ldy, float *ss_out, void *workspace,
-              int64_t workspace_bytes, int64_t counter_bytes, hipStream_t st) {
-    const int64_t wcols = silu ? 2 * N : N;
-    // wide tiles only: a narrow output (Qwen2.5-0.5B down, N 896) stays on decode_gemm
-    if (M <= 0 || M > 64 || K % kWKC || K < kWKC || wcols % kWNB || wcols < 1024 || N % 16) return 1;
-    const int64_t ncb = wcols / kWNB;
+              int64_t workspace_bytes, int64_t counter_bytes, int32_t packed, hipStream_t st) {
+    if (!wide_gemm_eligible(M, N, K, silu)) return 1;
+    const int64_t ncb = (silu ? 2 * N : N) / kWNB;
     const int s = wide_split(N, K, silu);
-    if (ncb > 65535 || ncb * (int64_t)sizeof(int) > counter_bytes) return 1;
+    if (ncb * (int64_t)sizeof(int) > counter_bytes) return 1;
     float *slabs = nullptr;
     if (s > 1) {
         if (!workspace || workspace_bytes < counter_bytes + ncb * s * 64 * kWNB * (int64_t)sizeof(float)) return 1;
@@ -366,17 +404,54 @@ int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, flo
     auto *R = static_cast<uint16_t *>(residual);
     auto *Y = static_cast<uint16_t *>(y);
     const int m = (int)M, n = (int)N, k = (int)K, ld = (int)ldy;
-    if (silu) {
-        if (ss_in) return launch_wide<WEPI_SILU, 2, false>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
-        return launch_wide<WEPI_SILU, 0, false>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
+    if (packed) return dispatch_wide<true>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr, silu);
+    return dispatch_wide<false>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr, silu);
+}
+
+namespace {
+
+// Fragment order of a [wcols, K] weight (wcols = 2N with the SiLU pairing):
+//   dst[((((g * nr + q) * 4 + s) * 4 + kg) * 16 + rl) * 8 + e] = W'[row(16 g + rl)][128 q + 32 s + 8 kg + e]
+// g = 16-row group in tile order (SiLU tiles: lanes 0-7 gate rows, 8-15 the matching up
+// rows), q = 128-k round, s = k-step, (kg, rl) = the MFMA B-fragment lane.  W' = W, or the
+// folded RMSNorm weight bf16(W * w_norm) (swh_fold_norm's product) when norm_w is given.
+// One 16-B piece per thread, grid-stride; the stores are contiguous.
+__global__ __launch_bounds__(256) void wide_pack_kernel(const uint16_t *__restrict__ src,
+                                                        const uint16_t *__restrict__ nw, int64_t N, int64_t K,
+                                                        int silu, uint16_t *__restrict__ dst, int64_t npieces) {
+    const int64_t nr = K / kWKC;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npieces; p += (int64_t)gridDim.x * blockDim.x) {
+        const int rl = (int)(p & 15), kg = (int)((p >> 4) & 3), s = (int)((p >> 6) & 3);
+        const int64_t rest = p >> 8, q = rest % nr, g = rest / nr;
+        const int64_t t = g * 16 + rl;
+        const int64_t row = silu ? ((t & 15) < 8 ? (t >> 4) * 8 + (t & 7) : N + (t >> 4) * 8 + (t & 7)) : t;
+        const int64_t k0 = q * kWKC + 32 * s + 8 * kg;
+        uint4 v = *reinterpret_cast<const uint4 *>(src + row * K + k0);
+        if (nw) {
+            float a[8], b[8];
+            unpack16<SWH_BF16>(v, a);
+            unpack16<SWH_BF16>(*reinterpret_cast<const uint4 *>(nw + k0), b);
+            uint32_t o[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                o[c] = (uint32_t)f32_to_bf16_bits(a[2 * c] * b[2 * c]) |
+                       ((uint32_t)f32_to_bf16_bits(a[2 * c + 1] * b[2 * c + 1]) << 16);
+            v = uint4{o[0], o[1], o[2], o[3]};
+        }
+        *reinterpret_cast<uint4 *>(dst + p * 8) = v;
     }
-    if (residual) return launch_wide<WEPI_RESIDUAL, 0, false>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
-    if (B) {
-        if (ss_in) return launch_wide<WEPI_PLAIN, 2, true>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
-        return launch_wide<WEPI_PLAIN, 0, true>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
-    }
-    if (ss_in) return launch_wide<WEPI_PLAIN, 2, false>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
-    return launch_wide<WEPI_PLAIN, 0, false>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
+}
+
+}  // namespace
+
+int wide_pack(const void *src, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, hipStream_t st) {
+    if (!wide_gemm_eligible(1, N, K, silu)) return SWH_E_ARG;
+    const int64_t npieces = (silu ? 2 * N : N) * K / 8;
+    const int64_t grid = (npieces + 255) / 256 < 8192 ? (npieces + 255) / 256 : 8192;
+    wide_pack_kernel<<<dim3((unsigned)grid), 256, 0, st>>>(static_cast<const uint16_t *>(src),
+                                                             static_cast<const uint16_t *>(norm_w), N, K, silu,
+                                                             static_cast<uint16_t *>(dst), npieces);
+    return launch_status();
 }
 
 }  // namespace swh

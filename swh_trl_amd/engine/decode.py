@@ -101,6 +101,19 @@ class DecodeEngine:
                 self.fw[f"l{i}.qkv_w"] = torch.empty_like(model.p[f"l{i}.qkv_w"])
                 self.fw[f"l{i}.gu_w"] = torch.empty_like(model.p[f"l{i}.gu_w"])
             self.fw["lm"] = torch.empty_like(model.lm_weight())
+        # Bandwidth-regime projections (Llama-3-8B widths: K >= SWH_WIDE_KMIN, >= 1024 weight
+        # rows) read a copy of their weight in wide_gemm's fragment order (contiguous 4 KB
+        # runs per wave and round instead of 16 rows 64 B each, csrc/wide_gemm.hip), the
+        # folded norm applied while packing; SWH_WIDE_PACK=0 keeps the row-major weights
+        self.packed = {}
+        if self.fold and os.environ.get("SWH_WIDE_PACK", "1") != "0" and \
+                os.environ.get("SWH_WIDE_GEMM", "1") != "0":
+            kmin = int(os.environ.get("SWH_WIDE_KMIN", "2048"))
+            for name, (N, K, silu, _norm) in self._projections().items():
+                if K >= kmin and nn_ops.wide_gemm_eligible(B, N, K, silu):
+                    self.packed[name] = torch.empty(N * K * (2 if silu else 1), **bf)
+                    if name != "lm" or K > 1024:  # (the fused lm-head sampler, K <= 1024, reads fw["lm"])
+                        self.fw.pop(name, None)  # served by the packed copy only
         self.graph = None
         self.graph_k = None
         self._prefill_graphs = {}
@@ -139,40 +152,70 @@ class DecodeEngine:
         return (self.fused and not self.want_logp and os.environ.get("SWH_FUSED_SAMPLE", "1") != "0" and
                 nn_ops.lm_head_sample_supported(self.params, self.cfg.vocab_size, self.cfg.hidden_size))
 
+    def _projections(self) -> dict:
+        """name -> (N, K, silu, RMSNorm weight name or None) of the decode GEMMs."""
+        c = self.cfg
+        out = {}
+        for i in range(c.num_hidden_layers):
+            out[f"l{i}.qkv_w"] = (c.qkv_dim, c.hidden_size, False, f"l{i}.ln_in")
+            out[f"l{i}.o_w"] = (c.hidden_size, c.q_dim, False, None)
+            out[f"l{i}.gu_w"] = (c.intermediate_size, c.hidden_size, True, f"l{i}.ln_post")
+            out[f"l{i}.down_w"] = (c.hidden_size, c.intermediate_size, False, None)
+        out["lm"] = (c.vocab_size, c.hidden_size, False, "norm")
+        return out
+
+    def _weight(self, name: str) -> torch.Tensor:
+        return self.model.lm_weight() if name == "lm" else self.model.p[name]
+
     def _fold_jobs(self):
         """Device table of (W, w_norm, W') jobs for swh_fold_norm (built once)."""
         p = self.model.p
-        trip = []
-        for i in range(self.cfg.num_hidden_layers):
-            trip.append((p[f"l{i}.qkv_w"], p[f"l{i}.ln_in"], self.fw[f"l{i}.qkv_w"]))
-            trip.append((p[f"l{i}.gu_w"], p[f"l{i}.ln_post"], self.fw[f"l{i}.gu_w"]))
-        trip.append((self.model.lm_weight(), p["norm"], self.fw["lm"]))
+        projs = self._projections()
         rows, tab = 0, []
-        for w, nw, out in trip:
+        for name, out in self.fw.items():
+            w, nw = self._weight(name), p[projs[name][3]]
             tab += [w.data_ptr(), nw.data_ptr(), out.data_ptr(), w.shape[0], w.shape[1], rows]
             rows += w.shape[0]
-        self._fold_tab = torch.tensor(tab, dtype=torch.int64).to(self.dev)
+        self._fold_tab = torch.tensor(tab, dtype=torch.int64).to(self.dev) if tab else None
         self._fold_rows = rows
-        self._fold_n = len(trip)
+        self._fold_n = len(self.fw)
+        self._fold_built = True
 
     @torch.no_grad()
     def refresh_folded(self):
         """Re-derive the folded weights from the current parameters (once per
         generate(): the optimizer changes both W and the norm weights) — one
-        launch for all 2L + 1 matrices (swh_fold_norm)."""
+        launch for all row-major folded matrices (swh_fold_norm) and one
+        swh_wide_pack per packed projection."""
         if not self.fold:
             return
-        if getattr(self, "_fold_tab", None) is None:
+        if not getattr(self, "_fold_built", False):
             self._fold_jobs()
-        call("swh_fold_norm", self._fold_tab.data_ptr(), self._fold_n, self._fold_rows, ops._stream())
+        if self._fold_n:
+            call("swh_fold_norm", self._fold_tab.data_ptr(), self._fold_n, self._fold_rows, ops._stream())
+        projs = self._projections()
+        for name, buf in self.packed.items():
+            N, K, silu, norm = projs[name]
+            nn_ops.wide_pack(self._weight(name), self.model.p[norm] if norm else None, silu=silu, out=buf)
 
     def _normed(self, name: str, norm: str):
         """(weight, norm_w) of a normed projection: folded weight + row scale,
         or the raw weight + in-kernel RMSNorm."""
         if self.fold:
             return self.fw[name], None
-        w = self.model.lm_weight() if name == "lm" else self.model.p[name]
-        return w, self.model.p[norm]
+        return self._weight(name), self.model.p[norm]
+
+    def _proj(self, name: str, x: torch.Tensor, **kw):
+        """One decode projection: the packed wide GEMM, or decode_gemm on the
+        folded / raw weight (kw: bias, residual, silu, y, ss_in, ss_out)."""
+        eps = self.cfg.rms_norm_eps
+        if name in self.packed:
+            return nn_ops.wide_gemm_packed(x, self.packed[name], self._projections()[name][0], eps=eps, **kw)
+        norm = self._projections()[name][3]
+        if norm is None:
+            return nn_ops.decode_gemm(x, self._weight(name), eps=eps, **kw)
+        w, nw = self._normed(name, norm)
+        return nn_ops.decode_gemm(x, w, norm_w=nw, eps=eps, **kw)
 
     def _step_fused(self):
         c, m = self.cfg, self.model
@@ -182,22 +225,22 @@ class DecodeEngine:
         if not self._chained():
             nn_ops.embed_gather(p["embed"], self.cur, self.s, ss_out=ss)
         for i in range(c.num_hidden_layers):
-            w, nw = self._normed(f"l{i}.qkv_w", f"l{i}.ln_in")
-            nn_ops.decode_gemm(self.s, w, norm_w=nw, eps=eps, bias=p.get(f"l{i}.qkv_b"), y=self.qkv, ss_in=ss)
-            w, nw = self._normed(f"l{i}.gu_w", f"l{i}.ln_post")
+            self._proj(f"l{i}.qkv_w", self.s, bias=p.get(f"l{i}.qkv_b"), y=self.qkv, ss_in=ss)
+            pf = self._normed(f"l{i}.gu_w", f"l{i}.ln_post")[0] if self.prefetch and f"l{i}.gu_w" not in \
+                self.packed else None
             nn_ops.attn_decode(self.qkv, self.kv[i, 0], self.kv[i, 1], self.cos, self.sin, self.plen, self.state,
                                c.num_attention_heads, c.num_key_value_heads, c.head_dim, c.head_dim ** -0.5,
-                               out=self.att, prefetch_gate_up=w if self.prefetch else None)
-            nn_ops.decode_gemm(self.att, p[f"l{i}.o_w"], residual=self.s, ss_out=ss)
-            nn_ops.decode_gemm(self.s, w, norm_w=nw, eps=eps, silu=True, y=self.act, ss_in=ss)
-            nn_ops.decode_gemm(self.act, p[f"l{i}.down_w"], residual=self.s, ss_out=ss)
-        w, nw = self._normed("lm", "norm")
+                               out=self.att, prefetch_gate_up=pf)
+            self._proj(f"l{i}.o_w", self.att, residual=self.s, ss_out=ss)
+            self._proj(f"l{i}.gu_w", self.s, silu=True, y=self.act, ss_in=ss)
+            self._proj(f"l{i}.down_w", self.act, residual=self.s, ss_out=ss)
         if self._fused_sample():
+            w, nw = self._normed("lm", "norm")
             nn_ops.lm_head_sample_step(self.s, w, self.params, self.rng, self.state[0:1], self.finished,
                                        self.out, self.cur, p["embed"], self.s, ss, norm_w=nw, eps=eps, ss_in=ss,
                                        workspace=self.sample_ws)
         else:
-            nn_ops.decode_gemm(self.s, w, norm_w=nw, eps=eps, y=self.logits_buf, ss_in=ss)
+            self._proj("lm", self.s, y=self.logits_buf, ss_in=ss)
 
     def _step_unfused(self):
         c, m = self.cfg, self.model
@@ -245,6 +288,10 @@ class DecodeEngine:
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             kv_saved = self.kv.clone()
+            # a step index inside the buffers: after a finished generation the step
+            # counter sits at max_new_tokens, one column past out / out_logp (whose
+            # last row would then write past the allocation into its neighbour)
+            self.state[0] = 1
             self._step()
         torch.cuda.current_stream().wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
@@ -297,30 +344,24 @@ class DecodeEngine:
         # weights per step streams from HBM; one layer's alone would sit in the
         # 256 MiB Infinity Cache and time optimistically)
         ops_ = {
-            "decode_gemm.qkv": (lambda i: nn_ops.decode_gemm(self.s, self._normed(f"l{i}.qkv_w", f"l{i}.ln_in")[0],
-                                                             norm_w=self._normed(f"l{i}.qkv_w", f"l{i}.ln_in")[1],
-                                                             eps=eps, bias=p.get(f"l{i}.qkv_b"), y=self.qkv,
-                                                             ss_in=ss),
+            "decode_gemm.qkv": (lambda i: self._proj(f"l{i}.qkv_w", self.s, bias=p.get(f"l{i}.qkv_b"), y=self.qkv,
+                                                     ss_in=ss),
                                 gemm_bytes(c.qkv_dim, H), L),
             "attn_decode": (lambda i: nn_ops.attn_decode(self.qkv, self.kv[i, 0], self.kv[i, 1], self.cos, self.sin,
                                                          self.plen, self.state, c.num_attention_heads,
                                                          c.num_key_value_heads, c.head_dim, c.head_dim ** -0.5,
                                                          out=self.att,
                                                          prefetch_gate_up=self._normed(f"l{i}.gu_w", "")[0]
-                                                         if self.prefetch else None),
+                                                         if self.prefetch and f"l{i}.gu_w" not in self.packed
+                                                         else None),
                             att_bytes, L),
-            "decode_gemm.o": (lambda i: nn_ops.decode_gemm(self.att, p[f"l{i}.o_w"], residual=self.s, ss_out=ss),
+            "decode_gemm.o": (lambda i: self._proj(f"l{i}.o_w", self.att, residual=self.s, ss_out=ss),
                               gemm_bytes(H, c.q_dim), L),
-            "decode_gemm.gate_up": (lambda i: nn_ops.decode_gemm(self.s, self._normed(f"l{i}.gu_w", f"l{i}.ln_post")[0],
-                                                                 norm_w=self._normed(f"l{i}.gu_w", f"l{i}.ln_post")[1],
-                                                                 eps=eps, silu=True, y=self.act, ss_in=ss),
+            "decode_gemm.gate_up": (lambda i: self._proj(f"l{i}.gu_w", self.s, silu=True, y=self.act, ss_in=ss),
                                     gemm_bytes(I, H, silu=True), L),
-            "decode_gemm.down": (lambda i: nn_ops.decode_gemm(self.act, p[f"l{i}.down_w"], residual=self.s,
-                                                              ss_out=ss),
+            "decode_gemm.down": (lambda i: self._proj(f"l{i}.down_w", self.act, residual=self.s, ss_out=ss),
                                  gemm_bytes(H, I), L),
-            "decode_gemm.lm_head": (lambda i: nn_ops.decode_gemm(self.s, self._normed("lm", "norm")[0],
-                                                                 norm_w=self._normed("lm", "norm")[1], eps=eps,
-                                                                 y=self.logits_buf, ss_in=ss),
+            "decode_gemm.lm_head": (lambda i: self._proj("lm", self.s, y=self.logits_buf, ss_in=ss),
                                     c.vocab_size * H * bf + B * c.vocab_size * bf, 1),
             "sample_step": (lambda i: self._sample(), B * c.vocab_size * bf, 1),
         }

@@ -157,6 +157,44 @@ def decode_gemm(x: torch.Tensor, w: torch.Tensor, *, norm_w: Optional[torch.Tens
     return residual if residual is not None else y
 
 
+def wide_gemm_eligible(M: int, N: int, K: int, silu: bool = False) -> bool:
+    """Shapes swh_wide_gemm_packed serves (include/swh_trl_amd.h)."""
+    return bool(_lib.load().swh_wide_gemm_eligible(M, N, K, int(bool(silu))))
+
+
+def wide_pack(w: torch.Tensor, norm_w: Optional[torch.Tensor] = None, *, silu: bool = False,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """w [N, K] (or [2N, K] gate|up with silu) in swh_wide_gemm_packed's
+    fragment order, optionally folded with the RMSNorm weight (swh_wide_pack).
+    Returns a flat bf16 tensor of w.numel() elements."""
+    _dev(w, "wide_pack")
+    rows, K = w.shape
+    N = rows // 2 if silu else rows
+    if out is None:
+        out = torch.empty(w.numel(), device=w.device, dtype=w.dtype)
+    call("swh_wide_pack", w.data_ptr(), _p(norm_w), N, K, int(bool(silu)), out.data_ptr(), _stream())
+    return out
+
+
+def wide_gemm_packed(x: torch.Tensor, w_packed: torch.Tensor, N: int, *, eps: float = 1e-6,
+                     bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None, silu: bool = False,
+                     y: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
+                     ss_in: Optional[torch.Tensor] = None, ss_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """decode_gemm over a wide_pack'ed weight (include/swh_trl_amd.h
+    swh_wide_gemm_packed); N output columns."""
+    _dev(x, "wide_gemm_packed")
+    M, K = x.shape
+    if w_packed.numel() != (2 if silu else 1) * N * K:
+        raise ValueError("wide_gemm_packed: packed weight size does not match N, K")
+    if residual is None and y is None:
+        y = torch.empty(M, N, device=x.device, dtype=x.dtype)
+    ldy = residual.stride(0) if residual is not None else y.stride(0)
+    ws = workspace if workspace is not None else gemm_workspace(x.device)
+    call("swh_wide_gemm_packed", x.data_ptr(), w_packed.data_ptr(), M, N, K, float(eps), _p(bias), _p(residual),
+         int(bool(silu)), _p(y), ldy, _p(ss_in), _p(ss_out), ws.data_ptr(), ws.numel(), _stream())
+    return residual if residual is not None else y
+
+
 def lm_head_sample_supported(params, V: int, K: int) -> bool:
     """The fused lm-head sampler covers unfiltered sampling (temperature,
     greedy, EOS suppression); the rest goes through logits + sample_step."""

@@ -599,3 +599,59 @@ def test_shared_prompt_forward_matches_per_row(dev, dtype, left_pad):
         tol = 3e-2
     rel = ((g2 - g1).norm() / g1.norm()).item()
     assert rel <= tol, rel
+
+
+@pytest.mark.parametrize("kmin", ["2048", "1024"])
+def test_packed_wide_projections_generate_identically(dev, monkeypatch, kmin):
+    """DecodeEngine with the bandwidth-regime projections on packed weights
+    (swh_wide_pack + swh_wide_gemm_packed; SWH_WIDE_KMIN 2048 packs down,
+    1024 packs every projection and the lm head) generates the same tokens and
+    log-probs as the row-major weights (SWH_WIDE_PACK=0), greedy and sampled."""
+    from swh_trl_amd.engine import DecodeEngine
+    m = _tiny_llama(dev, seed=5)
+    g = torch.Generator().manual_seed(5)
+    B, P, C = 16, 12, 24
+    ids = torch.randint(0, m.cfg.vocab_size, (B, P), generator=g).to(dev)
+    mask = torch.ones(B, P, dtype=torch.int64, device=dev)
+    mask[3, :4] = 0
+    monkeypatch.setenv("SWH_WIDE_KMIN", kmin)
+    outs = {}
+    for pack in ("1", "0"):
+        monkeypatch.setenv("SWH_WIDE_PACK", pack)
+        eng = DecodeEngine(m, B, P, C)
+        if pack == "1":
+            assert "l0.down_w" in eng.packed and (kmin == "2048") == ("l0.qkv_w" not in eng.packed)
+        else:
+            assert not eng.packed
+        greedy = eng.generate(ids, mask, C, greedy=True)
+        sampled = eng.generate(ids, mask, C, temperature=0.9, seed=11)
+        with_logp = eng.generate(ids, mask, C, temperature=0.9, seed=12, return_logp=True)
+        outs[pack] = (greedy, sampled, with_logp)
+        del eng
+    monkeypatch.delenv("SWH_WIDE_KMIN")
+    for a, b in zip(outs["1"], outs["0"]):
+        for x, y in zip(a, b):
+            if isinstance(x, torch.Tensor):
+                assert torch.equal(x, y)
+
+
+def test_graph_recapture_after_generation_is_clean(dev):
+    """Regression: a generation whose sampling parameters differ from the
+    previous one's recaptures the decode graph; its warm-up step must run at a
+    step index inside the output buffers (it ran at max_new_tokens, writing
+    past out_logp's last row into the prompt-length buffer: NaN log-probs for
+    row 0).  Fused-sampler run, then a log-prob run, equals a fresh engine."""
+    from swh_trl_amd.engine import DecodeEngine
+    m = _tiny_llama(dev, seed=5)
+    g = torch.Generator().manual_seed(5)
+    B, P, C = 16, 12, 24
+    ids = torch.randint(0, m.cfg.vocab_size, (B, P), generator=g).to(dev)
+    mask = torch.ones(B, P, dtype=torch.int64, device=dev)
+    mask[3, :4] = 0
+    eng = DecodeEngine(m, B, P, C)
+    eng.generate(ids, mask, C, greedy=True)
+    out, lp = eng.generate(ids, mask, C, temperature=0.9, seed=12, return_logp=True)
+    fresh = DecodeEngine(m, B, P, C)
+    out2, lp2 = fresh.generate(ids, mask, C, temperature=0.9, seed=12, return_logp=True)
+    assert not torch.isnan(lp).any()
+    assert torch.equal(out, out2) and torch.equal(lp, lp2)

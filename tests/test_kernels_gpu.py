@@ -1201,3 +1201,63 @@ def test_wide_gemm_bandwidth_regime(ops, dev, name, M, N, K):
     ref = (x.float() @ w.float().t()) * rstd + (b.float() if b is not None else 0.0)
     torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=2e-2)
     assert torch.equal(y, nn_ops.decode_gemm(x, w, ss_in=ss, eps=1e-5, bias=b))
+
+
+def _wide_pack_ref(w, nw, silu):
+    """Fragment order of swh_wide_pack restated in torch: tile row T -> weight
+    row (SiLU: 8 gate rows then the 8 matching up rows per 16-row group), then
+    [group, round, k-step, lane group, lane row, 8 elements]."""
+    rows, K = w.shape
+    wf = (w * nw) if nw is not None else w  # torch's bf16 mul: one rounding of the fp32 product
+    if silu:
+        N = rows // 2
+        T = torch.arange(rows, device=w.device)
+        base = (T >> 4) * 8 + (T & 7)
+        wf = wf[torch.where((T & 15) < 8, base, N + base)]
+    return wf.view(rows // 16, 16, K // 128, 4, 4, 8).permute(0, 2, 3, 4, 1, 5).reshape(-1)
+
+
+@pytest.mark.parametrize("name,M,N,K", [("qkv_bias", 64, 6144, 4096), ("o_res", 64, 4096, 4096),
+                                        ("gate_up", 64, 14336, 4096), ("down", 37, 4096, 14336),
+                                        ("lm_head", 64, 128256, 4096), ("small", 5, 1024, 2048)])
+def test_wide_gemm_packed_equals_row_major(ops, dev, name, M, N, K):
+    """swh_wide_pack writes the fragment order (checked element for element
+    against a torch restatement, with the folded norm), and
+    swh_wide_gemm_packed over it equals the row-major wide GEMM on the folded
+    weight bit for bit (same k order, same split-K reduction order)."""
+    from swh_trl_amd import nn_ops
+    g = _gen(36)
+    silu = name == "gate_up"
+    normed = name in ("qkv_bias", "gate_up", "lm_head", "small")
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
+    ss = x.float().view(M, K // 16, 16).pow(2).sum(-1).contiguous()
+    w = (torch.randn(2 * N if silu else N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(dev)
+    nw = (1.0 + 0.1 * torch.randn(K, generator=g)).to(torch.bfloat16).to(dev) if normed else None
+    assert nn_ops.wide_gemm_eligible(M, N, K, silu)
+    wp = nn_ops.wide_pack(w, nw, silu=silu)
+    assert torch.equal(wp, _wide_pack_ref(w, nw, silu))
+    wf = w * nw if normed else w
+    if name.startswith(("o_", "down")):
+        s0 = torch.randn(M, N, generator=g).to(torch.bfloat16).to(dev)
+        s1, s2 = s0.clone(), s0.clone()
+        so1, so2 = torch.empty(M, N // 16, device=dev), torch.empty(M, N // 16, device=dev)
+        nn_ops.decode_gemm(x, wf, residual=s1, ss_out=so1)
+        nn_ops.wide_gemm_packed(x, wp, N, residual=s2, ss_out=so2)
+        assert torch.equal(s1, s2) and torch.equal(so1, so2)
+        return
+    b = (0.1 * torch.randn(N, generator=g)).to(torch.bfloat16).to(dev) if name == "qkv_bias" else None
+    y1 = nn_ops.decode_gemm(x, wf, silu=silu, ss_in=ss, eps=1e-5, bias=b)
+    y2 = nn_ops.wide_gemm_packed(x, wp, N, silu=silu, ss_in=ss, eps=1e-5, bias=b)
+    assert torch.equal(y1, y2)
+
+
+def test_wide_gemm_packed_rejects_ineligible(ops, dev):
+    """No row-major fallback behind the packed entry: shapes wide_gemm does
+    not serve are argument errors."""
+    from swh_trl_amd import nn_ops
+    assert not nn_ops.wide_gemm_eligible(64, 896, 4864)       # narrow output (0.5B down)
+    assert not nn_ops.wide_gemm_eligible(65, 4096, 4096)      # more than 64 rows
+    x = torch.zeros(65, 4096, dtype=torch.bfloat16, device=dev)
+    wp = torch.zeros(4096 * 4096, dtype=torch.bfloat16, device=dev)
+    with pytest.raises(ValueError):
+        nn_ops.wide_gemm_packed(x, wp, 4096)
