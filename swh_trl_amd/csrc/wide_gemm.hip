@@ -37,17 +37,25 @@ typedef float f32x4w __attribute__((ext_vector_type(4)));
 
 constexpr int kWW = 8;                 // waves per workgroup
 constexpr int kWT = 64 * kWW;          // threads
-constexpr int kWCB = 1;                // 16-column blocks per wave
-constexpr int kWNB = 16 * kWCB * kWW;  // weight rows (tile columns) per workgroup: 128
 constexpr int kWKS = 4;                // k-steps (of 32) per round
 constexpr int kWKC = 32 * kWKS;        // k per round: 128 (256-B rows of 16 pieces)
-constexpr int kWD = 7;                 // rounds in flight (register ring depth: 24 VGPRs per round)
 constexpr int kWXB = 64 * kWKC * 2;    // X bytes of a round (16 KB)
 constexpr int kWXU = kWXB / 16 / kWT;  // X pieces per thread per round (2)
-constexpr int kWLdt = kWNB + 4;        // epilogue tile row stride (f32)
-constexpr int kWAux = 64 * kWLdt * 4;  // the epilogue tile (the two X slots live inside it), then rstd + flag
-constexpr int kWLds = kWAux + 64 * 4 + 16;
-static_assert(2 * kWXB <= kWAux, "the two X slots must fit under the epilogue tile");
+
+// Geometry per CB = 16-row weight groups per wave: a workgroup owns NB = 128 CB weight
+// rows.  CB 2 halves the X bytes every workgroup ingests per weight byte (the wide-N
+// shapes: Llama-3-8B gate/up and lm head); its ring is 4 rounds deep (VGPR budget:
+// 40 registers per round against 24).
+template <int CB>
+struct WGeo {
+    static constexpr int NB = 16 * CB * kWW;
+    static constexpr int D = CB == 1 ? 7 : 4;  // rounds in flight (register ring depth)
+    static constexpr int LDT = NB + 4;         // epilogue tile row stride (f32)
+    static constexpr int AUX = 64 * LDT * 4;   // the epilogue tile (the two X slots live inside it), then rstd + flag
+    static constexpr int LDS = AUX + 64 * 4 + 16;
+    static_assert(2 * kWXB <= AUX, "the two X slots must fit under the epilogue tile");
+};
+constexpr int kWNB = WGeo<1>::NB;      // the narrowest tile: eligibility and the packed layout's 16-row groups
 
 enum : int { WEPI_PLAIN = 0, WEPI_RESIDUAL = 1, WEPI_SILU = 2 };
 
@@ -74,15 +82,16 @@ __device__ __forceinline__ uint4 pack8w(const float *v) {
 // LDS-DMA notes), so the compiler's counted waits keep kWD - 1 rounds in
 // flight; one LDS array (a second __shared__ object makes hipcc wait before
 // LDS reads).
-template <int EPI, int NM, bool BIAS, bool PACKED>
+template <int EPI, int NM, bool BIAS, bool PACKED, int CB>
 __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restrict__ x, const uint16_t *__restrict__ w,
                                                         int M, int N, int K, float eps, const float *__restrict__ ss_in,
                                                         const uint16_t *__restrict__ bias, uint16_t *__restrict__ res,
                                                         float *__restrict__ ss_out, uint16_t *__restrict__ y, int ldy,
                                                         float *__restrict__ slabs, int *__restrict__ counters) {
+    constexpr int NB = WGeo<CB>::NB, WD = WGeo<CB>::D, LDT = WGeo<CB>::LDT, AUX = WGeo<CB>::AUX;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    float *rstd_s = reinterpret_cast<float *>(lds + kWAux);
-    int *flag_s = reinterpret_cast<int *>(lds + kWAux + 64 * 4);
+    float *rstd_s = reinterpret_cast<float *>(lds + AUX);
+    int *flag_s = reinterpret_cast<int *>(lds + AUX + 64 * 4);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, rl = lane & 15, kg = lane >> 4;
     const int S = gridDim.y, sidx = blockIdx.y, cb = blockIdx.x;
     const int nr_all = K / kWKC;
@@ -100,29 +109,29 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
         if (sub == 0) rstd_s[tid >> 2] = rsqrtf(v / (float)K + eps);
     }
 
-    // ---- operands: a register ring kWD rounds deep per thread (X pieces + this wave's weight
+    // ---- operands: a register ring WD rounds deep per thread (X pieces + this wave's weight
     // fragments; plain loads, so hipcc counts vmcnt per round), X then copied into one of two
     // LDS slots per round.  LDS piece (row, p) holds X piece (row, p ^ (row & 15)): the 16 rows
     // an MFMA fragment reads sit in distinct banks.  Tile row t -> weight row: wave t / 16,
     // lane t % 16; SiLU tiles pair gate rows (lanes 0-7) with the matching up rows (lanes 8-15).
     auto wrow_of = [&](int t) -> int {
         if constexpr (EPI == WEPI_SILU) {
-            const int oc = cb * (kWNB / 2) + (t >> 4) * 8 + (t & 7);
+            const int oc = cb * (NB / 2) + (t >> 4) * 8 + (t & 7);
             return (t & 15) < 8 ? oc : N + oc;
         } else {
-            return cb * kWNB + t;
+            return cb * NB + t;
         }
     };
     // weight element strides of a round and of a k-step in the two layouts
     constexpr int kRS = PACKED ? 16 * kWKC : kWKC, kSS = PACKED ? 16 * 32 : 32;
-    const uint16_t *wp[kWCB];
+    const uint16_t *wp[CB];
 #pragma unroll
-    for (int j = 0; j < kWCB; ++j) {
+    for (int j = 0; j < CB; ++j) {
         if constexpr (PACKED) {
-            const int64_t bw = (int64_t)cb * (kWNB / 16) + wid * kWCB + j;  // 16-row group in tile order
+            const int64_t bw = (int64_t)cb * (NB / 16) + wid * CB + j;  // 16-row group in tile order
             wp[j] = w + (bw * nr_all + r0) * (16 * kWKC) + (kg * 16 + rl) * 8;
         } else {
-            wp[j] = w + (int64_t)wrow_of(wid * 16 * kWCB + 16 * j + rl) * K + kbase + 8 * kg;
+            wp[j] = w + (int64_t)wrow_of(wid * 16 * CB + 16 * j + rl) * K + kbase + 8 * kg;
         }
     }
     const uint16_t *xp[kWXU];
@@ -131,23 +140,23 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
         const int id = tid + kWT * u, row = id >> 4;
         xp[u] = x + (int64_t)min(row, M - 1) * K + kbase + (id & 15) * 8;
     }
-    u32x4 xr[kWD][kWXU];  // vector type, not the uint4 struct: an aggregate copy kept the ring in scratch
-    uint4 wr[kWD][kWKS][kWCB];
+    u32x4 xr[WD][kWXU];  // vector type, not the uint4 struct: an aggregate copy kept the ring in scratch
+    uint4 wr[WD][kWKS][CB];
 #define SWH_WIDE_ISSUE(q, D)                                                                                    \
     do {                                                                                                        \
         _Pragma("unroll") for (int u = 0; u < kWXU; ++u) xr[D][u] =                                            \
             *reinterpret_cast<const u32x4 *>(xp[u] + (q) * kWKC);                                               \
-        _Pragma("unroll") for (int s = 0; s < kWKS; ++s) _Pragma("unroll") for (int j = 0; j < kWCB; ++j)       \
+        _Pragma("unroll") for (int s = 0; s < kWKS; ++s) _Pragma("unroll") for (int j = 0; j < CB; ++j)       \
             wr[D][s][j] = *reinterpret_cast<const uint4 *>(wp[j] + (q) * kRS + kSS * s);                         \
         __builtin_amdgcn_sched_barrier(0); /* rounds issue in order: the counted waits rely on it */            \
     } while (0)
-    f32x4w acc[4][kWCB];
+    f32x4w acc[4][CB];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < kWCB; ++j) acc[i][j] = f32x4w{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < CB; ++j) acc[i][j] = f32x4w{0.f, 0.f, 0.f, 0.f};
     // one round: X(r) into LDS slot r & 1, barrier, 4 k-steps x 4 row blocks of MFMAs, refill
-    // the registers round r used with round r + kWD
+    // the registers round r used with round r + WD
 #define SWH_WIDE_ROUND(r, D, REFILL)                                                                            \
     do {                                                                                                        \
         unsigned char *xs = lds + ((r) & 1) * kWXB;                                                             \
@@ -160,33 +169,33 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
             uint4 a[4];                                                                                         \
             _Pragma("unroll") for (int i = 0; i < 4; ++i) a[i] =                                                \
                 *reinterpret_cast<const uint4 *>(xs + (16 * i + rl) * (kWKC * 2) + (((4 * s + kg) ^ rl) * 16));  \
-            _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < kWCB; ++j)      \
+            _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < CB; ++j)      \
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf8(a[i]), as_bf8(wr[D][s][j]),          \
                                                                     acc[i][j], 0, 0, 0);                         \
         }                                                                                                       \
         __builtin_amdgcn_sched_barrier(0);                                                                      \
-        if (REFILL) SWH_WIDE_ISSUE((r) + kWD, D);                                                               \
+        if (REFILL) SWH_WIDE_ISSUE((r) + WD, D);                                                               \
     } while (0)
     int rb = 0;
-    if (nr >= 2 * kWD) {
+    if (nr >= 2 * WD) {
         // unconditional prologue and steady state: every refill is in range, so hipcc's counted
-        // waits see one fixed pattern at the loop header (kWD - 1 rounds stay in flight)
+        // waits see one fixed pattern at the loop header (WD - 1 rounds stay in flight)
 #pragma unroll
-        for (int d = 0; d < kWD; ++d) SWH_WIDE_ISSUE(d, d);
-        for (; rb + 2 * kWD <= nr; rb += kWD) {
+        for (int d = 0; d < WD; ++d) SWH_WIDE_ISSUE(d, d);
+        for (; rb + 2 * WD <= nr; rb += WD) {
 #pragma unroll
-            for (int d = 0; d < kWD; ++d) SWH_WIDE_ROUND(rb + d, d, true);
+            for (int d = 0; d < WD; ++d) SWH_WIDE_ROUND(rb + d, d, true);
         }
     } else {
 #pragma unroll
-        for (int d = 0; d < kWD; ++d)
+        for (int d = 0; d < WD; ++d)
             if (d < nr) SWH_WIDE_ISSUE(d, d);
     }
-    // tail: the last kWD .. 2 kWD - 1 rounds (or all of them when nr < 2 kWD)
+    // tail: the last WD .. 2 WD - 1 rounds (or all of them when nr < 2 WD)
 #pragma unroll
-    for (int d = 0; d < 2 * kWD; ++d) {
+    for (int d = 0; d < 2 * WD; ++d) {
         const int r = rb + d;
-        if (r < nr) SWH_WIDE_ROUND(r, d % kWD, r + kWD < nr);
+        if (r < nr) SWH_WIDE_ROUND(r, d % WD, r + WD < nr);
     }
 #undef SWH_WIDE_ROUND
     wide_lds_barrier();  // every wave is past its last X read: the slots become the epilogue tile
@@ -197,9 +206,9 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < kWCB; ++j)
+        for (int j = 0; j < CB; ++j)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) tile[(16 * i + 4 * kg + e) * kWLdt + wid * 16 * kWCB + 16 * j + rl] = acc[i][j][e];
+            for (int e = 0; e < 4; ++e) tile[(16 * i + 4 * kg + e) * LDT + wid * 16 * CB + 16 * j + rl] = acc[i][j][e];
     __syncthreads();
 
     // ---- split K (the in-launch slab hand-off of cdna_hip_programming.md, projection GEMMs item 2,
@@ -207,11 +216,11 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
     // ticket; the last arriver acquires once and sums the S slabs with plain 16-B loads in fixed
     // order (deterministic for any placement of the S workgroups over the XCDs)
     if (S > 1) {
-        float *my = slabs + ((int64_t)cb * S + sidx) * (64 * kWNB);
-        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(my, 0, 64 * kWNB * 4, 0x00020000);
-        for (int idx = tid; idx < 64 * kWNB / 4; idx += kWT) {
-            const int r = idx / (kWNB / 4), c4 = idx % (kWNB / 4);
-            const float4 v = *reinterpret_cast<const float4 *>(tile + r * kWLdt + 4 * c4);
+        float *my = slabs + ((int64_t)cb * S + sidx) * (64 * NB);
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(my, 0, 64 * NB * 4, 0x00020000);
+        for (int idx = tid; idx < 64 * NB / 4; idx += kWT) {
+            const int r = idx / (NB / 4), c4 = idx % (NB / 4);
+            const float4 v = *reinterpret_cast<const float4 *>(tile + r * LDT + 4 * c4);
             __builtin_amdgcn_raw_buffer_store_b128(
                 u32x4{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)}, rsrc,
                 idx * 16, 0, 16 /* sc1: write-through */);
@@ -228,15 +237,15 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
         }
         __syncthreads();
         if (!*flag_s) return;
-        const float4 *base = reinterpret_cast<const float4 *>(slabs + (int64_t)cb * S * (64 * kWNB));
-        for (int idx = tid; idx < 64 * kWNB / 4; idx += kWT) {
+        const float4 *base = reinterpret_cast<const float4 *>(slabs + (int64_t)cb * S * (64 * NB));
+        for (int idx = tid; idx < 64 * NB / 4; idx += kWT) {
             float4 v[8];
             float4 sum = float4{0.f, 0.f, 0.f, 0.f};
             for (int q0 = 0; q0 < S; q0 += 8) {  // up to eight slab loads in flight per thread
                 const int nq = min(8, S - q0);
 #pragma unroll
                 for (int q = 0; q < 8; ++q)
-                    if (q < nq) v[q] = base[(int64_t)(q0 + q) * (64 * kWNB / 4) + idx];
+                    if (q < nq) v[q] = base[(int64_t)(q0 + q) * (64 * NB / 4) + idx];
 #pragma unroll
                 for (int q = 0; q < 8; ++q)
                     if (q < nq) {
@@ -246,8 +255,8 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
                         sum.w += v[q].w;
                     }
             }
-            const int r = idx / (kWNB / 4), c4 = idx % (kWNB / 4);
-            *reinterpret_cast<float4 *>(tile + r * kWLdt + 4 * c4) = sum;
+            const int r = idx / (NB / 4), c4 = idx % (NB / 4);
+            *reinterpret_cast<float4 *>(tile + r * LDT + 4 * c4) = sum;
         }
         if (tid == 0) __hip_atomic_store(counters + cb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
@@ -256,25 +265,25 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
     // ---- epilogue
     if constexpr (EPI == WEPI_SILU) {
         // 64 rows x 8 groups of 8 output columns: tile columns 16 g + c (gate) and 16 g + 8 + c (up)
-        for (int idx = tid; idx < 64 * 8; idx += kWT) {
-            const int r = idx >> 3, g = idx & 7;
+        for (int idx = tid; idx < 64 * (NB / 16); idx += kWT) {
+            const int r = idx / (NB / 16), g = idx % (NB / 16);
             if (r >= M) continue;
             const float sc = NM == 2 ? rstd_s[r] : 1.f;
             float o[8];
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
-                const float gv = round_bf16(tile[r * kWLdt + 16 * g + c] * sc);
-                const float uv = round_bf16(tile[r * kWLdt + 16 * g + 8 + c] * sc);
+                const float gv = round_bf16(tile[r * LDT + 16 * g + c] * sc);
+                const float uv = round_bf16(tile[r * LDT + 16 * g + 8 + c] * sc);
                 o[c] = round_bf16(gv / (1.f + expf(-gv))) * uv;
             }
-            *reinterpret_cast<uint4 *>(y + (int64_t)r * ldy + cb * (kWNB / 2) + 8 * g) = pack8w(o);
+            *reinterpret_cast<uint4 *>(y + (int64_t)r * ldy + cb * (NB / 2) + 8 * g) = pack8w(o);
         }
     } else if constexpr (EPI == WEPI_RESIDUAL) {
         // 64 rows x 8 chunks of 16 columns: s = bf16(s + bf16(acc)), chunk sum of squares of the new s
-        for (int idx = tid; idx < 64 * 8; idx += kWT) {
-            const int r = idx >> 3, j = idx & 7;
+        for (int idx = tid; idx < 64 * (NB / 16); idx += kWT) {
+            const int r = idx / (NB / 16), j = idx % (NB / 16);
             if (r >= M) continue;
-            uint4 *sp = reinterpret_cast<uint4 *>(res + (int64_t)r * ldy + cb * kWNB + 16 * j);
+            uint4 *sp = reinterpret_cast<uint4 *>(res + (int64_t)r * ldy + cb * NB + 16 * j);
             const uint4 s0 = sp[0], s1 = sp[1];
             float a[16], nv[16];
             unpack16<SWH_BF16>(s0, a);
@@ -282,23 +291,23 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
             float ss = 0.f;
 #pragma unroll
             for (int c = 0; c < 16; ++c) {
-                nv[c] = round_bf16(a[c] + round_bf16(tile[r * kWLdt + 16 * j + c]));
+                nv[c] = round_bf16(a[c] + round_bf16(tile[r * LDT + 16 * j + c]));
                 ss = fmaf(nv[c], nv[c], ss);
             }
             sp[0] = pack8w(nv);
             sp[1] = pack8w(nv + 8);
-            if (ss_out) ss_out[(int64_t)r * (N / 16) + cb * (kWNB / 16) + j] = ss;
+            if (ss_out) ss_out[(int64_t)r * (N / 16) + cb * (NB / 16) + j] = ss;
         }
     } else {
         // 64 rows x 16 groups of 8 columns
-        for (int idx = tid; idx < 64 * 16; idx += kWT) {
-            const int r = idx >> 4, j = idx & 15;
+        for (int idx = tid; idx < 64 * (NB / 8); idx += kWT) {
+            const int r = idx / (NB / 8), j = idx % (NB / 8);
             if (r >= M) continue;
             const float sc = NM == 2 ? rstd_s[r] : 1.f;
-            const int col = cb * kWNB + 8 * j;
+            const int col = cb * NB + 8 * j;
             float v[8];
 #pragma unroll
-            for (int c = 0; c < 8; ++c) v[c] = tile[r * kWLdt + 8 * j + c] * sc;
+            for (int c = 0; c < 8; ++c) v[c] = tile[r * LDT + 8 * j + c] * sc;
             if constexpr (BIAS) {
                 float b[8];
                 unpack16<SWH_BF16>(*reinterpret_cast<const uint4 *>(bias + col), b);
@@ -310,7 +319,7 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
     }
 }
 
-int wide_split(int64_t N, int64_t K, int32_t silu) {
+int wide_split(int64_t ncb, int64_t K) {
     static int ncu = 0;
     if (!ncu) {
         int dev = 0;
@@ -318,7 +327,7 @@ int wide_split(int64_t N, int64_t K, int32_t silu) {
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
             ncu = 256;
     }
-    const int64_t ncb = (silu ? 2 * N : N) / kWNB, nr = K / kWKC;
+    const int64_t nr = K / kWKC;
     int64_t s = (ncu + ncb / 2) / ncb;  // about one workgroup per CU
     static int smax = 0;
     if (!smax) {  // the last arriver reads S x 32 KB of slabs (SWH_WIDE_SMAX: A/B)
@@ -332,31 +341,36 @@ int wide_split(int64_t N, int64_t K, int32_t silu) {
     return (int)s;
 }
 
-template <int EPI, int NM, bool BIAS, bool PACKED>
+// 16-row weight groups per wave: 2 when the 256-row tiles alone fill the CUs (no K split:
+// the Llama-3-8B lm head, 4.57 -> 4.96 TB/s), where halving the X bytes per weight byte
+// pays; with a split (gate/up: 112 tiles x 2) the hand-off costs more (58 -> 68 us).
+// SWH_WIDE_CB=1/2 forces one (A/B)
+int wide_cb(int64_t wcols, int64_t K) {
+    const char *e = getenv("SWH_WIDE_CB");
+    const int forced = e ? atoi(e) : 0;
+    const bool two_ok = wcols % WGeo<2>::NB == 0;
+    if (forced == 1 || !two_ok) return 1;
+    if (forced == 2) return 2;
+    return wide_split(wcols / WGeo<2>::NB, K) == 1 ? 2 : 1;
+}
+
+template <int EPI, int NM, bool BIAS, bool PACKED, int CB>
 int launch_wide(dim3 grid, hipStream_t st, const uint16_t *x, const uint16_t *w, int M, int N, int K, float eps,
                 const float *ss_in, const uint16_t *bias, uint16_t *res, float *ss_out, uint16_t *y, int ldy,
                 float *slabs, int *counters) {
     static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in once per kernel
     if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&wide_gemm_kernel<EPI, NM, BIAS, PACKED>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kWLds) != hipSuccess)
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&wide_gemm_kernel<EPI, NM, BIAS, PACKED, CB>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, WGeo<CB>::LDS) != hipSuccess)
             return SWH_E_LAUNCH;
         attr = true;
     }
-    wide_gemm_kernel<EPI, NM, BIAS, PACKED><<<grid, kWT, kWLds, st>>>(x, w, M, N, K, eps, ss_in, bias, res, ss_out, y,
-                                                                      ldy, slabs, counters);
+    wide_gemm_kernel<EPI, NM, BIAS, PACKED, CB><<<grid, kWT, WGeo<CB>::LDS, st>>>(
+        x, w, M, N, K, eps, ss_in, bias, res, ss_out, y, ldy, slabs, counters);
     return launch_status();
 }
 
 }  // namespace
-
-// Bytes of fp32 slabs the split-K reduction needs (0 when the shape is not eligible or S == 1).
-int64_t wide_gemm_slab_bytes(int64_t M, int64_t N, int64_t K, int32_t silu) {
-    if (!wide_gemm_eligible(M, N, K, silu)) return 0;
-    const int64_t ncb = (silu ? 2 * N : N) / kWNB;
-    const int s = wide_split(N, K, silu);
-    return s > 1 ? ncb * s * 64 * kWNB * (int64_t)sizeof(float) : 0;
-}
 
 // wide tiles only: a narrow output (Qwen2.5-0.5B down, N 896) stays on decode_gemm
 bool wide_gemm_eligible(int64_t M, int64_t N, int64_t K, int32_t silu) {
@@ -365,35 +379,46 @@ bool wide_gemm_eligible(int64_t M, int64_t N, int64_t K, int32_t silu) {
            wcols / kWNB <= 65535 && K < (1 << 29);
 }
 
-template <bool P>
+// Bytes of fp32 slabs the split-K reduction needs (0 when the shape is not eligible or S == 1).
+int64_t wide_gemm_slab_bytes(int64_t M, int64_t N, int64_t K, int32_t silu) {
+    if (!wide_gemm_eligible(M, N, K, silu)) return 0;
+    int64_t most = 0;
+    for (int cb = 1; cb <= 2; ++cb) {  // either tiling (SWH_WIDE_CB may change between calls)
+        const int64_t wcols = silu ? 2 * N : N, nb = (int64_t)kWNB * cb;
+        if (wcols % nb) continue;
+        const int s = wide_split(wcols / nb, K);
+        const int64_t b = s > 1 ? wcols / nb * s * 64 * nb * (int64_t)sizeof(float) : 0;
+        most = b > most ? b : most;
+    }
+    return most;
+}
+
+template <bool P, int CB>
 int dispatch_wide(dim3 grid, hipStream_t st, const uint16_t *X, const uint16_t *W, int m, int n, int k, float eps,
                   const float *ss_in, const uint16_t *B, uint16_t *R, float *ss_out, uint16_t *Y, int ld, float *slabs,
                   int *ctr, bool silu) {
-    if (silu) {
-        if (ss_in) return launch_wide<WEPI_SILU, 2, false, P>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
-        return launch_wide<WEPI_SILU, 0, false, P>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
-    }
-    if (R) return launch_wide<WEPI_RESIDUAL, 0, false, P>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
-    if (B) {
-        if (ss_in) return launch_wide<WEPI_PLAIN, 2, true, P>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
-        return launch_wide<WEPI_PLAIN, 0, true, P>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
-    }
-    if (ss_in) return launch_wide<WEPI_PLAIN, 2, false, P>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
-    return launch_wide<WEPI_PLAIN, 0, false, P>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr);
+#define SWH_WL(E, NMV, BI) launch_wide<E, NMV, BI, P, CB>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr)
+    if (silu) return ss_in ? SWH_WL(WEPI_SILU, 2, false) : SWH_WL(WEPI_SILU, 0, false);
+    if (R) return SWH_WL(WEPI_RESIDUAL, 0, false);
+    if (B) return ss_in ? SWH_WL(WEPI_PLAIN, 2, true) : SWH_WL(WEPI_PLAIN, 0, true);
+    return ss_in ? SWH_WL(WEPI_PLAIN, 2, false) : SWH_WL(WEPI_PLAIN, 0, false);
+#undef SWH_WL
 }
 
 // 1 = not eligible (the caller uses decode_gemm), else a SWH status.  packed: w is in
-// wide_pack's fragment order.
+// wide_pack's fragment order (the same for either tiling).
 int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, float eps, const float *ss_in,
               const void *bias, void *residual, int32_t silu, void *y, int64_t ldy, float *ss_out, void *workspace,
               int64_t workspace_bytes, int64_t counter_bytes, int32_t packed, hipStream_t st) {
     if (!wide_gemm_eligible(M, N, K, silu)) return 1;
-    const int64_t ncb = (silu ? 2 * N : N) / kWNB;
-    const int s = wide_split(N, K, silu);
+    const int64_t wcols = silu ? 2 * N : N;
+    const int cb = wide_cb(wcols, K);
+    const int64_t nb = (int64_t)kWNB * cb, ncb = wcols / nb;
+    const int s = wide_split(ncb, K);
     if (ncb * (int64_t)sizeof(int) > counter_bytes) return 1;
     float *slabs = nullptr;
     if (s > 1) {
-        if (!workspace || workspace_bytes < counter_bytes + ncb * s * 64 * kWNB * (int64_t)sizeof(float)) return 1;
+        if (!workspace || workspace_bytes < counter_bytes + ncb * s * 64 * nb * (int64_t)sizeof(float)) return 1;
         slabs = reinterpret_cast<float *>(static_cast<char *>(workspace) + counter_bytes);
     }
     int *ctr = static_cast<int *>(workspace);
@@ -404,8 +429,12 @@ int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, flo
     auto *R = static_cast<uint16_t *>(residual);
     auto *Y = static_cast<uint16_t *>(y);
     const int m = (int)M, n = (int)N, k = (int)K, ld = (int)ldy;
-    if (packed) return dispatch_wide<true>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr, silu);
-    return dispatch_wide<false>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr, silu);
+    if (cb == 2) {
+        if (packed) return dispatch_wide<true, 2>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr, silu);
+        return dispatch_wide<false, 2>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr, silu);
+    }
+    if (packed) return dispatch_wide<true, 1>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr, silu);
+    return dispatch_wide<false, 1>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr, silu);
 }
 
 namespace {

@@ -1261,3 +1261,26 @@ def test_wide_gemm_packed_rejects_ineligible(ops, dev):
     wp = torch.zeros(4096 * 4096, dtype=torch.bfloat16, device=dev)
     with pytest.raises(ValueError):
         nn_ops.wide_gemm_packed(x, wp, 4096)
+
+
+@pytest.mark.parametrize("name,N,K", [("gate_up", 14336, 4096), ("lm_head", 128256, 4096), ("plain", 16384, 2048)])
+def test_wide_gemm_tilings_agree(ops, dev, monkeypatch, name, N, K):
+    """The two wide_gemm tilings (128 and 256 weight rows per workgroup,
+    SWH_WIDE_CB=1/2) compute the same GEMM: they differ only in the K split,
+    i.e. in fp32 summation order."""
+    from swh_trl_amd import nn_ops
+    g = _gen(37)
+    silu = name == "gate_up"
+    M = 64
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
+    ss = x.float().view(M, K // 16, 16).pow(2).sum(-1).contiguous()
+    w = (torch.randn(2 * N if silu else N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(dev)
+    wp = nn_ops.wide_pack(w, silu=silu)
+    outs = []
+    for cb in ("1", "2"):
+        monkeypatch.setenv("SWH_WIDE_CB", cb)
+        outs.append(nn_ops.wide_gemm_packed(x, wp, N, silu=silu, ss_in=ss, eps=1e-5))
+        assert torch.equal(outs[-1], nn_ops.wide_gemm_packed(x, wp, N, silu=silu, ss_in=ss, eps=1e-5))
+    a, b = outs[0].float(), outs[1].float()
+    torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-2)
+    assert (a != b).float().mean().item() < 0.02
