@@ -79,7 +79,7 @@ __device__ __forceinline__ uint4 pack8w(const float *v) {
 // (K x 2 B) apart; same k-slot mapping, so the results are bit-identical.
 // Plain register loads only (no LDS-DMA: hipcc drains vmcnt(0) at the use of
 // any register load while an LDS-DMA is in flight — cdna_hip_programming.md,
-// LDS-DMA notes), so the compiler's counted waits keep kWD - 1 rounds in
+// LDS-DMA notes), so the compiler's counted waits keep WD - 1 rounds in
 // flight; one LDS array (a second __shared__ object makes hipcc wait before
 // LDS reads).
 template <int EPI, int NM, bool BIAS, bool PACKED, int CB>
@@ -177,25 +177,43 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
         if (REFILL) SWH_WIDE_ISSUE((r) + WD, D);                                                               \
     } while (0)
     int rb = 0;
-    if (nr >= 2 * WD) {
-        // unconditional prologue and steady state: every refill is in range, so hipcc's counted
-        // waits see one fixed pattern at the loop header (WD - 1 rounds stay in flight)
+    if (nr % WD == 0) {
+        // a whole number of WD-round blocks: the prologue, the steady loop and the last WD
+        // rounds are one fixed, branch-free pattern, and hipcc's counted waits keep WD - 1
+        // rounds in flight to the end (lm head, down: 2-3 % faster than the tail below)
 #pragma unroll
         for (int d = 0; d < WD; ++d) SWH_WIDE_ISSUE(d, d);
-        for (; rb + 2 * WD <= nr; rb += WD) {
+        for (; rb + WD < nr; rb += WD) {
 #pragma unroll
             for (int d = 0; d < WD; ++d) SWH_WIDE_ROUND(rb + d, d, true);
         }
+#pragma unroll
+        for (int d = 0; d < WD; ++d) SWH_WIDE_ROUND(rb + d, d, false);
     } else {
+        // The `if (r < nr)` tail makes the wait analysis merge paths: it waits for every load
+        // each tail round (one round in flight).  Padding nr up to a multiple of WD with
+        // masked rounds removes that but costs more than it saves when the padding is large
+        // (o at 4 rounds: 16.0 -> 18.0 us; gate/up 32 -> 35 rounds: 58.2 -> 59.1 us).
+        if (nr >= 2 * WD) {
+            // unconditional prologue and steady state: every refill is in range, so the counted
+            // waits see one fixed pattern at the loop header (WD - 1 rounds stay in flight)
 #pragma unroll
-        for (int d = 0; d < WD; ++d)
-            if (d < nr) SWH_WIDE_ISSUE(d, d);
-    }
-    // tail: the last WD .. 2 WD - 1 rounds (or all of them when nr < 2 WD)
+            for (int d = 0; d < WD; ++d) SWH_WIDE_ISSUE(d, d);
+            for (; rb + 2 * WD <= nr; rb += WD) {
 #pragma unroll
-    for (int d = 0; d < 2 * WD; ++d) {
-        const int r = rb + d;
-        if (r < nr) SWH_WIDE_ROUND(r, d % WD, r + WD < nr);
+                for (int d = 0; d < WD; ++d) SWH_WIDE_ROUND(rb + d, d, true);
+            }
+        } else {
+#pragma unroll
+            for (int d = 0; d < WD; ++d)
+                if (d < nr) SWH_WIDE_ISSUE(d, d);
+        }
+        // tail: the last WD .. 2 WD - 1 rounds (or all of them when nr < 2 WD)
+#pragma unroll
+        for (int d = 0; d < 2 * WD; ++d) {
+            const int r = rb + d;
+            if (r < nr) SWH_WIDE_ROUND(r, d % WD, r + WD < nr);
+        }
     }
 #undef SWH_WIDE_ROUND
     wide_lds_barrier();  // every wave is past its last X read: the slots become the epilogue tile
@@ -238,25 +256,33 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
         __syncthreads();
         if (!*flag_s) return;
         const float4 *base = reinterpret_cast<const float4 *>(slabs + (int64_t)cb * S * (64 * NB));
-        for (int idx = tid; idx < 64 * NB / 4; idx += kWT) {
-            float4 v[8];
-            float4 sum = float4{0.f, 0.f, 0.f, 0.f};
-            for (int q0 = 0; q0 < S; q0 += 8) {  // up to eight slab loads in flight per thread
-                const int nq = min(8, S - q0);
+        // every slab load of a pass in flight at once (up to 4 x S <= 32 per thread: the ring
+        // registers are free by now), so the reduction costs about one memory latency per pass
+        constexpr int IT = 64 * NB / 4 / kWT;  // 16-B slab pieces per thread (4 or 8)
+        constexpr int IP = IT < 4 ? IT : 4;    // pieces per pass
+#pragma unroll
+        for (int p0 = 0; p0 < IT; p0 += IP) {
+            float4 v[IP][8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (q < S) {
+#pragma unroll
+                    for (int i = 0; i < IP; ++i) v[i][q] = base[(int64_t)q * (64 * NB / 4) + tid + kWT * (p0 + i)];
+                }
+#pragma unroll
+            for (int i = 0; i < IP; ++i) {
+                float4 sum = float4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int q = 0; q < 8; ++q)
-                    if (q < nq) v[q] = base[(int64_t)(q0 + q) * (64 * NB / 4) + idx];
-#pragma unroll
-                for (int q = 0; q < 8; ++q)
-                    if (q < nq) {
-                        sum.x += v[q].x;
-                        sum.y += v[q].y;
-                        sum.z += v[q].z;
-                        sum.w += v[q].w;
+                    if (q < S) {
+                        sum.x += v[i][q].x;
+                        sum.y += v[i][q].y;
+                        sum.z += v[i][q].z;
+                        sum.w += v[i][q].w;
                     }
+                const int idx = tid + kWT * (p0 + i), r = idx / (NB / 4), c4 = idx % (NB / 4);
+                *reinterpret_cast<float4 *>(tile + r * LDT + 4 * c4) = sum;
             }
-            const int r = idx / (NB / 4), c4 = idx % (NB / 4);
-            *reinterpret_cast<float4 *>(tile + r * LDT + 4 * c4) = sum;
         }
         if (tid == 0) __hip_atomic_store(counters + cb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
@@ -334,6 +360,7 @@ int wide_split(int64_t ncb, int64_t K) {
         const char *e = getenv("SWH_WIDE_SMAX");
         smax = e ? atoi(e) : 8;
         if (smax < 1) smax = 1;
+        if (smax > 8) smax = 8;  // the last arriver's reduction holds up to 8 slabs per piece
     }
     if (s > smax) s = smax;
     if (s < 1) s = 1;
