@@ -32,6 +32,7 @@ for step in "$@"; do
     kern) run kern 600 python -m pytest tests/test_kernels_gpu.py -q -m gpu ;;
     kernx) run kernx 600 python -m pytest tests/test_kernels_gpu.py -q -m gpu -x ;;
     pack) run pack 400 python -u -m pytest tests -v -m gpu --timeout 200 --timeout-method thread -k "wide_gemm or packed_wide or llama or recapture" && run l8d1 300 python tools/bench_llama8b_decode.py && SWH_WIDE_PACK=0 run l8d0 300 python tools/bench_llama8b_decode.py ;;
+    tune8) cp swh_trl_amd/tuning/gemm_mi355x.csv gpurun_out/gemm_tuned8b.csv && SWH_GEMM_TUNING=tune SWH_GEMM_TABLE=gpurun_out/gemm_tuned8b.csv run tune8 1050 python tools/bench_llama8b.py --prompts 8 --P 256 --C 1024 --steps 1 --warmup 1 --fuse-budget 16384 ;;
     l8d) run l8d1 300 python tools/bench_llama8b_decode.py ;;
     l8dt) run wt 300 python -u -m pytest tests/test_kernels_gpu.py -v -m gpu --timeout 200 --timeout-method thread -k "wide_gemm" && run l8d1 300 python tools/bench_llama8b_decode.py ;;
     splitk) run splitk 400 python -u -m pytest tests/test_kernels_gpu.py -v -m gpu --timeout 200 --timeout-method thread -k "decode_gemm" && SWH_SWEEP_CFGS="None;1,1,2;1,1,4;2,1,2;2,1,4;4,1,2;4,1,4;4,2,2;4,2,4;1,2,2;2,2,2;2,2,4;1,1,8;4,1,8;4,4,2,0,4;4,4,4,0,4;2,2,2,0,2;2,2,4,0,2" run ksweep 400 python tools/bench_decode.py --ku ;;
