@@ -474,52 +474,26 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
         SWH_GEMM_TRACE(5);
 
         // ---- cross-workgroup split-K: publish, ticket, last arriver reduces
-        // (write-through form, as csrc/wide_gemm.hip: sc1 16-B slab stores drained by every
-        // wave, one relaxed agent-scope ticket, one acquire in the last arriver, which sums
-        // the S slabs with plain 16-B loads in fixed order)
         if (S > 1) {
             const int blk = mt * ncb + cbk;
             float *my = slabs + ((int64_t)blk * S + sidx) * (MR * NBT);
-            const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(my, 0, MR * NBT * 4, 0x00020000);
-            for (int i4 = tid; i4 < MR * NBT / 4; i4 += NT) {
-                const int r = i4 / (NBT / 4), c = (i4 - r * (NBT / 4)) * 4;
-                __builtin_amdgcn_raw_buffer_store_b128(
-                    u32x4{__float_as_uint(slot(F, r, c)), __float_as_uint(slot(F, r, c + 1)),
-                          __float_as_uint(slot(F, r, c + 2)), __float_as_uint(slot(F, r, c + 3))},
-                    rsrc, i4 * 16, 0, 16 /* sc1: write-through */);
-            }
+            for (int idx = tid; idx < MR * NBT; idx += NT)
+                __hip_atomic_store(my + idx, slot(F, idx / NBT, idx % NBT), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (tid == 0) {
                 const int t = __hip_atomic_fetch_add(counters + blk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 flag_s[0] = (t == S - 1);
-                if (t == S - 1) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
             }
             __syncthreads();
             if (!flag_s[0]) return;  // S > 1 never loops over column blocks
-            const float4 *base = reinterpret_cast<const float4 *>(slabs + (int64_t)blk * S * (MR * NBT));
-            for (int i4 = tid; i4 < MR * NBT / 4; i4 += NT) {
-                float4 v[8];
-                float4 sum = float4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int q = 0; q < 8; ++q)
-                    if (q < S) v[q] = base[(int64_t)q * (MR * NBT / 4) + i4];
-#pragma unroll
-                for (int q = 0; q < 8; ++q)
-                    if (q < S) {
-                        sum.x += v[q].x;
-                        sum.y += v[q].y;
-                        sum.z += v[q].z;
-                        sum.w += v[q].w;
-                    }
-                const int r = i4 / (NBT / 4), c = (i4 - r * (NBT / 4)) * 4;
-                slot(F, r, c) = sum.x;
-                slot(F, r, c + 1) = sum.y;
-                slot(F, r, c + 2) = sum.z;
-                slot(F, r, c + 3) = sum.w;
+            const float *base = slabs + (int64_t)blk * S * (MR * NBT);
+            for (int idx = tid; idx < MR * NBT; idx += NT) {
+                float v = 0.f;
+                for (int q = 0; q < S; ++q)
+                    v += __hip_atomic_load(base + (int64_t)q * MR * NBT + idx, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                slot(F, idx / NBT, idx % NBT) = v;
             }
             if (tid == 0) __hip_atomic_store(counters + blk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __syncthreads();
