@@ -394,6 +394,16 @@ int swh_attn_decode_prefetch(const void *qkv, void *k_cache, void *v_cache, cons
                              const float *rope_sin, const int32_t *prompt_len, const int32_t *state, int64_t B,
                              int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax, float scale, void *out,
                              const void *pf_w, int64_t pf_n, int64_t pf_k, void *stream);
+/* swh_attn_decode_prefetch where the prompt keys / values of row b (cache slots
+ * P - prompt_len[b] .. P - 1) are read from row prompt_row[b]'s cache: the G
+ * generations of a GRPO prompt (RepeatSampler copies, trl/trainer/grpo_trainer.py:1096-1130)
+ * hold identical prompt K/V, so one copy serves the group (HBM reads it once).
+ * prompt_row int32 [B] (rows of one group: equal prompts and prompt_len); NULL
+ * is the own row.  Generated keys and the appended slot stay per row. */
+int swh_attn_decode_shared(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
+                           const float *rope_sin, const int32_t *prompt_len, const int32_t *prompt_row,
+                           const int32_t *state, int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax,
+                           float scale, void *out, const void *pf_w, int64_t pf_n, int64_t pf_k, void *stream);
 
 /* Weight-streaming decode GEMM Y[M,N] = X[M,K] W[N,K]^T (bf16, fp32 MFMA
  * accumulation, K % 64 == 0, 16-B aligned operands, ldy % 8 == 0) with the

@@ -33,11 +33,14 @@ for step in "$@"; do
     kernx) run kernx 600 python -m pytest tests/test_kernels_gpu.py -q -m gpu -x ;;
     pack) run pack 400 python -u -m pytest tests -v -m gpu --timeout 200 --timeout-method thread -k "wide_gemm or packed_wide or llama or recapture" && run l8d1 300 python tools/bench_llama8b_decode.py && SWH_WIDE_PACK=0 run l8d0 300 python tools/bench_llama8b_decode.py ;;
     tune8) cp swh_trl_amd/tuning/gemm_mi355x.csv gpurun_out/gemm_tuned8b.csv && SWH_GEMM_TUNING=tune SWH_GEMM_TABLE=gpurun_out/gemm_tuned8b.csv run tune8 1050 python tools/bench_llama8b.py --prompts 8 --P 256 --C 1024 --steps 1 --warmup 1 --fuse-budget 16384 ;;
+    shkv) run shkv 500 python -u -m pytest tests -v -m gpu --timeout 200 --timeout-method thread -k "shared_prompt or attn_decode or greedy or packed_wide or recapture or fused_sampler" && run dec 300 python tools/bench_decode.py && run l8d1 300 python tools/bench_llama8b_decode.py ;;
+    shkvb) run l8d1 300 python tools/bench_llama8b_decode.py && SWH_DECODE_SHARED_KV=0 run l8d0 300 python tools/bench_llama8b_decode.py && run benchq 600 python bench.py --steps 3 --warmup 2 --no-cpu-baseline ;;
     l8d) run l8d1 300 python tools/bench_llama8b_decode.py ;;
     l8dt) run wt 300 python -u -m pytest tests/test_kernels_gpu.py -v -m gpu --timeout 200 --timeout-method thread -k "wide_gemm" && run l8d1 300 python tools/bench_llama8b_decode.py ;;
     splitk) run splitk 400 python -u -m pytest tests/test_kernels_gpu.py -v -m gpu --timeout 200 --timeout-method thread -k "decode_gemm" && SWH_SWEEP_CFGS="None;1,1,2;1,1,4;2,1,2;2,1,4;4,1,2;4,1,4;4,2,2;4,2,4;1,2,2;2,2,2;2,2,4;1,1,8;4,1,8;4,4,2,0,4;4,4,4,0,4;2,2,2,0,2;2,2,4,0,2" run ksweep 400 python tools/bench_decode.py --ku ;;
     decw) SWH_WIDE_KMIN=512 run decw 300 python tools/bench_decode.py ;;
     dec) run dec 300 python tools/bench_decode.py ;;
+    decsteps) run dec0 200 python tools/bench_decode.py --step 1 && run dec128 200 python tools/bench_decode.py --step 128 && run dec255 200 python tools/bench_decode.py --step 255 ;;
     ku) run ku 400 python tools/bench_decode.py --ku ;;
     dual) run dual 300 python tools/bench_decode.py --dual ;;
     sweep) run sweep 300 python tools/bench_decode.py --sweep ;;

@@ -1021,9 +1021,10 @@ __device__ __forceinline__ bf16x4s lds_read_tr16(const uint16_t *p) {
 // consume them (tile t runs on XCD t mod 8 there, workgroup id mod 8 here), by
 // LDS-DMA into a scratch tile (no registers, nothing consumed).
 struct AttnPrefetch {
-    const uint16_t *w;  // [2N, K] gate/up weights, or null
-    int n, k;           // N (SiLU pairs), K
-    int rows;           // attention rows (B): grid rows past it prefetch
+    const uint16_t *w;     // [2N, K] gate/up weights, or null
+    int n, k;              // N (SiLU pairs), K
+    int rows;              // attention rows (B): grid rows past it prefetch
+    const int32_t *prow;   // [B] row whose cache holds this row's prompt keys / values, or null (own row)
 };
 
 template <int D, int GQ>
@@ -1082,6 +1083,12 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
     const int64_t cbase = (b * Hkv + kvh) * (int64_t)Tmax * D;
     const uint16_t *kb = kc + cbase + (int64_t)start * D + g * 8;
     const uint16_t *vb = vc + cbase + (int64_t)start * D + g * 8;
+    // prompt keys (index < pl, slots start .. P-1) from the row that holds the group's prompt:
+    // the G rows of a GRPO group read one copy (HBM once, the rest from the caches)
+    const int64_t prow = pf.prow ? (int64_t)min(max(pf.prow[b], 0), pf.rows - 1) : b;
+    const int64_t pbase = (prow * Hkv + kvh) * (int64_t)Tmax * D;
+    const uint16_t *kbp = kc + pbase + (int64_t)start * D + g * 8;
+    const uint16_t *vbp = vc + pbase + (int64_t)start * D + g * 8;
 
     // lane (g, c16) loads key c16 of each block, dims 32 c + 8 g: the A fragment of K Q^T
     u32x4 kr[JB][DC], vr[JB][DC];  // vector types: uint4 structs defeat SROA under selects
@@ -1090,9 +1097,10 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
         const int k0_ = (base_) + (wid + i * kAttnWaves) * 16;                                 \
         if (k0_ < n) {                                                                         \
             const int kk = max(min(k0_ + c16, n - 2), 0);                                      \
+            const uint16_t *ks_ = kk < pl ? kbp : kb, *vs_ = kk < pl ? vbp : vb;               \
             _Pragma("unroll") for (int c = 0; c < DC; ++c) {                                   \
-                kr[i][c] = *reinterpret_cast<const u32x4 *>(kb + (int64_t)kk * D + c * 32);    \
-                vr[i][c] = *reinterpret_cast<const u32x4 *>(vb + (int64_t)kk * D + c * 32);    \
+                kr[i][c] = *reinterpret_cast<const u32x4 *>(ks_ + (int64_t)kk * D + c * 32);   \
+                vr[i][c] = *reinterpret_cast<const u32x4 *>(vs_ + (int64_t)kk * D + c * 32);   \
             }                                                                                  \
         }                                                                                      \
     }
@@ -1489,10 +1497,11 @@ int launch_tiles(int nm, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X
 
 using namespace swh;
 
-extern "C" int swh_attn_decode_prefetch(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
-                                        const float *rope_sin, const int32_t *prompt_len, const int32_t *state,
-                                        int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax, float scale,
-                                        void *out, const void *pf_w, int64_t pf_n, int64_t pf_k, void *stream) {
+extern "C" int swh_attn_decode_shared(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
+                                      const float *rope_sin, const int32_t *prompt_len, const int32_t *prompt_row,
+                                      const int32_t *state, int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax,
+                                      float scale, void *out, const void *pf_w, int64_t pf_n, int64_t pf_k,
+                                      void *stream) {
     if (!qkv || !k_cache || !v_cache || !rope_cos || !rope_sin || !prompt_len || !state || !out || B < 0 || Hkv <= 0 ||
         Hq % Hkv || Tmax <= 0 || B > 65535)
         return SWH_E_ARG;
@@ -1505,10 +1514,18 @@ extern "C" int swh_attn_decode_prefetch(const void *qkv, void *k_cache, void *v_
     auto *kc = static_cast<uint16_t *>(k_cache), *vc = static_cast<uint16_t *>(v_cache);
     auto *o = static_cast<uint16_t *>(out);
     const int gq = Hq / Hkv;
-    const AttnPrefetch pf{static_cast<const uint16_t *>(pf_w), (int)pf_n, (int)pf_k, (int)B};
+    const AttnPrefetch pf{static_cast<const uint16_t *>(pf_w), (int)pf_n, (int)pf_k, (int)B, prompt_row};
     if (D == 64) return attn_dispatch_gq<64>(gq, q, kc, vc, rope_cos, rope_sin, prompt_len, state, B, Hq, Hkv, Tmax, scale, o, s, pf);
     if (D == 128) return attn_dispatch_gq<128>(gq, q, kc, vc, rope_cos, rope_sin, prompt_len, state, B, Hq, Hkv, Tmax, scale, o, s, pf);
     return SWH_E_ARG;
+}
+
+extern "C" int swh_attn_decode_prefetch(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
+                                        const float *rope_sin, const int32_t *prompt_len, const int32_t *state,
+                                        int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax, float scale,
+                                        void *out, const void *pf_w, int64_t pf_n, int64_t pf_k, void *stream) {
+    return swh_attn_decode_shared(qkv, k_cache, v_cache, rope_cos, rope_sin, prompt_len, nullptr, state, B, Hq, Hkv,
+                                  D, Tmax, scale, out, pf_w, pf_n, pf_k, stream);
 }
 
 extern "C" int swh_attn_decode(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,

@@ -81,6 +81,11 @@ class DecodeEngine:
         self.out = torch.zeros(B, max_new_tokens, device=dev, dtype=torch.int64)
         self.out_logp = torch.zeros(B, max_new_tokens, device=dev, dtype=torch.float32)
         self.plen = torch.zeros(B, device=dev, dtype=torch.int32)
+        # GRPO's G copies of a prompt read one copy of its prompt K/V in the decode attention
+        # (swh_attn_decode_shared; SWH_DECODE_SHARED_KV=0: every row its own copy)
+        self.shared_kv = os.environ.get("SWH_DECODE_SHARED_KV", "1") != "0"
+        self._own_rows = torch.arange(B, device=dev, dtype=torch.int32)
+        self.prow = self._own_rows.clone()
         self.seen = torch.zeros(B, (c.vocab_size + 31) // 32, device=dev, dtype=torch.int32)
         self.ws = torch.empty(ops._lib.load().swh_sample_workspace_bytes(B, c.vocab_size), device=dev,
                               dtype=torch.uint8)
@@ -230,7 +235,7 @@ class DecodeEngine:
                 self.packed else None
             nn_ops.attn_decode(self.qkv, self.kv[i, 0], self.kv[i, 1], self.cos, self.sin, self.plen, self.state,
                                c.num_attention_heads, c.num_key_value_heads, c.head_dim, c.head_dim ** -0.5,
-                               out=self.att, prefetch_gate_up=pf)
+                               out=self.att, prefetch_gate_up=pf, prompt_row=self.prow)
             self._proj(f"l{i}.o_w", self.att, residual=self.s, ss_out=ss)
             self._proj(f"l{i}.gu_w", self.s, silu=True, y=self.act, ss_in=ss)
             self._proj(f"l{i}.down_w", self.act, residual=self.s, ss_out=ss)
@@ -255,7 +260,7 @@ class DecodeEngine:
                 torch.mm(self.h, p[f"l{i}.qkv_w"].t(), out=self.qkv)
             nn_ops.attn_decode(self.qkv, self.kv[i, 0], self.kv[i, 1], self.cos, self.sin, self.plen, self.state,
                                c.num_attention_heads, c.num_key_value_heads, c.head_dim, c.head_dim ** -0.5,
-                               out=self.att)
+                               out=self.att, prompt_row=self.prow)
             torch.mm(self.att, p[f"l{i}.o_w"].t(), out=self.o)
             nn_ops.rmsnorm_residual(self.o, self.s, p[f"l{i}.ln_post"], c.rms_norm_eps, y=self.h, s_out=self.s)
             torch.mm(self.h, p[f"l{i}.gu_w"].t(), out=self.gu)
@@ -332,7 +337,10 @@ class DecodeEngine:
         self.state[0] = step_index
         keys = P + step_index  # upper bound over rows (left padding shortens some)
         bf = 2
-        att_bytes = B * c.num_key_value_heads * keys * c.head_dim * bf * 2 + B * (c.qkv_dim + c.q_dim) * bf
+        # shared prompt K/V (self.prow): each distinct prompt row's keys are read once
+        U = int(torch.unique(self.prow).numel())
+        att_bytes = ((U * P + B * (keys - P)) * c.num_key_value_heads * c.head_dim * bf * 2 +
+                     B * (c.qkv_dim + c.q_dim) * bf)
 
         def gemm_bytes(N, K, silu=False):
             wN = 2 * N if silu else N
@@ -353,7 +361,7 @@ class DecodeEngine:
                                                          out=self.att,
                                                          prefetch_gate_up=self._normed(f"l{i}.gu_w", "")[0]
                                                          if self.prefetch and f"l{i}.gu_w" not in self.packed
-                                                         else None),
+                                                         else None, prompt_row=self.prow),
                             att_bytes, L),
             "decode_gemm.o": (lambda i: self._proj(f"l{i}.o_w", self.att, residual=self.s, ss_out=ss),
                               gemm_bytes(H, c.q_dim), L),
@@ -429,15 +437,21 @@ class DecodeEngine:
         rep.scatter_(0, inv, torch.arange(B, device=key.device))
         return rep, inv
 
-    def _prefill_body(self, ids, mask, inv, padded: bool):
-        """The prefill forward on (distinct) prompt rows, K/V broadcast through
-        `inv` into the cache, last-position logits into logits_buf.  No host
+    def _prefill_body(self, ids, mask, inv, rep, padded: bool):
+        """The prefill forward on (distinct) prompt rows, K/V into the cache —
+        into the representative rows `rep` only when the decode attention reads
+        each group's prompt from there (`self.prow`), else broadcast through
+        `inv` to every row — and last-position logits into logits_buf.  No host
         sync inside (graph-capturable)."""
         m = self.model
         P = ids.shape[1]
         pos = (mask.long().cumsum(-1) - 1).clamp(min=0)
 
         def kv_out(i, k, v):
+            if inv is not None and self.shared_kv:
+                self.kv[i, 0, :, :, :P].index_copy_(0, rep, k)
+                self.kv[i, 1, :, :, :P].index_copy_(0, rep, v)
+                return
             if inv is not None:
                 k, v = k.index_select(0, inv), v.index_select(0, inv)
             self.kv[i, 0, :, :, :P].copy_(k)
@@ -457,37 +471,42 @@ class DecodeEngine:
         static input buffers (SWH_PREFILL_GRAPH=0: eager)."""
         m = self.model
         dedup = self._unique_prompts(prompt_ids, prompt_mask, group_size)
-        inv = None
+        inv = rep = None
         if dedup is not None:
             rep, inv = dedup
             prompt_ids, prompt_mask = prompt_ids[rep], prompt_mask[rep]
+            # row b's prompt keys / values live in row rep[inv[b]] (swh_attn_decode_shared)
+            self.prow.copy_(rep[inv] if self.shared_kv else self._own_rows)
+        else:
+            self.prow.copy_(self._own_rows)
         padded = not bool(prompt_mask.bool().all())
         with torch.no_grad():
             saved = m.grad
             m.grad = None  # no grad accumulation in prefill
             try:
                 if not (self.use_graph and os.environ.get("SWH_PREFILL_GRAPH", "1") != "0"):
-                    self._prefill_body(prompt_ids, prompt_mask, inv, padded)
+                    self._prefill_body(prompt_ids, prompt_mask, inv, rep, padded)
                     return
                 key = (tuple(prompt_ids.shape), inv is None, padded)
                 gp = self._prefill_graphs.get(key)
                 if gp is None:
                     st = {"ids": prompt_ids.clone(), "mask": prompt_mask.clone(),
-                          "inv": None if inv is None else inv.clone()}
+                          "inv": None if inv is None else inv.clone(), "rep": None if rep is None else rep.clone()}
                     side = torch.cuda.Stream()
                     side.wait_stream(torch.cuda.current_stream())
                     with torch.cuda.stream(side):  # warm-up (library workspaces) outside capture
-                        self._prefill_body(st["ids"], st["mask"], st["inv"], padded)
+                        self._prefill_body(st["ids"], st["mask"], st["inv"], st["rep"], padded)
                     torch.cuda.current_stream().wait_stream(side)
                     g = torch.cuda.CUDAGraph()
                     with _capture(g):
-                        self._prefill_body(st["ids"], st["mask"], st["inv"], padded)
+                        self._prefill_body(st["ids"], st["mask"], st["inv"], st["rep"], padded)
                     gp = self._prefill_graphs[key] = (g, st)
                 g, st = gp
                 st["ids"].copy_(prompt_ids)
                 st["mask"].copy_(prompt_mask)
                 if inv is not None:
                     st["inv"].copy_(inv)
+                    st["rep"].copy_(rep)
                 g.replay()
             finally:
                 m.grad = saved

@@ -655,3 +655,30 @@ def test_graph_recapture_after_generation_is_clean(dev):
     out2, lp2 = fresh.generate(ids, mask, C, temperature=0.9, seed=12, return_logp=True)
     assert not torch.isnan(lp).any()
     assert torch.equal(out, out2) and torch.equal(lp, lp2)
+
+
+def test_shared_prompt_kv_generates_identically(dev, monkeypatch):
+    """GRPO groups (G copies of each prompt, left padding in one group): the
+    decode attention reading each group's prompt K/V from one row
+    (SWH_DECODE_SHARED_KV, default) generates the same tokens and log-probs as
+    every row keeping its own copy."""
+    from swh_trl_amd.engine import DecodeEngine
+    m = _tiny(dev, seed=13, layers=2)
+    g = torch.Generator().manual_seed(13)
+    G, U, P, C = 4, 3, 10, 12
+    ids = torch.randint(0, m.cfg.vocab_size, (U, P), generator=g).repeat_interleave(G, 0).to(dev)
+    mask = torch.ones(U * G, P, dtype=torch.int64, device=dev)
+    mask[G:2 * G, :3] = 0
+    outs = {}
+    for shared in ("1", "0"):
+        monkeypatch.setenv("SWH_DECODE_SHARED_KV", shared)
+        eng = DecodeEngine(m, U * G, P, C)
+        r = (eng.generate(ids, mask, C, temperature=0.9, seed=3, group_size=G),
+             eng.generate(ids, mask, C, temperature=0.9, seed=4, return_logp=True, group_size=G))
+        if shared == "1":
+            assert eng.prow.tolist() == [b // G * G for b in range(U * G)]
+        outs[shared] = r
+    for a, b in zip(outs["1"], outs["0"]):
+        for x, y in zip(a, b):
+            if x is not None:
+                assert torch.equal(x, y)

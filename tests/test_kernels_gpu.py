@@ -841,6 +841,41 @@ def test_attn_decode_prefetch_is_result_neutral(ops, dev, B, Hkv, I):
     assert torch.equal(a, b) and torch.equal(k1, k2) and torch.equal(v1, v2)
 
 
+@pytest.mark.parametrize("D,Hkv,G,P,step", [(64, 2, 8, 128, 100), (128, 8, 8, 256, 300), (64, 2, 4, 41, 5)])
+def test_attn_decode_shared_prompt_rows(ops, dev, D, Hkv, G, P, step):
+    """swh_attn_decode_shared: the rows of a group read their prompt keys /
+    values from the group's first row (the other rows' prompt slots hold
+    garbage here) and equal swh_attn_decode over a cache where every row holds
+    its own copy — output and appended slot, bit for bit; left padding included."""
+    from swh_trl_amd import nn_ops
+    g = _gen(24)
+    U, Hq, Tmax = 3, 4 * Hkv, P + step + 8
+    B = U * G
+    plen_u = torch.tensor([P, max(1, P - 7), 1], dtype=torch.int32)
+    plen = plen_u.repeat_interleave(G).to(dev)
+    kc = torch.randn(B, Hkv, Tmax, D, generator=g).to(torch.bfloat16).to(dev)
+    vc = torch.randn(B, Hkv, Tmax, D, generator=g).to(torch.bfloat16).to(dev)
+    rep = torch.arange(0, B, G, device=dev)
+    full_k, full_v = kc.clone(), vc.clone()  # every row its group's prompt
+    full_k[:, :, :P] = kc[rep].repeat_interleave(G, 0)[:, :, :P]
+    full_v[:, :, :P] = vc[rep].repeat_interleave(G, 0)[:, :, :P]
+    qkv = torch.randn(B, (Hq + 2 * Hkv) * D, generator=g).to(torch.bfloat16).to(dev)
+    cos, sin = _rope_tables(D, 2048, 1e6, dev)
+    state = torch.tensor([step + 1, P], dtype=torch.int32, device=dev)
+    prow = rep.repeat_interleave(G).to(torch.int32)
+    a = nn_ops.attn_decode(qkv, full_k, full_v, cos, sin, plen, state, Hq, Hkv, D, D ** -0.5)
+    k2, v2 = kc.clone(), vc.clone()
+    b = nn_ops.attn_decode(qkv, k2, v2, cos, sin, plen, state, Hq, Hkv, D, D ** -0.5, prompt_row=prow)
+    assert torch.equal(a, b)
+    slot = P + step
+    assert torch.equal(k2[:, :, slot], full_k[:, :, slot]) and torch.equal(v2[:, :, slot], full_v[:, :, slot])
+    # own rows (prompt_row = arange) is swh_attn_decode
+    k3, v3 = full_k.clone(), full_v.clone()
+    own = torch.arange(B, device=dev, dtype=torch.int32)
+    c = nn_ops.attn_decode(qkv, k3, v3, cos, sin, plen, state, Hq, Hkv, D, D ** -0.5, prompt_row=own)
+    assert torch.equal(a, c)
+
+
 # --------------------------------------------------------------------------- fused decode GEMM
 def _ref_norm(x, w, eps):
     xf = x.float()

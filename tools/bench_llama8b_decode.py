@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--P", type=int, default=256)
     ap.add_argument("--step", type=int, default=512)
     ap.add_argument("--B", type=int, default=64)
+    ap.add_argument("--distinct", action="store_true", help="64 distinct prompts instead of 8 x G 8")
     args = ap.parse_args()
     from swh_trl_amd.engine import CausalLM, DecodeEngine, llama3_8b
     t0 = time.perf_counter()
@@ -29,15 +30,17 @@ def main():
     m = CausalLM(cfg, torch.device("cuda:0"), seed=0, init_std=0.02)
     eng = DecodeEngine(m, args.B, args.P, args.step + 8)
     g = torch.Generator().manual_seed(0)
-    ids = torch.randint(0, cfg.vocab_size - 1000, (args.B, args.P), generator=g).cuda()
+    G = 1 if args.distinct else 8  # config 5: 8 prompts x G 8 generations per GPU
+    ids = torch.randint(0, cfg.vocab_size - 1000, (args.B // G, args.P), generator=g).repeat_interleave(G, 0).cuda()
     mask = torch.ones_like(ids)
-    eng.generate(ids, mask, 4, temperature=1.0, seed=1)
+    eng.generate(ids, mask, 4, temperature=1.0, seed=1, group_size=G)
     torch.cuda.synchronize()
     print(f"[l8dec] setup {time.perf_counter() - t0:.1f}s, packed {len(eng.packed)} matrices", file=sys.stderr,
           flush=True)
     dec = eng.kernel_timings(args.step)
     out = {"workload": "Llama-3-8B decode kernels, 1 GPU", "B": args.B, "P": args.P, "step": args.step,
-           "wide_pack": os.environ.get("SWH_WIDE_PACK", "1"), "packed": len(eng.packed)}
+           "wide_pack": os.environ.get("SWH_WIDE_PACK", "1"), "packed": len(eng.packed),
+           "prompt_groups": int(torch.unique(eng.prow).numel())}
     for k, v in dec.items():
         e = {"avg_us": round(v["avg_us"], 2)}
         if v.get("bytes_per_launch"):
