@@ -303,9 +303,11 @@ def test_grpo_trainer_smoke(dev):
 
 @pytest.mark.parametrize("left_pad", [False, True])
 def test_prefill_dedup_matches_full_prefill(dev, monkeypatch, left_pad):
-    """GRPO groups: G copies of each prompt are prefilled once and broadcast.
-    The K/V cache and first-token logits equal the row-by-row prefill within
-    bf16 GEMM-order tolerance, and greedy rollouts agree token for token."""
+    """GRPO groups: G copies of each prompt are prefilled once, their K/V
+    written to the group's first row, which the decode attention reads for
+    every row of the group (`eng.prow`).  The K/V each row attends to and the
+    first-token logits equal the row-by-row prefill within bf16 GEMM-order
+    tolerance, and greedy rollouts agree token for token."""
     from swh_trl_amd.engine import DecodeEngine
     m = _tiny(dev, seed=7)
     G, n, P, C = 4, 3, 12, 16
@@ -324,7 +326,7 @@ def test_prefill_dedup_matches_full_prefill(dev, monkeypatch, left_pad):
         eng = DecodeEngine(m, n * G, P, C)
         eng.state[0], eng.state[1] = 0, P
         eng._prefill(ids, mask)
-        kv, lg = eng.kv[:, :, :, :, :P].clone(), eng.logits_buf.clone()
+        kv, lg = eng.kv[:, :, eng.prow.long(), :, :P].clone(), eng.logits_buf.clone()
         comp, _ = eng.generate(ids, mask, C, greedy=True)
         outs[flag] = (kv, lg, comp)
     torch.testing.assert_close(outs["1"][0].float(), outs["0"][0].float(), rtol=2e-2, atol=2e-2)
