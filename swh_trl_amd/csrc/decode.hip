@@ -567,6 +567,155 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Register-streamed short-K projection (decode qkv and o_proj at K <= 2048:
+// 16 MS-row x 16-column tiles over the full K, no K split): decode_gemm_kernel
+// <1, MS, NM, EPI, BIAS> with the X slice read as MFMA A fragments straight
+// into registers beside the weight fragments.  A wave's A operand is X[MR rows,
+// its own k-steps], which no other wave reads, so the LDS image — and its
+// landing wait (vmcnt(0)) before the first MFMA — goes: every k-step of the
+// wave is issued at once (KW of them) and the MFMAs consume them in arrival
+// order.  Same k-step split, wave order, merge tree, row statistic and
+// epilogues as decode_gemm_kernel, so the result is bit-identical.  At long K
+// (down_proj, K 4864) the fragment-order X loads (64 B of a row per lane group,
+// twice the lines of the image's whole-row loads) cost more than the landing
+// wait saves (11.4 -> 12.4 us), so it serves K <= 2048 only.
+// ---------------------------------------------------------------------------
+template <int KW, int MS, int NM, int EPI, bool BIAS, int KL>
+__global__ __launch_bounds__(512) void xstream_gemm_kernel(const uint16_t *__restrict__ x,
+                                                           const uint16_t *__restrict__ w, int M, int N, int K,
+                                                           float eps, const float *__restrict__ ss_in,
+                                                           const uint16_t *__restrict__ bias,
+                                                           uint16_t *__restrict__ res, float *__restrict__ ss_out,
+                                                           uint16_t *__restrict__ y, int ldy) {
+    static_assert(EPI != EPI_SILU && NM != 1, "plain / residual epilogues, folded or no norm");
+    constexpr int NW = 8, NT = 512, MR = 16 * MS, NB = 16, LDR = MR + 4, G8 = NB / 8, F = NW;
+    __shared__ __attribute__((aligned(16))) float part[(NW + 1) * NB * LDR];
+    __shared__ float rstd_s[MR];
+    const int tid = threadIdx.x, lane = tid & 63, kw = tid >> 6;
+    const int ncb = N / NB, nmt = (M + MR - 1) / MR;
+    const int xcd = blockIdx.x & 7, jj = blockIdx.x >> 3;  // the nmt M tiles of a column block on one XCD
+    const int cbk = (jj / nmt) * 8 + xcd, mt = jj % nmt;
+    if (cbk >= ncb) return;
+    const int m0 = mt * MR, n0 = cbk * NB;
+    const int KS = K / 32, ksw0 = KS * kw / NW, ksw1 = KS * (kw + 1) / NW;
+    const int rl = lane & 15, kq = (lane >> 4) * 8;
+    SWH_GEMM_TRACE(0);
+    // epilogue operands and the row statistic's partials (oldest in the queue)
+    uint4 pre_ep;
+    {
+        const int idx = min(tid, MR * G8 - 1);
+        const int r = idx / G8, gc = n0 + (idx - r * G8) * 8;
+        if constexpr (EPI == EPI_RESIDUAL)
+            pre_ep = *reinterpret_cast<const uint4 *>(res + (int64_t)min(m0 + r, M - 1) * ldy + gc);
+        else if constexpr (BIAS)
+            pre_ep = *reinterpret_cast<const uint4 *>(bias + gc);
+    }
+    const int nc = K / 64;
+    float4 ss8[8];
+    if constexpr (NM == 2) {
+        const int r = min(m0 + (tid >> 3), M - 1), sub = tid & 7;
+        const float4 *row = reinterpret_cast<const float4 *>(ss_in + (int64_t)r * (K / 16));
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (sub + 8 * j < nc) ss8[j] = row[sub + 8 * j];
+    }
+    const uint16_t *wr = w + (int64_t)(n0 + rl) * K + kq;
+    const uint16_t *xr[MS];
+#pragma unroll
+    for (int i = 0; i < MS; ++i) xr[i] = x + (int64_t)min(m0 + i * 16 + rl, M - 1) * K + kq;
+    uint4 xa[KW][MS], bv[KW];
+#pragma unroll
+    for (int u = 0; u < KW; ++u) {
+        const int ks = min(ksw0 + u, ksw1 - 1);  // past the wave's range: a repeated, unused load (no branch)
+        bv[u] = ld_w(wr + ks * 32);
+#pragma unroll
+        for (int i = 0; i < MS; ++i) xa[u][i] = *reinterpret_cast<const uint4 *>(xr[i] + ks * 32);
+    }
+    SWH_GEMM_TRACE(1);
+    if constexpr (NM == 2) {  // read by the epilogue only, behind the merge barriers
+        const int r = tid >> 3, sub = tid & 7;
+        float v = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (sub + 8 * j < nc) v += ((ss8[j].x + ss8[j].y) + ss8[j].z) + ss8[j].w;
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        if (r < MR && sub == 0) rstd_s[r] = rsqrtf(v / (float)K + eps);
+    }
+    f32x4 acc[MS];
+#pragma unroll
+    for (int i = 0; i < MS; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < KW; ++u)
+        if (ksw0 + u < ksw1) {
+#pragma unroll
+            for (int i = 0; i < MS; ++i)
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xa[u][i]), as_bf16x8(bv[u]), acc[i], 0, 0, 0);
+        }
+    SWH_GEMM_TRACE(4);
+    // merge the 8 waves: decode_gemm_kernel's fixed-order tree -> slot F
+    auto slot = [&](int s, int r, int c) -> float & { return part[(s * NB + c) * LDR + r]; };
+    auto park = [&](int s) {
+#pragma unroll
+        for (int i = 0; i < MS; ++i) *reinterpret_cast<f32x4 *>(&slot(s, i * 16 + (lane >> 4) * 4, rl)) = acc[i];
+    };
+    for (int h = NW >> 1; h >= 1; h >>= 1) {
+        if (kw >= h && kw < 2 * h) park(kw - h);
+        lds_barrier();
+        if (kw < h) {
+#pragma unroll
+            for (int i = 0; i < MS; ++i) acc[i] += *reinterpret_cast<const f32x4 *>(&slot(kw, i * 16 + (lane >> 4) * 4, rl));
+        }
+        lds_barrier();
+    }
+    if (kw == 0) park(F);
+    lds_barrier();
+    SWH_GEMM_TRACE(5);
+    // epilogue, 8 output columns (16 B) per thread
+    if (tid < MR * G8) {
+        const int r = tid / G8, c8 = (tid - r * G8) * 8;
+        const int gr = m0 + r, gc = n0 + c8;
+        if (gr < M) {
+            float v[8];
+            const float sc = (NM == 2) ? rstd_s[r] : 1.f;  // folded RMSNorm: y = rstd * (x W'^T)
+#pragma unroll
+            for (int cc = 0; cc < 8; ++cc) v[cc] = slot(F, r, c8 + cc) * sc;
+            if constexpr (EPI == EPI_RESIDUAL) {
+                float sres[8];
+                unpack16<SWH_BF16>(pre_ep, sres);
+#pragma unroll
+                for (int cc = 0; cc < 8; ++cc) {
+                    sres[cc] = round_bf16(sres[cc] + round_bf16(v[cc]));
+                    slot(F, r, c8 + cc) = sres[cc];
+                }
+                *reinterpret_cast<uint4 *>(res + (int64_t)gr * ldy + gc) = pack8(sres);
+            } else {
+                if constexpr (BIAS) {
+                    float b[8];
+                    unpack16<SWH_BF16>(pre_ep, b);
+#pragma unroll
+                    for (int cc = 0; cc < 8; ++cc) v[cc] += b[cc];
+                }
+                *reinterpret_cast<uint4 *>(y + (int64_t)gr * ldy + gc) = pack8(v);
+            }
+        }
+    }
+    if constexpr (EPI == EPI_RESIDUAL) {
+        if (ss_out) {  // partial sums of squares of the new rows over this 16-column chunk
+            __syncthreads();
+            if (tid < MR && m0 + tid < M) {
+                float ss = 0.f;
+#pragma unroll
+                for (int cc = 0; cc < 16; ++cc) ss = fmaf(slot(F, tid, cc), slot(F, tid, cc), ss);
+                ss_out[(int64_t)(m0 + tid) * (N / 16) + n0 / 16] = ss;
+            }
+        }
+    }
+    SWH_GEMM_TRACE(6);
+}
+
+// ---------------------------------------------------------------------------
 // Tile kernel (many 16-column tiles, K <= 1024: the lm head, gate/up):
 // persistent workgroups, one per CU (per M tile); the X image [64 x K] is
 // staged (and normalised) once, then every wave owns whole 16-column tiles
@@ -1430,6 +1579,43 @@ int launch_gemm(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const ui
                                                           ss_out, Y, ld, slab, ctr);
 }
 
+// the register-streamed short-K projection; 1 = not eligible
+template <int KW, int MS, int NM, int EPI, bool BIAS>
+int launch_xstream_kw(const GemmCfg &c, hipStream_t s, const uint16_t *X, const uint16_t *W, int m, int n, int k,
+                      float eps, const float *ss_in, const uint16_t *Bs, uint16_t *R, float *ss_out, uint16_t *Y,
+                      int ld) {
+    xstream_gemm_kernel<KW, MS, NM, EPI, BIAS, 0><<<dim3((unsigned)c.gx), 512, 0, s>>>(X, W, m, n, k, eps, ss_in, Bs, R,
+                                                                                   ss_out, Y, ld);
+    return launch_status();
+}
+
+template <int MS, int NM, int EPI, bool BIAS>
+int launch_xstream_ms(const GemmCfg &c, hipStream_t s, const uint16_t *X, const uint16_t *W, int m, int n, int k,
+                      float eps, const float *ss_in, const uint16_t *Bs, uint16_t *R, float *ss_out, uint16_t *Y,
+                      int ld) {
+    const int ks = k / 32, kwn = (ks + 7) / 8;
+    if (kwn <= 2) return launch_xstream_kw<2, MS, NM, EPI, BIAS>(c, s, X, W, m, n, k, eps, ss_in, Bs, R, ss_out, Y, ld);
+    if (kwn <= 4) return launch_xstream_kw<4, MS, NM, EPI, BIAS>(c, s, X, W, m, n, k, eps, ss_in, Bs, R, ss_out, Y, ld);
+    return launch_xstream_kw<8, MS, NM, EPI, BIAS>(c, s, X, W, m, n, k, eps, ss_in, Bs, R, ss_out, Y, ld);
+}
+
+int launch_xstream(const GemmCfg &c, hipStream_t s, const uint16_t *X, const uint16_t *W, int m, int n, int k, int nm,
+                   float eps, const float *ss_in, const uint16_t *Bs, uint16_t *R, float *ss_out, uint16_t *Y, int ld) {
+    const char *e = getenv("SWH_XSTREAM");  // A/B: 0 = decode_gemm_kernel's LDS image
+    const int ks = k / 32;
+    if ((e && e[0] == '0') || c.cb != 1 || c.wn != 1 || c.s != 1 || c.persist || c.nw != 8 || n % 16 || ks < 8 ||
+        ks > 64 || (c.ms != 1 && c.ms != 2))
+        return 1;
+    if (R) {  // o_proj: s += x W^T (+ the next norm's partial sums)
+        if (nm != 0 || Bs || c.ms != 1) return 1;
+        return launch_xstream_ms<1, 0, EPI_RESIDUAL, false>(c, s, X, W, m, n, k, eps, nullptr, nullptr, R, ss_out, nullptr, ld);
+    }
+    if (nm != 2 || !ss_in || !Bs || !Y) return 1;  // qkv: folded norm + bias
+    if (c.ms == 1)
+        return launch_xstream_ms<1, 2, EPI_PLAIN, true>(c, s, X, W, m, n, k, eps, ss_in, Bs, nullptr, nullptr, Y, ld);
+    return launch_xstream_ms<2, 2, EPI_PLAIN, true>(c, s, X, W, m, n, k, eps, ss_in, Bs, nullptr, nullptr, Y, ld);
+}
+
 template <int MS, int NM, int EPI, bool BIAS>
 int launch_gemm_cb(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W,
                    int m, int n, int k, const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs,
@@ -1627,12 +1813,20 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
         SWH_GEMM(0, EPI_SILU, false);
     }
     if (residual) {
+        if (nm == 0) {
+            const int rc = launch_xstream(c, s, X, W, m, n, k, nm, eps, ss_in, Bs, R, ss_out, nullptr, ld);
+            if (rc != 1) return rc;
+        }
         if (nm == 1) SWH_GEMM(1, EPI_RESIDUAL, false);
         SWH_GEMM(0, EPI_RESIDUAL, false);
     }
     if (Bs) {
         if (nm == 1) SWH_GEMM(1, EPI_PLAIN, true);
-        if (nm == 2) SWH_GEMM(2, EPI_PLAIN, true);
+        if (nm == 2) {
+            const int rc = launch_xstream(c, s, X, W, m, n, k, nm, eps, ss_in, Bs, nullptr, nullptr, Y, ld);
+            if (rc != 1) return rc;
+            SWH_GEMM(2, EPI_PLAIN, true);
+        }
         SWH_GEMM(0, EPI_PLAIN, true);
     }
     if (nm == 1) SWH_GEMM(1, EPI_PLAIN, false);

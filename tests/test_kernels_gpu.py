@@ -1143,6 +1143,57 @@ def test_decode_gemm_folded_norm(ops, dev, M, N, K, silu):
     torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=3e-2)  # rounding of the fold, then SiLU's
 
 
+@pytest.mark.parametrize("M,N,K", [(64, 896, 896), (64, 896, 4864), (37, 896, 4864), (5, 256, 512), (64, 896, 2048)])
+def test_xstream_residual_equals_lds_image_kernel(ops, dev, monkeypatch, M, N, K):
+    """o_proj / down_proj with X fragments streamed into registers
+    (xstream_gemm_kernel) vs decode_gemm_kernel's LDS image (SWH_XSTREAM=0):
+    the new residual rows and their chunk sums of squares are bit-identical
+    (same k split, same wave merge tree), and equal the fp32 reference within
+    bf16 rounding."""
+    from swh_trl_amd import nn_ops
+    g = _gen(43)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(dev)
+    s0 = torch.randn(M, N, generator=g).to(torch.bfloat16).to(dev)
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SWH_XSTREAM", flag)
+        r = s0.clone()
+        ss = torch.full((M, N // 16), float("nan"), device=dev)
+        nn_ops.decode_gemm(x, w, residual=r, ss_out=ss)
+        outs[flag] = (r, ss)
+    torch.cuda.synchronize()
+    assert torch.equal(outs["1"][0], outs["0"][0])
+    assert torch.equal(outs["1"][1], outs["0"][1])
+    ref = s0.float() + (x.float() @ w.float().t()).to(torch.bfloat16).float()
+    torch.testing.assert_close(outs["1"][0].float(), ref, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(outs["1"][1], outs["1"][0].float().view(M, N // 16, 16).pow(2).sum(-1),
+                               rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 1152, 896), (37, 1152, 896), (64, 384, 512), (20, 1152, 896)])
+def test_xstream_qkv_equals_lds_image_kernel(ops, dev, monkeypatch, M, N, K):
+    """The qkv projection (folded RMSNorm row scale from the producer's chunk
+    sums, bias) with X fragments streamed into registers equals
+    decode_gemm_kernel's LDS-image form bit for bit (SWH_XSTREAM=0), and the
+    reference within the fold's rounding."""
+    from swh_trl_amd import nn_ops
+    g = _gen(47)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(dev)
+    nw = (1 + 0.1 * torch.randn(K, generator=g)).to(torch.bfloat16).to(dev)
+    b = (0.1 * torch.randn(N, generator=g)).to(torch.bfloat16).to(dev)
+    ss = _chunk_ss(x)
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SWH_XSTREAM", flag)
+        outs[flag] = nn_ops.decode_gemm(x, w * nw, ss_in=ss, eps=1e-6, bias=b)
+    torch.cuda.synchronize()
+    assert torch.equal(outs["1"], outs["0"])
+    ref = _ref_norm(x, nw, 1e-6).float() @ w.float().t() + b.float()
+    torch.testing.assert_close(outs["1"].float(), ref, rtol=2e-2, atol=3e-2)
+
+
 # --------------------------------------------------------------------------- training attention (csrc/attn.hip)
 def _ref_attention(q, k, v, scale, km=None):
     """fp32 reference: transformers' padded causal mask (a query with no valid

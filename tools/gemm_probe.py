@@ -22,7 +22,8 @@ def build():
         return
     os.makedirs(os.path.dirname(SO), exist_ok=True)
     subprocess.check_call(["hipcc", "-O3", "--offload-arch=gfx950", "-fPIC", "-shared", "-std=c++17",
-                           "-munsafe-fp-atomics", os.path.join(ROOT, "tools", "gemm_probe.hip"), "-o", SO])
+                           "-munsafe-fp-atomics", os.path.join(ROOT, "tools", "gemm_probe.hip"),
+                           os.path.join(ROOT, "swh_trl_amd", "csrc", "wide_gemm.hip"), "-o", SO])
 
 
 def main():
