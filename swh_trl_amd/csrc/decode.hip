@@ -35,6 +35,7 @@ int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, flo
 int64_t wide_gemm_slab_bytes(int64_t M, int64_t N, int64_t K, int32_t silu);
 bool wide_gemm_eligible(int64_t M, int64_t N, int64_t K, int32_t silu);
 int wide_pack(const void *src, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, hipStream_t stream);
+int frag_pack(const void *src, int64_t N, int64_t K, void *dst, hipStream_t stream);
 
 namespace {
 
@@ -162,7 +163,7 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
     const uint16_t *__restrict__ norm_w, float eps, const float *__restrict__ ss_in,
     const uint16_t *__restrict__ bias, uint16_t *__restrict__ res, float *__restrict__ ss_out,
     uint16_t *__restrict__ y, int ldy, float *__restrict__ slabs, int *__restrict__ counters, int persist,
-    int wn) {
+    int wn, int fw) {
     // a wave computes NB = 16 CB columns; the WN column groups of NW / WN waves each
     // make a tile of NBT = WN NB columns (the waves of a group split K)
     constexpr int NB = 16 * CB, MR = 16 * MS, LDR = MR + 4;  // merge slots column-major: b128 parks
@@ -214,9 +215,12 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
             } else {
                 n = n0 + (cg * CB + j) * 16 + rl;
             }
-            wrow[j] = w + (int64_t)n * K + kq;
+            // fw: the swh_frag_pack layout — 16-row group g, k-step ks, lane at ((g KS + ks) 64 + lane) 8
+            wrow[j] = fw ? w + ((int64_t)((n0 + (cg * CB + j) * 16) >> 4) * KS * 64 + lane) * 8
+                         : w + (int64_t)n * K + kq;
         }
     };
+    const int wstep = fw ? 512 : 32;  // elements between a lane's consecutive k-steps
     uint4 bv[kU][CB];
     auto issue = [&](int ks) {  // only this wave's k-steps: no duplicate loads
 #pragma unroll
@@ -224,7 +228,7 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
             if (ks + u < ksw1) {
 #pragma unroll
                 for (int j = 0; j < CB; ++j)  // plain loads: the line's other half is the next k-step's load
-                    bv[u][j] = ld_w(wrow[j] + (ks + u) * 32);
+                    bv[u][j] = ld_w(wrow[j] + (ks + u) * wstep);
             }
         }
     };
@@ -414,7 +418,7 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
                         // its MFMAs have read them, so kU k-steps stay in flight per wave
 #pragma unroll
                         for (int j = 0; j < CB; ++j)
-                            bv[u][j] = ld_w(wrow[j] + (ks + kU + u) * 32);
+                            bv[u][j] = ld_w(wrow[j] + (ks + kU + u) * wstep);
                     }
                 }
             }
@@ -586,7 +590,7 @@ __global__ __launch_bounds__(512) void xstream_gemm_kernel(const uint16_t *__res
                                                            float eps, const float *__restrict__ ss_in,
                                                            const uint16_t *__restrict__ bias,
                                                            uint16_t *__restrict__ res, float *__restrict__ ss_out,
-                                                           uint16_t *__restrict__ y, int ldy) {
+                                                           uint16_t *__restrict__ y, int ldy, int fw) {
     static_assert(EPI != EPI_SILU && NM != 1, "plain / residual epilogues, folded or no norm");
     constexpr int NW = 8, NT = 512, MR = 16 * MS, NB = 16, LDR = MR + 4, G8 = NB / 8, F = NW;
     __shared__ __attribute__((aligned(16))) float part[(NW + 1) * NB * LDR];
@@ -619,7 +623,9 @@ __global__ __launch_bounds__(512) void xstream_gemm_kernel(const uint16_t *__res
         for (int j = 0; j < 8; ++j)
             if (sub + 8 * j < nc) ss8[j] = row[sub + 8 * j];
     }
-    const uint16_t *wr = w + (int64_t)(n0 + rl) * K + kq;
+    // fw: the swh_frag_pack layout (one contiguous 1 KB per wave and k-step)
+    const uint16_t *wr = fw ? w + ((int64_t)(n0 >> 4) * KS * 64 + lane) * 8 : w + (int64_t)(n0 + rl) * K + kq;
+    const int wstep = fw ? 512 : 32;
     const uint16_t *xr[MS];
 #pragma unroll
     for (int i = 0; i < MS; ++i) xr[i] = x + (int64_t)min(m0 + i * 16 + rl, M - 1) * K + kq;
@@ -627,7 +633,7 @@ __global__ __launch_bounds__(512) void xstream_gemm_kernel(const uint16_t *__res
 #pragma unroll
     for (int u = 0; u < KW; ++u) {
         const int ks = min(ksw0 + u, ksw1 - 1);  // past the wave's range: a repeated, unused load (no branch)
-        bv[u] = ld_w(wr + ks * 32);
+        bv[u] = ld_w(wr + ks * wstep);
 #pragma unroll
         for (int i = 0; i < MS; ++i) xa[u][i] = *reinterpret_cast<const uint4 *>(xr[i] + ks * 32);
     }
@@ -1450,6 +1456,7 @@ struct GemmCfg {
     int ms, cb, nw, s, gx;  // 16-row blocks, 16-col blocks (tile), waves, K split, grid.x
     bool persist;
     int wn = 1;             // column groups: a wave computes cb / wn column blocks over K / (nw / wn)
+    int fw = 0;             // weights in the swh_frag_pack layout
 };
 
 int cu_count() {
@@ -1563,7 +1570,7 @@ int launch_gemm_kl(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const
         attr = true;
     }
     decode_gemm_kernel<CB, MS, NM, EPI, BIAS, MAXT, KL><<<grid, 64u * c.nw, lds, s>>>(
-        X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr, c.persist ? 1 : 0, c.wn);
+        X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr, c.persist ? 1 : 0, c.wn, c.fw);
     return launch_status();
 }
 
@@ -1585,7 +1592,7 @@ int launch_xstream_kw(const GemmCfg &c, hipStream_t s, const uint16_t *X, const 
                       float eps, const float *ss_in, const uint16_t *Bs, uint16_t *R, float *ss_out, uint16_t *Y,
                       int ld) {
     xstream_gemm_kernel<KW, MS, NM, EPI, BIAS, 0><<<dim3((unsigned)c.gx), 512, 0, s>>>(X, W, m, n, k, eps, ss_in, Bs, R,
-                                                                                   ss_out, Y, ld);
+                                                                                   ss_out, Y, ld, c.fw);
     return launch_status();
 }
 
@@ -1734,10 +1741,13 @@ extern "C" int64_t swh_decode_gemm_workspace_bytes(int64_t M, int64_t N, int64_t
     return kCounterBytes + (a > b ? a : b);
 }
 
-extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, const void *norm_w,
-                               float eps, const void *bias, void *residual, int32_t silu, void *y, int64_t ldy,
-                               const float *ss_in, float *ss_out, void *workspace, int64_t workspace_bytes,
-                               void *stream) {
+// fw: W in the swh_frag_pack layout (no norm_w, no SiLU, K % 128 == 0): the
+// library-tile and wide paths read row-major weights only, so it takes pick_cfg's
+static int decode_gemm_impl(const void *x, const void *w, int64_t M, int64_t N, int64_t K, const void *norm_w,
+                            float eps, const void *bias, void *residual, int32_t silu, void *y, int64_t ldy,
+                            const float *ss_in, float *ss_out, void *workspace, int64_t workspace_bytes, void *stream,
+                            int fw) {
+    if (fw && (norm_w || silu || K % 128)) return SWH_E_ARG;
     if (!x || !w || M <= 0 || N <= 0 || K <= 0 || K % 64 || M > (1 << 20) || N >= (1 << 29) || K >= (1 << 29))
         return SWH_E_ARG;
     if (residual && (silu || bias)) return SWH_E_ARG;
@@ -1753,7 +1763,7 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int64_t wcols = silu ? 2 * N : N;
     const int nm = norm_w ? 1 : (ss_in ? 2 : 0);
-    if (nm != 1 && K >= wide_gemm_kmin() && wide_gemm_enabled()) {  // the bandwidth regime (8B decode): csrc/wide_gemm.hip
+    if (!fw && nm != 1 && K >= wide_gemm_kmin() && wide_gemm_enabled()) {  // the bandwidth regime (8B decode): csrc/wide_gemm.hip
         const int st = wide_gemm(x, w, M, N, K, eps, ss_in, bias, residual, silu, y, ldy, ss_out, workspace,
                                  workspace_bytes, kCounterBytes, 0, s);
         if (st != 1) return st;
@@ -1764,7 +1774,7 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
         const bool force = e && e[0] == 't';  // tuning: "t" forces the tile kernel
         // gate/up (SiLU tiles) from one tile per CU up: 11.2 vs 12.4 us at N 9728 (tools/bench_decode.py --ku)
         const int64_t min_tiles = (silu ? 1 : 8) * (int64_t)cu_count();
-        if (!residual && K <= 32 * kLmMaxKS && (force || (!e && ntile >= min_tiles))) {
+        if (!fw && !residual && K <= 32 * kLmMaxKS && (force || (!e && ntile >= min_tiles))) {
             const int64_t nmt = (M + 63) / 64;
             const GemmLds L = gemm_lds(1, 64, 8, (int)K, (int)K, nm, false);
             int64_t per = cu_count() / nmt > 0 ? cu_count() / nmt : 1;
@@ -1781,7 +1791,8 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
             return launch_tiles<EPI_PLAIN, false>(nm, grid, lds, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Bs, Y, (int)ldy);
         }
     }
-    const GemmCfg c = pick_cfg(M, wcols, K, silu != 0, nm);
+    GemmCfg c = pick_cfg(M, wcols, K, silu != 0, nm);
+    c.fw = fw;
     const int64_t MR = 16 * c.ms, nmt = (M + MR - 1) / MR, ncb = wcols / (16 * c.cb);
     // workspace: [counters (zeroed once, self-resetting) | fp32 slabs]
     int *ctr = static_cast<int *>(workspace);
@@ -1833,6 +1844,27 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
     if (nm == 2) SWH_GEMM(2, EPI_PLAIN, false);
     SWH_GEMM(0, EPI_PLAIN, false);
 #undef SWH_GEMM
+}
+
+extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, const void *norm_w,
+                               float eps, const void *bias, void *residual, int32_t silu, void *y, int64_t ldy,
+                               const float *ss_in, float *ss_out, void *workspace, int64_t workspace_bytes,
+                               void *stream) {
+    return decode_gemm_impl(x, w, M, N, K, norm_w, eps, bias, residual, silu, y, ldy, ss_in, ss_out, workspace,
+                            workspace_bytes, stream, 0);
+}
+
+extern "C" int swh_decode_gemm_fragw(const void *x, const void *w, int64_t M, int64_t N, int64_t K, float eps,
+                                     const void *bias, void *residual, void *y, int64_t ldy, const float *ss_in,
+                                     float *ss_out, void *workspace, int64_t workspace_bytes, void *stream) {
+    return decode_gemm_impl(x, w, M, N, K, nullptr, eps, bias, residual, 0, y, ldy, ss_in, ss_out, workspace,
+                            workspace_bytes, stream, 1);
+}
+
+extern "C" int swh_frag_pack(const void *w, int64_t N, int64_t K, void *dst, void *stream) {
+    if (!w || !dst || w == dst || N <= 0 || N % 16 || K <= 0 || K % 128) return SWH_E_ARG;
+    if ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(dst)) & 15) return SWH_E_ARG;
+    return frag_pack(w, N, K, dst, static_cast<hipStream_t>(stream));
 }
 
 // [partials (M x per x 8 LmPart) | 256 B: the finalize ticket (zero at allocation)]

@@ -119,6 +119,20 @@ class DecodeEngine:
                     self.packed[name] = torch.empty(N * K * (2 if silu else 1), **bf)
                     if name != "lm" or K > 1024:  # (the fused lm-head sampler, K <= 1024, reads fw["lm"])
                         self.fw.pop(name, None)  # served by the packed copy only
+        # Fragment-order copies of the un-normed short-K projections (o_proj, down_proj at
+        # the 0.5B widths): each weight load of a wave is one contiguous 1 KB run instead of
+        # 16 rows x 64 B (swh_frag_pack / swh_decode_gemm_fragw, bit-identical results);
+        # SWH_FRAGW=0 keeps the row-major weights
+        # (not the shapes decode_gemm hands to the row-major wide GEMM: those keep its result)
+        self.fragw = {}
+        if self.fused and os.environ.get("SWH_FRAGW", "1") != "0":
+            wide_on = os.environ.get("SWH_WIDE_GEMM", "1") != "0"
+            kmin = int(os.environ.get("SWH_WIDE_KMIN", "2048"))
+            for name, (N, K, silu, norm) in self._projections().items():
+                wide = wide_on and K >= kmin and nn_ops.wide_gemm_eligible(B, N, K, silu)
+                if norm is None and not silu and not wide and name not in self.packed and N % 16 == 0 and \
+                        K % 128 == 0:
+                    self.fragw[name] = torch.empty(N, K, **bf)
         self.graph = None
         self.graph_k = None
         self._prefill_graphs = {}
@@ -191,7 +205,9 @@ class DecodeEngine:
         """Re-derive the folded weights from the current parameters (once per
         generate(): the optimizer changes both W and the norm weights) — one
         launch for all row-major folded matrices (swh_fold_norm) and one
-        swh_wide_pack per packed projection."""
+        swh_wide_pack per packed projection, swh_frag_pack per fragment-order copy."""
+        for name, buf in self.fragw.items():
+            nn_ops.frag_pack(self._weight(name), out=buf)
         if not self.fold:
             return
         if not getattr(self, "_fold_built", False):
@@ -216,6 +232,8 @@ class DecodeEngine:
         eps = self.cfg.rms_norm_eps
         if name in self.packed:
             return nn_ops.wide_gemm_packed(x, self.packed[name], self._projections()[name][0], eps=eps, **kw)
+        if name in self.fragw:
+            return nn_ops.decode_gemm_fragw(x, self.fragw[name], eps=eps, **kw)
         norm = self._projections()[name][3]
         if norm is None:
             return nn_ops.decode_gemm(x, self._weight(name), eps=eps, **kw)

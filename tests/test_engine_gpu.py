@@ -603,6 +603,41 @@ def test_shared_prompt_forward_matches_per_row(dev, dtype, left_pad):
     assert rel <= tol, rel
 
 
+def test_fragw_projections_generate_identically(dev, monkeypatch):
+    """DecodeEngine with o_proj / down_proj read from fragment-order copies
+    (swh_frag_pack + swh_decode_gemm_fragw, refreshed every generate()) gives
+    the same tokens and log-probs as the row-major weights (SWH_FRAGW=0),
+    greedy and sampled, also after the weights changed between generations."""
+    from swh_trl_amd.engine import CausalLM, DecodeEngine, tiny_qwen2
+    m = CausalLM(tiny_qwen2(1024, 2), dev, seed=7)
+    g = torch.Generator().manual_seed(7)
+    B, P, C = 16, 12, 24
+    ids = torch.randint(0, m.cfg.vocab_size, (B, P), generator=g).to(dev)
+    mask = torch.ones(B, P, dtype=torch.int64, device=dev)
+    mask[2, :5] = 0
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SWH_FRAGW", flag)
+        eng = DecodeEngine(m, B, P, C)
+        assert ("l1.down_w" in eng.fragw and "l0.o_w" in eng.fragw) == (flag == "1")
+        greedy = eng.generate(ids, mask, C, greedy=True)
+        sampled = eng.generate(ids, mask, C, temperature=0.9, seed=11)
+        with_logp = eng.generate(ids, mask, C, temperature=0.9, seed=12, return_logp=True)
+        orig = m.p["l1.down_w"].clone()
+        with torch.no_grad():
+            m.p["l1.down_w"].mul_(1.5)  # a changed weight must reach the packed copy
+        after = eng.generate(ids, mask, C, greedy=True)
+        with torch.no_grad():
+            m.p["l1.down_w"].copy_(orig)
+        outs[flag] = (greedy, sampled, with_logp, after)
+        del eng
+    for a, b in zip(outs["1"], outs["0"]):
+        for x, y in zip(a, b):
+            if isinstance(x, torch.Tensor):
+                assert torch.equal(x, y)
+
+
+
 @pytest.mark.parametrize("kmin", ["2048", "1024"])
 def test_packed_wide_projections_generate_identically(dev, monkeypatch, kmin):
     """DecodeEngine with the bandwidth-regime projections on packed weights

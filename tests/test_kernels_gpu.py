@@ -1171,6 +1171,42 @@ def test_xstream_residual_equals_lds_image_kernel(ops, dev, monkeypatch, M, N, K
                                rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("M,N,K,kind", [(64, 896, 896, "res"), (64, 896, 4864, "res"), (37, 896, 4864, "res"),
+                                        (5, 256, 512, "res"), (64, 1152, 896, "qkv"), (37, 1152, 896, "qkv"),
+                                        (64, 256, 1024, "plain")])
+@pytest.mark.parametrize("cfg", [None, "1,1,2", "2,1,1", "4,2,1,1"])
+def test_decode_gemm_fragw_equals_row_major(ops, dev, monkeypatch, M, N, K, kind, cfg):
+    """swh_frag_pack's layout element for element against a torch restatement,
+    and swh_decode_gemm_fragw on it bit-identical to swh_decode_gemm on the
+    row-major weight: residual + chunk sums of squares (o / down), folded norm
+    + bias (qkv), plain — under the cost model's geometry and forced split-K /
+    32-row / persistent ones (SWH_GEMM_CFG)."""
+    from swh_trl_amd import nn_ops
+    g = _gen(53)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(dev)
+    wp = nn_ops.frag_pack(w)
+    # restatement: element ((grp KS + ks) 64 + lane) 8 + e = W[16 grp + lane % 16, 32 ks + 8 (lane / 16) + e]
+    ref = w.view(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(N, K)
+    assert torch.equal(wp, ref)
+    if cfg:
+        monkeypatch.setenv("SWH_GEMM_CFG", cfg)
+    outs = []
+    for fw in (True, False):
+        kw = {}
+        if kind == "res":
+            kw = dict(residual=torch.randn(M, N, generator=_gen(5)).to(torch.bfloat16).to(dev),
+                      ss_out=torch.full((M, N // 16), float("nan"), device=dev))
+        elif kind == "qkv":
+            kw = dict(bias=(0.1 * torch.randn(N, generator=_gen(6))).to(torch.bfloat16).to(dev), ss_in=_chunk_ss(x))
+        out = (nn_ops.decode_gemm_fragw(x, wp, eps=1e-6, **kw) if fw else nn_ops.decode_gemm(x, w, eps=1e-6, **kw))
+        outs.append((out, kw.get("ss_out")))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    if kind == "res":
+        assert torch.equal(outs[0][1], outs[1][1])
+
+
 @pytest.mark.parametrize("M,N,K", [(64, 1152, 896), (37, 1152, 896), (64, 384, 512), (20, 1152, 896)])
 def test_xstream_qkv_equals_lds_image_kernel(ops, dev, monkeypatch, M, N, K):
     """The qkv projection (folded RMSNorm row scale from the producer's chunk
