@@ -442,18 +442,20 @@ int swh_wide_gemm_packed(const void *x, const void *w, int64_t M, int64_t N, int
                          void *workspace, int64_t workspace_bytes, void *stream);
 
 /* swh_decode_gemm over a weight in the MFMA-fragment order (the Qwen2.5-0.5B
- * o_proj / down_proj of the decode step; same reference call sites as
+ * decode projections: qkv, o, gate/up, down; same reference call sites as
  * swh_decode_gemm, trl/trainer/grpo_trainer.py:1114-1130): swh_frag_pack
- * writes W [N, K] (N % 16 == 0, K % 128 == 0) as swh_wide_pack does without a
- * norm — per 16-row group and 32-wide k-step, the 64 lanes' 16-B fragments
- * contiguous — so each weight load of a wave is one 1 KB run instead of 16
- * rows x 64 B.  swh_decode_gemm_fragw then computes what swh_decode_gemm
- * computes on the row-major W with norm_w == NULL and silu == 0
- * (bit-identical): residual / bias / folded-norm row scale (ss_in) epilogues. */
-int swh_frag_pack(const void *w, int64_t N, int64_t K, void *dst, void *stream);
+ * writes W [N, K] ([2N, K] gate|up with silu; K % 128 == 0), or the folded-norm
+ * weight bf16(W * norm_w), in swh_wide_pack's order for any 16-row group
+ * count — per 16-row group (8 gate + 8 up rows with silu) and 32-wide k-step,
+ * the 64 lanes' 16-B fragments contiguous — so each weight load of a wave is
+ * one 1 KB run instead of 16 rows x 64 B.  swh_decode_gemm_fragw then computes
+ * what swh_decode_gemm computes on the row-major W with norm_w == NULL
+ * (bit-identical): residual, bias, SiLU-gate and folded-norm row scale (ss_in)
+ * epilogues. */
+int swh_frag_pack(const void *w, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, void *stream);
 int swh_decode_gemm_fragw(const void *x, const void *w, int64_t M, int64_t N, int64_t K, float eps, const void *bias,
-                          void *residual, void *y, int64_t ldy, const float *ss_in, float *ss_out, void *workspace,
-                          int64_t workspace_bytes, void *stream);
+                          void *residual, int32_t silu, void *y, int64_t ldy, const float *ss_in, float *ss_out,
+                          void *workspace, int64_t workspace_bytes, void *stream);
 
 /* Decode lm head with the sampler fused into its epilogue: RMSNorm(X) W^T
  * (as swh_decode_gemm with norm_w / ss_in) and, per row, the token that

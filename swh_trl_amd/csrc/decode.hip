@@ -35,7 +35,7 @@ int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, flo
 int64_t wide_gemm_slab_bytes(int64_t M, int64_t N, int64_t K, int32_t silu);
 bool wide_gemm_eligible(int64_t M, int64_t N, int64_t K, int32_t silu);
 int wide_pack(const void *src, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, hipStream_t stream);
-int frag_pack(const void *src, int64_t N, int64_t K, void *dst, hipStream_t stream);
+int frag_pack(const void *src, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, hipStream_t stream);
 
 namespace {
 
@@ -216,8 +216,9 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
                 n = n0 + (cg * CB + j) * 16 + rl;
             }
             // fw: the swh_frag_pack layout — 16-row group g, k-step ks, lane at ((g KS + ks) 64 + lane) 8
-            wrow[j] = fw ? w + ((int64_t)((n0 + (cg * CB + j) * 16) >> 4) * KS * 64 + lane) * 8
-                         : w + (int64_t)n * K + kq;
+            // (SiLU: a 16-lane group is 8 gate + the 8 matching up rows = pack group (first gate row) / 8)
+            const int64_t grp = (EPI == EPI_SILU) ? (n0 + (cg * CB + j) * 8) >> 3 : (n0 + (cg * CB + j) * 16) >> 4;
+            wrow[j] = fw ? w + (grp * KS * 64 + lane) * 8 : w + (int64_t)n * K + kq;
         }
     };
     const int wstep = fw ? 512 : 32;  // elements between a lane's consecutive k-steps
@@ -747,6 +748,7 @@ struct LmSample {
     const int32_t *step;
     LmPart *part;  // [M][pstride]
     int pstride;
+    int fw = 0;    // weights in the swh_frag_pack layout (tile t = 16-row group t)
 };
 
 // KSC: K / 32 at compile time (0 = read from K): with a constant trip count the
@@ -780,11 +782,16 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
         if constexpr (EPI == EPI_SILU) return (rl < 8) ? tile * 8 + rl : N + tile * 8 + rl - 8;  // gate, then up
         return (int64_t)tile * 16 + rl;
     };
+    // fw: tile t's fragments for k-step ks at ((t KS + ks) 64 + lane) 8 (one 1 KB run per load)
+    const int wst = smp.fw ? 512 : 32;
+    auto wbase = [&](int tile) -> const uint16_t * {
+        return smp.fw ? w + ((int64_t)tile * KS * 64 + lane) * 8 : w + wrow_of(tile) * K + kq;
+    };
     auto issue = [&](int tile) {
-        const uint16_t *wr = w + wrow_of(tile) * K + kq;
+        const uint16_t *wr = wbase(tile);
 #pragma unroll
         for (int ks = 0; ks < KSA; ++ks)
-            if (KSC || ks < KS) bv[ks] = ld_w(wr + ks * 32);
+            if (KSC || ks < KS) bv[ks] = ld_w(wr + ks * wst);
     };
     if (t < ntile) issue(t);  // the weight stream first
     // RMSNorm partials and norm weights (L2), then the X image by LDS-DMA
@@ -930,7 +937,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
         // ring refill: k-step ks's weight register takes the next tile's fragment as
         // soon as its MFMA has read it, so a wave always has KS loads in flight
         const bool ring = SWH_LM_RING && KSC != 0 && t + tstep < ntile;
-        const uint16_t *wnext = w + wrow_of(ring ? t + tstep : t) * K + kq;
+        const uint16_t *wnext = wbase(ring ? t + tstep : t);
         if constexpr (KSC != 0) {
             // A fragments double-buffered one k-step ahead; the scheduling barrier
             // keeps the compiler from hoisting every read (register pressure)
@@ -948,7 +955,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
                 for (int i = 0; i < 4; ++i)
                     acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[ks & 1][i]), as_bf16x8(bv[ks]),
                                                                     acc[i], 0, 0, 0);
-                if (ring) bv[ks] = ld_w(wnext + ks * 32);
+                if (ring) bv[ks] = ld_w(wnext + ks * wst);
                 __builtin_amdgcn_sched_barrier(0);
             }
         } else {
@@ -1678,8 +1685,10 @@ int launch_lm(dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uin
 // the tile kernel for plain / bias / SiLU epilogues
 template <int EPI, bool BIAS>
 int launch_tiles(int nm, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W, int M, int N,
-                 int K, const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs, uint16_t *Y, int ldy) {
-    const LmSample none{};
+                 int K, const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs, uint16_t *Y, int ldy,
+                 int fw) {
+    LmSample none{};
+    none.fw = fw;
     if (nm == 1) return launch_lm<1, EPI, BIAS, false>(grid, lds, s, X, W, M, N, K, NWt, eps, ss_in, Bs, Y, ldy, none);
     if (nm == 2) return launch_lm<2, EPI, BIAS, false>(grid, lds, s, X, W, M, N, K, nullptr, eps, ss_in, Bs, Y, ldy, none);
     return launch_lm<0, EPI, BIAS, false>(grid, lds, s, X, W, M, N, K, nullptr, eps, nullptr, Bs, Y, ldy, none);
@@ -1741,13 +1750,13 @@ extern "C" int64_t swh_decode_gemm_workspace_bytes(int64_t M, int64_t N, int64_t
     return kCounterBytes + (a > b ? a : b);
 }
 
-// fw: W in the swh_frag_pack layout (no norm_w, no SiLU, K % 128 == 0): the
-// library-tile and wide paths read row-major weights only, so it takes pick_cfg's
+// fw: W in the swh_frag_pack layout (no norm_w, K % 128 == 0): the wide path
+// reads row-major or its own packed weights only, so fw skips it
 static int decode_gemm_impl(const void *x, const void *w, int64_t M, int64_t N, int64_t K, const void *norm_w,
                             float eps, const void *bias, void *residual, int32_t silu, void *y, int64_t ldy,
                             const float *ss_in, float *ss_out, void *workspace, int64_t workspace_bytes, void *stream,
                             int fw) {
-    if (fw && (norm_w || silu || K % 128)) return SWH_E_ARG;
+    if (fw && (norm_w || K % 128)) return SWH_E_ARG;
     if (!x || !w || M <= 0 || N <= 0 || K <= 0 || K % 64 || M > (1 << 20) || N >= (1 << 29) || K >= (1 << 29))
         return SWH_E_ARG;
     if (residual && (silu || bias)) return SWH_E_ARG;
@@ -1774,7 +1783,7 @@ static int decode_gemm_impl(const void *x, const void *w, int64_t M, int64_t N, 
         const bool force = e && e[0] == 't';  // tuning: "t" forces the tile kernel
         // gate/up (SiLU tiles) from one tile per CU up: 11.2 vs 12.4 us at N 9728 (tools/bench_decode.py --ku)
         const int64_t min_tiles = (silu ? 1 : 8) * (int64_t)cu_count();
-        if (!fw && !residual && K <= 32 * kLmMaxKS && (force || (!e && ntile >= min_tiles))) {
+        if (!residual && K <= 32 * kLmMaxKS && (force || (!e && ntile >= min_tiles))) {
             const int64_t nmt = (M + 63) / 64;
             const GemmLds L = gemm_lds(1, 64, 8, (int)K, (int)K, nm, false);
             int64_t per = cu_count() / nmt > 0 ? cu_count() / nmt : 1;
@@ -1786,9 +1795,9 @@ static int decode_gemm_impl(const void *x, const void *w, int64_t M, int64_t N, 
             const auto *Bs = static_cast<const uint16_t *>(bias);
             auto *Y = static_cast<uint16_t *>(y);
             const size_t lds = (size_t)L.total;
-            if (silu) return launch_tiles<EPI_SILU, false>(nm, grid, lds, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Bs, Y, (int)ldy);
-            if (Bs) return launch_tiles<EPI_PLAIN, true>(nm, grid, lds, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Bs, Y, (int)ldy);
-            return launch_tiles<EPI_PLAIN, false>(nm, grid, lds, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Bs, Y, (int)ldy);
+            if (silu) return launch_tiles<EPI_SILU, false>(nm, grid, lds, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Bs, Y, (int)ldy, fw);
+            if (Bs) return launch_tiles<EPI_PLAIN, true>(nm, grid, lds, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Bs, Y, (int)ldy, fw);
+            return launch_tiles<EPI_PLAIN, false>(nm, grid, lds, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Bs, Y, (int)ldy, fw);
         }
     }
     GemmCfg c = pick_cfg(M, wcols, K, silu != 0, nm);
@@ -1855,16 +1864,20 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
 }
 
 extern "C" int swh_decode_gemm_fragw(const void *x, const void *w, int64_t M, int64_t N, int64_t K, float eps,
-                                     const void *bias, void *residual, void *y, int64_t ldy, const float *ss_in,
-                                     float *ss_out, void *workspace, int64_t workspace_bytes, void *stream) {
-    return decode_gemm_impl(x, w, M, N, K, nullptr, eps, bias, residual, 0, y, ldy, ss_in, ss_out, workspace,
+                                     const void *bias, void *residual, int32_t silu, void *y, int64_t ldy,
+                                     const float *ss_in, float *ss_out, void *workspace, int64_t workspace_bytes,
+                                     void *stream) {
+    return decode_gemm_impl(x, w, M, N, K, nullptr, eps, bias, residual, silu, y, ldy, ss_in, ss_out, workspace,
                             workspace_bytes, stream, 1);
 }
 
-extern "C" int swh_frag_pack(const void *w, int64_t N, int64_t K, void *dst, void *stream) {
-    if (!w || !dst || w == dst || N <= 0 || N % 16 || K <= 0 || K % 128) return SWH_E_ARG;
-    if ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(dst)) & 15) return SWH_E_ARG;
-    return frag_pack(w, N, K, dst, static_cast<hipStream_t>(stream));
+extern "C" int swh_frag_pack(const void *w, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst,
+                             void *stream) {
+    const int64_t rows = silu ? 2 * N : N;
+    if (!w || !dst || w == dst || N <= 0 || rows % 16 || (silu && N % 8) || K <= 0 || K % 128) return SWH_E_ARG;
+    if ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(norm_w)) & 15)
+        return SWH_E_ARG;
+    return frag_pack(w, norm_w, N, K, silu, dst, static_cast<hipStream_t>(stream));
 }
 
 // [partials (M x per x 8 LmPart) | 256 B: the finalize ticket (zero at allocation)]

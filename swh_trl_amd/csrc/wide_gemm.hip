@@ -501,10 +501,11 @@ __global__ __launch_bounds__(256) void wide_pack_kernel(const uint16_t *__restri
 }  // namespace
 
 // the same fragment order for any 16-row group count (decode_gemm / xstream with fw)
-int frag_pack(const void *src, int64_t N, int64_t K, void *dst, hipStream_t st) {
-    const int64_t npieces = N * K / 8;
+int frag_pack(const void *src, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, hipStream_t st) {
+    const int64_t npieces = (silu ? 2 * N : N) * K / 8;
     const int64_t grid = (npieces + 255) / 256 < 8192 ? (npieces + 255) / 256 : 8192;
-    wide_pack_kernel<<<dim3((unsigned)grid), 256, 0, st>>>(static_cast<const uint16_t *>(src), nullptr, N, K, 0,
+    wide_pack_kernel<<<dim3((unsigned)grid), 256, 0, st>>>(static_cast<const uint16_t *>(src),
+                                                             static_cast<const uint16_t *>(norm_w), N, K, silu,
                                                              static_cast<uint16_t *>(dst), npieces);
     return launch_status();
 }

@@ -119,20 +119,24 @@ class DecodeEngine:
                     self.packed[name] = torch.empty(N * K * (2 if silu else 1), **bf)
                     if name != "lm" or K > 1024:  # (the fused lm-head sampler, K <= 1024, reads fw["lm"])
                         self.fw.pop(name, None)  # served by the packed copy only
-        # Fragment-order copies of the un-normed short-K projections (o_proj, down_proj at
-        # the 0.5B widths): each weight load of a wave is one contiguous 1 KB run instead of
-        # 16 rows x 64 B (swh_frag_pack / swh_decode_gemm_fragw, bit-identical results);
-        # SWH_FRAGW=0 keeps the row-major weights
-        # (not the shapes decode_gemm hands to the row-major wide GEMM: those keep its result)
+        # Fragment-order copies of the per-layer projections at the 0.5B widths (qkv and
+        # gate/up folded with their RMSNorm weight, o, down): each weight load of a wave is
+        # one contiguous 1 KB run instead of 16 rows x 64 B (swh_frag_pack /
+        # swh_decode_gemm_fragw, bit-identical results); SWH_FRAGW=0 keeps the row-major
+        # weights.  Not the shapes decode_gemm hands to the row-major wide GEMM (those keep
+        # its result), nor the lm head (the fused sampler reads fw["lm"]).
         self.fragw = {}
         if self.fused and os.environ.get("SWH_FRAGW", "1") != "0":
             wide_on = os.environ.get("SWH_WIDE_GEMM", "1") != "0"
             kmin = int(os.environ.get("SWH_WIDE_KMIN", "2048"))
             for name, (N, K, silu, norm) in self._projections().items():
+                if name == "lm" or (norm is not None and not self.fold):
+                    continue
                 wide = wide_on and K >= kmin and nn_ops.wide_gemm_eligible(B, N, K, silu)
-                if norm is None and not silu and not wide and name not in self.packed and N % 16 == 0 and \
-                        K % 128 == 0:
-                    self.fragw[name] = torch.empty(N, K, **bf)
+                rows = 2 * N if silu else N
+                if not wide and name not in self.packed and rows % 16 == 0 and K % 128 == 0:
+                    self.fragw[name] = torch.empty(rows, K, **bf)
+                    self.fw.pop(name, None)  # served by the fragment-order copy only
         self.graph = None
         self.graph_k = None
         self._prefill_graphs = {}
@@ -206,8 +210,10 @@ class DecodeEngine:
         generate(): the optimizer changes both W and the norm weights) — one
         launch for all row-major folded matrices (swh_fold_norm) and one
         swh_wide_pack per packed projection, swh_frag_pack per fragment-order copy."""
+        projs = self._projections()
         for name, buf in self.fragw.items():
-            nn_ops.frag_pack(self._weight(name), out=buf)
+            N, K, silu, norm = projs[name]
+            nn_ops.frag_pack(self._weight(name), self.model.p[norm] if norm else None, silu=silu, out=buf)
         if not self.fold:
             return
         if not getattr(self, "_fold_built", False):
@@ -250,7 +256,7 @@ class DecodeEngine:
         for i in range(c.num_hidden_layers):
             self._proj(f"l{i}.qkv_w", self.s, bias=p.get(f"l{i}.qkv_b"), y=self.qkv, ss_in=ss)
             pf = self._normed(f"l{i}.gu_w", f"l{i}.ln_post")[0] if self.prefetch and f"l{i}.gu_w" not in \
-                self.packed else None
+                self.packed and f"l{i}.gu_w" not in self.fragw else None
             nn_ops.attn_decode(self.qkv, self.kv[i, 0], self.kv[i, 1], self.cos, self.sin, self.plen, self.state,
                                c.num_attention_heads, c.num_key_value_heads, c.head_dim, c.head_dim ** -0.5,
                                out=self.att, prefetch_gate_up=pf, prompt_row=self.prow)
@@ -379,6 +385,7 @@ class DecodeEngine:
                                                          out=self.att,
                                                          prefetch_gate_up=self._normed(f"l{i}.gu_w", "")[0]
                                                          if self.prefetch and f"l{i}.gu_w" not in self.packed
+                                                         and f"l{i}.gu_w" not in self.fragw
                                                          else None, prompt_row=self.prow),
                             att_bytes, L),
             "decode_gemm.o": (lambda i: self._proj(f"l{i}.o_w", self.att, residual=self.s, ss_out=ss),

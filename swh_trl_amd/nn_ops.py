@@ -161,31 +161,34 @@ def decode_gemm(x: torch.Tensor, w: torch.Tensor, *, norm_w: Optional[torch.Tens
     return residual if residual is not None else y
 
 
-def frag_pack(w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """w [N, K] (N % 16 == 0, K % 128 == 0) in the MFMA-fragment order that
-    decode_gemm(fragw=True) reads (swh_frag_pack); same shape as w."""
+def frag_pack(w: torch.Tensor, norm_w: Optional[torch.Tensor] = None, *, silu: bool = False,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """w [N, K] ([2N, K] gate|up with silu; K % 128 == 0), optionally folded
+    with the RMSNorm weight, in the MFMA-fragment order decode_gemm_fragw reads
+    (swh_frag_pack); same shape as w."""
     _dev(w, "frag_pack")
-    N, K = w.shape
+    rows, K = w.shape
+    N = rows // 2 if silu else rows
     out = torch.empty_like(w) if out is None else out
-    call("swh_frag_pack", w.data_ptr(), N, K, out.data_ptr(), _stream())
+    call("swh_frag_pack", w.data_ptr(), _p(norm_w), N, K, int(bool(silu)), out.data_ptr(), _stream())
     return out
 
 
 def decode_gemm_fragw(x: torch.Tensor, w: torch.Tensor, *, eps: float = 1e-6, bias: Optional[torch.Tensor] = None,
-                      residual: Optional[torch.Tensor] = None, y: Optional[torch.Tensor] = None,
+                      residual: Optional[torch.Tensor] = None, silu: bool = False, y: Optional[torch.Tensor] = None,
                       workspace: Optional[torch.Tensor] = None, ss_in: Optional[torch.Tensor] = None,
                       ss_out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """decode_gemm (no norm_w, no SiLU) over w packed by frag_pack [N, K]
-    (include/swh_trl_amd.h swh_decode_gemm_fragw): bit-identical results."""
+    """decode_gemm (no norm_w) over w packed by frag_pack ([N, K], [2N, K] with
+    silu) (include/swh_trl_amd.h swh_decode_gemm_fragw): bit-identical results."""
     _dev(x, "decode_gemm_fragw")
     M, K = x.shape
-    N = w.shape[0]
+    N = w.shape[0] // 2 if silu else w.shape[0]
     if residual is None and y is None:
         y = torch.empty(M, N, device=x.device, dtype=x.dtype)
     ldy = residual.stride(0) if residual is not None else y.stride(0)
     ws = workspace if workspace is not None else gemm_workspace(x.device)
-    call("swh_decode_gemm_fragw", x.data_ptr(), w.data_ptr(), M, N, K, float(eps), _p(bias), _p(residual), _p(y),
-         ldy, _p(ss_in), _p(ss_out), ws.data_ptr(), ws.numel(), _stream())
+    call("swh_decode_gemm_fragw", x.data_ptr(), w.data_ptr(), M, N, K, float(eps), _p(bias), _p(residual),
+         int(bool(silu)), _p(y), ldy, _p(ss_in), _p(ss_out), ws.data_ptr(), ws.numel(), _stream())
     return residual if residual is not None else y
 
 

@@ -1173,7 +1173,8 @@ def test_xstream_residual_equals_lds_image_kernel(ops, dev, monkeypatch, M, N, K
 
 @pytest.mark.parametrize("M,N,K,kind", [(64, 896, 896, "res"), (64, 896, 4864, "res"), (37, 896, 4864, "res"),
                                         (5, 256, 512, "res"), (64, 1152, 896, "qkv"), (37, 1152, 896, "qkv"),
-                                        (64, 256, 1024, "plain")])
+                                        (64, 256, 1024, "plain"), (64, 4864, 896, "silu"), (37, 4864, 896, "silu"),
+                                        (16, 512, 256, "silu")])
 @pytest.mark.parametrize("cfg", [None, "1,1,2", "2,1,1", "4,2,1,1"])
 def test_decode_gemm_fragw_equals_row_major(ops, dev, monkeypatch, M, N, K, kind, cfg):
     """swh_frag_pack's layout element for element against a torch restatement,
@@ -1189,6 +1190,14 @@ def test_decode_gemm_fragw_equals_row_major(ops, dev, monkeypatch, M, N, K, kind
     # restatement: element ((grp KS + ks) 64 + lane) 8 + e = W[16 grp + lane % 16, 32 ks + 8 (lane / 16) + e]
     ref = w.view(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(N, K)
     assert torch.equal(wp, ref)
+    if kind == "silu":  # 16-row groups of 8 gate + the 8 matching up rows, folded with the norm weight
+        nw = (1 + 0.1 * torch.randn(K, generator=g)).to(torch.bfloat16).to(dev)
+        wu = torch.cat([w, w.flip(0)])
+        wp = nn_ops.frag_pack(wu, nw, silu=True)
+        inter = torch.stack([wu[:N].view(N // 8, 8, K), wu[N:].view(N // 8, 8, K)], 1).reshape(2 * N, K)
+        ref = (inter.float() * nw.float()).to(torch.bfloat16)
+        assert torch.equal(wp, ref.view(2 * N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(2 * N, K))
+        w = (wu.float() * nw.float()).to(torch.bfloat16)
     if cfg:
         monkeypatch.setenv("SWH_GEMM_CFG", cfg)
     outs = []
@@ -1199,6 +1208,8 @@ def test_decode_gemm_fragw_equals_row_major(ops, dev, monkeypatch, M, N, K, kind
                       ss_out=torch.full((M, N // 16), float("nan"), device=dev))
         elif kind == "qkv":
             kw = dict(bias=(0.1 * torch.randn(N, generator=_gen(6))).to(torch.bfloat16).to(dev), ss_in=_chunk_ss(x))
+        elif kind == "silu":
+            kw = dict(silu=True, ss_in=_chunk_ss(x))
         out = (nn_ops.decode_gemm_fragw(x, wp, eps=1e-6, **kw) if fw else nn_ops.decode_gemm(x, w, eps=1e-6, **kw))
         outs.append((out, kw.get("ss_out")))
     torch.cuda.synchronize()
