@@ -125,7 +125,7 @@ def cpu_cfg1(threads: int, steps: int = 2) -> dict:
                       f"{steps} steps in {wall:.3f}s"}
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r2_pmc_decode.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r2_v5_pmc_decode.json")
 
 
 def pmc_traffic(kernel: str):
