@@ -486,6 +486,17 @@ int swh_lm_head_sample_step(const void *x, const void *w, int64_t M, int64_t V, 
                             int32_t *step, int32_t *finished, int64_t *out_tokens, int64_t out_ld,
                             int64_t *cur_tokens, const void *embed, void *x_next, float *ss_next, void *workspace,
                             int64_t workspace_bytes, void *stream);
+/* The two entries above over the folded lm-head weight packed by swh_frag_pack
+ * (norm_w NULL: the row scale comes from ss_in; K % 128 == 0): same draws. */
+int swh_lm_head_sample_fragw(const void *x, const void *w, int64_t M, int64_t V, int64_t K, float eps,
+                             const float *ss_in, const swh_sample_params *params, const uint64_t *rng,
+                             const int32_t *step, int32_t *finished, int64_t *out_tokens, int64_t out_ld,
+                             int64_t *cur_tokens, void *workspace, int64_t workspace_bytes, void *stream);
+int swh_lm_head_sample_step_fragw(const void *x, const void *w, int64_t M, int64_t V, int64_t K, float eps,
+                                  const float *ss_in, const swh_sample_params *params, const uint64_t *rng,
+                                  int32_t *step, int32_t *finished, int64_t *out_tokens, int64_t out_ld,
+                                  int64_t *cur_tokens, const void *embed, void *x_next, float *ss_next,
+                                  void *workspace, int64_t workspace_bytes, void *stream);
 
 /* ---- GPT-2 family (BASELINE.json config 1) --------------------------------
  * transformers GPT2Block's LayerNorms and NewGELUActivation (the modeling code

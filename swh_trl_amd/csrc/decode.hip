@@ -1895,7 +1895,9 @@ extern "C" int64_t swh_lm_head_sample_workspace_bytes(int64_t M, int64_t V, int6
 static int lm_head_sample_impl(const void *x, const void *w, int64_t M, int64_t V, int64_t K, const void *norm_w,
                                float eps, const float *ss_in, const swh_sample_params *params, const uint64_t *rng,
                                const int32_t *step, int32_t *finished, int64_t *out_tokens, int64_t out_ld,
-                               int64_t *cur_tokens, void *workspace, int64_t workspace_bytes, LmNext nx, void *stream) {
+                               int64_t *cur_tokens, void *workspace, int64_t workspace_bytes, LmNext nx, void *stream,
+                               int fw = 0) {
+    if (fw && (norm_w || K % 128)) return SWH_E_ARG;  // fragment order: folded weight (ss_in row scale) only
     if (!x || !w || !params || !rng || !step || !finished || !out_tokens || !workspace || M <= 0 || V <= 0 ||
         K <= 0 || K % 64 || K > 32 * kLmMaxKS || V % 16 || V >= ((int64_t)1 << 31) || M > (1 << 20))
         return SWH_E_ARG;
@@ -1912,7 +1914,7 @@ static int lm_head_sample_impl(const void *x, const void *w, int64_t M, int64_t 
     const int nm = norm_w ? 1 : (ss_in ? 2 : 0);
     const GemmLds L = gemm_lds(1, 64, 8, (int)K, (int)K, nm, false);
     const dim3 grid((unsigned)(per * nmt));
-    LmSample smp{p, rng, step, static_cast<LmPart *>(workspace), (int)per};  // one partial per (row, workgroup)
+    LmSample smp{p, rng, step, static_cast<LmPart *>(workspace), (int)per, fw};  // one partial per (row, workgroup)
     const auto *X = static_cast<const uint16_t *>(x);
     const auto *W = static_cast<const uint16_t *>(w);
     const auto *NWt = static_cast<const uint16_t *>(norm_w);
@@ -1972,17 +1974,45 @@ extern "C" int swh_lm_head_sample(const void *x, const void *w, int64_t M, int64
                                cur_tokens, workspace, workspace_bytes, LmNext{}, stream);
 }
 
-extern "C" int swh_lm_head_sample_step(const void *x, const void *w, int64_t M, int64_t V, int64_t K,
-                                       const void *norm_w, float eps, const float *ss_in,
-                                       const swh_sample_params *params, const uint64_t *rng, int32_t *step,
-                                       int32_t *finished, int64_t *out_tokens, int64_t out_ld, int64_t *cur_tokens,
-                                       const void *embed, void *x_next, float *ss_next, void *workspace,
-                                       int64_t workspace_bytes, void *stream) {
+static int lm_head_sample_step_impl(const void *x, const void *w, int64_t M, int64_t V, int64_t K,
+                                    const void *norm_w, float eps, const float *ss_in,
+                                    const swh_sample_params *params, const uint64_t *rng, int32_t *step,
+                                    int32_t *finished, int64_t *out_tokens, int64_t out_ld, int64_t *cur_tokens,
+                                    const void *embed, void *x_next, float *ss_next, void *workspace,
+                                    int64_t workspace_bytes, void *stream, int fw) {
     if (!embed || !x_next || !cur_tokens || K % 16) return SWH_E_ARG;
     if ((reinterpret_cast<uintptr_t>(embed) | reinterpret_cast<uintptr_t>(x_next)) & 15) return SWH_E_ARG;
     if (workspace_bytes < swh_lm_head_sample_workspace_bytes(M, V, K)) return SWH_E_ARG;
     LmNext nx{static_cast<const uint16_t *>(embed), static_cast<uint16_t *>(x_next), ss_next, step,
               reinterpret_cast<int32_t *>(static_cast<char *>(workspace) + lm_part_bytes(M)), (int)K, (int)M};
     return lm_head_sample_impl(x, w, M, V, K, norm_w, eps, ss_in, params, rng, step, finished, out_tokens, out_ld,
-                               cur_tokens, workspace, workspace_bytes, nx, stream);
+                               cur_tokens, workspace, workspace_bytes, nx, stream, fw);
+}
+
+extern "C" int swh_lm_head_sample_step(const void *x, const void *w, int64_t M, int64_t V, int64_t K,
+                                       const void *norm_w, float eps, const float *ss_in,
+                                       const swh_sample_params *params, const uint64_t *rng, int32_t *step,
+                                       int32_t *finished, int64_t *out_tokens, int64_t out_ld, int64_t *cur_tokens,
+                                       const void *embed, void *x_next, float *ss_next, void *workspace,
+                                       int64_t workspace_bytes, void *stream) {
+    return lm_head_sample_step_impl(x, w, M, V, K, norm_w, eps, ss_in, params, rng, step, finished, out_tokens,
+                                    out_ld, cur_tokens, embed, x_next, ss_next, workspace, workspace_bytes, stream, 0);
+}
+
+extern "C" int swh_lm_head_sample_fragw(const void *x, const void *w, int64_t M, int64_t V, int64_t K, float eps,
+                                        const float *ss_in, const swh_sample_params *params, const uint64_t *rng,
+                                        const int32_t *step, int32_t *finished, int64_t *out_tokens, int64_t out_ld,
+                                        int64_t *cur_tokens, void *workspace, int64_t workspace_bytes, void *stream) {
+    return lm_head_sample_impl(x, w, M, V, K, nullptr, eps, ss_in, params, rng, step, finished, out_tokens, out_ld,
+                               cur_tokens, workspace, workspace_bytes, LmNext{}, stream, 1);
+}
+
+extern "C" int swh_lm_head_sample_step_fragw(const void *x, const void *w, int64_t M, int64_t V, int64_t K,
+                                             float eps, const float *ss_in, const swh_sample_params *params,
+                                             const uint64_t *rng, int32_t *step, int32_t *finished,
+                                             int64_t *out_tokens, int64_t out_ld, int64_t *cur_tokens,
+                                             const void *embed, void *x_next, float *ss_next, void *workspace,
+                                             int64_t workspace_bytes, void *stream) {
+    return lm_head_sample_step_impl(x, w, M, V, K, nullptr, eps, ss_in, params, rng, step, finished, out_tokens,
+                                    out_ld, cur_tokens, embed, x_next, ss_next, workspace, workspace_bytes, stream, 1);
 }

@@ -124,13 +124,13 @@ class DecodeEngine:
         # one contiguous 1 KB run instead of 16 rows x 64 B (swh_frag_pack /
         # swh_decode_gemm_fragw, bit-identical results); SWH_FRAGW=0 keeps the row-major
         # weights.  Not the shapes decode_gemm hands to the row-major wide GEMM (those keep
-        # its result), nor the lm head (the fused sampler reads fw["lm"]).
+        # its result).  The lm head's copy serves the fused sampler and the logits path alike.
         self.fragw = {}
         if self.fused and os.environ.get("SWH_FRAGW", "1") != "0":
             wide_on = os.environ.get("SWH_WIDE_GEMM", "1") != "0"
             kmin = int(os.environ.get("SWH_WIDE_KMIN", "2048"))
             for name, (N, K, silu, norm) in self._projections().items():
-                if name == "lm" or (norm is not None and not self.fold):
+                if norm is not None and not self.fold:
                     continue
                 wide = wide_on and K >= kmin and nn_ops.wide_gemm_eligible(B, N, K, silu)
                 rows = 2 * N if silu else N
@@ -232,6 +232,12 @@ class DecodeEngine:
             return self.fw[name], None
         return self._weight(name), self.model.p[norm]
 
+    def _lm_head_weight(self):
+        """(weight, norm_w, fragment order?) the fused lm-head sampler reads."""
+        if "lm" in self.fragw:
+            return self.fragw["lm"], None, True
+        return (*self._normed("lm", "norm"), False)
+
     def _proj(self, name: str, x: torch.Tensor, **kw):
         """One decode projection: the packed wide GEMM, or decode_gemm on the
         folded / raw weight (kw: bias, residual, silu, y, ss_in, ss_out)."""
@@ -264,10 +270,10 @@ class DecodeEngine:
             self._proj(f"l{i}.gu_w", self.s, silu=True, y=self.act, ss_in=ss)
             self._proj(f"l{i}.down_w", self.act, residual=self.s, ss_out=ss)
         if self._fused_sample():
-            w, nw = self._normed("lm", "norm")
+            w, nw, fr = self._lm_head_weight()
             nn_ops.lm_head_sample_step(self.s, w, self.params, self.rng, self.state[0:1], self.finished,
                                        self.out, self.cur, p["embed"], self.s, ss, norm_w=nw, eps=eps, ss_in=ss,
-                                       workspace=self.sample_ws)
+                                       workspace=self.sample_ws, fragw=fr)
         else:
             self._proj("lm", self.s, y=self.logits_buf, ss_in=ss)
 
@@ -401,10 +407,10 @@ class DecodeEngine:
         if self._fused_sample():  # what the decode graph runs instead of lm head + sample_step
             del ops_["decode_gemm.lm_head"], ops_["sample_step"]
             ops_["lm_head_sample"] = (
-                lambda i: nn_ops.lm_head_sample(self.s, self._normed("lm", "norm")[0], self.params, self.rng,
+                lambda i: nn_ops.lm_head_sample(self.s, self._lm_head_weight()[0], self.params, self.rng,
                                                 self.state[0:1], self.finished, self.out, self.cur,
-                                                norm_w=self._normed("lm", "norm")[1], eps=eps, ss_in=ss,
-                                                workspace=self.sample_ws),
+                                                norm_w=self._lm_head_weight()[1], eps=eps, ss_in=ss,
+                                                workspace=self.sample_ws, fragw=self._lm_head_weight()[2]),
                 c.vocab_size * H * bf, 1)
         nn_ops.embed_gather(p["embed"], self.cur, self.s, ss_out=ss)
         out = {}

@@ -240,10 +240,11 @@ def lm_head_sample_supported(params, V: int, K: int) -> bool:
 def lm_head_sample(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Tensor, step: torch.Tensor,
                    finished: torch.Tensor, out_tokens: torch.Tensor, cur_tokens: Optional[torch.Tensor] = None, *,
                    norm_w: Optional[torch.Tensor] = None, eps: float = 1e-6, ss_in: Optional[torch.Tensor] = None,
-                   workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+                   workspace: Optional[torch.Tensor] = None, fragw: bool = False) -> torch.Tensor:
     """lm head + the unfiltered sampler in one pass, no logits tensor
-    (include/swh_trl_amd.h swh_lm_head_sample).  Writes out_tokens[:, *step],
-    cur_tokens, finished; returns out_tokens."""
+    (include/swh_trl_amd.h swh_lm_head_sample; fragw: w packed by frag_pack,
+    swh_lm_head_sample_fragw).  Writes out_tokens[:, *step], cur_tokens,
+    finished; returns out_tokens."""
     import ctypes
     _dev(x, "lm_head_sample")
     M, K = x.shape
@@ -251,7 +252,10 @@ def lm_head_sample(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Tensor, 
     need = _lib.load().swh_lm_head_sample_workspace_bytes(M, V, K)
     if workspace is None or workspace.numel() < need:
         workspace = torch.empty(need, dtype=torch.uint8, device=x.device)
-    call("swh_lm_head_sample", x.data_ptr(), w.data_ptr(), M, V, K, _p(norm_w), float(eps), _p(ss_in),
+    head = (x.data_ptr(), w.data_ptr(), M, V, K) + (() if fragw else (_p(norm_w),)) + (float(eps), _p(ss_in))
+    if fragw and norm_w is not None:
+        raise ValueError("lm_head_sample: a fragment-order weight carries the folded norm (norm_w must be None)")
+    call("swh_lm_head_sample_fragw" if fragw else "swh_lm_head_sample", *head,
          ctypes.byref(params), rng.data_ptr(), step.data_ptr(), finished.data_ptr(), out_tokens.data_ptr(),
          out_tokens.stride(0), _p(cur_tokens), workspace.data_ptr(), workspace.numel(), _stream())
     return out_tokens
@@ -261,7 +265,7 @@ def lm_head_sample_step(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Ten
                         finished: torch.Tensor, out_tokens: torch.Tensor, cur_tokens: torch.Tensor,
                         embed: torch.Tensor, x_next: torch.Tensor, ss_next: Optional[torch.Tensor], *,
                         norm_w: Optional[torch.Tensor] = None, eps: float = 1e-6, ss_in: Optional[torch.Tensor] = None,
-                        workspace: torch.Tensor) -> torch.Tensor:
+                        workspace: torch.Tensor, fragw: bool = False) -> torch.Tensor:
     """lm_head_sample + the next step's input: x_next = embed[drawn token]
     (+ RMSNorm partials ss_next) and *step += 1 once every row has read it
     (include/swh_trl_amd.h swh_lm_head_sample_step).  `workspace` must have
@@ -272,7 +276,10 @@ def lm_head_sample_step(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Ten
     V = w.shape[0]
     if workspace.numel() < _lib.load().swh_lm_head_sample_workspace_bytes(M, V, K):
         raise ValueError("lm_head_sample_step: workspace too small")
-    call("swh_lm_head_sample_step", x.data_ptr(), w.data_ptr(), M, V, K, _p(norm_w), float(eps), _p(ss_in),
+    if fragw and norm_w is not None:
+        raise ValueError("lm_head_sample_step: a fragment-order weight carries the folded norm (norm_w must be None)")
+    head = (x.data_ptr(), w.data_ptr(), M, V, K) + (() if fragw else (_p(norm_w),)) + (float(eps), _p(ss_in))
+    call("swh_lm_head_sample_step_fragw" if fragw else "swh_lm_head_sample_step", *head,
          ctypes.byref(params), rng.data_ptr(), step.data_ptr(), finished.data_ptr(), out_tokens.data_ptr(),
          out_tokens.stride(0), cur_tokens.data_ptr(), embed.data_ptr(), x_next.data_ptr(), _p(ss_next),
          workspace.data_ptr(), workspace.numel(), _stream())

@@ -365,21 +365,32 @@ def test_layer_grad_hooks_fire_when_layer_grads_are_final(dev):
         assert torch.equal(snaps[i], m.grad[s:e]) and snaps[i].abs().sum() > 0
 
 
-def test_fold_kernel_equals_torch_mul_and_group_dedup(dev):
+def test_fold_kernel_equals_torch_mul_and_group_dedup(dev, monkeypatch):
     """swh_fold_norm (all folded decode weights in one launch) is bit-identical
-    to torch's bf16 W * w; the group-size hint gives the same prefill plan as
-    the generic unique() path."""
+    to torch's bf16 W * w, and so are the fragment-order copies (folded while
+    packing) after unpacking; the group-size hint gives the same prefill plan
+    as the generic unique() path."""
+    from swh_trl_amd import nn_ops
     from swh_trl_amd.engine import DecodeEngine
     m = _tiny(dev, seed=10, layers=2)
     with torch.no_grad():
         for k in ("l0.ln_in", "l1.ln_post", "norm"):
             m.p[k].copy_(1 + 0.1 * torch.randn_like(m.p[k].float()).to(m.p[k].dtype))
+    monkeypatch.setenv("SWH_FRAGW", "0")
     eng = DecodeEngine(m, 8, 6, 4)
     eng.refresh_folded()
     p = m.p
     assert torch.equal(eng.fw["l0.qkv_w"], p["l0.qkv_w"] * p["l0.ln_in"])
     assert torch.equal(eng.fw["l1.gu_w"], p["l1.gu_w"] * p["l1.ln_post"])
     assert torch.equal(eng.fw["lm"], m.lm_weight() * p["norm"])
+    monkeypatch.setenv("SWH_FRAGW", "1")
+    eng2 = DecodeEngine(m, 8, 6, 4)
+    eng2.refresh_folded()
+    assert set(eng2.fragw) >= {"l0.qkv_w", "l1.gu_w", "l1.down_w", "lm"} and "l0.qkv_w" not in eng2.fw
+    assert torch.equal(eng2.fragw["l0.qkv_w"], nn_ops.frag_pack(p["l0.qkv_w"] * p["l0.ln_in"]))
+    assert torch.equal(eng2.fragw["lm"], nn_ops.frag_pack(m.lm_weight() * p["norm"]))
+    assert torch.equal(eng2.fragw["l1.gu_w"], nn_ops.frag_pack(p["l1.gu_w"] * p["l1.ln_post"], silu=True))
+    assert torch.equal(eng2.fragw["l1.down_w"], nn_ops.frag_pack(p["l1.down_w"]))
     ids = torch.randint(0, m.cfg.vocab_size, (2, 6), device=dev).repeat_interleave(4, 0)
     mask = torch.ones_like(ids, dtype=torch.int32)
     rep, inv = DecodeEngine._unique_prompts(ids, mask, 4)

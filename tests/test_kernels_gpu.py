@@ -1071,7 +1071,8 @@ def test_decode_gemm_persistent_epilogues(ops, dev):
 
 @pytest.mark.parametrize("kw", [dict(), dict(temperature=0.7), dict(greedy=True), dict(min_new_tokens=5),
                                 dict(temperature=1.3, min_new_tokens=1)])
-@pytest.mark.parametrize("M,V,fold", [(64, 151936, False), (70, 32768, False), (64, 151936, True)])
+@pytest.mark.parametrize("M,V,fold", [(64, 151936, False), (70, 32768, False), (64, 151936, True),
+                                      (64, 151936, "fragw"), (70, 32768, "fragw")])
 def test_lm_head_sample_equals_logits_then_sampler(ops, dev, kw, M, V, fold):
     """The fused lm head + sampler draws, bit for bit, the token swh_sample_step
     draws from the materialised bf16 logits (same rng, same step), including
@@ -1101,7 +1102,11 @@ def test_lm_head_sample_equals_logits_then_sampler(ops, dev, kw, M, V, fold):
     out_b = torch.full((M, 4), -1, dtype=torch.int64, device=dev)
     cur_b = torch.empty(M, dtype=torch.int64, device=dev)
     fin_b = fin0.clone()
-    nn_ops.lm_head_sample(x, w, params, rng, stp, fin_b, out_b, cur_b, norm_w=nw, eps=1e-6, ss_in=ss)
+    if fold == "fragw":  # the folded weight in fragment order (swh_lm_head_sample_fragw)
+        nn_ops.lm_head_sample(x, nn_ops.frag_pack(w), params, rng, stp, fin_b, out_b, cur_b, eps=1e-6, ss_in=ss,
+                              fragw=True)
+    else:
+        nn_ops.lm_head_sample(x, w, params, rng, stp, fin_b, out_b, cur_b, norm_w=nw, eps=1e-6, ss_in=ss)
     assert torch.equal(out_b, out_a)
     assert torch.equal(cur_b, cur_a)
     assert torch.equal(fin_b, fin_a)
