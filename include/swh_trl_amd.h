@@ -451,11 +451,15 @@ int swh_wide_gemm_packed(const void *x, const void *w, int64_t M, int64_t N, int
  * one 1 KB run instead of 16 rows x 64 B.  swh_decode_gemm_fragw then computes
  * what swh_decode_gemm computes on the row-major W with norm_w == NULL
  * (bit-identical): residual, bias, SiLU-gate and folded-norm row scale (ss_in)
- * epilogues. */
+ * epilogues.  act_frag (M % 16 == 0): bit 0 — the SiLU output y is written in
+ * the same fragment order over its [M, N] (N % 32 == 0; 16-row groups), bit 1 —
+ * X (a residual projection's input, e.g. that SiLU output) is read in it: the
+ * decode gate/up -> down hand-off without row-major activations.  A shape whose
+ * kernels cannot honour a requested bit is SWH_E_ARG (no fallback). */
 int swh_frag_pack(const void *w, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, void *stream);
 int swh_decode_gemm_fragw(const void *x, const void *w, int64_t M, int64_t N, int64_t K, float eps, const void *bias,
                           void *residual, int32_t silu, void *y, int64_t ldy, const float *ss_in, float *ss_out,
-                          void *workspace, int64_t workspace_bytes, void *stream);
+                          int32_t act_frag, void *workspace, int64_t workspace_bytes, void *stream);
 
 /* Decode lm head with the sampler fused into its epilogue: RMSNorm(X) W^T
  * (as swh_decode_gemm with norm_w / ss_in) and, per row, the token that

@@ -118,7 +118,7 @@ SIGNATURES = {
     "swh_wide_pack": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp]),
     "swh_frag_pack": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp]),
     "swh_decode_gemm_fragw": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_f32, c_vp, c_vp, c_i32, c_vp, c_i64, c_vp,
-                                      c_vp, c_vp, c_i64, c_vp]),
+                                      c_vp, c_i32, c_vp, c_i64, c_vp]),
     "swh_wide_gemm_packed": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_f32, c_vp, c_vp, c_i32, c_vp, c_i64, c_vp,
                                      c_vp, c_vp, c_i64, c_vp]),
 }

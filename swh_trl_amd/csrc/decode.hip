@@ -591,7 +591,7 @@ __global__ __launch_bounds__(512) void xstream_gemm_kernel(const uint16_t *__res
                                                            float eps, const float *__restrict__ ss_in,
                                                            const uint16_t *__restrict__ bias,
                                                            uint16_t *__restrict__ res, float *__restrict__ ss_out,
-                                                           uint16_t *__restrict__ y, int ldy, int fw) {
+                                                           uint16_t *__restrict__ y, int ldy, int fw, int xf) {
     static_assert(EPI != EPI_SILU && NM != 1, "plain / residual epilogues, folded or no norm");
     constexpr int NW = 8, NT = 512, MR = 16 * MS, NB = 16, LDR = MR + 4, G8 = NB / 8, F = NW;
     __shared__ __attribute__((aligned(16))) float part[(NW + 1) * NB * LDR];
@@ -627,16 +627,21 @@ __global__ __launch_bounds__(512) void xstream_gemm_kernel(const uint16_t *__res
     // fw: the swh_frag_pack layout (one contiguous 1 KB per wave and k-step)
     const uint16_t *wr = fw ? w + ((int64_t)(n0 >> 4) * KS * 64 + lane) * 8 : w + (int64_t)(n0 + rl) * K + kq;
     const int wstep = fw ? 512 : 32;
+    // xf: X itself in the fragment order (16-row groups; written so by the SiLU tile
+    // epilogue, M % 16 == 0): one contiguous 1 KB run per A-fragment load as well
     const uint16_t *xr[MS];
 #pragma unroll
-    for (int i = 0; i < MS; ++i) xr[i] = x + (int64_t)min(m0 + i * 16 + rl, M - 1) * K + kq;
+    for (int i = 0; i < MS; ++i)
+        xr[i] = xf ? x + ((int64_t)((m0 >> 4) + i) * KS * 64 + lane) * 8
+                   : x + (int64_t)min(m0 + i * 16 + rl, M - 1) * K + kq;
+    const int xstep = xf ? 512 : 32;
     uint4 xa[KW][MS], bv[KW];
 #pragma unroll
     for (int u = 0; u < KW; ++u) {
         const int ks = min(ksw0 + u, ksw1 - 1);  // past the wave's range: a repeated, unused load (no branch)
         bv[u] = ld_w(wr + ks * wstep);
 #pragma unroll
-        for (int i = 0; i < MS; ++i) xa[u][i] = *reinterpret_cast<const uint4 *>(xr[i] + ks * 32);
+        for (int i = 0; i < MS; ++i) xa[u][i] = *reinterpret_cast<const uint4 *>(xr[i] + ks * xstep);
     }
     SWH_GEMM_TRACE(1);
     if constexpr (NM == 2) {  // read by the epilogue only, behind the merge barriers
@@ -749,6 +754,7 @@ struct LmSample {
     LmPart *part;  // [M][pstride]
     int pstride;
     int fw = 0;    // weights in the swh_frag_pack layout (tile t = 16-row group t)
+    int yf = 0;    // SiLU output in the fragment order down_proj's A operand reads (N % 32 == 0)
 };
 
 // KSC: K / 32 at compile time (0 = read from K): with a constant trip count the
@@ -1006,8 +1012,13 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
                     const float v = round_bf16(acc[i][e] * rsr[i][e]);
                     const float u = __shfl_xor(v, 8, kWave);
                     const int row = m0 + i * 16 + 4 * g + e;
-                    if (rl < 8 && row < M)
-                        y[(int64_t)row * ldy + t * 8 + rl] = f32_to_bf16_bits(round_bf16(v / (1.f + expf(-v))) * u);
+                    if (rl < 8 && row < M) {
+                        const int col = t * 8 + rl;  // yf: ((row/16 * N/32 + col/32) 64 + lane) 8 + col % 8
+                        const int64_t at = smp.yf ? ((((int64_t)(row >> 4) * (N >> 5) + (col >> 5)) * 64 +
+                                                      ((col >> 3) & 3) * 16 + (row & 15)) * 8 + (col & 7))
+                                                  : (int64_t)row * ldy + col;
+                        y[at] = f32_to_bf16_bits(round_bf16(v / (1.f + expf(-v))) * u);
+                    }
                 }
         } else {
             // C layout: lane holds rows 16 i + 4 g + e of column rl
@@ -1464,6 +1475,7 @@ struct GemmCfg {
     bool persist;
     int wn = 1;             // column groups: a wave computes cb / wn column blocks over K / (nw / wn)
     int fw = 0;             // weights in the swh_frag_pack layout
+    int xf = 0;             // X (the SiLU activation) in the same fragment order (xstream only)
 };
 
 int cu_count() {
@@ -1599,7 +1611,7 @@ int launch_xstream_kw(const GemmCfg &c, hipStream_t s, const uint16_t *X, const 
                       float eps, const float *ss_in, const uint16_t *Bs, uint16_t *R, float *ss_out, uint16_t *Y,
                       int ld) {
     xstream_gemm_kernel<KW, MS, NM, EPI, BIAS, 0><<<dim3((unsigned)c.gx), 512, 0, s>>>(X, W, m, n, k, eps, ss_in, Bs, R,
-                                                                                   ss_out, Y, ld, c.fw);
+                                                                                   ss_out, Y, ld, c.fw, c.xf);
     return launch_status();
 }
 
@@ -1617,13 +1629,20 @@ int launch_xstream(const GemmCfg &c, hipStream_t s, const uint16_t *X, const uin
                    float eps, const float *ss_in, const uint16_t *Bs, uint16_t *R, float *ss_out, uint16_t *Y, int ld) {
     const char *e = getenv("SWH_XSTREAM");  // A/B: 0 = decode_gemm_kernel's LDS image
     const int ks = k / 32;
-    if ((e && e[0] == '0') || c.cb != 1 || c.wn != 1 || c.s != 1 || c.persist || c.nw != 8 || n % 16 || ks < 8 ||
-        ks > 64 || (c.ms != 1 && c.ms != 2))
+    if (((e && e[0] == '0') && !c.xf) || c.cb != 1 || c.wn != 1 || c.s != 1 || c.persist || c.nw != 8 || n % 16 ||
+        ks < 8 || ks > (c.xf ? 152 : 64) || (c.ms != 1 && c.ms != 2))
         return 1;
-    if (R) {  // o_proj: s += x W^T (+ the next norm's partial sums)
+    if (R) {  // o_proj: s += x W^T (+ the next norm's partial sums); down_proj over a fragment-order X
         if (nm != 0 || Bs || c.ms != 1) return 1;
+        if (c.xf) {
+            if (m % 16 || (ks + 7) / 8 > 19) return 1;
+            if ((ks + 7) / 8 > 8)
+                return launch_xstream_kw<19, 1, 0, EPI_RESIDUAL, false>(c, s, X, W, m, n, k, eps, nullptr, nullptr, R,
+                                                                       ss_out, nullptr, ld);
+        }
         return launch_xstream_ms<1, 0, EPI_RESIDUAL, false>(c, s, X, W, m, n, k, eps, nullptr, nullptr, R, ss_out, nullptr, ld);
     }
+    if (c.xf) return 1;
     if (nm != 2 || !ss_in || !Bs || !Y) return 1;  // qkv: folded norm + bias
     if (c.ms == 1)
         return launch_xstream_ms<1, 2, EPI_PLAIN, true>(c, s, X, W, m, n, k, eps, ss_in, Bs, nullptr, nullptr, Y, ld);
@@ -1686,9 +1705,10 @@ int launch_lm(dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uin
 template <int EPI, bool BIAS>
 int launch_tiles(int nm, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W, int M, int N,
                  int K, const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs, uint16_t *Y, int ldy,
-                 int fw) {
+                 int fw, int yf = 0) {
     LmSample none{};
     none.fw = fw;
+    none.yf = yf;
     if (nm == 1) return launch_lm<1, EPI, BIAS, false>(grid, lds, s, X, W, M, N, K, NWt, eps, ss_in, Bs, Y, ldy, none);
     if (nm == 2) return launch_lm<2, EPI, BIAS, false>(grid, lds, s, X, W, M, N, K, nullptr, eps, ss_in, Bs, Y, ldy, none);
     return launch_lm<0, EPI, BIAS, false>(grid, lds, s, X, W, M, N, K, nullptr, eps, nullptr, Bs, Y, ldy, none);
@@ -1755,8 +1775,11 @@ extern "C" int64_t swh_decode_gemm_workspace_bytes(int64_t M, int64_t N, int64_t
 static int decode_gemm_impl(const void *x, const void *w, int64_t M, int64_t N, int64_t K, const void *norm_w,
                             float eps, const void *bias, void *residual, int32_t silu, void *y, int64_t ldy,
                             const float *ss_in, float *ss_out, void *workspace, int64_t workspace_bytes, void *stream,
-                            int fw) {
+                            int fw, int act = 0) {
     if (fw && (norm_w || K % 128)) return SWH_E_ARG;
+    // act bit 0: the SiLU output in fragment order (tile path only); bit 1: X in fragment order (xstream only)
+    if (act & ~3 || ((act & 1) && (!silu || N % 32 || M % 16)) || ((act & 2) && (!residual || M % 16 || K % 32)))
+        return SWH_E_ARG;
     if (!x || !w || M <= 0 || N <= 0 || K <= 0 || K % 64 || M > (1 << 20) || N >= (1 << 29) || K >= (1 << 29))
         return SWH_E_ARG;
     if (residual && (silu || bias)) return SWH_E_ARG;
@@ -1795,13 +1818,15 @@ static int decode_gemm_impl(const void *x, const void *w, int64_t M, int64_t N, 
             const auto *Bs = static_cast<const uint16_t *>(bias);
             auto *Y = static_cast<uint16_t *>(y);
             const size_t lds = (size_t)L.total;
-            if (silu) return launch_tiles<EPI_SILU, false>(nm, grid, lds, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Bs, Y, (int)ldy, fw);
+            if (silu) return launch_tiles<EPI_SILU, false>(nm, grid, lds, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Bs, Y, (int)ldy, fw, act & 1);
             if (Bs) return launch_tiles<EPI_PLAIN, true>(nm, grid, lds, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Bs, Y, (int)ldy, fw);
             return launch_tiles<EPI_PLAIN, false>(nm, grid, lds, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Bs, Y, (int)ldy, fw);
         }
     }
+    if (act & 1) return SWH_E_ARG;  // the fragment-order SiLU output comes from the tile kernel only
     GemmCfg c = pick_cfg(M, wcols, K, silu != 0, nm);
     c.fw = fw;
+    c.xf = (act & 2) ? 1 : 0;
     const int64_t MR = 16 * c.ms, nmt = (M + MR - 1) / MR, ncb = wcols / (16 * c.cb);
     // workspace: [counters (zeroed once, self-resetting) | fp32 slabs]
     int *ctr = static_cast<int *>(workspace);
@@ -1837,6 +1862,7 @@ static int decode_gemm_impl(const void *x, const void *w, int64_t M, int64_t N, 
             const int rc = launch_xstream(c, s, X, W, m, n, k, nm, eps, ss_in, Bs, R, ss_out, nullptr, ld);
             if (rc != 1) return rc;
         }
+        if (c.xf) return SWH_E_ARG;  // a fragment-order X is read by xstream only
         if (nm == 1) SWH_GEMM(1, EPI_RESIDUAL, false);
         SWH_GEMM(0, EPI_RESIDUAL, false);
     }
@@ -1865,10 +1891,10 @@ extern "C" int swh_decode_gemm(const void *x, const void *w, int64_t M, int64_t 
 
 extern "C" int swh_decode_gemm_fragw(const void *x, const void *w, int64_t M, int64_t N, int64_t K, float eps,
                                      const void *bias, void *residual, int32_t silu, void *y, int64_t ldy,
-                                     const float *ss_in, float *ss_out, void *workspace, int64_t workspace_bytes,
-                                     void *stream) {
+                                     const float *ss_in, float *ss_out, int32_t act_frag, void *workspace,
+                                     int64_t workspace_bytes, void *stream) {
     return decode_gemm_impl(x, w, M, N, K, nullptr, eps, bias, residual, silu, y, ldy, ss_in, ss_out, workspace,
-                            workspace_bytes, stream, 1);
+                            workspace_bytes, stream, 1, act_frag);
 }
 
 extern "C" int swh_frag_pack(const void *w, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst,

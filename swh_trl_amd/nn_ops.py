@@ -177,9 +177,10 @@ def frag_pack(w: torch.Tensor, norm_w: Optional[torch.Tensor] = None, *, silu: b
 def decode_gemm_fragw(x: torch.Tensor, w: torch.Tensor, *, eps: float = 1e-6, bias: Optional[torch.Tensor] = None,
                       residual: Optional[torch.Tensor] = None, silu: bool = False, y: Optional[torch.Tensor] = None,
                       workspace: Optional[torch.Tensor] = None, ss_in: Optional[torch.Tensor] = None,
-                      ss_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                      ss_out: Optional[torch.Tensor] = None, act_frag: int = 0) -> torch.Tensor:
     """decode_gemm (no norm_w) over w packed by frag_pack ([N, K], [2N, K] with
-    silu) (include/swh_trl_amd.h swh_decode_gemm_fragw): bit-identical results."""
+    silu) (include/swh_trl_amd.h swh_decode_gemm_fragw): bit-identical results.
+    act_frag bit 0: write the SiLU output in fragment order; bit 1: read x in it."""
     _dev(x, "decode_gemm_fragw")
     M, K = x.shape
     N = w.shape[0] // 2 if silu else w.shape[0]
@@ -188,7 +189,7 @@ def decode_gemm_fragw(x: torch.Tensor, w: torch.Tensor, *, eps: float = 1e-6, bi
     ldy = residual.stride(0) if residual is not None else y.stride(0)
     ws = workspace if workspace is not None else gemm_workspace(x.device)
     call("swh_decode_gemm_fragw", x.data_ptr(), w.data_ptr(), M, N, K, float(eps), _p(bias), _p(residual),
-         int(bool(silu)), _p(y), ldy, _p(ss_in), _p(ss_out), ws.data_ptr(), ws.numel(), _stream())
+         int(bool(silu)), _p(y), ldy, _p(ss_in), _p(ss_out), int(act_frag), ws.data_ptr(), ws.numel(), _stream())
     return residual if residual is not None else y
 
 

@@ -614,6 +614,33 @@ def test_shared_prompt_forward_matches_per_row(dev, dtype, left_pad):
     assert rel <= tol, rel
 
 
+def test_act_frag_generates_identically(dev, monkeypatch):
+    """The decode step with gate/up writing its activation in fragment order and
+    down_proj reading it register-streamed (SWH_ACT_FRAG=1) generates the same
+    tokens and log-probs as the row-major activation."""
+    from swh_trl_amd.engine import CausalLM, DecoderConfig, DecodeEngine
+    cfg = DecoderConfig(vocab_size=1024, hidden_size=256, intermediate_size=2048, num_hidden_layers=2,
+                        num_attention_heads=4, num_key_value_heads=2, head_dim=64, rope_theta=10000.0,
+                        max_position_embeddings=4096)
+    m = CausalLM(cfg, dev, seed=9, init_std=0.05)
+    g = torch.Generator().manual_seed(9)
+    B, P, C = 32, 12, 20
+    ids = torch.randint(0, 1024, (B, P), generator=g).to(dev)
+    mask = torch.ones(B, P, dtype=torch.int64, device=dev)
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SWH_ACT_FRAG", flag)
+        eng = DecodeEngine(m, B, P, C)
+        assert eng.act_frag == (flag == "1")
+        outs[flag] = (eng.generate(ids, mask, C, greedy=True),
+                      eng.generate(ids, mask, C, temperature=0.9, seed=3, return_logp=True))
+        del eng
+    for a, b in zip(outs["1"], outs["0"]):
+        for x, y in zip(a, b):
+            if isinstance(x, torch.Tensor):
+                assert torch.equal(x, y)
+
+
 def test_fragw_projections_generate_identically(dev, monkeypatch):
     """DecodeEngine with o_proj / down_proj read from fragment-order copies
     (swh_frag_pack + swh_decode_gemm_fragw, refreshed every generate()) gives

@@ -1223,6 +1223,32 @@ def test_decode_gemm_fragw_equals_row_major(ops, dev, monkeypatch, M, N, K, kind
         assert torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("M", [64, 32])
+def test_act_frag_gate_up_to_down_equals_row_major(ops, dev, M):
+    """gate/up writing its SiLU output in fragment order (act_frag bit 0) is the
+    row-major output permuted (torch restatement), and down_proj reading it
+    (bit 1, register-streamed X at K 4864) equals down_proj over the row-major
+    activation bit for bit, residual rows and chunk sums of squares."""
+    from swh_trl_amd import nn_ops
+    g = _gen(59)
+    H, I = 896, 4864
+    x = torch.randn(M, H, generator=g).to(torch.bfloat16).to(dev)
+    wgu = nn_ops.frag_pack((torch.randn(2 * I, H, generator=g) * H ** -0.5).to(torch.bfloat16).to(dev), silu=True)
+    wd = nn_ops.frag_pack((torch.randn(H, I, generator=g) * I ** -0.5).to(torch.bfloat16).to(dev))
+    ss = _chunk_ss(x)
+    y_rm = nn_ops.decode_gemm_fragw(x, wgu, silu=True, ss_in=ss)
+    y_fr = nn_ops.decode_gemm_fragw(x, wgu, silu=True, ss_in=ss, act_frag=1)
+    assert torch.equal(y_fr, y_rm.view(M // 16, 16, I // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(M, I))
+    s0 = torch.randn(M, H, generator=g).to(torch.bfloat16).to(dev)
+    outs = []
+    for act, y in ((0, y_rm), (2, y_fr)):
+        r, so = s0.clone(), torch.full((M, H // 16), float("nan"), device=dev)
+        nn_ops.decode_gemm_fragw(y, wd, residual=r, ss_out=so, act_frag=act)
+        outs.append((r, so))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
 @pytest.mark.parametrize("M,N,K", [(64, 1152, 896), (37, 1152, 896), (64, 384, 512), (20, 1152, 896)])
 def test_xstream_qkv_equals_lds_image_kernel(ops, dev, monkeypatch, M, N, K):
     """The qkv projection (folded RMSNorm row scale from the producer's chunk
