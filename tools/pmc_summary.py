@@ -20,6 +20,7 @@ NAMES = {  # kernel template prefix -> the bench's kernel name
     "decode_gemm_kernel<1, 1, 0, 1, false, 512, 1>": "decode_gemm.down",  # K-class tag 1
     "xstream_gemm_kernel<4, 2, 2, 0, true": "decode_gemm.qkv",   # register-streamed X (round 2)
     "xstream_gemm_kernel<4, 1, 0, 1, false": "decode_gemm.o",
+    "xstream_gemm_kernel<19, 1, 0, 1, false": "decode_gemm.down",  # fragment-order activation (act_frag)
     "attn_decode_kernel<64, 7>": "attn_decode",
     "lm_head_kernel<2, 0, false, true": "lm_head_sample",
     # training kernels (tools/train_kernels.py)
