@@ -155,7 +155,11 @@ int swh_group_advantage(const float *rewards_per_func, const float *weights, int
  * Outputs: loss f32[1] (sum over segments of each segment's loss, times
  * row_scale), dlogp f32 [R, T] (d loss / d logp, may be NULL), metrics f32[8]:
  * {tokens, kl_sum, entropy_sum, low_clip_sum, high_clip_sum, region_clip_sum,
- *  seq_rows, 0}.  workspace >= swh_grpo_loss_workspace_bytes(R). */
+ *  seq_rows, 0}; seg_metrics f32 [num_segments, 8] nullable: the same sums
+ * per segment (clip sums over rows under sequence level, last-but-one = rows),
+ * from which the host forms each micro-batch's masked_batch_mean
+ * (:2143-2148) before the cross-rank gather (:2150-2174).
+ * workspace >= swh_grpo_loss_workspace_bytes(R). */
 #define SWH_LOSS_GRPO 0
 #define SWH_LOSS_BNPO 1
 #define SWH_LOSS_DR_GRPO 2
@@ -176,7 +180,7 @@ int swh_grpo_loss_fwd_bwd(const float *logp, const float *old_logp, const float 
                           const float *adv, const int32_t *mask, const uint8_t *ent_mask,
                           const float *entropy, const float *row_scale, const int32_t *seg, int64_t R,
                           int64_t T, const swh_grpo_loss_params *p, float *loss, float *dlogp,
-                          float *metrics, void *workspace, void *stream);
+                          float *metrics, float *seg_metrics, void *workspace, void *stream);
 
 /* ---- a17: masked mean / var / whiten (trl/core.py:43-76) -----------------
  * values f32 [N], mask int32 [N]; out f32 [N]; stats f32[3] = {mean, var,
@@ -215,14 +219,16 @@ int swh_ppo_truncate(const int64_t *responses, int64_t B, int64_t T, int64_t sto
 /* swh_ppo_rewards, per row after the value / reward-model forwards:
  * padding_mask = t > seq_len, padding_mask_p1 = t > seq_len + 1 (uint8 [B, T]);
  * logprobs / ref_logprobs f32 [B, T] set to INVALID_LOGPROB (1.0) under the
- * mask (in place); values bf16 [B, T] zeroed under mask_p1 (in place); scores
- * bf16 [B] minus missing_eos_penalty where no eos token is in post (has_penalty,
- * eos < 0 = none; in place); kl = -logr (k1) or (exp(logr) - 1) - logr (k3),
- * logr = ref - logp; non_score_reward = -kl_coef * kl; rewards = non_score_reward
- * + score at min(seq_len + 1, T - 1) (all f32 [B, T]). */
+ * mask (in place); values [B, T] zeroed under mask_p1 (in place); scores [B]
+ * minus missing_eos_penalty where no eos token is in post (has_penalty, eos < 0
+ * = none; in place, rounded to their dtype); values / scores are the score
+ * heads' outputs in `dtype` (SWH_BF16, or SWH_F32 in the reference-precision
+ * mode); kl = -logr (k1) or (exp(logr) - 1) - logr (k3), logr = ref - logp;
+ * non_score_reward = -kl_coef * kl; rewards = non_score_reward + score at
+ * min(seq_len + 1, T - 1) (all f32 [B, T]). */
 int swh_ppo_rewards(const int64_t *post, const int64_t *seq_len, int64_t B, int64_t T, int64_t eos_token_id,
                     float missing_eos_penalty, int32_t has_penalty, float kl_coef, int32_t kl_k3, float *logprobs,
-                    float *ref_logprobs, void *values_bf16, void *scores_bf16, uint8_t *padding_mask,
+                    float *ref_logprobs, void *values, void *scores, int32_t dtype, uint8_t *padding_mask,
                     uint8_t *padding_mask_p1, float *kl, float *non_score_reward, float *rewards, void *stream);
 
 /* ---- a20: value head (modeling_value_head.py:50-59; PPO score head

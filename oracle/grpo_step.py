@@ -37,6 +37,23 @@ def hf_qwen2_from_config(cfg: dict, seed: int = 0, dtype=torch.float32):
     return m
 
 
+def hf_llama_from_config(cfg: dict, seed: int = 0, dtype=torch.float32):
+    """Random-init transformers LlamaForCausalLM of the given architecture (the Llama-3
+    family of BASELINE.json config 5: no q/k/v bias, untied head)."""
+    from transformers import LlamaConfig, LlamaForCausalLM
+    torch.manual_seed(seed)
+    hc = LlamaConfig(vocab_size=cfg["vocab_size"], hidden_size=cfg["hidden_size"],
+                     intermediate_size=cfg["intermediate_size"], num_hidden_layers=cfg["num_hidden_layers"],
+                     num_attention_heads=cfg["num_attention_heads"], num_key_value_heads=cfg["num_key_value_heads"],
+                     head_dim=cfg["head_dim"], rope_theta=cfg["rope_theta"], rms_norm_eps=cfg["rms_norm_eps"],
+                     tie_word_embeddings=cfg["tie_word_embeddings"], attention_bias=cfg["attention_bias"],
+                     max_position_embeddings=cfg.get("max_position_embeddings", 8192))
+    hc._attn_implementation = "sdpa"
+    m = LlamaForCausalLM(hc).to(dtype)
+    m.eval()
+    return m
+
+
 def hf_gpt2_from_config(cfg: dict, seed: int = 0, dtype=torch.float32):
     """Random-init transformers GPT2LMHeadModel (BASELINE.json config 1), dropout
     off (`disable_dropout=True` in GRPOConfig terms: the engine has none)."""
@@ -58,6 +75,8 @@ def hf_from_config(cfg: dict, seed: int = 0, dtype=torch.float32):
     """The transformers model of cfg["model_type"] (GPT-2, or Qwen2 / Llama-style)."""
     if cfg.get("model_type") == "gpt2":
         return hf_gpt2_from_config(cfg, seed, dtype)
+    if cfg.get("model_type") == "llama":
+        return hf_llama_from_config(cfg, seed, dtype)
     return hf_qwen2_from_config(cfg, seed, dtype)
 
 
@@ -79,9 +98,11 @@ def generate(model, prompt_ids, prompt_mask, C: int, *, do_sample=True, temperat
 
 def per_token_logps(model, prompt_ids, prompt_mask, completion_ids, completion_mask, temperature=1.0,
                     compute_entropy=True):
-    """grpo_trainer.py:1205-1272 (one batch)."""
-    ids = torch.cat([prompt_ids, completion_ids], 1)
-    am = torch.cat([prompt_mask, completion_mask], 1)
+    """grpo_trainer.py:1205-1272 (one batch), on the model's device."""
+    dev = next(model.parameters()).device
+    ids = torch.cat([prompt_ids, completion_ids], 1).to(dev)
+    am = torch.cat([prompt_mask, completion_mask], 1).to(dev)
+    completion_ids = completion_ids.to(dev)
     C = completion_ids.shape[1]
     logits = model(input_ids=ids, attention_mask=am, logits_to_keep=C + 1).logits
     logits = logits[:, :-1][:, -C:] / temperature
@@ -93,66 +114,157 @@ def per_token_logps(model, prompt_ids, prompt_mask, completion_ids, completion_m
     return lp, ent
 
 
+def score_generation(model, g: dict, reward_fn: Callable, *, num_generations: int, temperature=1.0,
+                     eos_token_id=None, scale_rewards=True, beta=0.0, ref_model=None, need_old: bool = False,
+                     per_device_train_batch_size: Optional[int] = None):
+    """The scoring half of _generate_and_score_completions (grpo_trainer.py:1812-1938) on a
+    generation batch g = {prompt_ids, prompt_mask, completion_ids}: EOS mask, rewards,
+    group advantages, the old-policy log-probs when the steps are not aligned with the
+    generations (:1854-1869) and the frozen reference's (:1871-1899), both scored before
+    the shuffle in micro-batches of per_device_train_batch_size rows (the reference's
+    batch_size).
+
+    Data parallel: g["world_completion_ids"] (every rank's completions in rank order, the
+    accelerate gather of :1497) and g["rank"]: rewards and advantages are formed on the
+    global batch and this rank keeps its slice (:1914-1938)."""
+    eos = eos_token_id if eos_token_id is not None else -1
+    cids = g["completion_ids"]
+    B = cids.shape[0]
+    mask, lengths, _ = trl_ref.completion_mask_from_eos(cids, eos)
+    all_ids = g.get("world_completion_ids")
+    if all_ids is None:
+        all_ids, r0 = cids, 0
+    else:
+        r0 = int(g["rank"]) * B
+        assert torch.equal(all_ids[r0:r0 + B], cids)
+    all_mask, _, _ = trl_ref.completion_mask_from_eos(all_ids, eos)
+    rewards = torch.tensor([float(x) for x in reward_fn(all_ids, all_mask)], dtype=torch.float32).view(-1, 1)
+    adv, _, _, _, _ = trl_ref.group_advantages(rewards, torch.ones(1), num_generations, scale_rewards)
+    adv = adv[r0:r0 + B]
+    bs = per_device_train_batch_size or B
+
+    def scored(m):
+        parts = []
+        with torch.no_grad():
+            for r0 in range(0, B, bs):
+                sl = slice(r0, r0 + bs)
+                lp, _ = per_token_logps(m, g["prompt_ids"][sl], g["prompt_mask"][sl], cids[sl], mask[sl],
+                                        temperature, compute_entropy=False)
+                parts.append(lp)
+        return torch.cat(parts)
+    old = scored(model).cpu() if need_old else None
+    ref = None
+    if beta != 0.0:
+        if ref_model is None:
+            raise ValueError("beta != 0 needs ref_model")
+        ref = scored(ref_model).cpu()
+    return {"p": g["prompt_ids"], "pm": g["prompt_mask"], "c": cids, "cm": mask, "a": adv, "old": old, "ref": ref,
+            "rewards": rewards, "lengths": lengths}
+
+
+def grpo_train(model, optimizer, generations, reward_fn: Callable, *, num_generations: int, C: int,
+               per_device_train_batch_size: int, gradient_accumulation_steps: int, n_steps: int,
+               steps_per_generation: Optional[int] = None, num_iterations: int = 1, temperature=1.0,
+               eos_token_id=None, beta=0.0, epsilon=0.2, epsilon_high=None, loss_type="bnpo",
+               importance_sampling_level="token", scale_rewards=True, max_grad_norm=1.0, ref_model=None,
+               capture: bool = False):
+    """`n_steps` optimizer steps of the transformers Trainer around GRPOTrainer, with the
+    reference's buffering (_prepare_inputs, grpo_trainer.py:1411-1444): a new generation
+    every steps_per_generation * num_iterations micro-steps, shuffled (the permutation is
+    given: g["perm"], the reference draws it from the global RNG, :259) and split into
+    steps_per_generation micro-batches that are revisited num_iterations times; the old
+    log-probs enter when GA is not a multiple of that period (:1854-1869).  Each micro-batch
+    is a separate forward/backward of loss / GA (model_accepts_loss_kwargs False), then
+    clip_grad_norm_ and the optimizer step.
+
+    generations: iterable of {prompt_ids, prompt_mask, completion_ids, perm} consumed when a
+    generation is due.  Returns one dict per optimizer step: loss (sum of the micro losses /
+    GA), grad_norm, and with capture the micro-batch log-probs in training order ("logps"),
+    the pre-clip gradients ("grads"), plus "gens": the scored generation batches."""
+    GA = gradient_accumulation_steps
+    spg = steps_per_generation or GA
+    generate_every = spg * num_iterations
+    need_old = GA % generate_every != 0
+    it = iter(generations)
+    buffered, micro_step, gens, out = None, 0, [], []
+    for _ in range(n_steps):
+        losses, lps = [], []
+        for _ in range(GA):
+            if micro_step % generate_every == 0 or buffered is None:
+                g = next(it)
+                sc = score_generation(model, g, reward_fn, num_generations=num_generations,
+                                      temperature=temperature, eos_token_id=eos_token_id,
+                                      scale_rewards=scale_rewards, beta=beta, ref_model=ref_model,
+                                      need_old=need_old, per_device_train_batch_size=per_device_train_batch_size)
+                gens.append(sc)
+                keys = ("p", "pm", "c", "cm", "a", "old", "ref")
+                shuffled = trl_ref.permute_sequence_dict({k: sc[k] for k in keys}, g["perm"])
+                buffered = trl_ref.split_tensor_dict(shuffled, spg)
+            dev = next(model.parameters()).device
+            mb = {k: (None if v is None else v.to(dev)) for k, v in buffered[micro_step % spg].items()}
+            micro_step += 1
+            lp, ent = per_token_logps(model, mb["p"], mb["pm"], mb["c"], mb["cm"], temperature)
+            loss, _ = trl_ref.grpo_loss(lp, mb["a"], mb["cm"], old_per_token_logps=mb["old"],
+                                        ref_per_token_logps=mb["ref"], entropies=ent, beta=beta,
+                                        epsilon_low=epsilon, epsilon_high=epsilon_high or epsilon,
+                                        loss_type=loss_type, importance_sampling_level=importance_sampling_level,
+                                        max_completion_length=C)
+            (loss / GA).backward()
+            losses.append(float(loss.detach()) / GA)
+            lps.append(lp.detach().cpu())
+        grads = ({n: p.grad.detach().cpu().clone() for n, p in model.named_parameters() if p.grad is not None}
+                 if capture else None)
+        total = torch.nn.utils.clip_grad_norm_(model.parameters(), max_grad_norm)
+        optimizer.step()
+        optimizer.zero_grad()
+        rec = {"loss": sum(losses), "grad_norm": float(total), "losses": losses}
+        if capture:
+            rec.update(logps=torch.cat(lps), grads=grads)
+        out.append(rec)
+    if out:
+        out[0]["gens"] = gens
+    return out
+
+
 def grpo_step(model, optimizer, prompt_ids, prompt_mask, reward_fn: Callable, *, num_generations: int, C: int,
               per_device_train_batch_size: int, gradient_accumulation_steps: int, temperature=1.0,
               eos_token_id=None, pad_token_id=0, beta=0.0, epsilon=0.2, epsilon_high=None, loss_type="bnpo",
               importance_sampling_level="token", scale_rewards=True, max_grad_norm=1.0, do_sample=True,
               min_new_tokens=0, perm: Optional[torch.Tensor] = None, completion_ids=None, timings=None,
               ref_model=None, capture: bool = False):
-    """One optimizer step; returns (mean loss, dict of intermediates).
+    """One optimizer step over one generation batch (steps_per_generation = rows /
+    per_device_train_batch_size, as GRPOConfig derives it); returns (mean loss, dict of
+    intermediates).
 
-    ref_model (beta != 0): the frozen reference scored on the whole batch
-    before the shuffle (grpo_trainer.py:1871-1899).  capture=True adds the
-    per-token log-probs of every micro-batch ("logps", permuted row order),
-    the pre-clip gradients ("grads", name -> tensor) and the per-micro losses."""
+    completion_ids None: the completions come from transformers generate with the
+    reference's GenerationConfig.  ref_model (beta != 0): the frozen reference scored on
+    the whole batch before the shuffle (grpo_trainer.py:1871-1899).  capture=True adds
+    the per-token log-probs of every micro-batch ("logps", permuted row order), the
+    pre-clip gradients ("grads") and the per-micro losses."""
     t0 = time.perf_counter()
     if completion_ids is None:
         completion_ids = generate(model, prompt_ids, prompt_mask, C, do_sample=do_sample, temperature=temperature,
                                   min_new_tokens=min_new_tokens, pad_token_id=pad_token_id,
                                   eos_token_id=eos_token_id)
     t1 = time.perf_counter()
-    mask, lengths, _ = trl_ref.completion_mask_from_eos(completion_ids, eos_token_id if eos_token_id is not None
-                                                        else -1)
-    rewards = torch.tensor([float(x) for x in reward_fn(completion_ids, mask)], dtype=torch.float32).view(-1, 1)
-    adv, _, _, _, _ = trl_ref.group_advantages(rewards, torch.ones(1), num_generations, scale_rewards)
     B = completion_ids.shape[0]
-    ref_lp = None
-    if beta != 0.0:
-        if ref_model is None:
-            raise ValueError("beta != 0 needs ref_model")
-        with torch.no_grad():
-            ref_lp, _ = per_token_logps(ref_model, prompt_ids, prompt_mask, completion_ids, mask, temperature,
-                                        compute_entropy=False)
     perm = torch.arange(B) if perm is None else perm
-    data = {"p": prompt_ids[perm], "pm": prompt_mask[perm], "c": completion_ids[perm], "cm": mask[perm],
-            "a": adv[perm], "r": None if ref_lp is None else ref_lp[perm]}
     spg = B // per_device_train_batch_size
-    GA = gradient_accumulation_steps
-    losses = []
-    grads_of_logps = []
-    for j in range(min(spg, GA)):
-        sl = slice(j * per_device_train_batch_size, (j + 1) * per_device_train_batch_size)
-        lp, ent = per_token_logps(model, data["p"][sl], data["pm"][sl], data["c"][sl], data["cm"][sl], temperature)
-        lp.retain_grad()
-        loss, _ = trl_ref.grpo_loss(lp, data["a"][sl], data["cm"][sl],
-                                    ref_per_token_logps=None if data["r"] is None else data["r"][sl],
-                                    entropies=ent, beta=beta,
-                                    epsilon_low=epsilon, epsilon_high=epsilon_high or epsilon, loss_type=loss_type,
-                                    importance_sampling_level=importance_sampling_level, max_completion_length=C)
-        (loss / GA).backward()
-        losses.append(float(loss.detach()) / GA)
-        grads_of_logps.append(lp.detach())
-    grads = ({n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
-             if capture else None)
-    total = torch.nn.utils.clip_grad_norm_(model.parameters(), max_grad_norm)
-    optimizer.step()
-    optimizer.zero_grad()
+    gen = {"prompt_ids": prompt_ids, "prompt_mask": prompt_mask, "completion_ids": completion_ids, "perm": perm}
+    rec = grpo_train(model, optimizer, [gen], reward_fn, num_generations=num_generations, C=C,
+                     per_device_train_batch_size=per_device_train_batch_size,
+                     gradient_accumulation_steps=min(spg, gradient_accumulation_steps), n_steps=1,
+                     steps_per_generation=spg, temperature=temperature, eos_token_id=eos_token_id, beta=beta,
+                     epsilon=epsilon, epsilon_high=epsilon_high, loss_type=loss_type,
+                     importance_sampling_level=importance_sampling_level, scale_rewards=scale_rewards,
+                     max_grad_norm=max_grad_norm, ref_model=ref_model, capture=capture)[0]
     t2 = time.perf_counter()
     if timings is not None:
         timings["generate_s"] = t1 - t0
         timings["update_s"] = t2 - t1
-    out = {"completion_ids": completion_ids, "completion_mask": mask, "advantages": adv, "rewards": rewards,
-           "grad_norm": float(total), "perm": perm}
+    sc = rec["gens"][0]
+    out = {"completion_ids": completion_ids, "completion_mask": sc["cm"], "advantages": sc["a"],
+           "rewards": sc["rewards"], "grad_norm": rec["grad_norm"], "perm": perm}
     if capture:
-        out.update(logps=torch.cat(grads_of_logps), grads=grads, losses=losses)
-    return sum(losses), out
+        out.update(logps=rec["logps"], grads=rec["grads"], losses=rec["losses"])
+    return rec["loss"], out

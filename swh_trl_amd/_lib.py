@@ -53,7 +53,7 @@ SIGNATURES = {
                                     c_vp]),
     "swh_grpo_loss_workspace_bytes": (c_i64, [c_i64]),
     "swh_grpo_loss_fwd_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
-                                      C.POINTER(GRPOLossParams), c_vp, c_vp, c_vp, c_vp, c_vp]),
+                                      C.POINTER(GRPOLossParams), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "swh_masked_whiten_workspace_bytes": (c_i64, [c_i64]),
     "swh_masked_whiten": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "swh_gae_scan": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_vp, c_vp, c_vp]),
@@ -62,7 +62,7 @@ SIGNATURES = {
                                      c_f32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "swh_ppo_truncate": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "swh_ppo_rewards": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_f32, c_i32, c_f32, c_i32, c_vp, c_vp, c_vp, c_vp,
-                                c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+                                c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "swh_value_head_fwd": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "swh_sqnorm_partials": (c_i64, [c_i64]),
     "swh_grad_sqnorm": (c_i32, [c_vp, c_i32, c_i64, c_vp, c_vp]),

@@ -130,7 +130,7 @@ __global__ __launch_bounds__(kBig) void grpo_loss_kernel(
     const float *__restrict__ adv, const int32_t *__restrict__ mask, const uint8_t *__restrict__ em,
     const float *__restrict__ ent, const float *__restrict__ row_scale, const int32_t *__restrict__ seg,
     int64_t R, int64_t T, swh_grpo_loss_params p, float *__restrict__ loss, float *__restrict__ dlp,
-    float *__restrict__ metrics, LossWS ws) {
+    float *__restrict__ metrics, float *__restrict__ seg_metrics, LossWS ws) {
     __shared__ float red[8 * (kBig / kWave)];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
     const int S = p.num_segments;
@@ -243,6 +243,54 @@ __global__ __launch_bounds__(kBig) void grpo_loss_kernel(
             acc[4] += lo;
             acc[5] += hi;
             acc[6] += fmaxf(lo, hi);
+        }
+    }
+    // Phase 6 (optional): the same metric sums per normaliser segment — one GA
+    // micro-batch each — so the host forms the reference's per-micro-batch
+    // masked_batch_mean (:2143-2148) before its cross-rank gather.  One wave per
+    // segment, rows in index order: fixed summation order.
+    if (seg_metrics) {
+        for (int s = wid; s < S; s += nw) {
+            float sm[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // tok, kl, ent, low, high, region, rows
+            for (int64_t r = 0; r < R; ++r) {
+                if ((seg ? seg[r] : 0) != s) continue;
+                const float A = adv[r];
+                const ClipOut cs = clip_term(ws.row_x[r], A, p.epsilon_low, p.epsilon_high, p.delta);
+                for (int64_t t = lane; t < T; t += 64) {
+                    const int64_t i = r * T + t;
+                    const float m = (float)mask[i];
+                    sm[0] += m;
+                    if (p.beta != 0.f) {
+                        const float d = ref[i] - lp[i];
+                        sm[1] += (expf(d) - d - 1.f) * m;
+                    }
+                    if (ent) sm[2] += ent[i] * m;
+                    if (!seq) {
+                        const ClipOut c = clip_term(old ? lp[i] - old[i] : 0.f, A, p.epsilon_low, p.epsilon_high,
+                                                    p.delta);
+                        const float lo = (c.c1d < 1.f - p.epsilon_low && A < 0.f) ? 1.f : 0.f;
+                        const float hi = (c.c1d > 1.f + p.epsilon_high && A > 0.f) ? 1.f : 0.f;
+                        sm[3] += lo * m;
+                        sm[4] += hi * m;
+                        sm[5] += fmaxf(lo, hi) * m;
+                    }
+                }
+                if (seq && lane == 0) {
+                    const float lo = (cs.c1d < 1.f - p.epsilon_low && A < 0.f) ? 1.f : 0.f;
+                    const float hi = (cs.c1d > 1.f + p.epsilon_high && A > 0.f) ? 1.f : 0.f;
+                    sm[3] += lo;
+                    sm[4] += hi;
+                    sm[5] += fmaxf(lo, hi);
+                }
+                if (lane == 0) sm[6] += 1.f;
+            }
+#pragma unroll
+            for (int k = 0; k < 7; ++k) sm[k] = wave_sum(sm[k]);
+            if (lane == 0) {
+#pragma unroll
+                for (int k = 0; k < 7; ++k) seg_metrics[s * 8 + k] = sm[k];
+                seg_metrics[s * 8 + 7] = 0.f;
+            }
         }
     }
     block_sum<7>(acc, red);
@@ -444,10 +492,14 @@ __global__ __launch_bounds__(256) void ppo_truncate_kernel(const int64_t *__rest
     if (threadIdx.x == 0) seq_len[b] = (int64_t)fpad - 1;
 }
 
+// DT: dtype of the score heads' outputs (values / scores): bf16 for the bf16
+// engine, f32 in the reference-precision mode; every update rounds like the
+// reference's tensor of that dtype.
+template <int DT>
 __global__ __launch_bounds__(256) void ppo_rewards_kernel(
     const int64_t *__restrict__ post, const int64_t *__restrict__ seq_len, int64_t T, int64_t eos, float penalty,
     int32_t has_penalty, float kl_coef, int32_t k3, float *__restrict__ logp, float *__restrict__ ref,
-    uint16_t *__restrict__ values, uint16_t *__restrict__ scores, uint8_t *__restrict__ pmask,
+    typename Elem<DT>::T *__restrict__ values, typename Elem<DT>::T *__restrict__ scores, uint8_t *__restrict__ pmask,
     uint8_t *__restrict__ pmask1, float *__restrict__ kl, float *__restrict__ nsr, float *__restrict__ rewards) {
     __shared__ int red[4];
     const int64_t b = blockIdx.x;
@@ -456,8 +508,8 @@ __global__ __launch_bounds__(256) void ppo_rewards_kernel(
     if (eos >= 0)
         for (int64_t t = threadIdx.x; t < T; t += blockDim.x) has |= (post[b * T + t] == eos);
     has = -block_min_i32(-has, red);  // any
-    float score = bf16_bits_to_f32(scores[b]);
-    if (has_penalty && !has) score = round_bf16(score - penalty);  // bf16 tensor minus a Python float
+    float score = Elem<DT>::load(scores + b);
+    if (has_penalty && !has) score = Elem<DT>::round(score - penalty);  // the score tensor minus a Python float
     const int64_t end = (sl + 1 < T) ? sl + 1 : sl;                  // ppo_trainer.py:513-515
     for (int64_t t = threadIdx.x; t < T; t += blockDim.x) {
         const int64_t i = b * T + t;
@@ -476,7 +528,10 @@ __global__ __launch_bounds__(256) void ppo_rewards_kernel(
         nsr[i] = n;
         rewards[i] = (t == end) ? n + score : n;
     }
-    if (threadIdx.x == 0) scores[b] = f32_to_bf16_bits(score);
+    if (threadIdx.x == 0) {
+        if constexpr (DT == SWH_F32) scores[b] = score;
+        else scores[b] = f32_to_bf16_bits(score);
+    }
 }
 
 }  // namespace
@@ -511,7 +566,7 @@ extern "C" int swh_grpo_loss_fwd_bwd(const float *logp, const float *old_logp, c
                                      const float *adv, const int32_t *mask, const uint8_t *ent_mask,
                                      const float *entropy, const float *row_scale, const int32_t *seg, int64_t R,
                                      int64_t T, const swh_grpo_loss_params *p, float *loss, float *dlogp,
-                                     float *metrics, void *workspace, void *stream) {
+                                     float *metrics, float *seg_metrics, void *workspace, void *stream) {
     if (!logp || !adv || !mask || !p || !loss || !workspace || R <= 0 || T <= 0) return SWH_E_ARG;
     const swh_grpo_loss_params pp = *p;
     if (pp.num_segments < 1 || pp.num_segments > 4096 || pp.loss_type < 0 || pp.loss_type > 2 || pp.is_level < 0 ||
@@ -522,7 +577,7 @@ extern "C" int swh_grpo_loss_fwd_bwd(const float *logp, const float *old_logp, c
     LossWS ws{w, w + R, w + 2 * R, w + 3 * R, w + 4 * R, w + 4 * R + 4096};
     grpo_loss_kernel<<<1, kBig, 0, static_cast<hipStream_t>(stream)>>>(logp, old_logp, ref_logp, adv, mask, ent_mask,
                                                                      entropy, row_scale, seg, R, T, pp, loss, dlogp,
-                                                                     metrics, ws);
+                                                                     metrics, seg_metrics, ws);
     return launch_status();
 }
 
@@ -599,16 +654,24 @@ extern "C" int swh_ppo_truncate(const int64_t *responses, int64_t B, int64_t T, 
 
 extern "C" int swh_ppo_rewards(const int64_t *post, const int64_t *seq_len, int64_t B, int64_t T, int64_t eos_token_id,
                                float missing_eos_penalty, int32_t has_penalty, float kl_coef, int32_t kl_k3,
-                               float *logprobs, float *ref_logprobs, void *values_bf16, void *scores_bf16,
+                               float *logprobs, float *ref_logprobs, void *values, void *scores, int32_t dtype,
                                uint8_t *padding_mask, uint8_t *padding_mask_p1, float *kl, float *non_score_reward,
                                float *rewards, void *stream) {
-    if (!post || !seq_len || !logprobs || !ref_logprobs || !values_bf16 || !scores_bf16 || !padding_mask ||
-        !padding_mask_p1 || !kl || !non_score_reward || !rewards || B < 0 || T <= 0 || T > (1 << 30))
+    if (!post || !seq_len || !logprobs || !ref_logprobs || !values || !scores || !padding_mask ||
+        !padding_mask_p1 || !kl || !non_score_reward || !rewards || B < 0 || T <= 0 || T > (1 << 30) ||
+        (dtype != SWH_F32 && dtype != SWH_BF16))
         return SWH_E_ARG;
     if (B == 0) return SWH_OK;
-    ppo_rewards_kernel<<<dim3((unsigned)B), 256, 0, static_cast<hipStream_t>(stream)>>>(
-        post, seq_len, T, eos_token_id, missing_eos_penalty, has_penalty, kl_coef, kl_k3, logprobs, ref_logprobs,
-        static_cast<uint16_t *>(values_bf16), static_cast<uint16_t *>(scores_bf16), padding_mask, padding_mask_p1,
-        kl, non_score_reward, rewards);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (dtype == SWH_F32)
+        ppo_rewards_kernel<SWH_F32><<<dim3((unsigned)B), 256, 0, s>>>(
+            post, seq_len, T, eos_token_id, missing_eos_penalty, has_penalty, kl_coef, kl_k3, logprobs, ref_logprobs,
+            static_cast<float *>(values), static_cast<float *>(scores), padding_mask, padding_mask_p1, kl,
+            non_score_reward, rewards);
+    else
+        ppo_rewards_kernel<SWH_BF16><<<dim3((unsigned)B), 256, 0, s>>>(
+            post, seq_len, T, eos_token_id, missing_eos_penalty, has_penalty, kl_coef, kl_k3, logprobs, ref_logprobs,
+            static_cast<uint16_t *>(values), static_cast<uint16_t *>(scores), padding_mask, padding_mask_p1, kl,
+            non_score_reward, rewards);
     return launch_status();
 }

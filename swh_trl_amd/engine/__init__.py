@@ -1,8 +1,11 @@
 """Decoder models + rollout engines."""
+import torch
+
 from .config import DecoderConfig, llama3_8b, qwen2_5_0_5b, tiny_llama, tiny_qwen2
 from .decode import DecodeEngine
 from .gpt2 import GPT2DecodeEngine, GPT2LM, gpt2_config
 from .model import CausalLM
+from .ref_decode import RefDecodeEngine
 
 
 def build_model(cfg: DecoderConfig, device, **kw) -> CausalLM:
@@ -11,11 +14,15 @@ def build_model(cfg: DecoderConfig, device, **kw) -> CausalLM:
 
 
 def build_engine(model: CausalLM, batch_size: int, max_prompt_len: int, max_new_tokens: int, **kw):
-    """The rollout engine of `model`'s family."""
+    """The rollout engine of `model`'s family and precision: GPT-2 (its own dtype), the
+    bf16 Qwen2 / Llama DecodeEngine, or the fp32 reference-precision RefDecodeEngine."""
     if model.cfg.model_type == "gpt2":
         return GPT2DecodeEngine(model, batch_size, max_prompt_len, max_new_tokens, **kw)
+    if model.dtype == torch.float32:
+        return RefDecodeEngine(model, batch_size, max_prompt_len, max_new_tokens, **kw)
     return DecodeEngine(model, batch_size, max_prompt_len, max_new_tokens, **kw)
 
 
-__all__ = ["DecoderConfig", "CausalLM", "DecodeEngine", "GPT2LM", "GPT2DecodeEngine", "build_model", "build_engine",
+__all__ = ["DecoderConfig", "CausalLM", "DecodeEngine", "RefDecodeEngine", "GPT2LM", "GPT2DecodeEngine", "build_model",
+           "build_engine",
            "gpt2_config", "qwen2_5_0_5b", "llama3_8b", "tiny_qwen2", "tiny_llama"]

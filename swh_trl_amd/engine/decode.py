@@ -11,7 +11,10 @@ Differences in mechanism, not in result:
     value (step index, prompt width, RNG counter, finished flags) in device
     memory: no host sync per token (the reference pays one per token in
     `unfinished_sequences.max()` and B*C more in `.item()` loops);
-  * optional early exit checked every `check_every` tokens.
+  * early exit once every row has finished (HF `_sample` stops the batch
+    then): the host keeps at most two graph replays queued ahead of a pinned
+    all-finished flag, so the check never drains the stream
+    (`EarlyExitPoll`); `check_every` is the legacy synchronous poll.
 Prefill runs the full-sequence forward once over the prompt and writes the
 post-RoPE keys/values into the cache.
 """
@@ -28,6 +31,40 @@ from .. import nn_ops, ops
 from ..profiling import trace as _trace
 from .._lib import call
 from .model import CausalLM
+
+
+class EarlyExitPoll:
+    """Stop-when-all-finished without a host sync per token.  After each graph
+    replay the device writes min(finished) into a slot of a pinned host ring and
+    records an event; the host only waits for the event `depth` replays back,
+    by which time the stream still holds `depth` replays of queued work, so the
+    GPU never idles on the check.  Costs one tiny reduction + a 4-byte copy per
+    replay; finds the batch finished at most `depth` replays late (the extra
+    steps only write pad tokens)."""
+
+    def __init__(self, finished: torch.Tensor, depth: int = 2):
+        self.finished, self.depth = finished, depth
+        self.host = torch.zeros(depth + 2, dtype=torch.int32, pin_memory=True)
+        self.pending: list = []
+        self.n = 0
+
+    def reset(self):
+        self.pending.clear()
+        self.n = 0
+
+    def after_replay(self) -> bool:
+        """Queue the flag of the work issued so far; True once a flag shows every row finished."""
+        j = self.n % self.host.numel()
+        self.n += 1
+        self.host[j:j + 1].copy_(self.finished.min().view(1), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.pending.append((ev, j))
+        if len(self.pending) <= self.depth:
+            return False
+        ev0, j0 = self.pending.pop(0)
+        ev0.synchronize()
+        return bool(self.host[j0] != 0)
 
 
 @contextlib.contextmanager
@@ -154,6 +191,8 @@ class DecodeEngine:
         # the attention launch warms the gate/up weights into the consuming XCDs' L2:
         # gate/up gains what the longer attention launch loses, off
         self.prefetch = os.environ.get("SWH_DECODE_PREFETCH", "0") != "0"
+        self._exit_poll = EarlyExitPoll(self.finished)
+        self.steps_run = 0  # decode steps the last generate() ran (early exit: fewer than max_new_tokens - 1)
 
     # ------------------------------------------------------------------ one decode step (capturable)
     def _step(self):
@@ -556,10 +595,12 @@ class DecodeEngine:
     def generate(self, prompt_ids: torch.Tensor, prompt_mask: torch.Tensor, max_new_tokens: int, *,
                  temperature=1.0, top_p=1.0, top_k=None, min_p=None, repetition_penalty=1.0, greedy=False,
                  min_new_tokens=0, eos_token_id=None, pad_token_id=None, seed: int = 0, offset: int = 0,
-                 return_logp: bool = False, check_every: int = 0, group_size: int = 0):
+                 return_logp: bool = False, check_every: int = 0, group_size: int = 0, early_exit: bool = True):
         """prompt_ids [B, P] left-padded (B == engine batch).  Returns completion ids
         [B, max_new_tokens] (pad after EOS, like `_sample`) and optional per-token
-        log-probs of the drawn tokens under the processed distribution."""
+        log-probs of the drawn tokens under the processed distribution.
+        early_exit: stop replaying decode steps once every row has finished
+        (`EarlyExitPoll`, no per-token sync); the remaining columns stay pad."""
         B, P = prompt_ids.shape
         if B != self.B or P > self.Pmax or max_new_tokens > self.Cmax:
             raise ValueError(f"engine sized for B={self.B}, P<={self.Pmax}, C<={self.Cmax}; got {B}x{P}, "
@@ -591,17 +632,29 @@ class DecodeEngine:
             nn_ops.embed_gather(self.model.p["embed"], self.cur, self.s, ss_out=self.ss)
         s = 1
         K = self.steps_per_graph
+        poll = self._exit_poll if (early_exit and eos and not check_every) else None
+        if poll is not None:
+            poll.reset()
+        since = 0
         while s < max_new_tokens:
             if self.use_graph and self.graph_k is not None and not check_every and s + K <= max_new_tokens:
                 self.graph_k.replay()
                 s += K
+                if poll is not None and poll.after_replay():
+                    break
                 continue
             if self.use_graph:
                 self.graph.replay()
             else:
                 self._step()
-            if check_every and s % check_every == 0 and bool(self.finished.all()):
-                break
             s += 1
+            since += 1
+            if check_every and (s - 1) % check_every == 0 and bool(self.finished.all()):
+                break
+            if poll is not None and since >= K and poll.after_replay():
+                break
+            if since >= K:
+                since = 0
+        self.steps_run = s - 1
         comp = self.out[:, :max_new_tokens]
         return comp.clone(), (self.out_logp[:, :max_new_tokens].clone() if return_logp else None)

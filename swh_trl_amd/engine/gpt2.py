@@ -421,9 +421,12 @@ class GPT2DecodeEngine:
     def generate(self, prompt_ids: torch.Tensor, prompt_mask: torch.Tensor, max_new_tokens: int, *,
                  temperature=1.0, top_p=1.0, top_k=None, min_p=None, repetition_penalty=1.0, greedy=False,
                  min_new_tokens=0, eos_token_id=None, pad_token_id=None, seed: int = 0, offset: int = 0,
-                 return_logp: bool = False, check_every: int = 0, group_size: int = 0):
+                 return_logp: bool = False, check_every: int = 0, group_size: int = 0, early_exit: bool = True):
         """As DecodeEngine.generate: completion ids [B, max_new_tokens] (pad after
-        EOS) and optional per-token log-probs under the processed distribution."""
+        EOS) and optional per-token log-probs under the processed distribution;
+        early_exit: stop once every row has finished (polled every 8 steps,
+        `EarlyExitPoll`)."""
+        from .decode import EarlyExitPoll
         del group_size
         B, P = prompt_ids.shape
         if B != self.B or P > self.Pmax or max_new_tokens > self.Cmax:
@@ -461,12 +464,17 @@ class GPT2DecodeEngine:
         self.state[0], self.state[1] = 0, P
         self._sample()
         ops.step_advance(self.state[0:1])
+        poll = EarlyExitPoll(self.finished) if (early_exit and eos and not check_every) else None
+        self.steps_run = 0
         for s in range(1, max_new_tokens):
             if self.use_graph:
                 self.graph.replay()
             else:
                 self._step()
+            self.steps_run = s
             if check_every and s % check_every == 0 and bool(self.finished.all()):
+                break
+            if poll is not None and s % 8 == 0 and poll.after_replay():
                 break
         comp = self.out[:, :max_new_tokens]
         return comp.clone(), (self.out_logp[:, :max_new_tokens].clone() if return_logp else None)

@@ -251,8 +251,9 @@ def grpo_loss_fwd_bwd(per_token_logps: torch.Tensor, advantages: torch.Tensor, c
                       row_scale=None, segments=None, num_segments: int = 1, beta: float = 0.0,
                       epsilon_low: float = 0.2, epsilon_high: float = 0.2, delta: Optional[float] = None,
                       loss_type: str = "bnpo", importance_sampling_level: str = "token",
-                      max_completion_length: int = 256, need_grad: bool = True):
-    """grpo_trainer.py:2058-2175 fused: returns (loss[1], dlogp or None, metric sums[8])."""
+                      max_completion_length: int = 256, need_grad: bool = True, segment_metrics: bool = False):
+    """grpo_trainer.py:2058-2175 fused: returns (loss[1], dlogp or None, metric sums[8]); with
+    segment_metrics, metric sums [1 + num_segments, 8]: the totals, then one row per segment."""
     _dev(per_token_logps, "grpo_loss")
     if loss_type not in _lib.LOSS_TYPES:
         raise ValueError(f"Unknown loss type: {loss_type}")
@@ -279,11 +280,12 @@ def grpo_loss_fwd_bwd(per_token_logps: torch.Tensor, advantages: torch.Tensor, c
                        int(max_completion_length), int(num_segments))
     loss = torch.empty(1, device=dev, dtype=torch.float32)
     dlogp = torch.empty_like(lp) if need_grad else None
-    metrics = torch.empty(8, device=dev, dtype=torch.float32)
+    metrics = torch.empty((1 + num_segments) if segment_metrics else 1, 8, device=dev, dtype=torch.float32)
     ws = torch.empty(_lib.load().swh_grpo_loss_workspace_bytes(R) // 4 + 1, device=dev, dtype=torch.float32)
     call("swh_grpo_loss_fwd_bwd", lp.data_ptr(), _p(old), _p(ref), adv.data_ptr(), mask.data_ptr(), _p(em), _p(ent),
-         _p(rs), _p(seg), R, T, p, loss.data_ptr(), _p(dlogp), metrics.data_ptr(), ws.data_ptr(), _stream())
-    return loss, dlogp, metrics
+         _p(rs), _p(seg), R, T, p, loss.data_ptr(), _p(dlogp), metrics.data_ptr(),
+         metrics[1:].data_ptr() if segment_metrics else None, ws.data_ptr(), _stream())
+    return loss, dlogp, (metrics if segment_metrics else metrics[0])
 
 
 class _GRPOLossFn(torch.autograd.Function):
@@ -363,12 +365,13 @@ def ppo_rewards(post: torch.Tensor, sequence_lengths: torch.Tensor, logprobs: to
     """ppo_trainer.py:490-516 in one launch: masks, INVALID_LOGPROB fill, value
     masking, missing-EOS penalty, KL (k1 / k3) and KL-shaped rewards with the
     score scattered at min(seq_len + 1, T - 1).  values / scores are the bf16
-    outputs of the score heads (modified like the reference's tensors)."""
+    outputs of the score heads, bf16 or fp32 (reference-precision mode), modified
+    like the reference's tensors of that dtype."""
     _dev(post, "ppo_rewards")
     if kl_estimator not in ("k1", "k3"):
         raise ValueError(f"kl_estimator must be 'k1' or 'k3', got {kl_estimator!r}")
-    if values.dtype != torch.bfloat16 or scores.dtype != torch.bfloat16:
-        raise ValueError("ppo_rewards: values and scores are the bf16 score-head outputs")
+    if values.dtype != scores.dtype or values.dtype not in (torch.bfloat16, torch.float32):
+        raise ValueError("ppo_rewards: values and scores are the score-head outputs (both bf16 or both fp32)")
     B, T = post.shape
     lp = logprobs.to(torch.float32).contiguous().clone()
     rf = ref_logprobs.to(torch.float32).contiguous().clone()
@@ -381,7 +384,7 @@ def ppo_rewards(post: torch.Tensor, sequence_lengths: torch.Tensor, logprobs: to
          T, -1 if eos_token_id is None else int(eos_token_id),
          0.0 if missing_eos_penalty is None else float(missing_eos_penalty), int(missing_eos_penalty is not None),
          float(kl_coef), int(kl_estimator == "k3"), lp.data_ptr(), rf.data_ptr(), v.data_ptr(), s.data_ptr(),
-         pm.data_ptr(), pm1.data_ptr(), kl.data_ptr(), nsr.data_ptr(), rew.data_ptr(), _stream())
+         _dtype_code(v, "ppo_rewards"), pm.data_ptr(), pm1.data_ptr(), kl.data_ptr(), nsr.data_ptr(), rew.data_ptr(), _stream())
     return {"logprobs": lp, "ref_logprobs": rf, "values": v, "scores": s, "padding_mask": pm,
             "padding_mask_p1": pm1, "kl": kl, "non_score_reward": nsr, "rewards": rew}
 

@@ -14,14 +14,17 @@ ppo_trainer.py:752-758; PPOTrainer.save_model keeps only the policy,
                                         model.named_parameters() order, split
                                         into the Trainer's decay / no-decay
                                         param groups
-  scheduler.pt                          LambdaLR-style state (last_epoch, lrs)
+  scheduler.pt                          torch LambdaLR.state_dict() of the
+                                        Trainer's schedule (loads into
+                                        LambdaLR.load_state_dict)
   trainer_state.json                    transformers TrainerState fields
   README.md                             the trainer's model card
 
 plus the engine's own exact-resume state, which a transformers checkpoint
 does not carry: `swh_master.safetensors` (the fp32 master weights; the model
-file holds the bf16 weights) and `swh_trainer_state.pt` (tensors only: data
-stream position, shuffle / sampler generator states, buffered rollouts).
+file holds the bf16 weights) and one `swh_trainer_state_<rank>.pt` per rank
+(tensors only: data stream position, that rank's shuffle generator and
+buffered rollouts — as transformers keeps one rng_state_<rank>.pth per process).
 Loading reads safetensors / JSON, and torch.load(weights_only=True) only.
 """
 from __future__ import annotations
@@ -241,6 +244,39 @@ PPO_CITATION = ("@article{mziegler2019fine-tuning,\n    title        = {{Fine-Tu
                 "Preferences}},\n    author       = {Daniel M. Ziegler and Nisan Stiennon and Jeffrey Wu and Tom B. "
                 "Brown and Alec Radford and Dario Amodei and Paul F. Christiano and Geoffrey Irving},\n    year     "
                 "    = 2019,\n    eprint       = {arXiv:1909.08593},\n}")
+
+
+def _linear_lambda(step: int, *, warmup: int, total: int) -> float:
+    """transformers' _get_linear_schedule_with_warmup_lr_lambda."""
+    if step < warmup:
+        return float(step) / float(max(1, warmup))
+    return max(0.0, float(total - step) / float(max(1, total - warmup)))
+
+
+def _constant_lambda(_step: int) -> float:
+    return 1.0
+
+
+def scheduler_state_dict(global_step: int, total: int, lr: float, warmup: int, kind: str = "linear",
+                         n_groups: int = 2) -> dict:
+    """torch LambdaLR.state_dict() of the Trainer's scheduler after `global_step`
+    optimizer steps (transformers get_scheduler: linear warmup/decay, or
+    constant), over its `n_groups` param groups (decay / no decay).  Built from
+    a real LambdaLR so the keys are the installed torch's own (lr_lambdas
+    included: LambdaLR.load_state_dict pops it)."""
+    import functools
+    p = [torch.nn.Parameter(torch.zeros(1)) for _ in range(n_groups)]
+    opt = torch.optim.SGD([{"params": [q]} for q in p], lr=lr)
+    fn = functools.partial(_linear_lambda, warmup=warmup, total=total) if kind == "linear" else _constant_lambda
+    sch = torch.optim.lr_scheduler.LambdaLR(opt, fn)
+    sch.last_epoch = global_step
+    sch._step_count = global_step + 1
+    sch._last_lr = [lr * fn(global_step) for _ in range(n_groups)]
+    return sch.state_dict()
+
+
+def trainer_state_file(rank: int) -> str:
+    return f"swh_trainer_state_{rank}.pt"
 
 
 def save_master(opt, out_dir: str) -> None:

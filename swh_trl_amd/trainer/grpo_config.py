@@ -86,7 +86,8 @@ class GRPOConfig:
     # MI355X engine knobs (no reference counterpart)
     fuse_micro_batches: bool = True        # run the GA micro-batches as one forward/backward
     fuse_token_budget: int = 1 << 17       # max rows*(P+C) tokens per fused pass
-    decode_check_every: int = 0            # early-exit poll interval (0 = never; graph replays all steps)
+    decode_early_exit: bool = True         # stop decoding once every row has finished (HF _sample), no per-token sync
+    decode_check_every: int = 0            # legacy synchronous all-finished poll every k steps (0 = off)
     extra: dict = field(default_factory=dict)
 
     def __init__(self, **kwargs):

@@ -68,13 +68,22 @@ def model_dtype(model_init_kwargs: Optional[dict]) -> torch.dtype:
     raise ValueError(f"model dtype {d!r}: the MI355X engine trains bfloat16 or float32 models")
 
 
-def load_model(model, device, trainable=True, seed=0, head: str = "lm", dtype=torch.bfloat16) -> CausalLM:
+def load_model(model, device, trainable=True, seed=0, head: str = "lm", dtype=None) -> CausalLM:
     """`model` may be a CausalLM, a preset name ("qwen2.5-0.5b", "llama-3-8b",
     "tiny"), a DecoderConfig (random init), a local directory holding a
     transformers config.json + safetensors, or a transformers PreTrainedModel.
     head="score": a sequence-classification model (value / reward model, one
     output), as transformers' *ForSequenceClassification.  `dtype`: parameter
-    dtype of a newly built model (a CausalLM passed in keeps its own)."""
+    dtype of a model built from a name / config / directory (default bf16); a
+    model object keeps its own precision (a CausalLM as is; a transformers
+    module fp32 -> fp32, bf16 / fp16 -> bf16), as the reference trains the
+    module it is given in its dtype."""
+    if dtype is None:
+        dtype = torch.bfloat16
+        if hasattr(model, "parameters") and not isinstance(model, CausalLM):
+            p0 = next(iter(model.parameters()), None)
+            if p0 is not None and p0.dtype == torch.float32:
+                dtype = torch.float32
     if isinstance(model, CausalLM):
         if model.head != head:
             raise ValueError(f"expected a model with a {head!r} head, got {model.head!r}")
@@ -109,6 +118,19 @@ def load_model(model, device, trainable=True, seed=0, head: str = "lm", dtype=to
     raise TypeError(f"unsupported model type {type(model)}")
 
 
+def _pad_completions(mb: dict, W: int, pad_token_id: int) -> dict:
+    """A micro-batch's completion-side tensors right-padded to width W (pad ids,
+    mask 0, log-probs 0): the extra columns are masked out of every sum."""
+    out = dict(mb)
+    w = mb["completion_ids"].shape[1]
+    fill = {"completion_ids": pad_token_id, "completion_mask": 0, "old_per_token_logps": 0.0,
+            "ref_per_token_logps": 0.0}
+    for k, v in fill.items():
+        if k in mb and mb[k] is not None:
+            out[k] = torch.nn.functional.pad(mb[k], (0, W - w), value=v)
+    return out
+
+
 class GRPOTrainer:
     _tag_names = ["trl", "grpo"]
 
@@ -127,10 +149,7 @@ class GRPOTrainer:
         gemm_tuning.enable()
         torch.manual_seed(a.seed)
         self.model = load_model(model, self.device, trainable=True, seed=a.seed,
-                                dtype=model_dtype(a.model_init_kwargs))
-        # the decode engine's kernels are bf16: an fp32 model rolls out from a bf16
-        # copy of its weights, refreshed before every generation
-        self._rollout_model: Optional[CausalLM] = None
+                                dtype=None if hasattr(model, "parameters") else model_dtype(a.model_init_kwargs))
         self.processing_class = processing_class
         if not isinstance(reward_funcs, list):
             reward_funcs = [reward_funcs]
@@ -237,21 +256,11 @@ class GRPOTrainer:
             ids, mask = truncate_with_protected_tokens(ids, mask, self.max_prompt_length, [])
         return ids, mask, texts
 
-    def _generation_model(self) -> CausalLM:
-        """The bf16 weights the decode engine reads: the policy itself, or for an
-        fp32 policy a bf16 copy refreshed now (one cast of the flat buffer)."""
-        m = self.model
-        if m.dtype == torch.bfloat16 or m.cfg.model_type == "gpt2":  # the GPT-2 step runs in the model dtype
-            return m
-        if self._rollout_model is None:
-            self._rollout_model = build_model(m.cfg, self.device, seed=None, trainable=False,
-                                              dtype=torch.bfloat16)
-        self._rollout_model.flat.copy_(m.flat)
-        return self._rollout_model
-
     def _engine_for(self, B: int, P: int) -> DecodeEngine:
         C = self.max_completion_length
-        gm = self._generation_model()
+        # the policy itself: bf16 on the DecodeEngine, an fp32 policy on the fp32
+        # RefDecodeEngine (the reference generates in the model dtype, :1793-1810)
+        gm = self.model
         e = self._engine
         if e is None or e.B != B or e.Pmax < P or e.model is not gm:
             Pmax = max(P, self.max_prompt_length or P) if (self.max_prompt_length or 0) <= 4096 else P
@@ -271,12 +280,21 @@ class GRPOTrainer:
                                          eos_token_id=self.eos_token_id, pad_token_id=self.pad_token_id,
                                          seed=seed, offset=self._gen_count * (self.max_completion_length + 1),
                                          check_every=a.decode_check_every, group_size=self.num_generations,
-                                         **self.gen_kwargs)
+                                         early_exit=a.decode_early_exit, **self.gen_kwargs)
         self._gen_count += 1
         _trace("generated")
         eos = [] if self.eos_token_id is None else self.eos_token_id
         completion_mask, lengths, has_eos = ops.completion_mask(completion_ids, eos,
                                                                 self.mask_truncated_completions)
+        # HF generate stops the batch once every row has emitted EOS: the reference's
+        # completions are as wide as the longest row (:1793-1810); the columns past it
+        # are pad with mask 0 in every row, so dropping them changes no value and
+        # saves their scoring / training compute
+        lh = torch.stack([lengths.max().to(torch.int64), has_eos.min().to(torch.int64)]).cpu()
+        width = int(lh[0]) if int(lh[1]) else completion_ids.shape[1]
+        if width < completion_ids.shape[1]:
+            completion_ids = completion_ids[:, :width].contiguous()
+            completion_mask = completion_mask[:, :width].contiguous()
         rewards_per_func = self._calculate_rewards(examples, prompts_text, prompt_ids, prompt_mask, completion_ids,
                                                    completion_mask)
         _trace("rewards")
@@ -300,12 +318,15 @@ class GRPOTrainer:
         if self.beta != 0.0:
             out["ref_per_token_logps"] = self._score_logps(self.ref_model, out)
         m = self._metrics["train"]
-        m["_lengths"].append(lengths.float())
+        # per generation, resolved at the next log (no host sync here): this rank's
+        # lengths / EOS flags (gathered across ranks at the log, :1945-1960), its
+        # attention-mask token count (:1942), and the global reward statistics
+        m["_lengths"].append(torch.stack([lengths.float(), has_eos.float()], 1))
+        m["_tokens"].append((prompt_mask.sum() + completion_mask.sum()).float().view(1, 1))
         m["_rewards"].append(gmean)
         m["_reward_std"].append(gstd)
         m["_zero_std"].append(zstd.float())
         m["_rpf"].append(rewards_per_func)
-        self.state.num_input_tokens_seen += int(B * P + B * self.max_completion_length) * self.world
         return out
 
     def _completions_for_rewards(self, examples, ids_h, completion_ids_list):
@@ -425,6 +446,9 @@ class GRPOTrainer:
         a = self.args
         GA = a.gradient_accumulation_steps
         R_each = [m["completion_ids"].shape[0] for m in micro]
+        W = max(m["completion_ids"].shape[1] for m in micro)
+        if any(m["completion_ids"].shape[1] != W for m in micro):  # rollouts of different widths (early stop)
+            micro = [_pad_completions(m, W, self.pad_token_id) for m in micro]
         batch = {
             "prompt_ids": pad_left_cat([m["prompt_ids"] for m in micro], self.pad_token_id),
             "prompt_mask": pad_left_cat([m["prompt_mask"] for m in micro], 0),
@@ -456,7 +480,7 @@ class GRPOTrainer:
             entropy_mask=emask, entropies=ent, row_scale=row_scale, segments=seg, num_segments=len(micro),
             beta=self.beta, epsilon_low=self.epsilon_low, epsilon_high=self.epsilon_high, delta=a.delta,
             loss_type=self.loss_type, importance_sampling_level=self.importance_sampling_level,
-            max_completion_length=self.max_completion_length)
+            max_completion_length=self.max_completion_length, segment_metrics=True)
         _trace("loss")
         loss.backward()
         dw_sync(self.device)  # the weight-gradient side stream joins the compute stream
@@ -530,48 +554,106 @@ class GRPOTrainer:
         loss = sum(o["loss"] for o in outs) if len(outs) > 1 else outs[0]["loss"]
         if len(outs) > 1:
             loss = loss  # per-micro losses already carry the 1/GA row scale
-        met = sum(o["metrics"] for o in outs)
         m = self._metrics["train"]
         m["_loss"].append(loss)
-        m["_met"].append(met)
+        # one row of metric sums per GA micro-batch (the loss kernel's segments)
+        m["_met"].append(torch.cat([o["metrics"][1:] for o in outs]))
         m["_grad_norm"].append(norm.clone())
         m["_lr"].append(torch.tensor(lr))
         return {"loss": loss, "grad_norm": norm}
 
     def _flush_logs(self) -> dict:
-        """Average the device-side metric buffers (one host sync per log)."""
+        """GRPOTrainer.log (grpo_trainer.py:2185-2196): every metric list averaged
+        since the last log.  The per-rank quantities are gathered across ranks
+        as the reference gathers them — completion lengths and EOS flags
+        (:1945-1960), token counts (:1942), the per-micro-batch masked means of
+        KL / entropy / clip ratios (:2143-2174, nanmean / nanmin / nanmax over
+        ranks) and the loss (transformers' Trainer gathers tr_loss) — in one
+        host sync per log."""
         m = self._metrics["train"]
         if not m.get("_loss"):
             return {}
-        met = torch.stack(m["_met"]).sum(0).cpu()
-        tok = max(float(met[0]), 1.0)
-        lengths = torch.cat(m["_lengths"]).cpu()
-        log = {
-            "loss": float(torch.stack(m["_loss"]).mean()),
-            "grad_norm": float(torch.stack(m["_grad_norm"]).mean()),
-            "learning_rate": float(m["_lr"][-1]),
-            "num_tokens": self.state.num_input_tokens_seen,
-            "completions/mean_length": float(lengths.mean()),
-            "completions/min_length": float(lengths.min()),
-            "completions/max_length": float(lengths.max()),
-            "reward": float(torch.cat(m["_rewards"]).mean()) if m["_rewards"] else float("nan"),
-            "reward_std": float(torch.cat(m["_reward_std"]).mean()) if m["_reward_std"] else float("nan"),
-            "frac_reward_zero_std": float(torch.cat(m["_zero_std"]).mean()) if m["_zero_std"] else float("nan"),
-            "entropy": float(met[2]) / tok,
-            "clip_ratio/low_mean": float(met[3]) / tok,
-            "clip_ratio/high_mean": float(met[4]) / tok,
-            "clip_ratio/region_mean": float(met[5]) / tok,
-            "step": self.state.global_step,
-        }
+        gather = swh_dist.all_gather_rows
+        world = self.world
+        n_gen = len(m["_lengths"])
+        seg = gather(torch.cat(m["_met"])).cpu()                # [world * n_micro, 8]
+        lens = gather(torch.cat(m["_lengths"])).cpu()           # [world * n_gen * B, 2]
+        losses = gather(torch.stack(m["_loss"]).view(-1, 1).float()).cpu()
+        self._count_tokens()
+        n_micro = seg.shape[0] // world
+        seg = seg.view(world, n_micro, 8)
+        tok = seg[..., 0].clamp(min=1.0)
+        rows = seg[..., 6]
+        clip_den = rows if self.importance_sampling_level == "sequence" else tok
+
+        def over_ranks(x):  # [world, n_micro]: nanmean over ranks per micro-batch, then the log's mean
+            return float(torch.nanmean(x, 0).mean())
+
+        def nanmin(x):
+            return torch.stack([c[~c.isnan()].min() if (~c.isnan()).any() else torch.tensor(float("nan"))
+                                for c in x.t()])
+
+        def nanmax(x):
+            return torch.stack([c[~c.isnan()].max() if (~c.isnan()).any() else torch.tensor(float("nan"))
+                                for c in x.t()])
+
+        log = {"loss": float(losses.view(world, -1).mean(0).mean()),
+               "grad_norm": float(torch.stack(m["_grad_norm"]).mean()),
+               "learning_rate": float(m["_lr"][-1]),
+               "num_tokens": self.state.num_input_tokens_seen}
+        # completions (:1945-1960), one entry per generation, averaged
+        B = lens.shape[0] // (world * n_gen)
+        per_gen = lens.view(world, n_gen, B, 2).transpose(0, 1).reshape(n_gen, world * B, 2)
+        agg = {k: [] for k in ("mean_length", "min_length", "max_length", "clipped_ratio", "mean_terminated_length",
+                               "min_terminated_length", "max_terminated_length")}
+        for g in per_gen:
+            ln, eos = g[:, 0], g[:, 1].bool()
+            term = ln[eos] if bool(eos.any()) else torch.zeros(1)
+            agg["mean_length"].append(float(ln.mean()))
+            agg["min_length"].append(float(ln.min()))
+            agg["max_length"].append(float(ln.max()))
+            agg["clipped_ratio"].append(1.0 - float(eos.sum()) / ln.numel())
+            agg["mean_terminated_length"].append(float(term.mean()))
+            agg["min_terminated_length"].append(float(term.min()))
+            agg["max_terminated_length"].append(float(term.max()))
+        for k, v in agg.items():
+            log[f"completions/{k}"] = sum(v) / len(v)
+        # rewards (global after the gather at :1497), one entry per generation
+        for i, name in enumerate(self.reward_func_names):
+            means = [float(torch.nanmean(r[:, i].cpu())) for r in m["_rpf"]]
+            stds = []
+            for r in m["_rpf"]:
+                col = r[:, i].cpu()
+                col = col[~col.isnan()]
+                stds.append(float(col.std()) if col.numel() > 1 else float("nan"))
+            log[f"rewards/{name}/mean"] = sum(means) / len(means)
+            log[f"rewards/{name}/std"] = sum(stds) / len(stds)
+        log["reward"] = sum(float(x.mean()) for x in m["_rewards"]) / len(m["_rewards"])
+        log["reward_std"] = sum(float(x.mean()) for x in m["_reward_std"]) / len(m["_reward_std"])
+        log["frac_reward_zero_std"] = sum(float(x.mean()) for x in m["_zero_std"]) / len(m["_zero_std"])
+        # loss metrics (:2139-2174): per micro-batch masked means, gathered over ranks
         if self.beta != 0.0:
-            log["kl"] = float(met[1]) / tok
-        if m["_rpf"]:
-            rpf = torch.cat(m["_rpf"]).cpu()
-            for i, name in enumerate(self.reward_func_names):
-                log[f"rewards/{name}/mean"] = float(torch.nanmean(rpf[:, i]))
+            log["kl"] = over_ranks(seg[..., 1] / tok)
+        log["entropy"] = over_ranks(seg[..., 2] / tok)
+        low, high, region = seg[..., 3] / clip_den, seg[..., 4] / clip_den, seg[..., 5] / clip_den
+        log["clip_ratio/low_mean"] = over_ranks(low)
+        log["clip_ratio/low_min"] = float(nanmin(low).mean())
+        log["clip_ratio/high_mean"] = over_ranks(high)
+        log["clip_ratio/high_max"] = float(nanmax(high).mean())
+        log["clip_ratio/region_mean"] = over_ranks(region)
+        log["step"] = self.state.global_step
         m.clear()
         self.state.log_history.append(log)
         return log
+
+    def _count_tokens(self):
+        """Fold the pending per-generation attention-mask token counts of every
+        rank into state.num_input_tokens_seen (grpo_trainer.py:1942: the gathered
+        sum of prompt + completion mask tokens); one gather."""
+        m = self._metrics["train"]
+        if m.get("_tokens"):
+            self.state.num_input_tokens_seen += int(swh_dist.all_gather_rows(torch.cat(m["_tokens"])).sum())
+            m["_tokens"] = []
 
     # ------------------------------------------------------------------ checkpoints (SURVEY.md §8 f4)
     def save_model(self, output_dir: Optional[str] = None, _internal_call: bool = False):
@@ -610,19 +692,23 @@ class GRPOTrainer:
         name = a.hub_model_id.split("/")[-1] if a.hub_model_id else os.path.basename(os.path.normpath(a.output_dir))
         self.create_model_card(model_name=name)
         d = os.path.join(a.output_dir, f"checkpoint-{self.state.global_step}")
-        self.save_model(d)
+        self._count_tokens()  # every rank: a gather
+        self.save_model(d)  # rank 0 creates d; ends in a barrier
+        if not a.save_only_model:
+            # every rank its own data-stream state: its shuffle generator and buffered
+            # rollouts differ (transformers: rng_state_<process_index>.pth)
+            torch.save(self._resume_state(), os.path.join(d, ck.trainer_state_file(self.rank)))
         if self.rank == 0:
             if not a.save_only_model:
                 torch.save(ck.optimizer_state_dict(self.model, self.optimizer, a.weight_decay),
                            os.path.join(d, "optimizer.pt"))
-                torch.save({"last_epoch": self.state.global_step, "_step_count": self.state.global_step + 1,
-                            "base_lrs": [a.learning_rate, a.learning_rate], "_last_lr": [self._current_lr()] * 2},
+                torch.save(ck.scheduler_state_dict(self.state.global_step, max(1, self.state.max_steps),
+                                                   a.learning_rate, a.warmup_steps, a.lr_scheduler_type),
                            os.path.join(d, "scheduler.pt"))
                 ck.save_master(self.optimizer, d)
                 if self.ref_model is not None and a.sync_ref_model:  # the mixed reference is trainer state
                     from safetensors.torch import save_file
                     save_file({"ref": self.ref_model.flat.detach().cpu()}, os.path.join(d, "swh_ref.safetensors"))
-                torch.save(self._resume_state(), os.path.join(d, "swh_trainer_state.pt"))
             with open(os.path.join(d, "trainer_state.json"), "w") as f:
                 json.dump(ck.trainer_state_json(self.state, a, a.per_device_train_batch_size), f, indent=2)
             ck.rotate_checkpoints(a.output_dir, a.save_total_limit)
@@ -670,7 +756,10 @@ class GRPOTrainer:
         self.state.global_step = int(js["global_step"])
         self.state.log_history = list(js.get("log_history", []))
         self.state.num_input_tokens_seen = int(js.get("num_input_tokens_seen", 0))
-        sp = os.path.join(d, "swh_trainer_state.pt")
+        sp = os.path.join(d, ck.trainer_state_file(self.rank))
+        if not os.path.exists(sp) and any(f.startswith("swh_trainer_state_") for f in os.listdir(d)):
+            raise ValueError(f"{d}: no {ck.trainer_state_file(self.rank)} (checkpoint saved by fewer ranks); the "
+                             "exact-resume state is per rank")
         if os.path.exists(sp):
             st = torch.load(sp, weights_only=True)
             self._gen_count = int(st["gen_count"])
@@ -706,7 +795,8 @@ class GRPOTrainer:
                                          / a.gradient_accumulation_steps * a.num_train_epochs)))
         self.state.max_steps = total
         log_every = int(a.logging_steps) if a.logging_steps >= 1 else max(1, int(total * a.logging_steps))
-        save_every = int(a.save_steps) if a.save_steps >= 1 else max(1, int(total * a.save_steps))
+        # TrainingArguments: a fraction of max_steps, rounded up
+        save_every = int(a.save_steps) if a.save_steps >= 1 else max(1, math.ceil(total * a.save_steps))
         t0 = time.time()
         while self.state.global_step < total:
             self.training_step_group()

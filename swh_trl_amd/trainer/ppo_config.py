@@ -71,7 +71,10 @@ class PPOConfig:
     lam: float = 0.95
     ds3_gather_for_generation: bool = True
     # engine knobs (not in the reference)
-    decode_check_every: int = 8            # host check of "all finished" every k decode steps (0 = never)
+    model_init_kwargs: Optional[dict] = None  # {"torch_dtype": "float32"}: reference precision for models built
+    #                                           from names / configs (model objects keep their own dtype)
+    decode_early_exit: bool = True         # stop decoding once every row has finished (HF _sample), no per-token sync
+    decode_check_every: int = 0            # legacy synchronous all-finished poll every k steps (0 = off)
     fuse_micro_batches: bool = True        # a mini-batch's GA micro-batches as one forward/backward
     fuse_token_budget: int = 1 << 16       # max rows * (query + response) tokens per fused pass
     extra: dict = field(default_factory=dict)

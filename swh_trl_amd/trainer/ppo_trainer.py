@@ -37,7 +37,7 @@ from ..engine import build_engine, build_model
 from ..engine.decode import DecodeEngine
 from ..engine.model import CausalLM, dw_sync
 from ..optim import FlatAdamW
-from .grpo_trainer import TrainerState, _trace, load_model
+from .grpo_trainer import TrainerState, _trace, load_model, model_dtype
 from .ppo_config import PPOConfig
 from .utils import left_pad, linear_lr
 
@@ -140,16 +140,24 @@ class PPOTrainer:
         self.device = torch.device("cuda", self.local_rank)
         torch.cuda.set_device(self.device)
         gemm_tuning.enable()
-        # models: policy (lm head), frozen ref copy, value model + reward model (score heads)
-        self.policy_model = load_model(model, self.device, trainable=True, seed=args.seed)
+        # models: policy (lm head), frozen ref copy, value model + reward model (score heads).
+        # Model objects keep their precision (the reference trains the modules it is given,
+        # ppo_trainer.py:144-152); names / configs take model_init_kwargs' dtype (bf16
+        # default; "float32" = the reference-precision mode, fp32 rollout included)
+        dt = None if hasattr(model, "parameters") else model_dtype(args.model_init_kwargs)
+        self.policy_model = load_model(model, self.device, trainable=True, seed=args.seed, dtype=dt)
+        pdt = self.policy_model.dtype
+        side = lambda m: None if hasattr(m, "parameters") else pdt  # noqa: E731
         if ref_model is not None:
-            self.ref_model = load_model(ref_model, self.device, trainable=False, seed=args.seed)
+            self.ref_model = load_model(ref_model, self.device, trainable=False, seed=args.seed, dtype=side(ref_model))
         else:  # create_reference_model (modeling_base.py:592-664): a frozen deep copy
             self.ref_model = build_model(self.policy_model.cfg, self.device, seed=None, trainable=False,
                                          dtype=self.policy_model.dtype)
             self.ref_model.copy_from(self.policy_model)
-        self.value_model = load_model(value_model, self.device, trainable=True, seed=args.seed + 1, head="score")
-        self.reward_model = load_model(reward_model, self.device, trainable=False, seed=args.seed + 2, head="score")
+        self.value_model = load_model(value_model, self.device, trainable=True, seed=args.seed + 1, head="score",
+                                      dtype=side(value_model))
+        self.reward_model = load_model(reward_model, self.device, trainable=False, seed=args.seed + 2, head="score",
+                                       dtype=side(reward_model))
         self.train_dataset, self.eval_dataset = train_dataset, eval_dataset
         self.train_dataset_len = len(train_dataset)
         fill_batch_sizes(args, self.train_dataset_len, self.world)
@@ -224,7 +232,7 @@ class PPOTrainer:
                                   top_p=1.0, top_k=None, eos_token_id=self.stop_token_id,
                                   pad_token_id=self.pad_token_id, seed=seed,
                                   offset=self._gen_count * (a.response_length + 1), return_logp=True,
-                                  check_every=a.decode_check_every)
+                                  check_every=a.decode_check_every, early_exit=a.decode_early_exit)
         self._gen_count += 1
         T = resp.shape[1]
         if self.stop_token_id is not None:

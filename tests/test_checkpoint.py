@@ -127,3 +127,33 @@ def test_gpt2_checkpoint_round_trip_and_param_order(tmp_path):
     for name, (o, shape) in m.layout.items():
         want = name.endswith("_b") or "ln_" in name
         assert (o in nd) == want, name
+
+
+@pytest.mark.parametrize("kind,warmup", [("linear", 0), ("linear", 3), ("constant", 0)])
+def test_scheduler_state_loads_into_transformers_lambdalr(kind, warmup):
+    """scheduler.pt is the LambdaLR state_dict transformers' Trainer saves: it
+    loads into get_scheduler(...)'s LambdaLR (lr_lambdas key included) and
+    equals the state of that scheduler stepped the same number of times."""
+    import warnings
+
+    from transformers import get_scheduler
+    total, steps, lr = 10, 4, 1e-3
+
+    def fresh():
+        opt = torch.optim.AdamW([{"params": [torch.nn.Parameter(torch.zeros(1))]} for _ in range(2)], lr=lr)
+        return opt, get_scheduler(kind, opt, num_warmup_steps=warmup, num_training_steps=total)
+    opt, stepped = fresh()
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for _ in range(steps):
+            opt.step()
+            stepped.step()
+    sd = ck.scheduler_state_dict(steps, total, lr, warmup, kind)
+    _, loaded = fresh()
+    loaded.load_state_dict(sd)
+    assert loaded.last_epoch == stepped.last_epoch == steps
+    assert loaded.get_last_lr() == pytest.approx(stepped.get_last_lr())
+    want = stepped.state_dict()
+    assert set(sd) == set(want)
+    for k in ("base_lrs", "last_epoch", "_step_count"):
+        assert sd[k] == want[k], k

@@ -85,6 +85,173 @@ def test_dp_groups_straddling_ranks():
     assert got[0][2] == got[1][2]
 
 
+def _oracle_worker(rank, world, port, q, out_dir, pdb, ga, loss_type):
+    """One fp32 GRPO step on this rank; saves its rollout, shuffle permutation, the
+    all-reduced gradient and its log line for the parent's oracle check."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), SWH_DIST_BACKEND="gloo")
+    try:
+        from swh_trl_amd.engine import CausalLM, tiny_qwen2
+        from swh_trl_amd.trainer import GRPOConfig, GRPOTrainer
+        cfg = tiny_qwen2(512, 2)
+        ds = [{"prompt": None, "prompt_ids": list(range(3 + 5 * i, 11 + 5 * i))} for i in range(32)]
+
+        def rew(prompts=None, completions=None, completion_ids=None, **kw):
+            return [float(len(set(c)) % 5) for c in completion_ids]
+
+        args = GRPOConfig(per_device_train_batch_size=pdb, gradient_accumulation_steps=ga, num_generations=4,
+                          max_prompt_length=8, max_completion_length=16, max_steps=1, learning_rate=1e-3,
+                          lr_scheduler_type="constant", loss_type=loss_type, shuffle_dataset=False,
+                          generation_kwargs={"eos_token_id": 1, "pad_token_id": 0, "min_new_tokens": 4},
+                          model_init_kwargs={"torch_dtype": "float32"}, logging_steps=1, seed=7)
+        tr = GRPOTrainer(model=CausalLM(cfg, torch.device("cuda:0"), seed=3, init_std=0.05, dtype=torch.float32),
+                         reward_funcs=rew, args=args, train_dataset=ds)
+        w0 = {k: v.detach().cpu().clone() for k, v in tr.model.hf_state_dict().items()}
+        cap = {}
+        gen_fn = tr._generate_and_score_completions
+
+        def gen_capture(examples):
+            out = gen_fn(examples)
+            cap["gen"] = {k: v.detach().cpu().clone() for k, v in out.items()}
+            n = out["completion_ids"].shape[0]
+            cap["perm"] = torch.randperm(n, generator=torch.Generator().set_state(tr._shuffle_gen.get_state()))
+            return out
+
+        tr._generate_and_score_completions = gen_capture
+        tr.training_step_group()
+        torch.cuda.synchronize()
+        saved = tr.model.flat.clone()
+        tr.model.flat.copy_(tr.model.grad)  # the averaged gradient, through the transformers names
+        grads = {k: v.detach().cpu().clone() for k, v in tr.model.hf_state_dict().items()}
+        tr.model.flat.copy_(saved)
+        log = tr._flush_logs()
+        torch.save({"w0": w0, "gen": cap["gen"], "perm": cap["perm"], "grads": grads,
+                    "log": {k: float(v) for k, v in log.items()}}, os.path.join(out_dir, f"rank{rank}.pt"))
+        q.put((rank, "ok"))
+    except Exception as e:  # surface the failure to the parent
+        import traceback
+        q.put((rank, traceback.format_exc() + repr(e)))
+    finally:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("pdb,ga,loss_type", [(8, 2, "bnpo"), (2, 1, "bnpo"), (4, 2, "grpo")],
+                         ids=["whole-groups-bnpo", "straddling-bnpo", "whole-groups-grpo"])
+def test_dp_averaged_gradient_equals_mean_of_oracle_rank_gradients(tmp_path, pdb, ga, loss_type):
+    """two fp32 ranks, one step.  The gradient each rank holds after the
+    overlapped all-reduce equals the mean over ranks of the oracle's gradient on that
+    rank's own split (oracle/grpo_step.py grpo_train): rewards gathered across ranks,
+    advantages on the global batch sliced per rank (grpo_trainer.py:1497, :1933-1938;
+    pdb 2 with G 4 puts every group across both ranks) and the loss normalised by the
+    rank-local token count under bnpo (grpo_config.py:500-503).  The loss metrics of
+    the log are the reference's cross-rank gathers: both ranks log the same values."""
+    from oracle import grpo_step as og
+    from swh_trl_amd.engine import tiny_qwen2
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 33500 + (os.getpid() % 1000) + 13 * pdb + ga
+    ps = [ctx.Process(target=_oracle_worker, args=(r, world, port, q, str(tmp_path), pdb, ga, loss_type))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    assert all(v == "ok" for v in got.values()), got
+    runs = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
+    assert runs[0]["log"] == runs[1]["log"]
+    for k in runs[0]["grads"]:
+        assert torch.equal(runs[0]["grads"][k], runs[1]["grads"][k]), k  # one averaged gradient
+    all_ids = torch.cat([r["gen"]["completion_ids"] for r in runs])
+
+    def rew(cids, cmask):
+        return [float(len(set(row[m.bool()].tolist())) % 5) for row, m in zip(cids, cmask)]
+
+    cfg = tiny_qwen2(512, 2)
+    per_rank = []
+    for r, run in enumerate(runs):
+        hf = og.hf_qwen2_from_config(cfg.to_dict(), dtype=torch.float32)
+        hf.load_state_dict(run["w0"], strict=False)
+        opt = torch.optim.SGD(hf.parameters(), lr=0.0)
+        g = {"prompt_ids": run["gen"]["prompt_ids"], "prompt_mask": run["gen"]["prompt_mask"].long(),
+             "completion_ids": run["gen"]["completion_ids"], "perm": run["perm"], "world_completion_ids": all_ids,
+             "rank": r}
+        rec = og.grpo_train(hf, opt, [g], rew, num_generations=4, C=16, per_device_train_batch_size=pdb,
+                            gradient_accumulation_steps=ga, n_steps=1, eos_token_id=1, loss_type=loss_type,
+                            capture=True)[0]
+        torch.testing.assert_close(run["gen"]["advantages"], rec["gens"][0]["a"], rtol=0, atol=1e-6)
+        per_rank.append(rec["grads"])
+    for k, mine in runs[0]["grads"].items():
+        if k not in per_rank[0]:
+            continue
+        want = (per_rank[0][k] + per_rank[1][k]) / 2
+        rel = ((mine.float() - want).norm() / want.norm().clamp_min(1e-20)).item()
+        assert rel <= 1e-3, (k, rel)
+
+
+def _resume_worker(rank, world, port, q, out_dir, resume_from):
+    """GRPO on two gloo ranks with steps_per_generation 4 > GA 2 (a rollout feeds two
+    optimizer steps): 3 steps saving every step, or resumed from `resume_from`."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), SWH_DIST_BACKEND="gloo")
+    try:
+        from swh_trl_amd.engine import CausalLM, tiny_qwen2
+        from swh_trl_amd.trainer import GRPOConfig, GRPOTrainer
+        ds = [{"prompt": None, "prompt_ids": list(range(3 + 5 * i, 11 + 5 * i))} for i in range(32)]
+
+        def rew(prompts=None, completions=None, completion_ids=None, **kw):
+            return [float(len(set(c)) % 5) for c in completion_ids]
+
+        args = GRPOConfig(output_dir=out_dir, per_device_train_batch_size=4, gradient_accumulation_steps=2,
+                          steps_per_generation=4, num_generations=4, max_prompt_length=8, max_completion_length=16,
+                          max_steps=3, learning_rate=1e-3, save_steps=1 if resume_from is None else 10 ** 9,
+                          logging_steps=1, seed=7, generation_kwargs={"eos_token_id": 1, "pad_token_id": 0})
+        tr = GRPOTrainer(model=CausalLM(tiny_qwen2(512, 2), torch.device("cuda:0"), seed=3, init_std=0.05),
+                         reward_funcs=rew, args=args, train_dataset=ds)
+        tr.train(resume_from_checkpoint=resume_from)
+        torch.cuda.synchronize()
+        flat = tr.model.flat.float().cpu().numpy()
+        q.put((rank, hashlib.sha256(flat.tobytes()).hexdigest()))
+    except Exception as e:  # surface the failure to the parent
+        import traceback
+        q.put((rank, "ERR " + traceback.format_exc() + repr(e)))
+    finally:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _spawn(target, world, extra):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 34500 + (os.getpid() % 500) + abs(hash(str(extra))) % 400
+    ps = [ctx.Process(target=target, args=(r, world, port, q, *extra)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    assert not any(str(v).startswith("ERR") for v in got.values()), got
+    return got
+
+
+def test_dp_resume_restores_each_rank_state(tmp_path):
+    """Exact resume on two ranks: each rank saves its own data-stream state
+    (swh_trainer_state_<rank>.pt: its buffered rollouts and shuffle generator, which
+    differ per rank) and reloads its own.  Checkpoint-1 falls mid-generation
+    (steps_per_generation 4, GA 2): the resumed run must train step 2 on each rank's
+    buffered rollouts and end bit-identical to the uninterrupted run on both ranks."""
+    full = _spawn(_resume_worker, 2, (str(tmp_path / "a"), None))
+    assert full[0] == full[1]
+    for r in range(2):
+        assert (tmp_path / "a" / "checkpoint-1" / f"swh_trainer_state_{r}.pt").exists()
+    res = _spawn(_resume_worker, 2, (str(tmp_path / "b"), str(tmp_path / "a" / "checkpoint-1")))
+    assert res[0] == res[1] == full[0]
+
+
 def test_bench_launches_n_ranks_itself():
     """`python bench.py --gpus 2` (no torchrun environment) starts two ranks
     itself; rank 0 prints one line with n_gpus 2 and the world size the process

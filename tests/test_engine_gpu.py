@@ -558,9 +558,15 @@ def test_checkpoint_resume_is_bit_identical_and_loads_in_transformers(dev, tmp_p
     # the latest checkpoint, read by transformers
     d = tmp_path / "a" / "checkpoint-3"
     for f in ("config.json", "model.safetensors", "optimizer.pt", "scheduler.pt", "trainer_state.json",
-              "swh_master.safetensors", "swh_trainer_state.pt"):
+              "swh_master.safetensors", "swh_trainer_state_0.pt"):
         assert (d / f).exists(), f
     assert (tmp_path / "a" / "README.md").exists()
+    # scheduler.pt loads into the LambdaLR transformers' Trainer builds (linear schedule, 2 param groups)
+    from transformers import get_scheduler
+    opt = torch.optim.AdamW([{"params": [torch.nn.Parameter(torch.zeros(1))]} for _ in range(2)], lr=1e-3)
+    sch = get_scheduler("linear", opt, num_warmup_steps=0, num_training_steps=3)
+    sch.load_state_dict(torch.load(d / "scheduler.pt", weights_only=True))
+    assert sch.last_epoch == 3 and sch.get_last_lr() == [0.0, 0.0]
     hf = AutoModelForCausalLM.from_pretrained(str(d), dtype=torch.float32).to(dev).eval()
     g = torch.Generator().manual_seed(9)
     ids = torch.randint(0, cfg.vocab_size, (2, 20), generator=g).to(dev)
@@ -757,3 +763,82 @@ def test_shared_prompt_kv_generates_identically(dev, monkeypatch):
         for x, y in zip(a, b):
             if x is not None:
                 assert torch.equal(x, y)
+
+
+def test_early_exit_stops_when_every_row_finished(dev):
+    """HF `_sample` stops the batch once every row has finished (the reference
+    reaches it through grpo_trainer.py:1793-1810).  With the final norm weight
+    zeroed every logit is 0, so greedy picks the lowest allowed id: 1 while
+    min_new_tokens masks EOS (id 0), then EOS at step M in every row.  The early
+    exit (pinned all-finished flag, two graph replays of lookahead) ends the
+    decode loop within three 8-step replays of step M, and the ids equal a run
+    that replays every step."""
+    from swh_trl_amd.engine import DecodeEngine
+    m = _tiny(dev, seed=6)
+    m.p["norm"].zero_()
+    B, P, C = 8, 6, 120
+    ids = torch.randint(2, m.cfg.vocab_size, (B, P), device=dev)
+    mask = torch.ones(B, P, dtype=torch.int32, device=dev)
+    eng = DecodeEngine(m, B, P, C)
+    for M in (5, 30):
+        kw = dict(greedy=True, eos_token_id=0, pad_token_id=5, min_new_tokens=M)
+        a, _ = eng.generate(ids, mask, C, early_exit=True, **kw)
+        steps_early = eng.steps_run
+        b, _ = eng.generate(ids, mask, C, early_exit=False, **kw)
+        assert eng.steps_run == C - 1
+        assert torch.equal(a, b)
+        assert (a[:, :M] == 1).all() and (a[:, M] == 0).all() and (a[:, M + 1:] == 5).all()
+        assert steps_early < C - 1 and steps_early <= M + 3 * eng.steps_per_graph, (M, steps_early)
+    # rows that cannot finish (min_new_tokens = C) run every step
+    eng.generate(ids, mask, C, early_exit=True, greedy=True, eos_token_id=0, pad_token_id=5, min_new_tokens=C)
+    assert eng.steps_run == C - 1
+
+
+@pytest.mark.parametrize("family", ["qwen2.5-0.5b-width", "llama"])
+def test_fp32_greedy_matches_transformers_fp32_generate(dev, family):
+    """Reference-precision rollout (RefDecodeEngine, fp32 weights and activations):
+    the reference generates in the model dtype (grpo_trainer.py:1793-1810), so an
+    fp32 policy's greedy ids must equal transformers fp32 `generate` (on the same
+    device: torch's own kernels) token for token — left-padded prompts included —
+    except where the two candidates' fp32 logits are an fp32 tie: the first
+    divergence of a row is allowed only if their gap is within 64 fp32 ulps of
+    the top logit (summation-order noise of a K <= 4864 reduction), and at most one
+    row may diverge."""
+    from swh_trl_amd.engine import CausalLM, RefDecodeEngine, build_engine
+    from swh_trl_amd.engine.config import DecoderConfig, tiny_llama
+    if family == "llama":
+        m = CausalLM(tiny_llama(2048, 2), dev, seed=3, init_std=0.05, dtype=torch.float32)
+        B, P, C = 4, 10, 32
+    else:
+        m = CausalLM(DecoderConfig(num_hidden_layers=2), dev, seed=3, init_std=0.02, dtype=torch.float32)
+        B, P, C = 8, 16, 48
+    g = torch.Generator().manual_seed(3)
+    ids = torch.randint(2, m.cfg.vocab_size, (B, P), generator=g).to(dev)
+    mask = torch.ones(B, P, dtype=torch.int64, device=dev)
+    mask[1, :3] = 0   # a left-padded prompt
+    ids[1, :3] = 0
+    eng = build_engine(m, B, P, C)
+    assert isinstance(eng, RefDecodeEngine)
+    mine, _ = eng.generate(ids, mask, C, greedy=True, pad_token_id=0)
+    from oracle import grpo_step as og
+    hf = og.hf_from_config(m.cfg.to_dict(), dtype=torch.float32).to(dev)
+    hf.load_state_dict({k: v.detach() for k, v in m.hf_state_dict().items()}, strict=False)
+    with torch.no_grad():
+        ref = hf.generate(input_ids=ids, attention_mask=mask, max_new_tokens=C, do_sample=False, pad_token_id=0,
+                          eos_token_id=None, bos_token_id=None)[:, P:]
+    rep = []
+    for b in range(B):
+        neq = (mine[b] != ref[b]).nonzero()
+        if neq.numel() == 0:
+            rep.append((b, None, 0.0))
+            continue
+        t = int(neq[0])
+        seq = torch.cat([ids[b], ref[b, :t]]).unsqueeze(0)
+        am = torch.cat([mask[b], torch.ones(t, dtype=mask.dtype, device=dev)]).unsqueeze(0)
+        with torch.no_grad():
+            z = hf(input_ids=seq, attention_mask=am).logits[0, -1].double()
+        ulp = 2.0 ** (torch.tensor(z.max().abs().item()).log2().floor().item() - 23)
+        rep.append((b, t, abs(z[int(mine[b, t])] - z[int(ref[b, t])]).item() / ulp))
+    print(family, "fp32 greedy first divergences (row, step, gap in fp32 ulps):", rep)
+    diverged = [r for r in rep if r[1] is not None]
+    assert len(diverged) <= 1 and all(r[2] <= 64 for r in diverged), rep

@@ -34,20 +34,27 @@ def _hf(m, seqcls: bool):
     return hf.float().eval()
 
 
-def _trainer(dev, **kw):
+def _trainer(dev, dtype=torch.bfloat16, width="tiny", **kw):
+    import dataclasses
+
     from swh_trl_amd.engine import CausalLM, tiny_qwen2
+    from swh_trl_amd.engine.config import DecoderConfig
     from swh_trl_amd.trainer import PPOConfig, PPOTrainer
-    cfg = tiny_qwen2(512, 2)
-    policy = CausalLM(cfg, dev, seed=11, init_std=0.05)
+    if width == "tiny":
+        cfg, rcfg, std, mul = tiny_qwen2(512, 2), tiny_qwen2(512, 1), 0.05, 6.0
+    else:  # the Qwen2.5-0.5B width (H 896, I 4864, V 151936, 14:2 heads), 2 layers; a 1-layer reward model
+        cfg = DecoderConfig(num_hidden_layers=2)
+        rcfg, std, mul = dataclasses.replace(cfg, num_hidden_layers=1), 0.02, 60.0
+    policy = CausalLM(cfg, dev, seed=11, init_std=std, dtype=dtype)
     with torch.no_grad():  # make the stop token likely, so rows end at different lengths
-        policy.p["embed"][EOS].mul_(6.0)
-    value = CausalLM(cfg, dev, head="score", seed=12, init_std=0.05)
-    reward = CausalLM(tiny_qwen2(512, 1), dev, head="score", seed=13, init_std=0.05)
+        policy.p["embed"][EOS].mul_(mul)
+    value = CausalLM(cfg, dev, head="score", seed=12, init_std=std, dtype=dtype)
+    reward = CausalLM(rcfg, dev, head="score", seed=13, init_std=std, dtype=dtype)
     g = torch.Generator().manual_seed(3)
     ds = []
     for i in range(16):
         n = 6 + i % 5  # ragged prompts -> left padding
-        ds.append({"input_ids": torch.randint(2, 512, (n,), generator=g).tolist()})
+        ds.append({"input_ids": torch.randint(2, min(512, cfg.vocab_size), (n,), generator=g).tolist()})
     a = dict(per_device_train_batch_size=4, gradient_accumulation_steps=2, num_mini_batches=2, num_ppo_epochs=2,
              response_length=12, stop_token_id=EOS, temperature=0.7, learning_rate=1e-3, total_episodes=16,
              pad_token_id=PAD, eos_token_id=EOS, seed=5)
@@ -222,3 +229,64 @@ def test_ppo_fused_micro_batches_equal_separate(dev):
     torch.testing.assert_close(st_f, st_s, rtol=2e-3, atol=2e-4)
     assert float((gp_f - gp_s).norm() / gp_s.norm()) < 2e-2
     assert float((gv_f - gv_s).norm() / gv_s.norm()) < 2e-2
+
+
+def _grads(m):
+    saved = m.flat.clone()
+    m.flat.copy_(m.grad)
+    g = {k: v.float().cpu().clone() for k, v in m.hf_state_dict().items()}
+    m.flat.copy_(saved)
+    return g
+
+
+@pytest.mark.parametrize("width", ["tiny", "qwen2.5-0.5b-width"])
+def test_ppo_fp32_reference_precision_matches_oracle(dev, width):
+    """PPO in the reference-precision mode (fp32 policy / value / reward models, the
+    fp32 rollout engine): the whole rollout scoring (ppo_trainer.py:389-535) and a
+    micro-batch's loss and gradients (:557-605) against oracle/ppo_step.py with
+    transformers fp32 models — generation / ref log-probs, values, scores and the
+    derived rewards / returns / advantages within 1e-4, the loss terms within 1e-4,
+    every policy and value gradient within 1e-3 relative."""
+    from oracle import ppo_step
+    tr, ds = _trainer(dev, dtype=torch.float32, width=width, gradient_accumulation_steps=1, num_mini_batches=1,
+                      per_device_train_batch_size=8)
+    a = tr.args
+    assert tr.policy_model.dtype == tr.value_model.dtype == tr.reward_model.dtype == torch.float32
+    queries = tr._queries(ds[:a.local_batch_size])
+    responses, logprobs = tr.generate(queries)
+    ro = tr.rollout_from(queries, responses, logprobs)
+    pol, ref = _hf(tr.policy_model, False), _hf(tr.ref_model, False)
+    val, rm = _hf(tr.value_model, True), _hf(tr.reward_model, True)
+    q, r = queries.cpu(), responses.cpu()
+    o = ppo_step.rollout_scores(pol, ref, val, rm, q, r, logprobs.cpu().float(), pad_token_id=PAD,
+                                stop_token_id=tr.stop_token_id, eos_token_id=EOS, temperature=a.temperature,
+                                kl_coef=a.kl_coef, kl_estimator=a.kl_estimator, whiten_rewards=a.whiten_rewards,
+                                missing_eos_penalty=a.missing_eos_penalty, gamma=a.gamma, lam=a.lam)
+    mine = _cpu(ro)
+    assert (mine["sequence_lengths"] < responses.shape[1] - 1).any()  # ragged ends
+    for k in ("padding_mask", "padding_mask_p1", "sequence_lengths", "postprocessed_responses"):
+        assert torch.equal(mine[k], o[k]), k
+    keep = ~o["padding_mask"]
+    gl = ppo_step.generation_logprobs(pol, q, r, PAD, a.temperature)
+    assert (logprobs.cpu()[keep] - gl[keep]).abs().max() < 1e-4
+    for k in ("ref_logprobs", "values", "scores", "kl", "non_score_reward", "rewards", "returns", "advantages"):
+        torch.testing.assert_close(mine[k].float(), o[k].float(), rtol=1e-4, atol=1e-4, msg=k)
+    # one micro-batch: loss terms and every gradient
+    inds = torch.tensor([5, 0, 3, 6, 1, 2, 7, 4])
+    tr.policy_model.zero_grad()
+    tr.value_model.zero_grad()
+    st = tr._micro_step(ro, inds.to(dev))[0].cpu()
+    oro = _cpu(ro)
+    loss, ost = ppo_step.micro_batch_loss(pol, val, oro, inds, context_length=queries.shape[1], pad_token_id=PAD,
+                                          temperature=a.temperature, cliprange=a.cliprange,
+                                          cliprange_value=a.cliprange_value, vf_coef=a.vf_coef)
+    loss.backward()
+    for i, k in ((0, "pg_loss"), (1, "vf_loss"), (4, "approxkl"), (5, "ratio"), (8, "entropy")):
+        assert abs(float(st[i]) - ost[k]) <= 1e-4 * max(1.0, abs(ost[k])), (k, float(st[i]), ost[k])
+    for m, hf in ((tr.policy_model, pol), (tr.value_model, val)):
+        g = _grads(m)
+        for name, p in hf.named_parameters():
+            if p.grad is None:
+                continue
+            rel = ((g[name] - p.grad).norm() / p.grad.norm().clamp_min(1e-20)).item()
+            assert rel <= 1e-3, (name, rel)

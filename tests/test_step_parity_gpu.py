@@ -1,26 +1,50 @@
-"""Step-level GRPO parity (-m gpu): one GRPOTrainer optimizer step against the
-CPU restatement of the reference step (oracle/grpo_step.py, which follows
-grpo_trainer.py:1500-2003 rollout scoring, :1411-1444 shuffle/split,
-:2058-2175 loss, and the Trainer's clip_grad_norm_ + torch AdamW).
+"""Step-level GRPO parity (-m gpu): GRPOTrainer optimizer steps against the CPU
+restatement of the reference loop (oracle/grpo_step.py `grpo_train`, which
+follows grpo_trainer.py:1411-1444 buffering / shuffle / split, :1812-1938
+scoring, :1854-1869 old log-probs, :1871-1899 frozen reference, :2058-2175 loss,
+and the Trainer's loss / GA, clip_grad_norm_ + torch AdamW).
 
 Both sides start from the same weights and see the same prompts, the same
-completion ids (the engine's own rollout is handed to the oracle) and the same
-shuffle permutation.  The product runs in its fp32 reference-precision mode
-(`model_init_kwargs={"torch_dtype": "float32"}`: fp32 parameters through the
-same flat-buffer model, HIP norm / RoPE / SiLU / log-prob / loss / AdamW
-kernels; the rollout reads a bf16 copy), the oracle is transformers Qwen2 in
-fp32 on the host.  Checked:
+completion ids (the engine's own rollouts are handed to the oracle) and the
+same shuffle permutations.
+
+fp32 (reference-precision mode, `model_init_kwargs={"torch_dtype": "float32"}`:
+fp32 parameters through the same flat-buffer model, HIP norm / RoPE / SiLU /
+log-prob / loss / AdamW kernels, SDPA attention) against transformers fp32:
   * completion mask and advantages equal (1e-6);
   * per-token log-probs of every micro-batch within 1e-4;
   * the loss (sum of the GA micro-batch losses / GA) within 1e-4;
   * the pre-clip gradient norm within 1e-4 relative, each weight gradient
     within 1e-3 relative;
-  * the post-step weights: the AdamW step moves each weight by at most lr
-    (first step: lr * g / (|g| + eps)), and both sides' moves agree to 1e-3 lr
-    on all but a 1e-3 fraction of weights (those with |g| near eps, where the
-    first AdamW step is ill-conditioned).
-Run at the tiny Qwen2 preset and at the real Qwen2.5-0.5B width (H 896,
-I 4864, V 151936, 14:2 heads) with 2 layers.
+  * the post-step weights: each weight moves by at most lr, and both sides'
+    moves agree to 1e-3 lr on all but a 1e-3 fraction of weights (those with
+    |g| near eps, where the first AdamW step is ill-conditioned).
+
+bf16 (the benched path: bf16 weights, csrc/attn.hip training attention, the
+shared-prompt forward, the chunked lm-head log-prob, fp32 master AdamW)
+against the reference's own bf16 computation (SURVEY.md §7 "exact" mode:
+transformers bf16, bf16 logits / T, the bf16 branch of selective_log_softmax,
+bf16 AdamW on the parameters).  A 1e-4 bound is not meaningful against bf16
+outputs (one bf16 ulp of a log-prob near -12 is 0.0625), so the bound is
+derived from bf16 rounding itself: the oracle also runs in fp32 on the same
+(bf16-valued) weights, and delta_ref = |oracle_bf16 - oracle_fp32| measures
+how far the reference's bf16 arithmetic sits from exact.  Two bf16
+implementations of one function can each sit that far from it, in opposite
+directions, so the product must satisfy
+  * mask and advantages exactly (integer / fp32 arithmetic on equal inputs);
+  * log-probs: max |product - oracle_bf16| <= 2 max(delta_ref) + 1 ulp(bf16)
+    of the largest |log-prob| (the reference rounds its output to bf16, the
+    product keeps fp32), and the mean <= 2 mean(delta_ref) + ulp/2;
+  * the product at least as close to oracle_fp32 as the reference is:
+    mean |product - oracle_fp32| <= 1.5 mean(delta_ref) + ulp/4;
+  * loss: |product - oracle_bf16| <= 2 |oracle_bf16 - oracle_fp32| + 1e-3 |loss|;
+  * gradients: relative error against oracle_fp32 within 2x the reference's
+    own (|g_bf16 - g_fp32| / |g_fp32|) + 2^-8, per weight tensor.
+Run at the Qwen2.5-0.5B width (H 896, I 4864, V 151936, 14:2 heads) with 2
+layers, and in the fork's own configuration (examples/scripts/grpo_train.py:
+494-503: num_iterations 2, importance_sampling_level "sequence", beta 0.1),
+whose second optimizer step reuses the buffered rollouts against their old
+log-probs, in both precisions.
 """
 import pytest
 import torch
@@ -47,6 +71,173 @@ def _grads_by_name(model):
     return out
 
 
+def _weights(model):
+    return {k: v.detach().float().cpu().clone() for k, v in model.hf_state_dict().items()}
+
+
+def product_run(cfg, dtype, n_steps, *, std, lr, G=4, P=12, C=24, MB=8, GA=2, seed=11, n_prompts=None,
+                **grpo_kw):
+    """n_steps GRPOTrainer optimizer steps; captures every generation (its
+    output and the shuffle permutation drawn after it), every training pass's
+    log-probs, and the loss / grad norm / gradients / weights of every step."""
+    from swh_trl_amd.engine import CausalLM
+    from swh_trl_amd.trainer import GRPOConfig, GRPOTrainer
+
+    dev = torch.device("cuda:0")
+    spg = grpo_kw.get("steps_per_generation") or GA
+    if n_prompts is None:
+        n_prompts = MB * spg // G * max(1, n_steps)
+    g = torch.Generator().manual_seed(seed)
+    ds = [{"prompt": None, "prompt_ids": torch.randint(2, cfg.vocab_size, (P,), generator=g).tolist()}
+          for _ in range(n_prompts)]
+    args = GRPOConfig(per_device_train_batch_size=MB, gradient_accumulation_steps=GA, num_generations=G,
+                      max_prompt_length=P, max_completion_length=C, learning_rate=lr, max_steps=n_steps,
+                      lr_scheduler_type="constant", seed=5, shuffle_dataset=False,
+                      model_init_kwargs={"torch_dtype": "float32" if dtype == torch.float32 else "bfloat16"},
+                      generation_kwargs={"eos_token_id": EOS, "pad_token_id": PAD, "min_new_tokens": 4}, **grpo_kw)
+    model = CausalLM(cfg, dev, seed=3, init_std=std, dtype=dtype)
+    tr = GRPOTrainer(model=model, reward_funcs=_reward_product, args=args, train_dataset=ds)
+    assert tr.model.dtype == dtype
+    w0 = _weights(tr.model)
+    cap = {"gens": [], "logps": [], "masks": []}
+    gen_fn = tr._generate_and_score_completions
+
+    def gen_capture(examples):
+        out = gen_fn(examples)
+        rec = {k: v.detach().cpu().clone() for k, v in out.items()}
+        n = rec["completion_ids"].shape[0]
+        rec["perm"] = torch.randperm(n, generator=torch.Generator().set_state(tr._shuffle_gen.get_state()))
+        cap["gens"].append(rec)
+        return out
+
+    lp_fn = tr._completion_logps
+
+    def lp_capture(model_, batch, compute_entropy):
+        lp, ent = lp_fn(model_, batch, compute_entropy)
+        if compute_entropy:  # the training pass (the scoring passes run without entropy)
+            cap["logps"].append(lp.detach().float().cpu().clone())
+            cap["masks"].append(batch["completion_mask"].detach().cpu().clone())
+        return lp, ent
+
+    tr._generate_and_score_completions = gen_capture
+    tr._completion_logps = lp_capture
+    steps = []
+    for _ in range(n_steps):
+        out = tr.training_step_group()
+        torch.cuda.synchronize()
+        steps.append({"loss": float(out["loss"]), "grad_norm": float(out["grad_norm"]),
+                      "grads": _grads_by_name(tr.model), "w": _weights(tr.model),
+                      "logps": cap["logps"][-1], "mask": cap["masks"][-1]})
+    hip_attn = tr.model._hip_attn
+    del tr
+    torch.cuda.empty_cache()
+    return {"w0": w0, "gens": cap["gens"], "steps": steps, "hip_attn": hip_attn,
+            "geometry": dict(G=G, C=C, MB=MB, GA=GA)}
+
+
+def oracle_run(cfg, w0, dtype, prod, n_steps, *, lr, beta=0.0, loss_type="bnpo", device="cpu", **grpo_kw):
+    """The reference loop (oracle/grpo_step.py grpo_train) in `dtype` — on the host, or
+    for the 8B width with torch's own device kernels (the same restatement; the host
+    would take minutes) — from the product's initial weights, over its rollouts."""
+    from oracle import grpo_step as og
+    geo = prod["geometry"]
+    hf = og.hf_from_config(cfg.to_dict(), seed=0, dtype=dtype).to(device)
+    missing, unexpected = hf.load_state_dict({k: v.to(dtype) for k, v in w0.items()}, strict=False)
+    assert not unexpected and not [k for k in missing if "rotary" not in k], (missing, unexpected)
+    ref = None
+    if beta:
+        ref = og.hf_from_config(cfg.to_dict(), seed=0, dtype=dtype).to(device)
+        ref.load_state_dict({k: v.to(dtype) for k, v in w0.items()}, strict=False)
+    opt = torch.optim.AdamW(hf.parameters(), lr=lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, foreach=False)
+    gens = [{"prompt_ids": g["prompt_ids"], "prompt_mask": g["prompt_mask"].long(),
+             "completion_ids": g["completion_ids"], "perm": g["perm"]} for g in prod["gens"]]
+    recs = og.grpo_train(hf, opt, gens, _reward_oracle, num_generations=geo["G"], C=geo["C"],
+                         per_device_train_batch_size=geo["MB"], gradient_accumulation_steps=geo["GA"],
+                         n_steps=n_steps, eos_token_id=EOS, beta=beta, loss_type=loss_type, ref_model=ref,
+                         capture=True, **grpo_kw)
+    for r in recs:
+        r["grads"] = {k: v.float() for k, v in r["grads"].items()}
+    recs[0]["w_after"] = {k: p.detach().float().cpu().clone() for k, p in hf.named_parameters()}
+    del hf, ref, opt
+    if device != "cpu":
+        torch.cuda.empty_cache()
+    return recs
+
+
+def _check_rollout_bookkeeping(prod, orc):
+    for g, sc in zip(prod["gens"], orc[0]["gens"]):
+        assert torch.equal(sc["cm"].int(), g["completion_mask"].int())
+        torch.testing.assert_close(g["advantages"].float(), sc["a"].float(), rtol=0, atol=1e-6)
+    for st in prod["steps"]:
+        assert st["mask"].shape == st["logps"].shape
+
+
+def _check_fp32(name, prod, orc, lr):
+    _check_rollout_bookkeeping(prod, orc)
+    for s, (st, o) in enumerate(zip(prod["steps"], orc)):
+        m = st["mask"].bool()
+        d_lp = (st["logps"] - o["logps"].float()).abs()[m]
+        assert d_lp.max().item() <= 1e-4, (name, s, d_lp.max().item())
+        assert abs(st["loss"] - o["loss"]) <= 1e-4 * max(1.0, abs(o["loss"])), (name, s, st["loss"], o["loss"])
+        assert abs(st["grad_norm"] - o["grad_norm"]) <= 1e-4 * o["grad_norm"], (name, s, st["grad_norm"],
+                                                                                 o["grad_norm"])
+        for k, gr in o["grads"].items():
+            rel = ((st["grads"][k] - gr).norm() / gr.norm().clamp_min(1e-20)).item()
+            assert rel <= 1e-3, (name, s, k, rel)
+    if len(prod["steps"]) != 1:  # later steps' gradients already pin the weights the earlier steps left
+        return
+    w0, w1, params = prod["w0"], prod["steps"][0]["w"], orc[0]["w_after"]
+    frac_bad, total = 0.0, 0
+    for k, w_after in w1.items():
+        if k not in params:
+            continue
+        mv_p = w_after - w0[k]
+        mv_o = params[k] - w0[k]
+        assert mv_p.abs().max().item() <= lr * 1.001 + 1e-7, k
+        diff = (mv_p - mv_o).abs()
+        frac_bad += (diff > 1e-3 * lr).sum().item()
+        total += diff.numel()
+    assert frac_bad / total <= 1e-3, (name, frac_bad / total)
+
+
+def _ulp_bf16(x: float) -> float:
+    import math
+    return 2.0 ** (math.floor(math.log2(max(abs(x), 1e-30))) - 7)
+
+
+def _check_bf16(name, prod, orc_bf, orc_32):
+    """The bf16-rounding bounds of the module docstring; returns the measured figures."""
+    _check_rollout_bookkeeping(prod, orc_bf)
+    stats = []
+    for s, (st, ob, o32) in enumerate(zip(prod["steps"], orc_bf, orc_32)):
+        m = st["mask"].bool()
+        lp_p, lp_b, lp_32 = st["logps"][m], ob["logps"].float()[m], o32["logps"].float()[m]
+        d_ref = (lp_b - lp_32).abs()
+        d_pb = (lp_p - lp_b).abs()
+        d_p32 = (lp_p - lp_32).abs()
+        ulp = _ulp_bf16(lp_b.abs().max().item())
+        rec = {"step": s, "lp_max_ref": d_ref.max().item(), "lp_mean_ref": d_ref.mean().item(),
+               "lp_max_prod_vs_bf16": d_pb.max().item(), "lp_mean_prod_vs_bf16": d_pb.mean().item(),
+               "lp_mean_prod_vs_fp32": d_p32.mean().item(), "ulp": ulp,
+               "loss": (st["loss"], ob["loss"], o32["loss"])}
+        assert d_pb.max().item() <= 2 * d_ref.max().item() + ulp, (name, rec)
+        assert d_pb.mean().item() <= 2 * d_ref.mean().item() + ulp / 2, (name, rec)
+        assert d_p32.mean().item() <= 1.5 * d_ref.mean().item() + ulp / 4, (name, rec)
+        loss_band = 2 * abs(ob["loss"] - o32["loss"]) + 1e-3 * abs(o32["loss"]) + 1e-6
+        assert abs(st["loss"] - ob["loss"]) <= loss_band, (name, rec)
+        worst = []
+        for k, g32 in o32["grads"].items():
+            n32 = g32.norm().clamp_min(1e-20)
+            rel_ref = ((ob["grads"][k] - g32).norm() / n32).item()
+            rel_p = ((st["grads"][k] - g32).norm() / n32).item()
+            worst.append((rel_p - 2 * rel_ref, k, rel_p, rel_ref))
+            assert rel_p <= 2 * rel_ref + 2.0 ** -8, (name, s, k, rel_p, rel_ref)
+        rec["grad_worst"] = max(worst)
+        stats.append(rec)
+    print(name, stats)
+    return stats
+
+
 def _cases():
     from swh_trl_amd.engine.config import DecoderConfig, tiny_qwen2
     real = DecoderConfig(num_hidden_layers=2)  # Qwen2.5-0.5B width, 2 layers
@@ -57,102 +248,107 @@ def _cases():
 
 @pytest.mark.parametrize("name,cfg,std,loss_type,beta", _cases(), ids=[c[0] for c in _cases()])
 def test_grpo_step_matches_oracle_step_fp32(name, cfg, std, loss_type, beta):
-    from oracle import grpo_step as og
-    from swh_trl_amd.engine import CausalLM
-    from swh_trl_amd.trainer import GRPOConfig, GRPOTrainer
-
-    dev = torch.device("cuda:0")
-    G, P, C, MB, GA = 4, 12, 24, 8, 2
-    n_prompts = MB * GA // G
-    g = torch.Generator().manual_seed(11)
-    ds = [{"prompt": None, "prompt_ids": torch.randint(2, cfg.vocab_size, (P,), generator=g).tolist()}
-          for _ in range(n_prompts)]
     lr = 1e-3
-    args = GRPOConfig(per_device_train_batch_size=MB, gradient_accumulation_steps=GA, num_generations=G,
-                      max_prompt_length=P, max_completion_length=C, learning_rate=lr, beta=beta, loss_type=loss_type,
-                      max_steps=1, lr_scheduler_type="constant", seed=5, shuffle_dataset=False,
-                      model_init_kwargs={"torch_dtype": "float32"},
-                      generation_kwargs={"eos_token_id": EOS, "pad_token_id": PAD, "min_new_tokens": 4})
-    model = CausalLM(cfg, dev, seed=3, init_std=std, dtype=torch.float32)
-    tr = GRPOTrainer(model=model, reward_funcs=_reward_product, args=args, train_dataset=ds)
-    assert tr.model.dtype == torch.float32 and not tr.model._hip_attn
-    w0 = {k: v.detach().float().cpu().clone() for k, v in tr.model.hf_state_dict().items()}
+    prod = product_run(cfg, torch.float32, 1, std=std, lr=lr, beta=beta, loss_type=loss_type)
+    assert not prod["hip_attn"]
+    orc = oracle_run(cfg, prod["w0"], torch.float32, prod, 1, lr=lr, beta=beta, loss_type=loss_type)
+    _check_fp32(name, prod, orc, lr)
 
-    captured = {}
-    gen_fn = tr._generate_and_score_completions
 
-    def gen_capture(examples):
-        out = gen_fn(examples)
-        captured["gen"] = {k: v.detach().clone() for k, v in out.items()}
-        captured["shuffle_state"] = tr._shuffle_gen.get_state()
-        return out
+def test_grpo_step_bf16_benched_path_matches_oracle():
+    """The benched configuration's numerics (bf16, HIP training attention,
+    shared-prompt forward, chunked lm-head log-prob) against the reference's
+    bf16 step, at the Qwen2.5-0.5B width with 2 layers."""
+    from swh_trl_amd.engine.config import DecoderConfig
+    cfg = DecoderConfig(num_hidden_layers=2)
+    lr = 1e-3
+    prod = product_run(cfg, torch.bfloat16, 1, std=0.02, lr=lr)
+    assert prod["hip_attn"]
+    orc_bf = oracle_run(cfg, prod["w0"], torch.bfloat16, prod, 1, lr=lr)
+    orc_32 = oracle_run(cfg, prod["w0"], torch.float32, prod, 1, lr=lr)
+    _check_bf16("bf16-0.5b-width", prod, orc_bf, orc_32)
 
-    lp_fn = tr._completion_logps
 
-    def lp_capture(model_, batch, compute_entropy):
-        lp, ent = lp_fn(model_, batch, compute_entropy)
-        if compute_entropy:  # the training pass (the scoring passes run without entropy)
-            captured["logps"] = lp.detach().float().cpu().clone()
-            captured["mask"] = batch["completion_mask"].detach().cpu().clone()
-        return lp, ent
+FORK = dict(num_iterations=2, importance_sampling_level="sequence", beta=0.1)
 
-    tr._generate_and_score_completions = gen_capture
-    tr._completion_logps = lp_capture
-    out = tr.training_step_group()
-    torch.cuda.synchronize()
-    loss = float(out["loss"])
-    norm = float(out["grad_norm"])
-    grads = _grads_by_name(tr.model)
-    w1 = {k: v.detach().float().cpu().clone() for k, v in tr.model.hf_state_dict().items()}
 
-    gen = {k: v.cpu() for k, v in captured["gen"].items()}
-    n = gen["completion_ids"].shape[0]
-    perm = torch.randperm(n, generator=torch.Generator().set_state(captured["shuffle_state"]))
+def test_fork_config_fp32_matches_oracle():
+    """examples/scripts/grpo_train.py:494-503 (num_iterations 2, GSPO sequence-level
+    importance weights, beta 0.1): GA is not a multiple of steps_per_generation x
+    num_iterations, so the rollout is scored once more for old_per_token_logps
+    (grpo_trainer.py:1854-1869) and the second optimizer step revisits the buffered
+    micro-batches (:1425-1438) with the updated policy; fp32, two steps."""
+    from swh_trl_amd.engine.config import tiny_qwen2
+    cfg = tiny_qwen2(1024, 2)
+    lr = 1e-3
+    prod = product_run(cfg, torch.float32, 2, std=0.05, lr=lr, **FORK)
+    orc = oracle_run(cfg, prod["w0"], torch.float32, prod, 2, lr=lr, **FORK)
+    assert len(prod["gens"]) == 1 and "old_per_token_logps" in prod["gens"][0]
+    torch.testing.assert_close(prod["gens"][0]["old_per_token_logps"].float()[prod["gens"][0]["completion_mask"].bool()],
+                               orc[0]["gens"][0]["old"].float()[orc[0]["gens"][0]["cm"].bool()], rtol=0, atol=1e-4)
+    _check_fp32("fork-fp32", prod, orc, lr)
 
-    # the oracle: transformers Qwen2 fp32 on the host, same weights / completions / permutation
-    hf = og.hf_qwen2_from_config(cfg.to_dict(), seed=0, dtype=torch.float32)
-    missing, unexpected = hf.load_state_dict(w0, strict=False)
-    assert not unexpected and not [k for k in missing if "rotary" not in k], (missing, unexpected)
-    ref = None
-    if beta:
-        ref = og.hf_qwen2_from_config(cfg.to_dict(), seed=0, dtype=torch.float32)
-        ref.load_state_dict(w0, strict=False)
-    opt = torch.optim.AdamW(hf.parameters(), lr=lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, foreach=False)
-    oloss, inter = og.grpo_step(hf, opt, gen["prompt_ids"], gen["prompt_mask"].long(), _reward_oracle,
-                                num_generations=G, C=C, per_device_train_batch_size=MB,
-                                gradient_accumulation_steps=GA, eos_token_id=EOS, pad_token_id=PAD, beta=beta,
-                                loss_type=loss_type, completion_ids=gen["completion_ids"], perm=perm,
-                                ref_model=ref, capture=True)
 
-    # rollout bookkeeping and advantages
-    assert torch.equal(inter["completion_mask"].int(), gen["completion_mask"].int())
-    torch.testing.assert_close(gen["advantages"].float(), inter["advantages"].float(), rtol=0, atol=1e-6)
-    # per-token log-probs (the fused pass holds the GA micro-batches in permuted order)
-    m = captured["mask"].bool()
-    assert torch.equal(m, gen["completion_mask"][perm].bool())
-    d_lp = (captured["logps"] - inter["logps"].float()).abs()[m]
-    assert d_lp.max().item() <= 1e-4, (name, d_lp.max().item())
-    # loss and gradient norm
-    assert abs(loss - oloss) <= 1e-4 * max(1.0, abs(oloss)), (name, loss, oloss)
-    assert abs(norm - inter["grad_norm"]) <= 1e-4 * inter["grad_norm"], (name, norm, inter["grad_norm"])
-    # every weight gradient
-    og_grads = inter["grads"]
-    for k, gr in og_grads.items():
-        gm = grads[k]
-        rel = ((gm - gr).norm() / gr.norm().clamp_min(1e-20)).item()
-        assert rel <= 1e-3, (name, k, rel)
-    # post-step weights
-    params = dict(hf.named_parameters())
-    frac_bad, worst = 0.0, 0.0
-    total = 0
-    for k, w_after in w1.items():
-        if k not in params:
-            continue
-        mv_p = w_after - w0[k]
-        mv_o = params[k].detach().float() - w0[k]
-        assert mv_p.abs().max().item() <= lr * 1.001 + 1e-7, k
-        diff = (mv_p - mv_o).abs()
-        frac_bad += (diff > 1e-3 * lr).sum().item()
-        total += diff.numel()
-        worst = max(worst, diff.max().item())
-    assert frac_bad / total <= 1e-3, (name, frac_bad / total, worst)
+def test_fork_config_bf16_matches_oracle():
+    """The fork's configuration on the benched bf16 path (0.5B width, 2 layers), two
+    optimizer steps over one buffered rollout, against the reference's bf16 loop."""
+    from swh_trl_amd.engine.config import DecoderConfig
+    cfg = DecoderConfig(num_hidden_layers=2)
+    lr = 1e-3  # moves of several bf16 ulps: the second step sees a changed policy on both sides
+    prod = product_run(cfg, torch.bfloat16, 2, std=0.02, lr=lr, **FORK)
+    orc_bf = oracle_run(cfg, prod["w0"], torch.bfloat16, prod, 2, lr=lr, **FORK)
+    orc_32 = oracle_run(cfg, prod["w0"], torch.float32, prod, 2, lr=lr, **FORK)
+    _check_bf16("fork-bf16-0.5b-width", prod, orc_bf, orc_32)
+
+
+def test_steps_per_generation_below_ga_fp32_matches_oracle():
+    """steps_per_generation 2 < GA 4: one optimizer step draws two generation batches
+    (_prepare_inputs regenerates every spg micro-steps, :1425-1433) and trains on the
+    micro-batches of both, the second rollout coming from the same (not yet updated)
+    policy; against the oracle's loop."""
+    from swh_trl_amd.engine.config import tiny_qwen2
+    cfg = tiny_qwen2(1024, 2)
+    lr = 1e-3
+    prod = product_run(cfg, torch.float32, 1, std=0.05, lr=lr, MB=4, GA=4, steps_per_generation=2, loss_type="grpo")
+    assert len(prod["gens"]) == 2
+    orc = oracle_run(cfg, prod["w0"], torch.float32, prod, 1, lr=lr, steps_per_generation=2, loss_type="grpo")
+    _check_fp32("spg<GA", prod, orc, lr)
+
+
+def test_cfg5_llama8b_width_step_matches_oracle():
+    """BASELINE.json config 5's architecture at full width (Llama-3-8B: H 4096, I 14336,
+    V 128256, 32:8 heads x 128, untied head) with 2 layers: one bf16 GRPO step with
+    beta 0.04 against a frozen reference copy (grpo_trainer.py:1871-1899), 64 rows x
+    (32 + 128) = 10240 tokens in the fused training pass — the shapes at which two
+    hipBLASLt persistent solutions on the compute and weight-gradient streams once
+    deadlocked (engine/model.py `_main_gemm_fence`).  The rollout runs on
+    the bandwidth-regime decode GEMMs (csrc/wide_gemm.hip).  Checked against the
+    reference loop with the bf16-rounding bounds of this module."""
+    from swh_trl_amd.engine.config import llama3_8b
+    import dataclasses
+    cfg = dataclasses.replace(llama3_8b(), num_hidden_layers=2)
+    lr = 1e-3
+    kw = dict(G=8, P=32, C=128, MB=16, GA=4, beta=0.04)
+    prod = product_run(cfg, torch.bfloat16, 1, std=0.02, lr=lr, **kw)
+    assert prod["hip_attn"]
+    rows = prod["steps"][0]["mask"].shape[0]
+    assert rows * (32 + 128) >= 10240
+    orc_bf = oracle_run(cfg, prod["w0"], torch.bfloat16, prod, 1, lr=lr, beta=0.04, device="cuda:0")
+    orc_32 = oracle_run(cfg, prod["w0"], torch.float32, prod, 1, lr=lr, beta=0.04, device="cuda:0")
+    _check_bf16("cfg5-llama8b-width", prod, orc_bf, orc_32)
+
+
+def test_early_stopped_rollout_width_matches_oracle_fp32():
+    """A rollout in which every row emits EOS (vocabulary 16, near-uniform logits,
+    96-token budget): the trainer keeps the longest row's width, as transformers
+    generate returns it (grpo_trainer.py:1793-1810), and trains on it; the step
+    still equals the oracle's, dr_grpo's constant normaliser (max_completion_length,
+    :2134-2135) included."""
+    from swh_trl_amd.engine.config import tiny_qwen2
+    cfg = tiny_qwen2(16, 2)
+    lr = 1e-3
+    prod = product_run(cfg, torch.float32, 1, std=0.02, lr=lr, C=96, loss_type="dr_grpo")
+    w = prod["gens"][0]["completion_ids"].shape[1]
+    assert w < 96 and bool(prod["gens"][0]["completion_mask"][:, -1].any()), w
+    orc = oracle_run(cfg, prod["w0"], torch.float32, prod, 1, lr=lr, loss_type="dr_grpo")
+    _check_fp32("early-stop-width", prod, orc, lr)
