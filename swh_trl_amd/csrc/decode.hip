@@ -1223,6 +1223,7 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
     const int64_t b = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int g = lane >> 4, c16 = lane & 15;
+    SWH_GEMM_TRACE(0);  // phase stamps for tools/attn_probe.py (instrumented build only)
     if ((int)blockIdx.y >= pf.rows) {  // a prefetch workgroup
         const int lin = blockIdx.y * gridDim.x + blockIdx.x, p = lin - pf.rows * gridDim.x;
         const int npf = (gridDim.y - pf.rows) * gridDim.x / 8 * 8;  // whole groups of 8: every XCD covered
@@ -1278,6 +1279,7 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
         }                                                                                      \
     }
     SWH_ATTN_ISSUE(0)  // the KV stream is in flight during RoPE
+    SWH_GEMM_TRACE(1);
 
     const uint16_t *row = qkv + b * (int64_t)(Hq + 2 * Hkv) * D;
     for (int idx = tid; idx < (GQ + 1) * HD; idx += kAttnThreads) {
@@ -1298,6 +1300,7 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
     for (int idx = GQ * D + tid; idx < 16 * D; idx += kAttnThreads) q_s[idx] = 0;
     for (int d = tid; d < D; d += kAttnThreads) vn_s[d] = row[(Hq + Hkv + kvh) * D + d];
     lds_barrier();
+    SWH_GEMM_TRACE(2);
     for (int d = tid; d < D; d += kAttnThreads) {  // KV append (nobody reads the slot from memory this step)
         kc[cbase + (int64_t)slot_new * D + d] = kn_s[d];
         vc[cbase + (int64_t)slot_new * D + d] = vn_s[d];
@@ -1391,6 +1394,7 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
             }
         }
     }
+    SWH_GEMM_TRACE(3);
     // row sums across the 4 lane groups, then the waves merge through LDS
     l += __shfl_xor(l, 16, kWave);
     l += __shfl_xor(l, 32, kWave);
@@ -1403,6 +1407,7 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
         red_s[wid][c16][D + 1] = l;
     }
     __syncthreads();
+    SWH_GEMM_TRACE(4);
     for (int idx = tid; idx < GQ * D; idx += kAttnThreads) {
         const int h = idx / D, d = idx - h * D;
         float mxw = kNegInf;
@@ -1419,6 +1424,7 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
         }
         ob[idx] = f32_to_bf16_bits(A / Ls);
     }
+    SWH_GEMM_TRACE(5);
 #undef SWH_ATTN_ISSUE
 }
 

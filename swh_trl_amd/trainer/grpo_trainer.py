@@ -575,9 +575,9 @@ class GRPOTrainer:
             return {}
         gather = swh_dist.all_gather_rows
         world = self.world
-        n_gen = len(m["_lengths"])
+        n_gen = len(m["_lengths"])  # 0 when no rollout fell in this log interval (spg * mu > GA)
         seg = gather(torch.cat(m["_met"])).cpu()                # [world * n_micro, 8]
-        lens = gather(torch.cat(m["_lengths"])).cpu()           # [world * n_gen * B, 2]
+        lens = gather(torch.cat(m["_lengths"])).cpu() if n_gen else None  # [world * n_gen * B, 2]
         losses = gather(torch.stack(m["_loss"]).view(-1, 1).float()).cpu()
         self._count_tokens()
         n_micro = seg.shape[0] // world
@@ -602,8 +602,8 @@ class GRPOTrainer:
                "learning_rate": float(m["_lr"][-1]),
                "num_tokens": self.state.num_input_tokens_seen}
         # completions (:1945-1960), one entry per generation, averaged
-        B = lens.shape[0] // (world * n_gen)
-        per_gen = lens.view(world, n_gen, B, 2).transpose(0, 1).reshape(n_gen, world * B, 2)
+        B = lens.shape[0] // (world * n_gen) if n_gen else 0
+        per_gen = lens.view(world, n_gen, B, 2).transpose(0, 1).reshape(n_gen, world * B, 2) if n_gen else []
         agg = {k: [] for k in ("mean_length", "min_length", "max_length", "clipped_ratio", "mean_terminated_length",
                                "min_terminated_length", "max_terminated_length")}
         for g in per_gen:
@@ -617,9 +617,10 @@ class GRPOTrainer:
             agg["min_terminated_length"].append(float(term.min()))
             agg["max_terminated_length"].append(float(term.max()))
         for k, v in agg.items():
-            log[f"completions/{k}"] = sum(v) / len(v)
+            if v:
+                log[f"completions/{k}"] = sum(v) / len(v)
         # rewards (global after the gather at :1497), one entry per generation
-        for i, name in enumerate(self.reward_func_names):
+        for i, name in enumerate(self.reward_func_names if n_gen else []):
             means = [float(torch.nanmean(r[:, i].cpu())) for r in m["_rpf"]]
             stds = []
             for r in m["_rpf"]:
@@ -628,9 +629,10 @@ class GRPOTrainer:
                 stds.append(float(col.std()) if col.numel() > 1 else float("nan"))
             log[f"rewards/{name}/mean"] = sum(means) / len(means)
             log[f"rewards/{name}/std"] = sum(stds) / len(stds)
-        log["reward"] = sum(float(x.mean()) for x in m["_rewards"]) / len(m["_rewards"])
-        log["reward_std"] = sum(float(x.mean()) for x in m["_reward_std"]) / len(m["_reward_std"])
-        log["frac_reward_zero_std"] = sum(float(x.mean()) for x in m["_zero_std"]) / len(m["_zero_std"])
+        if n_gen:
+            log["reward"] = sum(float(x.mean()) for x in m["_rewards"]) / n_gen
+            log["reward_std"] = sum(float(x.mean()) for x in m["_reward_std"]) / n_gen
+            log["frac_reward_zero_std"] = sum(float(x.mean()) for x in m["_zero_std"]) / n_gen
         # loss metrics (:2139-2174): per micro-batch masked means, gathered over ranks
         if self.beta != 0.0:
             log["kl"] = over_ranks(seg[..., 1] / tok)

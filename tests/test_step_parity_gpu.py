@@ -55,11 +55,13 @@ EOS, PAD = 1, 0
 
 
 def _reward_oracle(cids, cmask):
-    return [float(len(set(r[m.bool()].tolist())) % 5) for r, m in zip(cids, cmask)]
+    return [float(sum(r[m.bool()].tolist()) % 7) for r, m in zip(cids, cmask)]
 
 
 def _reward_product(prompts=None, completions=None, completion_ids=None, **kw):
-    return [float(len(set(c)) % 5) for c in completion_ids]
+    # varies within every group at any vocabulary size (a count of distinct ids is
+    # constant once V >> C: all-zero advantages would leave nothing to compare)
+    return [float(sum(c) % 7) for c in completion_ids]
 
 
 def _grads_by_name(model):

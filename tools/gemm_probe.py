@@ -13,7 +13,7 @@ import sys
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SO = os.environ.get("SWH_PROBE_SO", os.path.join(ROOT, "tools", "_build", "libgemm_probe.so"))
+SO = os.environ.get("SWH_PROBE_SO", os.path.join(ROOT, "tools", "_probe", "libgemm_probe.so"))
 PHASES = ["p1", "p2", "p3", "p4", "p5", "exit"]
 
 
