@@ -259,33 +259,38 @@ __global__ __launch_bounds__(64) void filt_row_kernel(FiltRow *__restrict__ st, 
 // Partial histogram of digit `lvl` over split blockIdx.x: scores >= lo whose
 // resolved key bits match, weighted 1 (top-k) or e^(z - lse) (top-p).  Runs of
 // equal bins within a thread's elements are summed in registers first (scores
-// mostly share a few exponent bins), one LDS atomic per run.
+// mostly share a few exponent bins), one LDS atomic per run.  The weights are
+// summed as 2^-40 fixed point in 64-bit integers: integer adds commute, so the
+// bins (and the threshold) are the same in every run — float LDS atomics made
+// the top-p draw run-to-run nondeterministic (their order varies).  Sums stay
+// below V 2^40 < 2^64; a weight under 2^-40 (probability < e^-27.7) adds 0.
+constexpr float kHistScale = 1099511627776.0f;  // 2^40
 template <int DT, bool EXPW>
 __global__ __launch_bounds__(kSplitThreads) void filt_hist_kernel(
     const typename Elem<DT>::T *__restrict__ logits, int64_t V, int64_t ld, swh_sample_params p,
     const int32_t *__restrict__ step_p, const uint32_t *__restrict__ seen, int64_t words, int64_t chunk,
     const FiltRow *__restrict__ st, int lvl, float *__restrict__ phist) {
-    __shared__ float hist[kBins];
+    __shared__ unsigned long long hist[kBins];
     const int64_t b = blockIdx.y;
     const int t = threadIdx.x;
     const FiltRow r = st[b];
     if (!r.active) return;
     const int sh = lvl == 0 ? 21 : (lvl == 1 ? 10 : 0);
     const uint32_t dmask = lvl == 2 ? 0x3ffu : 0x7ffu;
-    for (int i = t; i < kBins; i += kSplitThreads) hist[i] = 0.f;
+    for (int i = t; i < kBins; i += kSplitThreads) hist[i] = 0ull;
     __syncthreads();
     const Proc pr = make_proc(p, *step_p, seen ? seen + b * words : nullptr);
     int64_t beg, end;
     split_range(V, chunk, beg, end);
     int run_bin = -1;
-    float run_w = 0.f;
+    unsigned long long run_w = 0ull;
     row_foreach<DT, false>(logits + b * ld, beg, end, t, kSplitThreads, [&](int64_t j, float x) {
         const float z = pr(j, x);
         if (!(z >= r.lo) || z == kNegInf) return;
         const uint32_t k = ord_key(z);
         if ((k & r.pmask) != r.prefix) return;
         const int bin = (int)((k >> sh) & dmask);
-        const float w = EXPW ? fast_exp(z - r.lse) : 1.0f;
+        const unsigned long long w = (unsigned long long)((EXPW ? fast_exp(z - r.lse) : 1.0f) * kHistScale);
         if (bin == run_bin) {
             run_w += w;
         } else {
@@ -297,7 +302,7 @@ __global__ __launch_bounds__(kSplitThreads) void filt_hist_kernel(
     if (run_bin >= 0) atomicAdd(&hist[run_bin], run_w);
     __syncthreads();
     float *dst = phist + (b * gridDim.x + blockIdx.x) * (int64_t)kBins;
-    for (int i = t; i < kBins; i += kSplitThreads) dst[i] = hist[i];
+    for (int i = t; i < kBins; i += kSplitThreads) dst[i] = (float)((double)hist[i] * (1.0 / 1099511627776.0));
 }
 
 // One radix level per row: the bin of digit `lvl` where the weight from the top

@@ -613,6 +613,8 @@ class DecodeEngine:
         self.plen.copy_(prompt_mask.sum(-1).to(torch.int32))
         self.finished.zero_()
         self.out.fill_(pad_token_id if pad_token_id is not None else 0)
+        if return_logp:  # columns an early exit never reaches read 0, not a previous generation's values
+            self.out_logp.zero_()
         self.rng[0], self.rng[1] = int(seed) & ((1 << 63) - 1), int(offset)
         if repetition_penalty != 1.0:
             # every prompt position, left pads included: transformers'

@@ -187,10 +187,15 @@ def _dw_split(tokens: int, outputs: int) -> int:
     """K split of a weight-gradient GEMM dW[N, M] = dY^T X over `tokens`: the
     small-output projections (o, qkv: <= 1.2M outputs = < 20 output tiles of
     256 x 256) leave most CUs idle at any token count (0.33-0.4 PFLOP/s at
-    24576 tokens); splitting the tokens gives S x the tiles.  SWH_DW_SPLIT=0
-    keeps the single GEMM."""
+    24576 tokens); splitting the tokens gives S x the tiles.  Measured at the
+    bench step's 17408 tokens with the fold included (tools/gemm_eff.py): qkv
+    (1.03M outputs) S 8 66 us against 147 at S 1; o (0.80M) S 2 75 us against
+    134 at S 8, where the fold of eight partials dominates; down (4.4M) S 2-8
+    200 us against 251.  SWH_DW_SPLIT=0 keeps the single GEMM."""
     if os.environ.get("SWH_DW_SPLIT", "1") == "0" or tokens < 8192:
         return 1
+    if outputs <= 900_000:
+        return 2
     if outputs <= 1_500_000:
         return 8
     if outputs <= 5_000_000:

@@ -160,6 +160,8 @@ class RefDecodeEngine:
         self.plen.copy_(mask.sum(-1))
         self.finished.zero_()
         self.out.fill_(pad_token_id if pad_token_id is not None else 0)
+        if return_logp:  # columns an early exit never reaches read 0, not a previous generation's values
+            self.out_logp.zero_()
         self.rng[0], self.rng[1] = int(seed) & ((1 << 63) - 1), int(offset)
         if repetition_penalty != 1.0:
             ops.seen_init(prompt_ids.to(torch.int64), None, self.cfg.vocab_size, self.seen)

@@ -842,3 +842,28 @@ def test_fp32_greedy_matches_transformers_fp32_generate(dev, family):
     print(family, "fp32 greedy first divergences (row, step, gap in fp32 ulps):", rep)
     diverged = [r for r in rep if r[1] is not None]
     assert len(diverged) <= 1 and all(r[2] <= 64 for r in diverged), rep
+
+
+def test_generation_is_run_to_run_deterministic(dev):
+    """The same seed gives the same completions and log-probs, bit for bit, in every
+    run and for every sampling mode (greedy, plain, top-p with log-probs) — the
+    reproducibility the checkpoint-resume and DP-replica tests rely on."""
+    import hashlib
+
+    from swh_trl_amd.engine import CausalLM, DecodeEngine
+    from swh_trl_amd.engine.config import DecoderConfig
+    m = CausalLM(DecoderConfig(num_hidden_layers=2), dev, seed=7, init_std=0.02)
+    B, P, C, G = 64, 32, 48, 8
+    g = torch.Generator().manual_seed(12)
+    ids = torch.randint(0, m.cfg.vocab_size, (B // G, P), generator=g).repeat_interleave(G, 0).to(dev)
+    mask = torch.ones(B, P, dtype=torch.int32, device=dev)
+    eng = DecodeEngine(m, B, P, C)
+    for kw in (dict(greedy=True), dict(seed=3), dict(seed=4, top_p=0.9, return_logp=True)):
+        hs = set()
+        for _ in range(4):
+            out, lp = eng.generate(ids, mask, C, eos_token_id=2, pad_token_id=0, group_size=G, **kw)
+            h = hashlib.sha256(out.cpu().numpy().tobytes())
+            if lp is not None:
+                h.update(lp.cpu().numpy().tobytes())
+            hs.add(h.hexdigest())
+        assert len(hs) == 1, (kw, hs)

@@ -571,6 +571,24 @@ def test_sampler_bf16_ties(ops, dev, kw):
             assert (logits[b][extra].float() == logits[b][kr[b]].float().min()).all()
 
 
+@pytest.mark.parametrize("kw", [dict(top_p=0.9), dict(top_p=0.8, top_k=500, min_p=0.01), dict(top_k=100)])
+def test_filtered_sampler_is_run_to_run_deterministic(ops, dev, kw):
+    """The filtered path's radix-select histograms sum top-p weights in 2^-40
+    fixed point (integer LDS atomics): the draw and its log-prob are the same
+    bits in every run.  (Float LDS atomics summed the weights in arrival order:
+    a top-p generation differed between runs of the same seed.)  bf16 logits
+    with many ties at the threshold, 64 rows x 151936, 12 launches."""
+    g = _gen(31)
+    logits = (torch.randn(64, 151936, generator=g) * 3).to(torch.bfloat16).to(dev)
+    params = ops.make_sample_params(**kw)
+    ref = None
+    for _ in range(12):
+        tok, _, lp, _, _ = _run_sampler(ops, dev, logits, params, seed=5, offset=2)
+        if ref is None:
+            ref = (tok, lp)
+        assert torch.equal(tok, ref[0]) and torch.equal(lp, ref[1])
+
+
 def test_sampler_distribution_chi2(ops, dev):
     """Empirical frequencies over 4096 independent draws match softmax(z)."""
     V, N = 16, 4096

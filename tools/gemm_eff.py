@@ -62,6 +62,30 @@ def main():
             print(f"{name:8s} {pn:9s} M={M:6d} N={N:6d} K={K:5d}  {ms * 1000:8.1f} us  {tf:6.0f} TF/s  "
                   f"x{per_step:2d} = {ms * per_step:6.2f} ms/step", flush=True)
     print(f"GEMM total {total:.1f} ms per training step", flush=True)
+    # token-split sweep of the weight gradients (bmm of S partials + the fixed-order fold)
+    from swh_trl_amd._lib import call
+    from swh_trl_amd.ops import _dtype_code, _stream
+    for name, (N, K) in {"qkv": (Q, H), "o": (H, H), "gate_up": (2 * I, H), "down": (H, I), "lm": (V, H)}.items():
+        M = CH if name == "lm" else T
+        x = torch.randn(M, K, **bf)
+        dy = torch.randn(M, N, **bf)
+        gw = torch.zeros(N, K, **bf)
+        res = []
+        for S in (1, 2, 4, 8):
+            if M % S:
+                continue
+            Kc = M // S
+            if S == 1:
+                def fn():
+                    gw.addmm_(dy.t(), x)
+            else:
+                def fn():
+                    parts = torch.bmm(dy.view(S, Kc, -1).transpose(1, 2), x.view(S, Kc, -1))
+                    call("swh_dw_reduce", parts.data_ptr(), S, gw.numel(), gw.data_ptr(), _dtype_code(gw, "dw"),
+                         _stream())
+            ms = _t(fn)
+            res.append(f"S{S} {ms * 1000:7.1f}us {2 * M * N * K / ms / 1e9:5.0f}TF")
+        print(f"wgrad split {name:8s} " + "  ".join(res), flush=True)
 
 
 if __name__ == "__main__":
