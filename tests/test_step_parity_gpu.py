@@ -37,7 +37,10 @@ directions, so the product must satisfy
     product keeps fp32), and the mean <= 2 mean(delta_ref) + ulp/2;
   * the product at least as close to oracle_fp32 as the reference is:
     mean |product - oracle_fp32| <= 1.5 mean(delta_ref) + ulp/4;
-  * loss: |product - oracle_bf16| <= 2 |oracle_bf16 - oracle_fp32| + 1e-3 |loss|;
+  * loss: |product - oracle_bf16| <= 2 |oracle_bf16 - oracle_fp32| + 1e-3 |loss|
+    + beta mean(delta_ref^2) / 2 (the product's frozen-reference and policy passes
+    see the rows in other GEMM positions, so their step-1 log-probs differ by bf16
+    noise and k3 KL ~ d^2 / 2 where the reference's is exactly 0);
   * gradients: relative error against oracle_fp32 within 2x the reference's
     own (|g_bf16 - g_fp32| / |g_fp32|) + 2^-8, per weight tensor.
 Run at the Qwen2.5-0.5B width (H 896, I 4864, V 151936, 14:2 heads) with 2
@@ -207,7 +210,7 @@ def _ulp_bf16(x: float) -> float:
     return 2.0 ** (math.floor(math.log2(max(abs(x), 1e-30))) - 7)
 
 
-def _check_bf16(name, prod, orc_bf, orc_32):
+def _check_bf16(name, prod, orc_bf, orc_32, beta=0.0):
     """The bf16-rounding bounds of the module docstring; returns the measured figures."""
     _check_rollout_bookkeeping(prod, orc_bf)
     stats = []
@@ -225,7 +228,12 @@ def _check_bf16(name, prod, orc_bf, orc_32):
         assert d_pb.max().item() <= 2 * d_ref.max().item() + ulp, (name, rec)
         assert d_pb.mean().item() <= 2 * d_ref.mean().item() + ulp / 2, (name, rec)
         assert d_p32.mean().item() <= 1.5 * d_ref.mean().item() + ulp / 4, (name, rec)
-        loss_band = 2 * abs(ob["loss"] - o32["loss"]) + 1e-3 * abs(o32["loss"]) + 1e-6
+        # the product scores the frozen reference and trains the policy in separate passes whose
+        # bf16 GEMMs see the rows in other positions (the shuffle), so at step 1 their log-probs
+        # differ by bf16 noise where the reference's are equal: k3 KL ~ d^2 / 2 per token
+        kl_noise = beta * float((d_ref ** 2).mean()) / 2
+        loss_band = 2 * abs(ob["loss"] - o32["loss"]) + 1e-3 * abs(o32["loss"]) + kl_noise + 1e-6
+        rec["kl_noise_band"] = kl_noise
         assert abs(st["loss"] - ob["loss"]) <= loss_band, (name, rec)
         worst = []
         for k, g32 in o32["grads"].items():
@@ -300,7 +308,7 @@ def test_fork_config_bf16_matches_oracle():
     prod = product_run(cfg, torch.bfloat16, 2, std=0.02, lr=lr, **FORK)
     orc_bf = oracle_run(cfg, prod["w0"], torch.bfloat16, prod, 2, lr=lr, **FORK)
     orc_32 = oracle_run(cfg, prod["w0"], torch.float32, prod, 2, lr=lr, **FORK)
-    _check_bf16("fork-bf16-0.5b-width", prod, orc_bf, orc_32)
+    _check_bf16("fork-bf16-0.5b-width", prod, orc_bf, orc_32, beta=FORK["beta"])
 
 
 def test_steps_per_generation_below_ga_fp32_matches_oracle():
@@ -337,7 +345,7 @@ def test_cfg5_llama8b_width_step_matches_oracle():
     assert rows * (32 + 128) >= 10240
     orc_bf = oracle_run(cfg, prod["w0"], torch.bfloat16, prod, 1, lr=lr, beta=0.04, device="cuda:0")
     orc_32 = oracle_run(cfg, prod["w0"], torch.float32, prod, 1, lr=lr, beta=0.04, device="cuda:0")
-    _check_bf16("cfg5-llama8b-width", prod, orc_bf, orc_32)
+    _check_bf16("cfg5-llama8b-width", prod, orc_bf, orc_32, beta=0.04)
 
 
 def test_early_stopped_rollout_width_matches_oracle_fp32():
