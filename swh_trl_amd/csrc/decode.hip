@@ -148,6 +148,9 @@ __device__ __forceinline__ uint4 ld_w(const uint16_t *p) {
 #define SWH_GEMM_RING 0  // decode_gemm k-loop: refill each k-step's weight registers right after its MFMAs (A/B)
 #endif
 static_assert(!(SWH_GEMM_RING && SWH_ROUND_PREFETCH), "the ring refill lives in the per-k-step loop");
+#ifndef SWH_SILU_ST16
+#define SWH_SILU_ST16 1  // gate/up SiLU epilogue: 16-B row stores through a per-wave LDS tile (A/B)
+#endif
 #ifndef SWH_LM_RING
 #define SWH_LM_RING 1  // lm-head tile loop: refill each weight register right after its MFMA (A/B)
 #endif
@@ -1003,8 +1006,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
                     }
                 }
             }
-        } else if constexpr (EPI == EPI_SILU) {
-            // lanes rl < 8 hold gate column t*8+rl, lanes rl+8 the matching up column
+        } else if constexpr (EPI == EPI_SILU && !SWH_SILU_ST16) {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1013,24 +1015,59 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
                     const float u = __shfl_xor(v, 8, kWave);
                     const int row = m0 + i * 16 + 4 * g + e;
                     if (rl < 8 && row < M) {
-                        const int col = t * 8 + rl;  // yf: ((row/16 * N/32 + col/32) 64 + lane) 8 + col % 8
+                        const int col = t * 8 + rl;
                         const int64_t at = smp.yf ? ((((int64_t)(row >> 4) * (N >> 5) + (col >> 5)) * 64 +
                                                       ((col >> 3) & 3) * 16 + (row & 15)) * 8 + (col & 7))
                                                   : (int64_t)row * ldy + col;
                         y[at] = f32_to_bf16_bits(round_bf16(v / (1.f + expf(-v))) * u);
                     }
                 }
-        } else {
-            // C layout: lane holds rows 16 i + 4 g + e of column rl
-            const float bz = BIAS ? bf16_bits_to_f32(bias[t * 16 + rl]) : 0.f;
+        } else if constexpr (EPI == EPI_SILU) {
+            // lanes rl < 8 hold gate column t*8+rl, lanes rl+8 the matching up column.
+            // Both lanes of a pair can form y = bf16(silu(gate)) * up of their column:
+            // the gate lanes take rows 0-31 of the tile, the up lanes rows 32-63, into
+            // the wave's 1 KB LDS tile [64 rows][8 columns]; then lane r stores row r's
+            // 8 columns (16 contiguous bytes in the fragment order and row-major alike)
+            // as one 16-B store instead of 16 scattered 2-B stores.
+            uint16_t *yt = reinterpret_cast<uint16_t *>(lds + L.total) + wid * 512;
+            const bool gl = rl < 8;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const int row = m0 + i * 16 + 4 * g + e;
-                    if (row < M)
-                        y[(int64_t)row * ldy + t * 16 + rl] = f32_to_bf16_bits(acc[i][e] * rsr[i][e] + bz);
+                    const float v = round_bf16(acc[i][e] * rsr[i][e]);
+                    const float u = __shfl_xor(v, 8, kWave);
+                    if (gl == (i < 2)) {
+                        const float gt = gl ? v : u, up = gl ? u : v;
+                        yt[(i * 16 + 4 * g + e) * 8 + (rl & 7)] = f32_to_bf16_bits(round_bf16(gt / (1.f + expf(-gt))) * up);
+                    }
                 }
+            const uint4 yr = *reinterpret_cast<const uint4 *>(yt + lane * 8);
+            const int row = m0 + lane, col = t * 8;  // yf: ((row/16 * N/32 + col/32) 64 + row%16 + 16 (col/8 % 4)) 8
+            if (row < M) {
+                const int64_t at = smp.yf ? (((int64_t)(row >> 4) * (N >> 5) + (col >> 5)) * 64 +
+                                             ((col >> 3) & 3) * 16 + (row & 15)) * 8
+                                          : (int64_t)row * ldy + col;
+                *reinterpret_cast<uint4 *>(y + at) = yr;
+            }
+        } else {
+            // C layout: lane holds rows 16 i + 4 g + e of column rl.  Through the wave's
+            // 2 KB LDS tile [64 rows][16 columns], lane r stores row r's 16 columns as
+            // two 16-B pieces (not 16 scattered 2-B stores).
+            const float bz = BIAS ? bf16_bits_to_f32(bias[t * 16 + rl]) : 0.f;
+            uint16_t *yt = reinterpret_cast<uint16_t *>(lds + L.total) + wid * 1024;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    yt[(i * 16 + 4 * g + e) * 16 + rl] = f32_to_bf16_bits(acc[i][e] * rsr[i][e] + bz);
+            const uint4 y0 = *reinterpret_cast<const uint4 *>(yt + lane * 16);
+            const uint4 y1 = *reinterpret_cast<const uint4 *>(yt + lane * 16 + 8);
+            if (m0 + lane < M) {
+                uint4 *dst = reinterpret_cast<uint4 *>(y + (int64_t)(m0 + lane) * ldy + t * 16);
+                dst[0] = y0;
+                dst[1] = y1;
+            }
         }
     }
     SWH_GEMM_TRACE(5);
@@ -1812,7 +1849,9 @@ static int decode_gemm_impl(const void *x, const void *w, int64_t M, int64_t N, 
         const bool force = e && e[0] == 't';  // tuning: "t" forces the tile kernel
         // gate/up (SiLU tiles) from one tile per CU up: 11.2 vs 12.4 us at N 9728 (tools/bench_decode.py --ku)
         const int64_t min_tiles = (silu ? 1 : 8) * (int64_t)cu_count();
-        if (!residual && K <= 32 * kLmMaxKS && (force || (!e && ntile >= min_tiles))) {
+        // (the epilogues store 8 columns of a row as one 16-B piece: row-major needs ldy % 8 == 0)
+        if (!residual && K <= 32 * kLmMaxKS && (force || (!e && ntile >= min_tiles)) &&
+            ((silu && (act & 1)) || ldy % 8 == 0)) {
             const int64_t nmt = (M + 63) / 64;
             const GemmLds L = gemm_lds(1, 64, 8, (int)K, (int)K, nm, false);
             int64_t per = cu_count() / nmt > 0 ? cu_count() / nmt : 1;
@@ -1823,7 +1862,7 @@ static int decode_gemm_impl(const void *x, const void *w, int64_t M, int64_t N, 
             const auto *NWt = static_cast<const uint16_t *>(norm_w);
             const auto *Bs = static_cast<const uint16_t *>(bias);
             auto *Y = static_cast<uint16_t *>(y);
-            const size_t lds = (size_t)L.total;
+            const size_t lds = (size_t)L.total + (silu ? 8 : 16) * 1024;  // + the epilogue's 1 / 2 KB per wave
             if (silu) return launch_tiles<EPI_SILU, false>(nm, grid, lds, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Bs, Y, (int)ldy, fw, act & 1);
             if (Bs) return launch_tiles<EPI_PLAIN, true>(nm, grid, lds, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Bs, Y, (int)ldy, fw);
             return launch_tiles<EPI_PLAIN, false>(nm, grid, lds, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Bs, Y, (int)ldy, fw);
