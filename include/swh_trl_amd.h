@@ -410,6 +410,16 @@ int swh_attn_decode_shared(const void *qkv, void *k_cache, void *v_cache, const 
                            const float *rope_sin, const int32_t *prompt_len, const int32_t *prompt_row,
                            const int32_t *state, int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax,
                            float scale, void *out, const void *pf_w, int64_t pf_n, int64_t pf_k, void *stream);
+/* swh_attn_decode_shared; out_frag = 1 writes `out` in the fragment order that
+ * swh_decode_gemm_fragw reads with act_frag bit 1 (element (b, c) of [B, Hq*D] at
+ * (((b/16) (Hq*D/32) + c/32) 64 + 16 ((c/8) % 4) + b % 16) 8 + c % 8), so o_proj
+ * takes its A operand as contiguous 1 KB runs.  Same values as out_frag = 0.
+ * out_frag = 1 needs B % 16 == 0, (Hq*D) % 32 == 0 and `out` 16-B aligned. */
+int swh_attn_decode_shared_frag(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
+                                const float *rope_sin, const int32_t *prompt_len, const int32_t *prompt_row,
+                                const int32_t *state, int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax,
+                                float scale, void *out, const void *pf_w, int64_t pf_n, int64_t pf_k,
+                                int32_t out_frag, void *stream);
 
 /* Weight-streaming decode GEMM Y[M,N] = X[M,K] W[N,K]^T (bf16, fp32 MFMA
  * accumulation, K % 64 == 0, 16-B aligned operands, ldy % 8 == 0) with the

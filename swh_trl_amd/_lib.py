@@ -101,6 +101,8 @@ SIGNATURES = {
                                          c_i32, c_f32, c_vp, c_vp, c_i64, c_i64, c_vp]),
     "swh_attn_decode_shared": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32,
                                        c_i32, c_f32, c_vp, c_vp, c_i64, c_i64, c_vp]),
+    "swh_attn_decode_shared_frag": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32,
+                                            c_i32, c_i32, c_f32, c_vp, c_vp, c_i64, c_i64, c_i32, c_vp]),
     "swh_decode_gemm_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "swh_lm_head_sample_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "swh_lm_head_sample": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_f32, c_vp, C.POINTER(SampleParams),

@@ -1235,7 +1235,15 @@ struct AttnPrefetch {
     int n, k;              // N (SiLU pairs), K
     int rows;              // attention rows (B): grid rows past it prefetch
     const int32_t *prow;   // [B] row whose cache holds this row's prompt keys / values, or null (own row)
+    int ofrag = 0;         // output in the fragment order o_proj's register-streamed A operand reads (B % 16 == 0)
 };
+
+// element (row b, column c) of a [B, K] activation in the fragment order of
+// xstream_gemm_kernel's A operand (the act_frag layout): per 16-row group and
+// 32-wide k-step one 1 KB run of 64 lanes x 8 consecutive columns
+__device__ __forceinline__ int64_t frag_at(int64_t b, int c, int K) {
+    return (((b >> 4) * (K >> 5) + (c >> 5)) * 64 + ((c >> 3) & 3) * 16 + (b & 15)) * 8 + (c & 7);
+}
 
 template <int D, int GQ>
 __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
@@ -1287,7 +1295,8 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
     const int pos = pl + step;
     uint16_t *ob = out + b * (int64_t)Hq * D + kvh * GQ * D;
     if (step < 0 || slot_new >= Tmax || pl < 0 || pl > P) {  // never write outside the cache
-        for (int idx = tid; idx < GQ * D; idx += kAttnThreads) ob[idx] = 0x7fc0;  // NaN: fail loudly
+        for (int idx = tid; idx < GQ * D; idx += kAttnThreads)  // NaN: fail loudly
+            out[pf.ofrag ? frag_at(b, kvh * GQ * D + idx, Hq * D) : b * (int64_t)Hq * D + kvh * GQ * D + idx] = 0x7fc0;
         return;
     }
     const int n = slot_new - start + 1;  // keys incl. the new one (index n-1)
@@ -1445,8 +1454,7 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
     }
     __syncthreads();
     SWH_GEMM_TRACE(4);
-    for (int idx = tid; idx < GQ * D; idx += kAttnThreads) {
-        const int h = idx / D, d = idx - h * D;
+    auto merged = [&](int h, int d) -> uint16_t {  // the waves' (m, l, acc) of head h, dim d
         float mxw = kNegInf;
 #pragma unroll
         for (int w2 = 0; w2 < kAttnWaves; ++w2) mxw = fmaxf(mxw, red_s[w2][h][D]);
@@ -1459,7 +1467,26 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
             Ls = fmaf(red_s[w2][h][D + 1], cq, Ls);
             A = fmaf(red_s[w2][h][d], cq, A);
         }
-        ob[idx] = f32_to_bf16_bits(A / Ls);
+        return f32_to_bf16_bits(A / Ls);
+    };
+    if (pf.ofrag) {
+        // one element per thread as below; lanes 8j .. 8j+7 hold 8 consecutive dims
+        // (GQ * D % 64 == 0: whole waves per pass), gathered by shuffles into lane 8j,
+        // which stores them as one 16-B piece at their fragment-order place
+        for (int idx = tid; idx < GQ * D; idx += kAttnThreads) {
+            const int h = idx / D, d = idx - h * D;
+            const uint32_t v = merged(h, d);
+            const uint32_t p2 = v | (__shfl_down(v, 1, kWave) << 16);
+            const uint32_t p4 = __shfl_down(p2, 2, kWave);
+            const uint32_t p6 = __shfl_down(p2, 4, kWave), p8 = __shfl_down(p2, 6, kWave);
+            if ((lane & 7) == 0)
+                *reinterpret_cast<uint4 *>(out + frag_at(b, (kvh * GQ + h) * D + d, Hq * D)) = uint4{p2, p4, p6, p8};
+        }
+    } else {
+        for (int idx = tid; idx < GQ * D; idx += kAttnThreads) {
+            const int h = idx / D, d = idx - h * D;
+            ob[idx] = merged(h, d);
+        }
     }
     SWH_GEMM_TRACE(5);
 #undef SWH_ATTN_ISSUE
@@ -1762,14 +1789,16 @@ int launch_tiles(int nm, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X
 
 using namespace swh;
 
-extern "C" int swh_attn_decode_shared(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
-                                      const float *rope_sin, const int32_t *prompt_len, const int32_t *prompt_row,
-                                      const int32_t *state, int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax,
-                                      float scale, void *out, const void *pf_w, int64_t pf_n, int64_t pf_k,
-                                      void *stream) {
+extern "C" int swh_attn_decode_shared_frag(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
+                                           const float *rope_sin, const int32_t *prompt_len,
+                                           const int32_t *prompt_row, const int32_t *state, int64_t B, int32_t Hq,
+                                           int32_t Hkv, int32_t D, int32_t Tmax, float scale, void *out,
+                                           const void *pf_w, int64_t pf_n, int64_t pf_k, int32_t out_frag,
+                                           void *stream) {
     if (!qkv || !k_cache || !v_cache || !rope_cos || !rope_sin || !prompt_len || !state || !out || B < 0 || Hkv <= 0 ||
-        Hq % Hkv || Tmax <= 0 || B > 65535)
+        Hq % Hkv || Tmax <= 0 || B > 65535 || (out_frag & ~1))
         return SWH_E_ARG;
+    if (out_frag && (B % 16 || (Hq * D) % 32 || (reinterpret_cast<uintptr_t>(out) & 15))) return SWH_E_ARG;
     if (pf_w && (pf_n <= 0 || pf_n % 8 || pf_k <= 0 || pf_k % 8 || pf_n >= (1 << 28) || pf_k >= (1 << 20) ||
                  (reinterpret_cast<uintptr_t>(pf_w) & 15)))
         return SWH_E_ARG;
@@ -1779,10 +1808,18 @@ extern "C" int swh_attn_decode_shared(const void *qkv, void *k_cache, void *v_ca
     auto *kc = static_cast<uint16_t *>(k_cache), *vc = static_cast<uint16_t *>(v_cache);
     auto *o = static_cast<uint16_t *>(out);
     const int gq = Hq / Hkv;
-    const AttnPrefetch pf{static_cast<const uint16_t *>(pf_w), (int)pf_n, (int)pf_k, (int)B, prompt_row};
+    const AttnPrefetch pf{static_cast<const uint16_t *>(pf_w), (int)pf_n, (int)pf_k, (int)B, prompt_row, out_frag};
     if (D == 64) return attn_dispatch_gq<64>(gq, q, kc, vc, rope_cos, rope_sin, prompt_len, state, B, Hq, Hkv, Tmax, scale, o, s, pf);
     if (D == 128) return attn_dispatch_gq<128>(gq, q, kc, vc, rope_cos, rope_sin, prompt_len, state, B, Hq, Hkv, Tmax, scale, o, s, pf);
     return SWH_E_ARG;
+}
+extern "C" int swh_attn_decode_shared(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
+                                      const float *rope_sin, const int32_t *prompt_len, const int32_t *prompt_row,
+                                      const int32_t *state, int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax,
+                                      float scale, void *out, const void *pf_w, int64_t pf_n, int64_t pf_k,
+                                      void *stream) {
+    return swh_attn_decode_shared_frag(qkv, k_cache, v_cache, rope_cos, rope_sin, prompt_len, prompt_row, state, B, Hq,
+                                       Hkv, D, Tmax, scale, out, pf_w, pf_n, pf_k, 0, stream);
 }
 
 extern "C" int swh_attn_decode_prefetch(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,

@@ -181,6 +181,10 @@ class DecodeEngine:
                              for i in range(c.num_hidden_layers)) and c.intermediate_size % 32 == 0 and
                          c.hidden_size <= 1024 and c.intermediate_size <= 4864 and  # tile gate/up, <= 19 k-steps/wave
                          c.intermediate_size // 8 >= torch.cuda.get_device_properties(dev).multi_processor_count)
+        # the attention writes its output in the fragment order o_proj reads (register-
+        # streamed A operand as contiguous 1 KB runs); SWH_ATT_FRAG=0 keeps it row-major
+        self.att_frag = (os.environ.get("SWH_ATT_FRAG", "1") != "0" and B % 16 == 0 and c.q_dim % 32 == 0 and
+                         all(f"l{i}.o_w" in self.fragw for i in range(c.num_hidden_layers)))
         self.graph = None
         self.graph_k = None
         self._prefill_graphs = {}
@@ -293,6 +297,8 @@ class DecodeEngine:
         if name in self.fragw:
             if self.act_frag and name.endswith(("gu_w", "down_w")):
                 kw["act_frag"] = 1 if name.endswith("gu_w") else 2
+            elif "act_frag" in kw and not name.endswith("o_w"):
+                raise ValueError(f"{name}: act_frag serves gate/up, down and o only")
             return nn_ops.decode_gemm_fragw(x, self.fragw[name], eps=eps, **kw)
         norm = self._projections()[name][3]
         if norm is None:
@@ -313,8 +319,11 @@ class DecodeEngine:
                 self.packed and f"l{i}.gu_w" not in self.fragw else None
             nn_ops.attn_decode(self.qkv, self.kv[i, 0], self.kv[i, 1], self.cos, self.sin, self.plen, self.state,
                                c.num_attention_heads, c.num_key_value_heads, c.head_dim, c.head_dim ** -0.5,
-                               out=self.att, prefetch_gate_up=pf, prompt_row=self.prow)
-            self._proj(f"l{i}.o_w", self.att, residual=self.s, ss_out=ss)
+                               out=self.att, prefetch_gate_up=pf, prompt_row=self.prow, out_frag=self.att_frag)
+            if self.att_frag:
+                self._proj(f"l{i}.o_w", self.att, residual=self.s, ss_out=ss, act_frag=2)
+            else:
+                self._proj(f"l{i}.o_w", self.att, residual=self.s, ss_out=ss)
             self._proj(f"l{i}.gu_w", self.s, silu=True, y=self.act, ss_in=ss)
             self._proj(f"l{i}.down_w", self.act, residual=self.s, ss_out=ss)
         if self._fused_sample():
@@ -440,9 +449,10 @@ class DecodeEngine:
                                                          prefetch_gate_up=self._normed(f"l{i}.gu_w", "")[0]
                                                          if self.prefetch and f"l{i}.gu_w" not in self.packed
                                                          and f"l{i}.gu_w" not in self.fragw
-                                                         else None, prompt_row=self.prow),
+                                                         else None, prompt_row=self.prow, out_frag=self.att_frag),
                             att_bytes, L),
-            "decode_gemm.o": (lambda i: self._proj(f"l{i}.o_w", self.att, residual=self.s, ss_out=ss),
+            "decode_gemm.o": (lambda i: self._proj(f"l{i}.o_w", self.att, residual=self.s, ss_out=ss,
+                                                   **({"act_frag": 2} if self.att_frag else {})),
                               gemm_bytes(H, c.q_dim), L),
             "decode_gemm.gate_up": (lambda i: self._proj(f"l{i}.gu_w", self.s, silu=True, y=self.act, ss_in=ss),
                                     gemm_bytes(I, H, silu=True), L),

@@ -109,23 +109,24 @@ def attn_decode(qkv: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                 rope_sin: torch.Tensor, prompt_len: torch.Tensor, state: torch.Tensor, Hq: int, Hkv: int, D: int,
                 scale: float, out: Optional[torch.Tensor] = None,
                 prefetch_gate_up: Optional[torch.Tensor] = None,
-                prompt_row: Optional[torch.Tensor] = None) -> torch.Tensor:
+                prompt_row: Optional[torch.Tensor] = None, out_frag: bool = False) -> torch.Tensor:
     """One decode step of GQA attention with in-kernel RoPE and KV append.
     k_cache / v_cache: [B, Hkv, Tmax, D] bf16 (one layer).  prefetch_gate_up
     [2 I, H] (optional): the layer's gate/up weights, read into the consuming
     XCDs' L2 by extra workgroups of the same launch (swh_attn_decode_prefetch).
     prompt_row int32 [B] (optional): row b reads its prompt keys / values from
-    row prompt_row[b]'s cache (swh_attn_decode_shared)."""
+    row prompt_row[b]'s cache (swh_attn_decode_shared).  out_frag: `out` in the
+    fragment order decode_gemm_fragw(act_frag=2) reads (swh_attn_decode_shared_frag)."""
     _dev(qkv, "attn_decode")
     B = qkv.shape[0]
     Tmax = k_cache.shape[2]
     if out is None:
         out = torch.empty(B, Hq * D, device=qkv.device, dtype=qkv.dtype)
     pw = prefetch_gate_up
-    call("swh_attn_decode_shared", qkv.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), rope_cos.data_ptr(),
+    call("swh_attn_decode_shared_frag", qkv.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), rope_cos.data_ptr(),
          rope_sin.data_ptr(), prompt_len.data_ptr(), _p(prompt_row), state.data_ptr(), B, Hq, Hkv, D, Tmax,
          float(scale), out.data_ptr(), _p(pw), 0 if pw is None else pw.shape[0] // 2,
-         0 if pw is None else pw.shape[1], _stream())
+         0 if pw is None else pw.shape[1], int(bool(out_frag)), _stream())
     return out
 
 

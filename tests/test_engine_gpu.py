@@ -647,6 +647,31 @@ def test_act_frag_generates_identically(dev, monkeypatch):
                 assert torch.equal(x, y)
 
 
+def test_att_frag_generates_identically(dev, monkeypatch):
+    """The decode step with the attention writing its output in o_proj's
+    fragment order (SWH_ATT_FRAG=1) generates the same tokens and log-probs as
+    the row-major output, greedy and sampled, left padding included."""
+    from swh_trl_amd.engine import CausalLM, DecodeEngine, tiny_qwen2
+    m = CausalLM(tiny_qwen2(1024, 2), dev, seed=5)
+    g = torch.Generator().manual_seed(5)
+    B, P, C = 32, 12, 20
+    ids = torch.randint(0, m.cfg.vocab_size, (B, P), generator=g).to(dev)
+    mask = torch.ones(B, P, dtype=torch.int64, device=dev)
+    mask[4, :3] = 0
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SWH_ATT_FRAG", flag)
+        eng = DecodeEngine(m, B, P, C)
+        assert eng.att_frag == (flag == "1")
+        outs[flag] = (eng.generate(ids, mask, C, greedy=True),
+                      eng.generate(ids, mask, C, temperature=0.9, seed=3, return_logp=True))
+        del eng
+    for a, b in zip(outs["1"], outs["0"]):
+        for x, y in zip(a, b):
+            if isinstance(x, torch.Tensor):
+                assert torch.equal(x, y)
+
+
 def test_fragw_projections_generate_identically(dev, monkeypatch):
     """DecodeEngine with o_proj / down_proj read from fragment-order copies
     (swh_frag_pack + swh_decode_gemm_fragw, refreshed every generate()) gives

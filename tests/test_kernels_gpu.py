@@ -894,6 +894,44 @@ def test_attn_decode_shared_prompt_rows(ops, dev, D, Hkv, G, P, step):
     assert torch.equal(a, c)
 
 
+@pytest.mark.parametrize("D,Hkv,Hq,B", [(64, 2, 14, 64), (128, 8, 32, 32)])
+def test_attn_decode_frag_output_feeds_o_proj(ops, dev, D, Hkv, Hq, B):
+    """swh_attn_decode_shared_frag with out_frag = 1 writes exactly the row-major
+    output permuted into o_proj's fragment order (torch restatement of the
+    layout), the same appended K/V slot, and o_proj reading it (act_frag bit 1)
+    equals o_proj over the row-major output bit for bit, residual rows and
+    chunk sums of squares."""
+    from swh_trl_amd import nn_ops
+    g = _gen(61)
+    P, step = 40, 17
+    Tmax = P + step + 8
+    kc = torch.randn(B, Hkv, Tmax, D, generator=g).to(torch.bfloat16).to(dev)
+    vc = torch.randn(B, Hkv, Tmax, D, generator=g).to(torch.bfloat16).to(dev)
+    qkv = torch.randn(B, (Hq + 2 * Hkv) * D, generator=g).to(torch.bfloat16).to(dev)
+    cos, sin = _rope_tables(D, 2048, 1e6, dev)
+    plen = torch.full((B,), P, dtype=torch.int32, device=dev)
+    plen[3] = 9
+    state = torch.tensor([step + 1, P], dtype=torch.int32, device=dev)
+    k1, v1, k2, v2 = kc.clone(), vc.clone(), kc.clone(), vc.clone()
+    a = nn_ops.attn_decode(qkv, k1, v1, cos, sin, plen, state, Hq, Hkv, D, D ** -0.5)
+    f = nn_ops.attn_decode(qkv, k2, v2, cos, sin, plen, state, Hq, Hkv, D, D ** -0.5, out_frag=True)
+    Q = Hq * D
+    assert torch.equal(f, a.view(B // 16, 16, Q // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(B, Q))
+    assert torch.equal(k1, k2) and torch.equal(v1, v2)
+    if Q != 896:  # o_proj on the fragment-order path: the 0.5B width (8B's o_proj is the packed wide GEMM)
+        return
+    H = 896
+    wo = nn_ops.frag_pack((torch.randn(H, Q, generator=g) * Q ** -0.5).to(torch.bfloat16).to(dev))
+    s0 = torch.randn(B, H, generator=g).to(torch.bfloat16).to(dev)
+    outs = []
+    for act, x in ((0, a), (2, f)):
+        r, so = s0.clone(), torch.full((B, H // 16), float("nan"), device=dev)
+        nn_ops.decode_gemm_fragw(x, wo, residual=r, ss_out=so, act_frag=act)
+        outs.append((r, so))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
 # --------------------------------------------------------------------------- fused decode GEMM
 def _ref_norm(x, w, eps):
     xf = x.float()
