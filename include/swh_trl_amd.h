@@ -350,6 +350,31 @@ int swh_attn_bwd_parts(const void *q, const void *k, const void *v, const void *
                        const float *lse, int64_t B, int32_t Hq, int32_t Hkv, int64_t L, int32_t D, float scale,
                        const int32_t *key_mask, const int32_t *first_valid, float *delta, void *dq, void *dk,
                        void *dv, int32_t parts, void *stream);
+/* The same attention over operands given as views: an operand indexed
+ * [B, H, L, D] (D contiguous, 16-B aligned) whose rows l < P live in segment 0
+ * at sequence index b / div[0] and rows l >= P in segment 1 at b / div[1], each
+ * with its own element strides per sequence, head and row (P = 0: segment 1
+ * only).  G > 0: queries l < P of sequences b % G != 0 are neither computed nor
+ * written (their output, lse and gradients do not exist; they contribute to no
+ * dK / dV).  This is the GRPO shared-prompt forward (engine/model.py
+ * hidden_states_grouped): Q/K/V of a group's prompt once per group (div G),
+ * each row's completion (div 1), the output token-major [prompt tokens of the
+ * groups | completion tokens of the rows, Hq D] for o_proj, dK / dV of the
+ * prompt keys per row (div 1, summed over the group by the caller).
+ * swh_attn_fwd / swh_attn_bwd_parts are these over plain [B, H, L, D] views. */
+typedef struct swh_attn_view {
+    void *base[2];
+    int64_t sb[2], sh[2], sl[2]; /* element strides: per sequence (index b / div), per head, per row */
+    int32_t div[2];
+} swh_attn_view;
+int swh_attn_fwd_v(const swh_attn_view *q, const swh_attn_view *k, const swh_attn_view *v, const swh_attn_view *out,
+                   int64_t B, int32_t Hq, int32_t Hkv, int64_t L, int64_t P, int32_t G, int32_t D, float scale,
+                   const int32_t *key_mask, const int32_t *first_valid, float *lse, void *stream);
+int swh_attn_bwd_v_parts(const swh_attn_view *q, const swh_attn_view *k, const swh_attn_view *v,
+                         const swh_attn_view *out, const swh_attn_view *dout, const float *lse, int64_t B, int32_t Hq,
+                         int32_t Hkv, int64_t L, int64_t P, int32_t G, int32_t D, float scale,
+                         const int32_t *key_mask, const int32_t *first_valid, float *delta, const swh_attn_view *dq,
+                         const swh_attn_view *dk, const swh_attn_view *dv, int32_t parts, void *stream);
 
 /* Folded RMSNorm weights for the decode GEMMs in ONE launch: for every job j of
  * the device-resident table jobs[njobs] = {W [rows, cols] bf16, w [cols] bf16,

@@ -20,6 +20,12 @@ LOSS_TYPES = {"grpo": 0, "bnpo": 1, "dr_grpo": 2}
 IS_LEVELS = {"token": 0, "sequence": 1}
 
 
+class AttnView(C.Structure):
+    """swh_attn_view (include/swh_trl_amd.h)."""
+    _fields_ = [("base", C.c_void_p * 2), ("sb", c_i64 * 2), ("sh", c_i64 * 2), ("sl", c_i64 * 2),
+                ("div", c_i32 * 2)]
+
+
 class SampleParams(C.Structure):
     """swh_sample_params (include/swh_trl_amd.h)."""
     _fields_ = [("temperature", c_f32), ("top_p", c_f32), ("min_p", c_f32), ("repetition_penalty", c_f32),
@@ -89,6 +95,11 @@ SIGNATURES = {
                              c_vp, c_vp, c_vp, c_vp, c_vp]),
     "swh_attn_bwd_parts": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i64, c_i32, c_f32, c_vp,
                                    c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp]),
+    "swh_attn_fwd_v": (c_i32, [C.POINTER(AttnView)] * 4 + [c_i64, c_i32, c_i32, c_i64, c_i64, c_i32, c_i32, c_f32,
+                                                            c_vp, c_vp, c_vp, c_vp]),
+    "swh_attn_bwd_v_parts": (c_i32, [C.POINTER(AttnView)] * 5 + [c_vp, c_i64, c_i32, c_i32, c_i64, c_i64, c_i32,
+                                                                  c_i32, c_f32, c_vp, c_vp, c_vp] +
+                             [C.POINTER(AttnView)] * 3 + [c_i32, c_vp]),
     "swh_fold_norm": (c_i32, [c_vp, c_i32, c_i64, c_vp]),
     "swh_embedding_bwd_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "swh_embedding_bwd": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp]),

@@ -48,15 +48,57 @@ __device__ __forceinline__ bf16x4sa fa_tr16(const uint16_t *p) {
         (__attribute__((address_space(3))) bf16x4sa *)(const_cast<uint16_t *>(p)));
 }
 
+// An operand indexed [B, H, L, D] (D contiguous) stored as up to two segments:
+// rows l < P in segment 0 at sequence index b / div0, rows l >= P in segment 1
+// at b / div1, each with its own element strides per sequence, head and row.
+// P = 0 is one plain segment.  This is how the GRPO shared-prompt forward
+// (engine/model.py hidden_states_grouped) hands over the group's prompt Q/K/V
+// once per group and each row's completion, and takes the output token-major
+// ([tokens, Hq D], the o_proj input) without any concatenation or transpose.
+struct FaView {
+    uint16_t *base0, *base1;
+    int64_t sb0, sh0, sl0, sb1, sh1, sl1;
+    int div0, div1;
+};
+// the rows of one sequence of a view: the divisions by div happen once per
+// workgroup here, not per row (a 32-bit division is ~40 instructions)
+struct FaRows {
+    uint16_t *p, *c;     // head 0 of the sequence in segment 0 / 1
+    int64_t hp, hc;      // head strides
+    int64_t sp, sc;      // row strides
+    int P;
+    __device__ __forceinline__ uint16_t *row(int h, int l) const {
+        return l < P ? p + (int64_t)h * hp + (int64_t)l * sp : c + (int64_t)h * hc + (int64_t)(l - P) * sc;
+    }
+};
+__device__ __forceinline__ FaRows fa_rows(const FaView &v, int P, int b) {
+    FaRows r;
+    r.p = v.base0 + (int64_t)(b / v.div0) * v.sb0;
+    r.c = v.base1 + (int64_t)(b / v.div1) * v.sb1;
+    r.hp = v.sh0;
+    r.hc = v.sh1;
+    r.sp = v.sl0;
+    r.sc = v.sl1;
+    r.P = P;
+    return r;
+}
+__device__ __forceinline__ uint16_t *fa_row(const FaView &v, int P, int b, int h, int l) {
+    return fa_rows(v, P, b).row(h, l);
+}
+
 struct FaArgs {
-    const uint16_t *q, *k, *v, *o, *dout;  // [B, H, L, D]
-    const int32_t *key_mask;               // [B, L] or null (no padding)
-    const int32_t *first_valid;            // [B] or null
-    float *lse, *delta;                    // [B, Hq, L]
-    uint16_t *out, *dq, *dk, *dv;
+    FaView q, k, v, o, dout, dq, dk, dv;
+    const int32_t *key_mask;     // [B, L] or null (no padding)
+    const int32_t *first_valid;  // [B] or null
+    float *lse, *delta;          // [B, Hq, L]
     int B, Hq, Hkv, L;
+    int P;                       // rows in segment 0 (0: plain layout)
+    int G;                       // > 0: queries l < P of sequences b % G != 0 are not computed (their
+                                 // output has no slot: the group's first sequence carries the prompt)
     float scale;
 };
+// a query that is computed and whose output / gradient exists
+__device__ __forceinline__ bool fa_qlive(const FaArgs &a, int b, int q) { return !(a.G && (b % a.G) && q < a.P); }
 
 // the 8 keys a lane holds in a 32-key block: k0 + 16 t + 4 g + r, t = 0, 1, r = 0..3
 struct FaKeyMask {
@@ -189,17 +231,16 @@ struct FaStage {
     static constexpr int kPer = kPieces / 256;        // per thread (blocks have >= 256 threads)
     u32x4 v[kPer];
 };
-template <int D>
-__device__ __forceinline__ void fa_stage_load(FaStage<D> &st, const uint16_t *kbase, const uint16_t *vbase, int r0,
-                                              int L, int tid, int nthr) {
+// rowp(which, row): the row of slab `which` (0: K / Q, 1: V / dO)
+template <int D, typename RowP>
+__device__ __forceinline__ void fa_stage_load(FaStage<D> &st, RowP rowp, int r0, int L, int tid, int nthr) {
 #pragma unroll
     for (int j = 0; j < FaStage<D>::kPer; ++j) {
         const int pc = tid + j * nthr;
         if (pc < FaStage<D>::kPieces) {
             const int which = pc / (32 * D / 8), rem = pc - which * (32 * D / 8);
             const int row = rem / (D / 8), col = rem - row * (D / 8);
-            const uint16_t *src = (which ? vbase : kbase) + (int64_t)min(r0 + row, L - 1) * D + col * 8;
-            st.v[j] = *reinterpret_cast<const u32x4 *>(src);
+            st.v[j] = *reinterpret_cast<const u32x4 *>(rowp(which, min(r0 + row, L - 1)) + col * 8);
         }
     }
 }
@@ -236,17 +277,19 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(FaArgs a) {
     const bool active = wid < G;  // waves past the group's heads only help staging (blocks >= 4 waves)
     const int h = kvh * G + min(wid, G - 1);
     const int q0 = blockIdx.x * 16 * QT;
+    if (!fa_qlive(a, b, q0 + 16 * QT - 1)) return;  // the whole tile: prompt queries another sequence carries
     const int fv = a.first_valid ? a.first_valid[b] : 0;
-    const uint16_t *kb_ = a.k + ((int64_t)b * a.Hkv + kvh) * L * D;
-    const uint16_t *vb_ = a.v + ((int64_t)b * a.Hkv + kvh) * L * D;
-    const uint16_t *qb_ = a.q + ((int64_t)b * a.Hq + h) * L * D;
+    const FaRows kr_b = fa_rows(a.k, a.P, b), vr_b = fa_rows(a.v, a.P, b), qr_b = fa_rows(a.q, a.P, b);
+    auto kvrow = [&](int which, int row) -> const uint16_t * {
+        return which ? vr_b.row(kvh, row) : kr_b.row(kvh, row);
+    };
     u32x4 qf[QT][DC];
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
         const int qc = min(q0 + 16 * t + c16, L - 1);  // this lane's query column of tile t
+        const uint16_t *qr_ = qr_b.row(h, qc);
 #pragma unroll
-        for (int c = 0; c < DC; ++c)
-            qf[t][c] = *reinterpret_cast<const u32x4 *>(qb_ + (int64_t)qc * D + c * 32 + g * 8);
+        for (int c = 0; c < DC; ++c) qf[t][c] = *reinterpret_cast<const u32x4 *>(qr_ + c * 32 + g * 8);
     }
     float m[QT], l[QT];
     f32x4a o[QT][DB];
@@ -259,13 +302,13 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(FaArgs a) {
     }
     const int kend = min(q0 + 16 * QT, L);  // causal: keys < kend
     FaStage<D> st;
-    fa_stage_load<D>(st, kb_, vb_, 0, L, tid, nthr);
+    fa_stage_load<D>(st, kvrow, 0, L, tid, nthr);
     fa_stage_store<D, VS>(st, kt[0], vt[0], tid, nthr);
     __syncthreads();
     int buf = 0;
     for (int k0 = 0; k0 < kend; k0 += 32, buf ^= 1) {
         const bool more = k0 + 32 < kend;
-        if (more) fa_stage_load<D>(st, kb_, vb_, k0 + 32, L, tid, nthr);  // next block streams meanwhile
+        if (more) fa_stage_load<D>(st, kvrow, k0 + 32, L, tid, nthr);  // next block streams meanwhile
         u32x4 kr[2][DC];
         fa_rows_lds<D, VS>(kr, kt[buf], c16, g);
         const FaKeyMask km = fa_key_mask(a, b, k0, g);
@@ -309,8 +352,8 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(FaArgs a) {
         lt += __shfl_xor(lt, 16, kWave);
         lt += __shfl_xor(lt, 32, kWave);
         const int q = q0 + 16 * t + c16;
-        if (active && q < L) {
-            uint16_t *ob = a.out + (((int64_t)b * a.Hq + h) * L + q) * D;
+        if (active && q < L && fa_qlive(a, b, q)) {
+            uint16_t *ob = fa_row(a.o, a.P, b, h, q);
             const float inv = 1.f / lt;
 #pragma unroll
             for (int d = 0; d < DB; ++d) {
@@ -328,10 +371,12 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(FaArgs a) {
 // ---- backward preprocess: delta[q] = sum_d dO[q][d] O[q][d] (one wave per 4 queries... one thread per query)
 template <int D>
 __global__ __launch_bounds__(256) void fa_delta_kernel(FaArgs a, int64_t rows) {
-    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;  // over [B, Hq, L]
     if (r >= rows) return;
-    const uint4 *o = reinterpret_cast<const uint4 *>(a.o + r * D);
-    const uint4 *d = reinterpret_cast<const uint4 *>(a.dout + r * D);
+    const int l = (int)(r % a.L), h = (int)((r / a.L) % a.Hq), b = (int)(r / ((int64_t)a.L * a.Hq));
+    if (!fa_qlive(a, b, l)) return;  // read by no one
+    const uint4 *o = reinterpret_cast<const uint4 *>(fa_row(a.o, a.P, b, h, l));
+    const uint4 *d = reinterpret_cast<const uint4 *>(fa_row(a.dout, a.P, b, h, l));
     float s = 0.f;
 #pragma unroll
     for (int c = 0; c < D / 8; ++c) {
@@ -356,16 +401,22 @@ __global__ __launch_bounds__(512) void fa_dq_kernel(FaArgs a) {
     const bool active = wid < G;
     const int h = kvh * G + min(wid, G - 1);
     const int q0 = blockIdx.x * 16;
+    if (!fa_qlive(a, b, q0 + 15)) return;  // the whole tile: prompt queries another sequence carries
     const int qc = min(q0 + c16, L - 1);
     const int fv = a.first_valid ? a.first_valid[b] : 0;
     const int64_t qrow = ((int64_t)b * a.Hq + h) * L;
-    const uint16_t *kb_ = a.k + ((int64_t)b * a.Hkv + kvh) * L * D;
-    const uint16_t *vb_ = a.v + ((int64_t)b * a.Hkv + kvh) * L * D;
+    const FaRows kr_b = fa_rows(a.k, a.P, b), vr_b = fa_rows(a.v, a.P, b);
+    auto kvrow = [&](int which, int row) -> const uint16_t * {
+        return which ? vr_b.row(kvh, row) : kr_b.row(kvh, row);
+    };
     u32x4 qf[DC], df[DC];
+    {
+        const uint16_t *qr_ = fa_row(a.q, a.P, b, h, qc), *dr_ = fa_row(a.dout, a.P, b, h, qc);
 #pragma unroll
-    for (int c = 0; c < DC; ++c) {
-        qf[c] = *reinterpret_cast<const u32x4 *>(a.q + (qrow + qc) * D + c * 32 + g * 8);
-        df[c] = *reinterpret_cast<const u32x4 *>(a.dout + (qrow + qc) * D + c * 32 + g * 8);
+        for (int c = 0; c < DC; ++c) {
+            qf[c] = *reinterpret_cast<const u32x4 *>(qr_ + c * 32 + g * 8);
+            df[c] = *reinterpret_cast<const u32x4 *>(dr_ + c * 32 + g * 8);
+        }
     }
     const float lse = a.lse[qrow + qc], dl = a.delta[qrow + qc];
     f32x4a acc[DB];
@@ -373,13 +424,13 @@ __global__ __launch_bounds__(512) void fa_dq_kernel(FaArgs a) {
     for (int d = 0; d < DB; ++d) acc[d] = f32x4a{0.f, 0.f, 0.f, 0.f};
     const int kend = min(q0 + 16, L);
     FaStage<D> st;
-    fa_stage_load<D>(st, kb_, vb_, 0, L, tid, nthr);
+    fa_stage_load<D>(st, kvrow, 0, L, tid, nthr);
     fa_stage_store<D, VS>(st, kt[0], vt[0], tid, nthr);
     __syncthreads();
     int buf = 0;
     for (int k0 = 0; k0 < kend; k0 += 32, buf ^= 1) {
         const bool more = k0 + 32 < kend;
-        if (more) fa_stage_load<D>(st, kb_, vb_, k0 + 32, L, tid, nthr);
+        if (more) fa_stage_load<D>(st, kvrow, k0 + 32, L, tid, nthr);
         u32x4 kr[2][DC], vr[2][DC];
         fa_rows_lds<D, VS>(kr, kt[buf], c16, g);
         fa_rows_lds<D, VS>(vr, vt[buf], c16, g);
@@ -400,8 +451,8 @@ __global__ __launch_bounds__(512) void fa_dq_kernel(FaArgs a) {
         if (more) fa_stage_store<D, VS>(st, kt[buf ^ 1], vt[buf ^ 1], tid, nthr);
         __syncthreads();
     }
-    if (active && q0 + c16 < L) {
-        uint16_t *qb = a.dq + (qrow + q0 + c16) * D;
+    if (active && q0 + c16 < L && fa_qlive(a, b, q0 + c16)) {
+        uint16_t *qb = fa_row(a.dq, a.P, b, h, q0 + c16);
 #pragma unroll
         for (int d = 0; d < DB; ++d) {
             const uint32_t lo = (uint32_t)f32_to_bf16_bits(acc[d][0] * a.scale) |
@@ -431,12 +482,14 @@ __global__ __launch_bounds__(256) void fa_dkdv_kernel(FaArgs a) {
     const int kc = min(k0w + c16, L - 1);  // this lane's key column
     const int fv = a.first_valid ? a.first_valid[b] : 0;
     const int kmv = a.key_mask ? a.key_mask[(int64_t)b * L + kc] : 1;
-    const int64_t kvrow = ((int64_t)b * a.Hkv + kvh) * L;
     u32x4 kf[DC], vf[DC];
+    {
+        const uint16_t *kr_ = fa_row(a.k, a.P, b, kvh, kc), *vr_ = fa_row(a.v, a.P, b, kvh, kc);
 #pragma unroll
-    for (int c = 0; c < DC; ++c) {
-        kf[c] = *reinterpret_cast<const u32x4 *>(a.k + (kvrow + kc) * D + c * 32 + g * 8);
-        vf[c] = *reinterpret_cast<const u32x4 *>(a.v + (kvrow + kc) * D + c * 32 + g * 8);
+        for (int c = 0; c < DC; ++c) {
+            kf[c] = *reinterpret_cast<const u32x4 *>(kr_ + c * 32 + g * 8);
+            vf[c] = *reinterpret_cast<const u32x4 *>(vr_ + c * 32 + g * 8);
+        }
     }
     f32x4a dk[DB], dv[DB];
 #pragma unroll
@@ -444,20 +497,26 @@ __global__ __launch_bounds__(256) void fa_dkdv_kernel(FaArgs a) {
         dk[d] = f32x4a{0.f, 0.f, 0.f, 0.f};
         dv[d] = f32x4a{0.f, 0.f, 0.f, 0.f};
     }
-    const int qstart = kb0;  // causal: queries >= the workgroup's first key
-    const int nb = (L - qstart + 32 * R - 1) / (32 * R), nit = G * nb;
+    // causal: queries >= the workgroup's first key (and past the prompt when another
+    // sequence carries this one's prompt queries)
+    const int qstart = fa_qlive(a, b, 0) ? kb0 : max(kb0, a.P);
+    const int nb = qstart < L ? (L - qstart + 32 * R - 1) / (32 * R) : 0, nit = G * nb;
     auto rows_of = [&](int it, int64_t &qrow, int &r0) {
         r0 = qstart + 32 * R * (it % nb);
         qrow = ((int64_t)b * a.Hq + kvh * G + it / nb) * L;
     };
     FaStage<D> st[R];
+    const FaRows qr_b = fa_rows(a.q, a.P, b), dr_b = fa_rows(a.dout, a.P, b);
     auto load = [&](int it) {
         int64_t qrow;
         int r0;
         rows_of(it, qrow, r0);
+        const int hq = kvh * G + it / nb;
+        auto qdrow = [&](int which, int row) -> const uint16_t * {
+            return which ? dr_b.row(hq, row) : qr_b.row(hq, row);
+        };
 #pragma unroll
-        for (int h = 0; h < R; ++h)
-            fa_stage_load<D>(st[h], a.q + qrow * D, a.dout + qrow * D, r0 + 32 * h, L, tid, nthr);
+        for (int h = 0; h < R; ++h) fa_stage_load<D>(st[h], qdrow, r0 + 32 * h, L, tid, nthr);
     };
     auto store = [&](int it, int buf) {  // staged blocks + the rows' lse / delta into LDS
         int64_t qrow;
@@ -468,8 +527,10 @@ __global__ __launch_bounds__(256) void fa_dkdv_kernel(FaArgs a) {
         if (tid < 32 * R) lse_s[buf][tid] = a.lse[qrow + min(r0 + tid, L - 1)];
         else if (tid < 64 * R) del_s[buf][tid - 32 * R] = a.delta[qrow + min(r0 + tid - 32 * R, L - 1)];
     };
-    load(0);
-    store(0, 0);
+    if (nit) {
+        load(0);
+        store(0, 0);
+    }
     __syncthreads();
     int buf = 0;
     for (int it = 0; it < nit; ++it, buf ^= 1) {
@@ -492,7 +553,7 @@ __global__ __launch_bounds__(256) void fa_dkdv_kernel(FaArgs a) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int qi = 32 * h + 16 * t + 4 * g + r, q = r0 + qi;
-                        const bool vis = (q < L) & fa_vis(q, k0w + c16, L, kmv, fv);
+                        const bool vis = (q < L) & fa_vis(q, k0w + c16, L, kmv, fv) & fa_qlive(a, b, q);
                         const float pv = vis ? __expf(s[t][r] * a.scale - lse_s[buf][qi]) : 0.f;
                         p[4 * t + r] = pv;
                         ds[4 * t + r] = vis ? pv * (dp[t][r] - del_s[buf][qi]) : 0.f;
@@ -505,8 +566,8 @@ __global__ __launch_bounds__(256) void fa_dkdv_kernel(FaArgs a) {
         __syncthreads();
     }
     if (k0w + c16 < L) {
-        uint16_t *kb = a.dk + (kvrow + k0w + c16) * D;
-        uint16_t *vb = a.dv + (kvrow + k0w + c16) * D;
+        uint16_t *kb = fa_row(a.dk, a.P, b, kvh, k0w + c16);
+        uint16_t *vb = fa_row(a.dv, a.P, b, kvh, k0w + c16);
 #pragma unroll
         for (int d = 0; d < DB; ++d) {
             const uint32_t klo = (uint32_t)f32_to_bf16_bits(dk[d][0] * a.scale) |
@@ -521,35 +582,70 @@ __global__ __launch_bounds__(256) void fa_dkdv_kernel(FaArgs a) {
     }
 }
 
-bool fa_args_ok(const void *q, const void *k, const void *v, int64_t B, int32_t Hq, int32_t Hkv, int64_t L,
-                int32_t D) {
-    return q && k && v && B > 0 && Hq > 0 && Hkv > 0 && Hq % Hkv == 0 && L > 0 && L <= (1 << 20) &&
-           B <= 65535 && Hq / Hkv <= 8 && (D == 64 || D == 128);  // a workgroup = the query heads of one KV head
-}
 
 }  // namespace
 }  // namespace swh
 
 using namespace swh;
 
-extern "C" int swh_attn_fwd(const void *q, const void *k, const void *v, int64_t B, int32_t Hq, int32_t Hkv,
-                            int64_t L, int32_t D, float scale, const int32_t *key_mask, const int32_t *first_valid,
-                            void *out, float *lse, void *stream) {
-    if (!fa_args_ok(q, k, v, B, Hq, Hkv, L, D) || !out || !lse || (!key_mask != !first_valid)) return SWH_E_ARG;
+namespace {
+FaView fa_view_of(const swh_attn_view &v) {
+    FaView f;
+    f.base0 = static_cast<uint16_t *>(v.base[0]);
+    f.base1 = static_cast<uint16_t *>(v.base[1]);
+    f.sb0 = v.sb[0];
+    f.sh0 = v.sh[0];
+    f.sl0 = v.sl[0];
+    f.sb1 = v.sb[1];
+    f.sh1 = v.sh[1];
+    f.sl1 = v.sl[1];
+    f.div0 = v.div[0];
+    f.div1 = v.div[1];
+    return f;
+}
+bool fa_view_ok(const swh_attn_view *v, int64_t P) {
+    return v && v->base[1] && v->div[1] >= 1 && (P == 0 || (v->base[0] && v->div[0] >= 1)) &&
+           ((reinterpret_cast<uintptr_t>(v->base[0]) | reinterpret_cast<uintptr_t>(v->base[1])) & 15) == 0 &&
+           ((v->sb[0] | v->sh[0] | v->sl[0] | v->sb[1] | v->sh[1] | v->sl[1]) & 7) == 0;
+}
+// the plain [B, H, L, D] layout as a view
+swh_attn_view fa_plain(const void *p, int64_t H, int64_t L, int32_t D) {
+    swh_attn_view v{};
+    v.base[1] = const_cast<void *>(p);
+    v.sb[1] = H * L * D;
+    v.sh[1] = L * D;
+    v.sl[1] = D;
+    v.div[0] = v.div[1] = 1;
+    return v;
+}
+bool fa_dims_ok(int64_t B, int32_t Hq, int32_t Hkv, int64_t L, int64_t P, int32_t G, int32_t D) {
+    return B > 0 && Hq > 0 && Hkv > 0 && Hq % Hkv == 0 && L > 0 && L <= (1 << 20) && B <= 65535 &&
+           Hq / Hkv <= 8 && (D == 64 || D == 128) && P >= 0 && P <= L && G >= 0 && (G == 0 || P > 0);
+}
+}  // namespace
+
+extern "C" int swh_attn_fwd_v(const swh_attn_view *q, const swh_attn_view *k, const swh_attn_view *v,
+                              const swh_attn_view *out, int64_t B, int32_t Hq, int32_t Hkv, int64_t L, int64_t P,
+                              int32_t G, int32_t D, float scale, const int32_t *key_mask, const int32_t *first_valid,
+                              float *lse, void *stream) {
+    if (!fa_dims_ok(B, Hq, Hkv, L, P, G, D) || !fa_view_ok(q, P) || !fa_view_ok(k, P) || !fa_view_ok(v, P) ||
+        !fa_view_ok(out, P) || !lse || (!key_mask != !first_valid))
+        return SWH_E_ARG;
     FaArgs a{};
-    a.q = static_cast<const uint16_t *>(q);
-    a.k = static_cast<const uint16_t *>(k);
-    a.v = static_cast<const uint16_t *>(v);
+    a.q = fa_view_of(*q);
+    a.k = fa_view_of(*k);
+    a.v = fa_view_of(*v);
+    a.o = fa_view_of(*out);
     a.key_mask = key_mask;
     a.first_valid = first_valid;
     a.lse = lse;
-    a.out = static_cast<uint16_t *>(out);
     a.B = (int)B;
     a.Hq = Hq;
     a.Hkv = Hkv;
     a.L = (int)L;
+    a.P = (int)P;
+    a.G = G;
     a.scale = scale;
-    const dim3 grid((unsigned)((L + 15) / 16), (unsigned)Hkv, (unsigned)B);
     const unsigned thr = 64u * (unsigned)(Hq / Hkv < 4 ? 4 : Hq / Hkv);
     hipStream_t s = static_cast<hipStream_t>(stream);
     // SWH_FA_FWD_QT 16-query tiles per wave (the K fragments of a block serve them all)
@@ -560,30 +656,35 @@ extern "C" int swh_attn_fwd(const void *q, const void *k, const void *v, int64_t
     return launch_status();
 }
 
-extern "C" int swh_attn_bwd_parts(const void *q, const void *k, const void *v, const void *out, const void *dout,
-                                  const float *lse, int64_t B, int32_t Hq, int32_t Hkv, int64_t L, int32_t D,
-                                  float scale, const int32_t *key_mask, const int32_t *first_valid, float *delta,
-                                  void *dq, void *dk, void *dv, int32_t parts, void *stream) {
-    if (!fa_args_ok(q, k, v, B, Hq, Hkv, L, D) || !out || !dout || !lse || !delta || !dq || !dk || !dv ||
-        (!key_mask != !first_valid) || parts <= 0 || parts > 7)
+extern "C" int swh_attn_bwd_v_parts(const swh_attn_view *q, const swh_attn_view *k, const swh_attn_view *v,
+                                    const swh_attn_view *out, const swh_attn_view *dout, const float *lse, int64_t B,
+                                    int32_t Hq, int32_t Hkv, int64_t L, int64_t P, int32_t G, int32_t D, float scale,
+                                    const int32_t *key_mask, const int32_t *first_valid, float *delta,
+                                    const swh_attn_view *dq, const swh_attn_view *dk, const swh_attn_view *dv,
+                                    int32_t parts, void *stream) {
+    if (!fa_dims_ok(B, Hq, Hkv, L, P, G, D) || !fa_view_ok(q, P) || !fa_view_ok(k, P) || !fa_view_ok(v, P) ||
+        !fa_view_ok(out, P) || !fa_view_ok(dout, P) || !fa_view_ok(dq, P) || !fa_view_ok(dk, P) ||
+        !fa_view_ok(dv, P) || !lse || !delta || (!key_mask != !first_valid) || parts <= 0 || parts > 7)
         return SWH_E_ARG;
     FaArgs a{};
-    a.q = static_cast<const uint16_t *>(q);
-    a.k = static_cast<const uint16_t *>(k);
-    a.v = static_cast<const uint16_t *>(v);
-    a.o = static_cast<const uint16_t *>(out);
-    a.dout = static_cast<const uint16_t *>(dout);
+    a.q = fa_view_of(*q);
+    a.k = fa_view_of(*k);
+    a.v = fa_view_of(*v);
+    a.o = fa_view_of(*out);
+    a.dout = fa_view_of(*dout);
+    a.dq = fa_view_of(*dq);
+    a.dk = fa_view_of(*dk);
+    a.dv = fa_view_of(*dv);
     a.key_mask = key_mask;
     a.first_valid = first_valid;
     a.lse = const_cast<float *>(lse);
     a.delta = delta;
-    a.dq = static_cast<uint16_t *>(dq);
-    a.dk = static_cast<uint16_t *>(dk);
-    a.dv = static_cast<uint16_t *>(dv);
     a.B = (int)B;
     a.Hq = Hq;
     a.Hkv = Hkv;
     a.L = (int)L;
+    a.P = (int)P;
+    a.G = G;
     a.scale = scale;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int64_t rows = B * Hq * L;
@@ -601,6 +702,27 @@ extern "C" int swh_attn_bwd_parts(const void *q, const void *k, const void *v, c
         if (parts & SWH_ATTN_BWD_DKDV) fa_dkdv_kernel<128><<<gk, 256, 0, s>>>(a);
     }
     return launch_status();
+}
+
+extern "C" int swh_attn_fwd(const void *q, const void *k, const void *v, int64_t B, int32_t Hq, int32_t Hkv,
+                            int64_t L, int32_t D, float scale, const int32_t *key_mask, const int32_t *first_valid,
+                            void *out, float *lse, void *stream) {
+    if (!q || !k || !v || !out) return SWH_E_ARG;
+    const swh_attn_view vq = fa_plain(q, Hq, L, D), vk = fa_plain(k, Hkv, L, D), vv = fa_plain(v, Hkv, L, D),
+                        vo = fa_plain(out, Hq, L, D);
+    return swh_attn_fwd_v(&vq, &vk, &vv, &vo, B, Hq, Hkv, L, 0, 0, D, scale, key_mask, first_valid, lse, stream);
+}
+
+extern "C" int swh_attn_bwd_parts(const void *q, const void *k, const void *v, const void *out, const void *dout,
+                                  const float *lse, int64_t B, int32_t Hq, int32_t Hkv, int64_t L, int32_t D,
+                                  float scale, const int32_t *key_mask, const int32_t *first_valid, float *delta,
+                                  void *dq, void *dk, void *dv, int32_t parts, void *stream) {
+    if (!q || !k || !v || !out || !dout || !dq || !dk || !dv) return SWH_E_ARG;
+    const swh_attn_view vq = fa_plain(q, Hq, L, D), vk = fa_plain(k, Hkv, L, D), vv = fa_plain(v, Hkv, L, D),
+                        vo = fa_plain(out, Hq, L, D), vd = fa_plain(dout, Hq, L, D), vdq = fa_plain(dq, Hq, L, D),
+                        vdk = fa_plain(dk, Hkv, L, D), vdv = fa_plain(dv, Hkv, L, D);
+    return swh_attn_bwd_v_parts(&vq, &vk, &vv, &vo, &vd, lse, B, Hq, Hkv, L, 0, 0, D, scale, key_mask, first_valid,
+                                delta, &vdq, &vdk, &vdv, parts, stream);
 }
 
 extern "C" int swh_attn_bwd(const void *q, const void *k, const void *v, const void *out, const void *dout,

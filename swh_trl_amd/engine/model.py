@@ -604,20 +604,23 @@ class CausalLM:
         if kv_out is not None:
             kv_out(i, k, v)
         o = self._attend(q, k, v, mask)
-        o = o.transpose(1, 2).reshape(B, L, c.q_dim)
         return self._post_attention(i, x, o)
 
     def _attend(self, q, k, v, mask):
-        """Causal GQA attention over [B, H, L, D] (padding mask as built by hidden_states)."""
+        """Causal GQA attention over [B, H, L, D] (padding mask as built by
+        hidden_states) -> token-major [B, L, Hq D], the o_proj input."""
         c = self.cfg
         D = c.head_dim
+        B, _, L, _ = q.shape
         if self._hip_attn:  # csrc/attn.hip: causal GQA flash attention, padding as transformers
             km, fv = (None, None) if mask is None else mask
-            return nn_ops.AttentionFn.apply(q, k, v, D ** -0.5, km, fv)
+            return nn_ops.AttentionTokFn.apply(q, k, v, D ** -0.5, km, fv)
         gqa = c.num_attention_heads != c.num_key_value_heads  # torch SDPA (aotriton), GQA inside the kernel
         if mask is None:
-            return F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=D ** -0.5, enable_gqa=gqa)
-        return F.scaled_dot_product_attention(q, k, v, attn_mask=mask, scale=D ** -0.5, enable_gqa=gqa)
+            o = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=D ** -0.5, enable_gqa=gqa)
+        else:
+            o = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, scale=D ** -0.5, enable_gqa=gqa)
+        return o.transpose(1, 2).reshape(B, L, c.q_dim)
 
     def _post_attention(self, i, x, o):
         """o-proj, residual + post-attention norm, the SiLU-gated MLP: (x + o, MLP output)."""
@@ -695,15 +698,22 @@ class CausalLM:
                 x, h = _AddRMSNorm.apply(x, d, self.p[f"l{i}.ln_in"], self._gv(f"l{i}.ln_in"), eps)
             qkv = _Linear.apply(h, self.p[f"l{i}.qkv_w"], self.p.get(f"l{i}.qkv_b"), self._gv(f"l{i}.qkv_w"),
                                 self._gv(f"l{i}.qkv_b"))
-            q_p, k_p, v_p = nn_ops.QKVRopeFn.apply(qkv[:NP].view(U, P, -1), pos_p, cos_t, sin_t, Hq, Hkv, D)
-            q_c, k_c, v_c = nn_ops.QKVRopeFn.apply(qkv[NP:].view(R, C, -1), pos_c, cos_t, sin_t, Hq, Hkv, D)
-            q = torch.cat([bcast(q_p), q_c], 2)
-            k = torch.cat([bcast(k_p), k_c], 2)
-            v = torch.cat([bcast(v_p), v_c], 2)
-            o = self._attend(q, k, v, mask)  # [R, Hq, P + C, D]
-            o_p = o.view(U, G, Hq, P + C, D)[:, 0, :, :P]  # the group's prompt rows, once
-            o_c = o[:, :, P:]
-            o = torch.cat([o_p.transpose(1, 2).reshape(NP, c.q_dim), o_c.transpose(1, 2).reshape(R * C, c.q_dim)])
+            if self._hip_attn:
+                # one node for both segments' RoPE; the attention reads the group's prompt
+                # Q/K/V in place and writes the token-major o_proj input (no cat / copies)
+                q_p, k_p, v_p, q_c, k_c, v_c = nn_ops.QKVRopeSegFn.apply(qkv, pos_p, pos_c, cos_t, sin_t, U, P, R,
+                                                                         C, Hq, Hkv, D)
+                km, fv = (None, None) if mask is None else mask
+                o = nn_ops.GroupedAttentionFn.apply(q_p, k_p, v_p, q_c, k_c, v_c, G, D ** -0.5, km, fv)
+            else:
+                q_p, k_p, v_p = nn_ops.QKVRopeFn.apply(qkv[:NP].view(U, P, -1), pos_p, cos_t, sin_t, Hq, Hkv, D)
+                q_c, k_c, v_c = nn_ops.QKVRopeFn.apply(qkv[NP:].view(R, C, -1), pos_c, cos_t, sin_t, Hq, Hkv, D)
+                q = torch.cat([bcast(q_p), q_c], 2)
+                k = torch.cat([bcast(k_p), k_c], 2)
+                v = torch.cat([bcast(v_p), v_c], 2)
+                o = self._attend(q, k, v, mask).view(R, P + C, c.q_dim)
+                o_p = o.view(U, G, P + C, c.q_dim)[:, 0, :P]  # the group's prompt rows, once
+                o = torch.cat([o_p.reshape(NP, c.q_dim), o[:, P:].reshape(R * C, c.q_dim)])
             x, d = self._post_attention(i, x, o)
         _, h = _AddRMSNorm.apply(x, d, self.p["norm"], self._gv("norm"), eps)
         return h[:NP].view(U, P, H)[:, P - 1], h[NP:].view(R, C, H)

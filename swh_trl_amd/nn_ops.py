@@ -336,6 +336,147 @@ class AttentionFn(torch.autograd.Function):
         return dq, dk, dv, None, None, None
 
 
+def attn_view(seg1, seg0=None):
+    """swh_attn_view of an attention operand: seg = (tensor, stride per sequence,
+    per head, per row, divisor) in elements; seg0 holds rows l < P (None: P = 0)."""
+    v = _lib.AttnView()
+    for i, seg in ((0, seg0), (1, seg1)):
+        if seg is None:
+            v.div[i] = 1
+            continue
+        t, sb, sh, sl, div = seg
+        v.base[i] = t.data_ptr()
+        v.sb[i], v.sh[i], v.sl[i], v.div[i] = int(sb), int(sh), int(sl), int(div)
+    return v
+
+
+def _bhld(t):
+    """plain [B, H, L, D] tensor -> its view segment."""
+    _, H, L, D = t.shape
+    return (t, H * L * D, L * D, D, 1)
+
+
+def _attn_bwd(views, lse, dims, scale, km, fv, delta, dviews, dev):
+    """swh_attn_bwd_v_parts, dK/dV on the auxiliary stream beside dQ when one is on."""
+    import ctypes as C
+    B, Hq, Hkv, L, P, G, D = dims
+    vq, vk, vv, vo, vd = (C.byref(x) for x in views)
+    dq, dk, dv = (C.byref(x) for x in dviews)
+    args = (vq, vk, vv, vo, vd, lse.data_ptr(), B, Hq, Hkv, L, P, G, D, float(scale), _p(km), _p(fv),
+            delta.data_ptr(), dq, dk, dv)
+    aux = _aux_stream(dev)
+    if aux is None:
+        call("swh_attn_bwd_v_parts", *args, 7, _stream())
+        return
+    main = torch.cuda.current_stream(dev)
+    call("swh_attn_bwd_v_parts", *args, 1, _stream())
+    aux.wait_stream(main)
+    with torch.cuda.stream(aux):
+        call("swh_attn_bwd_v_parts", *args, 4, _stream())
+    call("swh_attn_bwd_v_parts", *args, 2, _stream())
+    main.wait_stream(aux)
+
+
+class AttentionTokFn(torch.autograd.Function):
+    """AttentionFn with the output token-major, [B, L, Hq D] (the o_proj input
+    as it stands: no transpose copy forward or backward)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, scale: float, key_mask=None, first_valid=None):
+        _dev(q, "attention")
+        B, Hq, L, D = q.shape
+        Hkv = k.shape[1]
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        out = torch.empty(B, L, Hq * D, device=q.device, dtype=q.dtype)
+        lse = torch.empty(B, Hq, L, device=q.device, dtype=torch.float32)
+        vo = attn_view((out, L * Hq * D, D, Hq * D, 1))
+        import ctypes as C
+        call("swh_attn_fwd_v", *(C.byref(x) for x in (attn_view(_bhld(q)), attn_view(_bhld(k)),
+                                                    attn_view(_bhld(v)), vo)),
+             B, Hq, Hkv, L, 0, 0, D, float(scale), _p(key_mask), _p(first_valid), lse.data_ptr(), _stream())
+        ctx.save_for_backward(q, k, v, out, lse)
+        ctx.km, ctx.fv, ctx.scale = key_mask, first_valid, float(scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, out, lse = ctx.saved_tensors
+        B, Hq, L, D = q.shape
+        Hkv = k.shape[1]
+        dout = dout.contiguous()
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        delta = torch.empty(B, Hq, L, device=q.device, dtype=torch.float32)
+        tok = lambda t: attn_view((t, L * Hq * D, D, Hq * D, 1))  # noqa: E731
+        views = (attn_view(_bhld(q)), attn_view(_bhld(k)), attn_view(_bhld(v)), tok(out), tok(dout))
+        _attn_bwd(views, lse, (B, Hq, Hkv, L, 0, 0, D), ctx.scale, ctx.km, ctx.fv, delta,
+                  (attn_view(_bhld(dq)), attn_view(_bhld(dk)), attn_view(_bhld(dv))), q.device)
+        return dq, dk, dv, None, None, None
+
+
+class GroupedAttentionFn(torch.autograd.Function):
+    """Causal GQA attention of R = U G sequences whose first P positions are the
+    prompt of their group (G consecutive sequences share it) — the GRPO
+    shared-prompt forward (engine/model.py hidden_states_grouped).  The group's
+    prompt q_p / k_p / v_p [U, H, P, D] are read by all G sequences in place,
+    each sequence's completion q_c / k_c / v_c [R, H, C, D] are its own; the
+    prompt queries are computed once per group (the group's first sequence).
+    Output token-major [U P + R C, Hq D]: the groups' prompt tokens, then every
+    sequence's completion tokens (the o_proj input).  Backward: d prompt Q from
+    the first sequence, d prompt K / V summed over the group's sequences in
+    fixed order; no concatenated copies either way (swh_attn_fwd_v / _bwd_v_parts)."""
+
+    @staticmethod
+    def forward(ctx, q_p, k_p, v_p, q_c, k_c, v_c, G: int, scale: float, key_mask=None, first_valid=None):
+        _dev(q_c, "attention")
+        import ctypes as C
+        U, Hq, P, D = q_p.shape
+        R, Hkv, Cn = k_c.shape[0], k_c.shape[1], k_c.shape[2]
+        L = P + Cn
+        q_p, k_p, v_p, q_c, k_c, v_c = (t.contiguous() for t in (q_p, k_p, v_p, q_c, k_c, v_c))
+        NP = U * P
+        out = torch.empty(NP + R * Cn, Hq * D, device=q_c.device, dtype=q_c.dtype)
+        lse = torch.empty(R, Hq, L, device=q_c.device, dtype=torch.float32)
+        ctx.views = GroupedAttentionFn._views(q_p, k_p, v_p, q_c, k_c, v_c, out, G)
+        call("swh_attn_fwd_v", *(C.byref(x) for x in ctx.views), R, Hq, Hkv, L, P, G, D, float(scale),
+             _p(key_mask), _p(first_valid), lse.data_ptr(), _stream())
+        ctx.save_for_backward(q_p, k_p, v_p, q_c, k_c, v_c, out, lse)
+        ctx.km, ctx.fv, ctx.scale, ctx.G = key_mask, first_valid, float(scale), G
+        return out
+
+    @staticmethod
+    def _views(q_p, k_p, v_p, q_c, k_c, v_c, out, G):
+        U, Hq, P, D = q_p.shape
+        Cn = q_c.shape[2]
+
+        def seg(tp, tc):
+            return attn_view(_bhld(tc), (tp, tp.shape[1] * P * D, P * D, D, G))
+        vo = attn_view((out[U * P:], Cn * Hq * D, D, Hq * D, 1), (out, P * Hq * D, D, Hq * D, G))
+        return seg(q_p, q_c), seg(k_p, k_c), seg(v_p, v_c), vo
+
+    @staticmethod
+    def backward(ctx, dout):
+        q_p, k_p, v_p, q_c, k_c, v_c, out, lse = ctx.saved_tensors
+        U, Hq, P, D = q_p.shape
+        R, Hkv, Cn = k_c.shape[0], k_c.shape[1], k_c.shape[2]
+        G, L = ctx.G, P + Cn
+        dout = dout.contiguous()
+        vq, vk, vv, vo = GroupedAttentionFn._views(q_p, k_p, v_p, q_c, k_c, v_c, out, G)
+        vd = attn_view((dout[U * P:], Cn * Hq * D, D, Hq * D, 1), (dout, P * Hq * D, D, Hq * D, G))
+        dq_p, dq_c = torch.empty_like(q_p), torch.empty_like(q_c)
+        dk_c, dv_c = torch.empty_like(k_c), torch.empty_like(v_c)
+        dk_r = torch.empty(R, Hkv, P, D, device=q_c.device, dtype=q_c.dtype)  # per sequence: summed below
+        dv_r = torch.empty_like(dk_r)
+        vdq = attn_view(_bhld(dq_c), (dq_p, Hq * P * D, P * D, D, G))
+        vdk = attn_view(_bhld(dk_c), _bhld(dk_r))
+        vdv = attn_view(_bhld(dv_c), _bhld(dv_r))
+        delta = torch.empty(R, Hq, L, device=q_c.device, dtype=torch.float32)
+        _attn_bwd((vq, vk, vv, vo, vd), lse, (R, Hq, Hkv, L, P, G, D), ctx.scale, ctx.km, ctx.fv, delta,
+                  (vdq, vdk, vdv), q_c.device)
+        dk_p = dk_r.view(U, G, Hkv, P, D).sum(1)
+        dv_p = dv_r.view(U, G, Hkv, P, D).sum(1)
+        return dq_p, dk_p, dv_p, dq_c, dk_c, dv_c, None, None, None, None
+
+
 _AUX_STREAMS: dict = {}
 
 
@@ -353,6 +494,48 @@ def _aux_stream(dev: torch.device):
 
 def attention_supported(D: int) -> bool:
     return D in (64, 128)
+
+
+class QKVRopeSegFn(torch.autograd.Function):
+    """QKVRopeFn over the two token segments of the shared-prompt forward in one
+    node: qkv [U P + R C, (Hq+2Hkv) D] -> (q, k, v of the U prompts [U, H, P, D],
+    of the R completions [R, H, C, D]); the backward writes both parts of
+    d qkv into one buffer (no zero fill, copy and add of two slice gradients)."""
+
+    @staticmethod
+    def forward(ctx, qkv, pos_p, pos_c, cos, sin, U: int, P: int, R: int, C: int, Hq: int, Hkv: int, D: int):
+        _dev(qkv, "qkv_rope")
+        qkv_c = qkv.contiguous()
+        NP = U * P
+        outs = []
+        pp = pos_p.reshape(-1).to(torch.int64).contiguous()
+        pc = pos_c.reshape(-1).to(torch.int64).contiguous()
+        for (B, L, pos, x) in ((U, P, pp, qkv_c[:NP]), (R, C, pc, qkv_c[NP:])):
+            q = torch.empty(B, Hq, L, D, device=qkv.device, dtype=qkv.dtype)
+            k = torch.empty(B, Hkv, L, D, device=qkv.device, dtype=qkv.dtype)
+            v = torch.empty(B, Hkv, L, D, device=qkv.device, dtype=qkv.dtype)
+            call("swh_qkv_rope", x.data_ptr(), pos.data_ptr(), cos.data_ptr(), sin.data_ptr(), B, L, Hq, Hkv, D,
+                 q.data_ptr(), k.data_ptr(), v.data_ptr(), 0, _dtype_code(qkv_c, "qkv_rope"), _stream())
+            outs += [q, k, v]
+        ctx.save_for_backward(pp, pc, cos, sin)
+        ctx.dims = (U, P, R, C, Hq, Hkv, D)
+        ctx.dtype = qkv.dtype
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, dq_p, dk_p, dv_p, dq_c, dk_c, dv_c):
+        pp, pc, cos, sin = ctx.saved_tensors
+        U, P, R, C, Hq, Hkv, D = ctx.dims
+        dt = ctx.dtype
+        NP = U * P
+        dqkv = torch.empty(NP + R * C, (Hq + 2 * Hkv) * D, device=pp.device, dtype=dt)
+        for (B, L, pos, x, grads) in ((U, P, pp, dqkv[:NP], (dq_p, dk_p, dv_p)),
+                                      (R, C, pc, dqkv[NP:], (dq_c, dk_c, dv_c))):
+            dq, dk, dv = (torch.zeros(B, H, L, D, device=pp.device, dtype=dt) if t is None else t.contiguous()
+                          for t, H in zip(grads, (Hq, Hkv, Hkv)))
+            call("swh_qkv_rope", x.data_ptr(), pos.data_ptr(), cos.data_ptr(), sin.data_ptr(), B, L, Hq, Hkv, D,
+                 dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), 1, _dtype_code(dq, "qkv_rope"), _stream())
+        return dqkv, None, None, None, None, None, None, None, None, None, None, None
 
 
 class QKVRopeFn(torch.autograd.Function):

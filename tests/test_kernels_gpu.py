@@ -1380,6 +1380,87 @@ def test_attention_fwd_bwd_matches_reference(ops, dev, B, Hq, Hkv, L, D, pad):
         assert err <= 3e-2 * max(1.0, r.abs().max().item()), err
 
 
+@pytest.mark.parametrize("pad", [False, True])
+def test_attention_token_major_equals_plain(ops, dev, pad):
+    """AttentionTokFn (swh_attn_fwd_v / _bwd_v_parts, output token-major) is
+    AttentionFn's output transposed, and the same dq / dk / dv, bit for bit."""
+    from swh_trl_amd import nn_ops
+    g = _gen(71)
+    B, Hq, Hkv, L, D = 3, 14, 2, 150, 64
+    q = torch.randn(B, Hq, L, D, generator=g).to(torch.bfloat16).to(dev)
+    k = torch.randn(B, Hkv, L, D, generator=g).to(torch.bfloat16).to(dev)
+    v = torch.randn(B, Hkv, L, D, generator=g).to(torch.bfloat16).to(dev)
+    do = torch.randn(B, Hq, L, D, generator=g).to(torch.bfloat16).to(dev)
+    km = fv = None
+    if pad:
+        km = torch.ones(B, L, dtype=torch.int32)
+        km[1, :17] = 0
+        km = km.to(dev)
+        fv = (km.cumsum(-1) == 0).sum(-1).to(torch.int32)
+    res = []
+    for fn in (nn_ops.AttentionFn, nn_ops.AttentionTokFn):
+        qa, ka, va = (t.clone().requires_grad_(True) for t in (q, k, v))
+        o = fn.apply(qa, ka, va, D ** -0.5, km, fv)
+        if fn is nn_ops.AttentionTokFn:
+            o.backward(do.transpose(1, 2).reshape(B, L, Hq * D))
+            o = o.view(B, L, Hq, D).transpose(1, 2)
+        else:
+            o.backward(do)
+        res.append((o, qa.grad, ka.grad, va.grad))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("P,C,G,pad", [(128, 256, 8, False), (128, 96, 4, True), (41, 30, 3, True)])
+def test_grouped_attention_equals_concatenated(ops, dev, P, C, G, pad):
+    """GroupedAttentionFn (each group's prompt Q/K/V read in place by its G
+    sequences, prompt queries computed once, output token-major) against the
+    concatenated form the shared-prompt forward used before: AttentionFn over
+    cat(broadcast prompt, completion), the group's first prompt rows and every
+    completion row taken from its output, gradients through the same cat /
+    broadcast autograd.  Output, d prompt Q and completion gradients bit for
+    bit; d prompt K / V (summed over the group) bit for bit when P is a
+    multiple of 64 (the dK/dV query rounds align), else to fp32 rounding."""
+    from swh_trl_amd import nn_ops
+    g = _gen(72 + P)
+    U, Hq, Hkv, D = 2, 14, 2, 64
+    R, L = U * G, P + C
+    bf = dict(dtype=torch.bfloat16)
+    t = lambda *sh: torch.randn(*sh, generator=g).to(**bf).to(dev)  # noqa: E731
+    q_p, k_p, v_p = t(U, Hq, P, D), t(U, Hkv, P, D), t(U, Hkv, P, D)
+    q_c, k_c, v_c = t(R, Hq, C, D), t(R, Hkv, C, D), t(R, Hkv, C, D)
+    do = t(U * P + R * C, Hq * D)
+    km = fv = None
+    if pad:
+        kmu = torch.ones(U, P, dtype=torch.int32)
+        kmu[1, :P // 3] = 0
+        km = torch.cat([kmu.repeat_interleave(G, 0), torch.ones(R, C, dtype=torch.int32)], 1).to(dev)
+        fv = (km.cumsum(-1) == 0).sum(-1).to(torch.int32)
+
+    def bc(x):
+        return x[:, None].expand(U, G, *x.shape[1:]).reshape(R, *x.shape[1:])
+
+    ins1 = [x.clone().requires_grad_(True) for x in (q_p, k_p, v_p, q_c, k_c, v_c)]
+    o1 = nn_ops.GroupedAttentionFn.apply(*ins1, G, D ** -0.5, km, fv)
+    o1.backward(do)
+    ins2 = [x.clone().requires_grad_(True) for x in (q_p, k_p, v_p, q_c, k_c, v_c)]
+    q = torch.cat([bc(ins2[0]), ins2[3]], 2)
+    k = torch.cat([bc(ins2[1]), ins2[4]], 2)
+    v = torch.cat([bc(ins2[2]), ins2[5]], 2)
+    o = nn_ops.AttentionFn.apply(q, k, v, D ** -0.5, km, fv).transpose(1, 2).reshape(R, L, Hq * D)
+    o2 = torch.cat([o.view(U, G, L, -1)[:, 0, :P].reshape(U * P, -1), o[:, P:].reshape(R * C, -1)])
+    o2.backward(do)
+    assert torch.equal(o1, o2)
+    for i in (0, 3, 4, 5):
+        assert torch.equal(ins1[i].grad, ins2[i].grad), i
+    for i in (1, 2):
+        a, b = ins1[i].grad.float(), ins2[i].grad.float()
+        if P % 64 == 0:
+            assert torch.equal(a, b), i
+        else:
+            torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-2 * b.abs().max().item())
+
+
 @pytest.mark.parametrize("name,M,N,K", [("qkv_bias", 64, 6144, 4096), ("o_res", 8, 4096, 4096),
                                         ("gate_up", 33, 14336, 4096), ("down", 64, 4096, 14336),
                                         ("down_tiny_llama", 6, 1024, 2048), ("lm_head", 64, 128256, 4096)])

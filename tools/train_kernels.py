@@ -21,6 +21,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--layers", type=int, default=None)
+    ap.add_argument("--torch-prof", action="store_true",
+                    help="torch.profiler over one step: aten ops by device time, grouped by input shape")
     args = ap.parse_args()
     from swh_trl_amd import profiling
     from swh_trl_amd.engine.config import qwen2_5_0_5b
@@ -50,7 +52,9 @@ def main():
         sl = slice(j * MB, (j + 1) * MB)
         micro.append({"prompt_ids": prompt[sl], "prompt_mask": torch.ones(MB, P, dtype=torch.int32, device=dev),
                       "completion_ids": comp[sl], "completion_mask": torch.ones(MB, C, dtype=torch.int32, device=dev),
-                      "advantages": adv[sl]})
+                      "advantages": adv[sl],
+                      # generation-order group ids (as the rollout records them): the shared-prompt forward
+                      "prompt_group": torch.arange(B, device=dev)[sl] // G})
 
     def step():
         tr.model.zero_grad()
@@ -59,6 +63,15 @@ def main():
 
     step()
     torch.cuda.synchronize()
+    if args.torch_prof:
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+            step()
+            torch.cuda.synchronize()
+        ka = prof.key_averages(group_by_input_shape=True)
+        print(ka.table(sort_by="self_device_time_total", row_limit=70, max_name_column_width=40,
+                       max_shapes_column_width=90), flush=True)
+        return
     profiling.reset()
     profiling.enable(True)
     t0 = time.perf_counter()
