@@ -543,6 +543,15 @@ int swh_lm_head_sample_step_fragw(const void *x, const void *w, int64_t M, int64
                                   int64_t *cur_tokens, const void *embed, void *x_next, float *ss_next,
                                   void *workspace, int64_t workspace_bytes, void *stream);
 
+/* Infinity Cache warm-up: nwg workgroups read every byte of the njobs ranges
+ * jobs[j] = {const void *ptr, int64_t bytes / 16} (device memory, 16-B aligned)
+ * and keep nothing but a sink word (>= nwg * 256 uint32 of scratch, written
+ * only if an XOR of the data equals a magic constant).  Captured on a side
+ * branch of the decode graph to pull layer l+1's decode weights on-die while
+ * layer l runs (the per-token weight stream, grpo_trainer.py:1804's
+ * model.generate, exceeds the 256 MiB Infinity Cache).  nontemporal: nt loads. */
+int swh_l3_prefetch(const void *jobs, int32_t njobs, int32_t nwg, int32_t nontemporal, void *sink, void *stream);
+
 /* ---- GPT-2 family (BASELINE.json config 1) --------------------------------
  * transformers GPT2Block's LayerNorms and NewGELUActivation (the modeling code
  * the reference's tiny-random-GPT2 tests run through grpo_trainer.py:1249 /

@@ -195,6 +195,15 @@ class DecodeEngine:
         # the attention launch warms the gate/up weights into the consuming XCDs' L2:
         # gate/up gains what the longer attention launch loses, off
         self.prefetch = os.environ.get("SWH_DECODE_PREFETCH", "0") != "0"
+        # Infinity Cache warm-up (swh_l3_prefetch): a side branch of the decode graph
+        # reads layer l+1's decode weights while layer l runs (the step's ~1 GB weight
+        # stream misses the 256 MiB cache otherwise); SWH_DECODE_L3_PREFETCH = workgroups
+        # (0: off), SWH_DECODE_L3_AT = the op of layer l it starts beside (0 qkv, 1 attention,
+        # 2 gate/up), SWH_DECODE_L3_NT=1 nt loads
+        self.l3_nwg = int(os.environ.get("SWH_DECODE_L3_PREFETCH", "0")) if self.fused else 0
+        self.l3_at = int(os.environ.get("SWH_DECODE_L3_AT", "0"))
+        self.l3_nt = int(os.environ.get("SWH_DECODE_L3_NT", "0"))
+        self._l3_jobs = None
         self._exit_poll = EarlyExitPoll(self.finished)
         self.steps_run = 0  # decode steps the last generate() ran (early exit: fewer than max_new_tokens - 1)
 
@@ -306,15 +315,53 @@ class DecodeEngine:
         w, nw = self._normed(name, norm)
         return nn_ops.decode_gemm(x, w, norm_w=nw, eps=eps, **kw)
 
+    def _proj_weight(self, name: str) -> torch.Tensor:
+        """The buffer _proj streams for a projection."""
+        if name in self.packed:
+            return self.packed[name]
+        if name in self.fragw:
+            return self.fragw[name]
+        norm = self._projections()[name][3]
+        return self._weight(name) if norm is None else self._normed(name, norm)[0]
+
+    def _l3_tables(self):
+        """Per layer, a device table of {ptr, bytes/16} over its decode weights."""
+        if self._l3_jobs is None:
+            tabs = []
+            for i in range(self.cfg.num_hidden_layers):
+                t = []
+                for n in ("qkv_w", "o_w", "gu_w", "down_w"):
+                    w = self._proj_weight(f"l{i}.{n}")
+                    t += [w.data_ptr(), w.numel() * w.element_size() // 16]
+                tabs.append(torch.tensor(t, dtype=torch.int64).to(self.dev))
+            self._l3_jobs = tabs
+            self._l3_sink = torch.zeros(self.l3_nwg * 256, dtype=torch.int32, device=self.dev)
+            self._l3_side = torch.cuda.Stream()
+        return self._l3_jobs
+
+    def _l3_prefetch(self, layer: int):
+        """Fork the warm-up of `layer`'s weights onto the side stream."""
+        jobs = self._l3_tables()
+        self._l3_side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self._l3_side):
+            call("swh_l3_prefetch", jobs[layer].data_ptr(), 4, self.l3_nwg, self.l3_nt, self._l3_sink.data_ptr(),
+                 ops._stream())
+
     def _step_fused(self):
         c, m = self.cfg, self.model
         p = m.p
         eps = c.rms_norm_eps
         ss = self.ss  # every producer of s writes its RMSNorm partial sums, every normed GEMM reads them
+        L = c.num_hidden_layers
+        l3 = self.l3_nwg > 0
         if not self._chained():
             nn_ops.embed_gather(p["embed"], self.cur, self.s, ss_out=ss)
-        for i in range(c.num_hidden_layers):
+        for i in range(L):
+            if l3 and self.l3_at == 0 and i + 1 < L:
+                self._l3_prefetch(i + 1)
             self._proj(f"l{i}.qkv_w", self.s, bias=p.get(f"l{i}.qkv_b"), y=self.qkv, ss_in=ss)
+            if l3 and self.l3_at == 1 and i + 1 < L:
+                self._l3_prefetch(i + 1)
             pf = self._normed(f"l{i}.gu_w", f"l{i}.ln_post")[0] if self.prefetch and f"l{i}.gu_w" not in \
                 self.packed and f"l{i}.gu_w" not in self.fragw else None
             nn_ops.attn_decode(self.qkv, self.kv[i, 0], self.kv[i, 1], self.cos, self.sin, self.plen, self.state,
@@ -324,8 +371,12 @@ class DecodeEngine:
                 self._proj(f"l{i}.o_w", self.att, residual=self.s, ss_out=ss, act_frag=2)
             else:
                 self._proj(f"l{i}.o_w", self.att, residual=self.s, ss_out=ss)
+            if l3 and self.l3_at == 2 and i + 1 < L:
+                self._l3_prefetch(i + 1)
             self._proj(f"l{i}.gu_w", self.s, silu=True, y=self.act, ss_in=ss)
             self._proj(f"l{i}.down_w", self.act, residual=self.s, ss_out=ss)
+        if l3:
+            torch.cuda.current_stream().wait_stream(self._l3_side)
         if self._fused_sample():
             w, nw, fr = self._lm_head_weight()
             nn_ops.lm_head_sample_step(self.s, w, self.params, self.rng, self.state[0:1], self.finished,

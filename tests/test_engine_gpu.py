@@ -892,3 +892,42 @@ def test_generation_is_run_to_run_deterministic(dev):
                 h.update(lp.cpu().numpy().tobytes())
             hs.add(h.hexdigest())
         assert len(hs) == 1, (kw, hs)
+
+
+def test_l3_prefetch_branch_generates_identically(dev, monkeypatch):
+    """The decode graph with the Infinity Cache warm-up branch (swh_l3_prefetch
+    on a side stream, layer l+1's weights read while layer l runs) generates the
+    same tokens and log-probs as without it, and the kernel leaves the ranges it
+    reads unchanged."""
+    from swh_trl_amd import _lib
+    from swh_trl_amd.engine import CausalLM, DecodeEngine, tiny_qwen2
+    m = CausalLM(tiny_qwen2(1024, 3), dev, seed=6)
+    g = torch.Generator().manual_seed(6)
+    B, P, C = 32, 12, 20
+    ids = torch.randint(0, m.cfg.vocab_size, (B, P), generator=g).to(dev)
+    mask = torch.ones(B, P, dtype=torch.int64, device=dev)
+    mask[3, :2] = 0
+    outs = {}
+    for nwg, at in (("64", "0"), ("32", "1"), ("0", "0")):
+        monkeypatch.setenv("SWH_DECODE_L3_PREFETCH", nwg)
+        monkeypatch.setenv("SWH_DECODE_L3_AT", at)
+        eng = DecodeEngine(m, B, P, C)
+        assert eng.l3_nwg == int(nwg)
+        outs[nwg] = (eng.generate(ids, mask, C, greedy=True),
+                     eng.generate(ids, mask, C, temperature=0.9, seed=3, return_logp=True))
+        del eng
+    for k in ("64", "32"):
+        for a, b in zip(outs[k], outs["0"]):
+            for x, y in zip(a, b):
+                if isinstance(x, torch.Tensor):
+                    assert torch.equal(x, y)
+    # the kernel itself: odd sizes, several ranges, read-only
+    bufs = [torch.randint(-1000, 1000, (n,), dtype=torch.int32, device=dev) for n in (4, 4 * 1037, 4 * 70001)]
+    ref = [b.clone() for b in bufs]
+    tab = torch.tensor(sum([[b.data_ptr(), b.numel() * 4 // 16] for b in bufs], []), dtype=torch.int64).to(dev)
+    sink = torch.zeros(128 * 256, dtype=torch.int32, device=dev)
+    for nt in (0, 1):
+        assert _lib.load().swh_l3_prefetch(tab.data_ptr(), 3, 128, nt, sink.data_ptr(),
+                                           torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(bufs, ref))
