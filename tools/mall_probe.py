@@ -58,6 +58,7 @@ def main():
                                                    **af(2)),
     }
     print({k: len(v) for k, v in W.items()}, flush=True)
+    steps_only = "--steps-only" in sys.argv
     stream = torch.cuda.current_stream()
 
     def timed(fn, n, cycle, iters=5):
@@ -79,7 +80,7 @@ def main():
     # a 1 GB sweep between the graphs evicts the Infinity Cache
     flush = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
     print(f"{'kernel':10s} " + " ".join(f"{'c=' + str(c):>8s}" for c in ("all", 12, 6, 4, 2, 1)), flush=True)
-    for name, fn in ops_.items():
+    for name, fn in ([] if steps_only else ops_.items()):
         row = []
         for c in (len(W[{"qkv": "qkv_w", "o": "o_w", "gate_up": "gu_w", "down": "down_w"}[name]]), 12, 6, 4, 2, 1):
             flush.add_(1)
@@ -96,7 +97,7 @@ def main():
         ops_["gate_up"](i)
         ops_["down"](i)
 
-    for c in (24, 6, 4, 2):
+    for c in (() if steps_only else (24, 6, 4, 2)):
         flush.add_(1)
         print(f"layer chain cycling {c:2d} layers: {timed(layer, 48, c):8.2f} us per layer", flush=True)
     del W
@@ -109,8 +110,11 @@ def main():
         eng.state[0] = 100
         return timed(lambda i: eng._step_fused(), 4, 1, iters=6)
 
-    for nwg, at, nt in ((0, 0, 0), (32, 0, 0), (64, 0, 0), (128, 0, 0), (0, 0, 0), (64, 1, 0), (64, 2, 0),
-                        (64, 0, 1), (128, 1, 0), (256, 1, 0), (0, 0, 0)):
+    grid = ((0, 0, 0), (32, 0, 0), (64, 0, 0), (128, 0, 0), (0, 0, 0), (64, 1, 0), (64, 2, 0), (64, 0, 1), (128, 1, 0),
+            (256, 1, 0), (0, 0, 0))
+    if steps_only:
+        grid = ((0, 0, 0), (32, 0, 0), (128, 1, 0), (0, 0, 0))
+    for nwg, at, nt in grid:
         print(f"decode step  l3 nwg {nwg:3d} at {at} nt {nt}: {step_us(nwg, at, nt):8.1f} us", flush=True)
 
 
