@@ -543,6 +543,26 @@ int swh_lm_head_sample_step_fragw(const void *x, const void *w, int64_t M, int64
                                   int64_t *cur_tokens, const void *embed, void *x_next, float *ss_next,
                                   void *workspace, int64_t workspace_bytes, void *stream);
 
+/* swh_decode_gemm_fragw with l3_wgs Infinity Cache warm-up workgroups appended
+ * to its launch when the shape runs register-streamed (the decode qkv / o / down
+ * projections; other geometries ignore them): they read the l3_njobs (<= 8)
+ * ranges {const void *ptr, int64_t bytes / 16} on the CUs the projection's tiles
+ * leave idle; l3_sink >= l3_wgs x 512 uint32.  Results identical. */
+int swh_decode_gemm_fragw_l3(const void *x, const void *w, int64_t M, int64_t N, int64_t K, float eps,
+                             const void *bias, void *residual, int32_t silu, void *y, int64_t ldy, const float *ss_in,
+                             float *ss_out, int32_t act_frag, const void *l3_jobs, int32_t l3_njobs, int32_t l3_wgs,
+                             void *l3_sink, void *workspace, int64_t workspace_bytes, void *stream);
+/* swh_attn_decode_shared_frag whose launch also carries >= l3_wgs Infinity Cache
+ * warm-up workgroups (rounded up to whole grid rows of Hkv) on the CUs the
+ * attention's B x Hkv workgroups leave idle: they read the l3_njobs (<= 8)
+ * ranges {const void *ptr, int64_t bytes / 16} and discard the data, so the
+ * projections that follow (o_proj and down_proj of this layer, qkv of the next)
+ * find their weights on-die; l3_sink >= rounded workgroups x 512 uint32 of
+ * scratch.  Results identical to swh_attn_decode_shared_frag. */
+int swh_attn_decode_l3(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos, const float *rope_sin,
+                       const int32_t *prompt_len, const int32_t *prompt_row, const int32_t *state, int64_t B,
+                       int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax, float scale, void *out, int32_t out_frag,
+                       const void *l3_jobs, int32_t l3_njobs, int32_t l3_wgs, void *l3_sink, void *stream);
 /* Infinity Cache warm-up: nwg workgroups read every byte of the njobs ranges
  * jobs[j] = {const void *ptr, int64_t bytes / 16} (device memory, 16-B aligned)
  * and keep nothing but a sink word (>= nwg * 256 uint32 of scratch, written

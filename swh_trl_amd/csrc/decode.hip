@@ -574,6 +574,51 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
     SWH_GEMM_TRACE(6);
 }
 
+// Infinity Cache warm-up job: a device range read (and discarded) by warm-up workgroups
+struct L3Job {
+    const uint4 *p;
+    int64_t n16;  // 16-B units
+};
+constexpr int kL3MaxJobs = 8;
+
+// warm-up workgroups appended to a launch: blocks >= gx0 read one share of the jobs
+struct L3Warm {
+    const L3Job *jobs = nullptr;
+    int njobs = 0;
+    int gx0 = 0;               // the launch's own blocks (the rest warm)
+    uint32_t *sink = nullptr;  // >= warm-up blocks x NT words, written never in practice
+};
+
+// warm-up workgroup p of npf (NT threads): a contiguous share of the jobs' bytes,
+// 8 x 16-B loads in flight per thread, XOR-ed into a word stored only if it
+// equals a magic constant
+template <int NT>
+__device__ __forceinline__ void l3_warm_share(const L3Job *__restrict__ jobs, int njobs, int p, int npf,
+                                              uint32_t *__restrict__ sink) {
+    const int tid = threadIdx.x;
+    int64_t tot = 0;
+    for (int j = 0; j < njobs; ++j) tot += jobs[j].n16;
+    const int64_t share = (tot + npf - 1) / npf, lo = (int64_t)p * share, hi = min(tot, lo + share);
+    uint32_t acc = 0;
+    int64_t base = 0;
+    for (int j = 0; j < njobs; ++j) {
+        const int64_t n = jobs[j].n16, a = max(lo - base, (int64_t)0), e = min(hi - base, n);
+        const uint4 *src = jobs[j].p;
+        for (int64_t i = a + tid; i < e; i += 8 * NT) {
+            uint4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t q = i + u * NT;
+                v[u] = q < e ? src[q] : uint4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+        }
+        base += n;
+    }
+    if (acc == 0x9e3779b9u) sink[(int64_t)p * NT + tid] = acc;
+}
+
 // ---------------------------------------------------------------------------
 // Register-streamed short-K projection (decode qkv and o_proj at K <= 2048:
 // 16 MS-row x 16-column tiles over the full K, no K split): decode_gemm_kernel
@@ -594,8 +639,13 @@ __global__ __launch_bounds__(512) void xstream_gemm_kernel(const uint16_t *__res
                                                            float eps, const float *__restrict__ ss_in,
                                                            const uint16_t *__restrict__ bias,
                                                            uint16_t *__restrict__ res, float *__restrict__ ss_out,
-                                                           uint16_t *__restrict__ y, int ldy, int fw, int xf) {
+                                                           uint16_t *__restrict__ y, int ldy, int fw, int xf,
+                                                           L3Warm warm) {
     static_assert(EPI != EPI_SILU && NM != 1, "plain / residual epilogues, folded or no norm");
+    if (warm.jobs && (int)blockIdx.x >= warm.gx0) {  // Infinity Cache warm-up blocks past the tiles
+        l3_warm_share<512>(warm.jobs, warm.njobs, blockIdx.x - warm.gx0, gridDim.x - warm.gx0, warm.sink);
+        return;
+    }
     constexpr int NW = 8, NT = 512, MR = 16 * MS, NB = 16, LDR = MR + 4, G8 = NB / 8, F = NW;
     __shared__ __attribute__((aligned(16))) float part[(NW + 1) * NB * LDR];
     __shared__ float rstd_s[MR];
@@ -1236,6 +1286,10 @@ struct AttnPrefetch {
     int rows;              // attention rows (B): grid rows past it prefetch
     const int32_t *prow;   // [B] row whose cache holds this row's prompt keys / values, or null (own row)
     int ofrag = 0;         // output in the fragment order o_proj's register-streamed A operand reads (B % 16 == 0)
+    const L3Job *jobs = nullptr;  // Infinity Cache warm-up ranges (grid rows past `rows` read them), or null
+    int njobs = 0;
+    uint32_t *sink = nullptr;     // >= warm-up workgroups x 512 words, written never in practice
+    int nwg = 0;                  // warm-up workgroups wanted (rounded up to whole grid rows)
 };
 
 // element (row b, column c) of a [B, K] activation in the fragment order of
@@ -1269,6 +1323,11 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int g = lane >> 4, c16 = lane & 15;
     SWH_GEMM_TRACE(0);  // phase stamps for tools/attn_probe.py (instrumented build only)
+    if ((int)blockIdx.y >= pf.rows && pf.jobs) {  // an Infinity Cache warm-up workgroup
+        l3_warm_share<kAttnThreads>(pf.jobs, pf.njobs, (blockIdx.y - pf.rows) * gridDim.x + blockIdx.x,
+                                    (gridDim.y - pf.rows) * gridDim.x, pf.sink);
+        return;
+    }
     if ((int)blockIdx.y >= pf.rows) {  // a prefetch workgroup
         const int lin = blockIdx.y * gridDim.x + blockIdx.x, p = lin - pf.rows * gridDim.x;
         const int npf = (gridDim.y - pf.rows) * gridDim.x / 8 * 8;  // whole groups of 8: every XCD covered
@@ -1498,7 +1557,10 @@ int launch_attn(const uint16_t *q, uint16_t *kc, uint16_t *vc, const float *rc, 
                 const AttnPrefetch &pf) {
     // prefetch rows: about as many workgroups as the attention itself has, in groups of 8
     int64_t extra = 0;
-    if (pf.w) {
+    if (pf.jobs) {
+        extra = (pf.nwg + Hkv - 1) / Hkv;
+        if (B + extra > 65535) extra = 0;
+    } else if (pf.w) {
         static const int mult = getenv("SWH_PF_MULT") ? atoi(getenv("SWH_PF_MULT")) : 2;  // 1-3 measured
         const int64_t want = (mult * B * Hkv + 7) / 8 * 8;
         extra = (want + Hkv - 1) / Hkv;
@@ -1679,24 +1741,32 @@ int launch_gemm(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const ui
 template <int KW, int MS, int NM, int EPI, bool BIAS>
 int launch_xstream_kw(const GemmCfg &c, hipStream_t s, const uint16_t *X, const uint16_t *W, int m, int n, int k,
                       float eps, const float *ss_in, const uint16_t *Bs, uint16_t *R, float *ss_out, uint16_t *Y,
-                      int ld) {
-    xstream_gemm_kernel<KW, MS, NM, EPI, BIAS, 0><<<dim3((unsigned)c.gx), 512, 0, s>>>(X, W, m, n, k, eps, ss_in, Bs, R,
-                                                                                   ss_out, Y, ld, c.fw, c.xf);
+                      int ld, const L3Warm *warm) {
+    L3Warm wm;
+    int gx = c.gx;
+    if (warm && warm->jobs) {
+        wm = *warm;
+        wm.gx0 = c.gx;
+        gx += warm->gx0;  // (the caller passes the warm-up block count in gx0)
+    }
+    xstream_gemm_kernel<KW, MS, NM, EPI, BIAS, 0><<<dim3((unsigned)gx), 512, 0, s>>>(X, W, m, n, k, eps, ss_in, Bs, R,
+                                                                                 ss_out, Y, ld, c.fw, c.xf, wm);
     return launch_status();
 }
 
 template <int MS, int NM, int EPI, bool BIAS>
 int launch_xstream_ms(const GemmCfg &c, hipStream_t s, const uint16_t *X, const uint16_t *W, int m, int n, int k,
                       float eps, const float *ss_in, const uint16_t *Bs, uint16_t *R, float *ss_out, uint16_t *Y,
-                      int ld) {
+                      int ld, const L3Warm *warm) {
     const int ks = k / 32, kwn = (ks + 7) / 8;
-    if (kwn <= 2) return launch_xstream_kw<2, MS, NM, EPI, BIAS>(c, s, X, W, m, n, k, eps, ss_in, Bs, R, ss_out, Y, ld);
-    if (kwn <= 4) return launch_xstream_kw<4, MS, NM, EPI, BIAS>(c, s, X, W, m, n, k, eps, ss_in, Bs, R, ss_out, Y, ld);
-    return launch_xstream_kw<8, MS, NM, EPI, BIAS>(c, s, X, W, m, n, k, eps, ss_in, Bs, R, ss_out, Y, ld);
+    if (kwn <= 2) return launch_xstream_kw<2, MS, NM, EPI, BIAS>(c, s, X, W, m, n, k, eps, ss_in, Bs, R, ss_out, Y, ld, warm);
+    if (kwn <= 4) return launch_xstream_kw<4, MS, NM, EPI, BIAS>(c, s, X, W, m, n, k, eps, ss_in, Bs, R, ss_out, Y, ld, warm);
+    return launch_xstream_kw<8, MS, NM, EPI, BIAS>(c, s, X, W, m, n, k, eps, ss_in, Bs, R, ss_out, Y, ld, warm);
 }
 
 int launch_xstream(const GemmCfg &c, hipStream_t s, const uint16_t *X, const uint16_t *W, int m, int n, int k, int nm,
-                   float eps, const float *ss_in, const uint16_t *Bs, uint16_t *R, float *ss_out, uint16_t *Y, int ld) {
+                   float eps, const float *ss_in, const uint16_t *Bs, uint16_t *R, float *ss_out, uint16_t *Y, int ld,
+                   const L3Warm *warm = nullptr) {
     const char *e = getenv("SWH_XSTREAM");  // A/B: 0 = decode_gemm_kernel's LDS image
     const int ks = k / 32;
     if (((e && e[0] == '0') && !c.xf) || c.cb != 1 || c.wn != 1 || c.s != 1 || c.persist || c.nw != 8 || n % 16 ||
@@ -1708,15 +1778,16 @@ int launch_xstream(const GemmCfg &c, hipStream_t s, const uint16_t *X, const uin
             if (m % 16 || (ks + 7) / 8 > 19) return 1;
             if ((ks + 7) / 8 > 8)
                 return launch_xstream_kw<19, 1, 0, EPI_RESIDUAL, false>(c, s, X, W, m, n, k, eps, nullptr, nullptr, R,
-                                                                       ss_out, nullptr, ld);
+                                                                       ss_out, nullptr, ld, warm);
         }
-        return launch_xstream_ms<1, 0, EPI_RESIDUAL, false>(c, s, X, W, m, n, k, eps, nullptr, nullptr, R, ss_out, nullptr, ld);
+        return launch_xstream_ms<1, 0, EPI_RESIDUAL, false>(c, s, X, W, m, n, k, eps, nullptr, nullptr, R, ss_out, nullptr,
+                                                            ld, warm);
     }
     if (c.xf) return 1;
     if (nm != 2 || !ss_in || !Bs || !Y) return 1;  // qkv: folded norm + bias
     if (c.ms == 1)
-        return launch_xstream_ms<1, 2, EPI_PLAIN, true>(c, s, X, W, m, n, k, eps, ss_in, Bs, nullptr, nullptr, Y, ld);
-    return launch_xstream_ms<2, 2, EPI_PLAIN, true>(c, s, X, W, m, n, k, eps, ss_in, Bs, nullptr, nullptr, Y, ld);
+        return launch_xstream_ms<1, 2, EPI_PLAIN, true>(c, s, X, W, m, n, k, eps, ss_in, Bs, nullptr, nullptr, Y, ld, warm);
+    return launch_xstream_ms<2, 2, EPI_PLAIN, true>(c, s, X, W, m, n, k, eps, ss_in, Bs, nullptr, nullptr, Y, ld, warm);
 }
 
 template <int MS, int NM, int EPI, bool BIAS>
@@ -1813,6 +1884,37 @@ extern "C" int swh_attn_decode_shared_frag(const void *qkv, void *k_cache, void 
     if (D == 128) return attn_dispatch_gq<128>(gq, q, kc, vc, rope_cos, rope_sin, prompt_len, state, B, Hq, Hkv, Tmax, scale, o, s, pf);
     return SWH_E_ARG;
 }
+// swh_attn_decode_shared_frag whose launch also carries Infinity Cache warm-up
+// workgroups (on the CUs the attention leaves idle) over l3_jobs
+extern "C" int swh_attn_decode_l3(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
+                                  const float *rope_sin, const int32_t *prompt_len, const int32_t *prompt_row,
+                                  const int32_t *state, int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax,
+                                  float scale, void *out, int32_t out_frag, const void *l3_jobs, int32_t l3_njobs,
+                                  int32_t l3_wgs, void *l3_sink, void *stream) {
+    if (!qkv || !k_cache || !v_cache || !rope_cos || !rope_sin || !prompt_len || !state || !out || B < 0 || Hkv <= 0 ||
+        Hq % Hkv || Tmax <= 0 || B > 65535 || (out_frag & ~1))
+        return SWH_E_ARG;
+    if (out_frag && (B % 16 || (Hq * D) % 32 || (reinterpret_cast<uintptr_t>(out) & 15))) return SWH_E_ARG;
+    if (!l3_jobs || !l3_sink || l3_njobs <= 0 || l3_njobs > kL3MaxJobs || l3_wgs <= 0 || l3_wgs > 4096)
+        return SWH_E_ARG;
+    if (B == 0) return SWH_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const auto *q = static_cast<const uint16_t *>(qkv);
+    auto *kc = static_cast<uint16_t *>(k_cache), *vc = static_cast<uint16_t *>(v_cache);
+    auto *o = static_cast<uint16_t *>(out);
+    const int gq = Hq / Hkv;
+    // the sink holds one word per thread of every warm-up workgroup (whole grid rows)
+    const int wgs = (l3_wgs + Hkv - 1) / Hkv * Hkv;
+    AttnPrefetch pf{nullptr, 0, 0, (int)B, prompt_row, out_frag};
+    pf.jobs = static_cast<const L3Job *>(l3_jobs);
+    pf.njobs = l3_njobs;
+    pf.sink = static_cast<uint32_t *>(l3_sink);
+    pf.nwg = wgs;
+    if (D == 64) return attn_dispatch_gq<64>(gq, q, kc, vc, rope_cos, rope_sin, prompt_len, state, B, Hq, Hkv, Tmax, scale, o, s, pf);
+    if (D == 128) return attn_dispatch_gq<128>(gq, q, kc, vc, rope_cos, rope_sin, prompt_len, state, B, Hq, Hkv, Tmax, scale, o, s, pf);
+    return SWH_E_ARG;
+}
+
 extern "C" int swh_attn_decode_shared(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
                                       const float *rope_sin, const int32_t *prompt_len, const int32_t *prompt_row,
                                       const int32_t *state, int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax,
@@ -1855,7 +1957,7 @@ extern "C" int64_t swh_decode_gemm_workspace_bytes(int64_t M, int64_t N, int64_t
 static int decode_gemm_impl(const void *x, const void *w, int64_t M, int64_t N, int64_t K, const void *norm_w,
                             float eps, const void *bias, void *residual, int32_t silu, void *y, int64_t ldy,
                             const float *ss_in, float *ss_out, void *workspace, int64_t workspace_bytes, void *stream,
-                            int fw, int act = 0) {
+                            int fw, int act = 0, const L3Warm *warm = nullptr) {
     if (fw && (norm_w || K % 128)) return SWH_E_ARG;
     // act bit 0: the SiLU output in fragment order (tile path only); bit 1: X in fragment order (xstream only)
     if (act & ~3 || ((act & 1) && (!silu || N % 32 || M % 16)) || ((act & 2) && (!residual || M % 16 || K % 32)))
@@ -1941,7 +2043,7 @@ static int decode_gemm_impl(const void *x, const void *w, int64_t M, int64_t N, 
     }
     if (residual) {
         if (nm == 0) {
-            const int rc = launch_xstream(c, s, X, W, m, n, k, nm, eps, ss_in, Bs, R, ss_out, nullptr, ld);
+            const int rc = launch_xstream(c, s, X, W, m, n, k, nm, eps, ss_in, Bs, R, ss_out, nullptr, ld, warm);
             if (rc != 1) return rc;
         }
         if (c.xf) return SWH_E_ARG;  // a fragment-order X is read by xstream only
@@ -1951,7 +2053,7 @@ static int decode_gemm_impl(const void *x, const void *w, int64_t M, int64_t N, 
     if (Bs) {
         if (nm == 1) SWH_GEMM(1, EPI_PLAIN, true);
         if (nm == 2) {
-            const int rc = launch_xstream(c, s, X, W, m, n, k, nm, eps, ss_in, Bs, nullptr, nullptr, Y, ld);
+            const int rc = launch_xstream(c, s, X, W, m, n, k, nm, eps, ss_in, Bs, nullptr, nullptr, Y, ld, warm);
             if (rc != 1) return rc;
             SWH_GEMM(2, EPI_PLAIN, true);
         }
@@ -1977,6 +2079,24 @@ extern "C" int swh_decode_gemm_fragw(const void *x, const void *w, int64_t M, in
                                      int64_t workspace_bytes, void *stream) {
     return decode_gemm_impl(x, w, M, N, K, nullptr, eps, bias, residual, silu, y, ldy, ss_in, ss_out, workspace,
                             workspace_bytes, stream, 1, act_frag);
+}
+
+// swh_decode_gemm_fragw with l3_wgs Infinity Cache warm-up workgroups appended to
+// the register-streamed (xstream) launch; other geometries ignore them
+extern "C" int swh_decode_gemm_fragw_l3(const void *x, const void *w, int64_t M, int64_t N, int64_t K, float eps,
+                                        const void *bias, void *residual, int32_t silu, void *y, int64_t ldy,
+                                        const float *ss_in, float *ss_out, int32_t act_frag, const void *l3_jobs,
+                                        int32_t l3_njobs, int32_t l3_wgs, void *l3_sink, void *workspace,
+                                        int64_t workspace_bytes, void *stream) {
+    if (!l3_jobs || !l3_sink || l3_njobs <= 0 || l3_njobs > kL3MaxJobs || l3_wgs <= 0 || l3_wgs > 4096)
+        return SWH_E_ARG;
+    L3Warm wm;
+    wm.jobs = static_cast<const L3Job *>(l3_jobs);
+    wm.njobs = l3_njobs;
+    wm.gx0 = l3_wgs;  // the warm-up block count (launch_xstream_kw turns it into the tile count)
+    wm.sink = static_cast<uint32_t *>(l3_sink);
+    return decode_gemm_impl(x, w, M, N, K, nullptr, eps, bias, residual, silu, y, ldy, ss_in, ss_out, workspace,
+                            workspace_bytes, stream, 1, act_frag, &wm);
 }
 
 extern "C" int swh_frag_pack(const void *w, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst,
@@ -2139,10 +2259,6 @@ namespace {
 // on-die.  Read-only: results are unchanged by construction.  The loads feed
 // an XOR whose value is stored only if it equals `magic` (never, in practice:
 // it keeps the loads alive without a data-dependent store stream).
-struct L3Job {
-    const uint4 *p;
-    int64_t n16;  // 16-B units
-};
 
 template <bool NT>
 __global__ __launch_bounds__(256) void l3_prefetch_kernel(const L3Job *__restrict__ jobs, int njobs, uint32_t magic,

@@ -204,6 +204,18 @@ class DecodeEngine:
         self.l3_at = int(os.environ.get("SWH_DECODE_L3_AT", "0"))
         self.l3_nt = int(os.environ.get("SWH_DECODE_L3_NT", "0"))
         self._l3_jobs = None
+        # the same warm-up carried by the attention launch itself (swh_attn_decode_l3): its
+        # B x Hkv workgroups leave CUs idle, extra workgroups on them read the weights of
+        # the projections that follow (SWH_DECODE_L3_ATTN = workgroups, 0: off;
+        # SWH_DECODE_L3_SET: comma list of o, down, gu (this layer), qkv1, o1 (next layer))
+        self.l3_set = os.environ.get("SWH_DECODE_L3_SET", "o,down,qkv1")
+        self.l3_attn = int(os.environ.get("SWH_DECODE_L3_ATTN", str(self._l3_attn_default()))) if self.fused else 0
+        self._l3a_jobs = None
+        # and by the qkv launch (register-streamed: its tiles leave CUs idle too);
+        # SWH_DECODE_L3_QKV = workgroups, SWH_DECODE_L3_QKV_SET as SWH_DECODE_L3_SET
+        self.l3_qkv = int(os.environ.get("SWH_DECODE_L3_QKV", "0")) if self.fused else 0
+        self.l3_qkv_set = os.environ.get("SWH_DECODE_L3_QKV_SET", "gu")
+        self._l3q_jobs = None
         self._exit_poll = EarlyExitPoll(self.finished)
         self.steps_run = 0  # decode steps the last generate() ran (early exit: fewer than max_new_tokens - 1)
 
@@ -315,6 +327,17 @@ class DecodeEngine:
         w, nw = self._normed(name, norm)
         return nn_ops.decode_gemm(x, w, norm_w=nw, eps=eps, **kw)
 
+    def _l3_attn_default(self) -> int:
+        """Warm-up workgroups in the attention launch by default: 96 when the
+        attention's B x Hkv workgroups leave that many CUs idle and one layer's
+        o + down + next qkv weights are small beside the 256 MiB Infinity Cache
+        (Qwen2.5-0.5B at 64 rows: 12.3 MB; decode step 972 -> 925 us, DESIGN.md
+        §2e), else 0 (e.g. Llama-3-8B: 512 attention workgroups, 436 MB layers)."""
+        c = self.cfg
+        cus = torch.cuda.get_device_properties(self.dev).multi_processor_count
+        per_layer = 2 * c.hidden_size * (c.q_dim + c.intermediate_size + c.qkv_dim)
+        return 96 if self.B * c.num_key_value_heads + 96 <= cus and per_layer <= (64 << 20) else 0
+
     def _proj_weight(self, name: str) -> torch.Tensor:
         """The buffer _proj streams for a projection."""
         if name in self.packed:
@@ -339,6 +362,59 @@ class DecodeEngine:
             self._l3_side = torch.cuda.Stream()
         return self._l3_jobs
 
+    def _l3_job_tables(self, spec: str):
+        """Per layer, a device table {ptr, bytes / 16} of the weights `spec` names
+        (comma list of o, down, gu, qkv: this layer; o1, down1, gu1, qkv1: the next)."""
+        L = self.cfg.num_hidden_layers
+        names = {"o": (0, "o_w"), "down": (0, "down_w"), "gu": (0, "gu_w"), "qkv": (0, "qkv_w"),
+                 "qkv1": (1, "qkv_w"), "o1": (1, "o_w"), "gu1": (1, "gu_w"), "down1": (1, "down_w")}
+        sel = [names[k.strip()] for k in spec.split(",") if k.strip()]
+        tabs = []
+        for i in range(L):
+            t = []
+            for d, n in sel:
+                if i + d < L:
+                    w = self._proj_weight(f"l{i + d}.{n}")
+                    t += [w.data_ptr(), w.numel() * w.element_size() // 16]
+            tabs.append(torch.tensor(t, dtype=torch.int64).to(self.dev) if t else None)
+        return tabs
+
+    def _qkv(self, i: int):
+        p = self.model.p
+        name = f"l{i}.qkv_w"
+        if self.l3_qkv > 0 and name in self.fragw:
+            if self._l3q_jobs is None:
+                self._l3q_jobs = self._l3_job_tables(self.l3_qkv_set)
+                self._l3q_sink = torch.zeros(self.l3_qkv * 512, dtype=torch.int32, device=self.dev)
+            jobs = self._l3q_jobs[i]
+            if jobs is not None:
+                return nn_ops.decode_gemm_fragw(self.s, self.fragw[name], eps=self.cfg.rms_norm_eps,
+                                                bias=p.get(f"l{i}.qkv_b"), y=self.qkv, ss_in=self.ss,
+                                                l3=(jobs, self.l3_qkv, self._l3q_sink))
+        return self._proj(name, self.s, bias=p.get(f"l{i}.qkv_b"), y=self.qkv, ss_in=self.ss)
+
+    def _l3a_tables(self):
+        """Per layer, the device job table of swh_attn_decode_l3 (SWH_DECODE_L3_SET)."""
+        if self._l3a_jobs is None:
+            self._l3a_jobs = self._l3_job_tables(self.l3_set)
+            Hkv = self.cfg.num_key_value_heads
+            self._l3a_sink = torch.zeros(-(-self.l3_attn // Hkv) * Hkv * 512, dtype=torch.int32, device=self.dev)
+        return self._l3a_jobs
+
+    def _attn(self, i: int):
+        c = self.cfg
+        jobs = self._l3a_tables()[i] if self.l3_attn > 0 else None
+        if jobs is not None:
+            return nn_ops.attn_decode_l3(self.qkv, self.kv[i, 0], self.kv[i, 1], self.cos, self.sin, self.plen,
+                                         self.state, c.num_attention_heads, c.num_key_value_heads, c.head_dim,
+                                         c.head_dim ** -0.5, self.att, self.prow, self.att_frag, jobs, self.l3_attn,
+                                         self._l3a_sink)
+        pf = self._normed(f"l{i}.gu_w", f"l{i}.ln_post")[0] if self.prefetch and f"l{i}.gu_w" not in \
+            self.packed and f"l{i}.gu_w" not in self.fragw else None
+        return nn_ops.attn_decode(self.qkv, self.kv[i, 0], self.kv[i, 1], self.cos, self.sin, self.plen, self.state,
+                                  c.num_attention_heads, c.num_key_value_heads, c.head_dim, c.head_dim ** -0.5,
+                                  out=self.att, prefetch_gate_up=pf, prompt_row=self.prow, out_frag=self.att_frag)
+
     def _l3_prefetch(self, layer: int):
         """Fork the warm-up of `layer`'s weights onto the side stream."""
         jobs = self._l3_tables()
@@ -359,14 +435,10 @@ class DecodeEngine:
         for i in range(L):
             if l3 and self.l3_at == 0 and i + 1 < L:
                 self._l3_prefetch(i + 1)
-            self._proj(f"l{i}.qkv_w", self.s, bias=p.get(f"l{i}.qkv_b"), y=self.qkv, ss_in=ss)
+            self._qkv(i)
             if l3 and self.l3_at == 1 and i + 1 < L:
                 self._l3_prefetch(i + 1)
-            pf = self._normed(f"l{i}.gu_w", f"l{i}.ln_post")[0] if self.prefetch and f"l{i}.gu_w" not in \
-                self.packed and f"l{i}.gu_w" not in self.fragw else None
-            nn_ops.attn_decode(self.qkv, self.kv[i, 0], self.kv[i, 1], self.cos, self.sin, self.plen, self.state,
-                               c.num_attention_heads, c.num_key_value_heads, c.head_dim, c.head_dim ** -0.5,
-                               out=self.att, prefetch_gate_up=pf, prompt_row=self.prow, out_frag=self.att_frag)
+            self._attn(i)
             if self.att_frag:
                 self._proj(f"l{i}.o_w", self.att, residual=self.s, ss_out=ss, act_frag=2)
             else:
@@ -490,18 +562,9 @@ class DecodeEngine:
         # weights per step streams from HBM; one layer's alone would sit in the
         # 256 MiB Infinity Cache and time optimistically)
         ops_ = {
-            "decode_gemm.qkv": (lambda i: self._proj(f"l{i}.qkv_w", self.s, bias=p.get(f"l{i}.qkv_b"), y=self.qkv,
-                                                     ss_in=ss),
+            "decode_gemm.qkv": (lambda i: self._qkv(i),
                                 gemm_bytes(c.qkv_dim, H), L),
-            "attn_decode": (lambda i: nn_ops.attn_decode(self.qkv, self.kv[i, 0], self.kv[i, 1], self.cos, self.sin,
-                                                         self.plen, self.state, c.num_attention_heads,
-                                                         c.num_key_value_heads, c.head_dim, c.head_dim ** -0.5,
-                                                         out=self.att,
-                                                         prefetch_gate_up=self._normed(f"l{i}.gu_w", "")[0]
-                                                         if self.prefetch and f"l{i}.gu_w" not in self.packed
-                                                         and f"l{i}.gu_w" not in self.fragw
-                                                         else None, prompt_row=self.prow, out_frag=self.att_frag),
-                            att_bytes, L),
+            "attn_decode": (lambda i: self._attn(i), att_bytes, L),
             "decode_gemm.o": (lambda i: self._proj(f"l{i}.o_w", self.att, residual=self.s, ss_out=ss,
                                                    **({"act_frag": 2} if self.att_frag else {})),
                               gemm_bytes(H, c.q_dim), L),

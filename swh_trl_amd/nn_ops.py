@@ -130,6 +130,25 @@ def attn_decode(qkv: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
     return out
 
 
+def attn_decode_l3(qkv: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, rope_cos: torch.Tensor,
+                   rope_sin: torch.Tensor, prompt_len: torch.Tensor, state: torch.Tensor, Hq: int, Hkv: int, D: int,
+                   scale: float, out: torch.Tensor, prompt_row: Optional[torch.Tensor], out_frag: bool,
+                   l3_jobs: torch.Tensor, l3_wgs: int, l3_sink: torch.Tensor) -> torch.Tensor:
+    """attn_decode whose launch also carries Infinity Cache warm-up workgroups
+    over l3_jobs (int64 [n, 2] device table of {ptr, bytes / 16})
+    (swh_attn_decode_l3): identical results."""
+    _dev(qkv, "attn_decode_l3")
+    B = qkv.shape[0]
+    wgs = -(-l3_wgs // Hkv) * Hkv
+    if l3_sink.numel() * l3_sink.element_size() < wgs * 512 * 4:
+        raise ValueError("attn_decode_l3: l3_sink smaller than the warm-up workgroups x 512 words")
+    call("swh_attn_decode_l3", qkv.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), rope_cos.data_ptr(),
+         rope_sin.data_ptr(), prompt_len.data_ptr(), _p(prompt_row), state.data_ptr(), B, Hq, Hkv, D,
+         k_cache.shape[2], float(scale), out.data_ptr(), int(bool(out_frag)), l3_jobs.data_ptr(),
+         l3_jobs.numel() // 2, int(l3_wgs), l3_sink.data_ptr(), _stream())
+    return out
+
+
 _GEMM_WS: dict = {}
 
 
@@ -178,10 +197,13 @@ def frag_pack(w: torch.Tensor, norm_w: Optional[torch.Tensor] = None, *, silu: b
 def decode_gemm_fragw(x: torch.Tensor, w: torch.Tensor, *, eps: float = 1e-6, bias: Optional[torch.Tensor] = None,
                       residual: Optional[torch.Tensor] = None, silu: bool = False, y: Optional[torch.Tensor] = None,
                       workspace: Optional[torch.Tensor] = None, ss_in: Optional[torch.Tensor] = None,
-                      ss_out: Optional[torch.Tensor] = None, act_frag: int = 0) -> torch.Tensor:
+                      ss_out: Optional[torch.Tensor] = None, act_frag: int = 0,
+                      l3: Optional[tuple] = None) -> torch.Tensor:
     """decode_gemm (no norm_w) over w packed by frag_pack ([N, K], [2N, K] with
     silu) (include/swh_trl_amd.h swh_decode_gemm_fragw): bit-identical results.
-    act_frag bit 0: write the SiLU output in fragment order; bit 1: read x in it."""
+    act_frag bit 0: write the SiLU output in fragment order; bit 1: read x in it.
+    l3 = (jobs int64 [n, 2] {ptr, bytes / 16}, workgroups, sink): Infinity Cache
+    warm-up workgroups appended to a register-streamed launch (swh_decode_gemm_fragw_l3)."""
     _dev(x, "decode_gemm_fragw")
     M, K = x.shape
     N = w.shape[0] // 2 if silu else w.shape[0]
@@ -189,6 +211,14 @@ def decode_gemm_fragw(x: torch.Tensor, w: torch.Tensor, *, eps: float = 1e-6, bi
         y = torch.empty(M, N, device=x.device, dtype=x.dtype)
     ldy = residual.stride(0) if residual is not None else y.stride(0)
     ws = workspace if workspace is not None else gemm_workspace(x.device)
+    if l3 is not None:
+        jobs, nwg, sink = l3
+        if sink.numel() * sink.element_size() < nwg * 512 * 4:
+            raise ValueError("decode_gemm_fragw: l3 sink smaller than the warm-up workgroups x 512 words")
+        call("swh_decode_gemm_fragw_l3", x.data_ptr(), w.data_ptr(), M, N, K, float(eps), _p(bias), _p(residual),
+             int(bool(silu)), _p(y), ldy, _p(ss_in), _p(ss_out), int(act_frag), jobs.data_ptr(), jobs.numel() // 2,
+             int(nwg), sink.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
+        return residual if residual is not None else y
     call("swh_decode_gemm_fragw", x.data_ptr(), w.data_ptr(), M, N, K, float(eps), _p(bias), _p(residual),
          int(bool(silu)), _p(y), ldy, _p(ss_in), _p(ss_out), int(act_frag), ws.data_ptr(), ws.numel(), _stream())
     return residual if residual is not None else y

@@ -931,3 +931,55 @@ def test_l3_prefetch_branch_generates_identically(dev, monkeypatch):
                                            torch.cuda.current_stream().cuda_stream) == 0
     torch.cuda.synchronize()
     assert all(torch.equal(a, b) for a, b in zip(bufs, ref))
+
+
+def test_attn_l3_warmup_generates_identically(dev, monkeypatch):
+    """The attention launch carrying Infinity Cache warm-up workgroups
+    (swh_attn_decode_l3: o / down of this layer, qkv of the next) generates the
+    same tokens and log-probs as the plain attention launch."""
+    from swh_trl_amd.engine import CausalLM, DecodeEngine, tiny_qwen2
+    m = CausalLM(tiny_qwen2(1024, 3), dev, seed=7)
+    g = torch.Generator().manual_seed(7)
+    B, P, C = 32, 12, 20
+    ids = torch.randint(0, m.cfg.vocab_size, (B, P), generator=g).to(dev)
+    mask = torch.ones(B, P, dtype=torch.int64, device=dev)
+    mask[5, :4] = 0
+    outs = {}
+    for nwg, sel in (("128", "o,down,qkv1"), ("37", "gu,o1,down1"), ("0", "")):
+        monkeypatch.setenv("SWH_DECODE_L3_ATTN", nwg)
+        monkeypatch.setenv("SWH_DECODE_L3_SET", sel)
+        eng = DecodeEngine(m, B, P, C)
+        outs[nwg] = (eng.generate(ids, mask, C, greedy=True),
+                     eng.generate(ids, mask, C, temperature=0.9, seed=3, return_logp=True))
+        del eng
+    for k in ("128", "37"):
+        for a, b in zip(outs[k], outs["0"]):
+            for x, y in zip(a, b):
+                if isinstance(x, torch.Tensor):
+                    assert torch.equal(x, y)
+
+
+def test_qkv_l3_warmup_generates_identically(dev, monkeypatch):
+    """The register-streamed qkv launch carrying Infinity Cache warm-up
+    workgroups (swh_decode_gemm_fragw_l3) generates the same tokens and
+    log-probs as the plain launch (with the attention-launch warm-up on too)."""
+    from swh_trl_amd.engine import CausalLM, DecodeEngine, tiny_qwen2
+    m = CausalLM(tiny_qwen2(1024, 3), dev, seed=8)
+    g = torch.Generator().manual_seed(8)
+    B, P, C = 32, 12, 20
+    ids = torch.randint(0, m.cfg.vocab_size, (B, P), generator=g).to(dev)
+    mask = torch.ones(B, P, dtype=torch.int64, device=dev)
+    outs = {}
+    for qn, qsel, an in (("64", "gu", "96"), ("17", "o,down,gu1", "0"), ("0", "", "0")):
+        monkeypatch.setenv("SWH_DECODE_L3_QKV", qn)
+        monkeypatch.setenv("SWH_DECODE_L3_QKV_SET", qsel)
+        monkeypatch.setenv("SWH_DECODE_L3_ATTN", an)
+        eng = DecodeEngine(m, B, P, C)
+        outs[qn] = (eng.generate(ids, mask, C, greedy=True),
+                    eng.generate(ids, mask, C, temperature=0.9, seed=3, return_logp=True))
+        del eng
+    for k in ("64", "17"):
+        for a, b in zip(outs[k], outs["0"]):
+            for x, y in zip(a, b):
+                if isinstance(x, torch.Tensor):
+                    assert torch.equal(x, y)

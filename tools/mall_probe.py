@@ -58,7 +58,7 @@ def main():
                                                    **af(2)),
     }
     print({k: len(v) for k, v in W.items()}, flush=True)
-    steps_only = "--steps-only" in sys.argv
+    steps_only = "--steps-only" in sys.argv or "--attn-l3" in sys.argv
     stream = torch.cuda.current_stream()
 
     def timed(fn, n, cycle, iters=5):
@@ -114,9 +114,31 @@ def main():
             (256, 1, 0), (0, 0, 0))
     if steps_only:
         grid = ((0, 0, 0), (32, 0, 0), (128, 1, 0), (0, 0, 0))
+    if "--attn-l3" in sys.argv:
+        grid = ()
     for nwg, at, nt in grid:
         print(f"decode step  l3 nwg {nwg:3d} at {at} nt {nt}: {step_us(nwg, at, nt):8.1f} us", flush=True)
 
+    # the warm-up carried by the attention launch (swh_attn_decode_l3) and the qkv launch
+    # (swh_decode_gemm_fragw_l3)
+    def step_attn(nwg, sel, qn=0, qsel=""):
+        eng.l3_nwg = 0
+        eng.l3_attn, eng.l3_set = nwg, sel
+        eng.l3_qkv, eng.l3_qkv_set = qn, qsel
+        eng._l3a_jobs = eng._l3q_jobs = None
+        eng.state[0] = 100
+        return timed(lambda i: eng._step_fused(), 4, 1, iters=6)
+
+    if "--attn-l3" in sys.argv:
+        grid = [(0, "", 0, ""), (96, "o,down,qkv1", 0, ""), (96, "o,down,qkv1", 64, "gu"),
+                (96, "o,down,qkv1", 112, "gu"), (0, "", 0, ""), (96, "qkv1,gu", 112, "o,down"),
+                (64, "qkv1", 112, "o,down"), (96, "o,down,qkv1", 0, ""), (0, "", 0, "")]
+        env_grid = os.environ.get("SWH_PROBE_GRID")
+        if env_grid:  # "nwg:set:qkv_nwg:qkv_set;..."
+            grid = [(int(a), b, int(c), d) for a, b, c, d in (e.split(":") for e in env_grid.split(";"))]
+        for nwg, sel, qn, qsel in grid:
+            print(f"decode step  attn-l3 {nwg:3d} {sel:16s} qkv-l3 {qn:3d} {qsel:10s}: "
+                  f"{step_attn(nwg, sel, qn, qsel):8.1f} us", flush=True)
 
 if __name__ == "__main__":
     main()
