@@ -546,7 +546,7 @@ int swh_lm_head_sample_step_fragw(const void *x, const void *w, int64_t M, int64
 /* swh_decode_gemm_fragw with l3_wgs Infinity Cache warm-up workgroups appended
  * to its launch when the shape runs register-streamed (the decode qkv / o / down
  * projections; other geometries ignore them): they read the l3_njobs (<= 8)
- * ranges {const void *ptr, int64_t bytes / 16} on the CUs the projection's tiles
+ * ranges {const void *ptr, int64_t bytes / 16, int64_t stripe} (as swh_attn_decode_l3) on the CUs the projection's tiles
  * leave idle; l3_sink >= l3_wgs x 512 uint32.  Results identical. */
 int swh_decode_gemm_fragw_l3(const void *x, const void *w, int64_t M, int64_t N, int64_t K, float eps,
                              const void *bias, void *residual, int32_t silu, void *y, int64_t ldy, const float *ss_in,
@@ -555,7 +555,10 @@ int swh_decode_gemm_fragw_l3(const void *x, const void *w, int64_t M, int64_t N,
 /* swh_attn_decode_shared_frag whose launch also carries >= l3_wgs Infinity Cache
  * warm-up workgroups (rounded up to whole grid rows of Hkv) on the CUs the
  * attention's B x Hkv workgroups leave idle: they read the l3_njobs (<= 8)
- * ranges {const void *ptr, int64_t bytes / 16} and discard the data, so the
+ * ranges {const void *ptr, int64_t bytes / 16, int64_t stripe} and discard the
+ * data (stripe 0: contiguous shares; else the range is cut into column blocks of
+ * `stripe` 16-B units and block c is read by a workgroup of logical XCD c % 8,
+ * where decode_gemm's register-streamed and tile launches run it), so the
  * projections that follow (o_proj and down_proj of this layer, qkv of the next)
  * find their weights on-die; l3_sink >= rounded workgroups x 512 uint32 of
  * scratch.  Results identical to swh_attn_decode_shared_frag. */
@@ -564,7 +567,7 @@ int swh_attn_decode_l3(const void *qkv, void *k_cache, void *v_cache, const floa
                        int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax, float scale, void *out, int32_t out_frag,
                        const void *l3_jobs, int32_t l3_njobs, int32_t l3_wgs, void *l3_sink, void *stream);
 /* Infinity Cache warm-up: nwg workgroups read every byte of the njobs ranges
- * jobs[j] = {const void *ptr, int64_t bytes / 16} (device memory, 16-B aligned)
+ * jobs[j] = {const void *ptr, int64_t bytes / 16, int64_t 0} (device memory, 16-B aligned)
  * and keep nothing but a sink word (>= nwg * 256 uint32 of scratch, written
  * only if an XOR of the data equals a magic constant).  Captured on a side
  * branch of the decode graph to pull layer l+1's decode weights on-die while

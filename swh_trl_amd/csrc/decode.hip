@@ -577,7 +577,9 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
 // Infinity Cache warm-up job: a device range read (and discarded) by warm-up workgroups
 struct L3Job {
     const uint4 *p;
-    int64_t n16;  // 16-B units
+    int64_t n16;     // 16-B units
+    int64_t stripe;  // 0: a contiguous share per workgroup; else 16-B units per column block, block c read
+                     // by a workgroup of (logical) XCD c % 8, the XCD the consuming launch runs block c on
 };
 constexpr int kL3MaxJobs = 8;
 
@@ -594,16 +596,13 @@ struct L3Warm {
 // equals a magic constant
 template <int NT>
 __device__ __forceinline__ void l3_warm_share(const L3Job *__restrict__ jobs, int njobs, int p, int npf,
-                                              uint32_t *__restrict__ sink) {
+                                              uint32_t *__restrict__ sink, int lin) {
     const int tid = threadIdx.x;
     int64_t tot = 0;
-    for (int j = 0; j < njobs; ++j) tot += jobs[j].n16;
+    for (int j = 0; j < njobs; ++j) tot += jobs[j].stripe ? 0 : jobs[j].n16;
     const int64_t share = (tot + npf - 1) / npf, lo = (int64_t)p * share, hi = min(tot, lo + share);
     uint32_t acc = 0;
-    int64_t base = 0;
-    for (int j = 0; j < njobs; ++j) {
-        const int64_t n = jobs[j].n16, a = max(lo - base, (int64_t)0), e = min(hi - base, n);
-        const uint4 *src = jobs[j].p;
+    auto sweep = [&](const uint4 *src, int64_t a, int64_t e) {
         for (int64_t i = a + tid; i < e; i += 8 * NT) {
             uint4 v[8];
 #pragma unroll
@@ -614,6 +613,17 @@ __device__ __forceinline__ void l3_warm_share(const L3Job *__restrict__ jobs, in
 #pragma unroll
             for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
         }
+    };
+    int64_t base = 0;
+    const int xcd = lin & 7, q = p >> 3, nq = max(npf >> 3, 1);
+    for (int j = 0; j < njobs; ++j) {
+        const int64_t n = jobs[j].n16, st = jobs[j].stripe;
+        if (st) {  // column blocks c = xcd + 8 (q + nq t): into the L2 of the XCD that consumes them
+            for (int64_t c = xcd + 8 * (int64_t)q; c * st < n; c += 8 * (int64_t)nq)
+                sweep(jobs[j].p + c * st, 0, min(st, n - c * st));
+            continue;
+        }
+        sweep(jobs[j].p, max(lo - base, (int64_t)0), min(hi - base, n));
         base += n;
     }
     if (acc == 0x9e3779b9u) sink[(int64_t)p * NT + tid] = acc;
@@ -643,7 +653,7 @@ __global__ __launch_bounds__(512) void xstream_gemm_kernel(const uint16_t *__res
                                                            L3Warm warm) {
     static_assert(EPI != EPI_SILU && NM != 1, "plain / residual epilogues, folded or no norm");
     if (warm.jobs && (int)blockIdx.x >= warm.gx0) {  // Infinity Cache warm-up blocks past the tiles
-        l3_warm_share<512>(warm.jobs, warm.njobs, blockIdx.x - warm.gx0, gridDim.x - warm.gx0, warm.sink);
+        l3_warm_share<512>(warm.jobs, warm.njobs, blockIdx.x - warm.gx0, gridDim.x - warm.gx0, warm.sink, blockIdx.x);
         return;
     }
     constexpr int NW = 8, NT = 512, MR = 16 * MS, NB = 16, LDR = MR + 4, G8 = NB / 8, F = NW;
@@ -1325,7 +1335,7 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
     SWH_GEMM_TRACE(0);  // phase stamps for tools/attn_probe.py (instrumented build only)
     if ((int)blockIdx.y >= pf.rows && pf.jobs) {  // an Infinity Cache warm-up workgroup
         l3_warm_share<kAttnThreads>(pf.jobs, pf.njobs, (blockIdx.y - pf.rows) * gridDim.x + blockIdx.x,
-                                    (gridDim.y - pf.rows) * gridDim.x, pf.sink);
+                                    (gridDim.y - pf.rows) * gridDim.x, pf.sink, blockIdx.y * gridDim.x + blockIdx.x);
         return;
     }
     if ((int)blockIdx.y >= pf.rows) {  // a prefetch workgroup

@@ -355,7 +355,7 @@ class DecodeEngine:
                 t = []
                 for n in ("qkv_w", "o_w", "gu_w", "down_w"):
                     w = self._proj_weight(f"l{i}.{n}")
-                    t += [w.data_ptr(), w.numel() * w.element_size() // 16]
+                    t += [w.data_ptr(), w.numel() * w.element_size() // 16, 0]
                 tabs.append(torch.tensor(t, dtype=torch.int64).to(self.dev))
             self._l3_jobs = tabs
             self._l3_sink = torch.zeros(self.l3_nwg * 256, dtype=torch.int32, device=self.dev)
@@ -368,14 +368,18 @@ class DecodeEngine:
         L = self.cfg.num_hidden_layers
         names = {"o": (0, "o_w"), "down": (0, "down_w"), "gu": (0, "gu_w"), "qkv": (0, "qkv_w"),
                  "qkv1": (1, "qkv_w"), "o1": (1, "o_w"), "gu1": (1, "gu_w"), "down1": (1, "down_w")}
-        sel = [names[k.strip()] for k in spec.split(",") if k.strip()]
+        # "name@x": striped by 16-row column block (fragment-order weights), block c warmed
+        # on the XCD the consuming launch runs it on (c % 8)
+        sel = [(*names[k.strip().split("@")[0]], k.strip().endswith("@x")) for k in spec.split(",") if k.strip()]
         tabs = []
         for i in range(L):
             t = []
-            for d, n in sel:
+            for d, n, xs in sel:
                 if i + d < L:
-                    w = self._proj_weight(f"l{i + d}.{n}")
-                    t += [w.data_ptr(), w.numel() * w.element_size() // 16]
+                    nm = f"l{i + d}.{n}"
+                    w = self._proj_weight(nm)
+                    stripe = 2 * w.shape[-1] if xs and nm in self.fragw and w.dim() == 2 else 0
+                    t += [w.data_ptr(), w.numel() * w.element_size() // 16, stripe]
             tabs.append(torch.tensor(t, dtype=torch.int64).to(self.dev) if t else None)
         return tabs
 
@@ -420,7 +424,7 @@ class DecodeEngine:
         jobs = self._l3_tables()
         self._l3_side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self._l3_side):
-            call("swh_l3_prefetch", jobs[layer].data_ptr(), 4, self.l3_nwg, self.l3_nt, self._l3_sink.data_ptr(),
+            call("swh_l3_prefetch", jobs[layer].data_ptr(), jobs[layer].numel() // 3, self.l3_nwg, self.l3_nt, self._l3_sink.data_ptr(),
                  ops._stream())
 
     def _step_fused(self):

@@ -145,7 +145,7 @@ def attn_decode_l3(qkv: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
     call("swh_attn_decode_l3", qkv.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), rope_cos.data_ptr(),
          rope_sin.data_ptr(), prompt_len.data_ptr(), _p(prompt_row), state.data_ptr(), B, Hq, Hkv, D,
          k_cache.shape[2], float(scale), out.data_ptr(), int(bool(out_frag)), l3_jobs.data_ptr(),
-         l3_jobs.numel() // 2, int(l3_wgs), l3_sink.data_ptr(), _stream())
+         l3_jobs.numel() // 3, int(l3_wgs), l3_sink.data_ptr(), _stream())
     return out
 
 
@@ -202,7 +202,7 @@ def decode_gemm_fragw(x: torch.Tensor, w: torch.Tensor, *, eps: float = 1e-6, bi
     """decode_gemm (no norm_w) over w packed by frag_pack ([N, K], [2N, K] with
     silu) (include/swh_trl_amd.h swh_decode_gemm_fragw): bit-identical results.
     act_frag bit 0: write the SiLU output in fragment order; bit 1: read x in it.
-    l3 = (jobs int64 [n, 2] {ptr, bytes / 16}, workgroups, sink): Infinity Cache
+    l3 = (jobs int64 [n, 3] {ptr, bytes / 16, stripe}, workgroups, sink): Infinity Cache
     warm-up workgroups appended to a register-streamed launch (swh_decode_gemm_fragw_l3)."""
     _dev(x, "decode_gemm_fragw")
     M, K = x.shape
@@ -216,7 +216,7 @@ def decode_gemm_fragw(x: torch.Tensor, w: torch.Tensor, *, eps: float = 1e-6, bi
         if sink.numel() * sink.element_size() < nwg * 512 * 4:
             raise ValueError("decode_gemm_fragw: l3 sink smaller than the warm-up workgroups x 512 words")
         call("swh_decode_gemm_fragw_l3", x.data_ptr(), w.data_ptr(), M, N, K, float(eps), _p(bias), _p(residual),
-             int(bool(silu)), _p(y), ldy, _p(ss_in), _p(ss_out), int(act_frag), jobs.data_ptr(), jobs.numel() // 2,
+             int(bool(silu)), _p(y), ldy, _p(ss_in), _p(ss_out), int(act_frag), jobs.data_ptr(), jobs.numel() // 3,
              int(nwg), sink.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
         return residual if residual is not None else y
     call("swh_decode_gemm_fragw", x.data_ptr(), w.data_ptr(), M, N, K, float(eps), _p(bias), _p(residual),

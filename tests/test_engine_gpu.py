@@ -924,7 +924,7 @@ def test_l3_prefetch_branch_generates_identically(dev, monkeypatch):
     # the kernel itself: odd sizes, several ranges, read-only
     bufs = [torch.randint(-1000, 1000, (n,), dtype=torch.int32, device=dev) for n in (4, 4 * 1037, 4 * 70001)]
     ref = [b.clone() for b in bufs]
-    tab = torch.tensor(sum([[b.data_ptr(), b.numel() * 4 // 16] for b in bufs], []), dtype=torch.int64).to(dev)
+    tab = torch.tensor(sum([[b.data_ptr(), b.numel() * 4 // 16, 0] for b in bufs], []), dtype=torch.int64).to(dev)
     sink = torch.zeros(128 * 256, dtype=torch.int32, device=dev)
     for nt in (0, 1):
         assert _lib.load().swh_l3_prefetch(tab.data_ptr(), 3, 128, nt, sink.data_ptr(),
@@ -945,7 +945,7 @@ def test_attn_l3_warmup_generates_identically(dev, monkeypatch):
     mask = torch.ones(B, P, dtype=torch.int64, device=dev)
     mask[5, :4] = 0
     outs = {}
-    for nwg, sel in (("128", "o,down,qkv1"), ("37", "gu,o1,down1"), ("0", "")):
+    for nwg, sel in (("128", "o,down,qkv1"), ("37", "gu,o1@x,down1@x"), ("0", "")):
         monkeypatch.setenv("SWH_DECODE_L3_ATTN", nwg)
         monkeypatch.setenv("SWH_DECODE_L3_SET", sel)
         eng = DecodeEngine(m, B, P, C)

@@ -130,9 +130,9 @@ def main():
         return timed(lambda i: eng._step_fused(), 4, 1, iters=6)
 
     if "--attn-l3" in sys.argv:
-        grid = [(0, "", 0, ""), (96, "o,down,qkv1", 0, ""), (96, "o,down,qkv1", 64, "gu"),
-                (96, "o,down,qkv1", 112, "gu"), (0, "", 0, ""), (96, "qkv1,gu", 112, "o,down"),
-                (64, "qkv1", 112, "o,down"), (96, "o,down,qkv1", 0, ""), (0, "", 0, "")]
+        grid = [(0, "", 0, ""), (96, "o,down,qkv1", 0, ""), (96, "o@x,down@x,qkv1@x", 0, ""),
+                (96, "o,down@x,qkv1", 0, ""), (0, "", 0, ""), (128, "o@x,down@x,qkv1@x", 0, ""),
+                (96, "o,down,qkv1", 0, ""), (96, "o@x,down@x,qkv1@x", 0, ""), (0, "", 0, "")]
         env_grid = os.environ.get("SWH_PROBE_GRID")
         if env_grid:  # "nwg:set:qkv_nwg:qkv_set;..."
             grid = [(int(a), b, int(c), d) for a, b, c, d in (e.split(":") for e in env_grid.split(";"))]
