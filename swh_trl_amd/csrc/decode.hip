@@ -1853,132 +1853,6 @@ int launch_lm(dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uin
 }
 
 
-// ---------------------------------------------------------------------------
-// Row-split SiLU tile kernel (decode gate/up at 64 rows, folded RMSNorm,
-// fragment-order weights, K = 32 KSC).  The tile kernel above gives a
-// 16-column tile (8 gate + 8 up rows) to ONE wave over all 64 rows: 112 MFMAs
-// and 112 LDS A-reads in one dependent chain, then a 64-row SiLU epilogue, and
-// 5 of a workgroup's 8 waves idle (608 tiles on 256 workgroups).  Here a tile
-// is four tasks, one per 16-row group: wave w runs tasks w, w + 8, ... of its
-// workgroup's tiles (tile j of the workgroup, row group r = task & 3), so every
-// wave works and each chain is 28 MFMAs; the four waves of a tile load the same
-// weight fragments (one 1 KB run per load: the first miss fills L1/L2 for the
-// others).  Same MFMA accumulation order per output, same row scale, same SiLU
-// rounding, same output layout: bit-identical to lm_head_kernel<2, EPI_SILU>.
-// ---------------------------------------------------------------------------
-template <int KSC>
-__global__ __launch_bounds__(512) void silu_rows_kernel(const uint16_t *__restrict__ x, const uint16_t *__restrict__ w,
-                                                        int M, int N, int K, float eps, const float *__restrict__ ss_in,
-                                                        uint16_t *__restrict__ y, int ldy, int yf) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    constexpr int NT = 512, NW = 8;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int rl = lane & 15, kq = (lane >> 4) * 8, g = lane >> 4;
-    const int nmt = (M + 63) / 64, mt = blockIdx.x % nmt, m0 = mt * 64;
-    const int wgs = gridDim.x / nmt, wg = blockIdx.x / nmt;
-    const int ntile = N / 8, RS = K * 2 + 16;
-    float *rstd_s = reinterpret_cast<float *>(lds);                           // [64]
-    uint16_t *yt = reinterpret_cast<uint16_t *>(lds + 256) + wid * 128;      // per wave [16 rows][8 cols]
-    unsigned char *xs = lds + 4096;                                          // X image [64][RS]
-    const int ntw = ntile > wg ? (ntile - wg + wgs - 1) / wgs : 0;           // this workgroup's tiles
-    const int ntask = 4 * ntw;
-    uint4 bv[KSC];
-    auto issue = [&](int task) {
-        const int t = wg + wgs * (task >> 2);
-        const uint16_t *wr = w + ((int64_t)t * KSC * 64 + lane) * 8;
-#pragma unroll
-        for (int ks = 0; ks < KSC; ++ks) bv[ks] = ld_w(wr + ks * 512);
-    };
-    int task = wid;
-    if (task < ntask) issue(task);  // the weight stream first
-    // row statistics: 8 lanes per row sum the row's chunk partials (as lm_head_kernel's reg_rstd)
-    const int nc = K / 64;
-    float4 ss8[8];
-    {
-        const int r = min(m0 + (tid >> 3), M - 1), sub = tid & 7;
-        const float4 *row = reinterpret_cast<const float4 *>(ss_in + (int64_t)r * (K / 16));
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (sub + 8 * j < nc) ss8[j] = row[sub + 8 * j];
-    }
-    const int ppr = K / 8, jpl = (ppr + 63) >> 6;
-    for (int r = wid; r < 64; r += NW) {
-        const uint16_t *src = x + (int64_t)min(m0 + r, M - 1) * K;
-        for (int j = 0; j < jpl; ++j) {
-            const int c = lane + 64 * j;
-            if (c < ppr)
-                __builtin_amdgcn_global_load_lds(src + c * 8,
-                                                 (__attribute__((address_space(3))) void *)(xs + r * RS + j * 1024),
-                                                 16, 0, 0);
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // image (and this wave's first tile) landed
-    {
-        const int r = tid >> 3, sub = tid & 7;
-        float v = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (sub + 8 * j < nc) v += ((ss8[j].x + ss8[j].y) + ss8[j].z) + ss8[j].w;
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        v += __shfl_xor(v, 4);
-        if (r < 64 && sub == 0) rstd_s[r] = rsqrtf(v / (float)K + eps);
-    }
-    lds_barrier();
-    for (; task < ntask; task += NW) {
-        const int t = wg + wgs * (task >> 2), rg = task & 3;
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        const unsigned char *xrow = xs + (rg * 16 + rl) * RS + kq * 2;
-        uint4 a[2];
-        a[0] = *reinterpret_cast<const uint4 *>(xrow);
-#pragma unroll
-        for (int ks = 0; ks < KSC; ++ks) {
-            if (ks + 1 < KSC) a[(ks + 1) & 1] = *reinterpret_cast<const uint4 *>(xrow + (ks + 1) * 64);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[ks & 1]), as_bf16x8(bv[ks]), acc, 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (task + NW < ntask) issue(task + NW);
-        // lanes rl < 8: gate column t*8+rl of rows 4g+e; lanes rl+8: the matching up column.
-        // The gate lanes finish rows e = 0, 1, the up lanes rows e = 2, 3 (16 rows x 8 columns
-        // in the wave's LDS tile), then lanes 0-15 store one row's 8 columns as 16 B.
-        const bool gl = rl < 8;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const float v = round_bf16(acc[e] * rstd_s[rg * 16 + 4 * g + e]);
-            const float u = __shfl_xor(v, 8, kWave);
-            if (gl == (e < 2)) {
-                const float gt = gl ? v : u, up = gl ? u : v;
-                yt[(4 * g + e) * 8 + (rl & 7)] = f32_to_bf16_bits(round_bf16(gt / (1.f + expf(-gt))) * up);
-            }
-        }
-        if (lane < 16) {
-            const uint4 yr = *reinterpret_cast<const uint4 *>(yt + lane * 8);
-            const int row = m0 + rg * 16 + lane, col = t * 8;
-            if (row < M) {
-                const int64_t at = yf ? (((int64_t)(row >> 4) * (N >> 5) + (col >> 5)) * 64 +
-                                         ((col >> 3) & 3) * 16 + (row & 15)) * 8
-                                      : (int64_t)row * ldy + col;
-                *reinterpret_cast<uint4 *>(y + at) = yr;
-            }
-        }
-    }
-}
-
-template <int KSC>
-int launch_silu_rows(dim3 grid, hipStream_t s, const uint16_t *X, const uint16_t *W, int M, int N, int K, float eps,
-                     const float *ss_in, uint16_t *Y, int ldy, int yf) {
-    static bool attr = false;
-    const size_t lds = 4096 + (size_t)64 * (K * 2 + 16);
-    if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&silu_rows_kernel<KSC>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-            return SWH_E_LAUNCH;
-        attr = true;
-    }
-    silu_rows_kernel<KSC><<<grid, 512, lds, s>>>(X, W, M, N, K, eps, ss_in, Y, ldy, yf);
-    return launch_status();
-}
-
 // the tile kernel for plain / bias / SiLU epilogues
 template <int EPI, bool BIAS>
 int launch_tiles(int nm, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W, int M, int N,
@@ -2139,11 +2013,6 @@ static int decode_gemm_impl(const void *x, const void *w, int64_t M, int64_t N, 
             const auto *Bs = static_cast<const uint16_t *>(bias);
             auto *Y = static_cast<uint16_t *>(y);
             const size_t lds = (size_t)L.total + (silu ? 8 : 16) * 1024;  // + the epilogue's 1 / 2 KB per wave
-            // row-split SiLU tiles (every wave a 16-row task; SWH_GU_ROWSPLIT=0: one wave per tile)
-            const char *rse = getenv("SWH_GU_ROWSPLIT");
-            const bool rsplit = rse && rse[0] == '1';  // measured slower (11.65 vs 11.08 us): off
-            if (silu && rsplit && nm == 2 && fw && K == 896 && ss_in)
-                return launch_silu_rows<28>(grid, s, X, W, (int)M, (int)N, (int)K, eps, ss_in, Y, (int)ldy, act & 1);
             if (silu) return launch_tiles<EPI_SILU, false>(nm, grid, lds, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Bs, Y, (int)ldy, fw, act & 1);
             if (Bs) return launch_tiles<EPI_PLAIN, true>(nm, grid, lds, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Bs, Y, (int)ldy, fw);
             return launch_tiles<EPI_PLAIN, false>(nm, grid, lds, s, X, W, (int)M, (int)N, (int)K, NWt, eps, ss_in, Bs, Y, (int)ldy, fw);

@@ -1586,31 +1586,3 @@ def test_wide_gemm_tilings_agree(ops, dev, monkeypatch, name, N, K):
     torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-2)
     assert (a != b).float().mean().item() < 0.02
 
-
-@pytest.mark.parametrize("M", [64, 48, 128, 37])
-def test_silu_rows_equals_tile_kernel(ops, dev, monkeypatch, M):
-    """The row-split SiLU tile kernel (every wave one 16-row task of a tile,
-    swh_decode_gemm_fragw's gate/up at K 896 with the folded norm's chunk sums)
-    equals the one-wave-per-tile kernel (SWH_GU_ROWSPLIT=0) bit for bit, in the
-    row-major and the fragment-order output layouts, and the reference within
-    bf16 rounding."""
-    from swh_trl_amd import nn_ops
-    g = _gen(61 + M)
-    H, I = 896, 4864
-    x = torch.randn(M, H, generator=g).to(torch.bfloat16).to(dev)
-    wraw = (torch.randn(2 * I, H, generator=g) * H ** -0.5).to(torch.bfloat16).to(dev)
-    wgu = nn_ops.frag_pack(wraw, silu=True)
-    ss = _chunk_ss(x)
-    outs = {}
-    for flag in ("1", "0"):
-        monkeypatch.setenv("SWH_GU_ROWSPLIT", flag)
-        outs[flag] = [nn_ops.decode_gemm_fragw(x, wgu, silu=True, ss_in=ss, eps=1e-6)]
-        if M % 16 == 0:
-            outs[flag].append(nn_ops.decode_gemm_fragw(x, wgu, silu=True, ss_in=ss, eps=1e-6, act_frag=1))
-    torch.cuda.synchronize()
-    for a, b in zip(outs["1"], outs["0"]):
-        assert torch.equal(a, b)
-    xn = (x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-6))
-    gu = xn @ wraw.float().t()
-    ref = torch.nn.functional.silu(gu[:, :I]) * gu[:, I:]
-    torch.testing.assert_close(outs["1"][0].float(), ref, rtol=3e-2, atol=3e-2)
