@@ -1586,3 +1586,40 @@ def test_wide_gemm_tilings_agree(ops, dev, monkeypatch, name, N, K):
     torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-2)
     assert (a != b).float().mean().item() < 0.02
 
+
+
+@pytest.mark.parametrize("B,Hkv,G", [(64, 2, 8), (24, 2, 8), (12, 1, 4)])
+def test_attn_decode_xcd_rows_is_a_permutation(ops, dev, monkeypatch, B, Hkv, G):
+    """The XCD-contiguous order of the attention workgroups (SWH_ATTN_XCD_ROWS=1,
+    applied when Hkv x B % 8 == 0) only permutes which workgroup computes
+    which (row, KV head): output and appended K/V slot equal the plain order bit
+    for bit, shared prompt rows and left padding included, with and without
+    warm-up workgroups in the launch."""
+    from swh_trl_amd import nn_ops
+    g = _gen(77 + B)
+    D, P, step = 64, 40, 9
+    Hq, Tmax = 7 * Hkv, P + step + 8
+    plen = torch.tensor([P - (i % 5) for i in range(B // G)], dtype=torch.int32).repeat_interleave(G).to(dev)
+    kc = torch.randn(B, Hkv, Tmax, D, generator=g).to(torch.bfloat16).to(dev)
+    vc = torch.randn(B, Hkv, Tmax, D, generator=g).to(torch.bfloat16).to(dev)
+    qkv = torch.randn(B, (Hq + 2 * Hkv) * D, generator=g).to(torch.bfloat16).to(dev)
+    cos, sin = _rope_tables(D, 2048, 1e6, dev)
+    state = torch.tensor([step + 1, P], dtype=torch.int32, device=dev)
+    prow = torch.arange(0, B, G, device=dev).repeat_interleave(G).to(torch.int32)
+    junk = torch.randn(1 << 16, device=dev)
+    jobs = torch.tensor([junk.data_ptr(), junk.numel() * 4 // 16, 0], dtype=torch.int64).to(dev)
+    sink = torch.zeros(64 * 512, dtype=torch.int32, device=dev)
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SWH_ATTN_XCD_ROWS", flag)
+        k2, v2 = kc.clone(), vc.clone()
+        a = nn_ops.attn_decode(qkv, k2, v2, cos, sin, plen, state, Hq, Hkv, D, D ** -0.5, prompt_row=prow)
+        k3, v3 = kc.clone(), vc.clone()
+        out = torch.empty_like(a)
+        nn_ops.attn_decode_l3(qkv, k3, v3, cos, sin, plen, state, Hq, Hkv, D, D ** -0.5, out, prow, False, jobs, 32,
+                              sink)
+        res[flag] = (a, k2, v2, out, k3, v3)
+    torch.cuda.synchronize()
+    for x, y in zip(res["1"], res["0"]):
+        assert torch.equal(x, y)
+    assert torch.equal(res["1"][0], res["1"][3])
