@@ -370,7 +370,11 @@ class DecodeEngine:
                  "qkv1": (1, "qkv_w"), "o1": (1, "o_w"), "gu1": (1, "gu_w"), "down1": (1, "down_w")}
         # "name@x": striped by 16-row column block (fragment-order weights), block c warmed
         # on the XCD the consuming launch runs it on (c % 8)
-        sel = [(*names[k.strip().split("@")[0]], k.strip().endswith("@x")) for k in spec.split(",") if k.strip()]
+        keys = [k.strip() for k in spec.split(",") if k.strip()]
+        bad = [k for k in keys if k.split("@")[0] not in names or k.count("@") > 1 or ("@" in k and k[-2:] != "@x")]
+        if bad:
+            raise ValueError(f"warm-up set {spec!r}: unknown entries {bad} (expected {sorted(names)}, optional @x)")
+        sel = [(*names[k.split("@")[0]], k.endswith("@x")) for k in keys]
         tabs = []
         for i in range(L):
             t = []
