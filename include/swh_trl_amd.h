@@ -575,6 +575,24 @@ int swh_attn_decode_l3(const void *qkv, void *k_cache, void *v_cache, const floa
  * model.generate, exceeds the 256 MiB Infinity Cache).  nontemporal: nt loads. */
 int swh_l3_prefetch(const void *jobs, int32_t njobs, int32_t nwg, int32_t nontemporal, void *sink, void *stream);
 
+/* swh_frag_pack with kmajor = 1: the same 1 KB fragments with the k-step
+ * outermost (piece (ks * G + g) * 64 + lane, G = 16-row groups), so the lm-head
+ * tile kernel's waves that load k-step ks of consecutive tiles read one
+ * contiguous run; kmajor = 0 is swh_frag_pack. */
+int swh_frag_pack_kmajor(const void *w, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst,
+                         int32_t kmajor, void *stream);
+/* swh_lm_head_sample_fragw / swh_lm_head_sample_step_fragw over the k-major
+ * layout of swh_frag_pack_kmajor(..., 1, ...): same draws. */
+int swh_lm_head_sample_fragk(const void *x, const void *w, int64_t M, int64_t V, int64_t K, float eps,
+                             const float *ss_in, const swh_sample_params *params, const uint64_t *rng,
+                             const int32_t *step, int32_t *finished, int64_t *out_tokens, int64_t out_ld,
+                             int64_t *cur_tokens, void *workspace, int64_t workspace_bytes, void *stream);
+int swh_lm_head_sample_step_fragk(const void *x, const void *w, int64_t M, int64_t V, int64_t K, float eps,
+                                  const float *ss_in, const swh_sample_params *params, const uint64_t *rng,
+                                  int32_t *step, int32_t *finished, int64_t *out_tokens, int64_t out_ld,
+                                  int64_t *cur_tokens, const void *embed, void *x_next, float *ss_next,
+                                  void *workspace, int64_t workspace_bytes, void *stream);
+
 /* ---- GPT-2 family (BASELINE.json config 1) --------------------------------
  * transformers GPT2Block's LayerNorms and NewGELUActivation (the modeling code
  * the reference's tiny-random-GPT2 tests run through grpo_trainer.py:1249 /

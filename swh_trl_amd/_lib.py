@@ -135,6 +135,13 @@ SIGNATURES = {
     "swh_wide_gemm_packed": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_f32, c_vp, c_vp, c_i32, c_vp, c_i64, c_vp,
                                      c_vp, c_vp, c_i64, c_vp]),
     "swh_l3_prefetch": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp]),
+    "swh_frag_pack_kmajor": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i32, c_vp, c_i32, c_vp]),
+    "swh_lm_head_sample_step_fragk": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_f32, c_vp, C.POINTER(SampleParams),
+                                              c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
+                                              c_vp]),
+    "swh_lm_head_sample_fragk": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_f32, c_vp, C.POINTER(SampleParams),
+                                         c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
+
     "swh_decode_gemm_fragw_l3": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_f32, c_vp, c_vp, c_i32, c_vp, c_i64,
                                          c_vp, c_vp, c_i32, c_vp, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp]),
     "swh_attn_decode_l3": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32,

@@ -35,7 +35,8 @@ int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, flo
 int64_t wide_gemm_slab_bytes(int64_t M, int64_t N, int64_t K, int32_t silu);
 bool wide_gemm_eligible(int64_t M, int64_t N, int64_t K, int32_t silu);
 int wide_pack(const void *src, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, hipStream_t stream);
-int frag_pack(const void *src, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, hipStream_t stream);
+int frag_pack(const void *src, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, hipStream_t stream,
+              int32_t kmajor = 0);
 
 namespace {
 
@@ -851,9 +852,12 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
         if constexpr (EPI == EPI_SILU) return (rl < 8) ? tile * 8 + rl : N + tile * 8 + rl - 8;  // gate, then up
         return (int64_t)tile * 16 + rl;
     };
-    // fw: tile t's fragments for k-step ks at ((t KS + ks) 64 + lane) 8 (one 1 KB run per load)
-    const int wst = smp.fw ? 512 : 32;
+    // fw 1: tile t's fragments for k-step ks at ((t KS + ks) 64 + lane) 8 (one 1 KB run per load);
+    // fw 2 (k-major): at ((ks ntile + t) 64 + lane) 8, so the waves loading k-step ks of
+    // consecutive tiles read one contiguous run
+    const int64_t wst = smp.fw == 2 ? (int64_t)ntile * 512 : smp.fw ? 512 : 32;
     auto wbase = [&](int tile) -> const uint16_t * {
+        if (smp.fw == 2) return w + ((int64_t)tile * 64 + lane) * 8;
         return smp.fw ? w + ((int64_t)tile * KS * 64 + lane) * 8 : w + wrow_of(tile) * K + kq;
     };
     auto issue = [&](int tile) {
@@ -1992,6 +1996,12 @@ static int decode_gemm_impl(const void *x, const void *w, int64_t M, int64_t N, 
                             const float *ss_in, float *ss_out, void *workspace, int64_t workspace_bytes, void *stream,
                             int fw, int act = 0, const L3Warm *warm = nullptr) {
     if (fw && (norm_w || K % 128)) return SWH_E_ARG;
+    // act bit 2: W in the k-major fragment order (swh_frag_pack_kmajor; tile path only)
+    if (act & 4) {
+        if (!fw) return SWH_E_ARG;
+        fw = 2;
+        act &= 3;
+    }
     // act bit 0: the SiLU output in fragment order (tile path only); bit 1: X in fragment order (xstream only)
     if (act & ~3 || ((act & 1) && (!silu || N % 32 || M % 16)) || ((act & 2) && (!residual || M % 16 || K % 32)))
         return SWH_E_ARG;
@@ -2041,6 +2051,7 @@ static int decode_gemm_impl(const void *x, const void *w, int64_t M, int64_t N, 
         }
     }
     if (act & 1) return SWH_E_ARG;  // the fragment-order SiLU output comes from the tile kernel only
+    if (fw == 2) return SWH_E_ARG;  // k-major weights: the tile kernel only
     GemmCfg c = pick_cfg(M, wcols, K, silu != 0, nm);
     c.fw = fw;
     c.xf = (act & 2) ? 1 : 0;
@@ -2139,6 +2150,15 @@ extern "C" int swh_frag_pack(const void *w, const void *norm_w, int64_t N, int64
     if ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(norm_w)) & 15)
         return SWH_E_ARG;
     return frag_pack(w, norm_w, N, K, silu, dst, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int swh_frag_pack_kmajor(const void *w, const void *norm_w, int64_t N, int64_t K, int32_t silu,
+                                    void *dst, int32_t kmajor, void *stream) {
+    const int64_t rows = silu ? 2 * N : N;
+    if (!w || !dst || w == dst || N <= 0 || rows % 16 || (silu && N % 8) || K <= 0 || K % 128) return SWH_E_ARG;
+    if ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(norm_w)) & 15)
+        return SWH_E_ARG;
+    return (kmajor & ~1) ? SWH_E_ARG : frag_pack(w, norm_w, N, K, silu, dst, static_cast<hipStream_t>(stream), kmajor);
 }
 
 // [partials (M x per x 8 LmPart) | 256 B: the finalize ticket (zero at allocation)]
@@ -2276,6 +2296,25 @@ extern "C" int swh_lm_head_sample_step_fragw(const void *x, const void *w, int64
                                              int64_t workspace_bytes, void *stream) {
     return lm_head_sample_step_impl(x, w, M, V, K, nullptr, eps, ss_in, params, rng, step, finished, out_tokens,
                                     out_ld, cur_tokens, embed, x_next, ss_next, workspace, workspace_bytes, stream, 1);
+}
+
+// the two entries above over the k-major fragment order (swh_frag_pack_kmajor(..., 1, ...)): same draws
+extern "C" int swh_lm_head_sample_fragk(const void *x, const void *w, int64_t M, int64_t V, int64_t K, float eps,
+                                        const float *ss_in, const swh_sample_params *params, const uint64_t *rng,
+                                        const int32_t *step, int32_t *finished, int64_t *out_tokens, int64_t out_ld,
+                                        int64_t *cur_tokens, void *workspace, int64_t workspace_bytes, void *stream) {
+    return lm_head_sample_impl(x, w, M, V, K, nullptr, eps, ss_in, params, rng, step, finished, out_tokens, out_ld,
+                               cur_tokens, workspace, workspace_bytes, LmNext{}, stream, 2);
+}
+
+extern "C" int swh_lm_head_sample_step_fragk(const void *x, const void *w, int64_t M, int64_t V, int64_t K,
+                                             float eps, const float *ss_in, const swh_sample_params *params,
+                                             const uint64_t *rng, int32_t *step, int32_t *finished,
+                                             int64_t *out_tokens, int64_t out_ld, int64_t *cur_tokens,
+                                             const void *embed, void *x_next, float *ss_next, void *workspace,
+                                             int64_t workspace_bytes, void *stream) {
+    return lm_head_sample_step_impl(x, w, M, V, K, nullptr, eps, ss_in, params, rng, step, finished, out_tokens,
+                                    out_ld, cur_tokens, embed, x_next, ss_next, workspace, workspace_bytes, stream, 2);
 }
 
 namespace swh {

@@ -185,6 +185,13 @@ class DecodeEngine:
         # streamed A operand as contiguous 1 KB runs); SWH_ATT_FRAG=0 keeps it row-major
         self.att_frag = (os.environ.get("SWH_ATT_FRAG", "1") != "0" and B % 16 == 0 and c.q_dim % 32 == 0 and
                          all(f"l{i}.o_w" in self.fragw for i in range(c.num_hidden_layers)))
+        # the lm head's fragment-order copy with the k-step outermost (swh_frag_pack_kmajor):
+        # the sampler's waves loading k-step ks of consecutive tiles read one contiguous run
+        # (SWH_LM_KMAJOR=1; the logits path below keeps the tile-major copy)
+        self.lm_kmajor = os.environ.get("SWH_LM_KMAJOR", "0") != "0"
+        # the same for the gate/up copies (SWH_GU_KMAJOR=1): the tile kernel's waves load
+        # k-step ks of consecutive tiles together
+        self.gu_kmajor = os.environ.get("SWH_GU_KMAJOR", "0") != "0"
         self.graph = None
         self.graph_k = None
         self._prefill_graphs = {}
@@ -284,7 +291,8 @@ class DecodeEngine:
         projs = self._projections()
         for name, buf in self.fragw.items():
             N, K, silu, norm = projs[name]
-            nn_ops.frag_pack(self._weight(name), self.model.p[norm] if norm else None, silu=silu, out=buf)
+            nn_ops.frag_pack(self._weight(name), self.model.p[norm] if norm else None, silu=silu, out=buf,
+                             kmajor=self._kmajor(name))
         if not self.fold:
             return
         if not getattr(self, "_fold_built", False):
@@ -306,7 +314,7 @@ class DecodeEngine:
     def _lm_head_weight(self):
         """(weight, norm_w, fragment order?) the fused lm-head sampler reads."""
         if "lm" in self.fragw:
-            return self.fragw["lm"], None, True
+            return self.fragw["lm"], None, 2 if self.lm_kmajor else 1
         return (*self._normed("lm", "norm"), False)
 
     def _proj(self, name: str, x: torch.Tensor, **kw):
@@ -318,7 +326,9 @@ class DecodeEngine:
         if name in self.fragw:
             if self.act_frag and name.endswith(("gu_w", "down_w")):
                 kw["act_frag"] = 1 if name.endswith("gu_w") else 2
-            elif "act_frag" in kw and not name.endswith("o_w"):
+            if self._kmajor(name):
+                kw["act_frag"] = kw.get("act_frag", 0) | 4  # the k-major copy (tile kernel)
+            elif "act_frag" in kw and not name.endswith("o_w") and name != "lm":
                 raise ValueError(f"{name}: act_frag serves gate/up, down and o only")
             return nn_ops.decode_gemm_fragw(x, self.fragw[name], eps=eps, **kw)
         norm = self._projections()[name][3]
@@ -337,6 +347,10 @@ class DecodeEngine:
         cus = torch.cuda.get_device_properties(self.dev).multi_processor_count
         per_layer = 2 * c.hidden_size * (c.q_dim + c.intermediate_size + c.qkv_dim)
         return 96 if self.B * c.num_key_value_heads + 96 <= cus and per_layer <= (64 << 20) else 0
+
+    def _kmajor(self, name: str) -> bool:
+        """Is `name`'s fragment-order copy k-major (swh_frag_pack_kmajor)?"""
+        return (name == "lm" and self.lm_kmajor) or (name.endswith("gu_w") and self.gu_kmajor)
 
     def _proj_weight(self, name: str) -> torch.Tensor:
         """The buffer _proj streams for a projection."""

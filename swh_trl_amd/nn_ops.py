@@ -182,14 +182,18 @@ def decode_gemm(x: torch.Tensor, w: torch.Tensor, *, norm_w: Optional[torch.Tens
 
 
 def frag_pack(w: torch.Tensor, norm_w: Optional[torch.Tensor] = None, *, silu: bool = False,
-              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+              out: Optional[torch.Tensor] = None, kmajor: bool = False) -> torch.Tensor:
     """w [N, K] ([2N, K] gate|up with silu; K % 128 == 0), optionally folded
     with the RMSNorm weight, in the MFMA-fragment order decode_gemm_fragw reads
-    (swh_frag_pack); same shape as w."""
+    (swh_frag_pack); kmajor: k-step outermost (swh_frag_pack_kmajor, the lm-head
+    sampler's fragw=2 layout); same shape as w."""
     _dev(w, "frag_pack")
     rows, K = w.shape
     N = rows // 2 if silu else rows
     out = torch.empty_like(w) if out is None else out
+    if kmajor:
+        call("swh_frag_pack_kmajor", w.data_ptr(), _p(norm_w), N, K, int(bool(silu)), out.data_ptr(), 1, _stream())
+        return out
     call("swh_frag_pack", w.data_ptr(), _p(norm_w), N, K, int(bool(silu)), out.data_ptr(), _stream())
     return out
 
@@ -272,10 +276,10 @@ def lm_head_sample_supported(params, V: int, K: int) -> bool:
 def lm_head_sample(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Tensor, step: torch.Tensor,
                    finished: torch.Tensor, out_tokens: torch.Tensor, cur_tokens: Optional[torch.Tensor] = None, *,
                    norm_w: Optional[torch.Tensor] = None, eps: float = 1e-6, ss_in: Optional[torch.Tensor] = None,
-                   workspace: Optional[torch.Tensor] = None, fragw: bool = False) -> torch.Tensor:
+                   workspace: Optional[torch.Tensor] = None, fragw: int = 0) -> torch.Tensor:
     """lm head + the unfiltered sampler in one pass, no logits tensor
-    (include/swh_trl_amd.h swh_lm_head_sample; fragw: w packed by frag_pack,
-    swh_lm_head_sample_fragw).  Writes out_tokens[:, *step], cur_tokens,
+    (include/swh_trl_amd.h swh_lm_head_sample; fragw 1: w packed by frag_pack,
+    swh_lm_head_sample_fragw; 2: by frag_pack(kmajor=True), swh_lm_head_sample_fragk).  Writes out_tokens[:, *step], cur_tokens,
     finished; returns out_tokens."""
     import ctypes
     _dev(x, "lm_head_sample")
@@ -287,7 +291,8 @@ def lm_head_sample(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Tensor, 
     head = (x.data_ptr(), w.data_ptr(), M, V, K) + (() if fragw else (_p(norm_w),)) + (float(eps), _p(ss_in))
     if fragw and norm_w is not None:
         raise ValueError("lm_head_sample: a fragment-order weight carries the folded norm (norm_w must be None)")
-    call("swh_lm_head_sample_fragw" if fragw else "swh_lm_head_sample", *head,
+    call(("swh_lm_head_sample_fragk" if fragw == 2 else "swh_lm_head_sample_fragw") if fragw else "swh_lm_head_sample",
+         *head,
          ctypes.byref(params), rng.data_ptr(), step.data_ptr(), finished.data_ptr(), out_tokens.data_ptr(),
          out_tokens.stride(0), _p(cur_tokens), workspace.data_ptr(), workspace.numel(), _stream())
     return out_tokens
@@ -297,7 +302,7 @@ def lm_head_sample_step(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Ten
                         finished: torch.Tensor, out_tokens: torch.Tensor, cur_tokens: torch.Tensor,
                         embed: torch.Tensor, x_next: torch.Tensor, ss_next: Optional[torch.Tensor], *,
                         norm_w: Optional[torch.Tensor] = None, eps: float = 1e-6, ss_in: Optional[torch.Tensor] = None,
-                        workspace: torch.Tensor, fragw: bool = False) -> torch.Tensor:
+                        workspace: torch.Tensor, fragw: int = 0) -> torch.Tensor:
     """lm_head_sample + the next step's input: x_next = embed[drawn token]
     (+ RMSNorm partials ss_next) and *step += 1 once every row has read it
     (include/swh_trl_amd.h swh_lm_head_sample_step).  `workspace` must have
@@ -311,7 +316,8 @@ def lm_head_sample_step(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Ten
     if fragw and norm_w is not None:
         raise ValueError("lm_head_sample_step: a fragment-order weight carries the folded norm (norm_w must be None)")
     head = (x.data_ptr(), w.data_ptr(), M, V, K) + (() if fragw else (_p(norm_w),)) + (float(eps), _p(ss_in))
-    call("swh_lm_head_sample_step_fragw" if fragw else "swh_lm_head_sample_step", *head,
+    call(("swh_lm_head_sample_step_fragk" if fragw == 2 else "swh_lm_head_sample_step_fragw") if fragw
+         else "swh_lm_head_sample_step", *head,
          ctypes.byref(params), rng.data_ptr(), step.data_ptr(), finished.data_ptr(), out_tokens.data_ptr(),
          out_tokens.stride(0), cur_tokens.data_ptr(), embed.data_ptr(), x_next.data_ptr(), _p(ss_next),
          workspace.data_ptr(), workspace.numel(), _stream())

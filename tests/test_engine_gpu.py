@@ -983,3 +983,31 @@ def test_qkv_l3_warmup_generates_identically(dev, monkeypatch):
             for x, y in zip(a, b):
                 if isinstance(x, torch.Tensor):
                     assert torch.equal(x, y)
+
+
+def test_lm_kmajor_generates_identically(dev, monkeypatch):
+    """The lm head's and gate/up's fragment-order copies with the k-step
+    outermost (swh_frag_pack_kmajor; SWH_LM_KMAJOR=1, SWH_GU_KMAJOR=1) draw the
+    same tokens as the tile-major copies through the fused sampler, and the
+    logits path over them (log-probs, top-p) is unchanged too."""
+    from swh_trl_amd.engine import CausalLM, DecodeEngine, tiny_qwen2
+    m = CausalLM(tiny_qwen2(2048, 2), dev, seed=12)
+    g = torch.Generator().manual_seed(12)
+    B, P, C = 32, 10, 16
+    ids = torch.randint(0, m.cfg.vocab_size, (B, P), generator=g).to(dev)
+    mask = torch.ones(B, P, dtype=torch.int64, device=dev)
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SWH_LM_KMAJOR", flag)
+        monkeypatch.setenv("SWH_GU_KMAJOR", flag)
+        eng = DecodeEngine(m, B, P, C)
+        assert eng.lm_kmajor == eng.gu_kmajor == (flag == "1")
+        outs[flag] = (eng.generate(ids, mask, C, greedy=True),
+                      eng.generate(ids, mask, C, temperature=0.9, seed=5),
+                      eng.generate(ids, mask, C, temperature=0.9, seed=5, return_logp=True),
+                      eng.generate(ids, mask, C, temperature=0.9, top_p=0.8, seed=5))
+        del eng
+    for a, b in zip(outs["1"], outs["0"]):
+        for x, y in zip(a, b):
+            if isinstance(x, torch.Tensor):
+                assert torch.equal(x, y)
