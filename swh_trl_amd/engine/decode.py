@@ -326,10 +326,10 @@ class DecodeEngine:
         if name in self.fragw:
             if self.act_frag and name.endswith(("gu_w", "down_w")):
                 kw["act_frag"] = 1 if name.endswith("gu_w") else 2
+            elif "act_frag" in kw and not name.endswith("o_w"):
+                raise ValueError(f"{name}: act_frag serves gate/up, down and o only")
             if self._kmajor(name):
                 kw["act_frag"] = kw.get("act_frag", 0) | 4  # the k-major copy (tile kernel)
-            elif "act_frag" in kw and not name.endswith("o_w") and name != "lm":
-                raise ValueError(f"{name}: act_frag serves gate/up, down and o only")
             return nn_ops.decode_gemm_fragw(x, self.fragw[name], eps=eps, **kw)
         norm = self._projections()[name][3]
         if norm is None:
@@ -349,8 +349,17 @@ class DecodeEngine:
         return 96 if self.B * c.num_key_value_heads + 96 <= cus and per_layer <= (64 << 20) else 0
 
     def _kmajor(self, name: str) -> bool:
-        """Is `name`'s fragment-order copy k-major (swh_frag_pack_kmajor)?"""
-        return (name == "lm" and self.lm_kmajor) or (name.endswith("gu_w") and self.gu_kmajor)
+        """Is `name`'s fragment-order copy k-major (swh_frag_pack_kmajor)?  Only
+        shapes decode_gemm runs on its tile kernel (K <= 1024 and >= 8 tiles per
+        CU for the lm head's logits path, >= 1 SiLU tile per CU for gate/up;
+        csrc/decode.hip decode_gemm_impl) take it."""
+        c = self.cfg
+        cus = torch.cuda.get_device_properties(self.dev).multi_processor_count
+        if c.hidden_size > 1024:
+            return False
+        if name == "lm":
+            return self.lm_kmajor and c.vocab_size // 16 >= 8 * cus
+        return name.endswith("gu_w") and self.gu_kmajor and c.intermediate_size // 8 >= cus
 
     def _proj_weight(self, name: str) -> torch.Tensor:
         """The buffer _proj streams for a projection."""

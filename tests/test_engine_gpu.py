@@ -991,7 +991,12 @@ def test_lm_kmajor_generates_identically(dev, monkeypatch):
     same tokens as the tile-major copies through the fused sampler, and the
     logits path over them (log-probs, top-p) is unchanged too."""
     from swh_trl_amd.engine import CausalLM, DecodeEngine, tiny_qwen2
-    m = CausalLM(tiny_qwen2(2048, 2), dev, seed=12)
+    from swh_trl_amd.engine import DecoderConfig
+    # widths on decode_gemm's tile kernel: V / 16 >= 8 tiles per CU, I / 8 >= 1 per CU
+    cfg = DecoderConfig(vocab_size=40960, hidden_size=256, intermediate_size=2304, num_hidden_layers=2,
+                        num_attention_heads=4, num_key_value_heads=2, head_dim=64, rope_theta=10000.0,
+                        max_position_embeddings=4096, tie_word_embeddings=True)
+    m = CausalLM(cfg, dev, seed=12, init_std=0.05)
     g = torch.Generator().manual_seed(12)
     B, P, C = 32, 10, 16
     ids = torch.randint(0, m.cfg.vocab_size, (B, P), generator=g).to(dev)
@@ -1001,7 +1006,7 @@ def test_lm_kmajor_generates_identically(dev, monkeypatch):
         monkeypatch.setenv("SWH_LM_KMAJOR", flag)
         monkeypatch.setenv("SWH_GU_KMAJOR", flag)
         eng = DecodeEngine(m, B, P, C)
-        assert eng.lm_kmajor == eng.gu_kmajor == (flag == "1")
+        assert eng._kmajor("lm") == eng._kmajor("l0.gu_w") == (flag == "1")
         outs[flag] = (eng.generate(ids, mask, C, greedy=True),
                       eng.generate(ids, mask, C, temperature=0.9, seed=5),
                       eng.generate(ids, mask, C, temperature=0.9, seed=5, return_logp=True),
