@@ -825,8 +825,11 @@ struct LmSample {
 // compiler pipelines the A-fragment LDS reads across k-steps and waits on each
 // weight load in turn (vmcnt(k)), instead of one LDS round trip per MFMA
 // behind a wait for the whole tile (the lm head ran 5.6 us of MFMA per tile).
-template <int NM, int EPI, bool BIAS, bool SAMPLE, int KSC>
-__global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict__ x, const uint16_t *__restrict__ w,
+// RD: weight-ring depth in k-steps (0: the whole tile, KSC).  RD = KSC / 2 holds half a
+// tile per wave (the k-steps ks + RD of the same tile, then the next tile's, refill each
+// register), which fits three 12-wave... waves per SIMD: 768-thread workgroups.
+template <int NM, int EPI, bool BIAS, bool SAMPLE, int KSC, int RD = 0>
+__global__ __launch_bounds__(RD ? 768 : 512) void lm_head_kernel(const uint16_t *__restrict__ x, const uint16_t *__restrict__ w,
                                                       int M, int N, int K, const uint16_t *__restrict__ norm_w,
                                                       float eps, const float *__restrict__ ss_in,
                                                       const uint16_t *__restrict__ bias, uint16_t *__restrict__ y,
@@ -847,7 +850,9 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
     int t = wg + wgs * wid;  // tile t -> workgroup t % wgs
     SWH_GEMM_TRACE(0);
 
-    uint4 bv[KSA];
+    static_assert(RD == 0 || (KSC != 0 && KSC % RD == 0 && 2 * RD == KSC), "RD: half of a compile-time tile");
+    constexpr int KR = RD ? RD : KSA;  // weight registers per lane
+    uint4 bv[KR];
     auto wrow_of = [&](int tile) -> int64_t {
         if constexpr (EPI == EPI_SILU) return (rl < 8) ? tile * 8 + rl : N + tile * 8 + rl - 8;  // gate, then up
         return (int64_t)tile * 16 + rl;
@@ -863,7 +868,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
     auto issue = [&](int tile) {
         const uint16_t *wr = wbase(tile);
 #pragma unroll
-        for (int ks = 0; ks < KSA; ++ks)
+        for (int ks = 0; ks < KR; ++ks)
             if (KSC || ks < KS) bv[ks] = ld_w(wr + ks * wst);
     };
     if (t < ntile) issue(t);  // the weight stream first
@@ -1011,6 +1016,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
         // soon as its MFMA has read it, so a wave always has KS loads in flight
         const bool ring = SWH_LM_RING && KSC != 0 && t + tstep < ntile;
         const uint16_t *wnext = wbase(ring ? t + tstep : t);
+        const uint16_t *wcur = wbase(t);
         if constexpr (KSC != 0) {
             // A fragments double-buffered one k-step ahead; the scheduling barrier
             // keeps the compiler from hoisting every read (register pressure)
@@ -1026,9 +1032,14 @@ __global__ __launch_bounds__(512) void lm_head_kernel(const uint16_t *__restrict
                 }
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[ks & 1][i]), as_bf16x8(bv[ks]),
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[ks & 1][i]), as_bf16x8(bv[ks % KR]),
                                                                     acc[i], 0, 0, 0);
-                if (ring) bv[ks] = ld_w(wnext + ks * wst);
+                if constexpr (RD != 0) {  // half-tile ring: this tile's second half, then the next tile's first
+                    if (ks + KR < KSC) bv[ks % KR] = ld_w(wcur + (ks + KR) * wst);
+                    else if (ring) bv[ks % KR] = ld_w(wnext + (ks + KR - KSC) * wst);
+                } else if (ring) {
+                    bv[ks] = ld_w(wnext + ks * wst);
+                }
                 __builtin_amdgcn_sched_barrier(0);
             }
         } else {
@@ -1849,19 +1860,27 @@ int launch_gemm_ms(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const
     }
 }
 
-template <int NM, int EPI, bool BIAS, bool SAMPLE, int KSC>
+template <int NM, int EPI, bool BIAS, bool SAMPLE, int KSC, int RD = 0>
 int launch_lm_ks(dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W, int M, int N, int K,
                  const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs, uint16_t *Y, int ldy,
                  const LmSample &smp) {
     static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in once per kernel
     if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&lm_head_kernel<NM, EPI, BIAS, SAMPLE, KSC>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&lm_head_kernel<NM, EPI, BIAS, SAMPLE, KSC, RD>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
             return SWH_E_LAUNCH;
         attr = true;
     }
-    lm_head_kernel<NM, EPI, BIAS, SAMPLE, KSC><<<grid, 512, lds, s>>>(X, W, M, N, K, NWt, eps, ss_in, Bs, Y, ldy, smp);
+    lm_head_kernel<NM, EPI, BIAS, SAMPLE, KSC, RD><<<grid, RD ? 768 : 512, lds, s>>>(X, W, M, N, K, NWt, eps, ss_in, Bs,
+                                                                                  Y, ldy, smp);
     return launch_status();
+}
+
+// SWH_LM_RING14=1 (read per call): the fused sampler at K = 896 with the half-tile weight
+// ring and 12 waves per workgroup (three per SIMD)
+inline bool lm_ring14() {
+    const char *e = getenv("SWH_LM_RING14");
+    return e && e[0] == '1';
 }
 
 // compile-time k-step counts for the model widths in use (Qwen2.5-0.5B: H = 896)
@@ -1870,7 +1889,11 @@ int launch_lm(dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uin
               const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs, uint16_t *Y, int ldy,
               const LmSample &smp) {
     switch (K / 32) {
-    case 28: return launch_lm_ks<NM, EPI, BIAS, SAMPLE, 28>(grid, lds, s, X, W, M, N, K, NWt, eps, ss_in, Bs, Y, ldy, smp);
+    case 28:
+        if (SAMPLE && lm_ring14())
+            return launch_lm_ks<NM, EPI, BIAS, SAMPLE, 28, 14>(grid, lds, s, X, W, M, N, K, NWt, eps, ss_in, Bs, Y, ldy,
+                                                               smp);
+        return launch_lm_ks<NM, EPI, BIAS, SAMPLE, 28>(grid, lds, s, X, W, M, N, K, NWt, eps, ss_in, Bs, Y, ldy, smp);
     case 32: return launch_lm_ks<NM, EPI, BIAS, SAMPLE, 32>(grid, lds, s, X, W, M, N, K, NWt, eps, ss_in, Bs, Y, ldy, smp);
     default: return launch_lm_ks<NM, EPI, BIAS, SAMPLE, 0>(grid, lds, s, X, W, M, N, K, NWt, eps, ss_in, Bs, Y, ldy, smp);
     }

@@ -1016,3 +1016,28 @@ def test_lm_kmajor_generates_identically(dev, monkeypatch):
         for x, y in zip(a, b):
             if isinstance(x, torch.Tensor):
                 assert torch.equal(x, y)
+
+
+def test_lm_ring14_generates_identically(dev, monkeypatch):
+    """The fused lm-head sampler with the half-tile weight ring and 12 waves
+    per workgroup (SWH_LM_RING14=1, K = 896) draws the same tokens as the
+    whole-tile ring, greedy and sampled, across several tiles per wave."""
+    from swh_trl_amd.engine import CausalLM, DecoderConfig, DecodeEngine
+    cfg = DecoderConfig(vocab_size=65536, hidden_size=896, intermediate_size=1024, num_hidden_layers=1,
+                        num_attention_heads=14, num_key_value_heads=2, head_dim=64, rope_theta=10000.0,
+                        max_position_embeddings=4096, tie_word_embeddings=True)
+    m = CausalLM(cfg, dev, seed=13, init_std=0.05)
+    g = torch.Generator().manual_seed(13)
+    B, P, C = 64, 8, 12
+    ids = torch.randint(0, cfg.vocab_size, (B, P), generator=g).to(dev)
+    mask = torch.ones(B, P, dtype=torch.int64, device=dev)
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SWH_LM_RING14", flag)
+        eng = DecodeEngine(m, B, P, C)
+        outs[flag] = (eng.generate(ids, mask, C, greedy=True), eng.generate(ids, mask, C, temperature=0.9, seed=5))
+        del eng
+    for a, b in zip(outs["1"], outs["0"]):
+        for x, y in zip(a, b):
+            if isinstance(x, torch.Tensor):
+                assert torch.equal(x, y)
