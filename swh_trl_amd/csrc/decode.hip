@@ -1876,11 +1876,12 @@ int launch_lm_ks(dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const 
     return launch_status();
 }
 
-// SWH_LM_RING14=1 (read per call): the fused sampler at K = 896 with the half-tile weight
-// ring and 12 waves per workgroup (three per SIMD)
+// the fused sampler at K = 896 with the half-tile weight ring and 12 waves per workgroup
+// (three per SIMD): 58.2-58.8 against 60.3-60.4 us per launch, bench +0.6 % (SWH_LM_RING14=0: off;
+// read per call)
 inline bool lm_ring14() {
     const char *e = getenv("SWH_LM_RING14");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
 }
 
 // compile-time k-step counts for the model widths in use (Qwen2.5-0.5B: H = 896)
