@@ -156,6 +156,15 @@ def all_gather_rows(t: torch.Tensor) -> torch.Tensor:
     return torch.cat(parts).to(t.device)
 
 
+def all_gather_objects(items: list) -> list:
+    """accelerate gather_object: every rank's list concatenated in rank order."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return list(items)
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, list(items))
+    return [x for part in out for x in part]
+
+
 def barrier():
     if dist.is_available() and dist.is_initialized():
         if dist.get_backend() == "nccl":

@@ -246,33 +246,23 @@ PPO_CITATION = ("@article{mziegler2019fine-tuning,\n    title        = {{Fine-Tu
                 "    = 2019,\n    eprint       = {arXiv:1909.08593},\n}")
 
 
-def _linear_lambda(step: int, *, warmup: int, total: int) -> float:
-    """transformers' _get_linear_schedule_with_warmup_lr_lambda."""
-    if step < warmup:
-        return float(step) / float(max(1, warmup))
-    return max(0.0, float(total - step) / float(max(1, total - warmup)))
-
-
-def _constant_lambda(_step: int) -> float:
-    return 1.0
-
-
-def scheduler_state_dict(global_step: int, total: int, lr: float, warmup: int, kind: str = "linear",
-                         n_groups: int = 2) -> dict:
+def scheduler_state_dict(global_step: int, lr: float, fn, n_groups: int = 2) -> dict:
     """torch LambdaLR.state_dict() of the Trainer's scheduler after `global_step`
-    optimizer steps (transformers get_scheduler: linear warmup/decay, or
-    constant), over its `n_groups` param groups (decay / no decay).  Built from
-    a real LambdaLR so the keys are the installed torch's own (lr_lambdas
-    included: LambdaLR.load_state_dict pops it)."""
-    import functools
+    optimizer steps, `fn` the schedule's multiplier (schedule.py: the lambda of
+    transformers get_scheduler for the configured lr_scheduler_type / warmup),
+    over its `n_groups` param groups (decay / no decay).  Built from a real
+    LambdaLR so the keys are the installed torch's own (lr_lambdas included:
+    LambdaLR.load_state_dict pops it)."""
     p = [torch.nn.Parameter(torch.zeros(1)) for _ in range(n_groups)]
     opt = torch.optim.SGD([{"params": [q]} for q in p], lr=lr)
-    fn = functools.partial(_linear_lambda, warmup=warmup, total=total) if kind == "linear" else _constant_lambda
     sch = torch.optim.lr_scheduler.LambdaLR(opt, fn)
     sch.last_epoch = global_step
     sch._step_count = global_step + 1
     sch._last_lr = [lr * fn(global_step) for _ in range(n_groups)]
     return sch.state_dict()
+
+
+LEGACY_TRAINER_STATE = "swh_trainer_state.pt"  # the single-file exact-resume state of earlier builds
 
 
 def trainer_state_file(rank: int) -> str:

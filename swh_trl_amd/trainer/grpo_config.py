@@ -29,9 +29,15 @@ class GRPOConfig:
     adam_epsilon: float = 1e-8
     max_grad_norm: float = 1.0
     lr_scheduler_type: str = "linear"
-    warmup_steps: int = 0
+    lr_scheduler_kwargs: Optional[dict] = None
+    warmup_steps: float = 0
     warmup_ratio: float = 0.0
     logging_steps: float = 10
+    logging_first_step: bool = False
+    per_device_eval_batch_size: int = 8
+    eval_strategy: str = "no"              # "no" | "steps" (TrainingArguments)
+    eval_steps: Optional[float] = None     # default: logging_steps
+    eval_on_start: bool = False
     save_strategy: str = "steps"           # "steps" | "no" (TrainingArguments)
     save_steps: float = 500
     save_total_limit: Optional[int] = None
@@ -106,6 +112,14 @@ class GRPOConfig:
             raise ValueError("use_vllm=True: the vLLM generation path is out of scope; the device engine generates")
         if self.use_liger_loss:
             raise ValueError("use_liger_loss=True: the Liger (Triton) loss is out of scope; the fused HIP loss runs")
+        if "evaluation_strategy" in self.extra:  # the older TrainingArguments name
+            self.eval_strategy = self.extra.pop("evaluation_strategy")
+        self.eval_strategy = getattr(self.eval_strategy, "value", self.eval_strategy)
+        self.save_strategy = getattr(self.save_strategy, "value", self.save_strategy)
+        if self.eval_strategy not in ("no", "steps"):
+            raise ValueError(f"eval_strategy {self.eval_strategy!r}: the MI355X trainer evaluates on 'steps' (or 'no')")
+        if self.save_strategy not in ("no", "steps"):
+            raise ValueError(f"save_strategy {self.save_strategy!r}: the MI355X trainer saves on 'steps' (or 'no')")
         self.world_size = _world_size()
         n = self.world_size
         if self.generation_batch_size is None and self.steps_per_generation is None:
@@ -124,6 +138,14 @@ class GRPOConfig:
         if self.generation_batch_size % self.num_generations != 0:
             raise ValueError(f"generation_batch_size ({self.generation_batch_size}) must be divisible by "
                              f"num_generations ({self.num_generations}).")
+        if self.eval_strategy != "no":  # grpo_config.py: the eval batch must hold whole groups
+            global_eval = self.per_device_eval_batch_size * n
+            if global_eval % self.num_generations != 0:
+                possible = [g for g in range(2, global_eval + 1) if global_eval % g == 0]
+                raise ValueError(f"The global eval batch size ({n} x {self.per_device_eval_batch_size}) must be "
+                                 f"divisible by the number of generations per prompt ({self.num_generations}). Given "
+                                 f"the current eval batch size, the valid values for the number of generations are: "
+                                 f"{possible}.")
         if self.num_generations < 2:
             raise ValueError("GRPO requires at least 2 generations per prompt to calculate the advantages. You "
                              f"provided {self.num_generations}, which is less than the minimum required.")

@@ -35,23 +35,14 @@ from ..engine.gpt2 import warn_dropout
 from ..engine.decode import DecodeEngine
 from ..engine.model import CausalLM, dw_streams, dw_sync
 from ..optim import FlatAdamW, sync_ref_model
+from . import schedule
+from .callbacks import CallbackHandler, new_state
 from .grpo_config import GRPOConfig
-from .utils import generation_batch_indices, left_pad, linear_lr, pad_left_cat, split_tensor_dict, \
+from .utils import RepeatSampler, generation_batch_indices, left_pad, pad_left_cat, split_tensor_dict, \
     truncate_with_protected_tokens
 
 RewardFunc = Union[str, Callable, torch.nn.Module]
 from ..profiling import trace as _trace  # noqa: E402  (one clock for every phase line)
-
-
-class TrainerState:
-    """The fields of transformers.TrainerState the loop and reward functions read."""
-
-    def __init__(self):
-        self.global_step = 0
-        self.epoch = 0.0
-        self.max_steps = 0
-        self.num_input_tokens_seen = 0
-        self.log_history: list[dict] = []
 
 
 def model_dtype(model_init_kwargs: Optional[dict]) -> torch.dtype:
@@ -118,6 +109,76 @@ def load_model(model, device, trainable=True, seed=0, head: str = "lm", dtype=No
     raise TypeError(f"unsupported model type {type(model)}")
 
 
+def _is_pretrained_model(f) -> bool:
+    """transformers PreTrainedModel (without importing transformers when absent)."""
+    return any(c.__name__ == "PreTrainedModel" for c in type(f).__mro__)
+
+
+class RewardModel:
+    """A sequence-classification reward model (num_labels = 1) on the engine:
+    the frozen CausalLM with its score head, called like the transformers
+    module it replaces — `rm(input_ids=..., attention_mask=...).logits` is
+    [B, 1], the score Linear at the rightmost token that is not
+    `config.pad_token_id` (transformers GenericForSequenceClassification;
+    batch size > 1 needs a pad id), positions 0.. as transformers assigns them
+    without position_ids.  `config` is the transformers config object of a
+    converted module (so the trainer's pad-id assignment reaches it, as the
+    reference's does) or, for a directory, its config.json fields plus
+    `_name_or_path`."""
+
+    SUPPORTED = ("Qwen2ForSequenceClassification", "LlamaForSequenceClassification")
+
+    def __init__(self, model: CausalLM, config):
+        self.model, self.config = model, config
+        self.device = model.device
+
+    @classmethod
+    def supports(cls, module) -> bool:
+        score = getattr(module, "score", None)
+        return (type(module).__name__ in cls.SUPPORTED and getattr(module.config, "num_labels", 1) == 1
+                and getattr(score, "bias", None) is None)
+
+    @classmethod
+    def from_module(cls, module, device) -> "RewardModel":
+        return cls(load_model(module, device, trainable=False, head="score"), module.config)
+
+    @classmethod
+    def from_pretrained(cls, path: str, device, dtype) -> "RewardModel":
+        """AutoModelForSequenceClassification.from_pretrained(path, num_labels=1)
+        from a local directory (no hub access here)."""
+        import json
+        import types
+        if not os.path.isdir(path):
+            raise ValueError(f"reward model {path!r}: not a local directory (no hub access); pass a directory holding "
+                             "a transformers config.json + safetensors, or a model object")
+        with open(os.path.join(path, "config.json")) as f:
+            cj = json.load(f)
+        if cj.get("num_labels", len(cj.get("id2label", {0: 0}))) != 1:
+            raise ValueError(f"reward model {path!r}: num_labels must be 1")
+        cfg = types.SimpleNamespace(**cj)
+        cfg._name_or_path = path
+        cfg.pad_token_id = cj.get("pad_token_id")
+        return cls(load_model(path, device, trainable=False, head="score", dtype=dtype), cfg)
+
+    def __call__(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None, **unused):
+        import types
+        ids = input_ids.to(self.device)
+        B, L = ids.shape
+        pad = self.config.pad_token_id
+        if pad is None and B != 1:
+            raise ValueError("Cannot handle batch sizes > 1 if no padding token is defined.")
+        if pad is None:
+            last = torch.full((B,), L - 1, device=self.device, dtype=torch.int64)
+        else:
+            last = (torch.arange(L, device=self.device) * (ids != pad)).argmax(-1)
+        m = self.model
+        with torch.no_grad():
+            km = None if attention_mask is None else attention_mask.to(self.device)
+            h = m.hidden_states(ids, key_mask=km)
+            s = m.scores(h[torch.arange(B, device=self.device), last])
+        return types.SimpleNamespace(logits=s.view(B, 1))
+
+
 def _pad_completions(mb: dict, W: int, pad_token_id: int) -> dict:
     """A micro-batch's completion-side tensors right-padded to width W (pad ids,
     mask 0, log-probs 0): the extra columns are masked out of every sum."""
@@ -139,6 +200,11 @@ class GRPOTrainer:
                  callbacks=None, optimizers=(None, None), peft_config=None):
         if peft_config is not None:
             raise ValueError("peft_config: LoRA training is not part of the MI355X engine's scope")
+        if optimizers is not None and any(o is not None for o in optimizers):
+            raise ValueError("optimizers: the MI355X trainer updates its flat parameter buffer with the fused AdamW "
+                             "kernel, configured by the GRPOConfig fields (learning_rate, adam_beta1/2, adam_epsilon, "
+                             "weight_decay, max_grad_norm, lr_scheduler_type, lr_scheduler_kwargs, warmup_steps / "
+                             "warmup_ratio); a torch optimizer or scheduler object cannot drive it")
         self.args = args if args is not None else GRPOConfig(output_dir="grpo-out")
         a = self.args
         self.rank, self.world, self.local_rank = swh_dist.init_from_env()
@@ -153,9 +219,7 @@ class GRPOTrainer:
         self.processing_class = processing_class
         if not isinstance(reward_funcs, list):
             reward_funcs = [reward_funcs]
-        self.reward_funcs = reward_funcs
-        self.reward_func_names = [getattr(f, "__name__", None) or type(f).__name__ for f in reward_funcs]
-        self.reward_processing_classes = reward_processing_classes or [None] * len(reward_funcs)
+        self._setup_reward_funcs(reward_funcs, reward_processing_classes)
         if a.reward_weights is not None:
             if len(a.reward_weights) != len(reward_funcs):
                 raise ValueError(f"Number of reward weights ({len(a.reward_weights)}) must match number of reward "
@@ -200,15 +264,72 @@ class GRPOTrainer:
                                    weight_decay=a.weight_decay, max_grad_norm=a.max_grad_norm,
                                    no_decay_ranges=self.model.no_decay_ranges())
         self.optimizer.master.copy_(self.model.flat.float())
-        self.state = TrainerState()
+        self.state = new_state(self.rank, self.local_rank)
         self._step = 0
         self._buffered_inputs = None
         self._metrics = {"train": defaultdict(list), "eval": defaultdict(list)}
-        self._engine: Optional[DecodeEngine] = None
+        self._engine: Optional[DecodeEngine] = None   # the engine of the latest generation
+        self._engines: dict = {}
         self._gen_count = 0      # generation batches drawn so far (data-stream position, rollout RNG offset)
         self._shuffle_gen = torch.Generator().manual_seed(a.seed + 17 * self.rank)
         self._batches = None
-        self.callbacks = callbacks or []
+        self._eval_count = 0     # eval generations so far (rollout RNG offset of the eval stream)
+        self._ref_version = 0    # TR-DPO syncs of the reference so far
+        self.callback_handler = CallbackHandler(callbacks, self)
+        self.control = self.callback_handler.call("on_init_end")
+
+    # ------------------------------------------------------------------ callbacks (transformers Trainer API)
+    def add_callback(self, callback):
+        self.callback_handler.add_callback(callback)
+
+    def pop_callback(self, callback):
+        return self.callback_handler.pop_callback(callback)
+
+    def remove_callback(self, callback):
+        self.callback_handler.remove_callback(callback)
+
+    # ------------------------------------------------------------------ reward functions
+    def _setup_reward_funcs(self, reward_funcs: list, reward_processing_classes):
+        """grpo_trainer.py:727-772.  A string is a sequence-classification reward
+        model (AutoModelForSequenceClassification, num_labels=1): here a local
+        directory loaded onto the engine's score head.  A transformers Qwen2 /
+        Llama sequence classifier is copied onto the engine too (reward models
+        are frozen), so scoring runs the HIP forward; any other nn.Module is
+        called as given.  Names: the model's `config._name_or_path` last path
+        component, a callable's __name__.  A reward model without a processing
+        class gets AutoTokenizer.from_pretrained(_name_or_path); a tokenizer
+        without a pad token pads with EOS, and the model's config.pad_token_id
+        is set to the tokenizer's (the score is read at the last non-pad token)."""
+        dtype = model_dtype(self.args.model_init_kwargs)
+        funcs, names = [], []
+        for f in reward_funcs:
+            if isinstance(f, str):
+                f = RewardModel.from_pretrained(f, self.device, dtype)
+            elif isinstance(f, torch.nn.Module) and RewardModel.supports(f):
+                f = RewardModel.from_module(f, self.device)
+            if isinstance(f, (RewardModel, torch.nn.Module)):
+                names.append(f.config._name_or_path.split("/")[-1])
+            else:
+                names.append(getattr(f, "__name__", None) or type(f).__name__)
+            funcs.append(f)
+        if reward_processing_classes is None:
+            rpcs = [None] * len(funcs)
+        elif not isinstance(reward_processing_classes, list):
+            rpcs = [reward_processing_classes]
+        else:
+            if len(reward_processing_classes) != len(funcs):
+                raise ValueError("The number of reward processing classes must match the number of reward functions.")
+            rpcs = list(reward_processing_classes)
+        for i, (rtok, f) in enumerate(zip(rpcs, funcs)):
+            if isinstance(f, RewardModel) or _is_pretrained_model(f):
+                if rtok is None:
+                    from transformers import AutoTokenizer
+                    rtok = AutoTokenizer.from_pretrained(f.config._name_or_path)
+                if rtok.pad_token_id is None:
+                    rtok.pad_token = rtok.eos_token
+                f.config.pad_token_id = rtok.pad_token_id
+                rpcs[i] = rtok
+        self.reward_funcs, self.reward_func_names, self.reward_processing_classes = funcs, names, rpcs
 
     # ------------------------------------------------------------------ data
     def _local_gen_batch_size(self) -> int:
@@ -260,28 +381,36 @@ class GRPOTrainer:
         C = self.max_completion_length
         # the policy itself: bf16 on the DecodeEngine, an fp32 policy on the fp32
         # RefDecodeEngine (the reference generates in the model dtype, :1793-1810)
+        # one engine per batch size (training and evaluation batches differ), built once
         gm = self.model
-        e = self._engine
-        if e is None or e.B != B or e.Pmax < P or e.model is not gm:
+        e = self._engines.get(B)
+        if e is None or e.Pmax < P or e.model is not gm:
             Pmax = max(P, self.max_prompt_length or P) if (self.max_prompt_length or 0) <= 4096 else P
-            self._engine = build_engine(gm, B, Pmax, C)
-        return self._engine
+            e = self._engines[B] = build_engine(gm, B, Pmax, C)
+        self._engine = e
+        return e
 
     # ------------------------------------------------------------------ rollout + scoring
     @torch.no_grad()
-    def _generate_and_score_completions(self, examples: list[dict]) -> dict:
+    def _generate_and_score_completions(self, examples: list[dict], mode: str = "train") -> dict:
         a = self.args
         prompt_ids, prompt_mask, prompts_text = self._tokenize_prompts(examples)
         B, P = prompt_ids.shape
         _trace(f"prompts tokenized {B}x{P}")
         eng = self._engine_for(B, P)
-        seed = a.seed * 1_000_003 + self.rank
+        # the sampler's Philox stream: training generations and evaluation generations
+        # draw from separate keys, each advanced by its own generation count
+        if mode == "train":
+            seed, count = a.seed * 1_000_003 + self.rank, self._gen_count
+            self._gen_count += 1
+        else:
+            seed, count = a.seed * 1_000_003 + 7919 * (self.world + self.rank + 1), self._eval_count
+            self._eval_count += 1
         completion_ids, _ = eng.generate(prompt_ids, prompt_mask, self.max_completion_length,
                                          eos_token_id=self.eos_token_id, pad_token_id=self.pad_token_id,
-                                         seed=seed, offset=self._gen_count * (self.max_completion_length + 1),
+                                         seed=seed, offset=count * (self.max_completion_length + 1),
                                          check_every=a.decode_check_every, group_size=self.num_generations,
                                          early_exit=a.decode_early_exit, **self.gen_kwargs)
-        self._gen_count += 1
         _trace("generated")
         eos = [] if self.eos_token_id is None else self.eos_token_id
         completion_mask, lengths, has_eos = ops.completion_mask(completion_ids, eos,
@@ -311,23 +440,67 @@ class GRPOTrainer:
         same = (prompt_ids[1:] == prompt_ids[:-1]).all(1) & (prompt_mask[1:] == prompt_mask[:-1]).all(1)
         group = torch.cat([torch.zeros(1, dtype=torch.int64, device=self.device), (~same).long().cumsum(0)])
         out = {"prompt_ids": prompt_ids, "prompt_mask": prompt_mask, "completion_ids": completion_ids,
-               "completion_mask": completion_mask, "advantages": adv, "prompt_group": group + self._gen_count * B}
-        generate_every = a.steps_per_generation * self.num_iterations
-        if a.gradient_accumulation_steps % generate_every != 0:
+               "completion_mask": completion_mask, "advantages": adv, "prompt_group": group + count * B,
+               "row_index": torch.arange(B, device=self.device) + count * B}
+        # old-policy (:1854-1869) and frozen-reference (:1871-1899) log-probs: scored here only
+        # for the micro-batches whose first use would see another policy / reference; the rest
+        # are scored by the training pass itself, on its own batch layout (_loss_backward)
+        eager_old, eager_ref = self._eager_scoring(mode)
+        if eager_old:
             out["old_per_token_logps"] = self._score_logps(self.model, out)
-        if self.beta != 0.0:
+        if eager_ref:
             out["ref_per_token_logps"] = self._score_logps(self.ref_model, out)
-        m = self._metrics["train"]
+        m = self._metrics[mode]
         # per generation, resolved at the next log (no host sync here): this rank's
         # lengths / EOS flags (gathered across ranks at the log, :1945-1960), its
         # attention-mask token count (:1942), and the global reward statistics
         m["_lengths"].append(torch.stack([lengths.float(), has_eos.float()], 1))
-        m["_tokens"].append((prompt_mask.sum() + completion_mask.sum()).float().view(1, 1))
+        if mode == "train":  # :1941-1942: only training generations count toward num_input_tokens_seen
+            m["_tokens"].append((prompt_mask.sum() + completion_mask.sum()).float().view(1, 1))
         m["_rewards"].append(gmean)
         m["_reward_std"].append(gstd)
         m["_zero_std"].append(zstd.float())
         m["_rpf"].append(rewards_per_func)
         return out
+
+    def _needs_old_logps(self) -> bool:
+        """:1854-1869: the old-policy log-probs are kept when the optimizer steps do
+        not line up with the generations (GA not a multiple of spg x num_iterations)."""
+        a = self.args
+        return a.gradient_accumulation_steps % (a.steps_per_generation * self.num_iterations) != 0
+
+    def _eager_scoring(self, mode: str) -> tuple[bool, bool]:
+        """Whether the generation must be scored now for old-policy / reference
+        log-probs.  The reference scores both at generation time, but a value is the
+        same at the micro-batch's first use as long as the model that produced it has
+        not changed: the policy until the next optimizer step, the frozen reference
+        until the next TR-DPO sync.  Those micro-batches take the log-probs from the
+        training pass's own batch (same rows, same positions: with ref == policy the
+        k3 KL is exactly 0 and the first ratio exactly 1, as in the reference); the
+        others need the generation-time pass.  Generation slot j (of
+        steps_per_generation) is first used at micro-step k0 + j, in optimizer step
+        (k0 + j) // GA."""
+        a = self.args
+        if mode != "train":
+            return False, False
+        GA = a.gradient_accumulation_steps
+        k0, s0 = self._step, self._step // GA
+        slot_steps = [(k0 + j) // GA for j in range(a.steps_per_generation)]
+        eager_old = self._needs_old_logps() and any(st != s0 for st in slot_steps)
+        eager_ref = False
+        if self.beta != 0.0 and a.sync_ref_model:
+            # a sync after optimizer step t (0-based) happens when (t + 1) % ref_model_sync_steps == 0
+            eager_ref = any((t + 1) % a.ref_model_sync_steps == 0 for st in slot_steps for t in range(s0, st))
+        return eager_old, eager_ref
+
+    def _mark_fresh(self, mb: dict, mode: str) -> dict:
+        """Tag a micro-batch with the optimizer step and reference version of its
+        generation (tensors, so buffered micro-batches checkpoint with them)."""
+        if self._needs_old_logps() or mode != "train":
+            mb["_gen_step"] = torch.tensor(self.state.global_step)
+        if self.beta != 0.0:
+            mb["_ref_version"] = torch.tensor(self._ref_version)
+        return mb
 
     def _completions_for_rewards(self, examples, ids_h, completion_ids_list):
         """grpo_trainer.py:1901-1908: decoded completions; for conversational
@@ -364,7 +537,7 @@ class GRPOTrainer:
         kw["trainer_state"] = self.state
         conversational = self._is_conversational(examples[0])
         for i, (fn, rtok) in enumerate(zip(self.reward_funcs, self.reward_processing_classes)):
-            if isinstance(fn, torch.nn.Module):
+            if isinstance(fn, (RewardModel, torch.nn.Module)):
                 if rtok is None:
                     raise ValueError("a reward model needs its reward_processing_class (tokenizer)")
                 if conversational:
@@ -373,7 +546,7 @@ class GRPOTrainer:
                     texts = [p + c for p, c in zip(prompts, completions)]
                 enc = rtok(text=texts, return_tensors="pt", padding=True, padding_side="right",
                            add_special_tokens=False)
-                dev = next(fn.parameters()).device
+                dev = fn.device if isinstance(fn, RewardModel) else next(fn.parameters()).device
                 enc = {k: v.to(dev) for k, v in enc.items()}
                 with torch.inference_mode():
                     rpf[:, i] = fn(**enc).logits[:, 0].float().cpu()
@@ -415,18 +588,27 @@ class GRPOTrainer:
     def _prompt_groups(batch: dict):
         """(row order putting each prompt's rows consecutively, G) when every
         prompt of the batch appears exactly G >= 2 times (GRPO's generations of
-        one prompt, in any shuffled order); None otherwise.  SWH_SHARED_PREFIX=0
-        keeps the per-row forward."""
+        one prompt, in any shuffled order); None otherwise.  The order is the
+        generation's (`row_index`): a training pass over a whole shuffled
+        generation then runs every row at the position the generation-time
+        scoring pass gave it, so both see the same GEMM / attention layout and
+        produce the same bits whatever the kernels' row-position dependence.
+        SWH_SHARED_PREFIX=0 keeps the per-row forward."""
         if os.environ.get("SWH_SHARED_PREFIX", "1") == "0" or "prompt_group" not in batch:
             return None
+        gid = batch["prompt_group"]
+        key = batch.get("row_index")
+        order = torch.argsort(key) if key is not None else None
         rows: dict = {}
-        for r, gid in enumerate(batch["prompt_group"].tolist()):  # one small device -> host copy
-            rows.setdefault(gid, []).append(r)
+        g_host = (gid[order] if order is not None else gid).tolist()  # one small device -> host copy
+        for r, g in enumerate(g_host):
+            rows.setdefault(g, []).append(r)
         sizes = {len(v) for v in rows.values()}
         if len(sizes) != 1 or sizes.pop() < 2:
             return None
-        order = [r for v in rows.values() for r in v]
-        return torch.tensor(order, device=batch["prompt_ids"].device), len(order) // len(rows)
+        pos = [r for v in rows.values() for r in v]  # positions in the (sorted) sequence
+        pos_t = torch.tensor(pos, device=gid.device)
+        return (order[pos_t] if order is not None else pos_t), len(pos) // len(rows)
 
     @torch.no_grad()
     def _score_logps(self, model: CausalLM, batch: dict) -> torch.Tensor:
@@ -438,13 +620,16 @@ class GRPOTrainer:
         return lp
 
     # ------------------------------------------------------------------ loss over fused micro-batches
-    def _loss_backward(self, micro: list[dict]) -> dict:
+    def _loss_backward(self, micro: list[dict], train: bool = True) -> dict:
         """One forward/backward over the given micro-batches.  Segment j keeps
         micro-batch j's own normaliser (bnpo tokens / grpo rows), every row is
         scaled by 1/GA as the Trainer's loss division — the gradient equals the
-        reference's GA separate backward passes."""
+        reference's GA separate backward passes.  train=False: the evaluation
+        loss (prediction_step, grpo_trainer.py:2177-2183: compute_loss under
+        no_grad, no GA division), forward only."""
         a = self.args
-        GA = a.gradient_accumulation_steps
+        GA = a.gradient_accumulation_steps if train else 1
+        orig = micro
         R_each = [m["completion_ids"].shape[0] for m in micro]
         W = max(m["completion_ids"].shape[1] for m in micro)
         if any(m["completion_ids"].shape[1] != W for m in micro):  # rollouts of different widths (early stop)
@@ -456,17 +641,51 @@ class GRPOTrainer:
             "completion_mask": torch.cat([m["completion_mask"] for m in micro]),
             "advantages": torch.cat([m["advantages"] for m in micro]),
         }
-        if all("prompt_group" in m for m in micro):
-            batch["prompt_group"] = torch.cat([m["prompt_group"] for m in micro])
-        for k in ("old_per_token_logps", "ref_per_token_logps"):
-            if k in micro[0]:
+        for k in ("prompt_group", "row_index"):
+            if all(k in m for m in micro):
                 batch[k] = torch.cat([m[k] for m in micro])
-        seg = torch.cat([torch.full((r,), j, dtype=torch.int32) for j, r in enumerate(R_each)]).to(self.device)
+        for k in ("old_per_token_logps", "ref_per_token_logps"):
+            if any(k in m for m in micro):
+                batch[k] = torch.cat([m[k] if k in m else torch.zeros(m["completion_ids"].shape, device=self.device)
+                                      for m in micro])
+        # micro-batches at their first use whose generation-time model is unchanged take their
+        # old-policy / reference log-probs from this pass's own layout (_eager_scoring)
+        take_old = [self._needs_old_logps() and "_gen_step" in m and int(m["_gen_step"]) == self.state.global_step
+                    for m in orig]
+        take_ref = [self.beta != 0.0 and "_ref_version" in m and int(m["_ref_version"]) == self._ref_version
+                    for m in orig]
+        rows = torch.cat([torch.full((r,), j, dtype=torch.int64) for j, r in enumerate(R_each)]).to(self.device)
+        seg = rows.to(torch.int32)
         R = seg.numel()
         row_scale = torch.full((R,), 1.0 / GA, device=self.device)
+        if any(take_ref):
+            ref_lp = self._score_logps(self.ref_model, batch)
+            batch["ref_per_token_logps"] = self._merge_rows(batch.get("ref_per_token_logps"), ref_lp, take_ref, rows)
         _trace("loss inputs ready")
-        logp, ent = self._completion_logps(self.model, batch, True)
+        with torch.set_grad_enabled(train):
+            if train:
+                logp, ent = self._completion_logps(self.model, batch, True)
+            else:  # no weight-gradient accumulation into the flat buffer
+                saved, self.model.grad = self.model.grad, None
+                try:
+                    logp, ent = self._completion_logps(self.model, batch, True)
+                finally:
+                    self.model.grad = saved
         _trace("policy forward + lm head + logp/entropy")
+        if any(take_old):
+            batch["old_per_token_logps"] = self._merge_rows(batch.get("old_per_token_logps"), logp.detach(), take_old,
+                                                            rows)
+        # the buffered micro-batches keep what this pass scored for their later uses (num_iterations > 1)
+        r0 = 0
+        for j, (m, r) in enumerate(zip(orig, R_each)):
+            w = m["completion_ids"].shape[1]
+            if take_old[j]:
+                m["old_per_token_logps"] = batch["old_per_token_logps"][r0:r0 + r, :w].clone()
+            if take_ref[j]:
+                m["ref_per_token_logps"] = batch["ref_per_token_logps"][r0:r0 + r, :w].clone()
+            m.pop("_gen_step", None)
+            m.pop("_ref_version", None)
+            r0 += r
         emask = None
         if self.top_entropy_quantile < 1.0:
             emask = torch.zeros_like(batch["completion_mask"], dtype=torch.bool)
@@ -474,18 +693,30 @@ class GRPOTrainer:
             for j in range(len(micro)):
                 sl = seg == j
                 emask[sl] = get_high_entropy_mask(ent[sl], batch["completion_mask"][sl], 1 - self.top_entropy_quantile)
-        loss, metrics = ops.grpo_loss(
-            logp, batch["advantages"], batch["completion_mask"],
-            old_per_token_logps=batch.get("old_per_token_logps"), ref_per_token_logps=batch.get("ref_per_token_logps"),
-            entropy_mask=emask, entropies=ent, row_scale=row_scale, segments=seg, num_segments=len(micro),
-            beta=self.beta, epsilon_low=self.epsilon_low, epsilon_high=self.epsilon_high, delta=a.delta,
-            loss_type=self.loss_type, importance_sampling_level=self.importance_sampling_level,
-            max_completion_length=self.max_completion_length, segment_metrics=True)
+        kw = dict(old_per_token_logps=batch.get("old_per_token_logps"),
+                  ref_per_token_logps=batch.get("ref_per_token_logps"), entropy_mask=emask, entropies=ent,
+                  row_scale=row_scale, segments=seg, num_segments=len(micro), beta=self.beta,
+                  epsilon_low=self.epsilon_low, epsilon_high=self.epsilon_high, delta=a.delta,
+                  loss_type=self.loss_type, importance_sampling_level=self.importance_sampling_level,
+                  max_completion_length=self.max_completion_length, segment_metrics=True)
+        if not train:
+            loss, _, metrics = ops.grpo_loss_fwd_bwd(logp, batch["advantages"], batch["completion_mask"],
+                                                     need_grad=False, **kw)
+            return {"loss": loss[0], "metrics": metrics}
+        loss, metrics = ops.grpo_loss(logp, batch["advantages"], batch["completion_mask"], **kw)
         _trace("loss")
         loss.backward()
         dw_sync(self.device)  # the weight-gradient side stream joins the compute stream
         _trace("backward")
         return {"loss": loss.detach(), "metrics": metrics}
+
+    @staticmethod
+    def _merge_rows(prev: Optional[torch.Tensor], new: torch.Tensor, take: list, rows: torch.Tensor) -> torch.Tensor:
+        """Rows of micro-batch j from `new` where take[j], else from `prev`."""
+        if all(take) or prev is None:
+            return new.float()
+        sel = torch.tensor(take, device=new.device)[rows]
+        return torch.where(sel[:, None], new.float(), prev)
 
     # ------------------------------------------------------------------ the loop
     def _next_micro_batch(self) -> dict:
@@ -501,7 +732,7 @@ class GRPOTrainer:
             n = gen["completion_ids"].shape[0]
             perm = torch.randperm(n, generator=self._shuffle_gen).to(self.device)
             gen = {k: v[perm] for k, v in gen.items()}
-            self._buffered_inputs = split_tensor_dict(gen, a.steps_per_generation)
+            self._buffered_inputs = [self._mark_fresh(mb, "train") for mb in split_tensor_dict(gen, a.steps_per_generation)]
         inputs = self._buffered_inputs[self._step % a.steps_per_generation]
         self._step += 1
         return inputs
@@ -545,12 +776,15 @@ class GRPOTrainer:
         if ar is not None:
             ar.finish()
         lr = self._current_lr()
+        self.control = self.callback_handler.call("on_pre_optimizer_step")
         norm = self.optimizer.step(self.model.grad, model_out=self.model.flat, lr=lr)
+        self.control = self.callback_handler.call("on_optimizer_step")
         self.state.global_step += 1
         _trace(f"optimizer step {self.state.global_step}")
         if self.ref_model is not None and a.sync_ref_model and self.state.global_step % a.ref_model_sync_steps == 0:
             # TR-DPO mixup (callbacks.py:106-131): ref = alpha * policy + (1 - alpha) * ref
             sync_ref_model(self.ref_model.flat, self.model.flat, a.ref_model_mixup_alpha)
+            self._ref_version += 1
         loss = sum(o["loss"] for o in outs) if len(outs) > 1 else outs[0]["loss"]
         if len(outs) > 1:
             loss = loss  # per-micro losses already carry the 1/GA row scale
@@ -559,30 +793,47 @@ class GRPOTrainer:
         # one row of metric sums per GA micro-batch (the loss kernel's segments)
         m["_met"].append(torch.cat([o["metrics"][1:] for o in outs]))
         m["_grad_norm"].append(norm.clone())
-        m["_lr"].append(torch.tensor(lr))
         return {"loss": loss, "grad_norm": norm}
 
     def _flush_logs(self) -> dict:
-        """GRPOTrainer.log (grpo_trainer.py:2185-2196): every metric list averaged
-        since the last log.  The per-rank quantities are gathered across ranks
-        as the reference gathers them — completion lengths and EOS flags
-        (:1945-1960), token counts (:1942), the per-micro-batch masked means of
-        KL / entropy / clip ratios (:2143-2174, nanmean / nanmin / nanmax over
-        ranks) and the loss (transformers' Trainer gathers tr_loss) — in one
-        host sync per log."""
-        m = self._metrics["train"]
-        if not m.get("_loss"):
+        """GRPOTrainer.log (grpo_trainer.py:2185-2196) of a training interval:
+        every metric list averaged since the last log (`_metric_averages`),
+        with the Trainer's loss, grad_norm and learning_rate (the scheduler's
+        last lr, i.e. the rate of the next step, as transformers logs it)."""
+        log = self._metric_averages("train")
+        if not log:
+            return {}
+        log["step"] = self.state.global_step
+        self.state.log_history.append(log)
+        return log
+
+    def _metric_averages(self, mode: str) -> dict:
+        """The metrics of `mode` averaged since the last log.  The per-rank
+        quantities are gathered across ranks as the reference gathers them —
+        completion lengths and EOS flags (:1945-1960), token counts (:1942), the
+        per-micro-batch masked means of KL / entropy / clip ratios (:2143-2174,
+        nanmean / nanmin / nanmax over ranks) and the loss (transformers'
+        Trainer gathers tr_loss) — in one host sync per log.  Eval keys carry
+        the "eval_" prefix (:2191-2192)."""
+        m = self._metrics[mode]
+        if not m.get("_met"):
             return {}
         gather = swh_dist.all_gather_rows
         world = self.world
         n_gen = len(m["_lengths"])  # 0 when no rollout fell in this log interval (spg * mu > GA)
         seg = gather(torch.cat(m["_met"])).cpu()                # [world * n_micro, 8]
         lens = gather(torch.cat(m["_lengths"])).cpu() if n_gen else None  # [world * n_gen * B, 2]
-        losses = gather(torch.stack(m["_loss"]).view(-1, 1).float()).cpu()
-        self._count_tokens()
+        log = {}
+        if mode == "train":
+            losses = gather(torch.stack(m["_loss"]).view(-1, 1).float()).cpu()
+            self._count_tokens()
+            log = {"loss": float(losses.view(world, -1).mean(0).mean()),
+                   "grad_norm": float(torch.stack(m["_grad_norm"]).mean()),
+                   "learning_rate": self._lr_at(self.state.global_step)}
+        log["num_tokens"] = self.state.num_input_tokens_seen
         n_micro = seg.shape[0] // world
         seg = seg.view(world, n_micro, 8)
-        tok = seg[..., 0].clamp(min=1.0)
+        tok = seg[..., 0].clamp(min=1.0)  # completion_token_count = mask.sum().clamp(min=1.0) (:2142)
         rows = seg[..., 6]
         clip_den = rows if self.importance_sampling_level == "sequence" else tok
 
@@ -597,10 +848,6 @@ class GRPOTrainer:
             return torch.stack([c[~c.isnan()].max() if (~c.isnan()).any() else torch.tensor(float("nan"))
                                 for c in x.t()])
 
-        log = {"loss": float(losses.view(world, -1).mean(0).mean()),
-               "grad_norm": float(torch.stack(m["_grad_norm"]).mean()),
-               "learning_rate": float(m["_lr"][-1]),
-               "num_tokens": self.state.num_input_tokens_seen}
         # completions (:1945-1960), one entry per generation, averaged
         B = lens.shape[0] // (world * n_gen) if n_gen else 0
         per_gen = lens.view(world, n_gen, B, 2).transpose(0, 1).reshape(n_gen, world * B, 2) if n_gen else []
@@ -643,9 +890,9 @@ class GRPOTrainer:
         log["clip_ratio/high_mean"] = over_ranks(high)
         log["clip_ratio/high_max"] = float(nanmax(high).mean())
         log["clip_ratio/region_mean"] = over_ranks(region)
-        log["step"] = self.state.global_step
         m.clear()
-        self.state.log_history.append(log)
+        if mode == "eval":
+            log = {f"eval_{k}": v for k, v in log.items()}
         return log
 
     def _count_tokens(self):
@@ -704,8 +951,7 @@ class GRPOTrainer:
             if not a.save_only_model:
                 torch.save(ck.optimizer_state_dict(self.model, self.optimizer, a.weight_decay),
                            os.path.join(d, "optimizer.pt"))
-                torch.save(ck.scheduler_state_dict(self.state.global_step, max(1, self.state.max_steps),
-                                                   a.learning_rate, a.warmup_steps, a.lr_scheduler_type),
+                torch.save(ck.scheduler_state_dict(self.state.global_step, a.learning_rate, self._schedule()),
                            os.path.join(d, "scheduler.pt"))
                 ck.save_master(self.optimizer, d)
                 if self.ref_model is not None and a.sync_ref_model:  # the mixed reference is trainer state
@@ -717,15 +963,28 @@ class GRPOTrainer:
         swh_dist.barrier()
         return d
 
+    def _schedule(self):
+        """The LambdaLR multiplier of transformers get_scheduler for the config's
+        lr_scheduler_type / lr_scheduler_kwargs / warmup over max_steps (schedule.py)."""
+        total = max(1, self.state.max_steps)
+        key = (total, self.args.lr_scheduler_type)
+        if getattr(self, "_sched_key", None) != key:
+            self._sched_fn, self._sched_key = schedule.for_args(self.args, total), key
+        return self._sched_fn
+
+    def _lr_at(self, step: int) -> float:
+        return self.args.learning_rate * self._schedule()(step)
+
     def _current_lr(self) -> float:
-        a = self.args
-        return linear_lr(self.state.global_step, max(1, self.state.max_steps), a.learning_rate, a.warmup_steps) \
-            if a.lr_scheduler_type == "linear" else a.learning_rate
+        """The rate of the next optimizer step: the Trainer steps the scheduler after
+        the optimizer, so step k (0-based) uses lr * lambda(k)."""
+        return self._lr_at(self.state.global_step)
 
     def _resume_state(self) -> dict:
         """Tensors only (loaded with weights_only=True): the data-stream position,
         the shuffle generator, the rollouts still buffered for the next steps."""
         st = {"gen_count": torch.tensor(self._gen_count), "micro_step": torch.tensor(self._step),
+              "ref_version": torch.tensor(self._ref_version),
               "shuffle_gen": self._shuffle_gen.get_state(), "global_step": torch.tensor(self.state.global_step),
               "tokens_seen": torch.tensor(self.state.num_input_tokens_seen)}
         if self._buffered_inputs is not None:
@@ -762,16 +1021,24 @@ class GRPOTrainer:
         if not os.path.exists(sp) and any(f.startswith("swh_trainer_state_") for f in os.listdir(d)):
             raise ValueError(f"{d}: no {ck.trainer_state_file(self.rank)} (checkpoint saved by fewer ranks); the "
                              "exact-resume state is per rank")
+        legacy = os.path.join(d, ck.LEGACY_TRAINER_STATE)
+        if not os.path.exists(sp) and os.path.exists(legacy):
+            # written by a single-rank run before the state became per rank
+            if self.world != 1:
+                raise ValueError(f"{d}: holds the single-rank exact-resume state {ck.LEGACY_TRAINER_STATE}; it "
+                                 f"cannot resume a {self.world}-rank run")
+            sp = legacy
         if os.path.exists(sp):
             st = torch.load(sp, weights_only=True)
             self._gen_count = int(st["gen_count"])
             self._step = int(st["micro_step"])
+            self._ref_version = int(st.get("ref_version", 0))
             self._shuffle_gen.set_state(st["shuffle_gen"])
             bufs = {}
             for k, v in st.items():
                 if k.startswith("buf."):
                     _, i, name = k.split(".", 2)
-                    bufs.setdefault(int(i), {})[name] = v.to(self.device)
+                    bufs.setdefault(int(i), {})[name] = v if name.startswith("_") else v.to(self.device)
             self._buffered_inputs = [bufs[i] for i in sorted(bufs)] if bufs else None
         else:  # transformers checkpoint: position from the step count
             self._gen_count = self.state.global_step * self.args.gradient_accumulation_steps // (
@@ -779,7 +1046,28 @@ class GRPOTrainer:
             self._step = self.state.global_step * self.args.gradient_accumulation_steps
         self._batches = None
 
-    def train(self, resume_from_checkpoint=None):
+    def _total_steps(self) -> int:
+        a = self.args
+        if a.max_steps and a.max_steps > 0:
+            return a.max_steps
+        return max(1, int(math.ceil(self._steps_per_epoch() * a.num_train_epochs)))
+
+    def _steps_per_epoch(self) -> float:
+        a = self.args
+        per_epoch = len(self.train_dataset) // (a.generation_batch_size // self.num_generations)
+        return max(1e-9, per_epoch * a.steps_per_generation * self.num_iterations / a.gradient_accumulation_steps)
+
+    @staticmethod
+    def _interval(x, total: int) -> int:
+        """TrainingArguments logging/save/eval steps: an int, or a fraction of max_steps (rounded up)."""
+        return int(x) if x >= 1 else max(1, math.ceil(total * x))
+
+    def train(self, resume_from_checkpoint=None, trial=None, ignore_keys_for_eval=None, **kwargs):
+        """transformers Trainer.train / _inner_training_loop around the GRPO step:
+        callbacks (callbacks.py) with DefaultFlowCallback's log / evaluate / save
+        decisions, evaluation on eval_dataset (eval_strategy "steps"), and the
+        final train summary log.  Returns transformers' TrainOutput
+        (global_step, training_loss, metrics)."""
         a = self.args
         if self.train_dataset is None:
             raise ValueError("train_dataset is required")
@@ -789,24 +1077,155 @@ class GRPOTrainer:
             if d is None:
                 raise ValueError(f"No valid checkpoint found in output directory ({a.output_dir})")
             self._load_checkpoint(d)
-        if a.max_steps and a.max_steps > 0:
-            total = a.max_steps
-        else:
-            per_epoch = len(self.train_dataset) // (a.generation_batch_size // self.num_generations)
-            total = max(1, int(math.ceil(per_epoch * a.steps_per_generation * self.num_iterations
-                                         / a.gradient_accumulation_steps * a.num_train_epochs)))
-        self.state.max_steps = total
-        log_every = int(a.logging_steps) if a.logging_steps >= 1 else max(1, int(total * a.logging_steps))
-        # TrainingArguments: a fraction of max_steps, rounded up
-        save_every = int(a.save_steps) if a.save_steps >= 1 else max(1, math.ceil(total * a.save_steps))
-        t0 = time.time()
-        while self.state.global_step < total:
-            self.training_step_group()
-            if self.state.global_step % log_every == 0 or self.state.global_step == total:
-                log = self._flush_logs()
-                log["train_runtime"] = time.time() - t0
-                if self.rank == 0:
-                    print(log, flush=True)
-            if a.save_strategy == "steps" and a.output_dir and self.state.global_step % save_every == 0:
+        total = self._total_steps()
+        st = self.state
+        st.max_steps = total
+        st.num_train_epochs = int(math.ceil(total / self._steps_per_epoch()))
+        st.logging_steps = log_every = self._interval(a.logging_steps, total)
+        st.save_steps = save_every = self._interval(a.save_steps, total)
+        st.eval_steps = eval_every = self._interval(a.eval_steps if a.eval_steps is not None else a.logging_steps,
+                                                    total)
+        st.train_batch_size = a.per_device_train_batch_size
+        if a.eval_strategy == "steps" and self.eval_dataset is None:
+            raise ValueError("eval_strategy='steps' requires an eval_dataset")
+        cb = self.callback_handler
+        start_step, t0 = st.global_step, time.time()
+        self.control = cb.call("on_train_begin")
+        if a.eval_on_start and self.eval_dataset is not None:
+            self.evaluate()
+        self.control = cb.call("on_epoch_begin")
+        loss_sum = torch.zeros((), device=self.device)
+        while st.global_step < total and not self.control.should_training_stop:
+            self.control = cb.call("on_step_begin")
+            out = self.training_step_group()
+            loss_sum += out["loss"].detach().float()
+            st.epoch = st.global_step / self._steps_per_epoch()
+            # DefaultFlowCallback.on_step_end, then the user's callbacks may change the decisions
+            c, gs = self.control, st.global_step
+            if (gs == 1 and a.logging_first_step) or gs % log_every == 0:
+                c.should_log = True
+            if a.eval_strategy == "steps" and gs % eval_every == 0:
+                c.should_evaluate = True
+            if a.save_strategy == "steps" and gs % save_every == 0:
+                c.should_save = True
+            if gs >= total:
+                c.should_training_stop = True
+                if a.eval_strategy == "steps" and gs % eval_every != 0:
+                    c.should_evaluate = True
+                if a.save_strategy == "steps":
+                    c.should_save = True
+            self.control = cb.call("on_step_end")
+            self._maybe_log_save_evaluate(t0)
+        self.control = cb.call("on_epoch_end")
+        self._maybe_log_save_evaluate(t0)
+        runtime = time.time() - t0
+        steps_done = st.global_step - start_step
+        train_loss = float(loss_sum) / max(1, steps_done)
+        n_samples = steps_done * a.generation_batch_size * self.num_iterations // max(1, a.steps_per_generation)
+        metrics = {"train_runtime": round(runtime, 4), "train_samples_per_second": round(n_samples / runtime, 3),
+                   "train_steps_per_second": round(steps_done / runtime, 3), "total_flos": 0.0,
+                   "train_loss": train_loss}
+        self._log(metrics)  # GRPOTrainer.log merges whatever metrics are still pending (:2185-2196)
+        self.control = cb.call("on_train_end")
+        try:
+            from transformers.trainer_utils import TrainOutput
+            return TrainOutput(st.global_step, train_loss, metrics)
+        except ImportError:  # pragma: no cover
+            return st.global_step, train_loss, metrics
+
+    def _log(self, logs: dict) -> dict:
+        """GRPOTrainer.log + Trainer.log: pending training metrics merged in, epoch and
+        step added, appended to log_history, printed on the main process, on_log."""
+        pending = self._metric_averages("train")
+        logs = {**logs, **pending}
+        if self.state.epoch is not None:
+            logs["epoch"] = self.state.epoch
+        logs["step"] = self.state.global_step
+        self.state.log_history.append(logs)
+        if self.rank == 0:
+            print(logs, flush=True)
+        self.control = self.callback_handler.call("on_log", logs=logs)
+        return logs
+
+    def _maybe_log_save_evaluate(self, t0: float):
+        c = self.control
+        if c.should_log:
+            pending = self._metric_averages("train")
+            if pending:
+                pending["train_runtime"] = time.time() - t0
+                self._log(pending)
+            else:
+                c.should_log = False
+        if self.control.should_evaluate:
+            self.evaluate()
+        if self.control.should_save:
+            if self.args.output_dir:
                 self._save_checkpoint()
-        return self.state
+            self.control = self.callback_handler.call("on_save")
+
+    # ------------------------------------------------------------------ evaluation (Trainer.evaluate)
+    def _eval_batches(self, dataset):
+        """Local evaluation batches: RepeatSampler(eval_dataset, mini_repeat_count=G,
+        seed) (:1132-1138) in global batches of per_device_eval_batch_size x world,
+        each rank its contiguous slice (accelerate sharding; a short last batch
+        is completed from the start, as accelerate's even_batches does)."""
+        a = self.args
+        idx = list(RepeatSampler(range(len(dataset)), mini_repeat_count=self.num_generations, seed=a.seed))
+        gb = a.per_device_eval_batch_size * self.world
+        if gb % self.num_generations:
+            raise ValueError(f"The global eval batch size ({self.world} x {a.per_device_eval_batch_size}) must be "
+                             f"divisible by the number of generations per prompt ({self.num_generations}).")
+        for s in range(0, len(idx), gb):
+            chunk = idx[s:s + gb]
+            if len(chunk) < gb:
+                chunk = chunk + idx[:gb - len(chunk)]
+            mine = chunk[self.rank * a.per_device_eval_batch_size:(self.rank + 1) * a.per_device_eval_batch_size]
+            yield [dataset[i] for i in mine]
+
+    @torch.no_grad()
+    def evaluate(self, eval_dataset=None, ignore_keys=None, metric_key_prefix: str = "eval") -> dict:
+        """Trainer.evaluate with GRPO's prediction_step (grpo_trainer.py:2177-2183):
+        each local eval batch is generated and scored (no buffering, no
+        iterations, :1440-1443), its loss computed under no_grad; eval_loss is
+        the batch-size-weighted mean over every rank's batches, and the eval
+        metrics of _generate_and_score_completions / _compute_loss are logged
+        with the "eval_" prefix.  A dict of datasets is evaluated per entry
+        with the prefix eval_<name>."""
+        ds = eval_dataset if eval_dataset is not None else self.eval_dataset
+        if ds is None:
+            raise ValueError("Trainer: evaluation requires an eval_dataset.")
+        if isinstance(ds, dict):
+            out = {}
+            for name, d in ds.items():
+                out.update(self.evaluate(d, ignore_keys, f"{metric_key_prefix}_{name}"))
+            return out
+        t0 = time.time()
+        losses, sizes = [], []
+        n = 0
+        for examples in self._eval_batches(ds):
+            gen = self._mark_fresh(self._generate_and_score_completions(examples, mode="eval"), "eval")
+            out = self._loss_backward([gen], train=False)
+            m = self._metrics["eval"]
+            m["_met"].append(out["metrics"][1:])
+            losses.append(out["loss"].view(1).float())
+            sizes.append(float(len(examples)))
+            n += len(examples)
+        loss_rows = torch.stack([torch.cat(losses), torch.tensor(sizes, device=self.device)], 1)
+        allr = swh_dist.all_gather_rows(loss_rows).cpu()
+        runtime = time.time() - t0
+        steps = len(losses)
+        metrics = {f"{metric_key_prefix}_loss": float((allr[:, 0] * allr[:, 1]).sum() / allr[:, 1].sum()),
+                   f"{metric_key_prefix}_runtime": round(runtime, 4),
+                   f"{metric_key_prefix}_samples_per_second": round(n * self.world / runtime, 3),
+                   f"{metric_key_prefix}_steps_per_second": round(steps / runtime, 3)}
+        avg = self._metric_averages("eval")
+        metrics.update({metric_key_prefix + k[len("eval"):]: v for k, v in avg.items()})
+        if self.state.epoch is not None:
+            metrics["epoch"] = self.state.epoch
+        log = dict(metrics, step=self.state.global_step)
+        self.state.log_history.append(log)
+        if self.rank == 0:
+            print(log, flush=True)
+        self.control = self.callback_handler.call("on_log", logs=log)
+        self.control = self.callback_handler.call("on_evaluate", metrics=metrics)
+        return metrics

@@ -25,11 +25,13 @@ class PPOConfig:
     adam_beta2: float = 0.999
     adam_epsilon: float = 1e-8
     lr_scheduler_type: str = "linear"
-    warmup_steps: int = 0
+    lr_scheduler_kwargs: Optional[dict] = None
+    warmup_steps: float = 0
     warmup_ratio: float = 0.0
     logging_steps: float = 10              # OnPolicyConfig (utils.py:759)
     eval_steps: Optional[float] = None
     save_steps: float = 500
+    save_strategy: str = "steps"           # "steps" | "no" (TrainingArguments)
     seed: int = 42
     bf16: Optional[bool] = None            # OnPolicyConfig: not fp16 when unset (utils.py:870-873)
     fp16: bool = False

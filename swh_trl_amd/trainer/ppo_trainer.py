@@ -37,9 +37,11 @@ from ..engine import build_engine, build_model
 from ..engine.decode import DecodeEngine
 from ..engine.model import CausalLM, dw_sync
 from ..optim import FlatAdamW
-from .grpo_trainer import TrainerState, _trace, load_model, model_dtype
+from . import schedule
+from .callbacks import CallbackHandler, new_state
+from .grpo_trainer import _trace, load_model, model_dtype
 from .ppo_config import PPOConfig
-from .utils import left_pad, linear_lr
+from .utils import left_pad
 
 INVALID_LOGPROB = 1.0  # ppo_trainer.py:81
 
@@ -108,6 +110,11 @@ class PPOTrainer:
                              "same as `model`, you must make a copy of it, or `None` if you use peft.")
         if peft_config is not None:
             raise ValueError("peft_config: LoRA training is not part of the MI355X engine's scope")
+        if optimizers is not None and any(o is not None for o in optimizers):
+            raise ValueError("optimizers: the MI355X trainer updates policy and value with the fused AdamW kernel, "
+                             "configured by the PPOConfig fields (learning_rate, adam_beta1/2, adam_epsilon, "
+                             "weight_decay, lr_scheduler_type, lr_scheduler_kwargs, warmup_steps / warmup_ratio); a "
+                             "torch optimizer or scheduler object cannot drive it")
         self.args = args
         self.processing_class = processing_class
         tok = processing_class
@@ -171,9 +178,11 @@ class PPOTrainer:
         self.opt_policy, self.opt_value = mk(self.policy_model), mk(self.value_model)
         self.opt_policy.master.copy_(self.policy_model.flat.float())
         self.opt_value.master.copy_(self.value_model.flat.float())
-        self.state = TrainerState()
+        self.state = new_state(self.rank, self.local_rank)
         self.state.episode = 0
-        self.callbacks = callbacks or []
+        self.model, self.optimizer = self.policy_model, self.opt_policy   # what callbacks receive
+        self.callback_handler = CallbackHandler(callbacks, self)
+        self.control = self.callback_handler.control
         self._engine: Optional[DecodeEngine] = None
         self._gen_count = 0
         self._np_rng = np.random.default_rng(self.local_seed)
@@ -376,10 +385,8 @@ class PPOTrainer:
         _trace("generated")
         ro = self.rollout_from(queries, responses, logprobs)
         _trace("rollout scored")
-        total = max(1, a.num_total_batches)
-        warm = a.warmup_steps or int(math.ceil(a.warmup_ratio * total))
-        lr = linear_lr(self.state.global_step, total, a.learning_rate, warm) \
-            if a.lr_scheduler_type == "linear" else a.learning_rate
+        # create_optimizer_and_scheduler(num_training_steps=num_total_batches), stepped once per update (:232-234, :648)
+        lr = a.learning_rate * schedule.for_args(a, max(1, a.num_total_batches))(self.state.global_step)
         stats = self.ppo_update(ro, lr)
         _trace("ppo epochs")
         self.state.global_step += 1
@@ -473,23 +480,103 @@ class PPOTrainer:
         swh_dist.barrier()
         return d
 
-    def train(self):
+    def add_callback(self, callback):
+        self.callback_handler.add_callback(callback)
+
+    def pop_callback(self, callback):
+        return self.callback_handler.pop_callback(callback)
+
+    def remove_callback(self, callback):
+        self.callback_handler.remove_callback(callback)
+
+    @torch.no_grad()
+    def generate_completions(self, sampling: bool = False) -> dict:
+        """ppo_trainer.py:687-749: the policy's completions of the eval dataset
+        (per_device_eval_batch_size batches, drop_last, no shuffle) sampled at
+        temperature 0.01 + 1e-7, truncated after the stop token and scored by
+        the reward model; `sampling` stops after the first batch.  Returns the
+        table {"query", "model response", "score"} (rank 0 prints its first 5
+        rows); queries / responses are decoded when the processing class can."""
         a = self.args
-        self.state.global_step = 0
-        self.state.episode = 0
-        self.state.max_steps = a.num_total_batches
-        log_every = int(a.logging_steps) if a.logging_steps >= 1 else \
-            max(1, math.ceil(a.num_total_batches * a.logging_steps))
+        table = {"query": [], "model response": [], "score": []}
+        if self.eval_dataset is None:
+            return table
+        tok = self.processing_class
+        n, bs = len(self.eval_dataset), a.per_device_eval_batch_size
+        for s in range(0, n - bs + 1, bs):
+            query = self._queries([self.eval_dataset[i] for i in range(s, s + bs)])
+            B, P = query.shape
+            eng = self._engine_for(B, P)
+            attention_mask = (query != self.pad_token_id).to(torch.int32)
+            input_ids = torch.masked_fill(query, attention_mask == 0, 0)
+            resp, _ = eng.generate(input_ids, attention_mask, a.response_length, temperature=0.01 + 1e-7, top_p=1.0,
+                                   top_k=None, eos_token_id=self.stop_token_id, pad_token_id=self.pad_token_id,
+                                   seed=a.seed * 1_000_003 + 7919 * (self.rank + 1), offset=s * (a.response_length + 1),
+                                   early_exit=a.decode_early_exit)
+            post = resp
+            if self.stop_token_id is not None:
+                post, _ = ops.ppo_truncate(resp, self.stop_token_id, self.pad_token_id)
+            pqr = torch.cat([query, post], 1)
+            hr = self._no_grad_hidden(self.reward_model, pqr)
+            # get_reward: the score at the last non-pad token after the context
+            seq = first_true_indices(pqr[:, P:] == self.pad_token_id) - 1 + P
+            score = self.reward_model.scores(hr[torch.arange(B, device=hr.device), seq.clamp(min=0)])
+            dec = (lambda t, **k: tok.batch_decode(t, **k)) if hasattr(tok, "batch_decode") else \
+                (lambda t, **k: t.tolist())
+            table["query"].extend(swh_dist.all_gather_objects(dec(query.cpu(), skip_special_tokens=True)))
+            table["model response"].extend(swh_dist.all_gather_objects(dec(post.cpu())))
+            table["score"].extend(swh_dist.all_gather_rows(score.float().view(-1, 1)).view(-1).cpu().tolist())
+            if sampling:
+                break
+        if self.rank == 0:
+            for i in range(min(5, len(table["query"]))):
+                print({k: v[i] for k, v in table.items()}, flush=True)
+        return table
+
+    def train(self):
+        """ppo_trainer.py:347-685: per update a rollout, the PPO epochs, a log of
+        the metrics (self.log every update, :646), on_step_end with
+        DefaultFlowCallback's save decision (save_steps), sample generations on
+        the eval dataset every num_total_batches // num_sample_generations
+        updates (:657-659), on_train_end."""
+        a = self.args
+        st = self.state
+        st.global_step = 0
+        st.episode = 0
+        st.max_steps = a.num_total_batches
+        st.num_train_epochs = a.total_episodes / self.train_dataset_len
+        st.logging_steps = int(a.logging_steps) if a.logging_steps >= 1 else math.ceil(st.max_steps * a.logging_steps)
+        st.save_steps = int(a.save_steps) if a.save_steps >= 1 else max(1, math.ceil(st.max_steps * a.save_steps))
+        if a.eval_steps is not None:
+            st.eval_steps = int(a.eval_steps) if a.eval_steps >= 1 else math.ceil(st.max_steps * a.eval_steps)
+        sample_freq = max(1, a.num_total_batches // a.num_sample_generations) if a.num_sample_generations > 0 else 0
+        cb = self.callback_handler
+        self.control = cb.call("on_train_begin")
         t0 = time.time()
-        for _ in range(a.num_total_batches):
+        for update in range(1, a.num_total_batches + 1):
             self.training_step()
-            if self.state.global_step % log_every == 0 or self.state.global_step == a.num_total_batches:
-                log = self._flush_logs()
-                log["eps"] = int(self.state.episode / max(time.time() - t0, 1e-9))
-                if self.rank == 0:
-                    print(log, flush=True)
-            save_every = int(a.save_steps) if a.save_steps >= 1 else max(1, math.ceil(a.num_total_batches * a.save_steps))
-            if getattr(a, "save_strategy", "steps") == "steps" and a.output_dir and \
-                    self.state.global_step % save_every == 0:
+            log = self._flush_logs()
+            log["eps"] = int(st.episode / max(time.time() - t0, 1e-9))
+            st.epoch = st.episode / self.train_dataset_len
+            log["epoch"] = st.epoch
+            if self.rank == 0:
+                print(log, flush=True)
+            self.control = cb.call("on_log", logs=log)
+            # DefaultFlowCallback.on_step_end: save every save_steps
+            if a.save_strategy == "steps" and st.global_step % st.save_steps == 0:
+                self.control.should_save = True
+            self.control = cb.call("on_step_end")
+            if self.control.should_save:
+                if a.output_dir:
+                    self._save_checkpoint()
+                self.control = cb.call("on_save")
+            if sample_freq and (update - 1) % sample_freq == 0:
+                self.generate_completions(sampling=True)
+            if self.control.should_training_stop:
+                break
+        self.control = cb.call("on_train_end")
+        if self.control.should_save:
+            if a.output_dir:
                 self._save_checkpoint()
-        return self.state
+            self.control = cb.call("on_save")
+        return st

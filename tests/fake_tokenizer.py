@@ -16,3 +16,19 @@ def make_tokenizer(vocab_size: int = 512):
     tok.chat_template = ("{% for m in messages %}<{{ m['role'] }}> {{ m['content'] }} {% endfor %}"
                          "{% if add_generation_prompt %}<assistant> {% endif %}")
     return tok
+
+
+def make_byte_tokenizer():
+    """A byte-level BPE tokenizer without merges (ids 0-255 the bytes, 256
+    <|endoftext|> = EOS = pad): what AutoTokenizer rebuilds as Qwen2Tokenizer
+    from a Qwen2 model directory, so a reward-model directory can carry it."""
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers
+    from transformers import PreTrainedTokenizerFast
+    from transformers.convert_slow_tokenizer import bytes_to_unicode
+    b2u = bytes_to_unicode()
+    vocab = {b2u[b]: b for b in range(256)}
+    vocab["<|endoftext|>"] = 256
+    tk = Tokenizer(models.BPE(vocab=vocab, merges=[]))
+    tk.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    tk.decoder = decoders.ByteLevel()
+    return PreTrainedTokenizerFast(tokenizer_object=tk, eos_token="<|endoftext|>", pad_token="<|endoftext|>")

@@ -129,26 +129,67 @@ def test_gpt2_checkpoint_round_trip_and_param_order(tmp_path):
         assert (o in nd) == want, name
 
 
-@pytest.mark.parametrize("kind,warmup", [("linear", 0), ("linear", 3), ("constant", 0)])
-def test_scheduler_state_loads_into_transformers_lambdalr(kind, warmup):
+SCHEDULES = [("linear", 0, None), ("linear", 3, None), ("constant", 0, None), ("constant_with_warmup", 3, None),
+             ("cosine", 2, None), ("cosine", 0, {"num_cycles": 1.5}), ("cosine_with_restarts", 2, {"num_cycles": 3}),
+             ("polynomial", 2, {"lr_end": 1e-5, "power": 2.0}), ("inverse_sqrt", 3, None),
+             ("inverse_sqrt", 0, {"timescale": 4}), ("cosine_with_min_lr", 2, {"min_lr": 1e-4}),
+             ("cosine_with_min_lr", 0, {"min_lr_rate": 0.2}),
+             ("cosine_warmup_with_min_lr", 3, {"min_lr_rate": 0.1, "warmup_lr_rate": 0.05})]
+
+
+@pytest.mark.parametrize("kind,warmup,kw", SCHEDULES)
+def test_schedule_multiplier_matches_transformers(kind, warmup, kw):
+    """schedule.multiplier == the LambdaLR lambda of transformers get_scheduler at
+    every step of a 13-step run (and past its end), for each supported type."""
+    from transformers import get_scheduler
+
+    from swh_trl_amd.trainer import schedule
+    total, lr = 13, 1e-3
+    opt = torch.optim.SGD([torch.nn.Parameter(torch.zeros(1))], lr=lr)
+    ref = get_scheduler(kind, opt, num_warmup_steps=warmup, num_training_steps=total,
+                        scheduler_specific_kwargs=dict(kw or {}))
+    fn = schedule.multiplier(kind, total, warmup, lr, kw)
+    for s in range(total + 3):
+        assert fn(s) == pytest.approx(ref.lr_lambdas[0](s), rel=1e-12, abs=1e-15), (kind, s)
+
+
+def test_schedule_rejects_unsupported_and_warmup_ratio():
+    from types import SimpleNamespace
+
+    from swh_trl_amd.trainer import schedule
+    with pytest.raises(ValueError, match="not supported"):
+        schedule.multiplier("reduce_lr_on_plateau", 10, 0, 1e-3)
+    with pytest.raises(ValueError, match="min_lr"):
+        schedule.multiplier("cosine_with_min_lr", 10, 0, 1e-3)
+    # TrainingArguments.get_warmup_steps: warmup_steps wins, else ceil(total * warmup_ratio)
+    assert schedule.warmup_steps(SimpleNamespace(warmup_steps=0, warmup_ratio=0.25), 10) == 3
+    assert schedule.warmup_steps(SimpleNamespace(warmup_steps=4, warmup_ratio=0.25), 10) == 4
+    assert schedule.warmup_steps(SimpleNamespace(warmup_steps=0.5, warmup_ratio=0.0), 10) == 5
+
+
+@pytest.mark.parametrize("kind,warmup,kw", SCHEDULES)
+def test_scheduler_state_loads_into_transformers_lambdalr(kind, warmup, kw):
     """scheduler.pt is the LambdaLR state_dict transformers' Trainer saves: it
     loads into get_scheduler(...)'s LambdaLR (lr_lambdas key included) and
     equals the state of that scheduler stepped the same number of times."""
     import warnings
 
     from transformers import get_scheduler
+
+    from swh_trl_amd.trainer import schedule
     total, steps, lr = 10, 4, 1e-3
 
     def fresh():
         opt = torch.optim.AdamW([{"params": [torch.nn.Parameter(torch.zeros(1))]} for _ in range(2)], lr=lr)
-        return opt, get_scheduler(kind, opt, num_warmup_steps=warmup, num_training_steps=total)
+        return opt, get_scheduler(kind, opt, num_warmup_steps=warmup, num_training_steps=total,
+                                  scheduler_specific_kwargs=dict(kw or {}))
     opt, stepped = fresh()
     with warnings.catch_warnings():
         warnings.simplefilter("ignore")
         for _ in range(steps):
             opt.step()
             stepped.step()
-    sd = ck.scheduler_state_dict(steps, total, lr, warmup, kind)
+    sd = ck.scheduler_state_dict(steps, lr, schedule.multiplier(kind, total, warmup, lr, kw))
     _, loaded = fresh()
     loaded.load_state_dict(sd)
     assert loaded.last_epoch == stepped.last_epoch == steps

@@ -41,7 +41,7 @@ def _worker(rank, world, port, q, steps, pdb=8, ga=2):
         tr.train()
         torch.cuda.synchronize()
         flat = tr.model.flat.float().cpu().numpy()
-        log = tr.state.log_history[-1]
+        log = [h for h in tr.state.log_history if "loss" in h][-1]
         q.put((rank, (hashlib.sha256(flat.tobytes()).hexdigest(), float(flat.astype("float64").sum()),
                       log["reward"], log["loss"])))
     except Exception as e:  # surface the failure to the parent

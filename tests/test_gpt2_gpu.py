@@ -252,9 +252,10 @@ def test_cfg1_trainer_runs_saves_and_reloads(dev, tmp_path):
                       generation_kwargs={"eos_token_id": EOS, "pad_token_id": PAD})
     tr = GRPOTrainer(model=hf, reward_funcs=_reward_product, args=args, train_dataset=ds)
     before = tr.model.flat.clone()
-    state = tr.train()
-    assert state.global_step == 2 and not torch.equal(before, tr.model.flat)
-    assert math.isfinite(state.log_history[-1]["loss"])
+    out = tr.train()
+    assert out.global_step == 2 and tr.state.global_step == 2 and not torch.equal(before, tr.model.flat)
+    assert math.isfinite(out.training_loss)
+    assert math.isfinite([h for h in tr.state.log_history if "loss" in h][-1]["loss"])
     tr.save_model(str(tmp_path / "final"))
     back = GPT2LMHeadModel.from_pretrained(str(tmp_path / "final"), torch_dtype=torch.float32).to(dev).eval()
     ids = torch.randint(0, 1024, (2, 20), generator=_gen(0)).to(dev)

@@ -60,6 +60,40 @@ def test_grpo_config_bookkeeping():
     assert c.extra == {"some_unknown_field": 1}
 
 
+def test_grpo_config_eval_and_strategy_fields():
+    """TrainingArguments fields the drop-in honours: eval_strategy "no"/"steps"
+    (the older `evaluation_strategy` name too), eval batches of whole groups,
+    save_strategy "no"/"steps"; other strategies raise instead of being ignored."""
+    c = GRPOConfig(per_device_train_batch_size=8, num_generations=4, evaluation_strategy="steps",
+                   per_device_eval_batch_size=8, eval_steps=2, lr_scheduler_type="cosine",
+                   lr_scheduler_kwargs={"num_cycles": 1.0}, warmup_ratio=0.1)
+    assert c.eval_strategy == "steps" and c.eval_steps == 2 and "evaluation_strategy" not in c.extra
+    assert c.lr_scheduler_kwargs == {"num_cycles": 1.0} and c.warmup_ratio == 0.1
+    with pytest.raises(ValueError, match="eval batch"):
+        GRPOConfig(per_device_train_batch_size=8, num_generations=4, eval_strategy="steps",
+                   per_device_eval_batch_size=6)
+    for bad in ({"eval_strategy": "epoch"}, {"save_strategy": "epoch"}):
+        with pytest.raises(ValueError):
+            GRPOConfig(per_device_train_batch_size=8, num_generations=4, **bad)
+
+
+def test_trainers_refuse_user_optimizers():
+    """The reference hands `optimizers` to the transformers Trainer; the fused
+    AdamW of the drop-in cannot be driven by a torch optimizer / scheduler, so a
+    non-default `optimizers` raises (before anything touches a device)."""
+    from swh_trl_amd.trainer import GRPOTrainer, PPOConfig, PPOTrainer
+    p = torch.nn.Parameter(torch.zeros(1))
+    opt = torch.optim.AdamW([p])
+    with pytest.raises(ValueError, match="optimizers"):
+        GRPOTrainer(model="tiny", reward_funcs=lambda **k: [0.0], args=GRPOConfig(per_device_train_batch_size=8,
+                                                                                  num_generations=4),
+                    optimizers=(opt, None))
+    with pytest.raises(ValueError, match="optimizers"):
+        PPOTrainer(args=PPOConfig(), processing_class=None, model="tiny", ref_model=None, reward_model="tiny",
+                   train_dataset=[], value_model="tiny", optimizers=(None, torch.optim.lr_scheduler.LambdaLR(
+                       opt, lambda s: 1.0)))
+
+
 def test_ppo_config_bookkeeping():
     """ppo_trainer.py:224-250 derived batch sizes and their errors."""
     from swh_trl_amd.trainer import PPOConfig

@@ -18,7 +18,7 @@ import pytest
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from fake_tokenizer import make_tokenizer  # noqa: E402
+from fake_tokenizer import make_byte_tokenizer, make_tokenizer  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 V = 512
@@ -30,11 +30,17 @@ def _cfg():
 
 
 def _classifier(dev):
+    """A transformers reward model WITHOUT a pad id in its config: the trainer sets
+    config.pad_token_id from the reward tokenizer (grpo_trainer.py:766-771)."""
     from transformers import Qwen2Config, Qwen2ForSequenceClassification
     torch.manual_seed(0)
-    hc = Qwen2Config(vocab_size=V, hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=2,
-                     num_key_value_heads=1, num_labels=1, pad_token_id=0)
+    hc = Qwen2Config(vocab_size=V, hidden_size=128, intermediate_size=256, num_hidden_layers=2, num_attention_heads=2,
+                     num_key_value_heads=1, num_labels=1)
+    hc.pad_token_id = None
     return Qwen2ForSequenceClassification(hc).to(dev).eval()
+
+
+RM_TOL = dict(rtol=1e-4, atol=1e-4)  # the fp32 engine copy of the reward model against transformers fp32
 
 
 @pytest.mark.parametrize("bootstrap", [False, True])
@@ -94,7 +100,8 @@ def test_conversational_prompts_and_reward_model(bootstrap):
     enc = tok(text=msgs, return_tensors="pt", padding=True, padding_side="right", add_special_tokens=False)
     with torch.inference_mode():
         exp = rm(**{k: v.to(dev) for k, v in enc.items()}).logits[:, 0].float().cpu()
-    torch.testing.assert_close(got["rpf"][:, 1], exp)
+    torch.testing.assert_close(got["rpf"][:, 1], exp, **RM_TOL)
+    assert rm.config.pad_token_id == tok.pad_token_id  # set by the trainer (:770)
     torch.testing.assert_close(got["rpf"][:, 0], torch.tensor([float(len(c[0]["content"].split()) % 3)
                                                                for c in completions]))
 
@@ -125,7 +132,102 @@ def test_reward_model_plain_text_prompts():
     enc = tok(text=texts, return_tensors="pt", padding=True, padding_side="right", add_special_tokens=False)
     with torch.inference_mode():
         exp = rm(**{k: v.to(dev) for k, v in enc.items()}).logits[:, 0].float().cpu()
-    torch.testing.assert_close(got["rpf"][:, 0], exp)
+    torch.testing.assert_close(got["rpf"][:, 0], exp, **RM_TOL)
+
+
+def _text_dataset(n=4):
+    return [{"prompt": " ".join(f"w{5 + (7 * i + j) % 400}" for j in range(6)) + " "} for i in range(n)]
+
+
+def _train_and_capture(tr):
+    got = {}
+    calc = tr._calculate_rewards
+
+    def capture(examples, *a):
+        out = calc(examples, *a)
+        got["rpf"], got["examples"], got["ids"] = out.cpu().clone(), examples, a[3].cpu().clone()
+        return out
+
+    tr._calculate_rewards = capture
+    tr.train()
+    return got
+
+
+def _expected_scores(rm, tok, got, dev):
+    texts = [x["prompt"] + c for x, c in zip(got["examples"], tok.batch_decode(got["ids"], skip_special_tokens=True))]
+    enc = tok(text=texts, return_tensors="pt", padding=True, padding_side="right", add_special_tokens=False)
+    with torch.inference_mode():
+        return rm(**{k: v.to(dev) for k, v in enc.items()}).logits[:, 0].float().cpu()
+
+
+def test_string_reward_model_loads_from_local_directory(tmp_path):
+    """grpo_trainer.py:731-739, :754-771: a string reward function is loaded as
+    AutoModelForSequenceClassification(num_labels=1) (here from a local directory,
+    onto the engine's score head, in model_init_kwargs' dtype), named by the last
+    component of its path, its tokenizer loaded from the same place when
+    reward_processing_classes is None and its pad id written into the config."""
+    from transformers import AutoModelForSequenceClassification, AutoTokenizer
+
+    from swh_trl_amd.trainer import GRPOConfig, GRPOTrainer
+    from swh_trl_amd.trainer.grpo_trainer import RewardModel
+    dev = torch.device("cuda:0")
+    tok = make_tokenizer(V)
+    d = tmp_path / "my-reward-model"
+    _classifier("cpu").save_pretrained(str(d))
+    make_byte_tokenizer().save_pretrained(str(d))  # the reward model's own tokenizer, found through its path
+    args = GRPOConfig(per_device_train_batch_size=8, gradient_accumulation_steps=1, num_generations=4,
+                      max_prompt_length=16, max_completion_length=8, max_steps=1, seed=3, shuffle_dataset=False,
+                      save_strategy="no", model_init_kwargs={"torch_dtype": "float32"})
+    tr = GRPOTrainer(model=_cfg(), reward_funcs=str(d), args=args, train_dataset=_text_dataset(), processing_class=tok)
+    assert tr.reward_func_names == ["my-reward-model"]
+    assert isinstance(tr.reward_funcs[0], RewardModel) and tr.reward_funcs[0].model.dtype == torch.float32
+    rtok = AutoTokenizer.from_pretrained(str(d))
+    assert type(tr.reward_processing_classes[0]) is type(rtok) and rtok.pad_token_id == 256
+    assert tr.reward_funcs[0].config.pad_token_id == 256
+    got = _train_and_capture(tr)
+    rm = AutoModelForSequenceClassification.from_pretrained(str(d), num_labels=1, dtype=torch.float32).to(dev).eval()
+    rm.config.pad_token_id = rtok.pad_token_id
+    torch.testing.assert_close(got["rpf"][:, 0], _expected_scores(rm, rtok, got, dev), **RM_TOL)
+    assert any("rewards/my-reward-model/mean" in h for h in tr.state.log_history)
+    with pytest.raises(ValueError, match="not a local directory"):
+        GRPOTrainer(model=_cfg(), reward_funcs="org/some-hub-model", args=args, train_dataset=_text_dataset(),
+                    processing_class=tok)
+
+
+def test_module_reward_model_pads_with_eos_and_is_named_by_path(tmp_path):
+    """A reward tokenizer without a pad token pads with EOS (:766-767) and the
+    model's config.pad_token_id follows (:770), so the score is read at the last
+    non-EOS token, as transformers does.  A module's metric name is the last
+    path component of its config._name_or_path (:737)."""
+    from tokenizers import Tokenizer, models, pre_tokenizers
+    from transformers import PreTrainedTokenizerFast, Qwen2ForSequenceClassification
+
+    from swh_trl_amd.trainer import GRPOConfig, GRPOTrainer
+    dev = torch.device("cuda:0")
+    vocab = {"[PAD]": 0, "[EOS]": 1, "<system>": 2, "<user>": 3, "<assistant>": 4}
+    vocab.update({f"w{i}": i for i in range(5, V)})
+    tk = Tokenizer(models.WordLevel(vocab=vocab, unk_token="[PAD]"))
+    tk.pre_tokenizer = pre_tokenizers.WhitespaceSplit()
+    nopad = PreTrainedTokenizerFast(tokenizer_object=tk, eos_token="[EOS]")
+    assert nopad.pad_token_id is None
+    d = tmp_path / "rm-nopad"
+    _classifier("cpu").save_pretrained(str(d))
+    rm = Qwen2ForSequenceClassification.from_pretrained(str(d), dtype=torch.float32).to(dev).eval()
+    assert rm.config.pad_token_id is None
+    tok = make_tokenizer(V)
+    args = GRPOConfig(per_device_train_batch_size=8, gradient_accumulation_steps=1, num_generations=4,
+                      max_prompt_length=16, max_completion_length=8, max_steps=1, seed=4, shuffle_dataset=False,
+                      save_strategy="no")
+    tr = GRPOTrainer(model=_cfg(), reward_funcs=[rm], args=args, train_dataset=_text_dataset(), processing_class=tok,
+                     reward_processing_classes=nopad)
+    rtok = tr.reward_processing_classes[0]
+    assert rtok is nopad and rtok.pad_token == "[EOS]" and rtok.pad_token_id == 1
+    assert rm.config.pad_token_id == 1 and tr.reward_func_names == ["rm-nopad"]
+    got = _train_and_capture(tr)
+    torch.testing.assert_close(got["rpf"][:, 0], _expected_scores(rm, rtok, got, dev), **RM_TOL)
+    with pytest.raises(ValueError, match="number of reward processing classes"):
+        GRPOTrainer(model=_cfg(), reward_funcs=[rm], args=args, train_dataset=_text_dataset(),
+                    processing_class=tok, reward_processing_classes=[tok, tok])
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
