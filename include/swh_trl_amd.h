@@ -415,17 +415,7 @@ int swh_embed_gather(const void *table, const int64_t *ids, int64_t B, int64_t H
 int swh_attn_decode(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
                     const float *rope_sin, const int32_t *prompt_len, const int32_t *state, int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax, float scale, void *out,
                     void *stream);
-/* swh_attn_decode plus cache warming for the next weight-bound launch: extra
- * workgroup rows (about as many as the attention's Hkv x B) read the gate/up
- * weights pf_w bf16 [2 pf_n, pf_k] (SiLU pair layout: gate rows, then up rows)
- * tile by tile into the L2 of the XCD whose swh_decode_gemm(silu) workgroups
- * consume that tile.  Results are those of swh_attn_decode; pf_w == NULL is
- * swh_attn_decode.  pf_n % 8 == 0, pf_k % 8 == 0, pf_w 16-B aligned. */
-int swh_attn_decode_prefetch(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
-                             const float *rope_sin, const int32_t *prompt_len, const int32_t *state, int64_t B,
-                             int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax, float scale, void *out,
-                             const void *pf_w, int64_t pf_n, int64_t pf_k, void *stream);
-/* swh_attn_decode_prefetch where the prompt keys / values of row b (cache slots
+/* swh_attn_decode where the prompt keys / values of row b (cache slots
  * P - prompt_len[b] .. P - 1) are read from row prompt_row[b]'s cache: the G
  * generations of a GRPO prompt (RepeatSampler copies, trl/trainer/grpo_trainer.py:1096-1130)
  * hold identical prompt K/V, so one copy serves the group (HBM reads it once).
@@ -434,7 +424,7 @@ int swh_attn_decode_prefetch(const void *qkv, void *k_cache, void *v_cache, cons
 int swh_attn_decode_shared(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
                            const float *rope_sin, const int32_t *prompt_len, const int32_t *prompt_row,
                            const int32_t *state, int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax,
-                           float scale, void *out, const void *pf_w, int64_t pf_n, int64_t pf_k, void *stream);
+                           float scale, void *out, void *stream);
 /* swh_attn_decode_shared; out_frag = 1 writes `out` in the fragment order that
  * swh_decode_gemm_fragw reads with act_frag bit 1 (element (b, c) of [B, Hq*D] at
  * (((b/16) (Hq*D/32) + c/32) 64 + 16 ((c/8) % 4) + b % 16) 8 + c % 8), so o_proj
@@ -443,8 +433,7 @@ int swh_attn_decode_shared(const void *qkv, void *k_cache, void *v_cache, const 
 int swh_attn_decode_shared_frag(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
                                 const float *rope_sin, const int32_t *prompt_len, const int32_t *prompt_row,
                                 const int32_t *state, int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax,
-                                float scale, void *out, const void *pf_w, int64_t pf_n, int64_t pf_k,
-                                int32_t out_frag, void *stream);
+                                float scale, void *out, int32_t out_frag, void *stream);
 
 /* Weight-streaming decode GEMM Y[M,N] = X[M,K] W[N,K]^T (bf16, fp32 MFMA
  * accumulation, K % 64 == 0, 16-B aligned operands, ldy % 8 == 0) with the
@@ -543,55 +532,18 @@ int swh_lm_head_sample_step_fragw(const void *x, const void *w, int64_t M, int64
                                   int64_t *cur_tokens, const void *embed, void *x_next, float *ss_next,
                                   void *workspace, int64_t workspace_bytes, void *stream);
 
-/* swh_decode_gemm_fragw with l3_wgs Infinity Cache warm-up workgroups appended
- * to its launch when the shape runs register-streamed (the decode qkv / o / down
- * projections; other geometries ignore them): they read the l3_njobs (<= 8)
- * ranges {const void *ptr, int64_t bytes / 16, int64_t stripe} (as swh_attn_decode_l3) on the CUs the projection's tiles
- * leave idle; l3_sink >= l3_wgs x 512 uint32.  Results identical. */
-int swh_decode_gemm_fragw_l3(const void *x, const void *w, int64_t M, int64_t N, int64_t K, float eps,
-                             const void *bias, void *residual, int32_t silu, void *y, int64_t ldy, const float *ss_in,
-                             float *ss_out, int32_t act_frag, const void *l3_jobs, int32_t l3_njobs, int32_t l3_wgs,
-                             void *l3_sink, void *workspace, int64_t workspace_bytes, void *stream);
 /* swh_attn_decode_shared_frag whose launch also carries >= l3_wgs Infinity Cache
  * warm-up workgroups (rounded up to whole grid rows of Hkv) on the CUs the
  * attention's B x Hkv workgroups leave idle: they read the l3_njobs (<= 8)
- * ranges {const void *ptr, int64_t bytes / 16, int64_t stripe} and discard the
- * data (stripe 0: contiguous shares; else the range is cut into column blocks of
- * `stripe` 16-B units and block c is read by a workgroup of logical XCD c % 8,
- * where decode_gemm's register-streamed and tile launches run it), so the
- * projections that follow (o_proj and down_proj of this layer, qkv of the next)
- * find their weights on-die; l3_sink >= rounded workgroups x 512 uint32 of
+ * ranges {const void *ptr, int64_t bytes / 16, int64_t 0} (16-B aligned device
+ * memory) in contiguous shares and discard the data, so the projections that
+ * follow (o_proj and down_proj of this layer, qkv of the next) find their
+ * weights on-die; l3_sink >= rounded workgroups x 512 uint32 of
  * scratch.  Results identical to swh_attn_decode_shared_frag. */
 int swh_attn_decode_l3(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos, const float *rope_sin,
                        const int32_t *prompt_len, const int32_t *prompt_row, const int32_t *state, int64_t B,
                        int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax, float scale, void *out, int32_t out_frag,
                        const void *l3_jobs, int32_t l3_njobs, int32_t l3_wgs, void *l3_sink, void *stream);
-/* Infinity Cache warm-up: nwg workgroups read every byte of the njobs ranges
- * jobs[j] = {const void *ptr, int64_t bytes / 16, int64_t 0} (device memory, 16-B aligned)
- * and keep nothing but a sink word (>= nwg * 256 uint32 of scratch, written
- * only if an XOR of the data equals a magic constant).  Captured on a side
- * branch of the decode graph to pull layer l+1's decode weights on-die while
- * layer l runs (the per-token weight stream, grpo_trainer.py:1804's
- * model.generate, exceeds the 256 MiB Infinity Cache).  nontemporal: nt loads. */
-int swh_l3_prefetch(const void *jobs, int32_t njobs, int32_t nwg, int32_t nontemporal, void *sink, void *stream);
-
-/* swh_frag_pack with kmajor = 1: the same 1 KB fragments with the k-step
- * outermost (piece (ks * G + g) * 64 + lane, G = 16-row groups), so the lm-head
- * tile kernel's waves that load k-step ks of consecutive tiles read one
- * contiguous run; kmajor = 0 is swh_frag_pack. */
-int swh_frag_pack_kmajor(const void *w, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst,
-                         int32_t kmajor, void *stream);
-/* swh_lm_head_sample_fragw / swh_lm_head_sample_step_fragw over the k-major
- * layout of swh_frag_pack_kmajor(..., 1, ...): same draws. */
-int swh_lm_head_sample_fragk(const void *x, const void *w, int64_t M, int64_t V, int64_t K, float eps,
-                             const float *ss_in, const swh_sample_params *params, const uint64_t *rng,
-                             const int32_t *step, int32_t *finished, int64_t *out_tokens, int64_t out_ld,
-                             int64_t *cur_tokens, void *workspace, int64_t workspace_bytes, void *stream);
-int swh_lm_head_sample_step_fragk(const void *x, const void *w, int64_t M, int64_t V, int64_t K, float eps,
-                                  const float *ss_in, const swh_sample_params *params, const uint64_t *rng,
-                                  int32_t *step, int32_t *finished, int64_t *out_tokens, int64_t out_ld,
-                                  int64_t *cur_tokens, const void *embed, void *x_next, float *ss_next,
-                                  void *workspace, int64_t workspace_bytes, void *stream);
 
 /* ---- GPT-2 family (BASELINE.json config 1) --------------------------------
  * transformers GPT2Block's LayerNorms and NewGELUActivation (the modeling code

@@ -108,12 +108,10 @@ SIGNATURES = {
                              c_i32, c_vp]),
     "swh_attn_decode": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32,
                                 c_f32, c_vp, c_vp]),
-    "swh_attn_decode_prefetch": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32,
-                                         c_i32, c_f32, c_vp, c_vp, c_i64, c_i64, c_vp]),
     "swh_attn_decode_shared": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32,
-                                       c_i32, c_f32, c_vp, c_vp, c_i64, c_i64, c_vp]),
+                                       c_i32, c_f32, c_vp, c_vp]),
     "swh_attn_decode_shared_frag": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32,
-                                            c_i32, c_i32, c_f32, c_vp, c_vp, c_i64, c_i64, c_i32, c_vp]),
+                                            c_i32, c_i32, c_f32, c_vp, c_i32, c_vp]),
     "swh_decode_gemm_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "swh_lm_head_sample_workspace_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "swh_lm_head_sample": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_f32, c_vp, C.POINTER(SampleParams),
@@ -134,16 +132,6 @@ SIGNATURES = {
                                       c_vp, c_i32, c_vp, c_i64, c_vp]),
     "swh_wide_gemm_packed": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_f32, c_vp, c_vp, c_i32, c_vp, c_i64, c_vp,
                                      c_vp, c_vp, c_i64, c_vp]),
-    "swh_l3_prefetch": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp]),
-    "swh_frag_pack_kmajor": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i32, c_vp, c_i32, c_vp]),
-    "swh_lm_head_sample_step_fragk": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_f32, c_vp, C.POINTER(SampleParams),
-                                              c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
-                                              c_vp]),
-    "swh_lm_head_sample_fragk": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_f32, c_vp, C.POINTER(SampleParams),
-                                         c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
-
-    "swh_decode_gemm_fragw_l3": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_f32, c_vp, c_vp, c_i32, c_vp, c_i64,
-                                         c_vp, c_vp, c_i32, c_vp, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp]),
     "swh_attn_decode_l3": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32,
                                    c_f32, c_vp, c_i32, c_vp, c_i32, c_i32, c_vp, c_vp]),
 }

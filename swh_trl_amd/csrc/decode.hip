@@ -35,8 +35,7 @@ int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, flo
 int64_t wide_gemm_slab_bytes(int64_t M, int64_t N, int64_t K, int32_t silu);
 bool wide_gemm_eligible(int64_t M, int64_t N, int64_t K, int32_t silu);
 int wide_pack(const void *src, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, hipStream_t stream);
-int frag_pack(const void *src, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, hipStream_t stream,
-              int32_t kmajor = 0);
+int frag_pack(const void *src, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, hipStream_t stream);
 
 namespace {
 
@@ -578,29 +577,20 @@ __global__ __launch_bounds__(MAXT) void decode_gemm_kernel(
 // Infinity Cache warm-up job: a device range read (and discarded) by warm-up workgroups
 struct L3Job {
     const uint4 *p;
-    int64_t n16;     // 16-B units
-    int64_t stripe;  // 0: a contiguous share per workgroup; else 16-B units per column block, block c read
-                     // by a workgroup of (logical) XCD c % 8, the XCD the consuming launch runs block c on
+    int64_t n16;       // 16-B units
+    int64_t reserved;  // 0
 };
 constexpr int kL3MaxJobs = 8;
-
-// warm-up workgroups appended to a launch: blocks >= gx0 read one share of the jobs
-struct L3Warm {
-    const L3Job *jobs = nullptr;
-    int njobs = 0;
-    int gx0 = 0;               // the launch's own blocks (the rest warm)
-    uint32_t *sink = nullptr;  // >= warm-up blocks x NT words, written never in practice
-};
 
 // warm-up workgroup p of npf (NT threads): a contiguous share of the jobs' bytes,
 // 8 x 16-B loads in flight per thread, XOR-ed into a word stored only if it
 // equals a magic constant
 template <int NT>
 __device__ __forceinline__ void l3_warm_share(const L3Job *__restrict__ jobs, int njobs, int p, int npf,
-                                              uint32_t *__restrict__ sink, int lin) {
+                                              uint32_t *__restrict__ sink) {
     const int tid = threadIdx.x;
     int64_t tot = 0;
-    for (int j = 0; j < njobs; ++j) tot += jobs[j].stripe ? 0 : jobs[j].n16;
+    for (int j = 0; j < njobs; ++j) tot += jobs[j].n16;
     const int64_t share = (tot + npf - 1) / npf, lo = (int64_t)p * share, hi = min(tot, lo + share);
     uint32_t acc = 0;
     auto sweep = [&](const uint4 *src, int64_t a, int64_t e) {
@@ -616,14 +606,8 @@ __device__ __forceinline__ void l3_warm_share(const L3Job *__restrict__ jobs, in
         }
     };
     int64_t base = 0;
-    const int xcd = lin & 7, q = p >> 3, nq = max(npf >> 3, 1);
     for (int j = 0; j < njobs; ++j) {
-        const int64_t n = jobs[j].n16, st = jobs[j].stripe;
-        if (st) {  // column blocks c = xcd + 8 (q + nq t): into the L2 of the XCD that consumes them
-            for (int64_t c = xcd + 8 * (int64_t)q; c * st < n; c += 8 * (int64_t)nq)
-                sweep(jobs[j].p + c * st, 0, min(st, n - c * st));
-            continue;
-        }
+        const int64_t n = jobs[j].n16;
         sweep(jobs[j].p, max(lo - base, (int64_t)0), min(hi - base, n));
         base += n;
     }
@@ -650,13 +634,8 @@ __global__ __launch_bounds__(512) void xstream_gemm_kernel(const uint16_t *__res
                                                            float eps, const float *__restrict__ ss_in,
                                                            const uint16_t *__restrict__ bias,
                                                            uint16_t *__restrict__ res, float *__restrict__ ss_out,
-                                                           uint16_t *__restrict__ y, int ldy, int fw, int xf,
-                                                           L3Warm warm) {
+                                                           uint16_t *__restrict__ y, int ldy, int fw, int xf) {
     static_assert(EPI != EPI_SILU && NM != 1, "plain / residual epilogues, folded or no norm");
-    if (warm.jobs && (int)blockIdx.x >= warm.gx0) {  // Infinity Cache warm-up blocks past the tiles
-        l3_warm_share<512>(warm.jobs, warm.njobs, blockIdx.x - warm.gx0, gridDim.x - warm.gx0, warm.sink, blockIdx.x);
-        return;
-    }
     constexpr int NW = 8, NT = 512, MR = 16 * MS, NB = 16, LDR = MR + 4, G8 = NB / 8, F = NW;
     __shared__ __attribute__((aligned(16))) float part[(NW + 1) * NB * LDR];
     __shared__ float rstd_s[MR];
@@ -857,12 +836,9 @@ __global__ __launch_bounds__(RD ? 768 : 512) void lm_head_kernel(const uint16_t 
         if constexpr (EPI == EPI_SILU) return (rl < 8) ? tile * 8 + rl : N + tile * 8 + rl - 8;  // gate, then up
         return (int64_t)tile * 16 + rl;
     };
-    // fw 1: tile t's fragments for k-step ks at ((t KS + ks) 64 + lane) 8 (one 1 KB run per load);
-    // fw 2 (k-major): at ((ks ntile + t) 64 + lane) 8, so the waves loading k-step ks of
-    // consecutive tiles read one contiguous run
-    const int64_t wst = smp.fw == 2 ? (int64_t)ntile * 512 : smp.fw ? 512 : 32;
+    // fw 1: tile t's fragments for k-step ks at ((t KS + ks) 64 + lane) 8 (one 1 KB run per load)
+    const int64_t wst = smp.fw ? 512 : 32;
     auto wbase = [&](int tile) -> const uint16_t * {
-        if (smp.fw == 2) return w + ((int64_t)tile * 64 + lane) * 8;
         return smp.fw ? w + ((int64_t)tile * KS * 64 + lane) * 8 : w + wrow_of(tile) * K + kq;
     };
     auto issue = [&](int tile) {
@@ -1299,23 +1275,18 @@ __device__ __forceinline__ bf16x4s lds_read_tr16(const uint16_t *p) {
         (__attribute__((address_space(3))) bf16x4s *)(const_cast<uint16_t *>(p)));
 }
 
-// Cache warming riding on the attention launch: the attention grid covers only
-// Hkv x B workgroups (128 of 256 CUs at the bench shape), so extra workgroup rows
-// read the SAME layer's gate/up weight tiles (SiLU tile layout: tile t = gate rows
-// 8t.. and up rows N + 8t..) into the L2 of the XCD whose gate/up workgroups will
-// consume them (tile t runs on XCD t mod 8 there, workgroup id mod 8 here), by
-// LDS-DMA into a scratch tile (no registers, nothing consumed).
+// Per-launch options of the decode attention.  The attention grid covers only
+// Hkv x B workgroups (128 of 256 CUs at the bench shape); with `jobs`, extra grid
+// rows read the weights of the projections that follow into the Infinity Cache
+// (swh_attn_decode_l3) and exit.
 struct AttnPrefetch {
-    const uint16_t *w;     // [2N, K] gate/up weights, or null
-    int n, k;              // N (SiLU pairs), K
-    int rows;              // attention rows (B): grid rows past it prefetch
+    int rows;              // attention rows (B): grid rows past it warm the cache
     const int32_t *prow;   // [B] row whose cache holds this row's prompt keys / values, or null (own row)
     int ofrag = 0;         // output in the fragment order o_proj's register-streamed A operand reads (B % 16 == 0)
     const L3Job *jobs = nullptr;  // Infinity Cache warm-up ranges (grid rows past `rows` read them), or null
     int njobs = 0;
     uint32_t *sink = nullptr;     // >= warm-up workgroups x 512 words, written never in practice
     int nwg = 0;                  // warm-up workgroups wanted (rounded up to whole grid rows)
-    int xrows = 0;                // XCD-contiguous row order of the attention workgroups
 };
 
 // element (row b, column c) of a [B, K] activation in the fragment order of
@@ -1344,44 +1315,15 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
     __shared__ __attribute__((aligned(16))) uint16_t vt_s[kAttnWaves][32 * VS];
     __shared__ float red_s[kAttnWaves][16][D + 2];
 
-    // XCD-contiguous rows (speed only: a permutation of the workgroups): blocks are dealt
-    // round-robin over the 8 XCDs, so flat index f = xcd * (WGs / 8) + (lin / 8) gives each
-    // XCD a run of consecutive rows of one KV head — a GRPO group's rows, which read one
-    // copy of the group's prompt K/V, then hit in that XCD's L2 (SWH_ATTN_XCD_ROWS=1; off by default)
-    int kvh = blockIdx.x;
-    int64_t b = blockIdx.y;
-    {
-        const int nmain = Hkv * pf.rows, lin = blockIdx.y * gridDim.x + blockIdx.x;
-        if (pf.xrows && lin < nmain && (nmain & 7) == 0) {
-            const int f = (lin & 7) * (nmain >> 3) + (lin >> 3);
-            kvh = f / pf.rows;
-            b = f - kvh * pf.rows;
-        }
-    }
+    const int kvh = blockIdx.x;
+    const int64_t b = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int g = lane >> 4, c16 = lane & 15;
     SWH_GEMM_TRACE(0);  // phase stamps for tools/attn_probe.py (instrumented build only)
-    if ((int)blockIdx.y >= pf.rows && pf.jobs) {  // an Infinity Cache warm-up workgroup
-        l3_warm_share<kAttnThreads>(pf.jobs, pf.njobs, (blockIdx.y - pf.rows) * gridDim.x + blockIdx.x,
-                                    (gridDim.y - pf.rows) * gridDim.x, pf.sink, blockIdx.y * gridDim.x + blockIdx.x);
-        return;
-    }
-    if ((int)blockIdx.y >= pf.rows) {  // a prefetch workgroup
-        const int lin = blockIdx.y * gridDim.x + blockIdx.x, p = lin - pf.rows * gridDim.x;
-        const int npf = (gridDim.y - pf.rows) * gridDim.x / 8 * 8;  // whole groups of 8: every XCD covered
-        if (p >= npf) return;
-        const int xcd = lin & 7, j = p >> 3, per = npf >> 3;
-        const int ppr = pf.k / 8, ntile = pf.n / 8;
-        unsigned char *scratch = reinterpret_cast<unsigned char *>(vt_s[wid]);
-        for (int t = xcd + 8 * j; t < ntile; t += 8 * per) {
-            for (int pc = tid; pc < 16 * ppr; pc += kAttnThreads) {
-                const int r = pc / ppr, c = pc - r * ppr;
-                const int64_t row = (r < 8) ? (int64_t)t * 8 + r : (int64_t)pf.n + (int64_t)t * 8 + r - 8;
-                __builtin_amdgcn_global_load_lds(pf.w + row * pf.k + c * 8,
-                                                 (__attribute__((address_space(3))) void *)scratch, 16, 0, 0);
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if ((int)blockIdx.y >= pf.rows) {  // an Infinity Cache warm-up workgroup
+        if (pf.jobs)
+            l3_warm_share<kAttnThreads>(pf.jobs, pf.njobs, (blockIdx.y - pf.rows) * gridDim.x + blockIdx.x,
+                                        (gridDim.y - pf.rows) * gridDim.x, pf.sink);
         return;
     }
     // state[0] = index of the token sampled this step; the input token is state[0] - 1
@@ -1589,26 +1531,14 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
 #undef SWH_ATTN_ISSUE
 }
 
-// SWH_ATTN_XCD_ROWS=1 (read per call): XCD-contiguous attention rows.  Measured
-// 7.45-7.58 against 7.29-7.31 us per launch, decode step unchanged: off by default
-inline int attn_xcd_rows() {
-    const char *e = getenv("SWH_ATTN_XCD_ROWS");
-    return (e && e[0] == '1') ? 1 : 0;
-}
-
 template <int D, int GQ>
 int launch_attn(const uint16_t *q, uint16_t *kc, uint16_t *vc, const float *rc, const float *rs, const int32_t *pl,
                 const int32_t *st, int64_t B, int Hq, int Hkv, int Tmax, float scale, uint16_t *o, hipStream_t s,
                 const AttnPrefetch &pf) {
-    // prefetch rows: about as many workgroups as the attention itself has, in groups of 8
+    // warm-up rows: whole grid rows of Hkv workgroups
     int64_t extra = 0;
     if (pf.jobs) {
         extra = (pf.nwg + Hkv - 1) / Hkv;
-        if (B + extra > 65535) extra = 0;
-    } else if (pf.w) {
-        static const int mult = getenv("SWH_PF_MULT") ? atoi(getenv("SWH_PF_MULT")) : 2;  // 1-3 measured
-        const int64_t want = (mult * B * Hkv + 7) / 8 * 8;
-        extra = (want + Hkv - 1) / Hkv;
         if (B + extra > 65535) extra = 0;
     }
     attn_decode_kernel<D, GQ><<<dim3((unsigned)Hkv, (unsigned)(B + extra)), kAttnThreads, 0, s>>>(
@@ -1786,32 +1716,24 @@ int launch_gemm(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const ui
 template <int KW, int MS, int NM, int EPI, bool BIAS>
 int launch_xstream_kw(const GemmCfg &c, hipStream_t s, const uint16_t *X, const uint16_t *W, int m, int n, int k,
                       float eps, const float *ss_in, const uint16_t *Bs, uint16_t *R, float *ss_out, uint16_t *Y,
-                      int ld, const L3Warm *warm) {
-    L3Warm wm;
-    int gx = c.gx;
-    if (warm && warm->jobs) {
-        wm = *warm;
-        wm.gx0 = c.gx;
-        gx += warm->gx0;  // (the caller passes the warm-up block count in gx0)
-    }
-    xstream_gemm_kernel<KW, MS, NM, EPI, BIAS, 0><<<dim3((unsigned)gx), 512, 0, s>>>(X, W, m, n, k, eps, ss_in, Bs, R,
-                                                                                 ss_out, Y, ld, c.fw, c.xf, wm);
+                      int ld) {
+    xstream_gemm_kernel<KW, MS, NM, EPI, BIAS, 0><<<dim3((unsigned)c.gx), 512, 0, s>>>(X, W, m, n, k, eps, ss_in, Bs,
+                                                                                    R, ss_out, Y, ld, c.fw, c.xf);
     return launch_status();
 }
 
 template <int MS, int NM, int EPI, bool BIAS>
 int launch_xstream_ms(const GemmCfg &c, hipStream_t s, const uint16_t *X, const uint16_t *W, int m, int n, int k,
                       float eps, const float *ss_in, const uint16_t *Bs, uint16_t *R, float *ss_out, uint16_t *Y,
-                      int ld, const L3Warm *warm) {
+                      int ld) {
     const int ks = k / 32, kwn = (ks + 7) / 8;
-    if (kwn <= 2) return launch_xstream_kw<2, MS, NM, EPI, BIAS>(c, s, X, W, m, n, k, eps, ss_in, Bs, R, ss_out, Y, ld, warm);
-    if (kwn <= 4) return launch_xstream_kw<4, MS, NM, EPI, BIAS>(c, s, X, W, m, n, k, eps, ss_in, Bs, R, ss_out, Y, ld, warm);
-    return launch_xstream_kw<8, MS, NM, EPI, BIAS>(c, s, X, W, m, n, k, eps, ss_in, Bs, R, ss_out, Y, ld, warm);
+    if (kwn <= 2) return launch_xstream_kw<2, MS, NM, EPI, BIAS>(c, s, X, W, m, n, k, eps, ss_in, Bs, R, ss_out, Y, ld);
+    if (kwn <= 4) return launch_xstream_kw<4, MS, NM, EPI, BIAS>(c, s, X, W, m, n, k, eps, ss_in, Bs, R, ss_out, Y, ld);
+    return launch_xstream_kw<8, MS, NM, EPI, BIAS>(c, s, X, W, m, n, k, eps, ss_in, Bs, R, ss_out, Y, ld);
 }
 
 int launch_xstream(const GemmCfg &c, hipStream_t s, const uint16_t *X, const uint16_t *W, int m, int n, int k, int nm,
-                   float eps, const float *ss_in, const uint16_t *Bs, uint16_t *R, float *ss_out, uint16_t *Y, int ld,
-                   const L3Warm *warm = nullptr) {
+                   float eps, const float *ss_in, const uint16_t *Bs, uint16_t *R, float *ss_out, uint16_t *Y, int ld) {
     const char *e = getenv("SWH_XSTREAM");  // A/B: 0 = decode_gemm_kernel's LDS image
     const int ks = k / 32;
     if (((e && e[0] == '0') && !c.xf) || c.cb != 1 || c.wn != 1 || c.s != 1 || c.persist || c.nw != 8 || n % 16 ||
@@ -1823,16 +1745,16 @@ int launch_xstream(const GemmCfg &c, hipStream_t s, const uint16_t *X, const uin
             if (m % 16 || (ks + 7) / 8 > 19) return 1;
             if ((ks + 7) / 8 > 8)
                 return launch_xstream_kw<19, 1, 0, EPI_RESIDUAL, false>(c, s, X, W, m, n, k, eps, nullptr, nullptr, R,
-                                                                       ss_out, nullptr, ld, warm);
+                                                                       ss_out, nullptr, ld);
         }
         return launch_xstream_ms<1, 0, EPI_RESIDUAL, false>(c, s, X, W, m, n, k, eps, nullptr, nullptr, R, ss_out, nullptr,
-                                                            ld, warm);
+                                                            ld);
     }
     if (c.xf) return 1;
     if (nm != 2 || !ss_in || !Bs || !Y) return 1;  // qkv: folded norm + bias
     if (c.ms == 1)
-        return launch_xstream_ms<1, 2, EPI_PLAIN, true>(c, s, X, W, m, n, k, eps, ss_in, Bs, nullptr, nullptr, Y, ld, warm);
-    return launch_xstream_ms<2, 2, EPI_PLAIN, true>(c, s, X, W, m, n, k, eps, ss_in, Bs, nullptr, nullptr, Y, ld, warm);
+        return launch_xstream_ms<1, 2, EPI_PLAIN, true>(c, s, X, W, m, n, k, eps, ss_in, Bs, nullptr, nullptr, Y, ld);
+    return launch_xstream_ms<2, 2, EPI_PLAIN, true>(c, s, X, W, m, n, k, eps, ss_in, Bs, nullptr, nullptr, Y, ld);
 }
 
 template <int MS, int NM, int EPI, bool BIAS>
@@ -1919,30 +1841,35 @@ int launch_tiles(int nm, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X
 
 using namespace swh;
 
-extern "C" int swh_attn_decode_shared_frag(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
-                                           const float *rope_sin, const int32_t *prompt_len,
-                                           const int32_t *prompt_row, const int32_t *state, int64_t B, int32_t Hq,
-                                           int32_t Hkv, int32_t D, int32_t Tmax, float scale, void *out,
-                                           const void *pf_w, int64_t pf_n, int64_t pf_k, int32_t out_frag,
-                                           void *stream) {
+static int attn_decode_impl(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
+                            const float *rope_sin, const int32_t *prompt_len, const int32_t *prompt_row,
+                            const int32_t *state, int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax,
+                            float scale, void *out, int32_t out_frag, AttnPrefetch pf, void *stream) {
     if (!qkv || !k_cache || !v_cache || !rope_cos || !rope_sin || !prompt_len || !state || !out || B < 0 || Hkv <= 0 ||
         Hq % Hkv || Tmax <= 0 || B > 65535 || (out_frag & ~1))
         return SWH_E_ARG;
     if (out_frag && (B % 16 || (Hq * D) % 32 || (reinterpret_cast<uintptr_t>(out) & 15))) return SWH_E_ARG;
-    if (pf_w && (pf_n <= 0 || pf_n % 8 || pf_k <= 0 || pf_k % 8 || pf_n >= (1 << 28) || pf_k >= (1 << 20) ||
-                 (reinterpret_cast<uintptr_t>(pf_w) & 15)))
-        return SWH_E_ARG;
     if (B == 0) return SWH_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const auto *q = static_cast<const uint16_t *>(qkv);
     auto *kc = static_cast<uint16_t *>(k_cache), *vc = static_cast<uint16_t *>(v_cache);
     auto *o = static_cast<uint16_t *>(out);
     const int gq = Hq / Hkv;
-    AttnPrefetch pf{static_cast<const uint16_t *>(pf_w), (int)pf_n, (int)pf_k, (int)B, prompt_row, out_frag};
-    pf.xrows = attn_xcd_rows();
+    pf.rows = (int)B;
+    pf.prow = prompt_row;
+    pf.ofrag = out_frag;
     if (D == 64) return attn_dispatch_gq<64>(gq, q, kc, vc, rope_cos, rope_sin, prompt_len, state, B, Hq, Hkv, Tmax, scale, o, s, pf);
     if (D == 128) return attn_dispatch_gq<128>(gq, q, kc, vc, rope_cos, rope_sin, prompt_len, state, B, Hq, Hkv, Tmax, scale, o, s, pf);
     return SWH_E_ARG;
+}
+
+extern "C" int swh_attn_decode_shared_frag(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
+                                           const float *rope_sin, const int32_t *prompt_len,
+                                           const int32_t *prompt_row, const int32_t *state, int64_t B, int32_t Hq,
+                                           int32_t Hkv, int32_t D, int32_t Tmax, float scale, void *out,
+                                           int32_t out_frag, void *stream) {
+    return attn_decode_impl(qkv, k_cache, v_cache, rope_cos, rope_sin, prompt_len, prompt_row, state, B, Hq, Hkv, D,
+                            Tmax, scale, out, out_frag, AttnPrefetch{}, stream);
 }
 // swh_attn_decode_shared_frag whose launch also carries Infinity Cache warm-up
 // workgroups (on the CUs the attention leaves idle) over l3_jobs
@@ -1951,54 +1878,32 @@ extern "C" int swh_attn_decode_l3(const void *qkv, void *k_cache, void *v_cache,
                                   const int32_t *state, int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax,
                                   float scale, void *out, int32_t out_frag, const void *l3_jobs, int32_t l3_njobs,
                                   int32_t l3_wgs, void *l3_sink, void *stream) {
-    if (!qkv || !k_cache || !v_cache || !rope_cos || !rope_sin || !prompt_len || !state || !out || B < 0 || Hkv <= 0 ||
-        Hq % Hkv || Tmax <= 0 || B > 65535 || (out_frag & ~1))
+    if (!l3_jobs || !l3_sink || l3_njobs <= 0 || l3_njobs > kL3MaxJobs || l3_wgs <= 0 || l3_wgs > 4096 || Hkv <= 0)
         return SWH_E_ARG;
-    if (out_frag && (B % 16 || (Hq * D) % 32 || (reinterpret_cast<uintptr_t>(out) & 15))) return SWH_E_ARG;
-    if (!l3_jobs || !l3_sink || l3_njobs <= 0 || l3_njobs > kL3MaxJobs || l3_wgs <= 0 || l3_wgs > 4096)
-        return SWH_E_ARG;
-    if (B == 0) return SWH_OK;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    const auto *q = static_cast<const uint16_t *>(qkv);
-    auto *kc = static_cast<uint16_t *>(k_cache), *vc = static_cast<uint16_t *>(v_cache);
-    auto *o = static_cast<uint16_t *>(out);
-    const int gq = Hq / Hkv;
-    // the sink holds one word per thread of every warm-up workgroup (whole grid rows)
-    const int wgs = (l3_wgs + Hkv - 1) / Hkv * Hkv;
-    AttnPrefetch pf{nullptr, 0, 0, (int)B, prompt_row, out_frag};
-    pf.xrows = attn_xcd_rows();
+    AttnPrefetch pf{};
     pf.jobs = static_cast<const L3Job *>(l3_jobs);
     pf.njobs = l3_njobs;
     pf.sink = static_cast<uint32_t *>(l3_sink);
-    pf.nwg = wgs;
-    if (D == 64) return attn_dispatch_gq<64>(gq, q, kc, vc, rope_cos, rope_sin, prompt_len, state, B, Hq, Hkv, Tmax, scale, o, s, pf);
-    if (D == 128) return attn_dispatch_gq<128>(gq, q, kc, vc, rope_cos, rope_sin, prompt_len, state, B, Hq, Hkv, Tmax, scale, o, s, pf);
-    return SWH_E_ARG;
+    // the sink holds one word per thread of every warm-up workgroup (whole grid rows)
+    pf.nwg = (l3_wgs + Hkv - 1) / Hkv * Hkv;
+    return attn_decode_impl(qkv, k_cache, v_cache, rope_cos, rope_sin, prompt_len, prompt_row, state, B, Hq, Hkv, D,
+                            Tmax, scale, out, out_frag, pf, stream);
 }
 
 extern "C" int swh_attn_decode_shared(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
                                       const float *rope_sin, const int32_t *prompt_len, const int32_t *prompt_row,
                                       const int32_t *state, int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax,
-                                      float scale, void *out, const void *pf_w, int64_t pf_n, int64_t pf_k,
-                                      void *stream) {
+                                      float scale, void *out, void *stream) {
     return swh_attn_decode_shared_frag(qkv, k_cache, v_cache, rope_cos, rope_sin, prompt_len, prompt_row, state, B, Hq,
-                                       Hkv, D, Tmax, scale, out, pf_w, pf_n, pf_k, 0, stream);
-}
-
-extern "C" int swh_attn_decode_prefetch(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
-                                        const float *rope_sin, const int32_t *prompt_len, const int32_t *state,
-                                        int64_t B, int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax, float scale,
-                                        void *out, const void *pf_w, int64_t pf_n, int64_t pf_k, void *stream) {
-    return swh_attn_decode_shared(qkv, k_cache, v_cache, rope_cos, rope_sin, prompt_len, nullptr, state, B, Hq, Hkv,
-                                  D, Tmax, scale, out, pf_w, pf_n, pf_k, stream);
+                                       Hkv, D, Tmax, scale, out, 0, stream);
 }
 
 extern "C" int swh_attn_decode(const void *qkv, void *k_cache, void *v_cache, const float *rope_cos,
                                const float *rope_sin, const int32_t *prompt_len, const int32_t *state, int64_t B,
                                int32_t Hq, int32_t Hkv, int32_t D, int32_t Tmax, float scale, void *out,
                                void *stream) {
-    return swh_attn_decode_prefetch(qkv, k_cache, v_cache, rope_cos, rope_sin, prompt_len, state, B, Hq, Hkv, D, Tmax,
-                                    scale, out, nullptr, 0, 0, stream);
+    return swh_attn_decode_shared(qkv, k_cache, v_cache, rope_cos, rope_sin, prompt_len, nullptr, state, B, Hq, Hkv, D,
+                                  Tmax, scale, out, stream);
 }
 
 extern "C" int64_t swh_decode_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K) {
@@ -2018,14 +1923,8 @@ extern "C" int64_t swh_decode_gemm_workspace_bytes(int64_t M, int64_t N, int64_t
 static int decode_gemm_impl(const void *x, const void *w, int64_t M, int64_t N, int64_t K, const void *norm_w,
                             float eps, const void *bias, void *residual, int32_t silu, void *y, int64_t ldy,
                             const float *ss_in, float *ss_out, void *workspace, int64_t workspace_bytes, void *stream,
-                            int fw, int act = 0, const L3Warm *warm = nullptr) {
+                            int fw, int act = 0) {
     if (fw && (norm_w || K % 128)) return SWH_E_ARG;
-    // act bit 2: W in the k-major fragment order (swh_frag_pack_kmajor; tile path only)
-    if (act & 4) {
-        if (!fw) return SWH_E_ARG;
-        fw = 2;
-        act &= 3;
-    }
     // act bit 0: the SiLU output in fragment order (tile path only); bit 1: X in fragment order (xstream only)
     if (act & ~3 || ((act & 1) && (!silu || N % 32 || M % 16)) || ((act & 2) && (!residual || M % 16 || K % 32)))
         return SWH_E_ARG;
@@ -2075,7 +1974,6 @@ static int decode_gemm_impl(const void *x, const void *w, int64_t M, int64_t N, 
         }
     }
     if (act & 1) return SWH_E_ARG;  // the fragment-order SiLU output comes from the tile kernel only
-    if (fw == 2) return SWH_E_ARG;  // k-major weights: the tile kernel only
     GemmCfg c = pick_cfg(M, wcols, K, silu != 0, nm);
     c.fw = fw;
     c.xf = (act & 2) ? 1 : 0;
@@ -2111,7 +2009,7 @@ static int decode_gemm_impl(const void *x, const void *w, int64_t M, int64_t N, 
     }
     if (residual) {
         if (nm == 0) {
-            const int rc = launch_xstream(c, s, X, W, m, n, k, nm, eps, ss_in, Bs, R, ss_out, nullptr, ld, warm);
+            const int rc = launch_xstream(c, s, X, W, m, n, k, nm, eps, ss_in, Bs, R, ss_out, nullptr, ld);
             if (rc != 1) return rc;
         }
         if (c.xf) return SWH_E_ARG;  // a fragment-order X is read by xstream only
@@ -2121,7 +2019,7 @@ static int decode_gemm_impl(const void *x, const void *w, int64_t M, int64_t N, 
     if (Bs) {
         if (nm == 1) SWH_GEMM(1, EPI_PLAIN, true);
         if (nm == 2) {
-            const int rc = launch_xstream(c, s, X, W, m, n, k, nm, eps, ss_in, Bs, nullptr, nullptr, Y, ld, warm);
+            const int rc = launch_xstream(c, s, X, W, m, n, k, nm, eps, ss_in, Bs, nullptr, nullptr, Y, ld);
             if (rc != 1) return rc;
             SWH_GEMM(2, EPI_PLAIN, true);
         }
@@ -2149,24 +2047,6 @@ extern "C" int swh_decode_gemm_fragw(const void *x, const void *w, int64_t M, in
                             workspace_bytes, stream, 1, act_frag);
 }
 
-// swh_decode_gemm_fragw with l3_wgs Infinity Cache warm-up workgroups appended to
-// the register-streamed (xstream) launch; other geometries ignore them
-extern "C" int swh_decode_gemm_fragw_l3(const void *x, const void *w, int64_t M, int64_t N, int64_t K, float eps,
-                                        const void *bias, void *residual, int32_t silu, void *y, int64_t ldy,
-                                        const float *ss_in, float *ss_out, int32_t act_frag, const void *l3_jobs,
-                                        int32_t l3_njobs, int32_t l3_wgs, void *l3_sink, void *workspace,
-                                        int64_t workspace_bytes, void *stream) {
-    if (!l3_jobs || !l3_sink || l3_njobs <= 0 || l3_njobs > kL3MaxJobs || l3_wgs <= 0 || l3_wgs > 4096)
-        return SWH_E_ARG;
-    L3Warm wm;
-    wm.jobs = static_cast<const L3Job *>(l3_jobs);
-    wm.njobs = l3_njobs;
-    wm.gx0 = l3_wgs;  // the warm-up block count (launch_xstream_kw turns it into the tile count)
-    wm.sink = static_cast<uint32_t *>(l3_sink);
-    return decode_gemm_impl(x, w, M, N, K, nullptr, eps, bias, residual, silu, y, ldy, ss_in, ss_out, workspace,
-                            workspace_bytes, stream, 1, act_frag, &wm);
-}
-
 extern "C" int swh_frag_pack(const void *w, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst,
                              void *stream) {
     const int64_t rows = silu ? 2 * N : N;
@@ -2174,15 +2054,6 @@ extern "C" int swh_frag_pack(const void *w, const void *norm_w, int64_t N, int64
     if ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(norm_w)) & 15)
         return SWH_E_ARG;
     return frag_pack(w, norm_w, N, K, silu, dst, static_cast<hipStream_t>(stream));
-}
-
-extern "C" int swh_frag_pack_kmajor(const void *w, const void *norm_w, int64_t N, int64_t K, int32_t silu,
-                                    void *dst, int32_t kmajor, void *stream) {
-    const int64_t rows = silu ? 2 * N : N;
-    if (!w || !dst || w == dst || N <= 0 || rows % 16 || (silu && N % 8) || K <= 0 || K % 128) return SWH_E_ARG;
-    if ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(norm_w)) & 15)
-        return SWH_E_ARG;
-    return (kmajor & ~1) ? SWH_E_ARG : frag_pack(w, norm_w, N, K, silu, dst, static_cast<hipStream_t>(stream), kmajor);
 }
 
 // [partials (M x per x 8 LmPart) | 256 B: the finalize ticket (zero at allocation)]
@@ -2320,78 +2191,4 @@ extern "C" int swh_lm_head_sample_step_fragw(const void *x, const void *w, int64
                                              int64_t workspace_bytes, void *stream) {
     return lm_head_sample_step_impl(x, w, M, V, K, nullptr, eps, ss_in, params, rng, step, finished, out_tokens,
                                     out_ld, cur_tokens, embed, x_next, ss_next, workspace, workspace_bytes, stream, 1);
-}
-
-// the two entries above over the k-major fragment order (swh_frag_pack_kmajor(..., 1, ...)): same draws
-extern "C" int swh_lm_head_sample_fragk(const void *x, const void *w, int64_t M, int64_t V, int64_t K, float eps,
-                                        const float *ss_in, const swh_sample_params *params, const uint64_t *rng,
-                                        const int32_t *step, int32_t *finished, int64_t *out_tokens, int64_t out_ld,
-                                        int64_t *cur_tokens, void *workspace, int64_t workspace_bytes, void *stream) {
-    return lm_head_sample_impl(x, w, M, V, K, nullptr, eps, ss_in, params, rng, step, finished, out_tokens, out_ld,
-                               cur_tokens, workspace, workspace_bytes, LmNext{}, stream, 2);
-}
-
-extern "C" int swh_lm_head_sample_step_fragk(const void *x, const void *w, int64_t M, int64_t V, int64_t K,
-                                             float eps, const float *ss_in, const swh_sample_params *params,
-                                             const uint64_t *rng, int32_t *step, int32_t *finished,
-                                             int64_t *out_tokens, int64_t out_ld, int64_t *cur_tokens,
-                                             const void *embed, void *x_next, float *ss_next, void *workspace,
-                                             int64_t workspace_bytes, void *stream) {
-    return lm_head_sample_step_impl(x, w, M, V, K, nullptr, eps, ss_in, params, rng, step, finished, out_tokens,
-                                    out_ld, cur_tokens, embed, x_next, ss_next, workspace, workspace_bytes, stream, 2);
-}
-
-namespace swh {
-namespace {
-
-// ---------------------------------------------------------------------------
-// Infinity Cache warm-up of the next decode layer's weights.  The decode step
-// streams ~1 GB of weights per token (0.5B: 24 x 29.8 MB + the 272 MB lm head),
-// more than the 256 MiB Infinity Cache holds, so every projection's weight
-// loads miss to HBM (~900 cycles against ~545 for an Infinity Cache hit,
-// MI355X_MICROARCH.md constants).  The decode chain keeps HBM ~85 % idle; a
-// few workgroups on a side branch of the decode graph read layer l+1's
-// weights while layer l runs, so the latency-bound projections find them
-// on-die.  Read-only: results are unchanged by construction.  The loads feed
-// an XOR whose value is stored only if it equals `magic` (never, in practice:
-// it keeps the loads alive without a data-dependent store stream).
-
-template <bool NT>
-__global__ __launch_bounds__(256) void l3_prefetch_kernel(const L3Job *__restrict__ jobs, int njobs, uint32_t magic,
-                                                          uint32_t *__restrict__ sink) {
-    uint32_t acc = 0;
-    const int64_t stride = (int64_t)gridDim.x * 256 * 4;
-    for (int j = 0; j < njobs; ++j) {
-        const uint4 *p = jobs[j].p;
-        const int64_t n = jobs[j].n16;
-        for (int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x; i < n; i += stride) {
-            uint4 v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int64_t e = i + u * 256;
-                if (e < n) v[u] = NT ? ld_nt(p + e) : p[e];
-                else v[u] = uint4{0u, 0u, 0u, 0u};
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
-        }
-    }
-    if (acc == magic) sink[blockIdx.x * 256 + threadIdx.x] = acc;
-}
-
-}  // namespace
-}  // namespace swh
-
-extern "C" int swh_l3_prefetch(const void *jobs, int32_t njobs, int32_t nwg, int32_t nontemporal, void *sink,
-                               void *stream) {
-    if (!jobs || !sink || njobs <= 0 || nwg <= 0 || nwg > 4096) return SWH_E_ARG;
-    const auto *j = static_cast<const swh::L3Job *>(jobs);
-    auto *sk = static_cast<uint32_t *>(sink);
-    if (nontemporal)
-        swh::l3_prefetch_kernel<true><<<dim3((unsigned)nwg), 256, 0, static_cast<hipStream_t>(stream)>>>(
-            j, njobs, 0x9e3779b9u, sk);
-    else
-        swh::l3_prefetch_kernel<false><<<dim3((unsigned)nwg), 256, 0, static_cast<hipStream_t>(stream)>>>(
-            j, njobs, 0x9e3779b9u, sk);
-    return launch_status();
 }

@@ -472,14 +472,10 @@ namespace {
 // rows), q = 128-k round, s = k-step, (kg, rl) = the MFMA B-fragment lane.  W' = W, or the
 // folded RMSNorm weight bf16(W * w_norm) (swh_fold_norm's product) when norm_w is given.
 // One 16-B piece per thread, grid-stride; the stores are contiguous.
-// kmajor: the same 1 KB fragments with k-step outermost, piece (ks * G + g) * 64 + lane
-// (G = 16-row groups): the tile kernel's concurrently loading waves then read one
-// contiguous run per k-step instead of runs 16 K bytes apart
 __global__ __launch_bounds__(256) void wide_pack_kernel(const uint16_t *__restrict__ src,
                                                         const uint16_t *__restrict__ nw, int64_t N, int64_t K,
-                                                        int silu, uint16_t *__restrict__ dst, int64_t npieces,
-                                                        int kmajor = 0) {
-    const int64_t nr = K / kWKC, ngroups = (silu ? 2 * N : N) / 16;
+                                                        int silu, uint16_t *__restrict__ dst, int64_t npieces) {
+    const int64_t nr = K / kWKC;
     for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npieces; p += (int64_t)gridDim.x * blockDim.x) {
         const int rl = (int)(p & 15), kg = (int)((p >> 4) & 3), s = (int)((p >> 6) & 3);
         const int64_t rest = p >> 8, q = rest % nr, g = rest / nr;
@@ -498,22 +494,19 @@ __global__ __launch_bounds__(256) void wide_pack_kernel(const uint16_t *__restri
                        ((uint32_t)f32_to_bf16_bits(a[2 * c + 1] * b[2 * c + 1]) << 16);
             v = uint4{o[0], o[1], o[2], o[3]};
         }
-        const int64_t pd = kmajor ? ((q * 4 + s) * ngroups + g) * 64 + (p & 63) : p;
-        *reinterpret_cast<uint4 *>(dst + pd * 8) = v;
+        *reinterpret_cast<uint4 *>(dst + p * 8) = v;
     }
 }
 
 }  // namespace
 
-// the same fragment order for any 16-row group count (decode_gemm / xstream with fw);
-// kmajor: k-step outermost (the tile kernel's fw = 2)
-int frag_pack(const void *src, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, hipStream_t st,
-              int32_t kmajor) {
+// the same fragment order for any 16-row group count (decode_gemm / xstream with fw)
+int frag_pack(const void *src, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, hipStream_t st) {
     const int64_t npieces = (silu ? 2 * N : N) * K / 8;
     const int64_t grid = (npieces + 255) / 256 < 8192 ? (npieces + 255) / 256 : 8192;
     wide_pack_kernel<<<dim3((unsigned)grid), 256, 0, st>>>(static_cast<const uint16_t *>(src),
                                                              static_cast<const uint16_t *>(norm_w), N, K, silu,
-                                                             static_cast<uint16_t *>(dst), npieces, kmajor);
+                                                             static_cast<uint16_t *>(dst), npieces);
     return launch_status();
 }
 

@@ -185,13 +185,6 @@ class DecodeEngine:
         # streamed A operand as contiguous 1 KB runs); SWH_ATT_FRAG=0 keeps it row-major
         self.att_frag = (os.environ.get("SWH_ATT_FRAG", "1") != "0" and B % 16 == 0 and c.q_dim % 32 == 0 and
                          all(f"l{i}.o_w" in self.fragw for i in range(c.num_hidden_layers)))
-        # the lm head's fragment-order copy with the k-step outermost (swh_frag_pack_kmajor):
-        # the sampler's waves loading k-step ks of consecutive tiles read one contiguous run
-        # (SWH_LM_KMAJOR=1; the logits path below keeps the tile-major copy)
-        self.lm_kmajor = os.environ.get("SWH_LM_KMAJOR", "0") != "0"
-        # the same for the gate/up copies (SWH_GU_KMAJOR=1): the tile kernel's waves load
-        # k-step ks of consecutive tiles together
-        self.gu_kmajor = os.environ.get("SWH_GU_KMAJOR", "0") != "0"
         self.graph = None
         self.graph_k = None
         self._prefill_graphs = {}
@@ -199,30 +192,14 @@ class DecodeEngine:
         self._graph_params = None
         self.params = ops.make_sample_params()
         self.want_logp = False
-        # the attention launch warms the gate/up weights into the consuming XCDs' L2:
-        # gate/up gains what the longer attention launch loses, off
-        self.prefetch = os.environ.get("SWH_DECODE_PREFETCH", "0") != "0"
-        # Infinity Cache warm-up (swh_l3_prefetch): a side branch of the decode graph
-        # reads layer l+1's decode weights while layer l runs (the step's ~1 GB weight
-        # stream misses the 256 MiB cache otherwise); SWH_DECODE_L3_PREFETCH = workgroups
-        # (0: off), SWH_DECODE_L3_AT = the op of layer l it starts beside (0 qkv, 1 attention,
-        # 2 gate/up), SWH_DECODE_L3_NT=1 nt loads
-        self.l3_nwg = int(os.environ.get("SWH_DECODE_L3_PREFETCH", "0")) if self.fused else 0
-        self.l3_at = int(os.environ.get("SWH_DECODE_L3_AT", "0"))
-        self.l3_nt = int(os.environ.get("SWH_DECODE_L3_NT", "0"))
-        self._l3_jobs = None
-        # the same warm-up carried by the attention launch itself (swh_attn_decode_l3): its
+        # Infinity Cache warm-up carried by the attention launch (swh_attn_decode_l3): its
         # B x Hkv workgroups leave CUs idle, extra workgroups on them read the weights of
         # the projections that follow (SWH_DECODE_L3_ATTN = workgroups, 0: off;
-        # SWH_DECODE_L3_SET: comma list of o, down, gu (this layer), qkv1, o1 (next layer))
+        # SWH_DECODE_L3_SET: comma list of o, down, gu, qkv (this layer), qkv1, o1, gu1,
+        # down1 (next layer))
         self.l3_set = os.environ.get("SWH_DECODE_L3_SET", "o,down,qkv1")
         self.l3_attn = int(os.environ.get("SWH_DECODE_L3_ATTN", str(self._l3_attn_default()))) if self.fused else 0
         self._l3a_jobs = None
-        # and by the qkv launch (register-streamed: its tiles leave CUs idle too);
-        # SWH_DECODE_L3_QKV = workgroups, SWH_DECODE_L3_QKV_SET as SWH_DECODE_L3_SET
-        self.l3_qkv = int(os.environ.get("SWH_DECODE_L3_QKV", "0")) if self.fused else 0
-        self.l3_qkv_set = os.environ.get("SWH_DECODE_L3_QKV_SET", "gu")
-        self._l3q_jobs = None
         self._exit_poll = EarlyExitPoll(self.finished)
         self.steps_run = 0  # decode steps the last generate() ran (early exit: fewer than max_new_tokens - 1)
 
@@ -291,8 +268,7 @@ class DecodeEngine:
         projs = self._projections()
         for name, buf in self.fragw.items():
             N, K, silu, norm = projs[name]
-            nn_ops.frag_pack(self._weight(name), self.model.p[norm] if norm else None, silu=silu, out=buf,
-                             kmajor=self._kmajor(name))
+            nn_ops.frag_pack(self._weight(name), self.model.p[norm] if norm else None, silu=silu, out=buf)
         if not self.fold:
             return
         if not getattr(self, "_fold_built", False):
@@ -314,7 +290,7 @@ class DecodeEngine:
     def _lm_head_weight(self):
         """(weight, norm_w, fragment order?) the fused lm-head sampler reads."""
         if "lm" in self.fragw:
-            return self.fragw["lm"], None, 2 if self.lm_kmajor else 1
+            return self.fragw["lm"], None, 1
         return (*self._normed("lm", "norm"), False)
 
     def _proj(self, name: str, x: torch.Tensor, **kw):
@@ -328,8 +304,6 @@ class DecodeEngine:
                 kw["act_frag"] = 1 if name.endswith("gu_w") else 2
             elif "act_frag" in kw and not name.endswith("o_w"):
                 raise ValueError(f"{name}: act_frag serves gate/up, down and o only")
-            if self._kmajor(name):
-                kw["act_frag"] = kw.get("act_frag", 0) | 4  # the k-major copy (tile kernel)
             return nn_ops.decode_gemm_fragw(x, self.fragw[name], eps=eps, **kw)
         norm = self._projections()[name][3]
         if norm is None:
@@ -348,19 +322,6 @@ class DecodeEngine:
         per_layer = 2 * c.hidden_size * (c.q_dim + c.intermediate_size + c.qkv_dim)
         return 96 if self.B * c.num_key_value_heads + 96 <= cus and per_layer <= (64 << 20) else 0
 
-    def _kmajor(self, name: str) -> bool:
-        """Is `name`'s fragment-order copy k-major (swh_frag_pack_kmajor)?  Only
-        shapes decode_gemm runs on its tile kernel (K <= 1024 and >= 8 tiles per
-        CU for the lm head's logits path, >= 1 SiLU tile per CU for gate/up;
-        csrc/decode.hip decode_gemm_impl) take it."""
-        c = self.cfg
-        cus = torch.cuda.get_device_properties(self.dev).multi_processor_count
-        if c.hidden_size > 1024:
-            return False
-        if name == "lm":
-            return self.lm_kmajor and c.vocab_size // 16 >= 8 * cus
-        return name.endswith("gu_w") and self.gu_kmajor and c.intermediate_size // 8 >= cus
-
     def _proj_weight(self, name: str) -> torch.Tensor:
         """The buffer _proj streams for a projection."""
         if name in self.packed:
@@ -370,59 +331,29 @@ class DecodeEngine:
         norm = self._projections()[name][3]
         return self._weight(name) if norm is None else self._normed(name, norm)[0]
 
-    def _l3_tables(self):
-        """Per layer, a device table of {ptr, bytes/16} over its decode weights."""
-        if self._l3_jobs is None:
-            tabs = []
-            for i in range(self.cfg.num_hidden_layers):
-                t = []
-                for n in ("qkv_w", "o_w", "gu_w", "down_w"):
-                    w = self._proj_weight(f"l{i}.{n}")
-                    t += [w.data_ptr(), w.numel() * w.element_size() // 16, 0]
-                tabs.append(torch.tensor(t, dtype=torch.int64).to(self.dev))
-            self._l3_jobs = tabs
-            self._l3_sink = torch.zeros(self.l3_nwg * 256, dtype=torch.int32, device=self.dev)
-            self._l3_side = torch.cuda.Stream()
-        return self._l3_jobs
-
     def _l3_job_tables(self, spec: str):
-        """Per layer, a device table {ptr, bytes / 16} of the weights `spec` names
+        """Per layer, a device table {ptr, bytes / 16, 0} of the weights `spec` names
         (comma list of o, down, gu, qkv: this layer; o1, down1, gu1, qkv1: the next)."""
         L = self.cfg.num_hidden_layers
         names = {"o": (0, "o_w"), "down": (0, "down_w"), "gu": (0, "gu_w"), "qkv": (0, "qkv_w"),
                  "qkv1": (1, "qkv_w"), "o1": (1, "o_w"), "gu1": (1, "gu_w"), "down1": (1, "down_w")}
-        # "name@x": striped by 16-row column block (fragment-order weights), block c warmed
-        # on the XCD the consuming launch runs it on (c % 8)
         keys = [k.strip() for k in spec.split(",") if k.strip()]
-        bad = [k for k in keys if k.split("@")[0] not in names or k.count("@") > 1 or ("@" in k and k[-2:] != "@x")]
+        bad = [k for k in keys if k not in names]
         if bad:
-            raise ValueError(f"warm-up set {spec!r}: unknown entries {bad} (expected {sorted(names)}, optional @x)")
-        sel = [(*names[k.split("@")[0]], k.endswith("@x")) for k in keys]
+            raise ValueError(f"warm-up set {spec!r}: unknown entries {bad} (expected {sorted(names)})")
         tabs = []
         for i in range(L):
             t = []
-            for d, n, xs in sel:
+            for d, n in (names[k] for k in keys):
                 if i + d < L:
-                    nm = f"l{i + d}.{n}"
-                    w = self._proj_weight(nm)
-                    stripe = 2 * w.shape[-1] if xs and nm in self.fragw and w.dim() == 2 else 0
-                    t += [w.data_ptr(), w.numel() * w.element_size() // 16, stripe]
+                    w = self._proj_weight(f"l{i + d}.{n}")
+                    t += [w.data_ptr(), w.numel() * w.element_size() // 16, 0]
             tabs.append(torch.tensor(t, dtype=torch.int64).to(self.dev) if t else None)
         return tabs
 
     def _qkv(self, i: int):
         p = self.model.p
-        name = f"l{i}.qkv_w"
-        if self.l3_qkv > 0 and name in self.fragw:
-            if self._l3q_jobs is None:
-                self._l3q_jobs = self._l3_job_tables(self.l3_qkv_set)
-                self._l3q_sink = torch.zeros(self.l3_qkv * 512, dtype=torch.int32, device=self.dev)
-            jobs = self._l3q_jobs[i]
-            if jobs is not None:
-                return nn_ops.decode_gemm_fragw(self.s, self.fragw[name], eps=self.cfg.rms_norm_eps,
-                                                bias=p.get(f"l{i}.qkv_b"), y=self.qkv, ss_in=self.ss,
-                                                l3=(jobs, self.l3_qkv, self._l3q_sink))
-        return self._proj(name, self.s, bias=p.get(f"l{i}.qkv_b"), y=self.qkv, ss_in=self.ss)
+        return self._proj(f"l{i}.qkv_w", self.s, bias=p.get(f"l{i}.qkv_b"), y=self.qkv, ss_in=self.ss)
 
     def _l3a_tables(self):
         """Per layer, the device job table of swh_attn_decode_l3 (SWH_DECODE_L3_SET)."""
@@ -440,19 +371,9 @@ class DecodeEngine:
                                          self.state, c.num_attention_heads, c.num_key_value_heads, c.head_dim,
                                          c.head_dim ** -0.5, self.att, self.prow, self.att_frag, jobs, self.l3_attn,
                                          self._l3a_sink)
-        pf = self._normed(f"l{i}.gu_w", f"l{i}.ln_post")[0] if self.prefetch and f"l{i}.gu_w" not in \
-            self.packed and f"l{i}.gu_w" not in self.fragw else None
         return nn_ops.attn_decode(self.qkv, self.kv[i, 0], self.kv[i, 1], self.cos, self.sin, self.plen, self.state,
                                   c.num_attention_heads, c.num_key_value_heads, c.head_dim, c.head_dim ** -0.5,
-                                  out=self.att, prefetch_gate_up=pf, prompt_row=self.prow, out_frag=self.att_frag)
-
-    def _l3_prefetch(self, layer: int):
-        """Fork the warm-up of `layer`'s weights onto the side stream."""
-        jobs = self._l3_tables()
-        self._l3_side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self._l3_side):
-            call("swh_l3_prefetch", jobs[layer].data_ptr(), jobs[layer].numel() // 3, self.l3_nwg, self.l3_nt, self._l3_sink.data_ptr(),
-                 ops._stream())
+                                  out=self.att, prompt_row=self.prow, out_frag=self.att_frag)
 
     def _step_fused(self):
         c, m = self.cfg, self.model
@@ -460,26 +381,17 @@ class DecodeEngine:
         eps = c.rms_norm_eps
         ss = self.ss  # every producer of s writes its RMSNorm partial sums, every normed GEMM reads them
         L = c.num_hidden_layers
-        l3 = self.l3_nwg > 0
         if not self._chained():
             nn_ops.embed_gather(p["embed"], self.cur, self.s, ss_out=ss)
         for i in range(L):
-            if l3 and self.l3_at == 0 and i + 1 < L:
-                self._l3_prefetch(i + 1)
             self._qkv(i)
-            if l3 and self.l3_at == 1 and i + 1 < L:
-                self._l3_prefetch(i + 1)
             self._attn(i)
             if self.att_frag:
                 self._proj(f"l{i}.o_w", self.att, residual=self.s, ss_out=ss, act_frag=2)
             else:
                 self._proj(f"l{i}.o_w", self.att, residual=self.s, ss_out=ss)
-            if l3 and self.l3_at == 2 and i + 1 < L:
-                self._l3_prefetch(i + 1)
             self._proj(f"l{i}.gu_w", self.s, silu=True, y=self.act, ss_in=ss)
             self._proj(f"l{i}.down_w", self.act, residual=self.s, ss_out=ss)
-        if l3:
-            torch.cuda.current_stream().wait_stream(self._l3_side)
         if self._fused_sample():
             w, nw, fr = self._lm_head_weight()
             nn_ops.lm_head_sample_step(self.s, w, self.params, self.rng, self.state[0:1], self.finished,
@@ -526,14 +438,15 @@ class DecodeEngine:
         if self.graph is not None and self._graph_params == key:
             return
         # warm-up outside capture (hipBLASLt heuristics / workspaces), then capture.
-        # The warm-up writes the cache at slot P + step - 1, so it runs on a
-        # scratch copy of the mutable state and restores it afterwards.
+        # The warm-up runs on a scratch copy of the step state, restored afterwards.
+        # It also appends one K/V slot to the cache; that is not restored: every
+        # cache slot a generation reads, the same generation writes first (the
+        # prefill writes slots [0, P), decode step s appends slot P + s - 1 before
+        # attending over it), so the slot's old content is never read.
         saved = [t.clone() for t in (self.state, self.finished, self.cur, self.out, self.out_logp, self.seen)]
-        kv_saved = None
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
-            kv_saved = self.kv.clone()
             # a step index inside the buffers: after a finished generation the step
             # counter sits at max_new_tokens, one column past out / out_logp (whose
             # last row would then write past the allocation into its neighbour)
@@ -553,8 +466,6 @@ class DecodeEngine:
         self._graph_params = key
         for t, v in zip((self.state, self.finished, self.cur, self.out, self.out_logp, self.seen), saved):
             t.copy_(v)
-        self.kv.copy_(kv_saved)
-        del kv_saved
 
     # ------------------------------------------------------------------ live kernel timing
     @torch.no_grad()

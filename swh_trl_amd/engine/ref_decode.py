@@ -124,8 +124,9 @@ class RefDecodeEngine:
         key = self._params_key()
         if self.graph is not None and self._graph_params == key:
             return
-        saved = [t.clone() for t in (self.state, self.finished, self.cur, self.out, self.out_logp, self.seen,
-                                     self.keyok, self.kv)]
+        # the step state is restored after the warm-up; the K/V slot and key flag it appends are
+        # not: generate() resets keyok and every slot a generation reads it writes first
+        saved = [t.clone() for t in (self.state, self.finished, self.cur, self.out, self.out_logp, self.seen)]
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):  # warm-up (library workspaces) outside capture, at an in-range step
@@ -136,8 +137,7 @@ class RefDecodeEngine:
         with _capture(self.graph):
             self._step()
         self._graph_params = key
-        for t, v in zip((self.state, self.finished, self.cur, self.out, self.out_logp, self.seen, self.keyok, self.kv),
-                        saved):
+        for t, v in zip((self.state, self.finished, self.cur, self.out, self.out_logp, self.seen), saved):
             t.copy_(v)
 
     @torch.no_grad()

@@ -108,12 +108,9 @@ def embed_gather(table: torch.Tensor, ids: torch.Tensor, out: torch.Tensor,
 def attn_decode(qkv: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, rope_cos: torch.Tensor,
                 rope_sin: torch.Tensor, prompt_len: torch.Tensor, state: torch.Tensor, Hq: int, Hkv: int, D: int,
                 scale: float, out: Optional[torch.Tensor] = None,
-                prefetch_gate_up: Optional[torch.Tensor] = None,
                 prompt_row: Optional[torch.Tensor] = None, out_frag: bool = False) -> torch.Tensor:
     """One decode step of GQA attention with in-kernel RoPE and KV append.
-    k_cache / v_cache: [B, Hkv, Tmax, D] bf16 (one layer).  prefetch_gate_up
-    [2 I, H] (optional): the layer's gate/up weights, read into the consuming
-    XCDs' L2 by extra workgroups of the same launch (swh_attn_decode_prefetch).
+    k_cache / v_cache: [B, Hkv, Tmax, D] bf16 (one layer).
     prompt_row int32 [B] (optional): row b reads its prompt keys / values from
     row prompt_row[b]'s cache (swh_attn_decode_shared).  out_frag: `out` in the
     fragment order decode_gemm_fragw(act_frag=2) reads (swh_attn_decode_shared_frag)."""
@@ -122,11 +119,9 @@ def attn_decode(qkv: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
     Tmax = k_cache.shape[2]
     if out is None:
         out = torch.empty(B, Hq * D, device=qkv.device, dtype=qkv.dtype)
-    pw = prefetch_gate_up
     call("swh_attn_decode_shared_frag", qkv.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), rope_cos.data_ptr(),
          rope_sin.data_ptr(), prompt_len.data_ptr(), _p(prompt_row), state.data_ptr(), B, Hq, Hkv, D, Tmax,
-         float(scale), out.data_ptr(), _p(pw), 0 if pw is None else pw.shape[0] // 2,
-         0 if pw is None else pw.shape[1], int(bool(out_frag)), _stream())
+         float(scale), out.data_ptr(), int(bool(out_frag)), _stream())
     return out
 
 
@@ -135,7 +130,7 @@ def attn_decode_l3(qkv: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
                    scale: float, out: torch.Tensor, prompt_row: Optional[torch.Tensor], out_frag: bool,
                    l3_jobs: torch.Tensor, l3_wgs: int, l3_sink: torch.Tensor) -> torch.Tensor:
     """attn_decode whose launch also carries Infinity Cache warm-up workgroups
-    over l3_jobs (int64 [n, 2] device table of {ptr, bytes / 16})
+    over l3_jobs (int64 [n, 3] device table of {ptr, bytes / 16, 0})
     (swh_attn_decode_l3): identical results."""
     _dev(qkv, "attn_decode_l3")
     B = qkv.shape[0]
@@ -182,18 +177,14 @@ def decode_gemm(x: torch.Tensor, w: torch.Tensor, *, norm_w: Optional[torch.Tens
 
 
 def frag_pack(w: torch.Tensor, norm_w: Optional[torch.Tensor] = None, *, silu: bool = False,
-              out: Optional[torch.Tensor] = None, kmajor: bool = False) -> torch.Tensor:
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """w [N, K] ([2N, K] gate|up with silu; K % 128 == 0), optionally folded
     with the RMSNorm weight, in the MFMA-fragment order decode_gemm_fragw reads
-    (swh_frag_pack); kmajor: k-step outermost (swh_frag_pack_kmajor, the lm-head
-    sampler's fragw=2 layout); same shape as w."""
+    (swh_frag_pack); same shape as w."""
     _dev(w, "frag_pack")
     rows, K = w.shape
     N = rows // 2 if silu else rows
     out = torch.empty_like(w) if out is None else out
-    if kmajor:
-        call("swh_frag_pack_kmajor", w.data_ptr(), _p(norm_w), N, K, int(bool(silu)), out.data_ptr(), 1, _stream())
-        return out
     call("swh_frag_pack", w.data_ptr(), _p(norm_w), N, K, int(bool(silu)), out.data_ptr(), _stream())
     return out
 
@@ -201,13 +192,10 @@ def frag_pack(w: torch.Tensor, norm_w: Optional[torch.Tensor] = None, *, silu: b
 def decode_gemm_fragw(x: torch.Tensor, w: torch.Tensor, *, eps: float = 1e-6, bias: Optional[torch.Tensor] = None,
                       residual: Optional[torch.Tensor] = None, silu: bool = False, y: Optional[torch.Tensor] = None,
                       workspace: Optional[torch.Tensor] = None, ss_in: Optional[torch.Tensor] = None,
-                      ss_out: Optional[torch.Tensor] = None, act_frag: int = 0,
-                      l3: Optional[tuple] = None) -> torch.Tensor:
+                      ss_out: Optional[torch.Tensor] = None, act_frag: int = 0) -> torch.Tensor:
     """decode_gemm (no norm_w) over w packed by frag_pack ([N, K], [2N, K] with
     silu) (include/swh_trl_amd.h swh_decode_gemm_fragw): bit-identical results.
-    act_frag bit 0: write the SiLU output in fragment order; bit 1: read x in it.
-    l3 = (jobs int64 [n, 3] {ptr, bytes / 16, stripe}, workgroups, sink): Infinity Cache
-    warm-up workgroups appended to a register-streamed launch (swh_decode_gemm_fragw_l3)."""
+    act_frag bit 0: write the SiLU output in fragment order; bit 1: read x in it."""
     _dev(x, "decode_gemm_fragw")
     M, K = x.shape
     N = w.shape[0] // 2 if silu else w.shape[0]
@@ -215,14 +203,6 @@ def decode_gemm_fragw(x: torch.Tensor, w: torch.Tensor, *, eps: float = 1e-6, bi
         y = torch.empty(M, N, device=x.device, dtype=x.dtype)
     ldy = residual.stride(0) if residual is not None else y.stride(0)
     ws = workspace if workspace is not None else gemm_workspace(x.device)
-    if l3 is not None:
-        jobs, nwg, sink = l3
-        if sink.numel() * sink.element_size() < nwg * 512 * 4:
-            raise ValueError("decode_gemm_fragw: l3 sink smaller than the warm-up workgroups x 512 words")
-        call("swh_decode_gemm_fragw_l3", x.data_ptr(), w.data_ptr(), M, N, K, float(eps), _p(bias), _p(residual),
-             int(bool(silu)), _p(y), ldy, _p(ss_in), _p(ss_out), int(act_frag), jobs.data_ptr(), jobs.numel() // 3,
-             int(nwg), sink.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
-        return residual if residual is not None else y
     call("swh_decode_gemm_fragw", x.data_ptr(), w.data_ptr(), M, N, K, float(eps), _p(bias), _p(residual),
          int(bool(silu)), _p(y), ldy, _p(ss_in), _p(ss_out), int(act_frag), ws.data_ptr(), ws.numel(), _stream())
     return residual if residual is not None else y
@@ -279,7 +259,7 @@ def lm_head_sample(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Tensor, 
                    workspace: Optional[torch.Tensor] = None, fragw: int = 0) -> torch.Tensor:
     """lm head + the unfiltered sampler in one pass, no logits tensor
     (include/swh_trl_amd.h swh_lm_head_sample; fragw 1: w packed by frag_pack,
-    swh_lm_head_sample_fragw; 2: by frag_pack(kmajor=True), swh_lm_head_sample_fragk).  Writes out_tokens[:, *step], cur_tokens,
+    swh_lm_head_sample_fragw).  Writes out_tokens[:, *step], cur_tokens,
     finished; returns out_tokens."""
     import ctypes
     _dev(x, "lm_head_sample")
@@ -291,8 +271,7 @@ def lm_head_sample(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Tensor, 
     head = (x.data_ptr(), w.data_ptr(), M, V, K) + (() if fragw else (_p(norm_w),)) + (float(eps), _p(ss_in))
     if fragw and norm_w is not None:
         raise ValueError("lm_head_sample: a fragment-order weight carries the folded norm (norm_w must be None)")
-    call(("swh_lm_head_sample_fragk" if fragw == 2 else "swh_lm_head_sample_fragw") if fragw else "swh_lm_head_sample",
-         *head,
+    call("swh_lm_head_sample_fragw" if fragw else "swh_lm_head_sample", *head,
          ctypes.byref(params), rng.data_ptr(), step.data_ptr(), finished.data_ptr(), out_tokens.data_ptr(),
          out_tokens.stride(0), _p(cur_tokens), workspace.data_ptr(), workspace.numel(), _stream())
     return out_tokens
@@ -316,8 +295,7 @@ def lm_head_sample_step(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Ten
     if fragw and norm_w is not None:
         raise ValueError("lm_head_sample_step: a fragment-order weight carries the folded norm (norm_w must be None)")
     head = (x.data_ptr(), w.data_ptr(), M, V, K) + (() if fragw else (_p(norm_w),)) + (float(eps), _p(ss_in))
-    call(("swh_lm_head_sample_step_fragk" if fragw == 2 else "swh_lm_head_sample_step_fragw") if fragw
-         else "swh_lm_head_sample_step", *head,
+    call("swh_lm_head_sample_step_fragw" if fragw else "swh_lm_head_sample_step", *head,
          ctypes.byref(params), rng.data_ptr(), step.data_ptr(), finished.data_ptr(), out_tokens.data_ptr(),
          out_tokens.stride(0), cur_tokens.data_ptr(), embed.data_ptr(), x_next.data_ptr(), _p(ss_next),
          workspace.data_ptr(), workspace.numel(), _stream())

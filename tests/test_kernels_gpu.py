@@ -789,7 +789,8 @@ def test_qkv_rope_matches_torch_rotate_half(ops, dev, B, L, Hq, Hkv, D, left_pad
 
 
 @pytest.mark.parametrize("D,Hq,Hkv,Tmax,step", [(64, 14, 2, 320, 270), (128, 32, 8, 320, 270),
-                                                (64, 14, 2, 1280, 1200), (128, 32, 8, 700, 600)])
+                                                (64, 14, 2, 1280, 1200), (128, 32, 8, 700, 600),
+                                                (128, 32, 8, 1300, 1250)])  # config 5: 1,291 keys at D 128
 def test_attn_decode(ops, dev, D, Hq, Hkv, Tmax, step):
     """One key round (<= 512 keys for D=64, 256 for D=128) and several."""
     from swh_trl_amd import nn_ops
@@ -839,27 +840,8 @@ def test_attn_decode(ops, dev, D, Hq, Hkv, Tmax, step):
     assert torch.isnan(out2.float()).all() and torch.equal(before, kcd)
 
 
-@pytest.mark.parametrize("B,Hkv,I", [(64, 2, 4864), (5, 8, 1024), (3, 1, 24)])
-def test_attn_decode_prefetch_is_result_neutral(ops, dev, B, Hkv, I):
-    """swh_attn_decode_prefetch (extra workgroup rows warming the gate/up weights)
-    writes exactly what swh_attn_decode writes, output and cache, at any grid shape."""
-    from swh_trl_amd import nn_ops
-    g = _gen(22)
-    D, Hq, Tmax, P, step = 64, 4 * Hkv, 96, 40, 17
-    plen = torch.randint(1, P + 1, (B,), generator=g).to(torch.int32).to(dev)
-    kc = torch.randn(B, Hkv, Tmax, D, generator=g).to(torch.bfloat16).to(dev)
-    vc = torch.randn(B, Hkv, Tmax, D, generator=g).to(torch.bfloat16).to(dev)
-    qkv = torch.randn(B, (Hq + 2 * Hkv) * D, generator=g).to(torch.bfloat16).to(dev)
-    gu = torch.randn(2 * I, 896, generator=g).to(torch.bfloat16).to(dev)
-    cos, sin = _rope_tables(D, 2048, 1e6, dev)
-    state = torch.tensor([step + 1, P], dtype=torch.int32, device=dev)
-    k1, v1, k2, v2 = kc.clone(), vc.clone(), kc.clone(), vc.clone()
-    a = nn_ops.attn_decode(qkv, k1, v1, cos, sin, plen, state, Hq, Hkv, D, D ** -0.5)
-    b = nn_ops.attn_decode(qkv, k2, v2, cos, sin, plen, state, Hq, Hkv, D, D ** -0.5, prefetch_gate_up=gu)
-    assert torch.equal(a, b) and torch.equal(k1, k2) and torch.equal(v1, v2)
-
-
-@pytest.mark.parametrize("D,Hkv,G,P,step", [(64, 2, 8, 128, 100), (128, 8, 8, 256, 300), (64, 2, 4, 41, 5)])
+@pytest.mark.parametrize("D,Hkv,G,P,step", [(64, 2, 8, 128, 100), (128, 8, 8, 256, 300), (64, 2, 4, 41, 5),
+                                             (128, 8, 8, 256, 1023)])  # config 5's last decode step: 1,280 keys
 def test_attn_decode_shared_prompt_rows(ops, dev, D, Hkv, G, P, step):
     """swh_attn_decode_shared: the rows of a group read their prompt keys /
     values from the group's first row (the other rows' prompt slots hold
@@ -1589,12 +1571,11 @@ def test_wide_gemm_tilings_agree(ops, dev, monkeypatch, name, N, K):
 
 
 @pytest.mark.parametrize("B,Hkv,G", [(64, 2, 8), (24, 2, 8), (12, 1, 4)])
-def test_attn_decode_xcd_rows_is_a_permutation(ops, dev, monkeypatch, B, Hkv, G):
-    """The XCD-contiguous order of the attention workgroups (SWH_ATTN_XCD_ROWS=1,
-    applied when Hkv x B % 8 == 0) only permutes which workgroup computes
-    which (row, KV head): output and appended K/V slot equal the plain order bit
-    for bit, shared prompt rows and left padding included, with and without
-    warm-up workgroups in the launch."""
+def test_attn_decode_l3_warmup_is_result_neutral(ops, dev, B, Hkv, G):
+    """swh_attn_decode_l3 (warm-up workgroups reading {ptr, bytes/16, 0} ranges on
+    the CUs the attention leaves idle) writes exactly what swh_attn_decode_shared
+    writes — output and appended K/V slot — with shared prompt rows and left
+    padding, and leaves the ranges it reads unchanged."""
     from swh_trl_amd import nn_ops
     g = _gen(77 + B)
     D, P, step = 64, 40, 9
@@ -1606,20 +1587,15 @@ def test_attn_decode_xcd_rows_is_a_permutation(ops, dev, monkeypatch, B, Hkv, G)
     cos, sin = _rope_tables(D, 2048, 1e6, dev)
     state = torch.tensor([step + 1, P], dtype=torch.int32, device=dev)
     prow = torch.arange(0, B, G, device=dev).repeat_interleave(G).to(torch.int32)
-    junk = torch.randn(1 << 16, device=dev)
-    jobs = torch.tensor([junk.data_ptr(), junk.numel() * 4 // 16, 0], dtype=torch.int64).to(dev)
+    junk = [torch.randn(n, device=dev) for n in (4, 1 << 16, 4 * 7001)]
+    before = [j.clone() for j in junk]
+    jobs = torch.tensor(sum([[j.data_ptr(), j.numel() * 4 // 16, 0] for j in junk], []), dtype=torch.int64).to(dev)
     sink = torch.zeros(64 * 512, dtype=torch.int32, device=dev)
-    res = {}
-    for flag in ("1", "0"):
-        monkeypatch.setenv("SWH_ATTN_XCD_ROWS", flag)
-        k2, v2 = kc.clone(), vc.clone()
-        a = nn_ops.attn_decode(qkv, k2, v2, cos, sin, plen, state, Hq, Hkv, D, D ** -0.5, prompt_row=prow)
-        k3, v3 = kc.clone(), vc.clone()
-        out = torch.empty_like(a)
-        nn_ops.attn_decode_l3(qkv, k3, v3, cos, sin, plen, state, Hq, Hkv, D, D ** -0.5, out, prow, False, jobs, 32,
-                              sink)
-        res[flag] = (a, k2, v2, out, k3, v3)
+    k2, v2 = kc.clone(), vc.clone()
+    a = nn_ops.attn_decode(qkv, k2, v2, cos, sin, plen, state, Hq, Hkv, D, D ** -0.5, prompt_row=prow)
+    k3, v3 = kc.clone(), vc.clone()
+    out = torch.empty_like(a)
+    nn_ops.attn_decode_l3(qkv, k3, v3, cos, sin, plen, state, Hq, Hkv, D, D ** -0.5, out, prow, False, jobs, 32, sink)
     torch.cuda.synchronize()
-    for x, y in zip(res["1"], res["0"]):
-        assert torch.equal(x, y)
-    assert torch.equal(res["1"][0], res["1"][3])
+    assert torch.equal(a, out) and torch.equal(k2, k3) and torch.equal(v2, v3)
+    assert all(torch.equal(x, y) for x, y in zip(junk, before))

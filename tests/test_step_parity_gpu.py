@@ -80,7 +80,7 @@ def _weights(model):
 
 
 def product_run(cfg, dtype, n_steps, *, std, lr, G=4, P=12, C=24, MB=8, GA=2, seed=11, n_prompts=None,
-                **grpo_kw):
+                min_new_tokens=4, **grpo_kw):
     """n_steps GRPOTrainer optimizer steps; captures every generation (its
     output and the shuffle permutation drawn after it), every training pass's
     log-probs, and the loss / grad norm / gradients / weights of every step."""
@@ -98,7 +98,8 @@ def product_run(cfg, dtype, n_steps, *, std, lr, G=4, P=12, C=24, MB=8, GA=2, se
                       max_prompt_length=P, max_completion_length=C, learning_rate=lr, max_steps=n_steps,
                       lr_scheduler_type="constant", seed=5, shuffle_dataset=False,
                       model_init_kwargs={"torch_dtype": "float32" if dtype == torch.float32 else "bfloat16"},
-                      generation_kwargs={"eos_token_id": EOS, "pad_token_id": PAD, "min_new_tokens": 4}, **grpo_kw)
+                      generation_kwargs={"eos_token_id": EOS, "pad_token_id": PAD, "min_new_tokens": min_new_tokens},
+                      **grpo_kw)
     model = CausalLM(cfg, dev, seed=3, init_std=std, dtype=dtype)
     tr = GRPOTrainer(model=model, reward_funcs=_reward_product, args=args, train_dataset=ds)
     assert tr.model.dtype == dtype
@@ -355,6 +356,28 @@ def test_cfg5_llama8b_width_step_matches_oracle():
     orc_bf = oracle_run(cfg, prod["w0"], torch.bfloat16, prod, 1, lr=lr, beta=0.04, device="cuda:0")
     orc_32 = oracle_run(cfg, prod["w0"], torch.float32, prod, 1, lr=lr, beta=0.04, device="cuda:0")
     _check_bf16("cfg5-llama8b-width", prod, orc_bf, orc_32, beta=0.04)
+
+
+def test_cfg5_llama8b_width_full_length_step_matches_oracle():
+    """BASELINE.json config 5 at its own workload length (grpo_trainer.py:1793-1810,
+    :1871-1899): Llama-3-8B width with 2 layers, 8 prompts x G 8 of P 256, every row
+    decoding all 1024 completion tokens (min_new_tokens), beta 0.04 against a frozen
+    reference.  The rollout runs the D 128 shared-prompt decode attention out to 1,280
+    keys and 1023 graph-replayed decode steps of the wide GEMMs; the fused training
+    pass is 8 x 256 + 64 x 1024 = 67,584 tokens.  One bf16 step against the
+    reference loop (oracle on the device) with this module's bf16 bounds, and the
+    step-1 KL exactly 0."""
+    from swh_trl_amd.engine.config import llama3_8b
+    import dataclasses
+    cfg = dataclasses.replace(llama3_8b(), num_hidden_layers=2)
+    lr = 1e-3
+    kw = dict(G=8, P=256, C=1024, MB=16, GA=4, beta=0.04)
+    prod = product_run(cfg, torch.bfloat16, 1, std=0.02, lr=lr, min_new_tokens=1024, **kw)
+    g = prod["gens"][0]
+    assert g["completion_ids"].shape == (64, 1024) and bool(g["completion_mask"].all())
+    orc_bf = oracle_run(cfg, prod["w0"], torch.bfloat16, prod, 1, lr=lr, beta=0.04, device="cuda:0")
+    orc_32 = oracle_run(cfg, prod["w0"], torch.float32, prod, 1, lr=lr, beta=0.04, device="cuda:0")
+    _check_bf16("cfg5-llama8b-width-C1024", prod, orc_bf, orc_32, beta=0.04)
 
 
 def test_early_stopped_rollout_width_matches_oracle_fp32():

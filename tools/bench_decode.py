@@ -72,39 +72,6 @@ def sweep(eng, m):
     os.environ.pop("SWH_GEMM_CFG", None)
 
 
-def prefetch(eng, m):
-    """Does a read of a layer's gate/up weights just before its GEMM (caches warm,
-    e.g. the Infinity Cache) shorten the GEMM?  Per layer: [read W_i; gate_up_i]
-    against [read W_(i+12); gate_up_i] (same read cost, cold weights)."""
-    from swh_trl_amd import nn_ops
-    c, ss, L = eng.cfg, eng.ss, eng.cfg.num_hidden_layers
-    ws = [eng._normed(f"l{i}.gu_w", "")[0] for i in range(L)]
-    sink = torch.empty(L, 896, device=ws[0].device, dtype=torch.float32)
-
-    def run(shift, gemm=True):
-        for i in range(L):
-            torch.sum(ws[(i + shift) % L].view(-1, 896), dim=0, dtype=torch.float32, out=sink[i])
-            if gemm:
-                nn_ops.decode_gemm(eng.s, ws[i], silu=True, y=eng.act, ss_in=ss)
-
-    for name, fn in (("read own W, then gate_up", lambda: run(0)), ("read other W, then gate_up", lambda: run(12)),
-                     ("read only", lambda: run(0, False))):
-        fn()
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            fn()
-        g.replay()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(5):
-            g.replay()
-        e1.record()
-        e1.synchronize()
-        print(f"{name:28s} {1000 * e0.elapsed_time(e1) / 5 / L:8.2f} us per layer", flush=True)
-
-
 def ku_sweep(eng, m):
     """o / down / qkv under waves per workgroup (SWH_GEMM_NW) x geometry."""
     from swh_trl_amd import nn_ops
@@ -238,7 +205,6 @@ def main():
     ap.add_argument("--gemm-cfg", default=None)
     ap.add_argument("--sweep", action="store_true", help="time the GEMM shapes under several launch geometries")
     ap.add_argument("--dual", action="store_true", help="two half-batch chains on two streams vs one chain")
-    ap.add_argument("--prefetch", action="store_true", help="gate/up after reading its own vs another layer's weights")
     ap.add_argument("--ku", action="store_true", help="weight-round depth x waves x geometry sweep (o, down, qkv)")
     args = ap.parse_args()
     if args.gemm_cfg:
@@ -263,9 +229,6 @@ def main():
         return
     if args.dual:
         dual(eng, m)
-        return
-    if args.prefetch:
-        prefetch(eng, m)
         return
     if args.ku:
         ku_sweep(eng, m)

@@ -58,7 +58,7 @@ def main():
                                                    **af(2)),
     }
     print({k: len(v) for k, v in W.items()}, flush=True)
-    steps_only = "--steps-only" in sys.argv or "--attn-l3" in sys.argv
+    steps_only = False
     stream = torch.cuda.current_stream()
 
     def timed(fn, n, cycle, iters=5):
@@ -103,42 +103,6 @@ def main():
     del W
     torch.cuda.empty_cache()
 
-    # the whole decode step with the Infinity Cache warm-up branch (swh_l3_prefetch)
-    def step_us(nwg, at, nt):
-        eng.l3_nwg, eng.l3_at, eng.l3_nt = nwg, at, nt
-        eng._l3_jobs = None
-        eng.state[0] = 100
-        return timed(lambda i: eng._step_fused(), 4, 1, iters=6)
-
-    grid = ((0, 0, 0), (32, 0, 0), (64, 0, 0), (128, 0, 0), (0, 0, 0), (64, 1, 0), (64, 2, 0), (64, 0, 1), (128, 1, 0),
-            (256, 1, 0), (0, 0, 0))
-    if steps_only:
-        grid = ((0, 0, 0), (32, 0, 0), (128, 1, 0), (0, 0, 0))
-    if "--attn-l3" in sys.argv:
-        grid = ()
-    for nwg, at, nt in grid:
-        print(f"decode step  l3 nwg {nwg:3d} at {at} nt {nt}: {step_us(nwg, at, nt):8.1f} us", flush=True)
-
-    # the warm-up carried by the attention launch (swh_attn_decode_l3) and the qkv launch
-    # (swh_decode_gemm_fragw_l3)
-    def step_attn(nwg, sel, qn=0, qsel=""):
-        eng.l3_nwg = 0
-        eng.l3_attn, eng.l3_set = nwg, sel
-        eng.l3_qkv, eng.l3_qkv_set = qn, qsel
-        eng._l3a_jobs = eng._l3q_jobs = None
-        eng.state[0] = 100
-        return timed(lambda i: eng._step_fused(), 4, 1, iters=6)
-
-    if "--attn-l3" in sys.argv:
-        grid = [(0, "", 0, ""), (96, "o,down,qkv1", 0, ""), (96, "o@x,down@x,qkv1@x", 0, ""),
-                (96, "o,down@x,qkv1", 0, ""), (0, "", 0, ""), (128, "o@x,down@x,qkv1@x", 0, ""),
-                (96, "o,down,qkv1", 0, ""), (96, "o@x,down@x,qkv1@x", 0, ""), (0, "", 0, "")]
-        env_grid = os.environ.get("SWH_PROBE_GRID")
-        if env_grid:  # "nwg:set:qkv_nwg:qkv_set;..."
-            grid = [(int(a), b, int(c), d) for a, b, c, d in (e.split(":") for e in env_grid.split(";"))]
-        for nwg, sel, qn, qsel in grid:
-            print(f"decode step  attn-l3 {nwg:3d} {sel:16s} qkv-l3 {qn:3d} {qsel:10s}: "
-                  f"{step_attn(nwg, sel, qn, qsel):8.1f} us", flush=True)
 
 if __name__ == "__main__":
     main()
