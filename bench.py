@@ -65,13 +65,31 @@ def _cpu_model() -> str:
     return platform.processor() or platform.machine()
 
 
+def usable_cores() -> tuple:
+    """the cores this process may run on — its affinity set —
+    bounded by the cgroup CPU quota when one is set (threads beyond the quota
+    only time-slice).  Returns (count, how it was determined)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    if quota is not None and quota < aff:
+        return quota, f"cgroup cpu.max quota {quota} of {aff} CPUs in the affinity set"
+    return aff, f"sched_getaffinity: {aff} CPUs"
+
+
 def cpu_baseline(steps_note: str) -> dict:
     """The oracle's CPU restatement of the reference GRPO step (SURVEY.md §8d:
     reduced cfg2 = 1 prompt x G=8, P=128, C=256 at full length), timed on the
     host cores and reported per sample; nothing is extrapolated."""
     from oracle import grpo_step as og
     from swh_trl_amd.engine.config import qwen2_5_0_5b
-    threads = min(16, len(os.sched_getaffinity(0)))
+    threads, why = usable_cores()
     torch.set_num_threads(threads)
     cfg = qwen2_5_0_5b().to_dict()
     model = og.hf_qwen2_from_config(cfg, seed=0, dtype=torch.bfloat16)
@@ -90,7 +108,8 @@ def cpu_baseline(steps_note: str) -> dict:
     t0 = time.perf_counter()
     og.grpo_step(model, opt, prompt, pm, reward, C=C, min_new_tokens=C, timings=tm, **kw)
     wall = time.perf_counter() - t0
-    return {"value": G / wall, "unit": "samples/s", "cores": threads, "kind": "port", "cpu": _cpu_model(),
+    return {"value": G / wall, "unit": "samples/s", "cores": threads, "cores_source": why, "kind": "port",
+            "cpu": _cpu_model(),
             "cfg1": cpu_cfg1(threads),
             "sample": (f"oracle/grpo_step.py (CPU restatement, transformers Qwen2 bf16, torch {torch.__version__}) on "
                        f"1 prompt x G={G}, P={P}, C={C} (full length): generate {tm['generate_s']:.2f}s + update "
@@ -140,6 +159,36 @@ def pmc_traffic(kernel: str):
         return None if k is None else k["hbm_bytes_per_launch"]
     except (OSError, ValueError, KeyError):
         return None
+
+
+def kernel_roofline(kern: dict, eng, steps: int, C: int) -> dict:
+    """The `roofline` object of the bench line.  Eager kernels
+    (log-prob, loss, AdamW ...) are timed by HIP events around each launch
+    inside the timed region (`kern`, swh_trl_amd.profiling).  The decode
+    kernels run inside the captured decode-step graph, where per-launch events
+    do not exist, so each one is timed right after the timed region: the same
+    kernel on the same buffers, replayed from a graph between HIP events on its
+    stream (DecodeEngine.kernel_timings, mid-completion step C/2).  Dominant =
+    the largest device time per step; achieved = algorithmic bytes per launch /
+    its average duration; traffic = the committed PMC bytes per launch."""
+    kinfo = {k: {"avg_us": v["avg_us"], "bytes_per_launch": v["bytes_per_launch"],
+                 "per_step": v["launches"] / steps} for k, v in kern.items()}
+    if eng is not None and getattr(eng, "fused", False):
+        for k, v in eng.kernel_timings(C // 2).items():
+            if k != "decode_step":
+                kinfo[k] = {"avg_us": v["avg_us"], "bytes_per_launch": v["bytes_per_launch"],
+                            "per_step": v["launches_per_step"] * C}
+    dom_name, dom = max(kinfo.items(), key=lambda kv: kv[1]["avg_us"] * kv[1]["per_step"])
+    achieved = dom["bytes_per_launch"] / (dom["avg_us"] * 1e-6) / 1e9
+    return {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "avg_us": round(dom["avg_us"], 2), "bytes_per_launch": dom["bytes_per_launch"],
+            "traffic": pmc_traffic(dom_name), "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)",
+            "traffic_source": os.path.relpath(PMC_FILE, ROOT),
+            "all_kernels": {k: {"avg_us": round(v["avg_us"], 2), "launches_per_step": v["per_step"],
+                                "ms_per_step": round(v["avg_us"] * v["per_step"] / 1000.0, 2),
+                                "GB/s": round(v["bytes_per_launch"] / (v["avg_us"] * 1e-6) / 1e9, 1)}
+                            for k, v in kinfo.items()}}
 
 
 def _launch_ranks(n: int, argv: list) -> int:
@@ -217,32 +266,7 @@ def main():
     value = samples / elapsed
     ms = 1000.0 * elapsed / steps
 
-    # Kernel timings.  Eager kernels (log-prob, loss, AdamW ...) are timed by
-    # HIP events around each launch inside the timed region.  The decode kernels
-    # run inside the captured decode-step graph, where per-launch events do not
-    # exist, so each one is timed right after the timed region: the same
-    # kernel on the same buffers, replayed from a graph between HIP events on
-    # its stream (DecodeEngine.kernel_timings, mid-completion step C/2).
-    # Dominant = the largest device time per GRPO step.
-    kinfo = {k: {"avg_us": v["avg_us"], "bytes_per_launch": v["bytes_per_launch"],
-                 "per_step": v["launches"] / steps} for k, v in kern.items()}
-    eng = getattr(tr, "_engine", None)
-    if eng is not None and eng.fused:
-        for k, v in eng.kernel_timings(C // 2).items():
-            if k != "decode_step":
-                kinfo[k] = {"avg_us": v["avg_us"], "bytes_per_launch": v["bytes_per_launch"],
-                            "per_step": v["launches_per_step"] * C}
-    dom_name, dom = max(kinfo.items(), key=lambda kv: kv[1]["avg_us"] * kv[1]["per_step"])
-    achieved = dom["bytes_per_launch"] / (dom["avg_us"] * 1e-6) / 1e9
-    roof = {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "avg_us": round(dom["avg_us"], 2), "bytes_per_launch": dom["bytes_per_launch"],
-            "traffic": pmc_traffic(dom_name), "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)",
-            "traffic_source": os.path.relpath(PMC_FILE, ROOT),
-            "all_kernels": {k: {"avg_us": round(v["avg_us"], 2), "launches_per_step": v["per_step"],
-                                "ms_per_step": round(v["avg_us"] * v["per_step"] / 1000.0, 2),
-                                "GB/s": round(v["bytes_per_launch"] / (v["avg_us"] * 1e-6) / 1e9, 1)}
-                            for k, v in kinfo.items()}}
+    roof = kernel_roofline(kern, getattr(tr, "_engine", None), steps, C)
     # step-level roofline: t_roof = HBM bytes / 8 TB/s + FLOPs / 2.5 PF
     t_roof_ms = 70.5
     line = {"metric": METRIC, "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": steps,

@@ -136,9 +136,10 @@ def micro_batch_loss(policy, value_model, ro: dict, inds, *, context_length: int
 
 
 def ppo_update(policy, value_model, optimizer, ro: dict, permutations, *, local_mini_batch_size: int,
-               per_device_train_batch_size: int, gradient_accumulation_steps: int, **loss_kw):
+               per_device_train_batch_size: int, gradient_accumulation_steps: int, on_step=None, **loss_kw):
     """ppo_trainer.py:537-617: for each epoch's permutation, mini-batches of
-    GA micro-batches, loss / GA accumulated, one optimizer step per mini-batch."""
+    GA micro-batches, loss / GA accumulated, one optimizer step per mini-batch.
+    on_step(): called before each optimizer step (the accumulated gradients)."""
     n = ro["responses"].shape[0]
     all_stats = []
     for perm in permutations:
@@ -150,6 +151,8 @@ def ppo_update(policy, value_model, optimizer, ro: dict, permutations, *, local_
                                                **loss_kw)
                 (loss / gradient_accumulation_steps).backward()
                 all_stats.append(stats)
+            if on_step is not None:
+                on_step()
             optimizer.step()
             optimizer.zero_grad()
     return all_stats

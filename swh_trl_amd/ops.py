@@ -195,16 +195,17 @@ def masked_mean(values: torch.Tensor, mask: torch.Tensor, axis=None) -> torch.Te
 
 
 def masked_var(values: torch.Tensor, mask: torch.Tensor, unbiased: bool = True) -> torch.Tensor:
-    """trl/core.py:51-67 via the whitening kernel's statistics: the masked
-    variance, Bessel-corrected when `unbiased`; raises ValueError on an
-    all-zero mask when `unbiased` (core.py:57-62), NaN otherwise."""
+    """trl/core.py:51-67: the masked variance about the masked mean,
+    Bessel-corrected when `unbiased` (the whitening kernel's statistics;
+    raises ValueError on an all-zero mask, core.py:57-62).  unbiased=False is
+    the plain masked mean of the squared deviations, as the reference forms it
+    before its correction: 0 for a single unmasked element, NaN for none."""
     _, stats = masked_whiten_stats(values, mask)
     if unbiased:
         if float(stats[2]) == 0:
             raise ValueError(_ZERO_MASK_MSG)
         return stats[1]
-    n = stats[2]
-    return stats[1] * (n - 1) / n
+    return masked_mean((values.to(torch.float32) - stats[0]) ** 2, mask.to(torch.float32))
 
 
 # ---------------------------------------------------------------------------

@@ -281,6 +281,12 @@ def test_masked_whiten(ops, dev):
         ops.masked_whiten(v.to(dev), torch.zeros_like(m).to(dev))
     with pytest.raises(ValueError, match="sum of the mask is zero"):
         ops.masked_var(v.to(dev), torch.zeros_like(m).to(dev))
+    # core.py:51-56 without the correction: one unmasked element has variance 0, none is 0 / 0
+    one = torch.zeros_like(m)
+    one[3, 7] = True
+    assert float(ops.masked_var(v.to(dev), one.to(dev), unbiased=False)) == 0.0
+    assert float(trl_ref.masked_var(v.double(), one.double(), unbiased=False)) == 0.0
+    assert torch.isnan(ops.masked_var(v.to(dev), torch.zeros_like(m).to(dev), unbiased=False))
 
 
 @pytest.mark.parametrize("stop,est,pen", [(3, "k1", None), (3, "k3", 1.0), (None, "k1", 0.5)])

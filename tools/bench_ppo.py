@@ -41,19 +41,30 @@ def main():
                    eos_token_id=151645, seed=0)
     tr = PPOTrainer(pc, None, cfg, None, rm_cfg, ds, cfg)
     tr.state.global_step = 0
+    from bench import kernel_roofline
+    from swh_trl_amd import profiling
     for _ in range(args.warmup):
         tr.training_step()
     torch.cuda.synchronize()
+    profiling.reset()
+    profiling.enable(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         tr.training_step()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
+    profiling.enable(False)
+    kern = profiling.summary()
     log = tr._flush_logs()
+    # the rollout decodes with log-probs (logits + sampler path), the dominant kernel over the update
+    roof = kernel_roofline(kern, tr._engine, args.steps, pc.response_length)
     print(json.dumps({"metric": "PPO update samples/sec (rollout + 4 PPO epochs), Qwen2.5-0.5B policy+value",
                       "value": round(B / dt, 3), "unit": "samples/s", "ms_per_step": round(1000 * dt, 1),
-                      "config": {"queries": B, "query_len": P, "response_length": 53, "num_ppo_epochs": 4,
-                                 "micro_batch": 16, "grad_accum": 4, "dtype": "bf16"},
+                      "dtype": "bf16", "data": "synthetic (uniform query ids seed 1234, random-init weights)",
+                      "config": {"workload": "configs[2]: Qwen2.5-0.5B PPOTrainer + value head + tiny reward model",
+                                 "queries": B, "query_len": P, "response_length": 53, "num_ppo_epochs": 4,
+                                 "micro_batch": 16, "grad_accum": 4},
+                      "roofline": roof,
                       "log": {k: log.get(k) for k in ("objective/kl", "loss/policy_avg", "loss/value_avg",
                                                       "val/ratio")}}), flush=True)
 
