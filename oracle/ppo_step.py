@@ -113,8 +113,10 @@ def rollout_scores(policy, ref_policy, value_model, reward_model, queries, respo
 
 
 def micro_batch_loss(policy, value_model, ro: dict, inds, *, context_length: int, pad_token_id: int,
-                     temperature: float, cliprange: float, cliprange_value: float, vf_coef: float):
-    """ppo_trainer.py:557-605 for one micro-batch (differentiable loss, stats)."""
+                     temperature: float, cliprange: float, cliprange_value: float, vf_coef: float,
+                     token_terms: bool = False):
+    """ppo_trainer.py:557-605 for one micro-batch (differentiable loss, stats;
+    token_terms: stats["tokens"] = per-token terms of each statistic)."""
     qr = ro["query_responses"][inds]
     out = forward(policy, qr, pad_token_id)
     logits = out.logits[:, context_length - 1:-1] / (temperature + 1e-7)
@@ -126,13 +128,28 @@ def micro_batch_loss(policy, value_model, ro: dict, inds, *, context_length: int
     loss, pg_loss, vf_loss, stats = trl_ref.ppo_losses(
         new_logprobs, ro["logprobs"][inds], ro["advantages"][inds], vpred, ro["values"][inds],
         ro["returns"][inds], ro["padding_mask"][inds], ro["padding_mask_p1"][inds], cliprange, cliprange_value,
-        vf_coef)
+        vf_coef, token_terms=token_terms)
     with torch.no_grad():
         prob = torch.softmax(logits.float(), -1)
         entropy = torch.logsumexp(logits.float(), -1) - (prob * logits.float()).sum(-1)
     stats = dict(stats, pg_loss=float(pg_loss.detach()), vf_loss=float(vf_loss.detach()),
                      entropy=float(entropy.mean()))
+    if token_terms:
+        stats["tokens"]["entropy"] = entropy.flatten()
     return loss, stats
+
+
+def mini_batch_backward(policy, value_model, ro: dict, mini, *, per_device_train_batch_size: int,
+                        gradient_accumulation_steps: int, **loss_kw):
+    """ppo_trainer.py:551-605 for one mini-batch: its GA micro-batches, each
+    loss / GA back-propagated into the accumulated gradients; returns the
+    micro-batches' stats."""
+    stats = []
+    for u0 in range(0, len(mini), per_device_train_batch_size):
+        loss, st = micro_batch_loss(policy, value_model, ro, mini[u0:u0 + per_device_train_batch_size], **loss_kw)
+        (loss / gradient_accumulation_steps).backward()
+        stats.append(st)
+    return stats
 
 
 def ppo_update(policy, value_model, optimizer, ro: dict, permutations, *, local_mini_batch_size: int,
@@ -145,12 +162,9 @@ def ppo_update(policy, value_model, optimizer, ro: dict, permutations, *, local_
     for perm in permutations:
         perm = torch.as_tensor(perm)
         for m0 in range(0, n, local_mini_batch_size):
-            mini = perm[m0:m0 + local_mini_batch_size]
-            for u0 in range(0, local_mini_batch_size, per_device_train_batch_size):
-                loss, stats = micro_batch_loss(policy, value_model, ro, mini[u0:u0 + per_device_train_batch_size],
-                                               **loss_kw)
-                (loss / gradient_accumulation_steps).backward()
-                all_stats.append(stats)
+            all_stats += mini_batch_backward(policy, value_model, ro, perm[m0:m0 + local_mini_batch_size],
+                                             per_device_train_batch_size=per_device_train_batch_size,
+                                             gradient_accumulation_steps=gradient_accumulation_steps, **loss_kw)
             if on_step is not None:
                 on_step()
             optimizer.step()

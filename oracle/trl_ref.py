@@ -339,9 +339,12 @@ def gae(rewards: torch.Tensor, values: torch.Tensor, gamma: float, lam: float):
 
 
 def ppo_losses(new_logprobs, mb_logprobs, mb_advantage, vpred, mb_values, mb_return,
-               padding_mask, padding_mask_p1, cliprange: float, cliprange_value: float, vf_coef: float):
+               padding_mask, padding_mask_p1, cliprange: float, cliprange_value: float, vf_coef: float,
+               token_terms: bool = False):
     """ppo_trainer.py:557-605 — clipped value loss + clipped PG loss (inputs already
-    INVALID_LOGPROB / zero masked as at :562-566).  Parity unpinned."""
+    INVALID_LOGPROB / zero masked as at :562-566).  Parity unpinned.
+    token_terms: stats["tokens"] also holds each statistic's per-token terms
+    (the elements its mean runs over), for error estimates in the tests."""
     vclip = torch.clamp(vpred, mb_values - cliprange_value, mb_values + cliprange_value)
     v1 = (vpred - mb_return) ** 2
     v2 = (vclip - mb_return) ** 2
@@ -358,6 +361,10 @@ def ppo_losses(new_logprobs, mb_logprobs, mb_advantage, vpred, mb_values, mb_ret
         stats = dict(pg_clipfrac=masked_mean((p2 > p1).float(), ~padding_mask).item(),
                      vf_clipfrac=vf_clipfrac.item(), approxkl=(0.5 * (diff ** 2).mean()).item(),
                      ratio=ratio.mean().item())
+        if token_terms:
+            stats["tokens"] = dict(pg_loss=torch.max(p1, p2)[~padding_mask].float(),
+                                   vf_loss=0.5 * torch.max(v1, v2)[~padding_mask_p1].float(),
+                                   approxkl=0.5 * (diff ** 2).flatten().float(), ratio=ratio.flatten().float())
     return loss, pg_loss, vf_loss, stats
 
 

@@ -4,6 +4,8 @@ oracle/ppo_step.py (transformers Qwen2 models in fp32 on the host, loaded
 with the engine's bf16 weights).  Parity for this path is unpinned by the
 reference's own tests; tolerances below are the bf16
 engine against an fp32 restatement."""
+import math
+
 import pytest
 import torch
 
@@ -18,7 +20,7 @@ def dev():
     return torch.device("cuda:0")
 
 
-def _hf(m, seqcls: bool):
+def _hf(m, seqcls: bool, sd: dict = None):
     from transformers import Qwen2Config, Qwen2ForCausalLM, Qwen2ForSequenceClassification
     c = m.cfg
     hc = Qwen2Config(vocab_size=c.vocab_size, hidden_size=c.hidden_size, intermediate_size=c.intermediate_size,
@@ -28,7 +30,7 @@ def _hf(m, seqcls: bool):
                      num_labels=1, pad_token_id=PAD)
     hc._attn_implementation = "eager"
     hf = (Qwen2ForSequenceClassification if seqcls else Qwen2ForCausalLM)(hc)
-    sd = {k: v.detach().float().cpu() for k, v in m.hf_state_dict().items()}
+    sd = {k: v.detach().float().cpu() for k, v in (sd or m.hf_state_dict()).items()}
     missing, _ = hf.load_state_dict(sd, strict=False)
     assert not [k for k in missing if "rotary" not in k and k != "lm_head.weight"], missing
     return hf.float().eval()
@@ -130,11 +132,21 @@ def _check_grads_bf16(tag, prod: dict, orc_bf: dict, orc_32: dict):
     return max(worst)
 
 
-def _check_stat_bf16(tag, k, p, b, f):
-    """A loss term / statistic: |product - oracle_bf16| <= 2 |oracle_bf16 -
-    oracle_fp32| + one bf16 rounding of the fp32 value."""
-    band = 2 * abs(b - f) + BF16_TOL * abs(f) + 1e-6
-    assert abs(p - b) <= band, (tag, k, p, b, f, band)
+def _stat_band(k, sb: dict, sf: dict) -> float:
+    """The band for a statistic (a mean over tokens): twice the reference's own
+    bf16 error of it plus one bf16 rounding of the fp32 value.  That error is
+    taken as the larger of its realised value |oracle_bf16 - oracle_fp32| and
+    twice its expected size, the per-token error RMS over sqrt(n) (a single
+    realisation of a mean can land near zero by chance)."""
+    b, f = sb[k], sf[k]
+    tb, tf = sb["tokens"][k].float(), sf["tokens"][k].float()
+    se = float((tb - tf).pow(2).mean().sqrt()) / math.sqrt(max(tb.numel(), 1))
+    return 2 * max(abs(b - f), 2 * se) + BF16_TOL * abs(f) + 1e-6
+
+
+def _check_stat_bf16(tag, k, p, sb, sf):
+    band = _stat_band(k, sb, sf)
+    assert abs(p - sb[k]) <= band, (tag, k, p, sb[k], sf[k], band)
 
 
 WIDTHS = ["tiny", "qwen2.5-0.5b-width"]
@@ -167,12 +179,13 @@ def test_ppo_micro_batch_bf16_matches_oracle(dev, width):
         pol, val = _hf(tr.policy_model, False).to(dt), _hf(tr.value_model, True).to(dt)
         loss, ost = ppo_step.micro_batch_loss(pol, val, oro, inds, context_length=queries.shape[1], pad_token_id=PAD,
                                               temperature=a.temperature, cliprange=a.cliprange,
-                                              cliprange_value=a.cliprange_value, vf_coef=a.vf_coef)
+                                              cliprange_value=a.cliprange_value, vf_coef=a.vf_coef,
+                                              token_terms=True)
         loss.backward()
         res[dt] = (ost, _hf_grads(pol), _hf_grads(val))
     (sb, pb, vb), (sf, pf, vf) = res[torch.bfloat16], res[torch.float32]
     for i, k in ((0, "pg_loss"), (1, "vf_loss"), (4, "approxkl"), (5, "ratio"), (8, "entropy")):
-        _check_stat_bf16(width, k, float(st[i]), sb[k], sf[k])
+        _check_stat_bf16(width, k, float(st[i]), sb, sf)
     print(width, "policy", _check_grads_bf16(width + "-policy", gp, pb, pf))
     print(width, "value", _check_grads_bf16(width + "-value", gv, vb, vf))
 
@@ -180,12 +193,14 @@ def test_ppo_micro_batch_bf16_matches_oracle(dev, width):
 @pytest.mark.parametrize("width", WIDTHS)
 def test_ppo_update_schedule_bf16_matches_oracle(dev, width):
     """A full PPO update (ppo_trainer.py:537-617: epochs x mini-batches x GA, one
-    AdamW step per mini-batch, no clipping) on the bf16 path against the
-    reference loop in bf16 and in fp32 from the same weights and rollout: the
-    accumulated policy and value gradients of every optimizer step within the
-    bf16-rounding bounds (each side follows its own updated weights, so later
-    steps also carry the parameter precision: the reference updates bf16
-    parameters, the product fp32 master weights)."""
+    AdamW step per mini-batch, no clipping) on the bf16 path: before each
+    optimizer step the accumulated policy and value gradients equal the
+    reference's mini-batch (its GA micro-batches, loss / GA) evaluated in bf16
+    and in fp32 at the product's weights of that step, within the bf16-rounding
+    bounds.  Each step is checked from the product's own weights: after one
+    AdamW step (whose first update is ~lr * sign(grad)) two bf16 trajectories
+    part by the sign noise of near-zero gradient elements, which says nothing
+    about the schedule; the update itself is the AdamW kernel's own test."""
     from oracle import ppo_step
     tr, ds = _trainer(dev, width=width, learning_rate=1e-4)
     a = tr.args
@@ -196,33 +211,40 @@ def test_ppo_update_schedule_bf16_matches_oracle(dev, width):
              for e in range(a.num_ppo_epochs)]
     oro = _cpu(ro)
     oro["values"] = oro["values"].float()
-    models = {dt: (_hf(tr.policy_model, False).to(dt), _hf(tr.value_model, True).to(dt))
-              for dt in (torch.bfloat16, torch.float32)}
     prod_steps = []
     step_fn = tr._optimizer_step
 
+    def snap(m):
+        return {k: v.detach().cpu().clone() for k, v in m.hf_state_dict().items()}
+
     def capture(lr):
-        prod_steps.append((_grads(tr.policy_model), _grads(tr.value_model)))
+        prod_steps.append((snap(tr.policy_model), snap(tr.value_model), _grads(tr.policy_model),
+                           _grads(tr.value_model)))
         return step_fn(lr)
 
     tr._optimizer_step = capture
     tr.ppo_update(ro, a.learning_rate, permutations=perms)
-    orc_steps = {}
-    for dt, (pol, val) in models.items():
-        opt = torch.optim.AdamW(list(pol.parameters()) + list(val.parameters()), lr=a.learning_rate,
-                                betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0)
-        rec = orc_steps[dt] = []
-        ppo_step.ppo_update(pol, val, opt, oro, perms, local_mini_batch_size=a.local_mini_batch_size,
-                            per_device_train_batch_size=a.per_device_train_batch_size,
-                            gradient_accumulation_steps=a.gradient_accumulation_steps,
-                            context_length=queries.shape[1], pad_token_id=PAD, temperature=a.temperature,
-                            cliprange=a.cliprange, cliprange_value=a.cliprange_value, vf_coef=a.vf_coef,
-                            on_step=lambda p=pol, v=val, r=rec: r.append((_hf_grads(p), _hf_grads(v))))
-    n = a.num_ppo_epochs * a.num_mini_batches
-    assert len(prod_steps) == len(orc_steps[torch.bfloat16]) == len(orc_steps[torch.float32]) == n
-    for s, (pr, ob, of) in enumerate(zip(prod_steps, orc_steps[torch.bfloat16], orc_steps[torch.float32])):
-        _check_grads_bf16(f"{width}-step{s}-policy", pr[0], ob[0], of[0])
-        _check_grads_bf16(f"{width}-step{s}-value", pr[1], ob[1], of[1])
+    minis = [torch.as_tensor(p)[m0:m0 + a.local_mini_batch_size]
+             for p in perms for m0 in range(0, a.local_batch_size, a.local_mini_batch_size)]
+    assert len(prod_steps) == len(minis) == a.num_ppo_epochs * a.num_mini_batches
+    models = {dt: (_hf(tr.policy_model, False).to(dt), _hf(tr.value_model, True).to(dt))
+              for dt in (torch.bfloat16, torch.float32)}
+    for s, ((wp, wv, gp, gv), mini) in enumerate(zip(prod_steps, minis)):
+        grads = {}
+        for dt, (pol, val) in models.items():
+            pol.load_state_dict(wp, strict=False)
+            val.load_state_dict(wv, strict=False)
+            pol.zero_grad(set_to_none=True)
+            val.zero_grad(set_to_none=True)
+            ppo_step.mini_batch_backward(pol, val, oro, mini, per_device_train_batch_size=a.per_device_train_batch_size,
+                                         gradient_accumulation_steps=a.gradient_accumulation_steps,
+                                         context_length=queries.shape[1], pad_token_id=PAD,
+                                         temperature=a.temperature, cliprange=a.cliprange,
+                                         cliprange_value=a.cliprange_value, vf_coef=a.vf_coef)
+            grads[dt] = (_hf_grads(pol), _hf_grads(val))
+        ob, of = grads[torch.bfloat16], grads[torch.float32]
+        _check_grads_bf16(f"{width}-step{s}-policy", gp, ob[0], of[0])
+        _check_grads_bf16(f"{width}-step{s}-value", gv, ob[1], of[1])
 
 
 def test_ppo_trainer_train_runs(dev):
@@ -271,15 +293,15 @@ def test_ppo_fused_micro_batches_equal_separate(dev, width):
             loss, ost = ppo_step.micro_batch_loss(pol, val, oro, half, context_length=queries.shape[1],
                                                   pad_token_id=PAD, temperature=a.temperature,
                                                   cliprange=a.cliprange, cliprange_value=a.cliprange_value,
-                                                  vf_coef=a.vf_coef)
+                                                  vf_coef=a.vf_coef, token_terms=True)
             (loss / a.gradient_accumulation_steps).backward()
             stats.append(ost)
         res[dt] = (stats, _hf_grads(pol), _hf_grads(val))
     (sb, pb, vb), (sf, pf, vf) = res[torch.bfloat16], res[torch.float32]
     for j in range(2):
         for i, k in ((0, "pg_loss"), (1, "vf_loss"), (4, "approxkl"), (5, "ratio"), (8, "entropy")):
-            band = 2 * abs(sb[j][k] - sf[j][k]) + BF16_TOL * abs(sf[j][k]) + 1e-6
-            assert abs(float(st_f[j, i]) - float(st_s[j, i])) <= band, (width, j, k)
+            band = _stat_band(k, sb[j], sf[j])
+            assert abs(float(st_f[j, i]) - float(st_s[j, i])) <= band, (width, j, k, band)
     for fused, sep, ob, of in ((gp_f, gp_s, pb, pf), (gv_f, gv_s, vb, vf)):
         for k, g32 in of.items():
             n32 = g32.norm().clamp_min(1e-20)

@@ -160,6 +160,36 @@ def _expected_scores(rm, tok, got, dev):
         return rm(**{k: v.to(dev) for k, v in enc.items()}).logits[:, 0].float().cpu()
 
 
+@pytest.mark.parametrize("source", ["directory", "module"])
+def test_reward_model_scores_match_transformers_at_ragged_lengths(tmp_path, source):
+    """RewardModel (the engine's fp32 score-head copy, from a directory or from
+    the module) against transformers at right-padded ragged lengths across the
+    attention tile edges (1..130 tokens), with and without an attention mask."""
+    from transformers import AutoModelForSequenceClassification
+
+    from swh_trl_amd.trainer.grpo_trainer import RewardModel
+    dev = torch.device("cuda:0")
+    d = tmp_path / "rm"
+    _classifier("cpu").save_pretrained(str(d))
+    rm = AutoModelForSequenceClassification.from_pretrained(str(d), num_labels=1, dtype=torch.float32).to(dev).eval()
+    rm.config.pad_token_id = 256
+    mine = (RewardModel.from_pretrained(str(d), dev, torch.float32) if source == "directory"
+            else RewardModel.from_module(rm, dev))
+    mine.config.pad_token_id = 256
+    g = torch.Generator().manual_seed(7)
+    for L in (1, 17, 63, 64, 65, 100, 130):
+        lens = torch.tensor([L] + [int(x) for x in torch.randint(1, L + 1, (5,), generator=g)])
+        ids = torch.randint(0, 256, (6, L), generator=g)
+        am = (torch.arange(L)[None] < lens[:, None]).long()
+        ids = ids.masked_fill(am == 0, 256)
+        with torch.inference_mode():
+            exp = rm(input_ids=ids.to(dev), attention_mask=am.to(dev)).logits[:, 0].float().cpu()
+            got = mine(input_ids=ids.to(dev), attention_mask=am.to(dev)).logits[:, 0].float().cpu()
+            got_nomask = mine(input_ids=ids.to(dev)).logits[:, 0].float().cpu()
+        torch.testing.assert_close(got, exp, **RM_TOL, msg=lambda m, L=L: f"L={L}: {m}")
+        torch.testing.assert_close(got_nomask, exp, **RM_TOL, msg=lambda m, L=L: f"L={L} no mask: {m}")
+
+
 def test_string_reward_model_loads_from_local_directory(tmp_path):
     """grpo_trainer.py:731-739, :754-771: a string reward function is loaded as
     AutoModelForSequenceClassification(num_labels=1) (here from a local directory,

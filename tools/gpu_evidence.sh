@@ -4,11 +4,13 @@
 #   bash tools/gpu_evidence.sh <tag> <step>...
 # steps:
 #   suite    pytest -m gpu (whole suite, one process) + smoke()      -> <tag>_gpu_suite.log
+#   sel      pytest -m gpu -k "$SEL" (a subset, one process)         -> <tag>_gpu_sel.log
 #   pmc      rocprofv3 FETCH_SIZE / WRITE_SIZE passes over tools/bench_decode.py -> <tag>_pmc_decode.json
 #   bench    python bench.py (default K / W, CPU baseline included)  -> <tag>_bench.json
 #   prof     rocprofv3 --kernel-trace --stats of bench.py --steps 1 --warmup 1 -> <tag>_bench_kernel_stats.csv
 #   decode   tools/bench_decode.py (per-kernel decode timings)       -> <tag>_decode.log
 #   train    tools/train_kernels.py (training half-step)             -> <tag>_train.log
+#   trace    rocprofv3 kernel trace of one training half-step + tools/critical_path.py -> <tag>_critical_path.txt
 #   ppo      tools/bench_ppo.py (BASELINE config 3)                  -> <tag>_ppo_bench.json
 #   llama    tools/bench_llama8b.py (config 5's per-GPU shape)       -> <tag>_llama8b.json
 set -o pipefail
@@ -29,6 +31,11 @@ for step in "$@"; do
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" \
         > $O/${tag}_smoke.log 2>&1 || fail smoke $? $O/${tag}_smoke.log
       tail -1 $O/${tag}_smoke.log ;;
+    sel)
+      timeout -k 10 600 python -u -m pytest tests -v -m gpu -k "$SEL" --timeout 300 --timeout-method thread \
+        > $O/${tag}_gpu_sel.log 2>&1; rc=$?
+      grep -E "FAILED|ERROR|passed|failed" $O/${tag}_gpu_sel.log | tail -30
+      [ $rc -eq 0 ] || fail sel $rc $O/${tag}_gpu_sel.log ;;
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
         timeout -s KILL 240 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/pmc_$c -o run \
@@ -53,6 +60,13 @@ for step in "$@"; do
     train)
       timeout -k 10 300 python -u tools/train_kernels.py > $O/${tag}_train.log 2>&1 || fail train $? $O/${tag}_train.log
       tail -15 $O/${tag}_train.log ;;
+    trace)
+      rm -rf /tmp/trace_$tag
+      timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d /tmp/trace_$tag -o run \
+        -- python3 tools/train_kernels.py --reps 1 > $O/${tag}_trace.log 2>&1 || fail trace $? $O/${tag}_trace.log
+      python tools/critical_path.py "$(find /tmp/trace_$tag -name '*kernel_trace.csv' | head -1)" 150 \
+        > $O/${tag}_critical_path.txt 2>&1 || fail critical_path $? $O/${tag}_critical_path.txt
+      head -40 $O/${tag}_critical_path.txt ;;
     ppo)
       timeout -k 10 400 python -u tools/bench_ppo.py > $O/${tag}_ppo_bench.json 2> $O/${tag}_ppo_bench.err \
         || fail ppo $? $O/${tag}_ppo_bench.err
