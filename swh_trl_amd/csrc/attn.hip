@@ -100,29 +100,16 @@ struct FaArgs {
 // a query that is computed and whose output / gradient exists
 __device__ __forceinline__ bool fa_qlive(const FaArgs &a, int b, int q) { return !(a.G && (b % a.G) && q < a.P); }
 
-// the 8 keys a lane holds in a 32-key block: k0 + 16 t + 4 g + r, t = 0, 1, r = 0..3
-struct FaKeyMask {
-    int32_t v[8];  // key_mask of those keys (1 when unpadded)
-};
-__device__ __forceinline__ FaKeyMask fa_key_mask(const FaArgs &a, int b, int k0, int g) {
-    FaKeyMask m;
-    if (!a.key_mask) {  // uniform branch: the unpadded causal case reads nothing
-#pragma unroll
-        for (int j = 0; j < 8; ++j) m.v[j] = 1;
-        return m;
-    }
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const int k = k0 + 16 * t + 4 * g;  // 4 consecutive keys, 16-B aligned (k % 4 == 0, L % 4 not required:
-#pragma unroll                              // clamp each)
-        for (int r = 0; r < 4; ++r) m.v[4 * t + r] = a.key_mask[(int64_t)b * a.L + min(k + r, a.L - 1)];
-    }
-    return m;
+// Key validity of a 32-key block is a bit mask, bit j = key k0 + j inside the sequence
+// and unpadded (a ballot, lanes 32-63 repeating 0-31); a lane's 8 keys of the block are
+// k0 + 16 t + 4 g + r (t = 0, 1, r = 0..3): bit 16 t + 4 g + r.
+// visibility of key k for query q (transformers' mask): causal, unpadded (kv: the key's
+// validity bit), or the query itself when it has no valid key at or before it
+__device__ __forceinline__ bool fa_vis(int q, int k, bool kv, int fv) {
+    return (k <= q) & (kv | ((k == q) & (q < fv)));
 }
-// branch-free visibility of key k for query q (q < L): causal, padding, self when q has no valid key
-__device__ __forceinline__ bool fa_vis(int q, int k, int L, int km, int fv) {
-    return (k <= q) & (k < L) & ((km != 0) | ((k == q) & (q < fv)));
-}
+// scores are carried in log2 units (scale * log2 e folded into one FMA before v_exp_f32)
+__device__ __forceinline__ float fa_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // rows [r0, r0 + 32) of a [L, D] slab (clamped) as the two 16-row A fragments of
 // one 32-row block: lane (g, c16) <- row r0 + 16 t + c16, dims 32 c + 8 g
@@ -259,6 +246,23 @@ __device__ __forceinline__ void fa_stage_store(const FaStage<D> &st, uint16_t *k
 }
 
 
+#ifndef SWH_FA_PD
+#define SWH_FA_PD 1  // 32-row K/V blocks in flight (registers) ahead of the computed one (2-4: more VGPRs, slower)
+#endif
+#ifndef SWH_FA_PR
+#define SWH_FA_PR 2  // dK/dV: rounds (2 x 32 queries) in flight ahead of the round being computed
+#endif
+
+// A 32-row block of two slabs on its way to LDS, with the key-mask entry of key
+// r0 + (lane & 31) (the forward / dQ walks): loads are issued SWH_FA_PD blocks
+// ahead of use, so neither the K/V bytes nor the mask word is waited on at the
+// block that needs them.
+template <int D>
+struct FaBlk {
+    FaStage<D> s;
+    int km;
+};
+
 #ifndef SWH_FA_FWD_QT
 #define SWH_FA_FWD_QT 1  // query tiles per wave in the forward (2: 125 vs 102 us at the bench shape)
 #endif
@@ -301,50 +305,77 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(FaArgs a) {
         for (int d = 0; d < DB; ++d) o[t][d] = f32x4a{0.f, 0.f, 0.f, 0.f};
     }
     const int kend = min(q0 + 16 * QT, L);  // causal: keys < kend
-    FaStage<D> st;
-    fa_stage_load<D>(st, kvrow, 0, L, tid, nthr);
-    fa_stage_store<D, VS>(st, kt[0], vt[0], tid, nthr);
+    const float sl2 = a.scale * kLog2e;
+    constexpr int PD = SWH_FA_PD;
+    const int nblk = (kend + 31) >> 5;
+    FaBlk<D> ring[PD];  // block j in ring[j % PD] from its load to its LDS store
+    auto load = [&](FaBlk<D> &r, int j) {
+        fa_stage_load<D>(r.s, kvrow, 32 * j, L, tid, nthr);
+        r.km = a.key_mask ? a.key_mask[(int64_t)b * L + min(32 * j + (lane & 31), L - 1)] : 1;
+    };
+    auto put = [&](const FaBlk<D> &r, int j) -> uint32_t {  // LDS buffer j & 1; the block's key-validity bits
+        fa_stage_store<D, VS>(r.s, kt[j & 1], vt[j & 1], tid, nthr);
+        return (uint32_t)__ballot((32 * j + (lane & 31) < L) & (r.km != 0));
+    };
+    load(ring[0], 0);
+    uint32_t vm = put(ring[0], 0);
+#pragma unroll
+    for (int u = 1; u <= PD; ++u)
+        if (u < nblk) load(ring[u % PD], u);
     __syncthreads();
-    int buf = 0;
-    for (int k0 = 0; k0 < kend; k0 += 32, buf ^= 1) {
-        const bool more = k0 + 32 < kend;
-        if (more) fa_stage_load<D>(st, kvrow, k0 + 32, L, tid, nthr);  // next block streams meanwhile
-        u32x4 kr[2][DC];
-        fa_rows_lds<D, VS>(kr, kt[buf], c16, g);
-        const FaKeyMask km = fa_key_mask(a, b, k0, g);
+    for (int j0 = 0; j0 < nblk; j0 += PD) {
 #pragma unroll
-        for (int t = 0; t < QT; ++t) {
-            const int qt0 = q0 + 16 * t;
-            if (k0 >= qt0 + 16) continue;  // wave-uniform: the whole block is in this tile's future
-            f32x4a sc[2];
-            fa_abt<D>(sc, kr, qf[t]);
-            float sv[8], mx = m[t];
+        for (int u = 0; u < PD; ++u) {
+            const int j = j0 + u, k0 = 32 * j, buf = j & 1;
+            if (j >= nblk) break;
+            u32x4 kr[2][DC];
+            fa_rows_lds<D, VS>(kr, kt[buf], c16, g);
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
+            for (int t = 0; t < QT; ++t) {
+                const int qt0 = q0 + 16 * t;
+                if (k0 >= qt0 + 16) continue;  // wave-uniform: the whole block is in this tile's future
+                f32x4a sc[2];
+                fa_abt<D>(sc, kr, qf[t]);
+                float sv[8];
+                if (k0 + 31 <= qt0 && vm == 0xffffffffu) {  // wave-uniform: every key seen by every query
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int key = k0 + 16 * u + 4 * g + r;
-                    const float v = fa_vis(qt0 + c16, key, L, km.v[4 * u + r], fv) ? sc[u][r] * a.scale : kNegInf;
-                    sv[4 * u + r] = v;
-                    mx = fmaxf(mx, v);
+                    for (int e = 0; e < 8; ++e) sv[e] = sc[e >> 2][e & 3];
+                } else {
+#pragma unroll
+                    for (int w = 0; w < 2; ++w)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int kb = 16 * w + 4 * g + r;
+                            sv[4 * w + r] = fa_vis(qt0 + c16, k0 + kb, (vm >> kb) & 1u, fv) ? sc[w][r] : kNegInf;
+                        }
                 }
-            mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
-            mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
-            const float corr = (mx == kNegInf) ? 1.f : __expf(m[t] - mx);
-            l[t] *= corr;
+                float bm = fmaxf(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])),
+                                 fmaxf(fmaxf(sv[4], sv[5]), fmaxf(sv[6], sv[7])));
+                bm = fmaxf(bm, __shfl_xor(bm, 16, kWave));
+                bm = fmaxf(bm, __shfl_xor(bm, 32, kWave));
+                const float mx = fmaxf(m[t], bm * sl2);  // log2 units
+                if (__ballot(mx > m[t])) {  // wave-uniform: rescale only when some query's maximum grew
+                    const float corr = mx > m[t] ? fa_exp2(m[t] - mx) : 1.f;
+                    l[t] *= corr;
 #pragma unroll
-            for (int d = 0; d < DB; ++d) o[t][d] *= corr;
-            m[t] = mx;
-            float p[8];
+                    for (int d = 0; d < DB; ++d) o[t][d] *= corr;
+                    m[t] = mx;
+                }
+                const float nmx = mx == kNegInf ? 0.f : -mx;  // masked scores are -inf: p = 0 either way
+                float p[8];
 #pragma unroll
-            for (int jj = 0; jj < 8; ++jj) {
-                p[jj] = (mx == kNegInf) ? 0.f : __expf(sv[jj] - mx);
-                l[t] += p[jj];
+                for (int e = 0; e < 8; ++e) p[e] = fa_exp2(fmaf(sv[e], sl2, nmx));
+                l[t] += ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
+                fa_xty_shared<D, VS>(o[t], vt[buf], p, c16, g);
             }
-            fa_xty_shared<D, VS>(o[t], vt[buf], p, c16, g);
+            uint32_t vn = 0;
+            if (j + 1 < nblk) {
+                vn = put(ring[(u + 1) % PD], j + 1);
+                if (j + 1 + PD < nblk) load(ring[(u + 1) % PD], j + 1 + PD);
+            }
+            __syncthreads();
+            vm = vn;
         }
-        if (more) fa_stage_store<D, VS>(st, kt[buf ^ 1], vt[buf ^ 1], tid, nthr);
-        __syncthreads();
     }
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
@@ -363,7 +394,7 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(FaArgs a) {
                                     ((uint32_t)f32_to_bf16_bits(o[t][d][3] * inv) << 16);
                 *reinterpret_cast<uint2 *>(ob + d * 16 + 4 * g) = uint2{lo, hi};
             }
-            if (g == 0) a.lse[((int64_t)b * a.Hq + h) * L + q] = m[t] + logf(lt);
+            if (g == 0) a.lse[((int64_t)b * a.Hq + h) * L + q] = (m[t] + __log2f(lt)) * kLn2;
         }
     }
 }
@@ -418,38 +449,65 @@ __global__ __launch_bounds__(512) void fa_dq_kernel(FaArgs a) {
             df[c] = *reinterpret_cast<const u32x4 *>(dr_ + c * 32 + g * 8);
         }
     }
-    const float lse = a.lse[qrow + qc], dl = a.delta[qrow + qc];
+    const float sl2 = a.scale * kLog2e, nlse2 = -a.lse[qrow + qc] * kLog2e, dl = a.delta[qrow + qc];
     f32x4a acc[DB];
 #pragma unroll
     for (int d = 0; d < DB; ++d) acc[d] = f32x4a{0.f, 0.f, 0.f, 0.f};
     const int kend = min(q0 + 16, L);
-    FaStage<D> st;
-    fa_stage_load<D>(st, kvrow, 0, L, tid, nthr);
-    fa_stage_store<D, VS>(st, kt[0], vt[0], tid, nthr);
+    constexpr int PD = SWH_FA_PD;
+    const int nblk = (kend + 31) >> 5;
+    FaBlk<D> ring[PD];  // block j in ring[j % PD] from its load to its LDS store
+    auto load = [&](FaBlk<D> &r, int j) {
+        fa_stage_load<D>(r.s, kvrow, 32 * j, L, tid, nthr);
+        r.km = a.key_mask ? a.key_mask[(int64_t)b * L + min(32 * j + (lane & 31), L - 1)] : 1;
+    };
+    auto put = [&](const FaBlk<D> &r, int j) -> uint32_t {
+        fa_stage_store<D, VS>(r.s, kt[j & 1], vt[j & 1], tid, nthr);
+        return (uint32_t)__ballot((32 * j + (lane & 31) < L) & (r.km != 0));
+    };
+    load(ring[0], 0);
+    uint32_t vm = put(ring[0], 0);
+#pragma unroll
+    for (int u = 1; u <= PD; ++u)
+        if (u < nblk) load(ring[u % PD], u);
     __syncthreads();
-    int buf = 0;
-    for (int k0 = 0; k0 < kend; k0 += 32, buf ^= 1) {
-        const bool more = k0 + 32 < kend;
-        if (more) fa_stage_load<D>(st, kvrow, k0 + 32, L, tid, nthr);
-        u32x4 kr[2][DC], vr[2][DC];
-        fa_rows_lds<D, VS>(kr, kt[buf], c16, g);
-        fa_rows_lds<D, VS>(vr, vt[buf], c16, g);
-        f32x4a s[2], dp[2];
-        fa_abt<D>(s, kr, qf);
-        fa_abt<D>(dp, vr, df);
-        const FaKeyMask km = fa_key_mask(a, b, k0, g);
-        float ds[8];
+    for (int j0 = 0; j0 < nblk; j0 += PD) {
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int u = 0; u < PD; ++u) {
+            const int j = j0 + u, k0 = 32 * j, buf = j & 1;
+            if (j >= nblk) break;
+            u32x4 kr[2][DC], vr[2][DC];
+            fa_rows_lds<D, VS>(kr, kt[buf], c16, g);
+            fa_rows_lds<D, VS>(vr, vt[buf], c16, g);
+            f32x4a s[2], dp[2];
+            fa_abt<D>(s, kr, qf);
+            fa_abt<D>(dp, vr, df);
+            float ds[8];
+            if (k0 + 31 <= q0 && vm == 0xffffffffu) {  // wave-uniform: every key seen by every query
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int key = k0 + 16 * t + 4 * g + r;
-                const float p = fa_vis(q0 + c16, key, L, km.v[4 * t + r], fv) ? __expf(s[t][r] * a.scale - lse) : 0.f;
-                ds[4 * t + r] = p * (dp[t][r] - dl);
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) ds[4 * t + r] = fa_exp2(fmaf(s[t][r], sl2, nlse2)) * (dp[t][r] - dl);
+            } else {
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int kb = 16 * t + 4 * g + r;
+                        const float p =
+                            fa_vis(q0 + c16, k0 + kb, (vm >> kb) & 1u, fv) ? fa_exp2(fmaf(s[t][r], sl2, nlse2)) : 0.f;
+                        ds[4 * t + r] = p * (dp[t][r] - dl);
+                    }
             }
-        fa_xty_shared<D, VS>(acc, kt[buf], ds, c16, g);
-        if (more) fa_stage_store<D, VS>(st, kt[buf ^ 1], vt[buf ^ 1], tid, nthr);
-        __syncthreads();
+            fa_xty_shared<D, VS>(acc, kt[buf], ds, c16, g);
+            uint32_t vn = 0;
+            if (j + 1 < nblk) {
+                vn = put(ring[(u + 1) % PD], j + 1);
+                if (j + 1 + PD < nblk) load(ring[(u + 1) % PD], j + 1 + PD);
+            }
+            __syncthreads();
+            vm = vn;
+        }
     }
     if (active && q0 + c16 < L && fa_qlive(a, b, q0 + c16)) {
         uint16_t *qb = fa_row(a.dq, a.P, b, h, q0 + c16);
@@ -474,14 +532,16 @@ __global__ __launch_bounds__(256) void fa_dkdv_kernel(FaArgs a) {
     constexpr int DC = D / 32, DB = D / 16, VS = fa_vs<D>();
     constexpr int R = 2;  // 32-query sub-blocks per round: more work per barrier / prefetch
     __shared__ __attribute__((aligned(16))) uint16_t qt[2][R][32 * VS], dt[2][R][32 * VS];
-    __shared__ float lse_s[2][32 * R], del_s[2][32 * R];
+    __shared__ __attribute__((aligned(16))) float lse_s[2][32 * R], del_s[2][32 * R];  // lse_s: -lse log2 e
     const int tid = threadIdx.x, nthr = blockDim.x;
     const int lane = tid & 63, wid = tid >> 6, g = lane >> 4, c16 = lane & 15;
     const int b = blockIdx.z, kvh = blockIdx.y, L = a.L, G = a.Hq / a.Hkv;
     const int kb0 = blockIdx.x * 64, k0w = kb0 + wid * 16;
     const int kc = min(k0w + c16, L - 1);  // this lane's key column
     const int fv = a.first_valid ? a.first_valid[b] : 0;
-    const int kmv = a.key_mask ? a.key_mask[(int64_t)b * L + kc] : 1;
+    const bool kmv = (k0w + c16 < L) && (!a.key_mask || a.key_mask[(int64_t)b * L + kc] != 0);
+    const bool kall = __ballot(kmv) == ~0ull;  // every key of the wave inside the sequence and unpadded
+    const float sl2 = a.scale * kLog2e;
     u32x4 kf[DC], vf[DC];
     {
         const uint16_t *kr_ = fa_row(a.k, a.P, b, kvh, kc), *vr_ = fa_row(a.v, a.P, b, kvh, kc);
@@ -505,9 +565,16 @@ __global__ __launch_bounds__(256) void fa_dkdv_kernel(FaArgs a) {
         r0 = qstart + 32 * R * (it % nb);
         qrow = ((int64_t)b * a.Hq + kvh * G + it / nb) * L;
     };
-    FaStage<D> st[R];
+    // a round's Q / dO blocks and its rows' lse (threads < 32 R) or delta (< 64 R), in
+    // registers from load to LDS store; SWH_FA_PR rounds in flight ahead of the computed one
+    struct Round {
+        FaStage<D> st[R];
+        float sd;
+    };
+    constexpr int PR = SWH_FA_PR;
+    Round ring[PR];  // round it in ring[it % PR]
     const FaRows qr_b = fa_rows(a.q, a.P, b), dr_b = fa_rows(a.dout, a.P, b);
-    auto load = [&](int it) {
+    auto load = [&](Round &rd, int it) {
         int64_t qrow;
         int r0;
         rows_of(it, qrow, r0);
@@ -516,26 +583,29 @@ __global__ __launch_bounds__(256) void fa_dkdv_kernel(FaArgs a) {
             return which ? dr_b.row(hq, row) : qr_b.row(hq, row);
         };
 #pragma unroll
-        for (int h = 0; h < R; ++h) fa_stage_load<D>(st[h], qdrow, r0 + 32 * h, L, tid, nthr);
+        for (int h = 0; h < R; ++h) fa_stage_load<D>(rd.st[h], qdrow, r0 + 32 * h, L, tid, nthr);
+        if (tid < 32 * R) rd.sd = a.lse[qrow + min(r0 + tid, L - 1)];
+        else if (tid < 64 * R) rd.sd = a.delta[qrow + min(r0 + tid - 32 * R, L - 1)];
     };
-    auto store = [&](int it, int buf) {  // staged blocks + the rows' lse / delta into LDS
-        int64_t qrow;
-        int r0;
-        rows_of(it, qrow, r0);
+    auto store = [&](const Round &rd, int buf) {  // staged blocks + the rows' -lse log2 e / delta into LDS
 #pragma unroll
-        for (int h = 0; h < R; ++h) fa_stage_store<D, VS>(st[h], qt[buf][h], dt[buf][h], tid, nthr);
-        if (tid < 32 * R) lse_s[buf][tid] = a.lse[qrow + min(r0 + tid, L - 1)];
-        else if (tid < 64 * R) del_s[buf][tid - 32 * R] = a.delta[qrow + min(r0 + tid - 32 * R, L - 1)];
+        for (int h = 0; h < R; ++h) fa_stage_store<D, VS>(rd.st[h], qt[buf][h], dt[buf][h], tid, nthr);
+        if (tid < 32 * R) lse_s[buf][tid] = -rd.sd * kLog2e;
+        else if (tid < 64 * R) del_s[buf][tid - 32 * R] = rd.sd;
     };
     if (nit) {
-        load(0);
-        store(0, 0);
+        load(ring[0], 0);
+        store(ring[0], 0);
     }
+#pragma unroll
+    for (int u = 1; u <= PR; ++u)
+        if (u < nit) load(ring[u % PR], u);
     __syncthreads();
-    int buf = 0;
-    for (int it = 0; it < nit; ++it, buf ^= 1) {
-        const bool more = it + 1 < nit;
-        if (more) load(it + 1);  // the next round's Q / dO blocks stream while this one computes
+    for (int it0 = 0; it0 < nit; it0 += PR) {
+#pragma unroll
+    for (int u = 0; u < PR; ++u) {
+        const int it = it0 + u, buf = it & 1;
+        if (it >= nit) break;
         const int r0 = qstart + 32 * R * (it % nb);
 #pragma unroll
         for (int h = 0; h < R; ++h) {
@@ -548,22 +618,36 @@ __global__ __launch_bounds__(256) void fa_dkdv_kernel(FaArgs a) {
                 fa_abt<D>(s, qr, kf);   // S[q = rh + 16 t + 4 g + r][key c16]
                 fa_abt<D>(dp, dr, vf);  // dP likewise
                 float p[8], ds[8];
+                const bool full = rh >= k0w + 15 && rh + 31 < L && kall;  // wave-uniform
 #pragma unroll
-                for (int t = 0; t < 2; ++t)
+                for (int t = 0; t < 2; ++t) {
+                    const float4 nl = *reinterpret_cast<const float4 *>(&lse_s[buf][32 * h + 16 * t + 4 * g]);
+                    const float4 de = *reinterpret_cast<const float4 *>(&del_s[buf][32 * h + 16 * t + 4 * g]);
+                    const float nlv[4] = {nl.x, nl.y, nl.z, nl.w}, dev[4] = {de.x, de.y, de.z, de.w};
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const int qi = 32 * h + 16 * t + 4 * g + r, q = r0 + qi;
-                        const bool vis = (q < L) & fa_vis(q, k0w + c16, L, kmv, fv) & fa_qlive(a, b, q);
-                        const float pv = vis ? __expf(s[t][r] * a.scale - lse_s[buf][qi]) : 0.f;
-                        p[4 * t + r] = pv;
-                        ds[4 * t + r] = vis ? pv * (dp[t][r] - del_s[buf][qi]) : 0.f;
+                        const float e = fa_exp2(fmaf(s[t][r], sl2, nlv[r]));
+                        if (full) {
+                            p[4 * t + r] = e;
+                            ds[4 * t + r] = e * (dp[t][r] - dev[r]);
+                        } else {
+                            const int q = rh + 16 * t + 4 * g + r;
+                            const bool vis = (q < L) & fa_vis(q, k0w + c16, kmv, fv) & fa_qlive(a, b, q);
+                            p[4 * t + r] = vis ? e : 0.f;
+                            ds[4 * t + r] = vis ? e * (dp[t][r] - dev[r]) : 0.f;
+                        }
                     }
+                }
                 fa_xty_shared<D, VS>(dv, dt[buf][h], p, c16, g);
                 fa_xty_shared<D, VS>(dk, qt[buf][h], ds, c16, g);
             }
         }
-        if (more) store(it + 1, buf ^ 1);
+        if (it + 1 < nit) {
+            store(ring[(u + 1) % PR], (it + 1) & 1);
+            if (it + 1 + PR < nit) load(ring[(u + 1) % PR], it + 1 + PR);
+        }
         __syncthreads();
+    }
     }
     if (k0w + c16 < L) {
         uint16_t *kb = fa_row(a.dk, a.P, b, kvh, k0w + c16);

@@ -153,9 +153,11 @@ def _train_and_capture(tr):
     return got
 
 
-def _expected_scores(rm, tok, got, dev):
-    texts = [x["prompt"] + c for x, c in zip(got["examples"], tok.batch_decode(got["ids"], skip_special_tokens=True))]
-    enc = tok(text=texts, return_tensors="pt", padding=True, padding_side="right", add_special_tokens=False)
+def _expected_scores(rm, ptok, rtok, got, dev):
+    """The reference's scores: completions decoded by the policy tokenizer, the
+    texts encoded by the reward model's own."""
+    texts = [x["prompt"] + c for x, c in zip(got["examples"], ptok.batch_decode(got["ids"], skip_special_tokens=True))]
+    enc = rtok(text=texts, return_tensors="pt", padding=True, padding_side="right", add_special_tokens=False)
     with torch.inference_mode():
         return rm(**{k: v.to(dev) for k, v in enc.items()}).logits[:, 0].float().cpu()
 
@@ -217,7 +219,7 @@ def test_string_reward_model_loads_from_local_directory(tmp_path):
     got = _train_and_capture(tr)
     rm = AutoModelForSequenceClassification.from_pretrained(str(d), num_labels=1, dtype=torch.float32).to(dev).eval()
     rm.config.pad_token_id = rtok.pad_token_id
-    torch.testing.assert_close(got["rpf"][:, 0], _expected_scores(rm, rtok, got, dev), **RM_TOL)
+    torch.testing.assert_close(got["rpf"][:, 0], _expected_scores(rm, tok, rtok, got, dev), **RM_TOL)
     assert any("rewards/my-reward-model/mean" in h for h in tr.state.log_history)
     with pytest.raises(ValueError, match="not a local directory"):
         GRPOTrainer(model=_cfg(), reward_funcs="org/some-hub-model", args=args, train_dataset=_text_dataset(),
@@ -254,7 +256,7 @@ def test_module_reward_model_pads_with_eos_and_is_named_by_path(tmp_path):
     assert rtok is nopad and rtok.pad_token == "[EOS]" and rtok.pad_token_id == 1
     assert rm.config.pad_token_id == 1 and tr.reward_func_names == ["rm-nopad"]
     got = _train_and_capture(tr)
-    torch.testing.assert_close(got["rpf"][:, 0], _expected_scores(rm, rtok, got, dev), **RM_TOL)
+    torch.testing.assert_close(got["rpf"][:, 0], _expected_scores(rm, tok, rtok, got, dev), **RM_TOL)
     with pytest.raises(ValueError, match="number of reward processing classes"):
         GRPOTrainer(model=_cfg(), reward_funcs=[rm], args=args, train_dataset=_text_dataset(),
                     processing_class=tok, reward_processing_classes=[tok, tok])

@@ -1,72 +1,82 @@
-"""Training-attention timing at the GRPO scoring shape (B=64, 14/2 heads,
-L=384, D=64, causal, bf16): torch SDPA backends and GQA handling, forward
-and forward+backward.  Tuning aid.   python tools/bench_attn.py
+"""Training attention at the bench shape (tuning aid, not part of the product):
+the GRPO shared-prompt layout of config 2 — 8 groups x G 8, prompt 128 (left
+padded) + completion 256, 14 / 2 heads x 64 — forward and backward through
+nn_ops.GroupedAttentionFn, timed with events over graph-free repetitions.
+Run under rocprofv3 --kernel-trace --stats for the per-kernel split.
+
+    python tools/bench_attn.py [--reps 20]
 """
+import argparse
+import os
+import sys
+
 import torch
-import torch.nn.functional as F
-from torch.nn.attention import SDPBackend, sdpa_kernel
 
-
-def timeit(fn, it=10):
-    fn()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(it):
-        fn()
-    e1.record()
-    e1.synchronize()
-    return e0.elapsed_time(e1) / it
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--groups", type=int, default=8)
+    ap.add_argument("--G", type=int, default=8)
+    ap.add_argument("--P", type=int, default=128)
+    ap.add_argument("--C", type=int, default=256)
+    ap.add_argument("--D", type=int, default=64)
+    ap.add_argument("--hq", type=int, default=14)
+    ap.add_argument("--hkv", type=int, default=2)
+    a = ap.parse_args()
+    from swh_trl_amd import _lib, nn_ops
+    _lib.load()
     dev = torch.device("cuda:0")
-    B, Hq, Hkv, L, D = 64, 14, 2, 384, 64
-    q = torch.randn(B, Hq, L, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
-    k = torch.randn(B, Hkv, L, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
-    v = torch.randn(B, Hkv, L, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
-    do = torch.randn(B, Hq, L, D, device=dev, dtype=torch.bfloat16)
-    mask = torch.ones(L, L, device=dev, dtype=torch.bool).tril()[None, None].expand(B, 1, L, L)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    U, G, P, C, D = a.groups, a.G, a.P, a.C, a.D
+    R, L = U * G, a.P + a.C
 
-    def run(backend, gqa, use_mask, bwd):
-        def f():
-            kk, vv = (k, v) if gqa else (k.repeat_interleave(Hq // Hkv, 1), v.repeat_interleave(Hq // Hkv, 1))
-            ctx = sdpa_kernel([backend]) if backend is not None else torch.enable_grad()
-            with ctx:
-                if use_mask:
-                    o = F.scaled_dot_product_attention(q, kk, vv, attn_mask=mask, scale=D ** -0.5, enable_gqa=gqa)
-                else:
-                    o = F.scaled_dot_product_attention(q, kk, vv, is_causal=True, scale=D ** -0.5, enable_gqa=gqa)
-            if bwd:
-                o.backward(do)
-        return f
+    def t(*shape):
+        return (torch.randn(*shape, generator=g) * 0.5).to(dev, torch.bfloat16).requires_grad_(True)
+    q_p, k_p, v_p = t(U, a.hq, P, D), t(U, a.hkv, P, D), t(U, a.hkv, P, D)
+    q_c, k_c, v_c = t(R, a.hq, C, D), t(R, a.hkv, C, D), t(R, a.hkv, C, D)
+    pad = torch.randint(0, P // 4, (U,), generator=g).repeat_interleave(G)  # left padding per group
+    km = (torch.arange(L)[None] >= pad[:, None]).int()
+    ends = torch.randint(C // 2, C + 1, (R,), generator=g)  # right padding after each row's end
+    km[:, P:] &= (torch.arange(C)[None] < ends[:, None]).int()
+    fv = pad.int()
+    km, fv = km.to(dev), fv.to(dev)
+    scale = D ** -0.5
+    dout = torch.randn(U * P + R * C, a.hq * D, generator=g).to(dev, torch.bfloat16)
+    fn = nn_ops.GroupedAttentionFn.apply
 
-    import os
-    import sys
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    from swh_trl_amd import nn_ops
+    def fwd():
+        return fn(q_p, k_p, v_p, q_c, k_c, v_c, G, scale, km, fv)
 
-    def hip(bwd):
-        def f():
-            o = nn_ops.AttentionFn.apply(q, k, v, D ** -0.5, None, None)
-            if bwd:
-                o.backward(do)
-        return f
-    print(f"hip (csrc/attn.hip)     fwd {timeit(hip(False)) * 1000:8.1f} us  fwd+bwd {timeit(hip(True)) * 1000:8.1f} us",
-          flush=True)
-    if os.environ.get("HIP_ONLY"):
-        return
-    for name, be in (("default", None), ("flash", SDPBackend.FLASH_ATTENTION),
-                     ("efficient", SDPBackend.EFFICIENT_ATTENTION), ("math", SDPBackend.MATH)):
-        for gqa in (True, False):
-            for use_mask in (False, True):
-                try:
-                    tf = timeit(run(be, gqa, use_mask, False))
-                    tb = timeit(run(be, gqa, use_mask, True))
-                    print(f"{name:9s} gqa={int(gqa)} mask={int(use_mask)}  fwd {tf * 1000:8.1f} us  fwd+bwd {tb * 1000:8.1f} us",
-                          flush=True)
-                except Exception as e:  # backend refuses the combination
-                    print(f"{name:9s} gqa={int(gqa)} mask={int(use_mask)}  n/a ({type(e).__name__})", flush=True)
+    def step():
+        out = fwd()
+        torch.autograd.grad(out, (q_p, k_p, v_p, q_c, k_c, v_c), dout)
+
+    for f in (fwd, step):
+        f()
+    torch.cuda.synchronize()
+    res = {}
+    for name, f in (("forward", fwd), ("forward+backward", step)):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.reps):
+            f()
+        e1.record()
+        e1.synchronize()
+        res[name] = 1000 * e0.elapsed_time(e1) / a.reps
+    flops_fwd = 0
+    for r in range(R):
+        for qi in range(L):
+            if r % G and qi < P:
+                continue
+            flops_fwd += 4 * D * (qi + 1)
+    flops_fwd *= a.hq
+    print(f"R {R} L {L} (P {P} + C {C}) heads {a.hq}/{a.hkv} D {D}: forward {res['forward']:.1f} us "
+          f"({flops_fwd / res['forward'] / 1e6:.1f} TF/s causal), forward+backward {res['forward+backward']:.1f} us "
+          f"(backward {res['forward+backward'] - res['forward']:.1f} us, "
+          f"{2.5 * flops_fwd / (res['forward+backward'] - res['forward']) / 1e6:.1f} TF/s)", flush=True)
 
 
 if __name__ == "__main__":

@@ -18,13 +18,13 @@ import sys
 
 
 def family(name: str) -> str:
-    n = name.split("(")[0]
+    n = re.sub(r"\(anonymous namespace\)::", "", name)
+    n = re.sub(r"^void ", "", n).split("(")[0]
     if n.startswith(("Cijk", "Custom_Cijk")):
         m = re.search(r"MT(\d+x\d+x\d+)", n)
         return "GEMM " + (m.group(1) if m else "")
-    n = re.sub(r"^void ", "", n)
-    n = re.sub(r"swh::\(anonymous namespace\)::", "", n)
-    n = re.sub(r"at::native::(\(anonymous namespace\)::)?", "aten::", n)
+    n = re.sub(r"^swh::", "", n)
+    n = re.sub(r"^at::native::", "aten::", n)
     return n[:60]
 
 

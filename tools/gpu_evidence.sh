@@ -64,7 +64,8 @@ for step in "$@"; do
       rm -rf /tmp/trace_$tag
       timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d /tmp/trace_$tag -o run \
         -- python3 tools/train_kernels.py --reps 1 > $O/${tag}_trace.log 2>&1 || fail trace $? $O/${tag}_trace.log
-      python tools/critical_path.py "$(find /tmp/trace_$tag -name '*kernel_trace.csv' | head -1)" 150 \
+      cp "$(find /tmp/trace_$tag -name '*kernel_trace.csv' | head -1)" $O/${tag}_train_trace.csv
+      python tools/critical_path.py $O/${tag}_train_trace.csv 150 \
         > $O/${tag}_critical_path.txt 2>&1 || fail critical_path $? $O/${tag}_critical_path.txt
       head -40 $O/${tag}_critical_path.txt ;;
     ppo)
