@@ -300,7 +300,9 @@ int swh_rmsnorm_bwd(const void *x, const void *weight, const float *rstd, const 
  * branch; dx = bf16(bf16(norm backward) + dres), the sum autograd forms where
  * the residual stream forks into the next RMSNorm.  swh_rmsnorm_dw_accum folds
  * the partial weight-gradient column sums into the bf16 gradient view:
- * grad_w = bf16(grad_w + bf16(sum over blocks)) (f32: grad_w += sum). */
+ * grad_w = bf16(grad_w + bf16(sum over blocks)) (f32: grad_w += sum), in a fixed
+ * order; above 64 partial rows it sums ranges of 32 rows first and uses
+ * dw_partial as scratch (each range's first row is overwritten). */
 int swh_rmsnorm_dw_accum(const float *dw_partial, int64_t nblocks, int64_t H, void *grad_w, int32_t dtype,
                          void *stream);
 /* Column sums of x [rows, cols] (`dtype` bf16/f32, cols % 8 (bf16) / 4 (f32) == 0)

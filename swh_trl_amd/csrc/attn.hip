@@ -108,6 +108,24 @@ __device__ __forceinline__ bool fa_qlive(const FaArgs &a, int b, int q) { return
 __device__ __forceinline__ bool fa_vis(int q, int k, bool kv, int fv) {
     return (k <= q) & (kv | ((k == q) & (q < fv)));
 }
+// The key-validity words of blocks 0 .. nblk - 1 of sequence b into LDS (nblk <= kFaMaskWords),
+// one wave per word: the walk then reads its block's word from LDS instead of waiting on
+// a mask load per block.  Visible after the caller's next __syncthreads.
+constexpr int kFaMaskWords = 64;  // keys < 2048; longer walks ballot per block (fa_block_bits)
+__device__ __forceinline__ uint32_t fa_block_bits(const FaArgs &a, int b, int j, int lane) {
+    const int k = 32 * j + (lane & 31);
+    const bool v = (k < a.L) && (!a.key_mask || a.key_mask[(int64_t)b * a.L + min(k, a.L - 1)] != 0);
+    return (uint32_t)__ballot(v);
+}
+__device__ __forceinline__ void fa_mask_words(const FaArgs &a, int b, int nblk, uint32_t *words, int wid, int nw,
+                                              int lane) {
+    if (nblk > kFaMaskWords) return;
+    for (int j = wid; j < nblk; j += nw) {
+        const uint32_t m = fa_block_bits(a, b, j, lane);
+        if (lane == 0) words[j] = m;
+    }
+}
+
 // scores are carried in log2 units (scale * log2 e folded into one FMA before v_exp_f32)
 __device__ __forceinline__ float fa_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
@@ -223,12 +241,13 @@ template <int D, typename RowP>
 __device__ __forceinline__ void fa_stage_load(FaStage<D> &st, RowP rowp, int r0, int L, int tid, int nthr) {
 #pragma unroll
     for (int j = 0; j < FaStage<D>::kPer; ++j) {
-        const int pc = tid + j * nthr;
-        if (pc < FaStage<D>::kPieces) {
-            const int which = pc / (32 * D / 8), rem = pc - which * (32 * D / 8);
-            const int row = rem / (D / 8), col = rem - row * (D / 8);
-            st.v[j] = *reinterpret_cast<const u32x4 *>(rowp(which, min(r0 + row, L - 1)) + col * 8);
-        }
+        // every lane loads (surplus pieces repeat the last one and are not stored): no
+        // lane-divergent branch around a load, so the compiler's vmcnt waits stay counted
+        // instead of draining every load in flight
+        const int pc = min(tid + j * nthr, FaStage<D>::kPieces - 1);
+        const int which = pc / (32 * D / 8), rem = pc - which * (32 * D / 8);
+        const int row = rem / (D / 8), col = rem - row * (D / 8);
+        st.v[j] = *reinterpret_cast<const u32x4 *>(rowp(which, min(r0 + row, L - 1)) + col * 8);
     }
 }
 template <int D, int VS>
@@ -252,16 +271,6 @@ __device__ __forceinline__ void fa_stage_store(const FaStage<D> &st, uint16_t *k
 #ifndef SWH_FA_PR
 #define SWH_FA_PR 2  // dK/dV: rounds (2 x 32 queries) in flight ahead of the round being computed
 #endif
-
-// A 32-row block of two slabs on its way to LDS, with the key-mask entry of key
-// r0 + (lane & 31) (the forward / dQ walks): loads are issued SWH_FA_PD blocks
-// ahead of use, so neither the K/V bytes nor the mask word is waited on at the
-// block that needs them.
-template <int D>
-struct FaBlk {
-    FaStage<D> s;
-    int km;
-};
 
 #ifndef SWH_FA_FWD_QT
 #define SWH_FA_FWD_QT 1  // query tiles per wave in the forward (2: 125 vs 102 us at the bench shape)
@@ -308,26 +317,22 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(FaArgs a) {
     const float sl2 = a.scale * kLog2e;
     constexpr int PD = SWH_FA_PD;
     const int nblk = (kend + 31) >> 5;
-    FaBlk<D> ring[PD];  // block j in ring[j % PD] from its load to its LDS store
-    auto load = [&](FaBlk<D> &r, int j) {
-        fa_stage_load<D>(r.s, kvrow, 32 * j, L, tid, nthr);
-        r.km = a.key_mask ? a.key_mask[(int64_t)b * L + min(32 * j + (lane & 31), L - 1)] : 1;
-    };
-    auto put = [&](const FaBlk<D> &r, int j) -> uint32_t {  // LDS buffer j & 1; the block's key-validity bits
-        fa_stage_store<D, VS>(r.s, kt[j & 1], vt[j & 1], tid, nthr);
-        return (uint32_t)__ballot((32 * j + (lane & 31) < L) & (r.km != 0));
-    };
+    FaStage<D> ring[PD];  // K/V block j in ring[j % PD] from its load to its LDS store, PD blocks ahead
+    __shared__ uint32_t kvw[kFaMaskWords];
+    fa_mask_words(a, b, nblk, kvw, wid, nthr >> 6, lane);
+    auto load = [&](FaStage<D> &r, int j) { fa_stage_load<D>(r, kvrow, 32 * j, L, tid, nthr); };
+    auto put = [&](const FaStage<D> &r, int j) { fa_stage_store<D, VS>(r, kt[j & 1], vt[j & 1], tid, nthr); };
     load(ring[0], 0);
-    uint32_t vm = put(ring[0], 0);
+    put(ring[0], 0);
 #pragma unroll
-    for (int u = 1; u <= PD; ++u)
-        if (u < nblk) load(ring[u % PD], u);
+    for (int u = 1; u <= PD; ++u) load(ring[u % PD], min(u, nblk - 1));  // past the end: repeats, never stored
     __syncthreads();
     for (int j0 = 0; j0 < nblk; j0 += PD) {
 #pragma unroll
         for (int u = 0; u < PD; ++u) {
             const int j = j0 + u, k0 = 32 * j, buf = j & 1;
             if (j >= nblk) break;
+            const uint32_t vm = nblk <= kFaMaskWords ? __builtin_amdgcn_readfirstlane(kvw[j]) : fa_block_bits(a, b, j, lane);
             u32x4 kr[2][DC];
             fa_rows_lds<D, VS>(kr, kt[buf], c16, g);
 #pragma unroll
@@ -368,13 +373,9 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(FaArgs a) {
                 l[t] += ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
                 fa_xty_shared<D, VS>(o[t], vt[buf], p, c16, g);
             }
-            uint32_t vn = 0;
-            if (j + 1 < nblk) {
-                vn = put(ring[(u + 1) % PD], j + 1);
-                if (j + 1 + PD < nblk) load(ring[(u + 1) % PD], j + 1 + PD);
-            }
+            if (j + 1 < nblk) put(ring[(u + 1) % PD], j + 1);
+            load(ring[(u + 1) % PD], min(j + 1 + PD, nblk - 1));
             __syncthreads();
-            vm = vn;
         }
     }
 #pragma unroll
@@ -456,26 +457,22 @@ __global__ __launch_bounds__(512) void fa_dq_kernel(FaArgs a) {
     const int kend = min(q0 + 16, L);
     constexpr int PD = SWH_FA_PD;
     const int nblk = (kend + 31) >> 5;
-    FaBlk<D> ring[PD];  // block j in ring[j % PD] from its load to its LDS store
-    auto load = [&](FaBlk<D> &r, int j) {
-        fa_stage_load<D>(r.s, kvrow, 32 * j, L, tid, nthr);
-        r.km = a.key_mask ? a.key_mask[(int64_t)b * L + min(32 * j + (lane & 31), L - 1)] : 1;
-    };
-    auto put = [&](const FaBlk<D> &r, int j) -> uint32_t {
-        fa_stage_store<D, VS>(r.s, kt[j & 1], vt[j & 1], tid, nthr);
-        return (uint32_t)__ballot((32 * j + (lane & 31) < L) & (r.km != 0));
-    };
+    FaStage<D> ring[PD];  // K/V block j in ring[j % PD] from its load to its LDS store, PD blocks ahead
+    __shared__ uint32_t kvw[kFaMaskWords];
+    fa_mask_words(a, b, nblk, kvw, wid, nthr >> 6, lane);
+    auto load = [&](FaStage<D> &r, int j) { fa_stage_load<D>(r, kvrow, 32 * j, L, tid, nthr); };
+    auto put = [&](const FaStage<D> &r, int j) { fa_stage_store<D, VS>(r, kt[j & 1], vt[j & 1], tid, nthr); };
     load(ring[0], 0);
-    uint32_t vm = put(ring[0], 0);
+    put(ring[0], 0);
 #pragma unroll
-    for (int u = 1; u <= PD; ++u)
-        if (u < nblk) load(ring[u % PD], u);
+    for (int u = 1; u <= PD; ++u) load(ring[u % PD], min(u, nblk - 1));  // past the end: repeats, never stored
     __syncthreads();
     for (int j0 = 0; j0 < nblk; j0 += PD) {
 #pragma unroll
         for (int u = 0; u < PD; ++u) {
             const int j = j0 + u, k0 = 32 * j, buf = j & 1;
             if (j >= nblk) break;
+            const uint32_t vm = nblk <= kFaMaskWords ? __builtin_amdgcn_readfirstlane(kvw[j]) : fa_block_bits(a, b, j, lane);
             u32x4 kr[2][DC], vr[2][DC];
             fa_rows_lds<D, VS>(kr, kt[buf], c16, g);
             fa_rows_lds<D, VS>(vr, vt[buf], c16, g);
@@ -500,13 +497,9 @@ __global__ __launch_bounds__(512) void fa_dq_kernel(FaArgs a) {
                     }
             }
             fa_xty_shared<D, VS>(acc, kt[buf], ds, c16, g);
-            uint32_t vn = 0;
-            if (j + 1 < nblk) {
-                vn = put(ring[(u + 1) % PD], j + 1);
-                if (j + 1 + PD < nblk) load(ring[(u + 1) % PD], j + 1 + PD);
-            }
+            if (j + 1 < nblk) put(ring[(u + 1) % PD], j + 1);
+            load(ring[(u + 1) % PD], min(j + 1 + PD, nblk - 1));
             __syncthreads();
-            vm = vn;
         }
     }
     if (active && q0 + c16 < L && fa_qlive(a, b, q0 + c16)) {
@@ -584,8 +577,8 @@ __global__ __launch_bounds__(256) void fa_dkdv_kernel(FaArgs a) {
         };
 #pragma unroll
         for (int h = 0; h < R; ++h) fa_stage_load<D>(rd.st[h], qdrow, r0 + 32 * h, L, tid, nthr);
-        if (tid < 32 * R) rd.sd = a.lse[qrow + min(r0 + tid, L - 1)];
-        else if (tid < 64 * R) rd.sd = a.delta[qrow + min(r0 + tid - 32 * R, L - 1)];
+        const int si = tid < 32 * R ? tid : min(tid - 32 * R, 32 * R - 1);  // every lane loads (see fa_stage_load)
+        rd.sd = (tid < 32 * R ? a.lse : a.delta)[qrow + min(r0 + si, L - 1)];
     };
     auto store = [&](const Round &rd, int buf) {  // staged blocks + the rows' -lse log2 e / delta into LDS
 #pragma unroll
@@ -598,8 +591,7 @@ __global__ __launch_bounds__(256) void fa_dkdv_kernel(FaArgs a) {
         store(ring[0], 0);
     }
 #pragma unroll
-    for (int u = 1; u <= PR; ++u)
-        if (u < nit) load(ring[u % PR], u);
+    for (int u = 1; u <= PR; ++u) load(ring[u % PR], min(u, max(nit - 1, 0)));  // past the end: repeats
     __syncthreads();
     for (int it0 = 0; it0 < nit; it0 += PR) {
 #pragma unroll
@@ -642,10 +634,8 @@ __global__ __launch_bounds__(256) void fa_dkdv_kernel(FaArgs a) {
                 fa_xty_shared<D, VS>(dk, qt[buf][h], ds, c16, g);
             }
         }
-        if (it + 1 < nit) {
-            store(ring[(u + 1) % PR], (it + 1) & 1);
-            if (it + 1 + PR < nit) load(ring[(u + 1) % PR], it + 1 + PR);
-        }
+        if (it + 1 < nit) store(ring[(u + 1) % PR], (it + 1) & 1);
+        load(ring[(u + 1) % PR], min(it + 1 + PR, nit - 1));
         __syncthreads();
     }
     }

@@ -24,6 +24,7 @@
 //    online softmax and P.V stay in registers, lanes/waves merge (m, l, acc).
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.hpp"
 
@@ -807,7 +808,9 @@ struct LmSample {
 // RD: weight-ring depth in k-steps (0: the whole tile, KSC).  RD = KSC / 2 holds half a
 // tile per wave (the k-steps ks + RD of the same tile, then the next tile's, refill each
 // register), which fits three 12-wave... waves per SIMD: 768-thread workgroups.
-template <int NM, int EPI, bool BIAS, bool SAMPLE, int KSC, int RD = 0>
+// SAMPLE: 0 a plain GEMM epilogue, 1 the fused sampler, 2 the fused sampler with the
+// temperature division (T != 1)
+template <int NM, int EPI, bool BIAS, int SAMPLE, int KSC, int RD = 0>
 __global__ __launch_bounds__(RD ? 768 : 512) void lm_head_kernel(const uint16_t *__restrict__ x, const uint16_t *__restrict__ w,
                                                       int M, int N, int K, const uint16_t *__restrict__ norm_w,
                                                       float eps, const float *__restrict__ ss_in,
@@ -1034,10 +1037,14 @@ __global__ __launch_bounds__(RD ? 768 : 512) void lm_head_kernel(const uint16_t 
         SWH_GEMM_TRACE(4);
         if constexpr (SAMPLE) {
             const int col = t * 16 + rl;
-            bool masked = false;
+            // EOS suppression as an added -inf (x + 0 = x), not a branch per element; the
+            // temperature division only in the SAMPLE == 2 instantiation (T != 1): as a select,
+            // the IEEE division ran on every element at T = 1 too
+            float mask_add = 0.f;
             if (suppress) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) masked |= (e < smp.p.n_eos && col == smp.p.eos_ids[e]);
+                for (int e = 0; e < 4; ++e)
+                    if (e < smp.p.n_eos && col == smp.p.eos_ids[e]) mask_add = kNegInf;
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -1047,14 +1054,14 @@ __global__ __launch_bounds__(RD ? 768 : 512) void lm_head_kernel(const uint16_t 
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     float z = round_bf16(acc[i][e] * rsr[i][e]);  // the bf16 logit
-                    if (temp != 1.f) z = z / temp;
-                    const float key = masked ? kNegInf
-                                     : smp.p.greedy ? z
-                                                    : z - fast_log(-fast_log(u01_from_bits(wd[e])));
-                    if (key > bk[i][e] || (key == bk[i][e] && col < bi[i][e])) {
-                        bk[i][e] = key;
-                        bi[i][e] = col;
-                    }
+                    if constexpr (SAMPLE == 2) z = z / temp;
+                    float key = smp.p.greedy ? z : z - fast_log(-fast_log(u01_from_bits(wd[e])));
+                    key += mask_add;
+                    // branch-free: a lane's columns grow with t, so the index tie-break only
+                    // ever fires against the initial (-inf, INT_MAX) entry
+                    const bool better = (key > bk[i][e]) | ((key == bk[i][e]) & (col < bi[i][e]));
+                    bk[i][e] = better ? key : bk[i][e];
+                    bi[i][e] = better ? col : bi[i][e];
                 }
             }
         } else if constexpr (EPI == EPI_SILU && !SWH_SILU_ST16) {
@@ -1782,7 +1789,7 @@ int launch_gemm_ms(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const
     }
 }
 
-template <int NM, int EPI, bool BIAS, bool SAMPLE, int KSC, int RD = 0>
+template <int NM, int EPI, bool BIAS, int SAMPLE, int KSC, int RD = 0>
 int launch_lm_ks(dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W, int M, int N, int K,
                  const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs, uint16_t *Y, int ldy,
                  const LmSample &smp) {
@@ -1807,10 +1814,14 @@ inline bool lm_ring14() {
 }
 
 // compile-time k-step counts for the model widths in use (Qwen2.5-0.5B: H = 896)
-template <int NM, int EPI, bool BIAS, bool SAMPLE>
+template <int NM, int EPI, bool BIAS, int SAMPLE>
 int launch_lm(dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W, int M, int N, int K,
               const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs, uint16_t *Y, int ldy,
               const LmSample &smp) {
+    if constexpr (SAMPLE == 1) {  // the division instantiation when the rows are sampled at T != 1
+        if (!smp.p.greedy && smp.p.temperature != 1.0f)
+            return launch_lm<NM, EPI, BIAS, 2>(grid, lds, s, X, W, M, N, K, NWt, eps, ss_in, Bs, Y, ldy, smp);
+    }
     switch (K / 32) {
     case 28:
         if (SAMPLE && lm_ring14())

@@ -686,27 +686,35 @@ extern "C" int swh_rmsnorm_fwd(const void *x, const void *residual, void *residu
 }
 
 // d weight: gw[h] = bf16(gw[h] + bf16(sum_b part[b][h])) — the partial column sums of
-// swh_rmsnorm_bwd folded into the bf16 gradient view in one launch
-// a workgroup = 64 columns x 16 row slices: slice s sums partial rows s, s + 16, ...
-// (loads issued 8 at a time), then the 16 slice sums add in fixed order through LDS
+// swh_rmsnorm_bwd folded into the bf16 gradient view.  A workgroup = 64 columns x 16 row
+// slices: slice s sums partial rows s, s + 16, ... of its range (loads issued 8 at a time),
+// then the 16 slice sums add in fixed order through LDS.  Long column sums (the 544
+// partial rows of a 17408-token pass would leave H / 64 = 14 workgroups streaming 2 MB)
+// go in two stages: stage 1 splits the rows into ranges of `rps`, each range summed by
+// its own workgroup into the range's first row (read by no other workgroup); stage 2
+// sums those rows (stride rps) and folds them in.  Fixed order throughout.
 constexpr int kDwSlices = 16;
-template <int DT>
-__global__ __launch_bounds__(64 * kDwSlices) void rmsnorm_dw_accum_kernel(const float *__restrict__ part, int64_t nb,
-                                                                         int64_t H, typename Elem<DT>::T *__restrict__ gw) {
+constexpr int kDwRangeRows = 32;  // stage-1 rows per range
+template <int DT, bool FOLD>
+__global__ __launch_bounds__(64 * kDwSlices) void rmsnorm_dw_accum_kernel(float *__restrict__ part, int64_t nb,
+                                                                         int64_t H, int64_t stride,
+                                                                         typename Elem<DT>::T *__restrict__ gw) {
     __shared__ float red[kDwSlices][64];
     const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
     const int64_t h = (int64_t)blockIdx.x * 64 + c;
+    const int64_t r0 = FOLD ? 0 : (int64_t)blockIdx.y * kDwRangeRows;  // stage 1: this workgroup's range
+    const int64_t r1 = FOLD ? nb : min(nb, r0 + kDwRangeRows);
     float t = 0.f;
     if (h < H) {
-        int64_t b = sl;
-        for (; b + 7 * kDwSlices < nb; b += 8 * kDwSlices) {
+        int64_t b = r0 + sl;
+        for (; b + 7 * kDwSlices < r1; b += 8 * kDwSlices) {
             float v[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = part[(b + j * kDwSlices) * H + h];
+            for (int j = 0; j < 8; ++j) v[j] = part[(b + j * kDwSlices) * stride * H + h];
 #pragma unroll
             for (int j = 0; j < 8; ++j) t += v[j];
         }
-        for (; b < nb; b += kDwSlices) t += part[b * H + h];
+        for (; b < r1; b += kDwSlices) t += part[b * stride * H + h];
     }
     red[sl][c] = t;
     __syncthreads();
@@ -714,25 +722,33 @@ __global__ __launch_bounds__(64 * kDwSlices) void rmsnorm_dw_accum_kernel(const 
         float u = 0.f;
 #pragma unroll
         for (int q = 0; q < kDwSlices; ++q) u += red[q][c];
-        if constexpr (DT == SWH_F32) gw[h] += u;
+        if constexpr (!FOLD) part[r0 * H + h] = u;
+        else if constexpr (DT == SWH_F32) gw[h] += u;
         else gw[h] = f32_to_bf16_bits(bf16_bits_to_f32(gw[h]) + round_bf16(u));
     }
+}
+
+template <int DT>
+int dw_accum(float *part, int64_t nb, int64_t H, typename Elem<DT>::T *gw, hipStream_t st) {
+    const unsigned cb = (unsigned)((H + 63) / 64);
+    if (nb <= 2 * kDwRangeRows) {
+        rmsnorm_dw_accum_kernel<DT, true><<<dim3(cb), 64 * kDwSlices, 0, st>>>(part, nb, H, 1, gw);
+        return launch_status();
+    }
+    const int64_t nr = (nb + kDwRangeRows - 1) / kDwRangeRows;
+    rmsnorm_dw_accum_kernel<DT, false><<<dim3(cb, (unsigned)nr), 64 * kDwSlices, 0, st>>>(part, nb, H, 1, gw);
+    rmsnorm_dw_accum_kernel<DT, true><<<dim3(cb), 64 * kDwSlices, 0, st>>>(part, nr, H, kDwRangeRows, gw);
+    return launch_status();
 }
 
 extern "C" int swh_rmsnorm_dw_accum(const float *dw_partial, int64_t nblocks, int64_t H, void *grad_w, int32_t dtype,
                                     void *stream) {
     if (!dw_partial || !grad_w || nblocks <= 0 || H <= 0) return SWH_E_ARG;
-    const dim3 grid((unsigned)((H + 63) / 64));
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (dtype == SWH_BF16)
-        rmsnorm_dw_accum_kernel<SWH_BF16><<<grid, 64 * kDwSlices, 0, st>>>(dw_partial, nblocks, H,
-                                                                         static_cast<uint16_t *>(grad_w));
-    else if (dtype == SWH_F32)
-        rmsnorm_dw_accum_kernel<SWH_F32><<<grid, 64 * kDwSlices, 0, st>>>(dw_partial, nblocks, H,
-                                                                        static_cast<float *>(grad_w));
-    else
-        return SWH_E_DTYPE;
-    return launch_status();
+    float *part = const_cast<float *>(dw_partial);  // stage 1 writes each range's sum into its first row
+    if (dtype == SWH_BF16) return dw_accum<SWH_BF16>(part, nblocks, H, static_cast<uint16_t *>(grad_w), st);
+    if (dtype == SWH_F32) return dw_accum<SWH_F32>(part, nblocks, H, static_cast<float *>(grad_w), st);
+    return SWH_E_DTYPE;
 }
 
 extern "C" int swh_rmsnorm_bwd(const void *x, const void *weight, const float *rstd, const void *dy, int64_t rows,

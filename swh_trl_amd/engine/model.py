@@ -57,9 +57,21 @@ def dw_streams(dev: torch.device) -> list:
 _DW_KEEP: list = []  # tensors the side stream reads, alive until the compute stream has joined it
 
 
+_PENDING_DW: dict = {}  # device index -> weight-gradient launches not yet issued (see _accumulate_dw)
+_DEFER_DW = os.environ.get("SWH_DW_DEFER", "1") != "0"
+
+
+def issue_pending_dw(dev: torch.device) -> None:
+    """Issue the deferred weight-gradient launches (in order) on the side stream."""
+    lst = _PENDING_DW.pop(dev.index, None) if dev.type == "cuda" else None
+    for fn in lst or ():
+        fn()
+
+
 def dw_sync(dev: torch.device):
     """The current stream waits for every weight-gradient launch issued so far
     (called at the end of every backward by the embedding node, which runs last)."""
+    issue_pending_dw(dev)
     for st in dw_streams(dev):
         torch.cuda.current_stream(dev).wait_stream(st)
     _DW_KEEP.clear()
@@ -139,13 +151,30 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             _main_gemm_fence(dy.device)
             dx = dy @ w
+            # the previous projection's weight gradient starts now, behind this input-gradient
+            # GEMM, beside the HIP kernels that follow it (norm / SiLU / attention backward)
+            issue_pending_dw(dy.device)
         if ctx.gw is not None:
             _accumulate_dw(ctx.gw, ctx.gb, dy, x)
         return dx, None, None, None, None
 
 
 def _accumulate_dw(gw, gb, dy, x):
-    """gw += dy^T x (and gb += column sums of dy) on the weight-gradient stream."""
+    """gw += dy^T x (and gb += column sums of dy) on the weight-gradient stream,
+    issued when the NEXT input-gradient GEMM has been (SWH_DW_DEFER=0: now).
+    Library GEMMs never overlap (_main_gemm_fence): issued at once, a weight-
+    gradient GEMM made the very next input-gradient GEMM wait for it while the
+    compute stream had little else queued (o_proj's dX behind gate/up's dW, ~0.3 ms
+    a layer); deferred by one GEMM it runs beside the norm / SiLU / attention
+    backward that follows that next GEMM instead.  Flushed by dw_sync and before
+    a layer's gradient-ready hook (the DP all-reduce reads the layer's range)."""
+    if _DEFER_DW and _dw_stream(dy.device) is not None:
+        _PENDING_DW.setdefault(dy.device.index, []).append(lambda: _accumulate_dw_now(gw, gb, dy, x))
+    else:
+        _accumulate_dw_now(gw, gb, dy, x)
+
+
+def _accumulate_dw_now(gw, gb, dy, x):
     with _OnStream(_dw_stream(dy.device)) as side:
         side.keep(dy, x)
         dy2 = dy.reshape(-1, dy.shape[-1])
@@ -394,6 +423,7 @@ class _GradReady(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        issue_pending_dw(dy.device)  # the layer's last weight gradient is issued before the hook reads it
         ctx.cb(ctx.layer)
         return dy, None, None
 
@@ -652,7 +682,7 @@ class CausalLM:
     supports_shared_prefix = True
 
     def hidden_states_grouped(self, prompt_ids: torch.Tensor, prompt_mask: torch.Tensor,
-                              completion_ids: torch.Tensor, G: int):
+                              completion_ids: torch.Tensor, G: int, padded: Optional[bool] = None):
         """The scoring / training forward of `hidden_states(cat(prompt, completion))`
         for rows in groups of G consecutive rows that share one prompt (GRPO's
         num_generations copies, grpo_trainer.py:97-192): every token-wise op
@@ -663,7 +693,8 @@ class CausalLM:
         broadcast to the group's rows by expand (their gradients are the
         fixed-order sums over the rows).  Returns (h_last [U, H]: the final
         hidden state of the last prompt position of each group, h_comp
-        [R, C, H]: the completion positions)."""
+        [R, C, H]: the completion positions).  `padded`: whether any prompt
+        is left-padded, when the caller knows it on the host (None: read back)."""
         c = self.cfg
         R, C = completion_ids.shape
         if G < 1 or R % G:
@@ -679,7 +710,8 @@ class CausalLM:
         pos_p = torch.arange(P, device=dev).expand(U, P)
         pos_c = torch.arange(P, P + C, device=dev).expand(R, C)
         cos_t, sin_t = self.rope(P + C)
-        padded = not bool(pm.bool().all())
+        if padded is None:
+            padded = not bool(pm.bool().all())
         km = torch.cat([pm.to(torch.int32).repeat_interleave(G, 0), torch.ones(R, C, dtype=torch.int32, device=dev)], 1)
         mask = self._mask(km, P + C, padded, dev)
 

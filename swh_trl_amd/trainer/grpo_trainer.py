@@ -419,8 +419,16 @@ class GRPOTrainer:
         # completions are as wide as the longest row (:1793-1810); the columns past it
         # are pad with mask 0 in every row, so dropping them changes no value and
         # saves their scoring / training compute
-        lh = torch.stack([lengths.max().to(torch.int64), has_eos.min().to(torch.int64)]).cpu()
+        # rows of one prompt are consecutive here (RepeatSampler): a group id per row lets the
+        # training forward share each prompt's tokens after the shuffle (_prompt_groups); the
+        # group ids and per-row prompt padding travel to the host with the width (one sync),
+        # so the scoring / training passes never read them back from the device
+        same = (prompt_ids[1:] == prompt_ids[:-1]).all(1) & (prompt_mask[1:] == prompt_mask[:-1]).all(1)
+        group = torch.cat([torch.zeros(1, dtype=torch.int64, device=self.device), (~same).long().cumsum(0)])
+        lh = torch.cat([torch.stack([lengths.max().to(torch.int64), has_eos.min().to(torch.int64)]), group,
+                        (prompt_mask == 0).any(1).to(torch.int64)]).cpu()
         width = int(lh[0]) if int(lh[1]) else completion_ids.shape[1]
+        group_h, padded_h = lh[2:2 + B], lh[2 + B:].bool()
         if width < completion_ids.shape[1]:
             completion_ids = completion_ids[:, :width].contiguous()
             completion_mask = completion_mask[:, :width].contiguous()
@@ -435,13 +443,10 @@ class GRPOTrainer:
                                                                self.num_generations, self.scale_rewards)
         if self.world > 1:
             adv = adv[self.rank * B:(self.rank + 1) * B]
-        # rows of one prompt are consecutive here (RepeatSampler): a group id per row lets the
-        # training forward share each prompt's tokens after the shuffle (_prompt_groups)
-        same = (prompt_ids[1:] == prompt_ids[:-1]).all(1) & (prompt_mask[1:] == prompt_mask[:-1]).all(1)
-        group = torch.cat([torch.zeros(1, dtype=torch.int64, device=self.device), (~same).long().cumsum(0)])
+        # host tensors ("_" keys stay on the host through shuffle, split and checkpoints)
         out = {"prompt_ids": prompt_ids, "prompt_mask": prompt_mask, "completion_ids": completion_ids,
-               "completion_mask": completion_mask, "advantages": adv, "prompt_group": group + count * B,
-               "row_index": torch.arange(B, device=self.device) + count * B}
+               "completion_mask": completion_mask, "advantages": adv, "_prompt_group": group_h + count * B,
+               "_row_index": torch.arange(B) + count * B, "_prompt_padded": padded_h}
         # old-policy (:1854-1869) and frozen-reference (:1871-1899) log-probs: scored here only
         # for the micro-batches whose first use would see another policy / reference; the rest
         # are scored by the training pass itself, on its own batch layout (_loss_backward)
@@ -568,7 +573,9 @@ class GRPOTrainer:
             # the G copies of each prompt share one prompt forward (CausalLM.hidden_states_grouped)
             perm, G = grp
             cid = batch["completion_ids"][perm]
-            h_last, h_comp = model.hidden_states_grouped(batch["prompt_ids"][perm], batch["prompt_mask"][perm], cid, G)
+            padded = batch.get("_prompt_padded")
+            h_last, h_comp = model.hidden_states_grouped(batch["prompt_ids"][perm], batch["prompt_mask"][perm], cid, G,
+                                                         padded=None if padded is None else bool(padded.any()))
             R, C = cid.shape
             U, H = h_last.shape
             first = h_last[:, None, None].expand(U, G, 1, H).reshape(R, 1, H)  # predicts completion token 0
@@ -594,21 +601,25 @@ class GRPOTrainer:
         scoring pass gave it, so both see the same GEMM / attention layout and
         produce the same bits whatever the kernels' row-position dependence.
         SWH_SHARED_PREFIX=0 keeps the per-row forward."""
-        if os.environ.get("SWH_SHARED_PREFIX", "1") == "0" or "prompt_group" not in batch:
+        if os.environ.get("SWH_SHARED_PREFIX", "1") == "0":
             return None
-        gid = batch["prompt_group"]
-        key = batch.get("row_index")
-        order = torch.argsort(key) if key is not None else None
+        # the trainer's batches carry host copies ("_" keys: no device sync); device ids are
+        # read back once (tools / tests that build batches by hand)
+        gid = batch.get("_prompt_group", batch.get("prompt_group"))
+        key = batch.get("_row_index", batch.get("row_index"))
+        if gid is None:
+            return None
+        gid = gid.cpu()
+        order = torch.argsort(key.cpu()) if key is not None else None
         rows: dict = {}
-        g_host = (gid[order] if order is not None else gid).tolist()  # one small device -> host copy
-        for r, g in enumerate(g_host):
+        for r, g in enumerate((gid[order] if order is not None else gid).tolist()):
             rows.setdefault(g, []).append(r)
         sizes = {len(v) for v in rows.values()}
         if len(sizes) != 1 or sizes.pop() < 2:
             return None
-        pos = [r for v in rows.values() for r in v]  # positions in the (sorted) sequence
-        pos_t = torch.tensor(pos, device=gid.device)
-        return (order[pos_t] if order is not None else pos_t), len(pos) // len(rows)
+        pos = torch.tensor([r for v in rows.values() for r in v])  # positions in the (sorted) sequence
+        perm = order[pos] if order is not None else pos
+        return perm.to(batch["completion_ids"].device, non_blocking=True), len(pos) // len(rows)
 
     @torch.no_grad()
     def _score_logps(self, model: CausalLM, batch: dict) -> torch.Tensor:
@@ -641,7 +652,7 @@ class GRPOTrainer:
             "completion_mask": torch.cat([m["completion_mask"] for m in micro]),
             "advantages": torch.cat([m["advantages"] for m in micro]),
         }
-        for k in ("prompt_group", "row_index"):
+        for k in ("prompt_group", "row_index", "_prompt_group", "_row_index", "_prompt_padded"):
             if all(k in m for m in micro):
                 batch[k] = torch.cat([m[k] for m in micro])
         for k in ("old_per_token_logps", "ref_per_token_logps"):
@@ -730,8 +741,9 @@ class GRPOTrainer:
                     next(self._batches)
             gen = self._generate_and_score_completions(next(self._batches))
             n = gen["completion_ids"].shape[0]
-            perm = torch.randperm(n, generator=self._shuffle_gen).to(self.device)
-            gen = {k: v[perm] for k, v in gen.items()}
+            perm_h = torch.randperm(n, generator=self._shuffle_gen)
+            perm = perm_h.to(self.device)
+            gen = {k: v[perm_h if v.device.type == "cpu" else perm] for k, v in gen.items()}
             self._buffered_inputs = [self._mark_fresh(mb, "train") for mb in split_tensor_dict(gen, a.steps_per_generation)]
         inputs = self._buffered_inputs[self._step % a.steps_per_generation]
         self._step += 1

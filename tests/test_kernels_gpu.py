@@ -660,7 +660,7 @@ def test_rmsnorm_backward_dres_and_dw_accumulation(ops, dev, rows):
     """engine/model.py _norm_backward: dx + the residual branch's gradient in one
     pass, the weight gradient summed from the per-block partials (swh_rmsnorm_dw_accum)
     and added to an existing bf16 gradient; rows = one training micro-batch and a ragged count."""
-    from swh_trl_amd.engine.model import _norm_backward
+    from swh_trl_amd.engine.model import _norm_backward, dw_sync
     g = _gen(21)
     H = 896
     x = torch.randn(rows, H, generator=g).to(torch.bfloat16)
@@ -672,6 +672,7 @@ def test_rmsnorm_backward_dres_and_dw_accumulation(ops, dev, rows):
     rstd = torch.rsqrt(xf.pow(2).mean(-1) + 1e-6)
     gw = gw0.to(dev)
     dx = _norm_backward(x.to(dev), w.to(dev), rstd.to(dev), dy.to(dev), dres.to(dev), gw)
+    dw_sync(dev)  # the fold runs on the weight-gradient side stream
     xr, wr = x.double().requires_grad_(True), w.double().requires_grad_(True)
     yr = wr * (xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6))
     yr.backward(dy.double())

@@ -133,8 +133,8 @@ def product_run(cfg, dtype, n_steps, *, std, lr, G=4, P=12, C=24, MB=8, GA=2, se
         # old-policy log-probs scored by the training pass itself (the policy had not stepped
         # since the generation) live in the buffered micro-batches: back to generation order
         for mb in tr._buffered_inputs or []:
-            if "old_per_token_logps" in mb and "row_index" in mb:
-                for ri, row in zip(mb["row_index"].tolist(), mb["old_per_token_logps"].detach().cpu()):
+            if "old_per_token_logps" in mb and "_row_index" in mb:
+                for ri, row in zip(mb["_row_index"].tolist(), mb["old_per_token_logps"].detach().cpu()):
                     g = cap["gens"][ri // mb["completion_ids"].shape[0] // spg]
                     if "old_per_token_logps" not in g:
                         g["old_per_token_logps"] = torch.zeros(g["completion_ids"].shape)

@@ -198,6 +198,21 @@ def dual(eng, m):
           flush=True)
 
 
+def lm_ab(eng, reps=20):
+    """The fused lm-head sampler alone: sampling (Philox + Gumbel per element) against
+    greedy (argmax only) on the same weights — what the per-element RNG costs."""
+    from swh_trl_amd import nn_ops, ops
+    c = eng.cfg
+    w, nw, fw = eng._lm_head_weight()
+    for name, params in (("sample T=0.7", ops.make_sample_params(temperature=0.7)),
+                         ("sample T=1", ops.make_sample_params()),
+                         ("greedy", ops.make_sample_params(greedy=True))):
+        fn = lambda: nn_ops.lm_head_sample(eng.s, w, params, eng.rng, eng.state[0:1], eng.finished, eng.out,  # noqa
+                                           eng.cur, norm_w=nw, eps=c.rms_norm_eps, ss_in=eng.ss,
+                                           workspace=eng.sample_ws, fragw=fw)
+        print(f"lm_head_sample {name:14s} {_time(fn, reps=reps):8.2f} us", flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--step", type=int, default=128)
@@ -206,6 +221,7 @@ def main():
     ap.add_argument("--sweep", action="store_true", help="time the GEMM shapes under several launch geometries")
     ap.add_argument("--dual", action="store_true", help="two half-batch chains on two streams vs one chain")
     ap.add_argument("--ku", action="store_true", help="weight-round depth x waves x geometry sweep (o, down, qkv)")
+    ap.add_argument("--lm", action="store_true", help="lm-head sampler: sampling vs greedy")
     args = ap.parse_args()
     if args.gemm_cfg:
         os.environ["SWH_GEMM_CFG"] = args.gemm_cfg
@@ -232,6 +248,9 @@ def main():
         return
     if args.ku:
         ku_sweep(eng, m)
+        return
+    if args.lm:
+        lm_ab(eng)
         return
     res = eng.kernel_timings(args.step)
     tot = 0.0

@@ -69,6 +69,10 @@ def main(path: str, window_ms: float = 200.0):
                 over[family(n)] += min(e, b1) - max(b, e0)
         who = over.most_common(1)[0][0] if over else "(nothing: host / boundary)"
         blame[f"before {family(n1)} | elsewhere: {who}"] += g
+    big = sorted(((b1 - e0, e0 - t0, n0, n1) for (b0, e0, _, n0), (b1, _, _, n1) in zip(lst, lst[1:])), reverse=True)
+    print("\nlargest single compute-stream gaps (ms, at ms, after -> before):")
+    for g, at, n0, n1 in big[:12]:
+        print(f"  {g / 1e6:7.3f} at {at / 1e6:7.2f}  {family(n0)} -> {family(n1)}")
     print(f"\ncompute-stream gaps > 2 us: {gap_total / 1e6:.2f} ms")
     for k, v in blame.most_common(15):
         print(f"  {v / 1e6:7.2f} ms  {k}")

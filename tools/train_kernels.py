@@ -53,8 +53,9 @@ def main():
         micro.append({"prompt_ids": prompt[sl], "prompt_mask": torch.ones(MB, P, dtype=torch.int32, device=dev),
                       "completion_ids": comp[sl], "completion_mask": torch.ones(MB, C, dtype=torch.int32, device=dev),
                       "advantages": adv[sl],
-                      # generation-order group ids (as the rollout records them): the shared-prompt forward
-                      "prompt_group": torch.arange(B, device=dev)[sl] // G})
+                      # generation-order group ids and prompt padding, host copies as the rollout records
+                      # them: the shared-prompt forward without a device read-back
+                      "_prompt_group": torch.arange(B)[sl] // G, "_prompt_padded": torch.zeros(MB, dtype=torch.bool)})
 
     def step():
         tr.model.zero_grad()
