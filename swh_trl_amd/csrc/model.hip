@@ -686,14 +686,14 @@ extern "C" int swh_rmsnorm_fwd(const void *x, const void *residual, void *residu
 }
 
 // d weight: gw[h] = bf16(gw[h] + bf16(sum_b part[b][h])) — the partial column sums of
-// swh_rmsnorm_bwd folded into the bf16 gradient view.  A workgroup = 64 columns x 16 row
-// slices: slice s sums partial rows s, s + 16, ... of its range (loads issued 8 at a time),
-// then the 16 slice sums add in fixed order through LDS.  Long column sums (the 544
+// swh_rmsnorm_bwd folded into the bf16 gradient view.  A workgroup = 64 columns x 4 row
+// slices: slice s sums partial rows s, s + 4, ... of its range (loads issued 8 at a time),
+// then the 4 slice sums add in fixed order through LDS.  Long column sums (the 544
 // partial rows of a 17408-token pass would leave H / 64 = 14 workgroups streaming 2 MB)
 // go in two stages: stage 1 splits the rows into ranges of `rps`, each range summed by
 // its own workgroup into the range's first row (read by no other workgroup); stage 2
 // sums those rows (stride rps) and folds them in.  Fixed order throughout.
-constexpr int kDwSlices = 16;
+constexpr int kDwSlices = 4;       // 256-thread workgroups: they fit beside the GEMMs they overlap
 constexpr int kDwRangeRows = 32;  // stage-1 rows per range
 template <int DT, bool FOLD>
 __global__ __launch_bounds__(64 * kDwSlices) void rmsnorm_dw_accum_kernel(float *__restrict__ part, int64_t nb,

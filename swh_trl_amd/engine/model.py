@@ -57,21 +57,9 @@ def dw_streams(dev: torch.device) -> list:
 _DW_KEEP: list = []  # tensors the side stream reads, alive until the compute stream has joined it
 
 
-_PENDING_DW: dict = {}  # device index -> weight-gradient launches not yet issued (see _accumulate_dw)
-_DEFER_DW = os.environ.get("SWH_DW_DEFER", "1") != "0"
-
-
-def issue_pending_dw(dev: torch.device) -> None:
-    """Issue the deferred weight-gradient launches (in order) on the side stream."""
-    lst = _PENDING_DW.pop(dev.index, None) if dev.type == "cuda" else None
-    for fn in lst or ():
-        fn()
-
-
 def dw_sync(dev: torch.device):
     """The current stream waits for every weight-gradient launch issued so far
     (called at the end of every backward by the embedding node, which runs last)."""
-    issue_pending_dw(dev)
     for st in dw_streams(dev):
         torch.cuda.current_stream(dev).wait_stream(st)
     _DW_KEEP.clear()
@@ -151,30 +139,13 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             _main_gemm_fence(dy.device)
             dx = dy @ w
-            # the previous projection's weight gradient starts now, behind this input-gradient
-            # GEMM, beside the HIP kernels that follow it (norm / SiLU / attention backward)
-            issue_pending_dw(dy.device)
         if ctx.gw is not None:
             _accumulate_dw(ctx.gw, ctx.gb, dy, x)
         return dx, None, None, None, None
 
 
 def _accumulate_dw(gw, gb, dy, x):
-    """gw += dy^T x (and gb += column sums of dy) on the weight-gradient stream,
-    issued when the NEXT input-gradient GEMM has been (SWH_DW_DEFER=0: now).
-    Library GEMMs never overlap (_main_gemm_fence): issued at once, a weight-
-    gradient GEMM made the very next input-gradient GEMM wait for it while the
-    compute stream had little else queued (o_proj's dX behind gate/up's dW, ~0.3 ms
-    a layer); deferred by one GEMM it runs beside the norm / SiLU / attention
-    backward that follows that next GEMM instead.  Flushed by dw_sync and before
-    a layer's gradient-ready hook (the DP all-reduce reads the layer's range)."""
-    if _DEFER_DW and _dw_stream(dy.device) is not None:
-        _PENDING_DW.setdefault(dy.device.index, []).append(lambda: _accumulate_dw_now(gw, gb, dy, x))
-    else:
-        _accumulate_dw_now(gw, gb, dy, x)
-
-
-def _accumulate_dw_now(gw, gb, dy, x):
+    """gw += dy^T x (and gb += column sums of dy) on the weight-gradient stream."""
     with _OnStream(_dw_stream(dy.device)) as side:
         side.keep(dy, x)
         dy2 = dy.reshape(-1, dy.shape[-1])
@@ -423,7 +394,6 @@ class _GradReady(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        issue_pending_dw(dy.device)  # the layer's last weight gradient is issued before the hook reads it
         ctx.cb(ctx.layer)
         return dy, None, None
 
