@@ -5,7 +5,8 @@ the product).
     rocprofv3 --kernel-trace --output-format csv -d OUT -o run -- python3 tools/train_kernels.py --reps 1
     python tools/critical_path.py OUT/.../run_kernel_trace.csv
 
-The last `--window` ms of the trace (the timed step) is analysed: per stream
+The last `window` ms of the trace (the timed step; without --whole, from the
+last host gap > 5 ms on) is analysed: per stream
 its busy time and idle gaps; for the busiest stream (the compute stream) each
 gap is attributed to what the other streams ran meanwhile (the fence on the
 weight-gradient GEMMs, dK/dV, ...), and the kernels are grouped by family with
@@ -28,7 +29,7 @@ def family(name: str) -> str:
     return n[:60]
 
 
-def main(path: str, window_ms: float = 200.0):
+def main(path: str, window_ms: float = 200.0, cut_gaps: bool = True):
     rows = list(csv.DictReader(open(path)))
     key = "Stream_Id" if "Stream_Id" in rows[0] else "Queue_Id"
     ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r[key], r["Kernel_Name"]) for r in rows]
@@ -39,7 +40,7 @@ def main(path: str, window_ms: float = 200.0):
     cut = ks[0][0]
     prev_end = ks[0][1]
     for s, e, _, _ in ks:
-        if s - prev_end > 5e6:
+        if cut_gaps and s - prev_end > 5e6:
             cut = s
         prev_end = max(prev_end, e)
     cut = max(cut, t_end - int(window_ms * 1e6))
@@ -50,6 +51,20 @@ def main(path: str, window_ms: float = 200.0):
     for k in ks:
         by[k[2]].append(k)
     print(f"window {span / 1e6:.2f} ms, {len(ks)} kernels, streams {sorted(by)}")
+    iv = sorted((b, e) for b, e, _, _ in ks)  # GPU idle = no stream running anything
+    busy, (cs, ce), idle = 0, iv[0], []
+    for b, e in iv[1:]:
+        if b > ce:
+            busy += ce - cs
+            idle.append((b - ce, (ce - t0) / 1e6))
+            cs, ce = b, e
+        else:
+            ce = max(ce, e)
+    busy += ce - cs
+    small = sum(g for g, _ in idle if g < 50e3)
+    print(f"GPU busy (any stream) {busy / 1e6:.2f} ms, idle {(span - busy) / 1e6:.2f} ms "
+          f"({small / 1e6:.2f} ms in gaps < 50 us); largest idle gaps (ms at ms): "
+          + ", ".join(f"{g / 1e6:.2f}@{t:.1f}" for g, t in sorted(idle, reverse=True)[:10]))
     main_s = max(by, key=lambda s: sum(e - b for b, e, _, _ in by[s]))
     for s, lst in sorted(by.items()):
         busy = sum(e - b for b, e, _, _ in lst)
@@ -87,4 +102,4 @@ def main(path: str, window_ms: float = 200.0):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], float(sys.argv[2]) if len(sys.argv) > 2 else 200.0)
+    main(sys.argv[1], float(sys.argv[2]) if len(sys.argv) > 2 else 200.0, "--whole" not in sys.argv)

@@ -53,7 +53,9 @@ for step in "$@"; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_$tag -o run \
         -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $O/${tag}_prof.log 2>&1 \
         || fail prof $? $O/${tag}_prof.log
-      cp "$(find /tmp/prof_$tag -name '*kernel_stats.csv' | head -1)" $O/${tag}_bench_kernel_stats.csv ;;
+      cp "$(find /tmp/prof_$tag -name '*kernel_stats.csv' | head -1)" $O/${tag}_bench_kernel_stats.csv
+      python tools/critical_path.py "$(find /tmp/prof_$tag -name '*kernel_trace.csv' | head -1)" 330 --whole \
+        > $O/${tag}_bench_critical_path.txt 2>&1 || fail critical_path $? $O/${tag}_bench_critical_path.txt ;;
     decode)
       timeout -k 10 300 python -u tools/bench_decode.py > $O/${tag}_decode.log 2>&1 || fail decode $? $O/${tag}_decode.log
       tail -15 $O/${tag}_decode.log ;;

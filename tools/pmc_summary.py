@@ -15,6 +15,7 @@ import sys
 
 NAMES = {  # kernel template prefix -> the bench's kernel name
     "lm_head_kernel<2, 2, false, false": "decode_gemm.gate_up",   # tile kernel, folded norm, SiLU epilogue
+    "lm_head_kernel<2, 2, false, 0": "decode_gemm.gate_up",       # (round 4: SAMPLE is an int)
     "decode_gemm_kernel<1, 2, 2, 0, true": "decode_gemm.qkv",
     "decode_gemm_kernel<1, 1, 0, 1, false, 512, 0>": "decode_gemm.o",     # K-class tag 0: K <= 1024
     "decode_gemm_kernel<1, 1, 0, 1, false, 512, 1>": "decode_gemm.down",  # K-class tag 1
@@ -23,6 +24,7 @@ NAMES = {  # kernel template prefix -> the bench's kernel name
     "xstream_gemm_kernel<19, 1, 0, 1, false": "decode_gemm.down",  # fragment-order activation (act_frag)
     "attn_decode_kernel<64, 7>": "attn_decode",
     "lm_head_kernel<2, 0, false, true": "lm_head_sample",
+    "lm_head_kernel<2, 0, false, 1": "lm_head_sample",
     # training kernels (tools/train_kernels.py)
     "logp_entropy_fwd_kernel": "logp_entropy_fwd",
     "logp_bwd_kernel": "logp_bwd",
