@@ -265,6 +265,9 @@ __device__ __forceinline__ void fa_stage_store(const FaStage<D> &st, uint16_t *k
 }
 
 
+#ifndef SWH_FA_REVERSE
+#define SWH_FA_REVERSE 0  // forward / dQ: query tiles in reverse (longest first) dispatch order
+#endif
 #ifndef SWH_FA_PD
 #define SWH_FA_PD 1  // 32-row K/V blocks in flight (registers) ahead of the computed one (2-4: more VGPRs, slower)
 #endif
@@ -289,11 +292,15 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(FaArgs a) {
     const int b = blockIdx.z, kvh = blockIdx.y, G = a.Hq / a.Hkv, L = a.L;
     const bool active = wid < G;  // waves past the group's heads only help staging (blocks >= 4 waves)
     const int h = kvh * G + min(wid, G - 1);
+#if SWH_FA_REVERSE
+    const int q0 = (gridDim.x - 1 - blockIdx.x) * 16 * QT;  // the longest causal walks dispatch first
+#else
     const int q0 = blockIdx.x * 16 * QT;
+#endif
     if (!fa_qlive(a, b, q0 + 16 * QT - 1)) return;  // the whole tile: prompt queries another sequence carries
     const int fv = a.first_valid ? a.first_valid[b] : 0;
     const FaRows kr_b = fa_rows(a.k, a.P, b), vr_b = fa_rows(a.v, a.P, b), qr_b = fa_rows(a.q, a.P, b);
-    auto kvrow = [&](int which, int row) -> const uint16_t * {
+    auto kvrow = [=](int which, int row) -> const uint16_t * {  // by value: no stack object
         return which ? vr_b.row(kvh, row) : kr_b.row(kvh, row);
     };
     u32x4 qf[QT][DC];
@@ -320,7 +327,7 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(FaArgs a) {
     FaStage<D> ring[PD];  // K/V block j in ring[j % PD] from its load to its LDS store, PD blocks ahead
     __shared__ uint32_t kvw[kFaMaskWords];
     fa_mask_words(a, b, nblk, kvw, wid, nthr >> 6, lane);
-    auto load = [&](FaStage<D> &r, int j) { fa_stage_load<D>(r, kvrow, 32 * j, L, tid, nthr); };
+    auto load = [=](FaStage<D> &r, int j) { fa_stage_load<D>(r, kvrow, 32 * j, L, tid, nthr); };
     auto put = [&](const FaStage<D> &r, int j) { fa_stage_store<D, VS>(r, kt[j & 1], vt[j & 1], tid, nthr); };
     load(ring[0], 0);
     put(ring[0], 0);
@@ -432,13 +439,17 @@ __global__ __launch_bounds__(512) void fa_dq_kernel(FaArgs a) {
     const int b = blockIdx.z, kvh = blockIdx.y, G = a.Hq / a.Hkv, L = a.L;
     const bool active = wid < G;
     const int h = kvh * G + min(wid, G - 1);
+#if SWH_FA_REVERSE
+    const int q0 = (gridDim.x - 1 - blockIdx.x) * 16;  // the longest causal walks dispatch first
+#else
     const int q0 = blockIdx.x * 16;
+#endif
     if (!fa_qlive(a, b, q0 + 15)) return;  // the whole tile: prompt queries another sequence carries
     const int qc = min(q0 + c16, L - 1);
     const int fv = a.first_valid ? a.first_valid[b] : 0;
     const int64_t qrow = ((int64_t)b * a.Hq + h) * L;
     const FaRows kr_b = fa_rows(a.k, a.P, b), vr_b = fa_rows(a.v, a.P, b);
-    auto kvrow = [&](int which, int row) -> const uint16_t * {
+    auto kvrow = [=](int which, int row) -> const uint16_t * {  // by value: no stack object
         return which ? vr_b.row(kvh, row) : kr_b.row(kvh, row);
     };
     u32x4 qf[DC], df[DC];
@@ -460,7 +471,7 @@ __global__ __launch_bounds__(512) void fa_dq_kernel(FaArgs a) {
     FaStage<D> ring[PD];  // K/V block j in ring[j % PD] from its load to its LDS store, PD blocks ahead
     __shared__ uint32_t kvw[kFaMaskWords];
     fa_mask_words(a, b, nblk, kvw, wid, nthr >> 6, lane);
-    auto load = [&](FaStage<D> &r, int j) { fa_stage_load<D>(r, kvrow, 32 * j, L, tid, nthr); };
+    auto load = [=](FaStage<D> &r, int j) { fa_stage_load<D>(r, kvrow, 32 * j, L, tid, nthr); };
     auto put = [&](const FaStage<D> &r, int j) { fa_stage_store<D, VS>(r, kt[j & 1], vt[j & 1], tid, nthr); };
     load(ring[0], 0);
     put(ring[0], 0);
