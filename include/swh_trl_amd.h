@@ -275,6 +275,24 @@ int swh_ema_mix(void *target, const void *src, int dtype, int64_t N, float keep,
  * multiple of 8 (bf16) / 4 (f32).  Replaces the AccumulateGrad of the
  * reference's weight gradients (one GEMM per weight). */
 int swh_dw_reduce(const void *parts, int32_t S, int64_t n, void *grad, int32_t dtype, void *stream);
+/* Narrow-projection GEMM of the training forward / input gradient (the qkv and
+ * o projections the reference runs as nn.Linear inside transformers' Qwen2
+ * attention, through grpo_trainer.py:1793-1810 _get_per_token_logps_and_entropies
+ * and its backward): C[M, N] = A[M, K] B[N, K]^T (+ bias[N]), bf16 in and out,
+ * fp32 accumulation in a fixed K order.  N % 128 == 0, K % 64 == 0, leading
+ * dimensions multiples of 8 elements, pointers 16-B aligned; else SWH_E_ARG. */
+int swh_gemm_nt(const void *A, const void *B, const void *bias, void *C, int64_t M, int64_t N, int64_t K,
+                int64_t lda, int64_t ldb, int64_t ldc, void *stream);
+/* Their weight gradient dW[N, K] += dY[M, N]^T X[M, K] (the AccumulateGrad of
+ * the same nn.Linear weights), in two launches: swh_gemm_tn_partials writes
+ * part[s][N][K] (fp32) = the sum over split s's tokens (S ranges of whole
+ * 64-token steps, fp32 accumulation in token order), swh_gemm_tn_fold adds the S
+ * partials in split order to grad (bf16 / f32, n = N K elements) and rounds
+ * once.  M % 64 == 0, N % 128 == 0, K % 128 == 0, leading dimensions multiples
+ * of 8 elements, 16-B aligned pointers; else SWH_E_ARG. */
+int swh_gemm_tn_partials(const void *dY, const void *X, float *part, int64_t M, int64_t N, int64_t K,
+                         int64_t lddy, int64_t ldx, int32_t S, void *stream);
+int swh_gemm_tn_fold(const float *part, int32_t S, int64_t n, void *grad, int32_t dtype, void *stream);
 /* dst_f32[i] += src[i] (bf16/f32) — accumulate micro-batch grads in fp32. */
 int swh_accumulate(float *dst, const void *src, int dtype, int64_t N, float scale, void *stream);
 

@@ -130,6 +130,10 @@ class _Linear(torch.autograd.Function):
     def forward(ctx, x, w, b, gw, gb):
         ctx.save_for_backward(x, w)
         ctx.gw, ctx.gb = gw, gb
+        if _tgemm_serves(w.shape[0], w.shape[1]) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
+            x2 = x.reshape(-1, x.shape[-1])
+            if nn_ops.gemm_nt_eligible(x2, w) and (b is None or b.dtype == torch.bfloat16):
+                return nn_ops.gemm_nt(x2, w, b).view(*x.shape[:-1], w.shape[0])
         return F.linear(x, w, b)
 
     @staticmethod
@@ -137,11 +141,31 @@ class _Linear(torch.autograd.Function):
         x, w = ctx.saved_tensors
         dx = None
         if ctx.needs_input_grad[0]:
-            _main_gemm_fence(dy.device)
-            dx = dy @ w
+            dy2 = dy.reshape(-1, dy.shape[-1])
+            wt = None
+            if _tgemm_serves(w.shape[0], w.shape[1]) and w.shape[1] % 128 == 0 and w.shape[0] % 64 == 0 \
+                    and dy.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
+                wt = w.t().contiguous()  # dy w = dy (w^T)^T: the transposed weight (N K elements) as B
+            if wt is not None and nn_ops.gemm_nt_eligible(dy2, wt):
+                dx = nn_ops.gemm_nt(dy2, wt).view(*dy.shape[:-1], w.shape[1])
+            else:
+                _main_gemm_fence(dy.device)
+                dx = dy @ w
         if ctx.gw is not None:
             _accumulate_dw(ctx.gw, ctx.gb, dy, x)
         return dx, None, None, None, None
+
+
+# swh_gemm_nt / swh_gemm_tn (csrc/tgemm.hip) serve the narrow projections (qkv, o):
+# N <= 1536 outputs, where hipBLASLt's best solutions run at 0.43-0.69 PFLOP/s.
+# SWH_TGEMM=1 turns them on (A/B: tools/bench_tgemm.py, tools/train_kernels.py).
+_TGEMM = os.environ.get("SWH_TGEMM", "0") != "0"
+_TGEMM_MAX_N = 1536
+_TGEMM_SPLITS = int(os.environ.get("SWH_TGEMM_SPLITS", "8"))
+
+
+def _tgemm_serves(n_out: int, k_in: int) -> bool:
+    return _TGEMM and n_out <= _TGEMM_MAX_N and k_in <= _TGEMM_MAX_N
 
 
 def _accumulate_dw(gw, gb, dy, x):
@@ -151,6 +175,13 @@ def _accumulate_dw(gw, gb, dy, x):
         dy2 = dy.reshape(-1, dy.shape[-1])
         x2 = x.reshape(-1, x.shape[-1])
         S = _dw_split(dy2.shape[0], dy2.shape[1] * x2.shape[1])
+        if _tgemm_serves(dy2.shape[1], x2.shape[1]) and gw.is_contiguous() and nn_ops.gemm_tn_eligible(dy2, x2):
+            # fp32 partials over 8 token ranges (one per XCD), folded in order (no fence needed:
+            # the kernel is not persistent)
+            side.keep(nn_ops.gemm_tn_accumulate(gw.view(dy2.shape[1], x2.shape[1]), dy2, x2, _TGEMM_SPLITS))
+            if gb is not None:
+                bias_grad_accumulate(dy2, gb)
+            return
         if S > 1:
             # few output tiles over a long token dimension: split the tokens into S
             # batched GEMMs (S x the workgroups), sum the partials into the gradient

@@ -176,6 +176,60 @@ def decode_gemm(x: torch.Tensor, w: torch.Tensor, *, norm_w: Optional[torch.Tens
     return residual if residual is not None else y
 
 
+def gemm_nt_eligible(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """Shapes swh_gemm_nt serves: bf16, N % 128 == 0, K % 64 == 0, unit inner strides."""
+    return (x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 2 and w.dim() == 2
+            and x.shape[1] == w.shape[1] and w.shape[0] % 128 == 0 and w.shape[1] % 64 == 0
+            and x.stride(1) == 1 and w.stride(1) == 1 and x.stride(0) % 8 == 0 and w.stride(0) % 8 == 0
+            and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0)
+
+
+def gemm_nt(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x w^T (+ bias) on the training projection GEMM (include/swh_trl_amd.h
+    swh_gemm_nt): x [M, K], w [N, K], bf16."""
+    _dev(x, "gemm_nt")
+    if not gemm_nt_eligible(x, w):
+        raise ValueError(f"gemm_nt: unsupported operands {tuple(x.shape)} x {tuple(w.shape)}")
+    M, K = x.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=x.dtype)
+    if bias is not None and (bias.dtype != torch.bfloat16 or not bias.is_contiguous() or bias.numel() != N):
+        raise ValueError("gemm_nt: bias must be a contiguous bf16 vector of N elements")
+    call("swh_gemm_nt", x.data_ptr(), w.data_ptr(), _p(bias), out.data_ptr(), M, N, K, x.stride(0), w.stride(0),
+         out.stride(0), _stream())
+    return out
+
+
+def gemm_tn_eligible(dy: torch.Tensor, x: torch.Tensor) -> bool:
+    """Shapes swh_gemm_tn_partials serves: bf16 [M, N] / [M, K], M % 64, N and K % 128."""
+    return (dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dy.dim() == 2 and x.dim() == 2
+            and dy.shape[0] == x.shape[0] and dy.shape[0] % 64 == 0 and dy.shape[1] % 128 == 0
+            and x.shape[1] % 128 == 0 and dy.stride(1) == 1 and x.stride(1) == 1 and dy.stride(0) % 8 == 0
+            and x.stride(0) % 8 == 0 and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0)
+
+
+def gemm_tn_accumulate(grad: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, splits: int) -> torch.Tensor:
+    """grad [N, K] += dy^T x over the tokens (include/swh_trl_amd.h
+    swh_gemm_tn_partials + swh_gemm_tn_fold): `splits` token ranges in fp32
+    partials, folded in order and rounded once into grad (bf16 / f32).  Returns
+    the partials buffer (keep it alive until the stream has run both launches)."""
+    _dev(dy, "gemm_tn_accumulate")
+    if not gemm_tn_eligible(dy, x):
+        raise ValueError(f"gemm_tn_accumulate: unsupported operands {tuple(dy.shape)} / {tuple(x.shape)}")
+    M, N = dy.shape
+    K = x.shape[1]
+    if grad.numel() != N * K or not grad.is_contiguous():
+        raise ValueError("gemm_tn_accumulate: grad must be a contiguous [N, K] view")
+    part = torch.empty(splits, N, K, device=dy.device, dtype=torch.float32)
+    call("swh_gemm_tn_partials", dy.data_ptr(), x.data_ptr(), part.data_ptr(), M, N, K, dy.stride(0), x.stride(0),
+         int(splits), _stream())
+    call("swh_gemm_tn_fold", part.data_ptr(), int(splits), N * K, grad.data_ptr(),
+         _dtype_code(grad, "gemm_tn_accumulate"), _stream())
+    return part
+
+
 def frag_pack(w: torch.Tensor, norm_w: Optional[torch.Tensor] = None, *, silu: bool = False,
               out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """w [N, K] ([2N, K] gate|up with silu; K % 128 == 0), optionally folded

@@ -1606,3 +1606,86 @@ def test_attn_decode_l3_warmup_is_result_neutral(ops, dev, B, Hkv, G):
     torch.cuda.synchronize()
     assert torch.equal(a, out) and torch.equal(k2, k3) and torch.equal(v2, v3)
     assert all(torch.equal(x, y) for x, y in zip(junk, before))
+
+
+# --------------------------------------------------------------------------- training projection GEMM
+@pytest.mark.parametrize("M,N,K,bias", [(17408, 1152, 896, True), (300, 128, 64, False), (1000, 896, 896, True),
+                                        (2048, 896, 1152, False), (1, 256, 128, True)])
+def test_gemm_nt_matches_fp32_product(dev, M, N, K, bias):
+    """swh_gemm_nt (the qkv / o projections of the training pass) against the
+    fp32 product of the same bf16 operands: the kernel accumulates in fp32 and
+    rounds once, so each element is within one bf16 rounding of the fp32
+    result (2^-8 relative) plus the fp32 summation-order difference."""
+    from swh_trl_amd import _lib, nn_ops
+    _lib.load()
+    g = _gen(11)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(torch.bfloat16)
+    b = (torch.randn(N, generator=g) * 0.1).to(torch.bfloat16) if bias else None
+    ref = x.float() @ w.float().t() + (b.float() if bias else 0)
+    y = nn_ops.gemm_nt(x.to(dev), w.to(dev), b.to(dev) if bias else None).cpu().float()
+    bound = ref.abs() * 2.0 ** -8 + 1e-4 * float(ref.abs().max())
+    assert bool(((y - ref).abs() <= bound).all()), float(((y - ref).abs() - bound).max())
+
+
+def test_gemm_nt_row_invariant_and_strided(dev):
+    """A row's result does not depend on its place in the batch (fixed K order),
+    and strided views (a leading dimension larger than K) give the same bits."""
+    from swh_trl_amd import _lib, nn_ops
+    _lib.load()
+    g = _gen(12)
+    x = torch.randn(700, 1024, generator=g).to(torch.bfloat16).to(dev)
+    w = (torch.randn(256, 896, generator=g) * 0.05).to(torch.bfloat16).to(dev)
+    xs = x[:, :896]  # lda 1024
+    full = nn_ops.gemm_nt(xs, w)
+    perm = torch.randperm(700, generator=g).to(dev)
+    shuffled = nn_ops.gemm_nt(xs.contiguous()[perm], w)
+    assert torch.equal(shuffled, full[perm])
+    part = nn_ops.gemm_nt(xs[129:300].contiguous(), w)
+    assert torch.equal(part, full[129:300])
+    out = torch.empty(700, 384, device=dev, dtype=torch.bfloat16)
+    nn_ops.gemm_nt(xs, w, out=out[:, 64:320])
+    assert torch.equal(out[:, 64:320], full)
+
+
+@pytest.mark.parametrize("M,N,K,S,dtype", [(17408, 1152, 896, 8, torch.bfloat16), (17408, 896, 896, 4, torch.float32),
+                                           (640, 128, 256, 3, torch.bfloat16), (128, 256, 128, 5, torch.float32)])
+def test_gemm_tn_weight_gradient_matches_fp32(dev, M, N, K, S, dtype):
+    """swh_gemm_tn_partials + swh_gemm_tn_fold (the qkv / o weight gradients)
+    against grad + dY^T X in fp64 from the same bf16 operands: fp32 partial sums
+    over token ranges (S larger than the number of 64-token steps leaves empty
+    splits), one rounding into the gradient dtype."""
+    from swh_trl_amd import _lib, nn_ops
+    _lib.load()
+    g = _gen(13)
+    dy = (torch.randn(M, N, generator=g) * 0.01).to(torch.bfloat16)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    g0 = (torch.randn(N, K, generator=g) * 0.1).to(dtype)
+    ref = g0.double() + dy.double().t() @ x.double()
+    gd = g0.to(dev)
+    part = nn_ops.gemm_tn_accumulate(gd, dy.to(dev), x.to(dev), S)
+    torch.cuda.synchronize()
+    del part
+    got = gd.cpu().double()
+    ulp = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -23
+    scale = (dy.double().abs().t() @ x.double().abs())  # bound of the fp32 summation error
+    bound = ref.abs() * ulp + scale * 2.0 ** -22 * (M / S + S) + 1e-12
+    assert bool(((got - ref).abs() <= bound).all()), float(((got - ref).abs() - bound).max())
+
+
+def test_gemm_tn_partials_row_order_and_splits(dev):
+    """Tokens enter in a fixed order: the same tokens give the same partial bits,
+    and S = 1 equals the fp32 sum of an S = 2 split up to the fold's rounding."""
+    from swh_trl_amd import _lib, nn_ops
+    _lib.load()
+    g = _gen(14)
+    dy = (torch.randn(1024, 256, generator=g) * 0.01).to(torch.bfloat16).to(dev)
+    x = torch.randn(1024, 384, generator=g).to(torch.bfloat16).to(dev)
+    a = torch.zeros(256, 384, device=dev)
+    b = torch.zeros(256, 384, device=dev)
+    nn_ops.gemm_tn_accumulate(a, dy, x, 1)
+    nn_ops.gemm_tn_accumulate(b, dy, x, 1)
+    assert torch.equal(a, b)
+    c = torch.zeros(256, 384, device=dev)
+    nn_ops.gemm_tn_accumulate(c, dy, x, 2)
+    torch.testing.assert_close(c, a, rtol=1e-5, atol=1e-6)

@@ -1,0 +1,52 @@
+"""FlatAdamW at the Qwen2.5-0.5B width (tuning aid, not part of the product):
+one clipped update over a 494M-element flat buffer with bf16 gradients and the
+bf16 model copy refreshed, timed with events; prints the grad-norm and update
+times and the update's algorithmic HBM rate (28 B per element).
+
+    SWH_LIB_PATH=tools/_build/x.so python tools/bench_adamw.py [--numel N] [--reps 20]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--numel", type=int, default=494_032_768)
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    from swh_trl_amd import _lib
+    from swh_trl_amd.optim import FlatAdamW
+    _lib.load()
+    dev = torch.device("cuda:0")
+    n = a.numel
+    opt = FlatAdamW(n, dev, lr=1e-6, weight_decay=0.01, max_grad_norm=1.0, no_decay_ranges=[(0, 4096)])
+    grad = (torch.randn(n, device=dev) * 1e-3).to(torch.bfloat16)
+    model = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    for _ in range(3):
+        opt.step(grad, model)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    tn = tu = 0.0
+    for _ in range(a.reps):
+        ev[0].record()
+        opt.grad_norm(grad)
+        ev[1].record()
+        opt.step(grad, model)
+        ev[2].record()
+        ev[2].synchronize()
+        tn += ev[0].elapsed_time(ev[1])
+        tu += ev[1].elapsed_time(ev[2])
+    tn, tu = 1000 * tn / a.reps, 1000 * tu / a.reps
+    # step() runs its own grad-norm pass first: the update alone is tu - tn
+    upd = tu - tn
+    print(f"lib {os.environ.get('SWH_LIB_PATH', 'main')}: numel {n}: grad-norm {tn:.1f} us "
+          f"({2 * n / tn / 1e3:.0f} GB/s), update {upd:.1f} us ({28 * n / upd / 1e3:.0f} GB/s)", flush=True)
+
+
+if __name__ == "__main__":
+    main()
