@@ -102,6 +102,9 @@ __global__ __launch_bounds__(kThreads) void logp_entropy_fwd_kernel(
     }
 }
 
+#ifndef SWH_LOGP_BWD_U
+#define SWH_LOGP_BWD_U 4
+#endif
 template <int DT>
 __global__ __launch_bounds__(kThreads) void logp_bwd_kernel(
     const typename Elem<DT>::T *__restrict__ logits, RowAddr ra, int64_t V, const int64_t *__restrict__ ids,
@@ -139,7 +142,35 @@ __global__ __launch_bounds__(kThreads) void logp_bwd_kernel(
     for (int64_t j = threadIdx.x; j < head; j += kThreads) store(j, grad(Elem<DT>::load(row + j), j));
     const uint4 *vin = reinterpret_cast<const uint4 *>(row + head);
     uint4 *vout = reinterpret_cast<uint4 *>(drow + head);
-    for (int64_t v = threadIdx.x; v < nvec; v += kThreads) {
+    // SWH_LOGP_BWD_U vectors per thread and trip, every load issued before the math
+    constexpr int U = SWH_LOGP_BWD_U;
+    int64_t v = threadIdx.x;
+    for (; v + (U - 1) * kThreads < nvec; v += U * kThreads) {
+        uint4 in[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) in[u] = ld_nt(vin + v + u * kThreads);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float x[PV];
+            unpack16<DT>(in[u], x);
+            const int64_t j0 = head + (v + u * kThreads) * PV;
+            uint32_t w[4];
+            if constexpr (DT == SWH_F32) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) w[k] = __float_as_uint(grad(x[k], j0 + k));
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float lo = grad(x[2 * k], j0 + 2 * k), hi = grad(x[2 * k + 1], j0 + 2 * k + 1);
+                    const uint32_t blo = (DT == SWH_BF16) ? f32_to_bf16_bits(lo) : f32_to_f16_bits(lo);
+                    const uint32_t bhi = (DT == SWH_BF16) ? f32_to_bf16_bits(hi) : f32_to_f16_bits(hi);
+                    w[k] = blo | (bhi << 16);
+                }
+            }
+            st_nt(vout + v + u * kThreads, uint4{w[0], w[1], w[2], w[3]});
+        }
+    }
+    for (; v < nvec; v += kThreads) {
         float x[PV];
         unpack16<DT>(ld_nt(vin + v), x);
         const int64_t j0 = head + v * PV;

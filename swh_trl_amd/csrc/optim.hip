@@ -45,38 +45,6 @@ __global__ __launch_bounds__(kThreads) void finalize_clip_kernel(const float *__
 
 constexpr int kMaxNoDecay = 1024;  // no-decay ranges held in LDS
 
-#ifndef SWH_ADAM_U
-#define SWH_ADAM_U 2
-#endif
-#ifndef SWH_ADAM_NT
-#define SWH_ADAM_NT 0
-#endif
-template <typename T>
-__device__ __forceinline__ T ldg_nt(const T *p) {
-    if constexpr (SWH_ADAM_NT) return __builtin_nontemporal_load(p);
-    else return *p;
-}
-template <typename T>
-__device__ __forceinline__ void stg_nt(T *p, T v) {
-    if constexpr (SWH_ADAM_NT) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
-__device__ __forceinline__ float4 ldg4(const float4 *p) {
-    const float4 r{ldg_nt(&p->x), ldg_nt(&p->y), ldg_nt(&p->z), ldg_nt(&p->w)};
-    return r;
-}
-__device__ __forceinline__ uint2 ldg2(const uint2 *p) { return uint2{ldg_nt(&p->x), ldg_nt(&p->y)}; }
-__device__ __forceinline__ void stg4(float4 *p, float4 v) {
-    stg_nt(&p->x, v.x);
-    stg_nt(&p->y, v.y);
-    stg_nt(&p->z, v.z);
-    stg_nt(&p->w, v.w);
-}
-__device__ __forceinline__ void stg2(uint2 *p, uint2 v) {
-    stg_nt(&p->x, v.x);
-    stg_nt(&p->y, v.y);
-}
-
 // WM: 0 = no model copy, SWH_BF16 = bf16 copy, SWH_F32 = fp32 copy.  NR: the
 // no-decay range table is consulted (binary search in LDS per float4 group;
 // ranges are 4-aligned so a group never straddles one).
@@ -120,10 +88,8 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float *__restrict__ p, 
         const float denom = sqrtf(vv) / bc2_sqrt + eps;
         pp = pp - step_size * (mm / denom);
     };
-    // U grid-strided float4 groups per trip, every load of the trip issued before any math;
-    // the streams are touched once: non-temporal loads / stores (SWH_ADAM_NT) keep them out
-    // of the caches' way
-    constexpr int U = SWH_ADAM_U;
+    // U grid-strided float4 groups per trip, every load of the trip issued before any math
+    constexpr int U = 2;
     for (int64_t i0 = (int64_t)blockIdx.x * kThreads + threadIdx.x; i0 < n4; i0 += U * stride) {
         float4 pp[U], mm[U], vv[U];
         float gg[U][4];
@@ -131,14 +97,14 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float *__restrict__ p, 
         for (int u = 0; u < U; ++u) {
             const int64_t i = i0 + u * stride;
             if (i < n4) {
-                pp[u] = ldg4(reinterpret_cast<float4 *>(p) + i);
-                mm[u] = ldg4(reinterpret_cast<float4 *>(m) + i);
-                vv[u] = ldg4(reinterpret_cast<float4 *>(v) + i);
+                pp[u] = reinterpret_cast<float4 *>(p)[i];
+                mm[u] = reinterpret_cast<float4 *>(m)[i];
+                vv[u] = reinterpret_cast<float4 *>(v)[i];
                 if constexpr (GDT == SWH_F32) {
-                    const float4 t = ldg4(reinterpret_cast<const float4 *>(g) + i);
+                    const float4 t = reinterpret_cast<const float4 *>(g)[i];
                     gg[u][0] = t.x; gg[u][1] = t.y; gg[u][2] = t.z; gg[u][3] = t.w;
                 } else {
-                    const uint2 t = ldg2(reinterpret_cast<const uint2 *>(g) + i);
+                    const uint2 t = reinterpret_cast<const uint2 *>(g)[i];
                     gg[u][0] = Elem<GDT>::load(reinterpret_cast<const uint16_t *>(&t.x));
                     gg[u][1] = Elem<GDT>::load(reinterpret_cast<const uint16_t *>(&t.x) + 1);
                     gg[u][2] = Elem<GDT>::load(reinterpret_cast<const uint16_t *>(&t.y));
@@ -155,14 +121,14 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float *__restrict__ p, 
             upd(pp[u].y, mm[u].y, vv[u].y, gg[u][1], dc);
             upd(pp[u].z, mm[u].z, vv[u].z, gg[u][2], dc);
             upd(pp[u].w, mm[u].w, vv[u].w, gg[u][3], dc);
-            stg4(reinterpret_cast<float4 *>(p) + i, pp[u]);
-            stg4(reinterpret_cast<float4 *>(m) + i, mm[u]);
-            stg4(reinterpret_cast<float4 *>(v) + i, vv[u]);
-            if constexpr (WM == SWH_F32) stg4(reinterpret_cast<float4 *>(model32) + i, pp[u]);
+            reinterpret_cast<float4 *>(p)[i] = pp[u];
+            reinterpret_cast<float4 *>(m)[i] = mm[u];
+            reinterpret_cast<float4 *>(v)[i] = vv[u];
+            if constexpr (WM == SWH_F32) reinterpret_cast<float4 *>(model32)[i] = pp[u];
             if constexpr (WM == SWH_BF16) {
                 const uint32_t lo = (uint32_t)f32_to_bf16_bits(pp[u].x) | ((uint32_t)f32_to_bf16_bits(pp[u].y) << 16);
                 const uint32_t hi = (uint32_t)f32_to_bf16_bits(pp[u].z) | ((uint32_t)f32_to_bf16_bits(pp[u].w) << 16);
-                stg2(reinterpret_cast<uint2 *>(model) + i, uint2{lo, hi});
+                reinterpret_cast<uint2 *>(model)[i] = uint2{lo, hi};
             }
         }
     }

@@ -156,16 +156,19 @@ class _Linear(torch.autograd.Function):
         return dx, None, None, None, None
 
 
-# swh_gemm_nt / swh_gemm_tn (csrc/tgemm.hip) serve the narrow projections (qkv, o):
-# N <= 1536 outputs, where hipBLASLt's best solutions run at 0.43-0.69 PFLOP/s.
-# SWH_TGEMM=1 turns them on (A/B: tools/bench_tgemm.py, tools/train_kernels.py).
-_TGEMM = os.environ.get("SWH_TGEMM", "0") != "0"
+# swh_gemm_nt / swh_gemm_tn (csrc/tgemm.hip) for the narrow projections (qkv, o:
+# N, K <= 1536).  SWH_TGEMM = off | wgrad (the weight gradients only) | all (also
+# the forward and input-gradient GEMMs).  A/B: tools/bench_tgemm.py, tools/train_kernels.py.
+_TGEMM = os.environ.get("SWH_TGEMM", "wgrad")
 _TGEMM_MAX_N = 1536
 _TGEMM_SPLITS = int(os.environ.get("SWH_TGEMM_SPLITS", "8"))
+if _TGEMM not in ("off", "wgrad", "all"):
+    raise ValueError(f"SWH_TGEMM={_TGEMM!r}: expected off | wgrad | all")
 
 
-def _tgemm_serves(n_out: int, k_in: int) -> bool:
-    return _TGEMM and n_out <= _TGEMM_MAX_N and k_in <= _TGEMM_MAX_N
+def _tgemm_serves(n_out: int, k_in: int, wgrad: bool = False) -> bool:
+    on = _TGEMM == "all" or (wgrad and _TGEMM == "wgrad")
+    return on and n_out <= _TGEMM_MAX_N and k_in <= _TGEMM_MAX_N
 
 
 def _accumulate_dw(gw, gb, dy, x):
@@ -175,7 +178,7 @@ def _accumulate_dw(gw, gb, dy, x):
         dy2 = dy.reshape(-1, dy.shape[-1])
         x2 = x.reshape(-1, x.shape[-1])
         S = _dw_split(dy2.shape[0], dy2.shape[1] * x2.shape[1])
-        if _tgemm_serves(dy2.shape[1], x2.shape[1]) and gw.is_contiguous() and nn_ops.gemm_tn_eligible(dy2, x2):
+        if _tgemm_serves(dy2.shape[1], x2.shape[1], wgrad=True) and gw.is_contiguous() and nn_ops.gemm_tn_eligible(dy2, x2):
             # fp32 partials over 8 token ranges (one per XCD), folded in order (no fence needed:
             # the kernel is not persistent)
             side.keep(nn_ops.gemm_tn_accumulate(gw.view(dy2.shape[1], x2.shape[1]), dy2, x2, _TGEMM_SPLITS))

@@ -30,6 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tokens", type=int, default=17408)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--wgrad-only", action="store_true")
     a = ap.parse_args()
     from swh_trl_amd import _lib, gemm_tuning, nn_ops
     _lib.load()
@@ -37,7 +38,7 @@ def main():
     bf = dict(device="cuda", dtype=torch.bfloat16)
     g = torch.Generator(device="cpu").manual_seed(0)
     M = a.tokens
-    for name, N, K, bias in (("qkv fwd", 1152, 896, True), ("o fwd", 896, 896, False),
+    for name, N, K, bias in () if a.wgrad_only else (("qkv fwd", 1152, 896, True), ("o fwd", 896, 896, False),
                              ("qkv dgrad", 896, 1152, False), ("o dgrad", 896, 896, False),
                              ("down-shaped", 896, 4864, False), ("gate_up-shaped", 9728, 896, False)):
         x = torch.randn(M, K, generator=g).to(**bf)
@@ -56,7 +57,7 @@ def main():
     # weight gradients: the product's current path (token-split bmm + swh_dw_reduce) against gemm_tn
     from swh_trl_amd._lib import call
     from swh_trl_amd.engine.model import _dw_split
-    from swh_trl_amd.ops import _stream
+    from swh_trl_amd.ops import _dtype_code, _stream
     for name, N, K in (("qkv wgrad", 1152, 896), ("o wgrad", 896, 896), ("down wgrad", 896, 4864)):
         dy = (torch.randn(M, N, generator=g) * 0.01).to(**bf)
         x = torch.randn(M, K, generator=g).to(**bf)
@@ -67,7 +68,7 @@ def main():
         def lib():
             if S > 1:
                 parts = torch.bmm(dy[:S * Kc].view(S, Kc, -1).transpose(1, 2), x[:S * Kc].view(S, Kc, -1))
-                call("swh_dw_reduce", parts.data_ptr(), S, gw.numel(), gw.data_ptr(), 0, _stream())
+                call("swh_dw_reduce", parts.data_ptr(), S, gw.numel(), gw.data_ptr(), _dtype_code(gw, "dw"), _stream())
             else:
                 gw.addmm_(dy.t(), x)
         tl = _t(lib, a.reps)
