@@ -20,46 +20,94 @@ namespace swh {
 namespace {
 
 constexpr int kGT = 128;   // tile rows / columns
-constexpr int kGK = 64;    // K step
+constexpr int kGK = 64;    // K granule of the shapes served (the K step is BK = 32 or 64)
 constexpr int kGThreads = 256;
-constexpr int kGStage = kGT * kGK * 2;  // bytes of one operand tile (16 KB)
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8g __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ bf16x8g as_bf(const uint4 &v) { return __builtin_bit_cast(bf16x8g, v); }
 
-// byte offset of 16-B chunk c (0..7) of tile row r in the swizzled image
-__device__ __forceinline__ int gsw(int r, int c) { return r * (kGK * 2) + ((c ^ ((r >> 1) & 7)) << 4); }
+// LDS reads as inline asm, so that the next k-step's fragments are requested before the
+// current k-step's MFMAs (the compiler's own reads waited for each other); the caller
+// waits (lgkmcnt) before using the data.
+typedef uint32_t u32x4g __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2g __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t lds_off(const unsigned char *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) unsigned char *)p;
+}
+__device__ __forceinline__ uint4 lds_rd128(uint32_t a) {
+    u32x4g v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
+    return uint4{v.x, v.y, v.z, v.w};
+}
+__device__ __forceinline__ uint2 lds_rd_tr16(uint32_t a) {
+    u32x2g v;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
+    return uint2{v.x, v.y};
+}
+__device__ __forceinline__ void lgkm_wait0() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs behind the wait (they touch no memory)
+}
 
-template <bool BIAS>
+// byte offset of 16-B chunk c of tile row r in the swizzled [128][BK] image: rows of
+// 2 BK bytes, 256 / (2 BK) rows per 256-B bank row; chunk c sits at c ^ (bank row % chunks)
+template <int BK>
+__device__ __forceinline__ int gsw(int r, int c) {
+    constexpr int CPR = BK / 8, SH = (BK == 64) ? 1 : 2;
+    return r * (BK * 2) + ((c ^ ((r >> SH) & (CPR - 1))) << 4);
+}
+
+// The K loop over the two LDS stages: issue the next stage, compute this one, drain,
+// barrier.  (Deeper pipelines measured no faster: 3-4 stages of 32- or 64-wide K steps
+// with counted vmcnt waits across raw barriers)
+template <int NS, int LPS, typename Stage, typename Compute>
+__device__ __forceinline__ void gemm_kloop(int nk, Stage stage, Compute compute) {
+    static_assert(NS == 2, "two stages");
+    if (nk <= 0) return;
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int ks = 0; ks < nk; ++ks) {
+        if (ks + 1 < nk) stage((ks + 1) & 1, ks + 1);
+        compute(ks & 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+}
+
+template <bool BIAS, int NS, int BK>
 __global__ __launch_bounds__(kGThreads) void gemm_nt_kernel(const uint16_t *__restrict__ A,
                                                             const uint16_t *__restrict__ B,
                                                             const uint16_t *__restrict__ bias, uint16_t *__restrict__ C,
                                                             int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char gl[];  // [2 buffers][A | B] (64 KB)
+    extern __shared__ __attribute__((aligned(16))) unsigned char gl[];  // [NS buffers][A | B]
+    constexpr int SB = kGT * BK * 2, JL = BK / 16, CPR = BK / 8, RPI = 512 / BK, SH = (BK == 64) ? 1 : 2;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     // XCD-contiguous tile order: workgroup ids land on XCD id % 8 round robin
     const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q = nwg >> 3, r8 = nwg & 7;
     const int t = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
     const int ntn = N / kGT;
     const int m0 = (t / ntn) * kGT, n0 = (t % ntn) * kGT;
-    const int nk = K / kGK;
+    const int nk = K / BK;
 
-    // staging: wave w's load j fills image bytes [(4 j + w) KB, +1 KB) = rows 8 (4 j + w) .. +7,
-    // lane l -> row 8 (4 j + w) + l / 8, position l % 8, holding source chunk (l % 8) ^ swz
-    const uint16_t *asrc[4], *bsrc[4];
+    // staging: wave w's load j fills image bytes [(4 j + w) KB, +1 KB) = RPI rows from
+    // RPI (4 j + w), lane l -> row RPI (4 j + w) + l / CPR, position l % CPR, holding
+    // source chunk (l % CPR) ^ swz
+    const uint16_t *asrc[4], *bsrc[4];  // JL <= 4 used (a dependent extent breaks the host pass)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int row = 8 * (4 * j + wid) + (lane >> 3);
-        const int c = (lane & 7) ^ ((row >> 1) & 7);
+    for (int j = 0; j < JL; ++j) {
+        const int row = RPI * (4 * j + wid) + lane / CPR;
+        const int c = (lane % CPR) ^ ((row >> SH) & (CPR - 1));
         asrc[j] = A + (int64_t)min(m0 + row, M - 1) * lda + c * 8;
         bsrc[j] = B + (int64_t)(n0 + row) * ldb + c * 8;
     }
-    auto stage = [=](int buf, int k0) {
-        unsigned char *ai = gl + buf * 2 * kGStage, *bi = ai + kGStage;
+    auto stage = [=](int buf, int ks) {
+        unsigned char *ai = gl + buf * 2 * SB, *bi = ai + SB;
+        const int k0 = ks * BK;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < JL; ++j) {
             __builtin_amdgcn_global_load_lds(asrc[j] + k0, (__attribute__((address_space(3))) void *)(ai + (4 * j + wid) * 1024),
                                              16, 0, 0);
             __builtin_amdgcn_global_load_lds(bsrc[j] + k0, (__attribute__((address_space(3))) void *)(bi + (4 * j + wid) * 1024),
@@ -76,30 +124,30 @@ __global__ __launch_bounds__(kGThreads) void gemm_nt_kernel(const uint16_t *__re
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int ks = 0; ks < nk; ++ks) {
-        const int cur = ks & 1;
-        if (ks + 1 < nk) stage(cur ^ 1, (ks + 1) * kGK);
-        const unsigned char *ai = gl + cur * 2 * kGStage, *bi = ai + kGStage;
-#pragma unroll
-        for (int kk = 0; kk < kGK / 16; ++kk) {
-            uint4 a[2], b[2];
+    const uint32_t g0 = lds_off(gl);
+    gemm_kloop<NS, 2 * JL>(nk, stage, [&](int cur) {
+        const uint32_t ai = g0 + cur * 2 * SB, bi = ai + SB;
+        uint4 a[2][2], b[2][2];  // [k-step parity][block]: the next k-step's fragments load under the MFMAs
+        auto rd = [&](int kk) {
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                a[i] = *reinterpret_cast<const uint4 *>(ai + gsw(wm * 64 + i * 32 + r32, 2 * kk + h));
-                b[i] = *reinterpret_cast<const uint4 *>(bi + gsw(wn * 64 + i * 32 + r32, 2 * kk + h));
+                a[kk & 1][i] = lds_rd128(ai + gsw<BK>(wm * 64 + i * 32 + r32, 2 * kk + h));
+                b[kk & 1][i] = lds_rd128(bi + gsw<BK>(wn * 64 + i * 32 + r32, 2 * kk + h));
             }
+        };
+        rd(0);
+#pragma unroll
+        for (int kk = 0; kk < BK / 16; ++kk) {
+            lgkm_wait0();
+            if (kk + 1 < BK / 16) rd(kk + 1);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(a[i]), as_bf(b[j]), acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(a[kk & 1][i]), as_bf(b[kk & 1][j]),
+                                                                        acc[i][j], 0, 0, 0);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
+    });
 
     // epilogue: the wave's 64 x 64 bf16 tile through LDS (row pitch 72 elements), then
     // 16-B row stores: lane l -> row l / 8 + 8 it, columns 8 (l % 8) .. +7
@@ -145,47 +193,45 @@ __device__ __forceinline__ int tsw(int r, int c) { return r * 256 + ((c ^ (((r &
 // the 32 x 32 x 16 operand [32 columns from cb][16 tokens from tb] of an image: lane
 // (group G = l / 16, i = 4 q + p) reads rows tb + 8 (G >> 1) + q (+ 4), columns
 // cb + 16 (G & 1) + 4 p .. + 3; element j of the result is token 8 h + j of column l % 32
-__device__ __forceinline__ uint4 tr_operand(const unsigned char *img, int tb, int cb, int lane) {
+__device__ __forceinline__ uint4 tr_operand(uint32_t img, int tb, int cb, int lane) {
     const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
     const int row = tb + 8 * (G >> 1) + q, col = cb + 16 * (G & 1);
     const int ch = (col >> 3) + (p >> 1), hb = 8 * (p & 1);
-    const bf16x4t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) bf16x4t *)(img + tsw(row, ch) + hb));
-    const bf16x4t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) bf16x4t *)(img + tsw(row + 4, ch) + hb));
-    const uint2 l2 = __builtin_bit_cast(uint2, lo), h2 = __builtin_bit_cast(uint2, hi);
+    const uint2 l2 = lds_rd_tr16(img + tsw(row, ch) + hb), h2 = lds_rd_tr16(img + tsw(row + 4, ch) + hb);
     return uint4{l2.x, l2.y, h2.x, h2.y};
 }
 
+template <int NS, int BK>
 __global__ __launch_bounds__(kGThreads) void gemm_tn_kernel(const uint16_t *__restrict__ DY,
                                                             const uint16_t *__restrict__ X, float *__restrict__ part,
                                                             int M, int N, int K, int64_t lddy, int64_t ldx, int S,
                                                             int sps) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char gl[];  // [2 buffers][dY | X] (64 KB)
+    extern __shared__ __attribute__((aligned(16))) unsigned char gl[];  // [NS buffers][dY | X]
+    constexpr int SB = BK * kGT * 2, JL = BK / 16;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     const int ntn = N / kGT, ntk = K / kGT, tiles = ntn * ntk;
     const int s = t / tiles, tt = t - s * tiles;  // the tiles of one split share its token rows: one XCD
     const int n0 = (tt / ntk) * kGT, k0 = (tt % ntk) * kGT;
-    const int steps = M / kGK, st0 = s * sps, nk = max(0, min(sps, steps - st0));
+    const int steps = M / BK, st0 = s * sps, nk = max(0, min(sps, steps - st0));
 
-    const uint16_t *dsrc[4], *xsrc[4];
+    const uint16_t *dsrc[4], *xsrc[4];  // JL <= 4 used
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {  // load u = 4 j + w: rows 4 u .. 4 u + 3, lane -> row 4 u + l / 16, position l % 16
+    for (int j = 0; j < JL; ++j) {  // load u = 4 j + w: rows 4 u .. 4 u + 3, lane -> row 4 u + l / 16, position l % 16
         const int row = 4 * (4 * j + wid) + (lane >> 4), p = lane & 15;
         const int c = p ^ (((row & 3) << 2) | ((row >> 2) & 3));
-        const int64_t tok = (int64_t)st0 * kGK + row;
+        const int64_t tok = (int64_t)st0 * BK + row;
         dsrc[j] = DY + tok * lddy + n0 + c * 8;
         xsrc[j] = X + tok * ldx + k0 + c * 8;
     }
     auto stage = [=](int buf, int ks) {
-        unsigned char *di = gl + buf * 2 * kGStage, *xi = di + kGStage;
+        unsigned char *di = gl + buf * 2 * SB, *xi = di + SB;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            __builtin_amdgcn_global_load_lds(dsrc[j] + (int64_t)ks * kGK * lddy,
+        for (int j = 0; j < JL; ++j) {
+            __builtin_amdgcn_global_load_lds(dsrc[j] + (int64_t)ks * BK * lddy,
                                              (__attribute__((address_space(3))) void *)(di + (4 * j + wid) * 1024), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(xsrc[j] + (int64_t)ks * kGK * ldx,
+            __builtin_amdgcn_global_load_lds(xsrc[j] + (int64_t)ks * BK * ldx,
                                              (__attribute__((address_space(3))) void *)(xi + (4 * j + wid) * 1024), 16, 0, 0);
         }
     };
@@ -197,32 +243,30 @@ __global__ __launch_bounds__(kGThreads) void gemm_tn_kernel(const uint16_t *__re
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    if (nk > 0) {
-        stage(0, 0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
-    for (int ks = 0; ks < nk; ++ks) {
-        const int cur = ks & 1;
-        if (ks + 1 < nk) stage(cur ^ 1, ks + 1);
-        const unsigned char *di = gl + cur * 2 * kGStage, *xi = di + kGStage;
-#pragma unroll
-        for (int kk = 0; kk < kGK / 16; ++kk) {
-            uint4 a[2], b[2];
+    const uint32_t g0 = lds_off(gl);
+    gemm_kloop<NS, 2 * JL>(nk, stage, [&](int cur) {
+        const uint32_t di = g0 + cur * 2 * SB, xi = di + SB;
+        uint4 a[2][2], b[2][2];  // [k-step parity][block], as in gemm_nt_kernel
+        auto rd = [&](int kk) {
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                a[i] = tr_operand(di, kk * 16, wm * 64 + i * 32, lane);
-                b[i] = tr_operand(xi, kk * 16, wn * 64 + i * 32, lane);
+                a[kk & 1][i] = tr_operand(di, kk * 16, wm * 64 + i * 32, lane);
+                b[kk & 1][i] = tr_operand(xi, kk * 16, wn * 64 + i * 32, lane);
             }
+        };
+        rd(0);
+#pragma unroll
+        for (int kk = 0; kk < BK / 16; ++kk) {
+            lgkm_wait0();
+            if (kk + 1 < BK / 16) rd(kk + 1);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(a[i]), as_bf(b[j]), acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(a[kk & 1][i]), as_bf(b[kk & 1][j]),
+                                                                        acc[i][j], 0, 0, 0);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
+    });
     // fp32 partial: register e of block (i, j) is row n0 + 64 wm + 32 i + (e & 3) + 8 (e >> 2) + 4 h,
     // column k0 + 64 wn + 32 j + l % 32 (128 contiguous bytes per half-wave)
     float *ps = part + (int64_t)s * N * K;
@@ -274,6 +318,30 @@ __global__ __launch_bounds__(256) void tn_fold_kernel(const float *__restrict__ 
 
 using namespace swh;
 
+template <typename K>
+static bool lds_attr(K *kern, int bytes) {
+    return hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               bytes) == hipSuccess;
+}
+
+template <int NS, int BK>
+static int launch_nt(const void *A, const void *B, const void *bias, void *C, int64_t M, int64_t N, int64_t K,
+                     int64_t lda, int64_t ldb, int64_t ldc, int64_t tiles, hipStream_t s) {
+    constexpr int lds = NS * 2 * kGT * BK * 2;
+    static const bool attr =
+        lds_attr(&gemm_nt_kernel<true, NS, BK>, lds) && lds_attr(&gemm_nt_kernel<false, NS, BK>, lds);
+    if (!attr) return SWH_E_LAUNCH;
+    if (bias)
+        gemm_nt_kernel<true, NS, BK><<<(unsigned)tiles, kGThreads, lds, s>>>(
+            static_cast<const uint16_t *>(A), static_cast<const uint16_t *>(B), static_cast<const uint16_t *>(bias),
+            static_cast<uint16_t *>(C), (int)M, (int)N, (int)K, lda, ldb, ldc);
+    else
+        gemm_nt_kernel<false, NS, BK><<<(unsigned)tiles, kGThreads, lds, s>>>(
+            static_cast<const uint16_t *>(A), static_cast<const uint16_t *>(B), nullptr, static_cast<uint16_t *>(C),
+            (int)M, (int)N, (int)K, lda, ldb, ldc);
+    return launch_status();
+}
+
 extern "C" int swh_gemm_nt(const void *A, const void *B, const void *bias, void *C, int64_t M, int64_t N, int64_t K,
                            int64_t lda, int64_t ldb, int64_t ldc, void *stream) {
     if (!A || !B || !C || M < 0 || N < 0 || K <= 0) return SWH_E_ARG;
@@ -285,23 +353,19 @@ extern "C" int swh_gemm_nt(const void *A, const void *B, const void *bias, void 
     const int64_t tiles = ((M + kGT - 1) / kGT) * (N / kGT);
     if (tiles > INT32_MAX) return SWH_E_ARG;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    static bool attr = false;
-    if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&gemm_nt_kernel<true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kGStage) != hipSuccess ||
-            hipFuncSetAttribute(reinterpret_cast<const void *>(&gemm_nt_kernel<false>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kGStage) != hipSuccess)
-            return SWH_E_LAUNCH;
-        attr = true;
-    }
-    if (bias)
-        gemm_nt_kernel<true><<<(unsigned)tiles, kGThreads, 4 * kGStage, s>>>(
-            static_cast<const uint16_t *>(A), static_cast<const uint16_t *>(B), static_cast<const uint16_t *>(bias),
-            static_cast<uint16_t *>(C), (int)M, (int)N, (int)K, lda, ldb, ldc);
-    else
-        gemm_nt_kernel<false><<<(unsigned)tiles, kGThreads, 4 * kGStage, s>>>(
-            static_cast<const uint16_t *>(A), static_cast<const uint16_t *>(B), nullptr, static_cast<uint16_t *>(C),
-            (int)M, (int)N, (int)K, lda, ldb, ldc);
+    return launch_nt<2, 64>(A, B, bias, C, M, N, K, lda, ldb, ldc, tiles, s);
+}
+
+template <int NS, int BK>
+static int launch_tn(const void *dY, const void *X, float *part, int64_t M, int64_t N, int64_t K, int64_t lddy,
+                     int64_t ldx, int S, int64_t grid, hipStream_t s) {
+    constexpr int lds = NS * 2 * kGT * BK * 2;
+    static const bool attr = lds_attr(&gemm_tn_kernel<NS, BK>, lds);
+    if (!attr) return SWH_E_LAUNCH;
+    const int steps = (int)(M / BK), sps = (steps + S - 1) / S;
+    gemm_tn_kernel<NS, BK><<<(unsigned)grid, kGThreads, lds, s>>>(static_cast<const uint16_t *>(dY),
+                                                                   static_cast<const uint16_t *>(X), part, (int)M,
+                                                                   (int)N, (int)K, lddy, ldx, S, sps > 1 ? sps : 1);
     return launch_status();
 }
 
@@ -314,19 +378,8 @@ extern "C" int swh_gemm_tn_partials(const void *dY, const void *X, float *part, 
     if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX || S > 1024) return SWH_E_ARG;
     const int64_t grid = (N / kGT) * (K / kGT) * (int64_t)S;
     if (grid > INT32_MAX) return SWH_E_ARG;
-    const int steps = (int)(M / kGK), sps = (steps + S - 1) / S;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    static bool attr = false;
-    if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&gemm_tn_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kGStage) != hipSuccess)
-            return SWH_E_LAUNCH;
-        attr = true;
-    }
-    gemm_tn_kernel<<<(unsigned)grid, kGThreads, 4 * kGStage, s>>>(static_cast<const uint16_t *>(dY),
-                                                                   static_cast<const uint16_t *>(X), part, (int)M,
-                                                                   (int)N, (int)K, lddy, ldx, S, sps > 1 ? sps : 1);
-    return launch_status();
+    return launch_tn<2, 64>(dY, X, part, M, N, K, lddy, ldx, S, grid, s);
 }
 
 extern "C" int swh_gemm_tn_fold(const float *part, int32_t S, int64_t n, void *grad, int32_t dtype, void *stream) {
