@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--tokens", type=int, default=17408)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--wgrad-only", action="store_true")
+    ap.add_argument("--fwd-only", action="store_true")
     a = ap.parse_args()
     from swh_trl_amd import _lib, gemm_tuning, nn_ops
     _lib.load()
@@ -40,7 +41,8 @@ def main():
     M = a.tokens
     for name, N, K, bias in () if a.wgrad_only else (("qkv fwd", 1152, 896, True), ("o fwd", 896, 896, False),
                              ("qkv dgrad", 896, 1152, False), ("o dgrad", 896, 896, False),
-                             ("down-shaped", 896, 4864, False), ("gate_up-shaped", 9728, 896, False)):
+                             ("down-shaped", 896, 4864, False), ("gate_up-shaped", 9728, 896, False),
+                             ("down dgrad", 4864, 896, False), ("gate_up dgrad", 896, 9728, False)):
         x = torch.randn(M, K, generator=g).to(**bf)
         w = (torch.randn(N, K, generator=g) * 0.03).to(**bf)
         b = (torch.randn(N, generator=g) * 0.1).to(**bf) if bias else None
@@ -58,7 +60,7 @@ def main():
     from swh_trl_amd._lib import call
     from swh_trl_amd.engine.model import _dw_split
     from swh_trl_amd.ops import _dtype_code, _stream
-    for name, N, K in (("qkv wgrad", 1152, 896), ("o wgrad", 896, 896), ("down wgrad", 896, 4864)):
+    for name, N, K in () if a.fwd_only else (("qkv wgrad", 1152, 896), ("o wgrad", 896, 896), ("down wgrad", 896, 4864)):
         dy = (torch.randn(M, N, generator=g) * 0.01).to(**bf)
         x = torch.randn(M, K, generator=g).to(**bf)
         gw = torch.zeros(N, K, **bf)
