@@ -1610,7 +1610,8 @@ def test_attn_decode_l3_warmup_is_result_neutral(ops, dev, B, Hkv, G):
 
 # --------------------------------------------------------------------------- training projection GEMM
 @pytest.mark.parametrize("M,N,K,bias", [(17408, 1152, 896, True), (300, 128, 64, False), (1000, 896, 896, True),
-                                        (2048, 896, 1152, False), (1, 256, 128, True)])
+                                        (2048, 896, 1152, False), (1, 256, 128, True), (2048, 9728, 896, False),
+                                        (4096, 4864, 896, True), (300, 256, 64, False), (700, 512, 192, True)])
 def test_gemm_nt_matches_fp32_product(dev, M, N, K, bias):
     """swh_gemm_nt (the qkv / o projections of the training pass) against the
     fp32 product of the same bf16 operands: the kernel accumulates in fp32 and
