@@ -1,9 +1,11 @@
-// Training-side projection GEMM for the narrow projections (qkv: N 1152, o: N 896)
-// of the full-sequence forward / input-gradient passes, where hipBLASLt's best
-// solution for M = 17408, K = 896 runs at 0.43-0.69 PFLOP/s (profiles/r3_gemm_eff.log).
+// Training-side GEMMs for the narrow projections (qkv: N 1152, o: N 896) of the
+// full-sequence pass, where hipBLASLt's best solutions for M = 17408, K = 896 run at
+// 0.4-0.8 PFLOP/s (profiles/r3_gemm_eff.log, profiles/r4_tgemm_pipe.log):
 //
-//   C[M, N] = A[M, K] · B[N, K]^T (+ bias[N]),  bf16 in / out, fp32 accumulation
+//   gemm_nt:  C[M, N] = A[M, K] · B[N, K]^T (+ bias[N])   forward / input gradient (SWH_TGEMM=all)
+//   gemm_tn:  part[s] = dY[tokens of s]^T X, folded        weight gradient (default)
 //
+// bf16 in / out, fp32 accumulation.  gemm_nt:
 // 128 x 128 output tiles, 4 waves (2 x 2, 64 x 64 each on v_mfma_f32_32x32x16_bf16),
 // 64-wide K steps staged by LDS-DMA (global_load_lds, 16 B per lane) into a double
 // buffer of 64 KB (two workgroups per CU).  The LDS image is lane-linear; the bank
