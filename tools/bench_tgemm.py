@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--wgrad-only", action="store_true")
     ap.add_argument("--fwd-only", action="store_true")
+    ap.add_argument("--splits", type=int, nargs="*", default=None)
     a = ap.parse_args()
     from swh_trl_amd import _lib, gemm_tuning, nn_ops
     _lib.load()
@@ -76,7 +77,7 @@ def main():
         tl = _t(lib, a.reps)
         fl = 2 * M * N * K
         res = [f"{name:15s} M {M} N {N} K {K}: library S{S} {tl:7.1f} us ({fl / tl / 1e6:5.0f} TF/s)"]
-        for S2 in (4, 8, 16):
+        for S2 in (a.splits or (4, 8, 16)):
             g2 = torch.zeros(N, K, device="cuda", dtype=torch.float32)
             tm = _t(lambda: nn_ops.gemm_tn_accumulate(g2, dy, x, S2), a.reps)
             res.append(f"tn S{S2} {tm:7.1f} us ({fl / tm / 1e6:5.0f})")
