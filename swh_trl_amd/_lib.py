@@ -174,3 +174,17 @@ def check(status: int, name: str) -> None:
 
 def call(name: str, *args) -> None:
     check(getattr(load(), name)(*args), name)
+
+
+def dtype_code(t, name: str) -> int:
+    """The `int dtype` argument of an entry point, taken from the tensor it
+    describes.  The C-ABI cannot see buffer sizes, so a code that does not match
+    the buffer makes the kernel read / write the wrong element width (round 4:
+    a literal SWH_F32 passed for bf16 buffers wrote past both allocations);
+    every call site derives its code here (tests/test_abi.py checks that no
+    call passes a literal)."""
+    import torch
+    codes = {torch.float32: SWH_F32, torch.bfloat16: SWH_BF16, torch.float16: SWH_F16}
+    if t.dtype not in codes:
+        raise ValueError(f"swh_trl_amd.{name}: unsupported dtype {t.dtype}")
+    return codes[t.dtype]

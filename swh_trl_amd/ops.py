@@ -13,7 +13,6 @@ import torch
 from . import _lib, profiling
 from ._lib import GRPOLossParams, SampleParams, call
 
-_DT = {torch.float32: _lib.SWH_F32, torch.bfloat16: _lib.SWH_BF16, torch.float16: _lib.SWH_F16}
 
 
 def _dev(t: torch.Tensor, name: str) -> None:
@@ -29,10 +28,7 @@ def _stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
-def _dtype_code(t: torch.Tensor, name: str) -> int:
-    if t.dtype not in _DT:
-        raise ValueError(f"swh_trl_amd.{name}: unsupported dtype {t.dtype}")
-    return _DT[t.dtype]
+_dtype_code = _lib.dtype_code   # the one place a dtype code is made (from the tensor)
 
 
 # ---------------------------------------------------------------------------

@@ -1,13 +1,17 @@
 """GRPOConfig — field names and defaults of trl/trainer/grpo_config.py:227-616
 (the subset that shapes the per-step hot path, plus the TrainingArguments
-fields the loop reads).  Unknown keyword arguments are kept (and ignored)
-so reference configs construct unchanged; vLLM / Liger switches raise, as
-those paths are out of scope."""
+fields the loop reads).  Other TrainingArguments keywords are accepted only
+where they cannot change the result (trainer/training_args.py: reporting,
+hub, data-loader workers, ... kept in `extra`) and raise otherwise, e.g.
+`optim="adafactor"`, `logging_strategy="epoch"`, `fp16=True`; vLLM / Liger
+switches raise, as those paths are out of scope."""
 from __future__ import annotations
 
 import os
 from dataclasses import dataclass, field
 from typing import Any, Optional
+
+from .training_args import split_known
 
 
 def _world_size() -> int:
@@ -97,8 +101,7 @@ class GRPOConfig:
     extra: dict = field(default_factory=dict)
 
     def __init__(self, **kwargs):
-        known = {f for f in self.__dataclass_fields__ if f != "extra"}
-        extra = {k: kwargs.pop(k) for k in list(kwargs) if k not in known}
+        extra = split_known(type(self), kwargs, frozenset({"evaluation_strategy"}))
         for name, f in self.__dataclass_fields__.items():
             if name != "extra":
                 setattr(self, name, kwargs.get(name, f.default))
@@ -107,6 +110,9 @@ class GRPOConfig:
 
     def __post_init__(self):
         """grpo_config.py:574-616 batch bookkeeping and validation."""
+        if self.fp16:
+            raise ValueError("fp16=True: the MI355X engine trains bf16 (or fp32, model_init_kwargs torch_dtype) "
+                             "models; fp16 mixed precision is not implemented")
         self.bf16 = (not self.fp16) if self.bf16 is None else self.bf16
         if self.use_vllm:
             raise ValueError("use_vllm=True: the vLLM generation path is out of scope; the device engine generates")

@@ -109,6 +109,89 @@ def load_model(model, device, trainable=True, seed=0, head: str = "lm", dtype=No
     raise TypeError(f"unsupported model type {type(model)}")
 
 
+# GenerationConfig keys (transformers >= 4.53) -> how the engine treats them
+_GEN_IMPLEMENTED = frozenset({"max_new_tokens", "min_new_tokens", "min_length", "do_sample", "pad_token_id",
+                              "eos_token_id", "temperature", "top_p", "top_k", "min_p", "repetition_penalty"})
+# cannot change the returned completion ids: cache / paged-attention / compile plumbing, the BOS id of a
+# decoder-only prompt, beam-only knobs, extra outputs that generate() returns only with return_dict_in_generate,
+# renormalisation after the processors (the sampled distribution is the same), max_length under max_new_tokens
+_GEN_INERT = frozenset({"bos_token_id", "cache_implementation", "cache_config", "max_cache_len", "use_cache",
+                        "max_batch_tokens", "num_blocks", "block_size", "compile_config", "disable_compile",
+                        "prefill_chunk_size", "length_penalty", "early_stopping", "low_memory", "output_attentions",
+                        "output_hidden_states", "output_scores", "output_logits", "renormalize_logits", "max_length",
+                        "transformers_version", "_from_model_config", "_commit_hash", "decoder_start_token_id",
+                        "is_assistant"})
+# processors / search modes the engine does not implement: accepted only at their no-op value
+_GEN_NOOP_VALUES = {"num_beams": (None, 1), "num_return_sequences": (None, 1), "num_beam_groups": (None, 1),
+                    "typical_p": (None, 1.0), "epsilon_cutoff": (None, 0.0), "eta_cutoff": (None, 0.0),
+                    "encoder_repetition_penalty": (None, 1.0), "guidance_scale": (None, 1.0),
+                    "no_repeat_ngram_size": (None, 0), "encoder_no_repeat_ngram_size": (None, 0),
+                    "diversity_penalty": (None, 0.0), "top_h": (None,), "penalty_alpha": (None,),
+                    "bad_words_ids": (None,), "suppress_tokens": (None,), "begin_suppress_tokens": (None,),
+                    "forced_bos_token_id": (None,), "forced_eos_token_id": (None,), "sequence_bias": (None,),
+                    "exponential_decay_length_penalty": (None,), "watermarking_config": (None,),
+                    "stop_strings": (None,), "max_time": (None,), "constraints": (None,), "force_words_ids": (None,),
+                    "dola_layers": (None,), "prompt_lookup_num_tokens": (None,), "num_assistant_tokens": (None,),
+                    "assistant_confidence_threshold": (None,), "assistant_early_exit": (None,),
+                    "remove_invalid_values": (None, False), "return_dict_in_generate": (None, False),
+                    "token_healing": (None, False), "use_mtp": (None, False)}
+
+
+def generation_config(args: GRPOConfig, tokenizer=None) -> dict:
+    """The sampling parameters of one rollout, built as grpo_trainer.py:995-1014
+    builds its GenerationConfig: the config fields first (max_new_tokens =
+    max_completion_length, do_sample, the tokenizer's pad / bos / eos, temperature,
+    top_p, top_k, min_p, repetition_penalty, cache_implementation), then
+    `args.generation_kwargs` on top.  Returns the resolved keys the engine
+    implements (HF semantics: a key left None is off).  Keys that cannot change the
+    completions are accepted and dropped; a processor or search mode the engine
+    does not implement raises unless it is at its no-op value.  The scoring passes
+    keep dividing by `args.temperature` (:1249), whatever the rollout sampled at."""
+    g = {"max_new_tokens": args.max_completion_length, "do_sample": True,
+         "pad_token_id": getattr(tokenizer, "pad_token_id", None), "bos_token_id": getattr(tokenizer, "bos_token_id", None),
+         "eos_token_id": getattr(tokenizer, "eos_token_id", None), "temperature": args.temperature,
+         "top_p": args.top_p, "top_k": args.top_k, "min_p": args.min_p,
+         "repetition_penalty": args.repetition_penalty, "cache_implementation": args.cache_implementation}
+    g.update(args.generation_kwargs or {})
+    bad = []
+    for k, v in g.items():
+        if k in _GEN_IMPLEMENTED or k in _GEN_INERT:
+            continue
+        if k in _GEN_NOOP_VALUES:
+            if v not in _GEN_NOOP_VALUES[k]:
+                bad.append(f"{k}={v!r}")
+            continue
+        bad.append(f"{k}={v!r} (unknown generation key)")
+    if bad:
+        raise ValueError("generation_kwargs: the MI355X decode engine does not implement " + ", ".join(bad))
+    if g["max_new_tokens"] is None or int(g["max_new_tokens"]) < 1:
+        raise ValueError(f"max_new_tokens must be a positive integer, got {g['max_new_tokens']!r}")
+    do_sample = bool(g["do_sample"])
+    t = g["temperature"]
+    if do_sample and t is not None and not (float(t) > 0.0):
+        raise ValueError(f"`temperature` (={t}) has to be a strictly positive float, otherwise your next token "
+                         "scores will be invalid. If you're looking for greedy decoding strategies, set "
+                         "`do_sample=False`.")
+    if do_sample and g["top_p"] is not None and not (0.0 <= float(g["top_p"]) <= 1.0):
+        raise ValueError(f"`top_p` has to be a float > 0 and < 1, but is {g['top_p']}")
+    if do_sample and g["min_p"] is not None and not (0.0 <= float(g["min_p"]) <= 1.0):
+        raise ValueError(f"`min_p` has to be a float in the [0, 1] interval, but is {g['min_p']}")
+    if g["top_k"] is not None and int(g["top_k"]) < 0:
+        raise ValueError(f"`top_k` has to be a non-negative integer, but is {g['top_k']}")
+    rp = g["repetition_penalty"]
+    if rp is not None and not (float(rp) > 0.0):
+        raise ValueError(f"`penalty` has to be a strictly positive float, but is {rp}")
+    # _get_logits_processor: the warpers (temperature, top-k, top-p, min-p) only when sampling
+    return {"max_new_tokens": int(g["max_new_tokens"]), "min_new_tokens": int(g.get("min_new_tokens") or 0),
+            "min_length": int(g.get("min_length") or 0), "greedy": not do_sample,
+            "temperature": float(t) if (do_sample and t is not None) else 1.0,
+            "top_p": float(g["top_p"]) if (do_sample and g["top_p"] is not None) else 1.0,
+            "top_k": int(g["top_k"]) if (do_sample and g["top_k"]) else None,
+            "min_p": float(g["min_p"]) if (do_sample and g["min_p"] is not None) else None,
+            "repetition_penalty": float(rp) if rp is not None else 1.0,
+            "pad_token_id": g["pad_token_id"], "eos_token_id": g["eos_token_id"]}
+
+
 def _is_pretrained_model(f) -> bool:
     """transformers PreTrainedModel (without importing transformers when absent)."""
     return any(c.__name__ == "PreTrainedModel" for c in type(f).__mro__)
@@ -241,19 +324,28 @@ class GRPOTrainer:
         self.top_entropy_quantile = a.top_entropy_quantile
         self.max_prompt_length = a.max_prompt_length
         self.max_completion_length = a.max_completion_length
+        # the rollout's sampling parameters: config fields, then generation_kwargs on top (:995-1014)
+        gen = generation_config(a, processing_class)
+        # the trainer's own ids (prompt padding, completion mask :1812-1831) are the tokenizer's
+        # (:720-721); without a tokenizer (token-id datasets) the generation config's stand in
         tok = processing_class
         self.pad_token_id = getattr(tok, "pad_token_id", None)
         self.eos_token_id = getattr(tok, "eos_token_id", None)
-        gk = dict(a.generation_kwargs or {})
-        if "pad_token_id" in gk:
-            self.pad_token_id = gk["pad_token_id"]
-        if "eos_token_id" in gk:
-            self.eos_token_id = gk["eos_token_id"]
+        if self.eos_token_id is None:
+            self.eos_token_id = gen["eos_token_id"]
         if self.pad_token_id is None:
-            self.pad_token_id = self.eos_token_id if self.eos_token_id is not None else 0
-        self.gen_kwargs = dict(temperature=a.temperature, top_p=a.top_p, top_k=a.top_k, min_p=a.min_p,
-                               repetition_penalty=a.repetition_penalty, greedy=not gk.get("do_sample", True),
-                               min_new_tokens=int(gk.get("min_new_tokens", 0) or 0))
+            self.pad_token_id = gen["pad_token_id"]
+        if self.pad_token_id is None:
+            self.pad_token_id = self.eos_token_id if isinstance(self.eos_token_id, int) else 0
+        self.gen_max_new_tokens = gen.pop("max_new_tokens")
+        self.gen_min_length = gen.pop("min_length")
+        self.gen_eos_token_id = gen.pop("eos_token_id")
+        self.gen_pad_token_id = gen.pop("pad_token_id")
+        if self.gen_eos_token_id is None:
+            self.gen_eos_token_id = self.eos_token_id
+        if self.gen_pad_token_id is None:
+            self.gen_pad_token_id = self.pad_token_id
+        self.gen_kwargs = gen
         self.ref_model = None
         if self.beta != 0.0:
             self.ref_model = build_model(self.model.cfg, self.device, seed=None, trainable=False,
@@ -378,7 +470,7 @@ class GRPOTrainer:
         return ids, mask, texts
 
     def _engine_for(self, B: int, P: int) -> DecodeEngine:
-        C = self.max_completion_length
+        C = self.gen_max_new_tokens
         # the policy itself: bf16 on the DecodeEngine, an fp32 policy on the fp32
         # RefDecodeEngine (the reference generates in the model dtype, :1793-1810)
         # one engine per batch size (training and evaluation batches differ), built once
@@ -406,11 +498,14 @@ class GRPOTrainer:
         else:
             seed, count = a.seed * 1_000_003 + 7919 * (self.world + self.rank + 1), self._eval_count
             self._eval_count += 1
-        completion_ids, _ = eng.generate(prompt_ids, prompt_mask, self.max_completion_length,
-                                         eos_token_id=self.eos_token_id, pad_token_id=self.pad_token_id,
-                                         seed=seed, offset=count * (self.max_completion_length + 1),
+        gk = dict(self.gen_kwargs)
+        if self.gen_min_length:  # MinLengthLogitsProcessor counts the (padded) prompt: EOS off while P + t < min_length
+            gk["min_new_tokens"] = max(gk["min_new_tokens"], self.gen_min_length - P)
+        completion_ids, _ = eng.generate(prompt_ids, prompt_mask, self.gen_max_new_tokens,
+                                         eos_token_id=self.gen_eos_token_id, pad_token_id=self.gen_pad_token_id,
+                                         seed=seed, offset=count * (self.gen_max_new_tokens + 1),
                                          check_every=a.decode_check_every, group_size=self.num_generations,
-                                         early_exit=a.decode_early_exit, **self.gen_kwargs)
+                                         early_exit=a.decode_early_exit, **gk)
         _trace("generated")
         eos = [] if self.eos_token_id is None else self.eos_token_id
         completion_mask, lengths, has_eos = ops.completion_mask(completion_ids, eos,

@@ -2,13 +2,16 @@
 the OnPolicyConfig it extends (trl/trainer/utils.py:744-870), plus the
 TrainingArguments fields the loop reads.  The derived batch sizes
 (`local_batch_size`, `mini_batch_size`, ... ) are filled by PPOTrainer exactly
-as ppo_trainer.py:228-250 does.  Unknown keyword arguments are kept (and
-ignored) so reference configs construct unchanged."""
+as ppo_trainer.py:228-250 does.  Other TrainingArguments keywords are accepted
+only where they cannot change the result (trainer/training_args.py, kept in
+`extra`) and raise otherwise."""
 from __future__ import annotations
 
 import os
 from dataclasses import dataclass, field
 from typing import Any, Optional
+
+from .training_args import split_known
 
 
 @dataclass
@@ -32,6 +35,7 @@ class PPOConfig:
     eval_steps: Optional[float] = None
     save_steps: float = 500
     save_strategy: str = "steps"           # "steps" | "no" (TrainingArguments)
+    save_total_limit: Optional[int] = None
     seed: int = 42
     bf16: Optional[bool] = None            # OnPolicyConfig: not fp16 when unset (utils.py:870-873)
     fp16: bool = False
@@ -79,11 +83,14 @@ class PPOConfig:
     decode_check_every: int = 0            # legacy synchronous all-finished poll every k steps (0 = off)
     fuse_micro_batches: bool = True        # a mini-batch's GA micro-batches as one forward/backward
     fuse_token_budget: int = 1 << 16       # max rows * (query + response) tokens per fused pass
+    pad_token_id: Optional[int] = None     # token ids when no tokenizer object is given (processing_class None)
+    eos_token_id: Optional[int] = None
     extra: dict = field(default_factory=dict)
 
     def __init__(self, **kwargs):
-        known = {f for f in self.__dataclass_fields__ if f != "extra"}
-        extra = {k: kwargs.pop(k) for k in list(kwargs) if k not in known}
+        # the PPO loop logs every update and never runs Trainer.evaluate (ppo_trainer.py:646-659)
+        extra = split_known(type(self), kwargs, frozenset({"eval_strategy", "evaluation_strategy", "eval_on_start",
+                                                           "logging_first_step", "max_steps"}))
         for name, f in self.__dataclass_fields__.items():
             if name != "extra":
                 setattr(self, name, kwargs.get(name, f.default))
@@ -91,6 +98,14 @@ class PPOConfig:
         self.__post_init__()
 
     def __post_init__(self):
+        if self.fp16:
+            raise ValueError("fp16=True: the MI355X engine trains bf16 (or fp32) models; fp16 mixed precision is "
+                             "not implemented")
+        self.save_strategy = getattr(self.save_strategy, "value", self.save_strategy)
+        if self.save_strategy not in ("no", "steps"):
+            raise ValueError(f"save_strategy {self.save_strategy!r}: the MI355X trainer saves on 'steps' (or 'no')")
+        if self.push_to_hub:
+            raise ValueError("push_to_hub=True: no hub access from the MI355X trainer")
         self.bf16 = (not self.fp16) if self.bf16 is None else self.bf16
         if self.output_dir is None:
             self.output_dir = "trainer_output"

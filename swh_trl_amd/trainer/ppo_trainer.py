@@ -120,10 +120,10 @@ class PPOTrainer:
         tok = processing_class
         self.pad_token_id = getattr(tok, "pad_token_id", None)
         self.eos_token_id = getattr(tok, "eos_token_id", None)
-        if args.extra.get("pad_token_id") is not None:  # token ids without a tokenizer object
-            self.pad_token_id = args.extra["pad_token_id"]
-        if args.extra.get("eos_token_id") is not None:
-            self.eos_token_id = args.extra["eos_token_id"]
+        if args.pad_token_id is not None:  # token ids without a tokenizer object
+            self.pad_token_id = args.pad_token_id
+        if args.eos_token_id is not None:
+            self.eos_token_id = args.eos_token_id
         if self.pad_token_id is None:
             raise ValueError("PPOTrainer needs a pad token id (processing_class.pad_token_id)")
         # stop token (ppo_trainer.py:134-145)
@@ -184,6 +184,7 @@ class PPOTrainer:
         self.callback_handler = CallbackHandler(callbacks, self)
         self.control = self.callback_handler.control
         self._engine: Optional[DecodeEngine] = None
+        self._engines: dict = {}
         self._gen_count = 0
         self._np_rng = np.random.default_rng(self.local_seed)
         self._data_gen = torch.Generator().manual_seed(args.seed)
@@ -209,11 +210,15 @@ class PPOTrainer:
         return ids
 
     def _engine_for(self, B: int, P: int) -> DecodeEngine:
-        e = self._engine
+        """One engine per batch size (rollout and sample-generation batches may
+        differ), kept for the run: a rebuild repacks the weights and recaptures
+        the decode graph."""
         C = self.args.response_length
-        if e is None or e.B != B or e.Pmax < P:
-            self._engine = build_engine(self.policy_model, B, P, C)
-        return self._engine
+        e = self._engines.get(B)
+        if e is None or e.Pmax < P:
+            e = self._engines[B] = build_engine(self.policy_model, B, P, C)
+        self._engine = e
+        return e
 
     # ------------------------------------------------------------------ rollout (ppo_trainer.py:362-535)
     @torch.no_grad()
@@ -477,6 +482,7 @@ class PPOTrainer:
                 js = ck.trainer_state_json(self.state, a, a.per_device_train_batch_size)
                 js["episode"] = self.state.episode
                 json.dump(js, f, indent=2)
+            ck.rotate_checkpoints(a.output_dir, a.save_total_limit)
         swh_dist.barrier()
         return d
 
@@ -502,8 +508,12 @@ class PPOTrainer:
         if self.eval_dataset is None:
             return table
         tok = self.processing_class
+        # the eval DataLoader through accelerator.prepare (ppo_trainer.py:290): every
+        # global batch of bs x world rows is split into contiguous per-rank slices
         n, bs = len(self.eval_dataset), a.per_device_eval_batch_size
-        for s in range(0, n - bs + 1, bs):
+        glob = bs * self.world
+        for s0 in range(0, n - glob + 1, glob):
+            s = s0 + self.rank * bs
             query = self._queries([self.eval_dataset[i] for i in range(s, s + bs)])
             B, P = query.shape
             eng = self._engine_for(B, P)
@@ -562,9 +572,14 @@ class PPOTrainer:
             if self.rank == 0:
                 print(log, flush=True)
             self.control = cb.call("on_log", logs=log)
-            # DefaultFlowCallback.on_step_end: save every save_steps
+            # DefaultFlowCallback.on_step_end: save every save_steps, and stop (saving
+            # under the "steps" strategy) once max_steps is reached
             if a.save_strategy == "steps" and st.global_step % st.save_steps == 0:
                 self.control.should_save = True
+            if st.global_step >= st.max_steps:
+                self.control.should_training_stop = True
+                if a.save_strategy == "steps":
+                    self.control.should_save = True
             self.control = cb.call("on_step_end")
             if self.control.should_save:
                 if a.output_dir:

@@ -82,3 +82,65 @@ def test_ops_refuse_cpu_tensors(lib):
         ops.logp_entropy(torch.randn(2, 8), torch.zeros(2, dtype=torch.long))
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         ops.group_advantages(torch.randn(8, 1), torch.ones(1), 4)
+
+
+def _dtype_positions():
+    """{entry point: [argument positions whose C parameter is a dtype code]} from
+    the header's prototypes (parameters named `dtype`, `grad_dtype`, ...)."""
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for name, params in re.findall(r"(?:int|int64_t)\s+(swh_\w+)\(([^;{]*)\)\s*;", src):
+        names = [p.strip().split()[-1].lstrip("*") for p in params.split(",") if p.strip() and p.strip() != "void"]
+        pos = [i for i, n in enumerate(names) if n == "dtype" or n.endswith("_dtype")]
+        if pos:
+            out[name] = pos
+    return out
+
+
+def _python_sources():
+    skip = {os.path.join(ROOT, "tests", "test_abi.py")}  # the argument-error probes above pass bad codes on purpose
+    for top in ("swh_trl_amd", "tools", "tests"):
+        for d, _, files in os.walk(os.path.join(ROOT, top)):
+            for f in files:
+                if f.endswith(".py") and os.path.join(d, f) not in skip:
+                    yield os.path.join(d, f)
+    yield os.path.join(ROOT, "bench.py")
+    yield os.path.join(ROOT, "__graft_entry__.py")
+
+
+def test_no_call_site_passes_a_literal_dtype_code():
+    """Every dtype code handed to the C-ABI comes from the tensor it describes
+    (`_lib.dtype_code`).  Round 4's hipErrorIllegalAddress came from a literal 0
+    (SWH_F32) passed for bf16 buffers in a tool: the library cannot see buffer
+    sizes, so the kernel read and wrote 4-byte elements over 2-byte allocations.
+    Checked statically over every `call("swh_...", ...)` / `lib.swh_...(...)`."""
+    import ast
+    pos = _dtype_positions()
+    assert {"swh_dw_reduce", "swh_adamw", "swh_logp_entropy_fwd", "swh_rmsnorm_fwd"} <= set(pos)
+    assert pos["swh_adamw"] == [4, 6]
+    bad, seen = [], 0
+    for path in _python_sources():
+        tree = ast.parse(open(path).read(), path)
+        for node in ast.walk(tree):
+            if not isinstance(node, ast.Call):
+                continue
+            f, args = node.func, node.args
+            if isinstance(f, ast.Name) and f.id == "call" or isinstance(f, ast.Attribute) and f.attr == "call":
+                if not args or not isinstance(args[0], ast.Constant) or not isinstance(args[0].value, str):
+                    continue
+                name, args = args[0].value, args[1:]
+            elif isinstance(f, ast.Attribute) and f.attr.startswith("swh_"):
+                name = f.attr
+            else:
+                continue
+            for i in pos.get(name, []):
+                if i >= len(args):
+                    continue
+                seen += 1
+                a = args[i]
+                literal = isinstance(a, ast.Constant) or (isinstance(a, (ast.Name, ast.Attribute)) and
+                                                          (getattr(a, "id", None) or a.attr).startswith("SWH_"))
+                if literal:
+                    bad.append(f"{os.path.relpath(path, ROOT)}:{node.lineno} {name} arg {i}")
+    assert seen >= 30, seen
+    assert not bad, bad

@@ -195,6 +195,34 @@ def test_greedy_matches_transformers_generate(dev, monkeypatch, shape, fold):
     assert sum(t is None for _, t, _ in rep) >= len(rep) // 4, rep
 
 
+def test_greedy_bench_layout_first_divergence_is_a_bf16_tie(dev):
+    """Greedy ids in the benched layout (64 rows = 8 prompts x G 8, P 128, C 256,
+    the M = 64 decode tiles, shared prompt K/V, the fused lm-head sampler) at the
+    Qwen2.5-0.5B width with 2 layers, against transformers bf16 generate: the first
+    divergence of every row is reported and must sit at a bf16 tie (<= 2 ulps)."""
+    from swh_trl_amd.engine import CausalLM, DecodeEngine
+    from swh_trl_amd.engine.config import DecoderConfig
+    m = CausalLM(DecoderConfig(num_hidden_layers=2), dev, seed=3, init_std=0.02)
+    G, n, P, C = 8, 8, 128, 256
+    g = torch.Generator().manual_seed(11)
+    ids = torch.randint(0, m.cfg.vocab_size, (n, P), generator=g).repeat_interleave(G, 0).to(dev)
+    mask = torch.ones(n * G, P, dtype=torch.int64, device=dev)
+    eng = DecodeEngine(m, n * G, P, C)
+    mine, _ = eng.generate(ids, mask, C, greedy=True, group_size=G)
+    assert eng._fused_sample()
+    # every row of a group is the same greedy continuation (the shared prompt K/V rows included)
+    assert torch.equal(mine.view(n, G, C), mine.view(n, G, C)[:, :1].expand(n, G, C))
+    hf = _hf_from(m, torch.bfloat16)
+    firsts = ids[::G]
+    with torch.no_grad():
+        ref = hf.generate(input_ids=firsts, attention_mask=mask[::G], max_new_tokens=C, do_sample=False,
+                          pad_token_id=0, eos_token_id=None)[:, P:]
+    rep = _greedy_divergence_report(m, firsts, mine[::G], ref, max_ulps=2.0)
+    # how far the rows agree (first divergence per row, or the whole completion)
+    agree = [C if t is None else t for _, t, _ in rep]
+    print("bench-layout greedy agreement per prompt (tokens):", agree)
+
+
 def test_sampled_rollout_is_reproducible_and_respects_min_new_tokens(dev):
     from swh_trl_amd.engine import DecodeEngine
     m = _tiny(dev, seed=4)

@@ -56,8 +56,76 @@ def test_grpo_config_bookkeeping():
         GRPOConfig(generation_batch_size=64, steps_per_generation=2)
     with pytest.raises(ValueError):
         GRPOConfig(use_vllm=True)
-    c = GRPOConfig(some_unknown_field=1)
-    assert c.extra == {"some_unknown_field": 1}
+    with pytest.raises(ValueError, match="some_unknown_field"):
+        GRPOConfig(some_unknown_field=1)
+
+
+@pytest.mark.parametrize("bad", [{"optim": "adafactor"}, {"optim": "sgd"}, {"logging_strategy": "epoch"},
+                                 {"fp16": True}, {"tf32": True}, {"neftune_noise_alpha": 5.0},
+                                 {"load_best_model_at_end": True}, {"deepspeed": "ds.json"}, {"fsdp": "full_shard"},
+                                 {"use_cpu": True}, {"push_to_hub": True}, {"auto_find_batch_size": True},
+                                 {"dataloader_drop_last": True}, {"use_liger_kernel": True}, {"not_a_field": 0}])
+def test_configs_raise_on_result_changing_training_args(bad):
+    """The reference configs are TrainingArguments handed whole to the transformers
+    Trainer (grpo_trainer.py:837-846): a field the drop-in does not implement is
+    accepted only where it cannot change the result; these would, so they raise."""
+    from swh_trl_amd.trainer import PPOConfig
+    with pytest.raises(ValueError, match=next(iter(bad))):
+        GRPOConfig(per_device_train_batch_size=8, num_generations=4, **bad)
+    with pytest.raises(ValueError, match=next(iter(bad))):
+        PPOConfig(**bad)
+
+
+def test_configs_keep_inert_training_args():
+    """Reporting / hub / data-loader / DDP plumbing fields and the inert values
+    of the constrained ones construct unchanged and are kept in `extra`."""
+    from swh_trl_amd.trainer import PPOConfig
+    inert = dict(report_to=["wandb"], run_name="r", logging_dir="/tmp/x", dataloader_num_workers=4,
+                 dataloader_pin_memory=False, ddp_timeout=60, gradient_checkpointing=True, optim="adamw_torch",
+                 logging_strategy="steps", tf32=False, push_to_hub=False, hub_strategy="end",
+                 vllm_server_port=8000, save_safetensors=True, data_seed=3, fsdp="", deepspeed=None)
+    c = GRPOConfig(per_device_train_batch_size=8, num_generations=4, **inert)
+    assert c.extra == {k: v for k, v in inert.items() if k not in c.__dataclass_fields__}
+    assert c.report_to == ["wandb"] and c.extra["optim"] == "adamw_torch"
+    p = PPOConfig(**inert, eval_strategy="no")
+    assert p.extra["optim"] == "adamw_torch" and p.extra["eval_strategy"] == "no"
+
+
+def test_generation_config_overrides_follow_reference():
+    """grpo_trainer.py:995-1014: the GenerationConfig is the config fields with
+    `generation_kwargs` applied on top; keys the engine does not implement raise
+    unless at their no-op value; greedy decoding drops the warpers."""
+    from types import SimpleNamespace
+
+    from swh_trl_amd.trainer.grpo_trainer import generation_config
+    tok = SimpleNamespace(pad_token_id=7, eos_token_id=9, bos_token_id=None)
+    base = dict(per_device_train_batch_size=8, num_generations=4, max_completion_length=32, temperature=1.0,
+                top_p=0.9, top_k=None, min_p=None, repetition_penalty=1.0)
+    g = generation_config(GRPOConfig(**base), tok)
+    assert g == {"max_new_tokens": 32, "min_new_tokens": 0, "min_length": 0, "greedy": False, "temperature": 1.0,
+                 "top_p": 0.9, "top_k": None, "min_p": None, "repetition_penalty": 1.0, "pad_token_id": 7,
+                 "eos_token_id": 9}
+    over = dict(temperature=0.7, top_k=50, top_p=0.95, min_p=0.05, repetition_penalty=1.1, max_new_tokens=16,
+                min_new_tokens=4, eos_token_id=[9, 11], pad_token_id=3, num_beams=1, use_cache=True,
+                cache_implementation="static", output_scores=True)
+    g = generation_config(GRPOConfig(**base, generation_kwargs=over), tok)
+    assert (g["temperature"], g["top_k"], g["top_p"], g["min_p"], g["repetition_penalty"]) == (0.7, 50, 0.95, 0.05, 1.1)
+    assert (g["max_new_tokens"], g["min_new_tokens"], g["eos_token_id"], g["pad_token_id"]) == (16, 4, [9, 11], 3)
+    # the same values as config fields give the same parameters (the GPU test draws with both)
+    same = generation_config(GRPOConfig(**{**base, "temperature": 0.7, "top_k": 50, "top_p": 0.95, "min_p": 0.05,
+                                           "repetition_penalty": 1.1, "max_completion_length": 16},
+                                        generation_kwargs={"min_new_tokens": 4, "eos_token_id": [9, 11],
+                                                           "pad_token_id": 3}), tok)
+    assert same == g
+    greedy = generation_config(GRPOConfig(**base, generation_kwargs={"do_sample": False, "temperature": 0.5,
+                                                                     "top_k": 3, "repetition_penalty": 1.3}), tok)
+    assert greedy["greedy"] and greedy["temperature"] == 1.0 and greedy["top_k"] is None
+    assert greedy["top_p"] == 1.0 and greedy["repetition_penalty"] == 1.3  # the penalty is a processor, not a warper
+    for bad in ({"num_beams": 4}, {"no_repeat_ngram_size": 3}, {"typical_p": 0.5}, {"bad_words_ids": [[5]]},
+                {"num_return_sequences": 2}, {"return_dict_in_generate": True}, {"stop_strings": ["x"]},
+                {"not_a_generation_key": 1}, {"temperature": 0.0}, {"top_k": -1}, {"max_new_tokens": 0}):
+        with pytest.raises(ValueError):
+            generation_config(GRPOConfig(**base, generation_kwargs=bad), tok)
 
 
 def test_grpo_config_eval_and_strategy_fields():

@@ -80,7 +80,7 @@ def _weights(model):
 
 
 def product_run(cfg, dtype, n_steps, *, std, lr, G=4, P=12, C=24, MB=8, GA=2, seed=11, n_prompts=None,
-                min_new_tokens=4, **grpo_kw):
+                min_new_tokens=4, gen_extra=None, **grpo_kw):
     """n_steps GRPOTrainer optimizer steps; captures every generation (its
     output and the shuffle permutation drawn after it), every training pass's
     log-probs, and the loss / grad norm / gradients / weights of every step."""
@@ -98,7 +98,8 @@ def product_run(cfg, dtype, n_steps, *, std, lr, G=4, P=12, C=24, MB=8, GA=2, se
                       max_prompt_length=P, max_completion_length=C, learning_rate=lr, max_steps=n_steps,
                       lr_scheduler_type="constant", seed=5, shuffle_dataset=False,
                       model_init_kwargs={"torch_dtype": "float32" if dtype == torch.float32 else "bfloat16"},
-                      generation_kwargs={"eos_token_id": EOS, "pad_token_id": PAD, "min_new_tokens": min_new_tokens},
+                      generation_kwargs={"eos_token_id": EOS, "pad_token_id": PAD, "min_new_tokens": min_new_tokens,
+                                         **(gen_extra or {})},
                       **grpo_kw)
     model = CausalLM(cfg, dev, seed=3, init_std=std, dtype=dtype)
     tr = GRPOTrainer(model=model, reward_funcs=_reward_product, args=args, train_dataset=ds)
@@ -144,9 +145,12 @@ def product_run(cfg, dtype, n_steps, *, std, lr, G=4, P=12, C=24, MB=8, GA=2, se
                       "logps": cap["logps"][-1], "mask": cap["masks"][-1],
                       "seg_metrics": tr._metrics["train"]["_met"][-1].detach().cpu().clone()})
     hip_attn = tr.model._hip_attn
-    del tr
+    eng = tr._engine
+    engine = {"B": eng.B, "fused_sample": bool(getattr(eng, "fused", False) and eng._fused_sample()),
+              "gen_kwargs": dict(tr.gen_kwargs), "temperature": tr.temperature}
+    del tr, eng
     torch.cuda.empty_cache()
-    return {"w0": w0, "gens": cap["gens"], "steps": steps, "hip_attn": hip_attn,
+    return {"w0": w0, "gens": cap["gens"], "steps": steps, "hip_attn": hip_attn, "engine": engine,
             "geometry": dict(G=G, C=C, MB=MB, GA=GA)}
 
 
@@ -394,3 +398,44 @@ def test_early_stopped_rollout_width_matches_oracle_fp32():
     assert w < 96 and bool(prod["gens"][0]["completion_mask"][:, -1].any()), w
     orc = oracle_run(cfg, prod["w0"], torch.float32, prod, 1, lr=lr, loss_type="dr_grpo")
     _check_fp32("early-stop-width", prod, orc, lr)
+
+
+def test_generation_kwargs_temperature_step_matches_oracle_fp32():
+    """generation_kwargs on top of the config fields (grpo_trainer.py:995-1014): the
+    rollout samples at generation_kwargs' T 0.7 / top-k 50, while the scoring and
+    training passes divide by the config's temperature 1.0 (:1249), as the
+    reference's do; one fp32 step against the oracle loop scoring at T 1.0."""
+    from swh_trl_amd.engine.config import tiny_qwen2
+    cfg = tiny_qwen2(1024, 2)
+    lr = 1e-3
+    prod = product_run(cfg, torch.float32, 1, std=0.05, lr=lr, gen_extra={"temperature": 0.7, "top_k": 50})
+    assert prod["engine"]["gen_kwargs"]["temperature"] == 0.7 and prod["engine"]["gen_kwargs"]["top_k"] == 50
+    assert prod["engine"]["temperature"] == 1.0
+    orc = oracle_run(cfg, prod["w0"], torch.float32, prod, 1, lr=lr)
+    _check_fp32("gen-kwargs-T0.7", prod, orc, lr)
+
+
+BENCH_LAYOUT = dict(G=8, P=128, C=256, MB=16, GA=4)
+
+
+def test_bench_layout_bf16_step_matches_oracle():
+    """One bf16 GRPO step in exactly the benched workload's layout (bench.py:
+    8 prompts x G 8 = 64 rows, P 128, C 256 with min_new_tokens = C, micro-batch
+    16 x GA 4 fused into one training pass, beta 0) at the Qwen2.5-0.5B width with
+    2 layers: the rollout runs the M = 64 decode tiles (xstream / fragment-order
+    projections) and the fused lm-head sampler, the training pass the shared-prompt
+    HIP forward of 8 x 128 + 64 x 256 tokens.  Against the reference loop
+    (grpo_trainer.py:1500-2003, :2058-2175) in bf16 and fp32 with this module's
+    bf16-rounding bounds (oracle on the device: 16 x 384 x 151936 fp32 logits per
+    micro-batch)."""
+    from swh_trl_amd.engine.config import DecoderConfig
+    cfg = DecoderConfig(num_hidden_layers=2)
+    lr = 1e-3
+    prod = product_run(cfg, torch.bfloat16, 1, std=0.02, lr=lr, min_new_tokens=BENCH_LAYOUT["C"], **BENCH_LAYOUT)
+    assert prod["hip_attn"] and prod["engine"]["B"] == 64 and prod["engine"]["fused_sample"], prod["engine"]
+    g = prod["gens"][0]
+    assert g["completion_ids"].shape == (64, 256) and bool(g["completion_mask"].all())
+    assert prod["steps"][0]["mask"].shape == (64, 256)  # the four micro-batches in one fused pass
+    orc_bf = oracle_run(cfg, prod["w0"], torch.bfloat16, prod, 1, lr=lr, device="cuda:0")
+    orc_32 = oracle_run(cfg, prod["w0"], torch.float32, prod, 1, lr=lr, device="cuda:0")
+    _check_bf16("bench-layout-0.5b-width", prod, orc_bf, orc_32)

@@ -182,3 +182,40 @@ def test_evaluate_loss_matches_oracle_fp32_and_leaves_training_unchanged():
     b.train()
     assert len([h for h in a.state.log_history if "eval_loss" in h]) == 2
     assert torch.equal(a.model.flat, b.model.flat)
+
+
+def _first_rollout(args, **kw):
+    tr = _trainer(args, **kw)
+    examples = [tr.train_dataset[i] for i in range(4) for _ in range(tr.num_generations)]
+    out = tr._generate_and_score_completions(examples)
+    return out["completion_ids"].cpu(), tr
+
+
+def test_generation_kwargs_override_config_fields():
+    """grpo_trainer.py:995-1014: generation_kwargs are applied on top of the config
+    fields, so {"temperature": 0.7, "top_k": 50} there draws exactly what the
+    config fields temperature 0.7 / top_k 50 draw (same Philox stream), and not what
+    the config's T 1.0 draws; max_new_tokens / do_sample / min_new_tokens
+    overrides shape the rollout the same way; the scoring temperature stays
+    args.temperature (:1249)."""
+    gk = {"eos_token_id": EOS, "pad_token_id": PAD}
+    a, tra = _first_rollout(_args(temperature=0.7, top_k=50))
+    b, trb = _first_rollout(_args(generation_kwargs={**gk, "temperature": 0.7, "top_k": 50}))
+    c, _ = _first_rollout(_args())
+    assert torch.equal(a, b)
+    assert not torch.equal(a, c)
+    assert tra.temperature == 0.7 and trb.temperature == 1.0   # scoring divides by args.temperature
+    short, trs = _first_rollout(_args(generation_kwargs={**gk, "max_new_tokens": 5, "min_new_tokens": 5}))
+    assert short.shape[1] == 5 and trs._engine.Cmax == 5
+    g1, _ = _first_rollout(_args(seed=3, generation_kwargs={**gk, "do_sample": False, "temperature": 0.3}))
+    g2, _ = _first_rollout(_args(seed=9, generation_kwargs={**gk, "do_sample": False}))
+    assert torch.equal(g1, g2)   # greedy: independent of the sampler seed and of the (dropped) warpers
+
+
+@pytest.mark.parametrize("bad", [{"num_beams": 2}, {"no_repeat_ngram_size": 2}, {"typical_p": 0.9},
+                                 {"bad_words_ids": [[5]]}, {"num_return_sequences": 2}, {"penalty_alpha": 0.6}])
+def test_generation_kwargs_unimplemented_keys_raise(bad):
+    """HF generation keys the engine does not implement raise at construction
+    instead of being dropped."""
+    with pytest.raises(ValueError, match=next(iter(bad))):
+        _trainer(_args(generation_kwargs={"eos_token_id": EOS, "pad_token_id": PAD, **bad}))

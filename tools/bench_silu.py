@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     from swh_trl_amd import nn_ops
-    from swh_trl_amd._lib import call
+    from swh_trl_amd._lib import call, dtype_code
     from swh_trl_amd.ops import _stream
     T, I = 17408, 4864
     gu = torch.randn(T, 2 * I, device="cuda", dtype=torch.bfloat16)
@@ -34,7 +34,7 @@ def main():
         return e0.elapsed_time(e1) / reps * 1000
 
     fw = t(lambda: nn_ops.silu_mul(gu, out=out))
-    bw = t(lambda: call("swh_silu_mul_bwd", gu.data_ptr(), d.data_ptr(), T, I, dgu.data_ptr(), 1, _stream()))
+    bw = t(lambda: call("swh_silu_mul_bwd", gu.data_ptr(), d.data_ptr(), T, I, dgu.data_ptr(), dtype_code(gu, "silu_mul_bwd"), _stream()))
     print(f"silu_mul fwd {fw:7.1f} us {3 * T * I * 2 / fw / 1e3:6.0f} GB/s   bwd {bw:7.1f} us "
           f"{5 * T * I * 2 / bw / 1e3:6.0f} GB/s", flush=True)
 
