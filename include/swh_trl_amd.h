@@ -8,8 +8,13 @@
  *   - `stream` is a hipStream_t passed as void* (NULL = the null stream);
  *   - return value: 0 = launched, <0 = error (see SWH_E_*); argument errors are
  *     detected on the host before anything is launched;
- *   - no global mutable state: re-entrant across streams and devices, and safe
- *     to capture into a hipGraph (the decode step is captured and replayed).
+ *   - no hidden mutable state: the library holds only (1) per-device facts
+ *     queried once per device under std::call_once (CU count, each kernel's
+ *     dynamic-LDS opt-in) and (2) the launch policy below, set explicitly by
+ *     swh_set_launch_policy and read under a lock; it never reads the
+ *     environment.  Entry points are re-entrant across host threads, streams
+ *     and devices, and safe to capture into a hipGraph (the decode step is
+ *     captured and replayed).
  *
  * Each function cites the reference (shiwanghua/swh-trl @ TRL 0.21.0.dev0)
  * symbol it replaces, `path:line` relative to the reference tree.
@@ -36,6 +41,34 @@ extern "C" {
 /* ---- library ------------------------------------------------------------ */
 const char *swh_version(void);
 const char *swh_status_string(int status);
+
+/* Launch policy: geometry choices of the decode GEMMs and samplers that do not
+ * change any result (every alternative is bit-identical; tests pin that) and
+ * exist for A/B timing and geometry-coverage tests.  Process-wide, applied by
+ * launches issued after the call (a captured graph keeps the geometry it was
+ * captured with).  *_workspace_bytes size for the policy in force when they are
+ * called; a launch whose geometry needs more workspace than it is given returns
+ * SWH_E_ARG and writes nothing.  gemm_ms 0 means "the cost model decides" (the
+ * other geometry fields must then be 0). */
+typedef struct swh_launch_policy {
+    int64_t wide_kmin;     /* smallest K routed to the bandwidth-regime GEMM (csrc/wide_gemm.hip); 2048 */
+    int32_t wide_gemm;     /* 0: every decode projection on decode_gemm; 1 */
+    int32_t wide_smax;     /* largest K split of wide_gemm, 1..8; 8 */
+    int32_t wide_cb;       /* 16-row weight groups per wave of wide_gemm: 0 auto, 1, 2; 0 */
+    int32_t gemm_ms;       /* decode_gemm geometry override: 16-row blocks 1/2/4 (0 = cost model), */
+    int32_t gemm_cb;       /*   16-column blocks 1/2/4, */
+    int32_t gemm_s;        /*   K split 1..8, */
+    int32_t gemm_persist;  /*   persistent grid 0/1, */
+    int32_t gemm_wn;       /*   column groups 1/2/4; */
+    int32_t gemm_tile;     /* 1: force the tile kernel where it applies; 0 */
+    int32_t gemm_nw;       /* waves per decode_gemm workgroup 4/8/16 (0 = 8); 0 */
+    int32_t xstream;       /* 0: qkv / o through decode_gemm's LDS X image instead of register-streamed X; 1 */
+    int32_t lm_ring14;     /* 0: whole-tile weight ring in the fused lm-head sampler at K = 896; 1 */
+    int32_t filt_wgs;      /* target workgroups of one filtered-sampler pass, 64..65536; 1024 */
+} swh_launch_policy;
+int swh_launch_policy_default(swh_launch_policy *out);
+int swh_get_launch_policy(swh_launch_policy *out);
+int swh_set_launch_policy(const swh_launch_policy *p);  /* SWH_E_ARG when a field is out of range */
 
 /* ---- a6/a7/a8: log-probs + entropy of temperature-scaled logits ----------
  * Replaces trl/trainer/utils.py:1430-1462 (selective_log_softmax),

@@ -40,10 +40,22 @@ class GRPOLossParams(C.Structure):
                 ("num_segments", c_i32)]
 
 
+class LaunchPolicy(C.Structure):
+    """swh_launch_policy (include/swh_trl_amd.h): geometry choices that change no
+    result (every alternative is bit-identical), set explicitly."""
+    _fields_ = [("wide_kmin", c_i64), ("wide_gemm", c_i32), ("wide_smax", c_i32), ("wide_cb", c_i32),
+                ("gemm_ms", c_i32), ("gemm_cb", c_i32), ("gemm_s", c_i32), ("gemm_persist", c_i32),
+                ("gemm_wn", c_i32), ("gemm_tile", c_i32), ("gemm_nw", c_i32), ("xstream", c_i32),
+                ("lm_ring14", c_i32), ("filt_wgs", c_i32)]
+
+
 # name -> (restype, argtypes)
 SIGNATURES = {
     "swh_version": (C.c_char_p, []),
     "swh_status_string": (C.c_char_p, [c_i32]),
+    "swh_launch_policy_default": (c_i32, [C.POINTER(LaunchPolicy)]),
+    "swh_get_launch_policy": (c_i32, [C.POINTER(LaunchPolicy)]),
+    "swh_set_launch_policy": (c_i32, [C.POINTER(LaunchPolicy)]),
     "swh_logp_entropy_fwd": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_f32, c_i32,
                                      c_vp, c_vp, c_vp, c_vp]),
     "swh_log_softmax_gather_exact": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
@@ -160,7 +172,82 @@ def load() -> C.CDLL:
                 fn.restype = res
                 fn.argtypes = args
             _lib = lib
+            _policy_from_env(lib)
     return _lib
+
+
+# Tools-only A/B switches of the launch policy, read ONCE when the library is
+# loaded (the library itself never reads the environment).  A process that wants
+# another policy later calls set_launch_policy / launch_policy(...).
+_ENV_POLICY = {"SWH_WIDE_KMIN": "wide_kmin", "SWH_WIDE_GEMM": "wide_gemm", "SWH_WIDE_SMAX": "wide_smax",
+               "SWH_WIDE_CB": "wide_cb", "SWH_GEMM_NW": "gemm_nw", "SWH_XSTREAM": "xstream",
+               "SWH_LM_RING14": "lm_ring14", "SWH_FILT_WGS": "filt_wgs"}
+
+
+def _geometry_fields(cfg: str) -> dict:
+    """"ms,cb,s[,p[,wn]]" or "t" (the tile kernel) -> policy fields."""
+    if cfg == "t":
+        return {"gemm_tile": 1}
+    v = [int(x) for x in cfg.split(",")]
+    if len(v) < 3:
+        raise ValueError(f"decode_gemm geometry {cfg!r}: expected 'ms,cb,s[,persist[,wn]]'")
+    v = v + [0, 1][len(v) - 3:]  # persist 0, wn 1 unless given
+    return dict(zip(("gemm_ms", "gemm_cb", "gemm_s", "gemm_persist", "gemm_wn"), v))
+
+
+def _policy_from_env(lib) -> None:
+    kw = {f: int(os.environ[e]) for e, f in _ENV_POLICY.items() if os.environ.get(e)}
+    if os.environ.get("SWH_GEMM_CFG"):
+        kw.update(_geometry_fields(os.environ["SWH_GEMM_CFG"]))
+    if kw:
+        p = LaunchPolicy()
+        lib.swh_get_launch_policy(C.byref(p))
+        for k, v in kw.items():
+            setattr(p, k, v)
+        check(lib.swh_set_launch_policy(C.byref(p)), "swh_set_launch_policy")
+
+
+def get_launch_policy() -> dict:
+    p = LaunchPolicy()
+    check(load().swh_get_launch_policy(C.byref(p)), "swh_get_launch_policy")
+    return {f: getattr(p, f) for f, _ in LaunchPolicy._fields_}
+
+
+def set_launch_policy(**fields) -> dict:
+    """Set policy fields (the others keep their value); `gemm_cfg="ms,cb,s[,p[,wn]]"`
+    / "t" / None sets or clears the decode_gemm geometry override.  Returns the
+    previous policy."""
+    lib = load()
+    old = get_launch_policy()
+    new = dict(old)
+    if "gemm_cfg" in fields:
+        cfg = fields.pop("gemm_cfg")
+        new.update(gemm_ms=0, gemm_cb=0, gemm_s=0, gemm_persist=0, gemm_wn=0, gemm_tile=0)
+        if cfg:
+            new.update(_geometry_fields(cfg))
+    unknown = set(fields) - set(new)
+    if unknown:
+        raise ValueError(f"unknown launch policy fields {sorted(unknown)}")
+    new.update(fields)
+    check(lib.swh_set_launch_policy(C.byref(LaunchPolicy(**new))), "swh_set_launch_policy")
+    return old
+
+
+class launch_policy:
+    """Context manager: `with launch_policy(xstream=0): ...` runs the block's
+    launches (and graph captures) under the given policy, then restores it."""
+
+    def __init__(self, **fields):
+        self.fields = fields
+
+    def __enter__(self):
+        self.old = set_launch_policy(**self.fields)
+        return self
+
+    def __exit__(self, *exc):
+        lib = load()
+        check(lib.swh_set_launch_policy(C.byref(LaunchPolicy(**self.old))), "swh_set_launch_policy")
+        return False
 
 
 def check(status: int, name: str) -> None:

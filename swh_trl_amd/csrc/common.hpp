@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "../../include/swh_trl_amd.h"
 
 namespace swh {
@@ -296,5 +298,25 @@ __device__ __forceinline__ float u01_from_bits(uint32_t w) {
 
 // ---- launch helpers -----------------------------------------------------------
 inline int launch_status() { return hipGetLastError() == hipSuccess ? SWH_OK : SWH_E_LAUNCH; }
+
+// ---- the library's host-side state (csrc/lib.hip) ------------------------------
+// Per-device facts, each queried once per device under std::call_once, and the
+// launch policy of swh_set_launch_policy (a copy read under a lock).  Nothing
+// else in the library outlives a call, and nothing reads the environment.
+constexpr int kMaxDevices = 64;
+constexpr int kMaxDynLds = 160 * 1024;  // gfx950 LDS per workgroup
+
+int cu_count();                        // current device's CUs (256 if the query fails)
+swh_launch_policy launch_policy();     // a snapshot of the process-wide policy
+bool lds_opt_in_once(const void *kernel, std::once_flag *once, bool *ok);
+
+// Opt a kernel into > 64 KB of dynamic LDS, once per (kernel, device): the
+// attribute is per device, so the flags are a per-device table per kernel.
+template <auto Kernel>
+bool lds_opt_in() {
+    static std::once_flag once[kMaxDevices];
+    static bool ok[kMaxDevices];
+    return lds_opt_in_once(reinterpret_cast<const void *>(Kernel), once, ok);
+}
 
 }  // namespace swh

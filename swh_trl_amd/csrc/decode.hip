@@ -1571,18 +1571,9 @@ int attn_dispatch_gq(int gq, const uint16_t *q, uint16_t *kc, uint16_t *vc, cons
 }
 
 // ---- GEMM launch configuration -------------------------------------------
-// smallest K routed to csrc/wide_gemm.hip (SWH_WIDE_KMIN: A/B).  Read per call (host
-// side only, at graph capture in the decode loop) so it tracks the DecodeEngine's
-// choice of packed projections, which reads the same variable.
-int64_t wide_gemm_kmin() {
-    const char *e = getenv("SWH_WIDE_KMIN");
-    return e ? atoll(e) : 2048;
-}
-// SWH_WIDE_GEMM=0 keeps every shape on decode_gemm (A/B of csrc/wide_gemm.hip)
-bool wide_gemm_enabled() {
-    const char *e = getenv("SWH_WIDE_GEMM");
-    return !(e && e[0] == '0');
-}
+// The smallest K routed to csrc/wide_gemm.hip and whether that path is on come from
+// the launch policy (swh_set_launch_policy; the DecodeEngine reads the same policy to
+// choose its packed projections), read per call on the host (at graph capture).
 
 struct GemmCfg {
     int ms, cb, nw, s, gx;  // 16-row blocks, 16-col blocks (tile), waves, K split, grid.x
@@ -1591,17 +1582,6 @@ struct GemmCfg {
     int fw = 0;             // weights in the swh_frag_pack layout
     int xf = 0;             // X (the SiLU activation) in the same fragment order (xstream only)
 };
-
-int cu_count() {
-    static int n = 0;
-    if (!n) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
-    }
-    return n;
-}
 
 // 8 waves in every geometry: more k-steps in flight per CU (down 14.9 -> 11.5 us,
 // qkv 7.0 -> 6.3 us against 4 waves for 16- and 32-row tiles; tools/bench_decode.py --ku)
@@ -1656,10 +1636,10 @@ GemmCfg pick_cfg(int64_t M, int64_t wcols, int64_t K, bool silu, int nm) {
         if (c.gx > wcols / 32 * nmt64) c.gx = (int)(wcols / 32 * nmt64);
         if (gemm_cost(c, M, wcols, K, nm) < best_cost) best = c;
     }
-    if (const char *e = getenv("SWH_GEMM_CFG")) {  // tuning override "ms,cb,s[,p[,wn]]"
-        int a = 0, b = 0, d = 0, pz = 0, wn = 1;
-        const int got = sscanf(e, "%d,%d,%d,%d,%d", &a, &b, &d, &pz, &wn);
-        if (got >= 3 && (a == 1 || a == 2 || a == 4) && (b == 1 || b == 2 || b == 4) && d >= 1 && d <= KS && d <= 8 &&
+    const swh_launch_policy pol = launch_policy();
+    if (pol.gemm_ms) {  // geometry override of the launch policy (tests / A/B)
+        const int a = pol.gemm_ms, b = pol.gemm_cb, d = pol.gemm_s, pz = pol.gemm_persist, wn = pol.gemm_wn;
+        if ((a == 1 || a == 2 || a == 4) && (b == 1 || b == 2 || b == 4) && d >= 1 && d <= KS && d <= 8 &&
             wcols % (16 * b * align) == 0 && !(pz && d != 1) && (wn == 1 || wn == 2 || wn == 4)) {
             const int64_t nmt = (M + 16 * a - 1) / (16 * a);
             GemmCfg c{a, b, gemm_waves(a), d, 0, pz != 0, wn};
@@ -1673,11 +1653,11 @@ GemmCfg pick_cfg(int64_t M, int64_t wcols, int64_t K, bool silu, int nm) {
     if (!best.persist) best.gx = (int)(8 * ((M + 16 * best.ms - 1) / (16 * best.ms)) * ((wcols / (16 * best.cb) + 7) / 8));
     // one column block per wave (column groups split the waves, each group splits K):
     // a 4x smaller LDS merge; gate/up 14.7 -> 12.3 us (tools/bench_decode.py --ku)
-    if (!getenv("SWH_GEMM_CFG") && !best.persist && best.cb > 1 && best.nw % best.cb == 0 &&
+    if (!pol.gemm_ms && !best.persist && best.cb > 1 && best.nw % best.cb == 0 &&
         gemm_cost(GemmCfg{best.ms, best.cb, best.nw, best.s, best.gx, false, best.cb}, M, wcols, K, nm) < 1e29)
         best.wn = best.cb;
-    if (const char *e = getenv("SWH_GEMM_NW")) {  // tuning override: waves per workgroup (16: cb == 1 only)
-        const int v = atoi(e);
+    if (pol.gemm_nw) {  // policy override: waves per workgroup (16: cb == 1 only)
+        const int v = pol.gemm_nw;
         if ((v == 4 || v == 8 || (v == 16 && best.cb == best.wn)) &&
             gemm_cost(GemmCfg{best.ms, best.cb, v, best.s, best.gx, best.persist, best.wn}, M, wcols, K, nm) < 1e29)
             best.nw = v;
@@ -1695,13 +1675,7 @@ template <int CB, int MS, int NM, int EPI, bool BIAS, int MAXT, int KL>
 int launch_gemm_kl(const GemmCfg &c, dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W,
                    int m, int n, int k, const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs,
                    uint16_t *R, float *ss_out, uint16_t *Y, int ld, float *slab, int *ctr) {
-    static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in once per kernel
-    if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&decode_gemm_kernel<CB, MS, NM, EPI, BIAS, MAXT, KL>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-            return SWH_E_LAUNCH;
-        attr = true;
-    }
+    if (!lds_opt_in<&decode_gemm_kernel<CB, MS, NM, EPI, BIAS, MAXT, KL>>()) return SWH_E_LAUNCH;  // > 64 KB LDS
     decode_gemm_kernel<CB, MS, NM, EPI, BIAS, MAXT, KL><<<grid, 64u * c.nw, lds, s>>>(
         X, W, m, n, k, NWt, eps, ss_in, Bs, R, ss_out, Y, ld, slab, ctr, c.persist ? 1 : 0, c.wn, c.fw);
     return launch_status();
@@ -1741,9 +1715,9 @@ int launch_xstream_ms(const GemmCfg &c, hipStream_t s, const uint16_t *X, const 
 
 int launch_xstream(const GemmCfg &c, hipStream_t s, const uint16_t *X, const uint16_t *W, int m, int n, int k, int nm,
                    float eps, const float *ss_in, const uint16_t *Bs, uint16_t *R, float *ss_out, uint16_t *Y, int ld) {
-    const char *e = getenv("SWH_XSTREAM");  // A/B: 0 = decode_gemm_kernel's LDS image
+    const bool lds_image = !launch_policy().xstream;  // policy 0: decode_gemm_kernel's LDS image (A/B)
     const int ks = k / 32;
-    if (((e && e[0] == '0') && !c.xf) || c.cb != 1 || c.wn != 1 || c.s != 1 || c.persist || c.nw != 8 || n % 16 ||
+    if ((lds_image && !c.xf) || c.cb != 1 || c.wn != 1 || c.s != 1 || c.persist || c.nw != 8 || n % 16 ||
         ks < 8 || ks > (c.xf ? 152 : 64) || (c.ms != 1 && c.ms != 2))
         return 1;
     if (R) {  // o_proj: s += x W^T (+ the next norm's partial sums); down_proj over a fragment-order X
@@ -1793,25 +1767,16 @@ template <int NM, int EPI, bool BIAS, int SAMPLE, int KSC, int RD = 0>
 int launch_lm_ks(dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W, int M, int N, int K,
                  const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs, uint16_t *Y, int ldy,
                  const LmSample &smp) {
-    static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in once per kernel
-    if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&lm_head_kernel<NM, EPI, BIAS, SAMPLE, KSC, RD>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-            return SWH_E_LAUNCH;
-        attr = true;
-    }
+    if (!lds_opt_in<&lm_head_kernel<NM, EPI, BIAS, SAMPLE, KSC, RD>>()) return SWH_E_LAUNCH;  // > 64 KB LDS
     lm_head_kernel<NM, EPI, BIAS, SAMPLE, KSC, RD><<<grid, RD ? 768 : 512, lds, s>>>(X, W, M, N, K, NWt, eps, ss_in, Bs,
                                                                                   Y, ldy, smp);
     return launch_status();
 }
 
 // the fused sampler at K = 896 with the half-tile weight ring and 12 waves per workgroup
-// (three per SIMD): 58.2-58.8 against 60.3-60.4 us per launch, bench +0.6 % (SWH_LM_RING14=0: off;
-// read per call)
-inline bool lm_ring14() {
-    const char *e = getenv("SWH_LM_RING14");
-    return !(e && e[0] == '0');
-}
+// (three per SIMD): 58.2-58.8 against 60.3-60.4 us per launch, bench +0.6 % (launch policy
+// lm_ring14 = 0: off; read per call)
+inline bool lm_ring14() { return launch_policy().lm_ring14 != 0; }
 
 // compile-time k-step counts for the model widths in use (Qwen2.5-0.5B: H = 896)
 template <int NM, int EPI, bool BIAS, int SAMPLE>
@@ -1954,19 +1919,19 @@ static int decode_gemm_impl(const void *x, const void *w, int64_t M, int64_t N, 
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int64_t wcols = silu ? 2 * N : N;
     const int nm = norm_w ? 1 : (ss_in ? 2 : 0);
-    if (!fw && nm != 1 && K >= wide_gemm_kmin() && wide_gemm_enabled()) {  // the bandwidth regime (8B decode): csrc/wide_gemm.hip
+    const swh_launch_policy pol = launch_policy();
+    if (!fw && nm != 1 && K >= pol.wide_kmin && pol.wide_gemm) {  // the bandwidth regime (8B decode): csrc/wide_gemm.hip
         const int st = wide_gemm(x, w, M, N, K, eps, ss_in, bias, residual, silu, y, ldy, ss_out, workspace,
                                  workspace_bytes, kCounterBytes, 0, s);
         if (st != 1) return st;
     }
     {  // many 16-column tiles and a K that fits the X image: the tile kernel (lm head, gate/up)
         const int64_t ntile = silu ? N / 8 : N / 16;
-        const char *e = getenv("SWH_GEMM_CFG");
-        const bool force = e && e[0] == 't';  // tuning: "t" forces the tile kernel
+        const bool force = pol.gemm_tile != 0, overridden = pol.gemm_ms != 0;  // policy: force / bypass the tile kernel
         // gate/up (SiLU tiles) from one tile per CU up: 11.2 vs 12.4 us at N 9728 (tools/bench_decode.py --ku)
         const int64_t min_tiles = (silu ? 1 : 8) * (int64_t)cu_count();
         // (the epilogues store 8 columns of a row as one 16-B piece: row-major needs ldy % 8 == 0)
-        if (!residual && K <= 32 * kLmMaxKS && (force || (!e && ntile >= min_tiles)) &&
+        if (!residual && K <= 32 * kLmMaxKS && (force || (!overridden && ntile >= min_tiles)) &&
             ((silu && (act & 1)) || ldy % 8 == 0)) {
             const int64_t nmt = (M + 63) / 64;
             const GemmLds L = gemm_lds(1, 64, 8, (int)K, (int)K, nm, false);

@@ -471,8 +471,8 @@ int launch_filtered(const typename Elem<DT>::T *lg, int64_t B, int64_t V, int64_
                     const uint64_t *rng, const int32_t *step, const uint32_t *seen, int64_t words, void *workspace,
                     float *scores_out, hipStream_t s) {
     // more splits than the unfiltered path: each digit pass is bound by its
-    // workgroups' LDS histogram atomics, so spread a row over up to SWH_FILT_WGS
-    static const int target = getenv("SWH_FILT_WGS") ? atoi(getenv("SWH_FILT_WGS")) : 1024;
+    // workgroups' LDS histogram atomics, so spread a row over up to the policy's filt_wgs
+    const int target = launch_policy().filt_wgs;
     int S = 1;
     while (S < kFiltSplit && B * S < target && V / (S * 2) >= 2048) S *= 2;
     int64_t chunk = (V + S - 1) / S;

@@ -320,19 +320,12 @@ __global__ __launch_bounds__(256) void tn_fold_kernel(const float *__restrict__ 
 
 using namespace swh;
 
-template <typename K>
-static bool lds_attr(K *kern, int bytes) {
-    return hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               bytes) == hipSuccess;
-}
-
 template <int NS, int BK>
 static int launch_nt(const void *A, const void *B, const void *bias, void *C, int64_t M, int64_t N, int64_t K,
                      int64_t lda, int64_t ldb, int64_t ldc, int64_t tiles, hipStream_t s) {
     constexpr int lds = NS * 2 * kGT * BK * 2;
-    static const bool attr =
-        lds_attr(&gemm_nt_kernel<true, NS, BK>, lds) && lds_attr(&gemm_nt_kernel<false, NS, BK>, lds);
-    if (!attr) return SWH_E_LAUNCH;
+    if (!lds_opt_in<&gemm_nt_kernel<true, NS, BK>>() || !lds_opt_in<&gemm_nt_kernel<false, NS, BK>>())
+        return SWH_E_LAUNCH;
     if (bias)
         gemm_nt_kernel<true, NS, BK><<<(unsigned)tiles, kGThreads, lds, s>>>(
             static_cast<const uint16_t *>(A), static_cast<const uint16_t *>(B), static_cast<const uint16_t *>(bias),
@@ -362,8 +355,7 @@ template <int NS, int BK>
 static int launch_tn(const void *dY, const void *X, float *part, int64_t M, int64_t N, int64_t K, int64_t lddy,
                      int64_t ldx, int S, int64_t grid, hipStream_t s) {
     constexpr int lds = NS * 2 * kGT * BK * 2;
-    static const bool attr = lds_attr(&gemm_tn_kernel<NS, BK>, lds);
-    if (!attr) return SWH_E_LAUNCH;
+    if (!lds_opt_in<&gemm_tn_kernel<NS, BK>>()) return SWH_E_LAUNCH;
     const int steps = (int)(M / BK), sps = (steps + S - 1) / S;
     gemm_tn_kernel<NS, BK><<<(unsigned)grid, kGThreads, lds, s>>>(static_cast<const uint16_t *>(dY),
                                                                    static_cast<const uint16_t *>(X), part, (int)M,

@@ -345,23 +345,11 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
     }
 }
 
-int wide_split(int64_t ncb, int64_t K) {
-    static int ncu = 0;
-    if (!ncu) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-            ncu = 256;
-    }
+// K split: about one workgroup per CU, at most smax (the launch policy's wide_smax, 1..8:
+// the last arriver reads S x 32 KB of slabs and its reduction holds up to 8 per piece)
+int wide_split(int64_t ncb, int64_t K, int smax) {
     const int64_t nr = K / kWKC;
-    int64_t s = (ncu + ncb / 2) / ncb;  // about one workgroup per CU
-    static int smax = 0;
-    if (!smax) {  // the last arriver reads S x 32 KB of slabs (SWH_WIDE_SMAX: A/B)
-        const char *e = getenv("SWH_WIDE_SMAX");
-        smax = e ? atoi(e) : 8;
-        if (smax < 1) smax = 1;
-        if (smax > 8) smax = 8;  // the last arriver's reduction holds up to 8 slabs per piece
-    }
+    int64_t s = (cu_count() + ncb / 2) / ncb;
     if (s > smax) s = smax;
     if (s < 1) s = 1;
     if (s > nr) s = nr;
@@ -371,27 +359,19 @@ int wide_split(int64_t ncb, int64_t K) {
 // 16-row weight groups per wave: 2 when the 256-row tiles alone fill the CUs (no K split:
 // the Llama-3-8B lm head, 4.57 -> 4.96 TB/s), where halving the X bytes per weight byte
 // pays; with a split (gate/up: 112 tiles x 2) the hand-off costs more (58 -> 68 us).
-// SWH_WIDE_CB=1/2 forces one (A/B)
-int wide_cb(int64_t wcols, int64_t K) {
-    const char *e = getenv("SWH_WIDE_CB");
-    const int forced = e ? atoi(e) : 0;
+// The launch policy's wide_cb = 1 / 2 forces one (A/B).
+int wide_cb(int64_t wcols, int64_t K, const swh_launch_policy &pol) {
     const bool two_ok = wcols % WGeo<2>::NB == 0;
-    if (forced == 1 || !two_ok) return 1;
-    if (forced == 2) return 2;
-    return wide_split(wcols / WGeo<2>::NB, K) == 1 ? 2 : 1;
+    if (pol.wide_cb == 1 || !two_ok) return 1;
+    if (pol.wide_cb == 2) return 2;
+    return wide_split(wcols / WGeo<2>::NB, K, pol.wide_smax) == 1 ? 2 : 1;
 }
 
 template <int EPI, int NM, bool BIAS, bool PACKED, int CB>
 int launch_wide(dim3 grid, hipStream_t st, const uint16_t *x, const uint16_t *w, int M, int N, int K, float eps,
                 const float *ss_in, const uint16_t *bias, uint16_t *res, float *ss_out, uint16_t *y, int ldy,
                 float *slabs, int *counters) {
-    static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in once per kernel
-    if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&wide_gemm_kernel<EPI, NM, BIAS, PACKED, CB>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, WGeo<CB>::LDS) != hipSuccess)
-            return SWH_E_LAUNCH;
-        attr = true;
-    }
+    if (!lds_opt_in<&wide_gemm_kernel<EPI, NM, BIAS, PACKED, CB>>()) return SWH_E_LAUNCH;  // > 64 KB LDS
     wide_gemm_kernel<EPI, NM, BIAS, PACKED, CB><<<grid, kWT, WGeo<CB>::LDS, st>>>(
         x, w, M, N, K, eps, ss_in, bias, res, ss_out, y, ldy, slabs, counters);
     return launch_status();
@@ -410,10 +390,10 @@ bool wide_gemm_eligible(int64_t M, int64_t N, int64_t K, int32_t silu) {
 int64_t wide_gemm_slab_bytes(int64_t M, int64_t N, int64_t K, int32_t silu) {
     if (!wide_gemm_eligible(M, N, K, silu)) return 0;
     int64_t most = 0;
-    for (int cb = 1; cb <= 2; ++cb) {  // either tiling (SWH_WIDE_CB may change between calls)
+    for (int cb = 1; cb <= 2; ++cb) {  // either tiling and the largest split (the policy may change between calls)
         const int64_t wcols = silu ? 2 * N : N, nb = (int64_t)kWNB * cb;
         if (wcols % nb) continue;
-        const int s = wide_split(wcols / nb, K);
+        const int s = wide_split(wcols / nb, K, 8);
         const int64_t b = s > 1 ? wcols / nb * s * 64 * nb * (int64_t)sizeof(float) : 0;
         most = b > most ? b : most;
     }
@@ -439,9 +419,10 @@ int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, flo
               int64_t workspace_bytes, int64_t counter_bytes, int32_t packed, hipStream_t st) {
     if (!wide_gemm_eligible(M, N, K, silu)) return 1;
     const int64_t wcols = silu ? 2 * N : N;
-    const int cb = wide_cb(wcols, K);
+    const swh_launch_policy pol = launch_policy();
+    const int cb = wide_cb(wcols, K, pol);
     const int64_t nb = (int64_t)kWNB * cb, ncb = wcols / nb;
-    const int s = wide_split(ncb, K);
+    const int s = wide_split(ncb, K, pol.wide_smax);
     if (ncb * (int64_t)sizeof(int) > counter_bytes) return 1;
     float *slabs = nullptr;
     if (s > 1) {

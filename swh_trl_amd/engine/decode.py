@@ -27,7 +27,7 @@ from typing import Optional
 
 import torch
 
-from .. import nn_ops, ops
+from .. import _lib, nn_ops, ops
 from ..profiling import trace as _trace
 from .._lib import call
 from .model import CausalLM
@@ -143,14 +143,15 @@ class DecodeEngine:
                 self.fw[f"l{i}.qkv_w"] = torch.empty_like(model.p[f"l{i}.qkv_w"])
                 self.fw[f"l{i}.gu_w"] = torch.empty_like(model.p[f"l{i}.gu_w"])
             self.fw["lm"] = torch.empty_like(model.lm_weight())
-        # Bandwidth-regime projections (Llama-3-8B widths: K >= SWH_WIDE_KMIN, >= 1024 weight
+        # the launch policy's route to the bandwidth-regime GEMM (the library decides by it too)
+        pol = _lib.get_launch_policy()
+        wide_on, kmin = bool(pol["wide_gemm"]), int(pol["wide_kmin"])
+        # Bandwidth-regime projections (Llama-3-8B widths: K >= the policy's wide_kmin, >= 1024 weight
         # rows) read a copy of their weight in wide_gemm's fragment order (contiguous 4 KB
         # runs per wave and round instead of 16 rows 64 B each, csrc/wide_gemm.hip), the
         # folded norm applied while packing; SWH_WIDE_PACK=0 keeps the row-major weights
         self.packed = {}
-        if self.fold and os.environ.get("SWH_WIDE_PACK", "1") != "0" and \
-                os.environ.get("SWH_WIDE_GEMM", "1") != "0":
-            kmin = int(os.environ.get("SWH_WIDE_KMIN", "2048"))
+        if self.fold and os.environ.get("SWH_WIDE_PACK", "1") != "0" and wide_on:
             for name, (N, K, silu, _norm) in self._projections().items():
                 if K >= kmin and nn_ops.wide_gemm_eligible(B, N, K, silu):
                     self.packed[name] = torch.empty(N * K * (2 if silu else 1), **bf)
@@ -164,8 +165,6 @@ class DecodeEngine:
         # its result).  The lm head's copy serves the fused sampler and the logits path alike.
         self.fragw = {}
         if self.fused and os.environ.get("SWH_FRAGW", "1") != "0":
-            wide_on = os.environ.get("SWH_WIDE_GEMM", "1") != "0"
-            kmin = int(os.environ.get("SWH_WIDE_KMIN", "2048"))
             for name, (N, K, silu, norm) in self._projections().items():
                 if norm is not None and not self.fold:
                     continue

@@ -24,3 +24,20 @@ def cuda_device():
     if not torch.cuda.is_available():
         pytest.fail("GPU test run without a visible GPU")
     return torch.device("cuda:0")
+
+
+@pytest.fixture
+def launch_policy():
+    """Set fields of the library's launch policy (swh_set_launch_policy) for one
+    test; the policy in force before the first call is restored afterwards."""
+    from swh_trl_amd import _lib
+    saved = []
+
+    def set_(**fields):
+        old = _lib.set_launch_policy(**fields)
+        if not saved:
+            saved.append(old)
+
+    yield set_
+    if saved:
+        _lib.set_launch_policy(**saved[0])

@@ -144,3 +144,98 @@ def test_no_call_site_passes_a_literal_dtype_code():
                     bad.append(f"{os.path.relpath(path, ROOT)}:{node.lineno} {name} arg {i}")
     assert seen >= 30, seen
     assert not bad, bad
+
+
+def test_launch_policy_roundtrip_and_validation(lib):
+    """The launch policy is the library's only settable state: defaults, a
+    round trip, range checks on the host, and restore."""
+    from swh_trl_amd import _lib
+    d = _lib.LaunchPolicy()
+    assert lib.swh_launch_policy_default(ctypes.byref(d)) == 0
+    assert (d.wide_kmin, d.wide_gemm, d.wide_smax, d.xstream, d.lm_ring14, d.filt_wgs) == (2048, 1, 8, 1, 1, 1024)
+    before = _lib.get_launch_policy()
+    try:
+        with _lib.launch_policy(gemm_cfg="4,2,1,1", xstream=0, wide_cb=2):
+            p = _lib.get_launch_policy()
+            assert (p["gemm_ms"], p["gemm_cb"], p["gemm_s"], p["gemm_persist"], p["gemm_wn"]) == (4, 2, 1, 1, 1)
+            assert p["xstream"] == 0 and p["wide_cb"] == 2
+        assert _lib.get_launch_policy() == before
+        for bad in ({"wide_smax": 9}, {"wide_cb": 3}, {"gemm_cfg": "3,1,1"}, {"gemm_nw": 5}, {"filt_wgs": 1},
+                    {"gemm_cb": 2}):  # a geometry field without gemm_ms
+            with pytest.raises(ValueError):
+                _lib.set_launch_policy(**bad)
+            assert _lib.get_launch_policy() == before
+        with pytest.raises(ValueError, match="unknown"):
+            _lib.set_launch_policy(not_a_field=1)
+    finally:
+        _lib.set_launch_policy(**before)
+
+
+def test_host_entry_points_are_thread_safe(lib):
+    """Host-side entry points (eligibility, workspace sizing over the cost model
+    and the per-device CU table, the policy) called from 8 host threads at once,
+    while another thread flips the launch policy, agree with single-threaded
+    answers: the per-device tables are initialised under std::call_once and the
+    policy is read under a lock."""
+    import threading
+
+    from swh_trl_amd import _lib
+    shapes = [(64, 896, 896, 0), (64, 1152, 896, 0), (64, 4864, 896, 1), (64, 896, 4864, 0), (64, 4096, 4096, 0),
+              (64, 14336, 4096, 1), (64, 4096, 14336, 0), (64, 128256, 4096, 0), (5, 256, 512, 0)]
+
+    def answers():
+        out = []
+        for M, N, K, silu in shapes:
+            out.append((lib.swh_wide_gemm_eligible(M, N, K, silu), lib.swh_decode_gemm_workspace_bytes(M, N, K),
+                        lib.swh_lm_head_sample_workspace_bytes(M, N, K), lib.swh_sample_workspace_bytes(M, N)))
+        return out
+
+    want = answers()
+    before = _lib.get_launch_policy()
+    errors, stop = [], threading.Event()
+
+    def worker():
+        try:
+            for _ in range(200):
+                assert answers() == want
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    def flipper():  # policy changes that leave every answer above unchanged
+        while not stop.is_set():
+            for v in (0, 1):
+                _lib.set_launch_policy(xstream=v, lm_ring14=v)
+
+    ts = [threading.Thread(target=worker) for _ in range(8)]
+    f = threading.Thread(target=flipper)
+    f.start()
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    stop.set()
+    f.join()
+    _lib.set_launch_policy(**before)
+    assert not errors, errors
+
+
+def test_library_holds_no_hidden_state():
+    """csrc/ reads no environment variable and declares no mutable static
+    outside the call_once-guarded per-device tables (csrc/lib.hip, the LDS
+    opt-in of common.hpp) and the lock-guarded launch policy."""
+    csrc = os.path.join(ROOT, "swh_trl_amd", "csrc")
+    allowed = {("lib.hip", "static std::once_flag once[kMaxDevices];"), ("lib.hip", "static int cus[kMaxDevices];"),
+               ("common.hpp", "static std::once_flag once[kMaxDevices];"),
+               ("common.hpp", "static bool ok[kMaxDevices];")}
+    found = set()
+    for f in sorted(os.listdir(csrc)):
+        src = re.sub(r"/\*.*?\*/", "", open(os.path.join(csrc, f)).read(), flags=re.S)
+        for line in src.split("\n"):
+            code = line.split("//")[0].strip()
+            assert "getenv" not in code, (f, line)
+            m = re.match(r"static\s+(?!constexpr|inline|__|void\b)([\w:<>, ]+?)\s+(\w+)\s*(\[[^\]]*\])?\s*(=|;|\{)", code)
+            if m and "(" not in code.split("=")[0]:
+                found.add((f, code))
+    assert found == allowed, found ^ allowed
+    lib_src = open(os.path.join(csrc, "lib.hip")).read()
+    assert "std::lock_guard<std::mutex>" in lib_src and "std::call_once" in lib_src

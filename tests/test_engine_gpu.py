@@ -750,7 +750,7 @@ def test_fragw_projections_generate_identically(dev, monkeypatch):
 
 
 @pytest.mark.parametrize("kmin", ["2048", "1024"])
-def test_packed_wide_projections_generate_identically(dev, monkeypatch, kmin):
+def test_packed_wide_projections_generate_identically(dev, monkeypatch, kmin, launch_policy):
     """DecodeEngine with the bandwidth-regime projections on packed weights
     (swh_wide_pack + swh_wide_gemm_packed; SWH_WIDE_KMIN 2048 packs down,
     1024 packs every projection and the lm head) generates the same tokens and
@@ -762,7 +762,7 @@ def test_packed_wide_projections_generate_identically(dev, monkeypatch, kmin):
     ids = torch.randint(0, m.cfg.vocab_size, (B, P), generator=g).to(dev)
     mask = torch.ones(B, P, dtype=torch.int64, device=dev)
     mask[3, :4] = 0
-    monkeypatch.setenv("SWH_WIDE_KMIN", kmin)
+    launch_policy(wide_kmin=int(kmin))
     outs = {}
     for pack in ("1", "0"):
         monkeypatch.setenv("SWH_WIDE_PACK", pack)
@@ -776,7 +776,6 @@ def test_packed_wide_projections_generate_identically(dev, monkeypatch, kmin):
         with_logp = eng.generate(ids, mask, C, temperature=0.9, seed=12, return_logp=True)
         outs[pack] = (greedy, sampled, with_logp)
         del eng
-    monkeypatch.delenv("SWH_WIDE_KMIN")
     for a, b in zip(outs["1"], outs["0"]):
         for x, y in zip(a, b):
             if isinstance(x, torch.Tensor):
@@ -962,7 +961,7 @@ def test_attn_l3_warmup_generates_identically(dev, monkeypatch):
                     assert torch.equal(x, y)
 
 
-def test_lm_ring14_generates_identically(dev, monkeypatch):
+def test_lm_ring14_generates_identically(dev, launch_policy):
     """The fused lm-head sampler with the half-tile weight ring and 12 waves
     per workgroup (SWH_LM_RING14=1, K = 896) draws the same tokens as the
     whole-tile ring, greedy and sampled, across several tiles per wave."""
@@ -977,7 +976,7 @@ def test_lm_ring14_generates_identically(dev, monkeypatch):
     mask = torch.ones(B, P, dtype=torch.int64, device=dev)
     outs = {}
     for flag in ("1", "0"):
-        monkeypatch.setenv("SWH_LM_RING14", flag)
+        launch_policy(lm_ring14=int(flag))
         eng = DecodeEngine(m, B, P, C)
         outs[flag] = (eng.generate(ids, mask, C, greedy=True), eng.generate(ids, mask, C, temperature=0.9, seed=5))
         del eng

@@ -1055,14 +1055,12 @@ def test_rmsnorm_statistic_handoff(ops, dev):
                                     ("1,1,1", "4"), ("2,2,1", "4"), ("4,1,3", "16"), ("4,4,1,0,4", None),
                                     ("4,4,1,0,2", None), ("2,2,2,0,2", None), ("4,2,1,1,2", None),
                                     ("4,4,1,0,4", "4"), ("1,4,3,0,4", None)])
-def test_decode_gemm_launch_configs(ops, dev, cfg, nw, monkeypatch):
+def test_decode_gemm_launch_configs(ops, dev, cfg, nw, launch_policy):
     """Every (row blocks, column blocks, K split[, persistent]) geometry and
     wave count computes the same GEMM: normed + bias, residual + statistic,
     SiLU gate."""
     from swh_trl_amd import nn_ops
-    monkeypatch.setenv("SWH_GEMM_CFG", cfg)
-    if nw is not None:
-        monkeypatch.setenv("SWH_GEMM_NW", nw)
+    launch_policy(gemm_cfg=cfg, gemm_nw=int(nw) if nw is not None else 0)
     g = _gen(34)
     M, H, I = 40, 896, 1024
     s = torch.randn(M, H, generator=g).to(torch.bfloat16).to(dev)
@@ -1194,7 +1192,7 @@ def test_decode_gemm_folded_norm(ops, dev, M, N, K, silu):
 
 
 @pytest.mark.parametrize("M,N,K", [(64, 896, 896), (64, 896, 4864), (37, 896, 4864), (5, 256, 512), (64, 896, 2048)])
-def test_xstream_residual_equals_lds_image_kernel(ops, dev, monkeypatch, M, N, K):
+def test_xstream_residual_equals_lds_image_kernel(ops, dev, M, N, K, launch_policy):
     """o_proj / down_proj with X fragments streamed into registers
     (xstream_gemm_kernel) vs decode_gemm_kernel's LDS image (SWH_XSTREAM=0):
     the new residual rows and their chunk sums of squares are bit-identical
@@ -1207,7 +1205,7 @@ def test_xstream_residual_equals_lds_image_kernel(ops, dev, monkeypatch, M, N, K
     s0 = torch.randn(M, N, generator=g).to(torch.bfloat16).to(dev)
     outs = {}
     for flag in ("1", "0"):
-        monkeypatch.setenv("SWH_XSTREAM", flag)
+        launch_policy(xstream=int(flag))
         r = s0.clone()
         ss = torch.full((M, N // 16), float("nan"), device=dev)
         nn_ops.decode_gemm(x, w, residual=r, ss_out=ss)
@@ -1226,7 +1224,7 @@ def test_xstream_residual_equals_lds_image_kernel(ops, dev, monkeypatch, M, N, K
                                         (64, 256, 1024, "plain"), (64, 4864, 896, "silu"), (37, 4864, 896, "silu"),
                                         (16, 512, 256, "silu")])
 @pytest.mark.parametrize("cfg", [None, "1,1,2", "2,1,1", "4,2,1,1"])
-def test_decode_gemm_fragw_equals_row_major(ops, dev, monkeypatch, M, N, K, kind, cfg):
+def test_decode_gemm_fragw_equals_row_major(ops, dev, M, N, K, kind, cfg, launch_policy):
     """swh_frag_pack's layout element for element against a torch restatement,
     and swh_decode_gemm_fragw on it bit-identical to swh_decode_gemm on the
     row-major weight: residual + chunk sums of squares (o / down), folded norm
@@ -1249,7 +1247,7 @@ def test_decode_gemm_fragw_equals_row_major(ops, dev, monkeypatch, M, N, K, kind
         assert torch.equal(wp, ref.view(2 * N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(2 * N, K))
         w = (wu.float() * nw.float()).to(torch.bfloat16)
     if cfg:
-        monkeypatch.setenv("SWH_GEMM_CFG", cfg)
+        launch_policy(gemm_cfg=cfg)
     outs = []
     for fw in (True, False):
         kw = {}
@@ -1295,7 +1293,7 @@ def test_act_frag_gate_up_to_down_equals_row_major(ops, dev, M):
 
 
 @pytest.mark.parametrize("M,N,K", [(64, 1152, 896), (37, 1152, 896), (64, 384, 512), (20, 1152, 896)])
-def test_xstream_qkv_equals_lds_image_kernel(ops, dev, monkeypatch, M, N, K):
+def test_xstream_qkv_equals_lds_image_kernel(ops, dev, M, N, K, launch_policy):
     """The qkv projection (folded RMSNorm row scale from the producer's chunk
     sums, bias) with X fragments streamed into registers equals
     decode_gemm_kernel's LDS-image form bit for bit (SWH_XSTREAM=0), and the
@@ -1309,7 +1307,7 @@ def test_xstream_qkv_equals_lds_image_kernel(ops, dev, monkeypatch, M, N, K):
     ss = _chunk_ss(x)
     outs = {}
     for flag in ("1", "0"):
-        monkeypatch.setenv("SWH_XSTREAM", flag)
+        launch_policy(xstream=int(flag))
         outs[flag] = nn_ops.decode_gemm(x, w * nw, ss_in=ss, eps=1e-6, bias=b)
     torch.cuda.synchronize()
     assert torch.equal(outs["1"], outs["0"])
@@ -1554,7 +1552,7 @@ def test_wide_gemm_packed_rejects_ineligible(ops, dev):
 
 
 @pytest.mark.parametrize("name,N,K", [("gate_up", 14336, 4096), ("lm_head", 128256, 4096), ("plain", 16384, 2048)])
-def test_wide_gemm_tilings_agree(ops, dev, monkeypatch, name, N, K):
+def test_wide_gemm_tilings_agree(ops, dev, name, N, K, launch_policy):
     """The two wide_gemm tilings (128 and 256 weight rows per workgroup,
     SWH_WIDE_CB=1/2) compute the same GEMM: they differ only in the K split,
     i.e. in fp32 summation order."""
@@ -1568,7 +1566,7 @@ def test_wide_gemm_tilings_agree(ops, dev, monkeypatch, name, N, K):
     wp = nn_ops.wide_pack(w, silu=silu)
     outs = []
     for cb in ("1", "2"):
-        monkeypatch.setenv("SWH_WIDE_CB", cb)
+        launch_policy(wide_cb=int(cb))
         outs.append(nn_ops.wide_gemm_packed(x, wp, N, silu=silu, ss_in=ss, eps=1e-5))
         assert torch.equal(outs[-1], nn_ops.wide_gemm_packed(x, wp, N, silu=silu, ss_in=ss, eps=1e-5))
     a, b = outs[0].float(), outs[1].float()

@@ -33,7 +33,7 @@ def _time(fn, reps=20, iters=3):
 
 
 def sweep(eng, m):
-    from swh_trl_amd import nn_ops
+    from swh_trl_amd import _lib, nn_ops
     c, p = eng.cfg, m.p
     eps, ss = c.rms_norm_eps, eng.ss
     shapes = {
@@ -55,10 +55,7 @@ def sweep(eng, m):
             "2,2,4", "1,2,2", "4,4,4"]
     print("cfg      " + " ".join(f"{k:>14s}" for k in shapes), flush=True)
     for cf in cfgs:
-        if cf is None:
-            os.environ.pop("SWH_GEMM_CFG", None)
-        else:
-            os.environ["SWH_GEMM_CFG"] = cf
+        _lib.set_launch_policy(gemm_cfg=cf)
         row = []
         for k, fn in shapes.items():
             if k.startswith("lm") and cf not in (None, "4,2,1,1", "4,4,1,1"):
@@ -69,12 +66,12 @@ def sweep(eng, m):
             except Exception as e:  # a geometry the shape does not divide into
                 row.append(float("nan"))
         print(f"{str(cf):8s} " + " ".join(f"{v:14.2f}" for v in row), flush=True)
-    os.environ.pop("SWH_GEMM_CFG", None)
+    _lib.set_launch_policy(gemm_cfg=None)
 
 
 def ku_sweep(eng, m):
-    """o / down / qkv under waves per workgroup (SWH_GEMM_NW) x geometry."""
-    from swh_trl_amd import nn_ops
+    """o / down / qkv under waves per workgroup (launch policy gemm_nw) x geometry."""
+    from swh_trl_amd import _lib, nn_ops
     c, p = eng.cfg, m.p
     ss, L = eng.ss, c.num_hidden_layers
     shapes = {
@@ -110,11 +107,7 @@ def ku_sweep(eng, m):
     for cf in cfgs:
         for ku in ("",):
             for nw in ("8",):
-                for k, v in (("SWH_GEMM_CFG", cf), ("SWH_GEMM_NW", nw)):
-                    if v is None:
-                        os.environ.pop(k, None)
-                    else:
-                        os.environ[k] = v
+                _lib.set_launch_policy(gemm_cfg=cf, gemm_nw=int(nw))
                 row = []
                 for name, fn in shapes.items():
                     try:
@@ -122,14 +115,13 @@ def ku_sweep(eng, m):
                     except Exception:
                         row.append(float("nan"))
                 print(f"{str(cf):12s} {nw:>2s} " + " ".join(f"{v:9.2f}" for v in row), flush=True)
-    for k in ("SWH_GEMM_CFG", "SWH_GEMM_NW"):
-        os.environ.pop(k, None)
+    _lib.set_launch_policy(gemm_cfg=None, gemm_nw=0)
 
 
 def dual(eng, m):
     """Two half-batch chains on two streams of one graph vs one full-batch chain:
     does running independent decode kernels concurrently hide their latency?"""
-    from swh_trl_amd import nn_ops
+    from swh_trl_amd import _lib, nn_ops
     c, p = eng.cfg, m.p
     eps, ss, B = c.rms_norm_eps, eng.ss, eng.B
     L, h = c.num_hidden_layers, eng.B // 2
@@ -223,8 +215,9 @@ def main():
     ap.add_argument("--ku", action="store_true", help="weight-round depth x waves x geometry sweep (o, down, qkv)")
     ap.add_argument("--lm", action="store_true", help="lm-head sampler: sampling vs greedy")
     args = ap.parse_args()
+    from swh_trl_amd import _lib
     if args.gemm_cfg:
-        os.environ["SWH_GEMM_CFG"] = args.gemm_cfg
+        _lib.set_launch_policy(gemm_cfg=args.gemm_cfg)
     from swh_trl_amd.engine.config import qwen2_5_0_5b
     from swh_trl_amd.engine.decode import DecodeEngine
     from swh_trl_amd.engine.model import CausalLM

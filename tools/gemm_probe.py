@@ -23,17 +23,24 @@ def build():
     os.makedirs(os.path.dirname(SO), exist_ok=True)
     subprocess.check_call(["hipcc", "-O3", "--offload-arch=gfx950", "-fPIC", "-shared", "-std=c++17",
                            "-munsafe-fp-atomics", os.path.join(ROOT, "tools", "gemm_probe.hip"),
-                           os.path.join(ROOT, "swh_trl_amd", "csrc", "wide_gemm.hip"), "-o", SO])
+                           os.path.join(ROOT, "swh_trl_amd", "csrc", "wide_gemm.hip"),
+                           os.path.join(ROOT, "swh_trl_amd", "csrc", "lib.hip"), "-o", SO])
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cfg", default=None)
     args = ap.parse_args()
-    if args.cfg:
-        os.environ["SWH_GEMM_CFG"] = args.cfg
     build()
     lib = ctypes.CDLL(SO)
+    if args.cfg:  # the probe library's own launch policy (the library reads no environment)
+        sys.path.insert(0, ROOT)
+        from swh_trl_amd import _lib as L
+        pol = L.LaunchPolicy()
+        lib.swh_get_launch_policy(ctypes.byref(pol))
+        for k, v in L._geometry_fields(args.cfg).items():
+            setattr(pol, k, v)
+        assert lib.swh_set_launch_policy(ctypes.byref(pol)) == 0, args.cfg
     vp, i64, i32, f32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_float
     lib.swh_decode_gemm.argtypes = [vp, vp, i64, i64, i64, vp, f32, vp, vp, i32, vp, i64, vp, vp, vp, i64, vp]
     lib.swh_decode_gemm.restype = i32

@@ -32,7 +32,7 @@ for step in "$@"; do
         > $O/${tag}_smoke.log 2>&1 || fail smoke $? $O/${tag}_smoke.log
       tail -1 $O/${tag}_smoke.log ;;
     sel)
-      timeout -k 10 600 python -u -m pytest tests -v -m gpu -k "$SEL" --timeout 300 --timeout-method thread \
+      timeout -k 10 600 python -u -m pytest tests -v -rP -m gpu -k "$SEL" --timeout 300 --timeout-method thread \
         > $O/${tag}_gpu_sel.log 2>&1; rc=$?
       grep -E "FAILED|ERROR|passed|failed" $O/${tag}_gpu_sel.log | tail -30
       [ $rc -eq 0 ] || fail sel $rc $O/${tag}_gpu_sel.log ;;

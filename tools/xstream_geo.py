@@ -1,5 +1,5 @@
 """Time the register-streamed qkv / o projections (fragment-order weights) under
-the cost model's geometry and forced ones (SWH_GEMM_CFG)."""
+the cost model's geometry and forced ones (the launch policy's geometry override)."""
 import os
 import sys
 
@@ -29,10 +29,7 @@ def main():
         "o": lambda: nn_ops.decode_gemm_fragw(x, wo, residual=res, ss_out=sso),
     }
     for cfg in (None, "1,1,1", "2,1,1", "4,1,1", "1,2,1", "2,2,1"):
-        if cfg is None:
-            os.environ.pop("SWH_GEMM_CFG", None)
-        else:
-            os.environ["SWH_GEMM_CFG"] = cfg
+        _lib.set_launch_policy(gemm_cfg=cfg)
         row = []
         for name, fn in shapes.items():
             for _ in range(3):
