@@ -565,9 +565,13 @@ __global__ __launch_bounds__(256) void fa_dkdv_kernel(FaArgs a) {
     // sequence carries this one's prompt queries)
     const int qstart = fa_qlive(a, b, 0) ? kb0 : max(kb0, a.P);
     const int nb = qstart < L ? (L - qstart + 32 * R - 1) / (32 * R) : 0, nit = G * nb;
+    // the prologue below prefetches unconditionally (fixed issue order); with no round
+    // (nb == 0: qstart >= L) it must still address valid rows: round 0 of head 0, whose
+    // row reads clamp to L - 1 and whose values are never used
+    const int nbs = nb > 0 ? nb : 1;
     auto rows_of = [&](int it, int64_t &qrow, int &r0) {
-        r0 = qstart + 32 * R * (it % nb);
-        qrow = ((int64_t)b * a.Hq + kvh * G + it / nb) * L;
+        r0 = qstart + 32 * R * (it % nbs);
+        qrow = ((int64_t)b * a.Hq + kvh * G + it / nbs) * L;
     };
     // a round's Q / dO blocks and its rows' lse (threads < 32 R) or delta (< 64 R), in
     // registers from load to LDS store; SWH_FA_PR rounds in flight ahead of the computed one
@@ -582,7 +586,7 @@ __global__ __launch_bounds__(256) void fa_dkdv_kernel(FaArgs a) {
         int64_t qrow;
         int r0;
         rows_of(it, qrow, r0);
-        const int hq = kvh * G + it / nb;
+        const int hq = kvh * G + it / nbs;
         auto qdrow = [&](int which, int row) -> const uint16_t * {
             return which ? dr_b.row(hq, row) : qr_b.row(hq, row);
         };
