@@ -1303,24 +1303,35 @@ __device__ __forceinline__ int64_t frag_at(int64_t b, int c, int K) {
     return (((b >> 4) * (K >> 5) + (c >> 5)) * 64 + ((c >> 3) & 3) * 16 + (b & 15)) * 8 + (c & 7);
 }
 
+#ifndef SWH_ATTN_WPS128
+#define SWH_ATTN_WPS128 2  // A/B: waves per SIMD the D = 128 instantiation is compiled for
+#endif
+#ifndef SWH_ATTN_JB128
+#define SWH_ATTN_JB128 2   // A/B: 16-key blocks per wave per round at D = 128 (even)
+#endif
 template <int D, int GQ>
-__global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
+__global__ __launch_bounds__(kAttnThreads, D == 128 ? SWH_ATTN_WPS128 : 2) void attn_decode_kernel(
     const uint16_t *__restrict__ qkv, uint16_t *__restrict__ kc, uint16_t *__restrict__ vc,
     const float *__restrict__ rcos, const float *__restrict__ rsin, const int32_t *__restrict__ plen,
     const int32_t *__restrict__ state, int Hq, int Hkv, int Tmax, float scale, uint16_t *__restrict__ out,
     AttnPrefetch pf) {
     static_assert(GQ <= 16, "a kv head serves at most 16 query heads");
+    static_assert(SWH_ATTN_JB128 % 2 == 0, "P V takes the key blocks in pairs");
     constexpr int DC = D / 32;                 // 32-dim chunks: k-steps of K Q^T
     constexpr int DB = D / 16;                 // 16-dim blocks of O^T
-    constexpr int JB = (D == 64) ? 4 : 2;      // key blocks per wave per round (pairs for P V)
+    constexpr int JB = (D == 64) ? 4 : SWH_ATTN_JB128;  // key blocks per wave per round (pairs for P V)
     constexpr int KPR = JB * 16 * kAttnWaves;  // keys per round
     constexpr int HD = D / 2;
     constexpr int VS = D + (D == 64 ? 8 : 16);  // V tile row stride (elements): conflict-free transposed reads
     __shared__ __attribute__((aligned(16))) uint16_t q_s[16 * D];
     __shared__ __attribute__((aligned(16))) uint16_t kn_s[D];
     __shared__ __attribute__((aligned(16))) uint16_t vn_s[D];
-    __shared__ __attribute__((aligned(16))) uint16_t vt_s[kAttnWaves][32 * VS];
-    __shared__ float red_s[kAttnWaves][16][D + 2];
+    // a wave's V tile (its key loop) and, after its loop, its (acc, m, l) record for the
+    // merge share one LDS slot: 2 workgroups per CU fit at D = 128 (78 KB instead of 144)
+    constexpr int kRed = 16 * (D + 2) * 4, kVt = 32 * VS * 2;
+    constexpr int kSlot = (kRed > kVt ? kRed : kVt) / 16 * 16;
+    __shared__ __attribute__((aligned(16))) unsigned char slot_s[kAttnWaves][kSlot];
+    auto red_s = [&](int w2, int h) -> float * { return reinterpret_cast<float *>(slot_s[w2]) + h * (D + 2); };
 
     const int kvh = blockIdx.x;
     const int64_t b = blockIdx.y;
@@ -1406,7 +1417,7 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
     f32x4 o[DB];                 // O^T: dims 16 db + 4 g + r, head c16
 #pragma unroll
     for (int d = 0; d < DB; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-    uint16_t *vt = vt_s[wid];
+    uint16_t *vt = reinterpret_cast<uint16_t *>(slot_s[wid]);
 
     for (int base = 0; base < n; base += KPR) {
         if (base) {
@@ -1487,31 +1498,36 @@ __global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
         }
     }
     SWH_GEMM_TRACE(3);
-    // row sums across the 4 lane groups, then the waves merge through LDS
+    // row sums across the 4 lane groups, then the waves merge through LDS (the record
+    // overwrites this wave's own V tile: its last transposed reads must retire first)
     l += __shfl_xor(l, 16, kWave);
     l += __shfl_xor(l, 32, kWave);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    float *rec = red_s(wid, c16);
 #pragma unroll
     for (int d = 0; d < DB; ++d)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) red_s[wid][c16][d * 16 + 4 * g + r] = o[d][r];
+        for (int r = 0; r < 4; ++r) rec[d * 16 + 4 * g + r] = o[d][r];
     if (g == 0) {
-        red_s[wid][c16][D] = m;
-        red_s[wid][c16][D + 1] = l;
+        rec[D] = m;
+        rec[D + 1] = l;
     }
     __syncthreads();
     SWH_GEMM_TRACE(4);
     auto merged = [&](int h, int d) -> uint16_t {  // the waves' (m, l, acc) of head h, dim d
         float mxw = kNegInf;
 #pragma unroll
-        for (int w2 = 0; w2 < kAttnWaves; ++w2) mxw = fmaxf(mxw, red_s[w2][h][D]);
+        for (int w2 = 0; w2 < kAttnWaves; ++w2) mxw = fmaxf(mxw, red_s(w2, h)[D]);
         float Ls = 0.f, A = 0.f;
 #pragma unroll
         for (int w2 = 0; w2 < kAttnWaves; ++w2) {
-            const float mq = red_s[w2][h][D];
+            const float *rw = red_s(w2, h);
+            const float mq = rw[D];
             if (mq == kNegInf) continue;
             const float cq = expf(mq - mxw);
-            Ls = fmaf(red_s[w2][h][D + 1], cq, Ls);
-            A = fmaf(red_s[w2][h][d], cq, A);
+            Ls = fmaf(rw[D + 1], cq, Ls);
+            A = fmaf(rw[d], cq, A);
         }
         return f32_to_bf16_bits(A / Ls);
     };

@@ -251,6 +251,60 @@ def test_ppo_update_schedule_bf16_matches_oracle(dev, width):
         _check_grads_bf16(f"{width}-step{s}-value", gv, ob[1], of[1])
 
 
+@pytest.mark.parametrize("width", WIDTHS)
+def test_ppo_two_update_bf16_trajectory_within_reference_bands(dev, width):
+    """Two PPO optimizer updates on one rollout (1 epoch x 2 mini-batches of GA 2,
+    ppo_trainer.py:537-617) run as trajectories: the product's bf16 run, and the
+    reference loop's own bf16 and fp32 runs (oracle ppo_update: the same micro-
+    batches, loss / GA, torch AdamW over the policy + value parameters, no
+    clipping) from the same initial weights.  For every micro-batch of both
+    updates, the product's policy loss, value loss and approx-KL stay within
+    twice the reference's own bf16-vs-fp32 trajectory gap (or twice that
+    statistic's expected bf16 noise, whichever is larger) plus one bf16 rounding,
+    against the reference's bf16 run and against its fp32 run.  The second
+    update starts from weights one AdamW step apart on all three runs (the
+    reference's bf16 run updates its bf16 parameters directly, the product keeps
+    fp32 masters), so the band there is the reference's own trajectory spread."""
+    from oracle import ppo_step
+    lr = 1e-4 if width == "tiny" else 1e-5
+    tr, ds = _trainer(dev, width=width, learning_rate=lr, num_ppo_epochs=1)
+    a = tr.args
+    assert a.num_mini_batches == 2 and a.gradient_accumulation_steps == 2
+    queries = tr._queries(ds[:a.local_batch_size])
+    responses, logprobs = tr.generate(queries)
+    ro = tr.rollout_from(queries, responses, logprobs)
+    perms = [torch.randperm(a.local_batch_size, generator=torch.Generator().manual_seed(7)).tolist()]
+    pol0, val0 = _hf(tr.policy_model, False), _hf(tr.value_model, True)
+    stats = tr.ppo_update(ro, lr, permutations=perms).cpu().reshape(-1, 9)  # [updates x GA, 9]
+    oro = _cpu(ro)
+    oro["values"] = oro["values"].float()
+    runs = {}
+    for dt in (torch.bfloat16, torch.float32):
+        pol, val = _hf(tr.policy_model, False, pol0.state_dict()).to(dt), _hf(tr.value_model, True,
+                                                                             val0.state_dict()).to(dt)
+        opt = torch.optim.AdamW(list(pol.parameters()) + list(val.parameters()), lr=lr,
+                                betas=(a.adam_beta1, a.adam_beta2), eps=a.adam_epsilon, weight_decay=a.weight_decay,
+                                foreach=False)
+        runs[dt] = ppo_step.ppo_update(pol, val, opt, oro, perms, local_mini_batch_size=a.local_mini_batch_size,
+                                       per_device_train_batch_size=a.per_device_train_batch_size,
+                                       gradient_accumulation_steps=a.gradient_accumulation_steps,
+                                       context_length=queries.shape[1], pad_token_id=PAD, temperature=a.temperature,
+                                       cliprange=a.cliprange, cliprange_value=a.cliprange_value, vf_coef=a.vf_coef,
+                                       token_terms=True)
+        del pol, val, opt
+    ob, of = runs[torch.bfloat16], runs[torch.float32]
+    assert len(ob) == len(of) == stats.shape[0] == 4
+    report = []
+    for j in range(4):
+        for i, k in ((0, "pg_loss"), (1, "vf_loss"), (4, "approxkl")):
+            band = _stat_band(k, ob[j], of[j])
+            p = float(stats[j, i])
+            report.append((j // 2, k, p, ob[j][k], of[j][k], band))
+            assert abs(p - ob[j][k]) <= band, (width, report[-1])
+            assert abs(p - of[j][k]) <= band, (width, report[-1])
+    print(width, "update, stat, product, oracle bf16, oracle fp32, band:", report)
+
+
 def test_ppo_trainer_train_runs(dev):
     tr, _ = _trainer(dev)
     before = tr.policy_model.flat.clone()
