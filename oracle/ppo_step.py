@@ -152,21 +152,43 @@ def mini_batch_backward(policy, value_model, ro: dict, mini, *, per_device_train
     return stats
 
 
+def accelerate_sync(step: int, gradient_accumulation_steps: int, end_of_dataloader: bool):
+    """accelerate 1.x `Accelerator._do_sync` (third-party, pinned accelerate >= 1.4 by
+    setup.cfg:44-47; restated from the installed 1.14.0): entering
+    `accelerator.accumulate(model)` at the last batch of a data epoch
+    (DataLoaderShard flags end_of_dataloader one batch ahead) resets the counter and
+    syncs; otherwise the counter increments and syncs every GA-th micro-batch.
+    Returns (new step, sync)."""
+    if end_of_dataloader:
+        return 0, True
+    step += 1
+    return step, step % gradient_accumulation_steps == 0
+
+
 def ppo_update(policy, value_model, optimizer, ro: dict, permutations, *, local_mini_batch_size: int,
-               per_device_train_batch_size: int, gradient_accumulation_steps: int, on_step=None, **loss_kw):
+               per_device_train_batch_size: int, gradient_accumulation_steps: int, on_step=None,
+               accum_step: int = 0, end_of_dataloader: bool = False, **loss_kw):
     """ppo_trainer.py:537-617: for each epoch's permutation, mini-batches of
-    GA micro-batches, loss / GA accumulated, one optimizer step per mini-batch.
-    on_step(): called before each optimizer step (the accumulated gradients)."""
+    micro-batches, each inside `accelerator.accumulate(model)`: loss / GA
+    back-propagated (accelerator.backward), then optimizer.step() and
+    zero_grad(), which the AcceleratedOptimizer performs only on a sync
+    (accelerate_sync).  on_step(): called before each performed optimizer step
+    (the accumulated gradients).  Returns (per-micro stats, accumulation counter)."""
     n = ro["responses"].shape[0]
     all_stats = []
     for perm in permutations:
         perm = torch.as_tensor(perm)
         for m0 in range(0, n, local_mini_batch_size):
-            all_stats += mini_batch_backward(policy, value_model, ro, perm[m0:m0 + local_mini_batch_size],
-                                             per_device_train_batch_size=per_device_train_batch_size,
-                                             gradient_accumulation_steps=gradient_accumulation_steps, **loss_kw)
-            if on_step is not None:
-                on_step()
-            optimizer.step()
-            optimizer.zero_grad()
-    return all_stats
+            mini = perm[m0:m0 + local_mini_batch_size]
+            for u0 in range(0, len(mini), per_device_train_batch_size):
+                accum_step, sync = accelerate_sync(accum_step, gradient_accumulation_steps, end_of_dataloader)
+                loss, st = micro_batch_loss(policy, value_model, ro, mini[u0:u0 + per_device_train_batch_size],
+                                            **loss_kw)
+                (loss / gradient_accumulation_steps).backward()
+                all_stats.append(st)
+                if sync:
+                    if on_step is not None:
+                        on_step()
+                    optimizer.step()
+                    optimizer.zero_grad()
+    return all_stats, accum_step

@@ -1303,23 +1303,20 @@ __device__ __forceinline__ int64_t frag_at(int64_t b, int c, int K) {
     return (((b >> 4) * (K >> 5) + (c >> 5)) * 64 + ((c >> 3) & 3) * 16 + (b & 15)) * 8 + (c & 7);
 }
 
-#ifndef SWH_ATTN_WPS128
-#define SWH_ATTN_WPS128 2  // A/B: waves per SIMD the D = 128 instantiation is compiled for
-#endif
-#ifndef SWH_ATTN_JB128
-#define SWH_ATTN_JB128 2   // A/B: 16-key blocks per wave per round at D = 128 (even)
-#endif
+// Occupancy at D = 128 (Llama-3-8B), measured (profiles/r5_att_ab.log): 164 VGPRs, one
+// workgroup per CU.  Two per CU by a 128-VGPR bound spill (62 us against 41.5 us per
+// launch, Q fragments re-read from LDS 60 us); 4 key blocks per wave per round (256
+// VGPRs) 44.8 us.
 template <int D, int GQ>
-__global__ __launch_bounds__(kAttnThreads, D == 128 ? SWH_ATTN_WPS128 : 2) void attn_decode_kernel(
+__global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
     const uint16_t *__restrict__ qkv, uint16_t *__restrict__ kc, uint16_t *__restrict__ vc,
     const float *__restrict__ rcos, const float *__restrict__ rsin, const int32_t *__restrict__ plen,
     const int32_t *__restrict__ state, int Hq, int Hkv, int Tmax, float scale, uint16_t *__restrict__ out,
     AttnPrefetch pf) {
     static_assert(GQ <= 16, "a kv head serves at most 16 query heads");
-    static_assert(SWH_ATTN_JB128 % 2 == 0, "P V takes the key blocks in pairs");
     constexpr int DC = D / 32;                 // 32-dim chunks: k-steps of K Q^T
     constexpr int DB = D / 16;                 // 16-dim blocks of O^T
-    constexpr int JB = (D == 64) ? 4 : SWH_ATTN_JB128;  // key blocks per wave per round (pairs for P V)
+    constexpr int JB = (D == 64) ? 4 : 2;      // key blocks per wave per round (pairs for P V)
     constexpr int KPR = JB * 16 * kAttnWaves;  // keys per round
     constexpr int HD = D / 2;
     constexpr int VS = D + (D == 64 ? 8 : 16);  // V tile row stride (elements): conflict-free transposed reads

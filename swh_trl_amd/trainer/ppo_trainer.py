@@ -185,6 +185,7 @@ class PPOTrainer:
         self.control = self.callback_handler.control
         self._engine: Optional[DecodeEngine] = None
         self._engines: dict = {}
+        self._accum_step = 0     # accelerate's Accelerator.step (gradient-accumulation counter)
         self._gen_count = 0
         self._np_rng = np.random.default_rng(self.local_seed)
         self._data_gen = torch.Generator().manual_seed(args.seed)
@@ -193,15 +194,18 @@ class PPOTrainer:
     # ------------------------------------------------------------------ data
     def _batches(self):
         """DataLoader(shuffle=True, drop_last=True, batch_size=local_batch_size)
-        sharded over ranks, repeated forever (ppo_trainer.py:311-318, :358-362)."""
+        sharded over ranks, repeated forever (ppo_trainer.py:311-318, :358-362).
+        Yields (examples, last): `last` is accelerate's end_of_dataloader for the
+        batch (DataLoaderShard looks one batch ahead and flags the epoch's last)."""
         a = self.args
         n, per = self.train_dataset_len, a.local_batch_size
         glob = per * self.world
         while True:
             perm = torch.randperm(n, generator=self._data_gen).tolist()
-            for s in range(0, n - glob + 1, glob):
+            starts = list(range(0, n - glob + 1, glob))
+            for k, s in enumerate(starts):
                 mine = perm[s + self.rank * per: s + (self.rank + 1) * per]
-                yield [self.train_dataset[i] for i in mine]
+                yield [self.train_dataset[i] for i in mine], k == len(starts) - 1
 
     def _queries(self, examples) -> torch.Tensor:
         if "input_ids" not in examples[0]:
@@ -351,38 +355,72 @@ class PPOTrainer:
         self.policy_model.zero_grad()
         self.value_model.zero_grad()
 
-    def ppo_update(self, ro: dict, lr: float, permutations=None) -> torch.Tensor:
-        """num_ppo_epochs x mini-batches x GA micro-batches (ppo_trainer.py:537-617).
+    def _accumulate_sync(self, end_of_dataloader: bool) -> bool:
+        """accelerate's `Accelerator.accumulate` sync decision for one micro-batch
+        (accelerate/accelerator.py `_do_sync`, gradient_accumulation_steps = GA,
+        sync_with_dataloader on): at the data epoch's last batch every micro-batch
+        syncs (and the counter resets); otherwise the counter, which runs across
+        mini-batches, epochs and updates, syncs every GA-th.  The reference calls
+        optimizer.step() / zero_grad() after every micro-batch (ppo_trainer.py:
+        604-606); the AcceleratedOptimizer acts only on a sync."""
+        if end_of_dataloader:
+            self._accum_step = 0
+            return True
+        self._accum_step += 1
+        return self._accum_step % self.args.gradient_accumulation_steps == 0
+
+    def ppo_update(self, ro: dict, lr: float, permutations=None, end_of_dataloader: bool = False) -> torch.Tensor:
+        """num_ppo_epochs x mini-batches x micro-batches (ppo_trainer.py:537-617), with
+        the optimizer steps where the reference's accelerate accumulation takes them
+        (_accumulate_sync; loss / GA every micro-batch).  The micro-batches between
+        two steps see the same weights, so they run as ONE fused forward/backward
+        (each micro keeps its own masked means in the loss kernel; the gradient is
+        their sum) when the token budget allows.  Gradients of micro-batches after
+        the last sync stay accumulated for the next update, as the reference's do.
         `permutations` (tests): one index array per epoch instead of the RNG."""
         a = self.args
         stats = torch.zeros(a.num_ppo_epochs, a.num_mini_batches, a.gradient_accumulation_steps, 9,
                             device=self.device)
-        self.policy_model.zero_grad()
-        self.value_model.zero_grad()
+        mbs = a.per_device_train_batch_size
+        n_micro = a.local_mini_batch_size // mbs
+        width = ro["query_responses"].shape[1]
+        pending = []  # (epoch, mini, micro, row indices) since the last optimizer step
+
+        def run_pending():
+            if not pending:
+                return
+            if a.fuse_micro_batches and len(pending) * mbs * width <= a.fuse_token_budget:
+                out = self._micro_step(ro, torch.cat([p[3] for p in pending]), len(pending))
+                for (ep, mi, gi, _), row in zip(pending, out):
+                    stats[ep, mi, gi] = row
+            else:  # the reference schedule, one pass per micro-batch
+                for ep, mi, gi, inds in pending:
+                    stats[ep, mi, gi] = self._micro_step(ro, inds)[0]
+            pending.clear()
+
         for ep in range(a.num_ppo_epochs):
             b_inds = permutations[ep] if permutations is not None else self._np_rng.permutation(a.local_batch_size)
             b_inds = torch.as_tensor(np.asarray(b_inds), device=self.device, dtype=torch.long)
             for mi, mb0 in enumerate(range(0, a.local_batch_size, a.local_mini_batch_size)):
                 mini = b_inds[mb0:mb0 + a.local_mini_batch_size]
-                mbs = a.per_device_train_batch_size
-                n_micro = a.local_mini_batch_size // mbs
-                if a.fuse_micro_batches and mini.numel() * ro["query_responses"].shape[1] <= a.fuse_token_budget:
-                    stats[ep, mi, :n_micro] = self._micro_step(ro, mini[:n_micro * mbs], n_micro)
-                else:  # the reference schedule, one pass per micro-batch
-                    for gi in range(n_micro):
-                        stats[ep, mi, gi] = self._micro_step(ro, mini[gi * mbs:(gi + 1) * mbs])[0]
-                self._optimizer_step(lr)
+                for gi in range(n_micro):
+                    pending.append((ep, mi, gi, mini[gi * mbs:(gi + 1) * mbs]))
+                    if self._accumulate_sync(end_of_dataloader):
+                        run_pending()
+                        self._optimizer_step(lr)
+        run_pending()
         return stats
 
     # ------------------------------------------------------------------ the loop
-    def training_step(self, examples=None) -> dict:
+    def training_step(self, examples=None, end_of_dataloader: bool = False) -> dict:
         """One PPO update: rollout of local_batch_size queries, rewards, GAE,
-        then the PPO epochs (ppo_trainer.py:356-617)."""
+        then the PPO epochs (ppo_trainer.py:356-617).  Given `examples`, the batch
+        counts as a non-final batch of its data epoch unless `end_of_dataloader`."""
         a = self.args
         if examples is None:
             if getattr(self, "_iter", None) is None:
                 self._iter = self._batches()
-            examples = next(self._iter)
+            examples, end_of_dataloader = next(self._iter)
         self.state.episode += a.batch_size
         queries = self._queries(examples)
         _trace(f"queries {tuple(queries.shape)}")
@@ -392,7 +430,7 @@ class PPOTrainer:
         _trace("rollout scored")
         # create_optimizer_and_scheduler(num_training_steps=num_total_batches), stepped once per update (:232-234, :648)
         lr = a.learning_rate * schedule.for_args(a, max(1, a.num_total_batches))(self.state.global_step)
-        stats = self.ppo_update(ro, lr)
+        stats = self.ppo_update(ro, lr, end_of_dataloader=end_of_dataloader)
         _trace("ppo epochs")
         self.state.global_step += 1
         m = self._metrics

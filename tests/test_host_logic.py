@@ -313,3 +313,49 @@ def test_overlapped_allreduce_hooks_gloo():
     mean = (firsts[0][1] + firsts[1][1]) / 2
     for r in (0, 1):
         torch.testing.assert_close(reduced[r], mean)                       # released ranges + finish() remainder
+
+
+def test_ppo_accumulation_schedule_matches_accelerate():
+    """The reference PPO loop steps its optimizer inside `accelerator.accumulate`
+    (ppo_trainer.py:545-606): accelerate decides which micro-batches step.  The
+    oracle's restatement (oracle/ppo_step.py accelerate_sync) and the product's
+    counter (PPOTrainer._accumulate_sync) against the installed accelerate itself,
+    driven like the reference: a prepared DataLoader repeated forever, one batch per
+    update, every micro-batch of the PPO epochs inside `accumulate`; recorded: which
+    micro-batches sync.  Includes data epochs whose last batch makes every
+    micro-batch sync, and GA larger than the micro-batches of one mini-batch."""
+    from types import SimpleNamespace
+
+    from accelerate import Accelerator
+
+    from oracle import ppo_step
+    from swh_trl_amd.trainer.ppo_trainer import PPOTrainer
+
+    for GA, micros_per_update, n_batches, updates in [(2, 4, 3, 7), (4, 4, 2, 5), (2, 2, 1, 3), (3, 6, 4, 9)]:
+        acc = Accelerator(gradient_accumulation_steps=GA, cpu=True)
+        loader = acc.prepare(torch.utils.data.DataLoader(list(range(n_batches)), batch_size=1))
+        model = acc.prepare(torch.nn.Linear(1, 1))
+
+        def repeat():
+            while True:
+                yield from loader
+
+        it = iter(repeat())
+        want = []
+        for _ in range(updates):
+            next(it)
+            for _ in range(micros_per_update):
+                with acc.accumulate(model):
+                    want.append(acc.sync_gradients)
+        # restatements: end_of_dataloader = the update's batch is the data epoch's last
+        got_o, got_p, step = [], [], 0
+        prod = SimpleNamespace(_accum_step=0, args=SimpleNamespace(gradient_accumulation_steps=GA))
+        for u in range(updates):
+            eod = u % n_batches == n_batches - 1
+            for _ in range(micros_per_update):
+                step, sync = ppo_step.accelerate_sync(step, GA, eod)
+                got_o.append(sync)
+                got_p.append(PPOTrainer._accumulate_sync(prod, eod))
+        assert got_o == want, (GA, micros_per_update, n_batches, got_o, want)
+        assert got_p == want
+        acc.free_memory()

@@ -190,14 +190,36 @@ def test_ppo_micro_batch_bf16_matches_oracle(dev, width):
     print(width, "value", _check_grads_bf16(width + "-value", gv, vb, vf))
 
 
-@pytest.mark.parametrize("width", WIDTHS)
-def test_ppo_update_schedule_bf16_matches_oracle(dev, width):
-    """A full PPO update (ppo_trainer.py:537-617: epochs x mini-batches x GA, one
-    AdamW step per mini-batch, no clipping) on the bf16 path: before each
-    optimizer step the accumulated policy and value gradients equal the
-    reference's mini-batch (its GA micro-batches, loss / GA) evaluated in bf16
-    and in fp32 at the product's weights of that step, within the bf16-rounding
-    bounds.  Each step is checked from the product's own weights: after one
+def _sync_groups(a, perms, end_of_dataloader: bool, step0: int = 0):
+    """The micro-batches (row indices) between the reference's optimizer steps:
+    accelerate's accumulation (oracle/ppo_step.py accelerate_sync) over the
+    micro-batches of every epoch's permutation in order."""
+    from oracle import ppo_step
+    groups, cur, step = [], [], step0
+    for p in perms:
+        p = torch.as_tensor(p)
+        for m0 in range(0, a.local_batch_size, a.local_mini_batch_size):
+            mini = p[m0:m0 + a.local_mini_batch_size]
+            for u0 in range(0, len(mini), a.per_device_train_batch_size):
+                step, sync = ppo_step.accelerate_sync(step, a.gradient_accumulation_steps, end_of_dataloader)
+                cur.append(mini[u0:u0 + a.per_device_train_batch_size])
+                if sync:
+                    groups.append(torch.cat(cur))
+                    cur = []
+    return groups
+
+
+@pytest.mark.parametrize("width,eod", [("tiny", False), ("tiny", True), ("qwen2.5-0.5b-width", False)])
+def test_ppo_update_schedule_bf16_matches_oracle(dev, width, eod):
+    """A full PPO update (ppo_trainer.py:537-617: epochs x mini-batches x micro-
+    batches, no clipping) on the bf16 path, with the optimizer steps where the
+    reference's accelerate accumulation takes them: every GA-th micro-batch
+    across mini-batches (per-device 4 x GA 2 with 2 mini-batches: one step per two
+    mini-batches), or after every micro-batch at the data epoch's last batch
+    (end_of_dataloader).  Before each optimizer step the accumulated policy and
+    value gradients equal the reference's micro-batches since the previous step
+    (loss / GA each) evaluated in bf16 and in fp32 at the product's weights of
+    that step, within the bf16-rounding bounds.  Each step is checked from the product's own weights: after one
     AdamW step (whose first update is ~lr * sign(grad)) two bf16 trajectories
     part by the sign noise of near-zero gradient elements, which says nothing
     about the schedule; the update itself is the AdamW kernel's own test.  At
@@ -227,10 +249,10 @@ def test_ppo_update_schedule_bf16_matches_oracle(dev, width):
         return step_fn(lr)
 
     tr._optimizer_step = capture
-    tr.ppo_update(ro, a.learning_rate, permutations=perms)
-    minis = [torch.as_tensor(p)[m0:m0 + a.local_mini_batch_size]
-             for p in perms for m0 in range(0, a.local_batch_size, a.local_mini_batch_size)]
-    assert len(prod_steps) == len(minis) == a.num_ppo_epochs * a.num_mini_batches
+    tr.ppo_update(ro, a.learning_rate, permutations=perms, end_of_dataloader=eod)
+    minis = _sync_groups(a, perms, eod)
+    micros = a.num_ppo_epochs * a.local_batch_size // a.per_device_train_batch_size
+    assert len(prod_steps) == len(minis) == (micros if eod else micros // a.gradient_accumulation_steps)
     models = {dt: (_hf(tr.policy_model, False).to(dt), _hf(tr.value_model, True).to(dt))
               for dt in (torch.bfloat16, torch.float32)}
     for s, ((wp, wv, gp, gv), mini) in enumerate(zip(prod_steps, minis)):
@@ -253,8 +275,8 @@ def test_ppo_update_schedule_bf16_matches_oracle(dev, width):
 
 @pytest.mark.parametrize("width", WIDTHS)
 def test_ppo_two_update_bf16_trajectory_within_reference_bands(dev, width):
-    """Two PPO optimizer updates on one rollout (1 epoch x 2 mini-batches of GA 2,
-    ppo_trainer.py:537-617) run as trajectories: the product's bf16 run, and the
+    """Two PPO optimizer updates on one rollout (2 epochs x 1 mini-batch of GA 2
+    micro-batches, ppo_trainer.py:537-617) run as trajectories: the product's bf16 run, and the
     reference loop's own bf16 and fp32 runs (oracle ppo_update: the same micro-
     batches, loss / GA, torch AdamW over the policy + value parameters, no
     clipping) from the same initial weights.  For every micro-batch of both
@@ -267,15 +289,18 @@ def test_ppo_two_update_bf16_trajectory_within_reference_bands(dev, width):
     fp32 masters), so the band there is the reference's own trajectory spread."""
     from oracle import ppo_step
     lr = 1e-4 if width == "tiny" else 1e-5
-    tr, ds = _trainer(dev, width=width, learning_rate=lr, num_ppo_epochs=1)
+    # local batch = per-device 4 x GA 2 = 8 rows, one mini-batch of 2 micro-batches per epoch
+    tr, ds = _trainer(dev, width=width, learning_rate=lr, num_ppo_epochs=2, num_mini_batches=1)
     a = tr.args
-    assert a.num_mini_batches == 2 and a.gradient_accumulation_steps == 2
+    n_micro = a.local_mini_batch_size // a.per_device_train_batch_size
+    assert n_micro == a.gradient_accumulation_steps == 2 and a.local_batch_size == 8
     queries = tr._queries(ds[:a.local_batch_size])
     responses, logprobs = tr.generate(queries)
     ro = tr.rollout_from(queries, responses, logprobs)
-    perms = [torch.randperm(a.local_batch_size, generator=torch.Generator().manual_seed(7)).tolist()]
+    perms = [torch.randperm(a.local_batch_size, generator=torch.Generator().manual_seed(7 + e)).tolist()
+             for e in range(a.num_ppo_epochs)]
     pol0, val0 = _hf(tr.policy_model, False), _hf(tr.value_model, True)
-    stats = tr.ppo_update(ro, lr, permutations=perms).cpu().reshape(-1, 9)  # [updates x GA, 9]
+    stats = tr.ppo_update(ro, lr, permutations=perms).cpu()[:, :, :n_micro].reshape(-1, 9)  # [updates x micro, 9]
     oro = _cpu(ro)
     oro["values"] = oro["values"].float()
     runs = {}
@@ -285,7 +310,7 @@ def test_ppo_two_update_bf16_trajectory_within_reference_bands(dev, width):
         opt = torch.optim.AdamW(list(pol.parameters()) + list(val.parameters()), lr=lr,
                                 betas=(a.adam_beta1, a.adam_beta2), eps=a.adam_epsilon, weight_decay=a.weight_decay,
                                 foreach=False)
-        runs[dt] = ppo_step.ppo_update(pol, val, opt, oro, perms, local_mini_batch_size=a.local_mini_batch_size,
+        runs[dt], _ = ppo_step.ppo_update(pol, val, opt, oro, perms, local_mini_batch_size=a.local_mini_batch_size,
                                        per_device_train_batch_size=a.per_device_train_batch_size,
                                        gradient_accumulation_steps=a.gradient_accumulation_steps,
                                        context_length=queries.shape[1], pad_token_id=PAD, temperature=a.temperature,
@@ -299,7 +324,7 @@ def test_ppo_two_update_bf16_trajectory_within_reference_bands(dev, width):
         for i, k in ((0, "pg_loss"), (1, "vf_loss"), (4, "approxkl")):
             band = _stat_band(k, ob[j], of[j])
             p = float(stats[j, i])
-            report.append((j // 2, k, p, ob[j][k], of[j][k], band))
+            report.append((j // n_micro, k, p, ob[j][k], of[j][k], band))
             assert abs(p - ob[j][k]) <= band, (width, report[-1])
             assert abs(p - of[j][k]) <= band, (width, report[-1])
     print(width, "update, stat, product, oracle bf16, oracle fp32, band:", report)

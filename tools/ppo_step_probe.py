@@ -43,8 +43,7 @@ def main(width, lr):
 
     tr._optimizer_step = capture
     tr.ppo_update(ro, a.learning_rate, permutations=perms)
-    minis = [torch.as_tensor(p)[m0:m0 + a.local_mini_batch_size]
-             for p in perms for m0 in range(0, a.local_batch_size, a.local_mini_batch_size)]
+    minis = T._sync_groups(a, perms, False)  # the micro-batches between the reference's optimizer steps
     models = {dt: (T._hf(tr.policy_model, False).to(dt), T._hf(tr.value_model, True).to(dt))
               for dt in (torch.bfloat16, torch.float32)}
     kw = dict(context_length=queries.shape[1], pad_token_id=T.PAD, temperature=a.temperature,
