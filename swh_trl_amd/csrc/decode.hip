@@ -997,21 +997,27 @@ __global__ __launch_bounds__(RD ? 768 : 512) void lm_head_kernel(const uint16_t 
         const uint16_t *wnext = wbase(ring ? t + tstep : t);
         const uint16_t *wcur = wbase(t);
         if constexpr (KSC != 0) {
-            // A fragments double-buffered one k-step ahead; the scheduling barrier
-            // keeps the compiler from hoisting every read (register pressure)
-            uint4 a[2][4];
+            // A fragments in a ring APF k-steps ahead of the MFMAs (APF 1: double-buffered);
+            // the scheduling barrier keeps the compiler from hoisting every read
+#ifndef SWH_LM_APF
+#define SWH_LM_APF 1
+#endif
+            constexpr int APF = RD ? 1 : SWH_LM_APF, AR = APF + 1;
+            uint4 a[AR][4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) a[0][i] = *reinterpret_cast<const uint4 *>(xrow + i * 16 * RS);
+            for (int p = 0; p < APF; ++p)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) a[p][i] = *reinterpret_cast<const uint4 *>(xrow + i * 16 * RS + p * 64);
 #pragma unroll
             for (int ks = 0; ks < KSC; ++ks) {
-                if (ks + 1 < KSC) {
+                if (ks + APF < KSC) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
-                        a[(ks + 1) & 1][i] = *reinterpret_cast<const uint4 *>(xrow + i * 16 * RS + (ks + 1) * 64);
+                        a[(ks + APF) % AR][i] = *reinterpret_cast<const uint4 *>(xrow + i * 16 * RS + (ks + APF) * 64);
                 }
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[ks & 1][i]), as_bf16x8(bv[ks % KR]),
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[ks % AR][i]), as_bf16x8(bv[ks % KR]),
                                                                     acc[i], 0, 0, 0);
                 if constexpr (RD != 0) {  // half-tile ring: this tile's second half, then the next tile's first
                     if (ks + KR < KSC) bv[ks % KR] = ld_w(wcur + (ks + KR) * wst);

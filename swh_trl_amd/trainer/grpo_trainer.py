@@ -1154,15 +1154,40 @@ class GRPOTrainer:
         self._batches = None
 
     def _total_steps(self) -> int:
+        """transformers Trainer.set_initial_training_values: max_steps, or
+        ceil(num_train_epochs x optimizer steps per epoch)."""
         a = self.args
         if a.max_steps and a.max_steps > 0:
             return a.max_steps
         return max(1, int(math.ceil(self._steps_per_epoch() * a.num_train_epochs)))
 
-    def _steps_per_epoch(self) -> float:
+    def _micro_steps_per_epoch(self) -> int:
+        """len(train dataloader) per rank: the RepeatSampler's generation batches
+        (grpo_trainer.py:1096-1130) times their repeat count spg x num_iterations, at
+        batch size per_device x spg (:1075) — one training_step each."""
         a = self.args
-        per_epoch = len(self.train_dataset) // (a.generation_batch_size // self.num_generations)
-        return max(1e-9, per_epoch * a.steps_per_generation * self.num_iterations / a.gradient_accumulation_steps)
+        n_gen = len(self.train_dataset) // (a.generation_batch_size // self.num_generations)
+        return n_gen * a.steps_per_generation * self.num_iterations
+
+    def _steps_per_epoch(self) -> int:
+        """Optimizer steps per epoch: ceil(micro-steps / GA) (the Trainer's last
+        update of an epoch takes the remainder)."""
+        GA = self.args.gradient_accumulation_steps
+        return max(1, -(-self._micro_steps_per_epoch() // GA))
+
+    def _check_epoch_remainder(self, total: int) -> None:
+        """The transformers Trainer closes every epoch with an update over the
+        remaining micro-batches (fewer than GA, loss / their count).  This loop
+        always accumulates GA micro-batches, so a run that would cross an epoch
+        end with a remainder is refused instead of trained differently."""
+        a = self.args
+        GA, mse = a.gradient_accumulation_steps, self._micro_steps_per_epoch()
+        if mse % GA and total * GA > mse:
+            raise ValueError(
+                f"{mse} micro-batches per epoch (generation batches x steps_per_generation x num_iterations) is not a "
+                f"multiple of gradient_accumulation_steps ({GA}): the reference Trainer ends each epoch with a shorter "
+                "accumulation, which the MI355X trainer does not implement; choose steps_per_generation / "
+                "gradient_accumulation_steps so that GA divides it, or max_steps within the first epoch")
 
     @staticmethod
     def _interval(x, total: int) -> int:
@@ -1185,6 +1210,7 @@ class GRPOTrainer:
                 raise ValueError(f"No valid checkpoint found in output directory ({a.output_dir})")
             self._load_checkpoint(d)
         total = self._total_steps()
+        self._check_epoch_remainder(total)
         st = self.state
         st.max_steps = total
         st.num_train_epochs = int(math.ceil(total / self._steps_per_epoch()))

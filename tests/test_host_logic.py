@@ -359,3 +359,34 @@ def test_ppo_accumulation_schedule_matches_accelerate():
         assert got_o == want, (GA, micros_per_update, n_batches, got_o, want)
         assert got_p == want
         acc.free_memory()
+
+
+def test_grpo_epoch_accounting_follows_trainer():
+    """transformers Trainer.set_initial_training_values over GRPO's dataloader
+    (grpo_trainer.py:1063-1130: batches of per_device x spg, RepeatSampler repeating
+    each generation batch spg x num_iterations times): optimizer steps per epoch =
+    ceil(micro-steps / GA).  A run whose epoch ends with fewer than GA micro-batches
+    (the Trainer's shorter last accumulation) is refused, not trained differently."""
+    import types
+
+    from swh_trl_amd.trainer.grpo_trainer import GRPOTrainer
+
+    def fake(n_prompts, **kw):
+        a = GRPOConfig(**kw)
+        ns = types.SimpleNamespace(args=a, num_generations=a.num_generations, num_iterations=a.num_iterations,
+                                   train_dataset=list(range(n_prompts)))
+        for name in ("_micro_steps_per_epoch", "_steps_per_epoch", "_total_steps", "_check_epoch_remainder"):
+            setattr(ns, name, types.MethodType(getattr(GRPOTrainer, name), ns))
+        return ns
+
+    # default: spg = GA, so every epoch is whole accumulations
+    t = fake(20, per_device_train_batch_size=8, gradient_accumulation_steps=2, num_generations=4, num_train_epochs=2)
+    assert t._micro_steps_per_epoch() == (20 // 4) * 2 and t._steps_per_epoch() == 5 and t._total_steps() == 10
+    t._check_epoch_remainder(t._total_steps())
+    # spg 2, GA 4, 3 generation batches per epoch: 6 micro-steps = 4 + a remainder of 2
+    t = fake(6, per_device_train_batch_size=4, gradient_accumulation_steps=4, steps_per_generation=2,
+             num_generations=4, num_train_epochs=1)
+    assert t._micro_steps_per_epoch() == 6 and t._steps_per_epoch() == 2
+    with pytest.raises(ValueError, match="not a multiple of gradient_accumulation_steps"):
+        t._check_epoch_remainder(t._total_steps())
+    t._check_epoch_remainder(1)  # max_steps inside the first epoch: no remainder is ever reached

@@ -14,7 +14,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     from swh_trl_amd import ops
     dev = torch.device("cuda:0")
-    B, V = 64, 151936
+    B = 64
+    V = int(os.environ.get("SAMPLER_V", "151936"))
     scale = float(os.environ.get("LOGIT_SCALE", "1.0"))
     g = torch.Generator(device=dev).manual_seed(0)
     logits = (torch.randn(B, V, device=dev, generator=g) * scale).to(torch.bfloat16)
@@ -24,7 +25,8 @@ def main():
     out = torch.zeros(B, 8, dtype=torch.int64, device=dev)
     cur = torch.zeros(B, dtype=torch.int64, device=dev)
     ws = torch.empty(ops._lib.load().swh_sample_workspace_bytes(B, V), dtype=torch.uint8, device=dev)
-    for name, kw in (("unfiltered", {}), ("min_p 0.05", dict(min_p=0.05)), ("top_k 50", dict(top_k=50)),
+    for name, kw in (("unfiltered", {}), ("T 0.7", dict(temperature=0.7)), ("greedy", dict(greedy=True)),
+                     ("min_p 0.05", dict(min_p=0.05)), ("top_k 50", dict(top_k=50)),
                      ("top_p 0.9", dict(top_p=0.9)), ("top_p 0.5", dict(top_p=0.5))):
         p = ops.make_sample_params(**kw)
 
