@@ -997,12 +997,10 @@ __global__ __launch_bounds__(RD ? 768 : 512) void lm_head_kernel(const uint16_t 
         const uint16_t *wnext = wbase(ring ? t + tstep : t);
         const uint16_t *wcur = wbase(t);
         if constexpr (KSC != 0) {
-            // A fragments in a ring APF k-steps ahead of the MFMAs (APF 1: double-buffered);
+            // A fragments double-buffered one k-step ahead (2 and 3 ahead measured no faster
+            // for gate/up: 11.24 / 11.38-11.42 against 11.15-11.21 us, profiles/r5_gu_apf_ab.log);
             // the scheduling barrier keeps the compiler from hoisting every read
-#ifndef SWH_LM_APF
-#define SWH_LM_APF 1
-#endif
-            constexpr int APF = RD ? 1 : SWH_LM_APF, AR = APF + 1;
+            constexpr int APF = 1, AR = APF + 1;
             uint4 a[AR][4];
 #pragma unroll
             for (int p = 0; p < APF; ++p)

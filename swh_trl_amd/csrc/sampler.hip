@@ -169,7 +169,7 @@ __global__ __launch_bounds__(kSplitThreads) void sample_split4_kernel(
     int64_t words, int64_t chunk, Partial *__restrict__ part, float *__restrict__ scores_out) {
     using T = typename Elem<DT>::T;
     constexpr int PV = kPerVec<DT>;
-    __shared__ float red[5 * (kSplitThreads / kWave)];
+    __shared__ float red4[4 * 5 * (kSplitThreads / kWave)];
     const int64_t b0 = 4 * (int64_t)blockIdx.y;
     const int nr = (int)(B - b0 < 4 ? B - b0 : 4);
     const int S = gridDim.x, s = blockIdx.x, tid = threadIdx.x;
@@ -256,11 +256,36 @@ __global__ __launch_bounds__(kSplitThreads) void sample_split4_kernel(
             one(j, x);
         }
     }
+    // the four rows' block reductions in one LDS exchange (block_partial's order per row)
+    const int lane = tid & 63, wid = tid >> 6;
+    constexpr int NW = kSplitThreads / kWave;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        if (q >= nr) continue;
-        block_partial(st[q], bk[q], bi[q], red);
-        if (tid == 0) part[(b0 + q) * S + s] = Partial{st[q].m, st[q].s1, bk[q], bi[q]};
+        st[q] = wave_soft(st[q]);
+        wave_best(bk[q], bi[q]);
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float *r = red4 + q * 5 * NW;
+            r[wid] = st[q].m;
+            r[NW + wid] = st[q].s1;
+            r[2 * NW + wid] = st[q].s2;
+            r[3 * NW + wid] = bk[q];
+            r[4 * NW + wid] = __int_as_float(bi[q]);
+        }
+    }
+    __syncthreads();
+    if (tid < 4 && tid < nr) {
+        const float *r = red4 + tid * 5 * NW;
+        SoftState rs = soft_init();
+        float k = kNegInf;
+        int32_t i = 0x7fffffff;
+        for (int w = 0; w < NW; ++w) {
+            rs = soft_merge(rs, SoftState{r[w], r[NW + w], r[2 * NW + w]});
+            best_merge(k, i, r[3 * NW + w], __float_as_int(r[4 * NW + w]));
+        }
+        part[(b0 + tid) * S + s] = Partial{rs.m, rs.s1, k, i};
     }
 }
 
@@ -571,10 +596,14 @@ __global__ void step_advance_kernel(int32_t *step) { *step += 1; }
 #ifndef SWH_SAMPLE4
 #define SWH_SAMPLE4 1  // A/B: 0 keeps one row per workgroup (tools/bench_sampler.py)
 #endif
-// splits of the four-row unfiltered kernel: up to 1024 workgroups, chunks of >= 2048 elements
+#ifndef SWH_SAMPLE4_WGS
+#define SWH_SAMPLE4_WGS 256  // A/B: target workgroups of the four-row kernel
+#endif
+// splits of the four-row unfiltered kernel: about SWH_SAMPLE4_WGS workgroups, chunks of
+// >= 4096 elements (a split of a few vectors per thread is all reduction overhead)
 int choose_split4(int64_t B, int64_t V) {
     int S = 1;
-    while (S < kMaxSplit && (B + 3) / 4 * S < 1024 && V / (S * 2) >= 1024) S *= 2;
+    while (S < kMaxSplit && (B + 3) / 4 * S * 2 <= SWH_SAMPLE4_WGS && V / (S * 2) >= 4096) S *= 2;
     return S;
 }
 
