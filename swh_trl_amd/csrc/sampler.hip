@@ -156,139 +156,6 @@ __global__ __launch_bounds__(kSplitThreads) void sample_split_kernel(
     if (threadIdx.x == 0) part[b * S + s] = Partial{st.m, st.s1, bk, bi};
 }
 
-// Unfiltered, four rows per workgroup: rows 4 y .. 4 y + 3 draw their Gumbel noise from
-// the four words of ONE Philox4x32-10 block per column (the stream's definition,
-// gumbel_at), so a column costs one Philox call instead of four.  Each row's elements
-// are visited in row_foreach's order (same thread, same sequence) and each row's
-// partial is reduced as in sample_split_kernel: a row's partial over a given chunk is
-// the same.  Rows must share their 16-B alignment (ld * sizeof(T) % 16 == 0).
-template <int DT>
-__global__ __launch_bounds__(kSplitThreads) void sample_split4_kernel(
-    const typename Elem<DT>::T *__restrict__ logits, int64_t B, int64_t V, int64_t ld, swh_sample_params p,
-    const uint64_t *__restrict__ rng, const int32_t *__restrict__ step_p, const uint32_t *__restrict__ seen,
-    int64_t words, int64_t chunk, Partial *__restrict__ part, float *__restrict__ scores_out) {
-    using T = typename Elem<DT>::T;
-    constexpr int PV = kPerVec<DT>;
-    __shared__ float red4[4 * 5 * (kSplitThreads / kWave)];
-    const int64_t b0 = 4 * (int64_t)blockIdx.y;
-    const int nr = (int)(B - b0 < 4 ? B - b0 : 4);
-    const int S = gridDim.x, s = blockIdx.x, tid = threadIdx.x;
-    const int32_t step = *step_p;
-    Proc pr[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) pr[q] = make_proc(p, step, seen ? seen + (b0 + min(q, nr - 1)) * words : nullptr);
-    const uint64_t seed = rng[0], ctr = rng[1] + (uint64_t)step;
-    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-    const int64_t beg = (int64_t)s * chunk;
-    const int64_t end = beg + chunk < V ? beg + chunk : V;
-    SoftState st[4];
-    float bk[4];
-    int32_t bi[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        st[q] = soft_init();
-        bk[q] = kNegInf;
-        bi[q] = 0x7fffffff;
-    }
-    const T *row[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) row[q] = logits + (b0 + min(q, nr - 1)) * ld;
-    auto one = [&](int64_t j, const float (&x)[4]) {
-        U4 w{0u, 0u, 0u, 0u};
-        if (!p.greedy) w = philox4x32_10(U4{(uint32_t)j, (uint32_t)(b0 >> 2), (uint32_t)ctr, (uint32_t)(ctr >> 32)}, k0, k1);
-        const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            if (q >= nr) continue;  // workgroup-uniform
-            const float z = pr[q](j, x[q]);
-            if (scores_out) scores_out[(b0 + q) * V + j] = z;
-            if (z == kNegInf) continue;
-            soft_fold<1>(st[q], &z);
-            const float key = p.greedy ? z : z - fast_log(-fast_log(u01_from_bits(wd[q])));
-            best_merge(bk[q], bi[q], key, (int32_t)j);
-        }
-    };
-    if (end > beg) {  // row_foreach's traversal, four rows in lockstep
-        const uintptr_t a = reinterpret_cast<uintptr_t>(row[0] + beg);
-        int64_t head = (int64_t)(((16 - (a & 15)) & 15) / sizeof(T));
-        if ((a & (sizeof(T) - 1)) != 0) head = end - beg;
-        if (head > end - beg) head = end - beg;
-        for (int64_t j = beg + tid; j < beg + head; j += kSplitThreads) {
-            float x[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) x[q] = Elem<DT>::load(row[q] + j);
-            one(j, x);
-        }
-        const int64_t v0 = beg + head;
-        const int64_t nvec = (end - v0) / PV;
-        constexpr int U = 2;  // vectors per trip per row (row_foreach's grid-stride order, 8 loads in flight)
-        int64_t v = tid;
-        auto vec = [&](const uint4 (&raw)[4], int64_t vi) {
-            float xs[4][PV];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) unpack16<DT>(raw[q], xs[q]);
-            const int64_t j0 = v0 + vi * PV;
-#pragma unroll
-            for (int k = 0; k < PV; ++k) {
-                const float x[4] = {xs[0][k], xs[1][k], xs[2][k], xs[3][k]};
-                one(j0 + k, x);
-            }
-        };
-        for (; v + (U - 1) * (int64_t)kSplitThreads < nvec; v += U * (int64_t)kSplitThreads) {
-            uint4 raw[U][4];
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) raw[u][q] = reinterpret_cast<const uint4 *>(row[q] + v0)[v + u * kSplitThreads];
-#pragma unroll
-            for (int u = 0; u < U; ++u) vec(raw[u], v + u * kSplitThreads);
-        }
-        for (; v < nvec; v += kSplitThreads) {
-            uint4 raw[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) raw[q] = reinterpret_cast<const uint4 *>(row[q] + v0)[v];
-            vec(raw, v);
-        }
-        for (int64_t j = v0 + nvec * PV + tid; j < end; j += kSplitThreads) {
-            float x[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) x[q] = Elem<DT>::load(row[q] + j);
-            one(j, x);
-        }
-    }
-    // the four rows' block reductions in one LDS exchange (block_partial's order per row)
-    const int lane = tid & 63, wid = tid >> 6;
-    constexpr int NW = kSplitThreads / kWave;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        st[q] = wave_soft(st[q]);
-        wave_best(bk[q], bi[q]);
-    }
-    if (lane == 0) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            float *r = red4 + q * 5 * NW;
-            r[wid] = st[q].m;
-            r[NW + wid] = st[q].s1;
-            r[2 * NW + wid] = st[q].s2;
-            r[3 * NW + wid] = bk[q];
-            r[4 * NW + wid] = __int_as_float(bi[q]);
-        }
-    }
-    __syncthreads();
-    if (tid < 4 && tid < nr) {
-        const float *r = red4 + tid * 5 * NW;
-        SoftState rs = soft_init();
-        float k = kNegInf;
-        int32_t i = 0x7fffffff;
-        for (int w = 0; w < NW; ++w) {
-            rs = soft_merge(rs, SoftState{r[w], r[NW + w], r[2 * NW + w]});
-            best_merge(k, i, r[3 * NW + w], __float_as_int(r[4 * NW + w]));
-        }
-        part[(b0 + tid) * S + s] = Partial{rs.m, rs.s1, k, i};
-    }
-}
-
 // ---------------------------------------------------------------------------
 // Filtered: one workgroup per row, radix-select thresholds.
 // ---------------------------------------------------------------------------
@@ -593,20 +460,6 @@ __global__ void seen_init_kernel(const int64_t *ids, const int32_t *mask, int64_
 
 __global__ void step_advance_kernel(int32_t *step) { *step += 1; }
 
-#ifndef SWH_SAMPLE4
-#define SWH_SAMPLE4 1  // A/B: 0 keeps one row per workgroup (tools/bench_sampler.py)
-#endif
-#ifndef SWH_SAMPLE4_WGS
-#define SWH_SAMPLE4_WGS 256  // A/B: target workgroups of the four-row kernel
-#endif
-// splits of the four-row unfiltered kernel: about SWH_SAMPLE4_WGS workgroups, chunks of
-// >= 4096 elements (a split of a few vectors per thread is all reduction overhead)
-int choose_split4(int64_t B, int64_t V) {
-    int S = 1;
-    while (S < kMaxSplit && (B + 3) / 4 * S * 2 <= SWH_SAMPLE4_WGS && V / (S * 2) >= 4096) S *= 2;
-    return S;
-}
-
 int choose_split(int64_t B, int64_t V) {
     int S = 1;
     while (S < kMaxSplit && B * S < 512 && V / (S * 2) >= 2048) S *= 2;
@@ -685,12 +538,6 @@ extern "C" int swh_sample_step(const void *logits, int dtype, int64_t B, int64_t
         const TY *lg = static_cast<const TY *>(logits);                                                         \
         if (filtered) {                                                                                         \
             S = launch_filtered<DTC>(lg, B, V, ld, p, rng, step, seen, words, workspace, scores_out, s);         \
-        } else if (SWH_SAMPLE4 && (ld * (int64_t)sizeof(TY)) % 16 == 0 && B >= 4) {                           \
-            S = choose_split4(B, V);                                                                            \
-            int64_t chunk = (V + S - 1) / S;                                                                    \
-            chunk = (chunk + 7) / 8 * 8;                                                                        \
-            sample_split4_kernel<DTC><<<dim3((unsigned)S, (unsigned)((B + 3) / 4)), dim3(kSplitThreads), 0, s>>>( \
-                lg, B, V, ld, p, rng, step, seen, words, chunk, part, scores_out);                              \
         } else {                                                                                                \
             S = choose_split(B, V);                                                                             \
             int64_t chunk = (V + S - 1) / S;                                                                    \

@@ -12,7 +12,8 @@
 #   train    tools/train_kernels.py (training half-step)             -> <tag>_train.log
 #   trace    rocprofv3 kernel trace of one training half-step + tools/critical_path.py -> <tag>_critical_path.txt
 #   ppo      tools/bench_ppo.py (BASELINE config 3)                  -> <tag>_ppo_bench.json
-#   llama    tools/bench_llama8b.py (config 5's per-GPU shape)       -> <tag>_llama8b.json
+#   llama    tools/bench_llama8b.py (Llama-3-8B shapes, 1 prompt)      -> <tag>_llama8b.json
+#   llama5   tools/bench_llama8b.py at config 5's per-GPU shape        -> <tag>_llama8b_c1024.json
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
@@ -78,6 +79,10 @@ for step in "$@"; do
       timeout -k 10 900 python -u tools/bench_llama8b.py > $O/${tag}_llama8b.json 2> $O/${tag}_llama8b.err \
         || fail llama $? $O/${tag}_llama8b.err
       tail -c 400 $O/${tag}_llama8b.json ;;
+    llama5)  # config 5's per-GPU shape: 8 prompts x G 8, P 256, C 1024, beta 0.04, 16384-token passes
+      timeout -k 10 900 python -u tools/bench_llama8b.py --prompts 8 --P 256 --C 1024 --fuse-budget 16384 \
+        > $O/${tag}_llama8b_c1024.json 2> $O/${tag}_llama8b_c1024.err || fail llama5 $? $O/${tag}_llama8b_c1024.err
+      tail -c 600 $O/${tag}_llama8b_c1024.json ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
