@@ -31,7 +31,10 @@ def main():
                            num_attention_heads=1, num_key_value_heads=1, head_dim=64, rope_theta=cfg.rope_theta,
                            max_position_embeddings=cfg.max_position_embeddings)
     B, P = 64, 128
-    n = B * (args.steps + args.warmup)
+    # 16 batches per data epoch: the timed updates are ordinary ones.  At a data epoch's
+    # last batch the reference's accelerate accumulation steps after every micro-batch
+    # (PPOTrainer._accumulate_sync), a 4x costlier update at this configuration.
+    n = B * max(16, args.steps + args.warmup + 1)
     g = torch.Generator().manual_seed(1234)
     ids = torch.randint(2, cfg.vocab_size - 1000, (n, P), generator=g)
     ds = [{"input_ids": ids[i].tolist()} for i in range(n)]
