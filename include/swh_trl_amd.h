@@ -42,9 +42,11 @@ extern "C" {
 const char *swh_version(void);
 const char *swh_status_string(int status);
 
-/* Launch policy: geometry choices of the decode GEMMs and samplers that do not
- * change any result (every alternative is bit-identical; tests pin that) and
- * exist for A/B timing and geometry-coverage tests.  Process-wide, applied by
+/* Launch policy: geometry choices of the decode GEMMs and samplers, for A/B
+ * timing and geometry-coverage tests.  Every alternative is bit-identical
+ * (tests pin that) except wide_smax and wide_cb, which choose how
+ * wide_gemm splits K and so the fp32 summation order of its dot products
+ * (each deterministic for a given policy).  Process-wide, applied by
  * launches issued after the call (a captured graph keeps the geometry it was
  * captured with).  *_workspace_bytes size for the policy in force when they are
  * called; a launch whose geometry needs more workspace than it is given returns
@@ -321,9 +323,12 @@ int swh_gemm_nt(const void *A, const void *B, const void *bias, void *C, int64_t
  * part[s][N][K] (fp32) = the sum over split s's tokens (S ranges of whole
  * 64-token steps, fp32 accumulation in token order), swh_gemm_tn_fold adds the S
  * partials in split order to grad (bf16 / f32, n = N K elements) and rounds
- * once.  M % 64 == 0, N % 128 == 0, K % 128 == 0, leading dimensions multiples
- * of 8 elements, 16-B aligned pointers; else SWH_E_ARG. */
-int swh_gemm_tn_partials(const void *dY, const void *X, float *part, int64_t M, int64_t N, int64_t K,
+ * once.  colsum (nullable, [S][N] fp32): also the split's token sums of dY, the
+ * bias gradient of the same nn.Linear (replaces a swh_colsum_partials pass over
+ * dY), to be folded by swh_rmsnorm_dw_accum.  M % 64 == 0, N % 128 == 0,
+ * K % 128 == 0, leading dimensions multiples of 8 elements, 16-B aligned
+ * pointers; else SWH_E_ARG. */
+int swh_gemm_tn_partials(const void *dY, const void *X, float *part, float *colsum, int64_t M, int64_t N, int64_t K,
                          int64_t lddy, int64_t ldx, int32_t S, void *stream);
 int swh_gemm_tn_fold(const float *part, int32_t S, int64_t n, void *grad, int32_t dtype, void *stream);
 /* dst_f32[i] += src[i] (bf16/f32) — accumulate micro-batch grads in fp32. */

@@ -185,6 +185,8 @@ __global__ __launch_bounds__(kGThreads) void gemm_nt_kernel(const uint16_t *__re
 // fp32 partials in split order into the gradient and rounds once.  Both operands
 // are token-major, so both MFMA operands come from the LDS image through
 // ds_read_b64_tr_b16 (4 tokens x 1 column per lane, two reads per 8-token half).
+// With colsum, the first column tile of each split also writes colsum[s][N] = the
+// split's token sums of dY (the projection's bias gradient, from the staged image).
 // The image is [64 tokens][128 columns] with 256-B rows, 16-B chunk c of row r at
 // position c ^ (((r & 3) << 2) | ((r >> 2) & 3)) (conflict-free transposed reads).
 // ---------------------------------------------------------------------------
@@ -206,8 +208,8 @@ __device__ __forceinline__ uint4 tr_operand(uint32_t img, int tb, int cb, int la
 template <int NS, int BK>
 __global__ __launch_bounds__(kGThreads) void gemm_tn_kernel(const uint16_t *__restrict__ DY,
                                                             const uint16_t *__restrict__ X, float *__restrict__ part,
-                                                            int M, int N, int K, int64_t lddy, int64_t ldx, int S,
-                                                            int sps) {
+                                                            float *__restrict__ colsum, int M, int N, int K,
+                                                            int64_t lddy, int64_t ldx, int S, int sps) {
     extern __shared__ __attribute__((aligned(16))) unsigned char gl[];  // [NS buffers][dY | X]
     constexpr int SB = BK * kGT * 2, JL = BK / 16;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -246,6 +248,14 @@ __global__ __launch_bounds__(kGThreads) void gemm_tn_kernel(const uint16_t *__re
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
     const uint32_t g0 = lds_off(gl);
+    // colsum (the bias gradient's token sums): the first column tile of each split also sums
+    // its dY image over the tokens — thread (row group rg, chunk ch) rows rg + 16 u of every
+    // k-step, 8 columns, in token order; the 16 row groups meet in fixed order below
+    const bool cs_on = colsum != nullptr && k0 == 0;  // workgroup-uniform
+    const int cs_ch = tid & 15, cs_rg = tid >> 4;
+    float cs[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs[e] = 0.f;
     gemm_kloop<NS, 2 * JL>(nk, stage, [&](int cur) {
         const uint32_t di = g0 + cur * 2 * SB, xi = di + SB;
         uint4 a[2][2], b[2][2];  // [k-step parity][block], as in gemm_nt_kernel
@@ -268,7 +278,32 @@ __global__ __launch_bounds__(kGThreads) void gemm_tn_kernel(const uint16_t *__re
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(a[kk & 1][i]), as_bf(b[kk & 1][j]),
                                                                         acc[i][j], 0, 0, 0);
         }
+        if (cs_on) {
+            uint4 v[BK / 16];
+#pragma unroll
+            for (int u = 0; u < BK / 16; ++u) v[u] = lds_rd128(di + tsw(cs_rg + 16 * u, cs_ch));
+            lgkm_wait0();
+#pragma unroll
+            for (int u = 0; u < BK / 16; ++u) {
+                float f[8];
+                unpack16<SWH_BF16>(v[u], f);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) cs[e] += f[e];
+            }
+        }
     });
+    if (cs_on) {  // the stages are free (the K loop ends on a barrier): 16 row groups x 128 columns
+        float *red = reinterpret_cast<float *>(gl);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[cs_rg * kGT + 8 * cs_ch + e] = cs[e];
+        __syncthreads();
+        if (tid < kGT) {
+            float v = red[tid];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) v += red[r * kGT + tid];
+            colsum[(int64_t)s * N + n0 + tid] = v;
+        }
+    }
     // fp32 partial: register e of block (i, j) is row n0 + 64 wm + 32 i + (e & 3) + 8 (e >> 2) + 4 h,
     // column k0 + 64 wn + 32 j + l % 32 (128 contiguous bytes per half-wave)
     float *ps = part + (int64_t)s * N * K;
@@ -352,28 +387,30 @@ extern "C" int swh_gemm_nt(const void *A, const void *B, const void *bias, void 
 }
 
 template <int NS, int BK>
-static int launch_tn(const void *dY, const void *X, float *part, int64_t M, int64_t N, int64_t K, int64_t lddy,
-                     int64_t ldx, int S, int64_t grid, hipStream_t s) {
+static int launch_tn(const void *dY, const void *X, float *part, float *colsum, int64_t M, int64_t N, int64_t K,
+                     int64_t lddy, int64_t ldx, int S, int64_t grid, hipStream_t s) {
     constexpr int lds = NS * 2 * kGT * BK * 2;
     if (!lds_opt_in<&gemm_tn_kernel<NS, BK>>()) return SWH_E_LAUNCH;
     const int steps = (int)(M / BK), sps = (steps + S - 1) / S;
     gemm_tn_kernel<NS, BK><<<(unsigned)grid, kGThreads, lds, s>>>(static_cast<const uint16_t *>(dY),
-                                                                   static_cast<const uint16_t *>(X), part, (int)M,
-                                                                   (int)N, (int)K, lddy, ldx, S, sps > 1 ? sps : 1);
+                                                                   static_cast<const uint16_t *>(X), part, colsum,
+                                                                   (int)M, (int)N, (int)K, lddy, ldx, S,
+                                                                   sps > 1 ? sps : 1);
     return launch_status();
 }
 
-extern "C" int swh_gemm_tn_partials(const void *dY, const void *X, float *part, int64_t M, int64_t N, int64_t K,
-                                    int64_t lddy, int64_t ldx, int32_t S, void *stream) {
+extern "C" int swh_gemm_tn_partials(const void *dY, const void *X, float *part, float *colsum, int64_t M, int64_t N,
+                                    int64_t K, int64_t lddy, int64_t ldx, int32_t S, void *stream) {
     if (!dY || !X || !part || M < 0 || S < 1 || N <= 0 || K <= 0) return SWH_E_ARG;
     if (M % kGK || N % kGT || K % kGT || lddy < N || ldx < K || lddy % 8 || ldx % 8) return SWH_E_ARG;
     if ((reinterpret_cast<uintptr_t>(dY) | reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(part)) & 15)
         return SWH_E_ARG;
+    if (colsum && (reinterpret_cast<uintptr_t>(colsum) & 3)) return SWH_E_ARG;
     if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX || S > 1024) return SWH_E_ARG;
     const int64_t grid = (N / kGT) * (K / kGT) * (int64_t)S;
     if (grid > INT32_MAX) return SWH_E_ARG;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    return launch_tn<2, 64>(dY, X, part, M, N, K, lddy, ldx, S, grid, s);
+    return launch_tn<2, 64>(dY, X, part, colsum, M, N, K, lddy, ldx, S, grid, s);
 }
 
 extern "C" int swh_gemm_tn_fold(const float *part, int32_t S, int64_t n, void *grad, int32_t dtype, void *stream) {

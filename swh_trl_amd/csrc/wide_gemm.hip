@@ -59,7 +59,26 @@ constexpr int kWNB = WGeo<1>::NB;      // the narrowest tile: eligibility and th
 
 enum : int { WEPI_PLAIN = 0, WEPI_RESIDUAL = 1, WEPI_SILU = 2 };
 
+// Phase timestamps for tools/wide_probe.py (a build with SWH_WIDE_TRACE_ON defined,
+// tools/build_variant.py): wall clock (100 MHz) of thread 0 at each phase boundary.
+#ifdef SWH_WIDE_TRACE_ON
+__device__ unsigned long long *g_wide_trace;
+#define SWH_WIDE_TRACE(i)                                                                                      \
+    if (threadIdx.x == 0 && g_wide_trace)                                                                      \
+    g_wide_trace[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] = wall_clock64()
+#else
+#define SWH_WIDE_TRACE(i)
+#endif
+
 __device__ __forceinline__ bf16x8w as_bf8(const uint4 &v) { return __builtin_bit_cast(bf16x8w, v); }
+
+// Weight fragments are read once per launch: non-temporal loads keep the weight stream from
+// evicting X (re-read by every workgroup of an XCD) and the slabs from L2 (Llama-3-8B decode,
+// tools/wide_probe.py: gate/up 52 -> 48.4 us, down 29.1 -> 27.4, lm head 199 -> 184).
+__device__ __forceinline__ uint4 wload_nt(const uint16_t *p) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    return uint4{v.x, v.y, v.z, v.w};
+}
 
 // barrier that waits for LDS traffic only: LDS-DMA still in flight stays in flight
 __device__ __forceinline__ void wide_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -97,16 +116,28 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
     const int nr_all = K / kWKC;
     const int r0 = (int)((int64_t)nr_all * sidx / S), r1 = (int)((int64_t)nr_all * (sidx + 1) / S), nr = r1 - r0;
     const int kbase = r0 * kWKC;
+    SWH_WIDE_TRACE(0);
 
     // ---- the folded norm's row statistic (L2)
     if constexpr (NM == 2) {
-        const int r = min(tid >> 2, M - 1), sub = tid & 3, nc = K / 16;
-        const float *row = ss_in + (int64_t)r * nc;
-        float v = 0.f;
-        for (int c = sub; c < nc; c += 4) v += row[c];
+        // 8 lanes per row, 16-B loads 8 deep: one memory latency (a scalar walk of the
+        // row's K / 16 partial sums took 5-6 us at K 4096)
+        const int r = tid >> 3, sub = tid & 7, nc4 = K / 64;
+        const float4 *row = reinterpret_cast<const float4 *>(ss_in + (int64_t)min(r, M - 1) * (K / 16));
+        float4 a = float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+        for (int f = sub; f < nc4; f += 8) {
+            const float4 t = row[f];
+            a.x += t.x;
+            a.y += t.y;
+            a.z += t.z;
+            a.w += t.w;
+        }
+        float v = (a.x + a.y) + (a.z + a.w);
         v += __shfl_xor(v, 1);
         v += __shfl_xor(v, 2);
-        if (sub == 0) rstd_s[tid >> 2] = rsqrtf(v / (float)K + eps);
+        v += __shfl_xor(v, 4);
+        if (sub == 0) rstd_s[r] = rsqrtf(v / (float)K + eps);
     }
 
     // ---- operands: a register ring WD rounds deep per thread (X pieces + this wave's weight
@@ -147,7 +178,7 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
         _Pragma("unroll") for (int u = 0; u < kWXU; ++u) xr[D][u] =                                            \
             *reinterpret_cast<const u32x4 *>(xp[u] + (q) * kWKC);                                               \
         _Pragma("unroll") for (int s = 0; s < kWKS; ++s) _Pragma("unroll") for (int j = 0; j < CB; ++j)       \
-            wr[D][s][j] = *reinterpret_cast<const uint4 *>(wp[j] + (q) * kRS + kSS * s);                         \
+            wr[D][s][j] = wload_nt(wp[j] + (q) * kRS + kSS * s);                                                 \
         __builtin_amdgcn_sched_barrier(0); /* rounds issue in order: the counted waits rely on it */            \
     } while (0)
     f32x4w acc[4][CB];
@@ -216,35 +247,29 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
         }
     }
 #undef SWH_WIDE_ROUND
-    wide_lds_barrier();  // every wave is past its last X read: the slots become the epilogue tile
+    SWH_WIDE_TRACE(1);
 #undef SWH_WIDE_ISSUE
 
-    // ---- this workgroup's 64 x 128 fp32 tile (C layout: lane holds rows 16 i + 4 kg + e, column rl)
-    float *tile = reinterpret_cast<float *>(lds);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < CB; ++j)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) tile[(16 * i + 4 * kg + e) * LDT + wid * 16 * CB + 16 * j + rl] = acc[i][j][e];
-    __syncthreads();
-
     // ---- split K (the in-launch slab hand-off of cdna_hip_programming.md, projection GEMMs item 2,
-    // write-through form): sc1 16-B slab stores drained by every wave, one relaxed agent-scope
-    // ticket; the last arriver acquires once and sums the S slabs with plain 16-B loads in fixed
-    // order (deterministic for any placement of the S workgroups over the XCDs)
-    if (S > 1) {
+    // write-through form).  Slabs hold the accumulators in fragment order (per wave, row block
+    // and column group: 64 lanes x 16 B), so every workgroup stores straight from registers —
+    // no LDS tile, no barrier before the stores — drained by every wave, then one relaxed
+    // agent-scope ticket.  The last arriver acquires once, issues its epilogue operands and
+    // the other S - 1 slabs' pieces at once, and sums the S partials (its own from registers)
+    // in fixed slab order: deterministic for any placement of the S workgroups over the XCDs.
+    uint4 pre[CB][2];  // the residual epilogue's 16 columns per (row, chunk), prefetched
+    if (CB == 1 && S > 1) {  // 256-row tiles never split K (wide_split): no slab code, no spills
         float *my = slabs + ((int64_t)cb * S + sidx) * (64 * NB);
         const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(my, 0, 64 * NB * 4, 0x00020000);
-        for (int idx = tid; idx < 64 * NB / 4; idx += kWT) {
-            const int r = idx / (NB / 4), c4 = idx % (NB / 4);
-            const float4 v = *reinterpret_cast<const float4 *>(tile + r * LDT + 4 * c4);
-            __builtin_amdgcn_raw_buffer_store_b128(
-                u32x4{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)}, rsrc,
-                idx * 16, 0, 16 /* sc1: write-through */);
-        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 1; ++j)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rsrc,
+                                                       ((wid * 4 + i) * 64 + lane) * 16, 0, 16 /* sc1: write-through */);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        SWH_WIDE_TRACE(2);
         if (tid == 0) {
             const int t = __hip_atomic_fetch_add(counters + cb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             *flag_s = (t == S - 1);
@@ -254,39 +279,58 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
             }
         }
         __syncthreads();
+        SWH_WIDE_TRACE(3);
         if (!*flag_s) return;
-        const float4 *base = reinterpret_cast<const float4 *>(slabs + (int64_t)cb * S * (64 * NB));
-        // every slab load of a pass in flight at once (up to 4 x S <= 32 per thread: the ring
-        // registers are free by now), so the reduction costs about one memory latency per pass
-        constexpr int IT = 64 * NB / 4 / kWT;  // 16-B slab pieces per thread (4 or 8)
-        constexpr int IP = IT < 4 ? IT : 4;    // pieces per pass
+        if constexpr (EPI == WEPI_RESIDUAL) {
 #pragma unroll
-        for (int p0 = 0; p0 < IT; p0 += IP) {
-            float4 v[IP][8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-                if (q < S) {
-#pragma unroll
-                    for (int i = 0; i < IP; ++i) v[i][q] = base[(int64_t)q * (64 * NB / 4) + tid + kWT * (p0 + i)];
-                }
-#pragma unroll
-            for (int i = 0; i < IP; ++i) {
-                float4 sum = float4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int q = 0; q < 8; ++q)
-                    if (q < S) {
-                        sum.x += v[i][q].x;
-                        sum.y += v[i][q].y;
-                        sum.z += v[i][q].z;
-                        sum.w += v[i][q].w;
-                    }
-                const int idx = tid + kWT * (p0 + i), r = idx / (NB / 4), c4 = idx % (NB / 4);
-                *reinterpret_cast<float4 *>(tile + r * LDT + 4 * c4) = sum;
+            for (int u = 0; u < CB; ++u) {
+                const int idx = tid + kWT * u, r = min(idx / (NB / 16), M - 1), j = idx % (NB / 16);
+                const uint4 *sp = reinterpret_cast<const uint4 *>(res + (int64_t)r * ldy + cb * NB + 16 * j);
+                pre[u][0] = sp[0];
+                pre[u][1] = sp[1];
             }
         }
+        const f32x4w *base = reinterpret_cast<const f32x4w *>(slabs + (int64_t)cb * S * (64 * NB));
+        // every other slab's pieces in flight at once (4 x (S - 1) <= 28 per thread: the ring
+        // registers are free by now): about one memory latency
+        f32x4w v[4][8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (q < S && q != sidx) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[i][q] = base[(int64_t)q * (64 * NB / 4) + (wid * 4 + i) * 64 + lane];
+            }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            f32x4w sum = f32x4w{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (q < S) sum += q == sidx ? acc[i][0] : v[i][q];
+            acc[i][0] = sum;
+        }
         if (tid == 0) __hip_atomic_store(counters + cb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
+        SWH_WIDE_TRACE(4);
+    } else if constexpr (EPI == WEPI_RESIDUAL) {
+#pragma unroll
+        for (int u = 0; u < CB; ++u) {
+            const int idx = tid + kWT * u, r = min(idx / (NB / 16), M - 1), j = idx % (NB / 16);
+            const uint4 *sp = reinterpret_cast<const uint4 *>(res + (int64_t)r * ldy + cb * NB + 16 * j);
+            pre[u][0] = sp[0];
+            pre[u][1] = sp[1];
+        }
     }
+
+    // ---- this workgroup's 64 x 128 CB fp32 tile (C layout: lane holds rows 16 i + 4 kg + e,
+    // column rl); the X slots it overlays are dead once every wave is past its last round
+    wide_lds_barrier();
+    float *tile = reinterpret_cast<float *>(lds);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < CB; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) tile[(16 * i + 4 * kg + e) * LDT + wid * 16 * CB + 16 * j + rl] = acc[i][j][e];
+    __syncthreads();
 
     // ---- epilogue
     if constexpr (EPI == WEPI_SILU) {
@@ -306,14 +350,14 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
         }
     } else if constexpr (EPI == WEPI_RESIDUAL) {
         // 64 rows x 8 chunks of 16 columns: s = bf16(s + bf16(acc)), chunk sum of squares of the new s
-        for (int idx = tid; idx < 64 * (NB / 16); idx += kWT) {
-            const int r = idx / (NB / 16), j = idx % (NB / 16);
+#pragma unroll
+        for (int u = 0; u < CB; ++u) {
+            const int idx = tid + kWT * u, r = idx / (NB / 16), j = idx % (NB / 16);
             if (r >= M) continue;
             uint4 *sp = reinterpret_cast<uint4 *>(res + (int64_t)r * ldy + cb * NB + 16 * j);
-            const uint4 s0 = sp[0], s1 = sp[1];
             float a[16], nv[16];
-            unpack16<SWH_BF16>(s0, a);
-            unpack16<SWH_BF16>(s1, a + 8);
+            unpack16<SWH_BF16>(pre[u][0], a);
+            unpack16<SWH_BF16>(pre[u][1], a + 8);
             float ss = 0.f;
 #pragma unroll
             for (int c = 0; c < 16; ++c) {
@@ -343,6 +387,7 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
             *reinterpret_cast<uint4 *>(y + (int64_t)r * ldy + col) = pack8w(v);
         }
     }
+    SWH_WIDE_TRACE(5);
 }
 
 // K split: about one workgroup per CU, at most smax (the launch policy's wide_smax, 1..8:
@@ -358,8 +403,8 @@ int wide_split(int64_t ncb, int64_t K, int smax) {
 
 // 16-row weight groups per wave: 2 when the 256-row tiles alone fill the CUs (no K split:
 // the Llama-3-8B lm head, 4.57 -> 4.96 TB/s), where halving the X bytes per weight byte
-// pays; with a split (gate/up: 112 tiles x 2) the hand-off costs more (58 -> 68 us).
-// The launch policy's wide_cb = 1 / 2 forces one (A/B).
+// pays; with a split (gate/up: 112 tiles x 2) the hand-off cost more (58 -> 68 us), so
+// 256-row tiles never split K.  The launch policy's wide_cb = 1 / 2 forces one (A/B).
 int wide_cb(int64_t wcols, int64_t K, const swh_launch_policy &pol) {
     const bool two_ok = wcols % WGeo<2>::NB == 0;
     if (pol.wide_cb == 1 || !two_ok) return 1;
@@ -389,15 +434,10 @@ bool wide_gemm_eligible(int64_t M, int64_t N, int64_t K, int32_t silu) {
 // Bytes of fp32 slabs the split-K reduction needs (0 when the shape is not eligible or S == 1).
 int64_t wide_gemm_slab_bytes(int64_t M, int64_t N, int64_t K, int32_t silu) {
     if (!wide_gemm_eligible(M, N, K, silu)) return 0;
-    int64_t most = 0;
-    for (int cb = 1; cb <= 2; ++cb) {  // either tiling and the largest split (the policy may change between calls)
-        const int64_t wcols = silu ? 2 * N : N, nb = (int64_t)kWNB * cb;
-        if (wcols % nb) continue;
-        const int s = wide_split(wcols / nb, K, 8);
-        const int64_t b = s > 1 ? wcols / nb * s * 64 * nb * (int64_t)sizeof(float) : 0;
-        most = b > most ? b : most;
-    }
-    return most;
+    // 128-row tiles (the only ones that split) at the largest split the policy allows
+    const int64_t wcols = silu ? 2 * N : N;
+    const int s = wide_split(wcols / kWNB, K, 8);
+    return s > 1 ? wcols / kWNB * s * 64 * kWNB * (int64_t)sizeof(float) : 0;
 }
 
 template <bool P, int CB>
@@ -420,9 +460,15 @@ int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, flo
     if (!wide_gemm_eligible(M, N, K, silu)) return 1;
     const int64_t wcols = silu ? 2 * N : N;
     const swh_launch_policy pol = launch_policy();
+    const auto *X = static_cast<const uint16_t *>(x);
+    const auto *W = static_cast<const uint16_t *>(w);
+    const auto *B = static_cast<const uint16_t *>(bias);
+    auto *R = static_cast<uint16_t *>(residual);
+    auto *Y = static_cast<uint16_t *>(y);
+    const int m = (int)M, n = (int)N, k = (int)K, ld = (int)ldy;
     const int cb = wide_cb(wcols, K, pol);
     const int64_t nb = (int64_t)kWNB * cb, ncb = wcols / nb;
-    const int s = wide_split(ncb, K, pol.wide_smax);
+    const int s = cb == 1 ? wide_split(ncb, K, pol.wide_smax) : 1;
     if (ncb * (int64_t)sizeof(int) > counter_bytes) return 1;
     float *slabs = nullptr;
     if (s > 1) {
@@ -431,12 +477,6 @@ int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, flo
     }
     int *ctr = static_cast<int *>(workspace);
     const dim3 grid((unsigned)ncb, (unsigned)s);
-    const auto *X = static_cast<const uint16_t *>(x);
-    const auto *W = static_cast<const uint16_t *>(w);
-    const auto *B = static_cast<const uint16_t *>(bias);
-    auto *R = static_cast<uint16_t *>(residual);
-    auto *Y = static_cast<uint16_t *>(y);
-    const int m = (int)M, n = (int)N, k = (int)K, ld = (int)ldy;
     if (cb == 2) {
         if (packed) return dispatch_wide<true, 2>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr, silu);
         return dispatch_wide<false, 2>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr, silu);
@@ -500,5 +540,11 @@ int wide_pack(const void *src, const void *norm_w, int64_t N, int64_t K, int32_t
                                                              static_cast<uint16_t *>(dst), npieces);
     return launch_status();
 }
+
+#ifdef SWH_WIDE_TRACE_ON
+extern "C" int swh_wide_probe_set_trace(unsigned long long *p) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_wide_trace), &p, sizeof(p)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 }  // namespace swh

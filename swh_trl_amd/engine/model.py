@@ -162,6 +162,8 @@ class _Linear(torch.autograd.Function):
 _TGEMM = os.environ.get("SWH_TGEMM", "wgrad")
 _TGEMM_MAX_N = 1536
 _TGEMM_SPLITS = int(os.environ.get("SWH_TGEMM_SPLITS", "8"))
+# the qkv bias gradient from gemm_tn's staged dY (1) or a separate swh_colsum_partials pass (0, A/B)
+_TN_COLSUM = os.environ.get("SWH_TN_COLSUM", "1") != "0"
 if _TGEMM not in ("off", "wgrad", "all"):
     raise ValueError(f"SWH_TGEMM={_TGEMM!r}: expected off | wgrad | all")
 
@@ -183,8 +185,11 @@ def _accumulate_dw(gw, gb, dy, x):
             # the kernel is not persistent).  The partials are allocated on this side stream,
             # so the caching allocator reuses their block only for later side-stream work:
             # released here, not kept to the end of the backward (~33 MB per layer at 0.5B)
-            nn_ops.gemm_tn_accumulate(gw.view(dy2.shape[1], x2.shape[1]), dy2, x2, _TGEMM_SPLITS)
-            if gb is not None:
+            # (the bias gradient's token sums come out of the same kernel's staged dY)
+            fused = gb is not None and gb.is_contiguous() and _TN_COLSUM
+            nn_ops.gemm_tn_accumulate(gw.view(dy2.shape[1], x2.shape[1]), dy2, x2, _TGEMM_SPLITS,
+                                      bias_grad=gb if fused else None)
+            if gb is not None and not fused:
                 bias_grad_accumulate(dy2, gb)
             return
         if S > 1:

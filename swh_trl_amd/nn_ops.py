@@ -210,11 +210,15 @@ def gemm_tn_eligible(dy: torch.Tensor, x: torch.Tensor) -> bool:
             and x.stride(0) % 8 == 0 and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0)
 
 
-def gemm_tn_accumulate(grad: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, splits: int) -> torch.Tensor:
+def gemm_tn_accumulate(grad: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, splits: int,
+                       bias_grad: Optional[torch.Tensor] = None) -> torch.Tensor:
     """grad [N, K] += dy^T x over the tokens (include/swh_trl_amd.h
     swh_gemm_tn_partials + swh_gemm_tn_fold): `splits` token ranges in fp32
-    partials, folded in order and rounded once into grad (bf16 / f32).  Returns
-    the partials buffer (keep it alive until the stream has run both launches)."""
+    partials, folded in order and rounded once into grad (bf16 / f32).  With
+    bias_grad [N]: also bias_grad += the token sums of dy (the same kernel's
+    per-split column sums, folded in split order by swh_rmsnorm_dw_accum).
+    Returns the partials buffer (keep it alive until the stream has run the
+    launches)."""
     _dev(dy, "gemm_tn_accumulate")
     if not gemm_tn_eligible(dy, x):
         raise ValueError(f"gemm_tn_accumulate: unsupported operands {tuple(dy.shape)} / {tuple(x.shape)}")
@@ -222,11 +226,18 @@ def gemm_tn_accumulate(grad: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, sp
     K = x.shape[1]
     if grad.numel() != N * K or not grad.is_contiguous():
         raise ValueError("gemm_tn_accumulate: grad must be a contiguous [N, K] view")
-    part = torch.empty(splits, N, K, device=dy.device, dtype=torch.float32)
-    call("swh_gemm_tn_partials", dy.data_ptr(), x.data_ptr(), part.data_ptr(), M, N, K, dy.stride(0), x.stride(0),
-         int(splits), _stream())
+    if bias_grad is not None and (bias_grad.numel() != N or not bias_grad.is_contiguous()):
+        raise ValueError("gemm_tn_accumulate: bias_grad must be a contiguous [N] view")
+    part = torch.empty(splits * N * K + (splits * N if bias_grad is not None else 0), device=dy.device,
+                       dtype=torch.float32)
+    colsum = part[splits * N * K:] if bias_grad is not None else None
+    call("swh_gemm_tn_partials", dy.data_ptr(), x.data_ptr(), part.data_ptr(), _p(colsum), M, N, K, dy.stride(0),
+         x.stride(0), int(splits), _stream())
     call("swh_gemm_tn_fold", part.data_ptr(), int(splits), N * K, grad.data_ptr(),
          _dtype_code(grad, "gemm_tn_accumulate"), _stream())
+    if bias_grad is not None:
+        call("swh_rmsnorm_dw_accum", colsum.data_ptr(), int(splits), N, bias_grad.data_ptr(),
+             _dtype_code(bias_grad, "gemm_tn_accumulate"), _stream())
     return part
 
 

@@ -1450,7 +1450,8 @@ def test_grouped_attention_equals_concatenated(ops, dev, P, C, G, pad):
 
 @pytest.mark.parametrize("name,M,N,K", [("qkv_bias", 64, 6144, 4096), ("o_res", 8, 4096, 4096),
                                         ("gate_up", 33, 14336, 4096), ("down", 64, 4096, 14336),
-                                        ("down_tiny_llama", 6, 1024, 2048), ("lm_head", 64, 128256, 4096)])
+                                        ("down_tiny_llama", 6, 1024, 2048), ("lm_head", 64, 128256, 4096),
+                                        ("norm_long_k", 21, 4096, 14336)])
 def test_wide_gemm_bandwidth_regime(ops, dev, name, M, N, K):
     """csrc/wide_gemm.hip (decode GEMMs with K >= 2048, the Llama-3-8B decode
     shapes of config 5) through swh_decode_gemm, in the forms the decode step
@@ -1662,7 +1663,9 @@ def test_gemm_tn_weight_gradient_matches_fp32(dev, M, N, K, S, dtype):
     g0 = (torch.randn(N, K, generator=g) * 0.1).to(dtype)
     ref = g0.double() + dy.double().t() @ x.double()
     gd = g0.to(dev)
-    part = nn_ops.gemm_tn_accumulate(gd, dy.to(dev), x.to(dev), S)
+    b0 = (torch.randn(N, generator=g) * 0.1).to(dtype)
+    bd = b0.to(dev)
+    part = nn_ops.gemm_tn_accumulate(gd, dy.to(dev), x.to(dev), S, bias_grad=bd)
     torch.cuda.synchronize()
     del part
     got = gd.cpu().double()
@@ -1670,6 +1673,14 @@ def test_gemm_tn_weight_gradient_matches_fp32(dev, M, N, K, S, dtype):
     scale = (dy.double().abs().t() @ x.double().abs())  # bound of the fp32 summation error
     bound = ref.abs() * ulp + scale * 2.0 ** -22 * (M / S + S) + 1e-12
     assert bool(((got - ref).abs() <= bound).all()), float(((got - ref).abs() - bound).max())
+    # the bias gradient from the same kernel (the split's token sums of dY, folded in split
+    # order as swh_rmsnorm_dw_accum folds: bf16(grad + bf16(sum)) for bf16, grad + sum for f32)
+    cs = dy.double().sum(0)
+    bref = b0.double() + cs
+    bgot = bd.cpu().double()
+    bscale = dy.double().abs().sum(0)
+    bbound = bref.abs() * 2 * ulp + (cs.abs() * ulp if dtype == torch.bfloat16 else 0) + bscale * 2.0 ** -22 * (M / S + S) + 1e-12
+    assert bool(((bgot - bref).abs() <= bbound).all()), float(((bgot - bref).abs() - bbound).max())
 
 
 def test_gemm_tn_partials_row_order_and_splits(dev):

@@ -7,7 +7,10 @@ barrier, main loop done (S = K Q^T, softmax, P V), wave merge barrier, exit
 `--step`; each timed call follows a 1 GiB write so the caches hold what the
 decode graph leaves them (the other 23 layers' weights have passed).
 
-    python tools/attn_probe.py [--step 128] [--reps 5]
+    python tools/attn_probe.py [--step 128] [--reps 5] [--llama]
+
+--llama: the Llama-3-8B shape of config 5 (8 KV heads x 4 query heads x 128, prompt
+256, 8 GRPO groups of 8 rows; two workgroups per CU in sequence).
 """
 import argparse
 import ctypes
@@ -29,13 +32,15 @@ def build():
     os.makedirs(os.path.dirname(SO), exist_ok=True)
     subprocess.check_call(["hipcc", "-O3", "--offload-arch=gfx950", "-fPIC", "-shared", "-std=c++17",
                            "-munsafe-fp-atomics", os.path.join(ROOT, "tools", "gemm_probe.hip"),
-                           os.path.join(ROOT, "swh_trl_amd", "csrc", "wide_gemm.hip"), "-o", SO])
+                           os.path.join(ROOT, "swh_trl_amd", "csrc", "wide_gemm.hip"),
+                           os.path.join(ROOT, "swh_trl_amd", "csrc", "lib.hip"), "-o", SO])
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--step", type=int, default=128)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--llama", action="store_true")
     args = ap.parse_args()
     build()
     lib = ctypes.CDLL(SO)
@@ -47,7 +52,12 @@ def main():
     from swh_trl_amd.engine.config import DecoderConfig
     from swh_trl_amd.engine.model import rope_tables
     dev = torch.device("cuda:0")
+    cfg = DecoderConfig()
     B, Hq, Hkv, D, P, C, G = 64, 14, 2, 64, 128, 256, 8
+    if args.llama:
+        from swh_trl_amd.engine import llama3_8b
+        cfg = llama3_8b()
+        Hq, Hkv, D, P, C = 32, 8, 128, 256, 1024
     T = P + C
     g = torch.Generator(device=dev).manual_seed(0)
     bf = torch.bfloat16
@@ -55,7 +65,7 @@ def main():
     vc = torch.randn(B, Hkv, T, D, generator=g, device=dev).to(bf)
     qkv = torch.randn(B, (Hq + 2 * Hkv) * D, generator=g, device=dev).to(bf)
     out = torch.empty(B, Hq * D, dtype=bf, device=dev)
-    cos, sin = rope_tables(DecoderConfig(), T + 1, dev)
+    cos, sin = rope_tables(cfg, T + 1, dev)
     plen = torch.full((B,), P, dtype=torch.int32, device=dev)
     prow = (torch.arange(B, device=dev, dtype=torch.int32) // G) * G
     state = torch.tensor([args.step + 1, P], dtype=torch.int32, device=dev)
@@ -91,6 +101,10 @@ def main():
         print(f"rep {rep} keys={P + args.step + 1} WGs={t.shape[0]} event={1000 * e0.elapsed_time(e1):6.2f}us "
               f"span={span:6.2f}us entry p50={float((entry - t0).float().median()) / 100:5.2f} "
               f"max={float(entry.max() - t0) / 100:5.2f}")
+        for i, ph in enumerate(PHASES, start=1):
+            col = (t[:, i] - t0).float() / 100.0
+            print(f"    at {ph:7s} p50 {float(col.median()):6.2f}  p90 {float(col.quantile(0.9)):6.2f}  "
+                  f"max {float(col.max()):6.2f}")
         prev = entry
         for i, ph in enumerate(PHASES, start=1):
             col = t[:, i]
