@@ -145,6 +145,15 @@ __device__ __forceinline__ uint4 ld_w(const uint16_t *p) {
     if constexpr (SWH_W_NT) return ld_nt(reinterpret_cast<const uint4 *>(p));
     return *reinterpret_cast<const uint4 *>(p);
 }
+// the same with the non-temporal policy chosen per kernel: the gate/up tiles (fragment-order
+// weights, whole 1 KB runs per load) gain from it (11.15 -> 10.7 us), while the projections
+// whose weights the attention launch warms into the Infinity Cache (qkv, o, down) and the
+// lm-head sampler lose (profiles/r5_wnt_ab.log, r5_gunt_ab.log)
+template <bool NT>
+__device__ __forceinline__ uint4 ld_wt(const uint16_t *p) {
+    if constexpr (NT) return ld_nt(reinterpret_cast<const uint4 *>(p));
+    return ld_w(p);
+}
 #ifndef SWH_GEMM_RING
 #define SWH_GEMM_RING 0  // decode_gemm k-loop: refill each k-step's weight registers right after its MFMAs (A/B)
 #endif
@@ -848,7 +857,7 @@ __global__ __launch_bounds__(RD ? 768 : 512) void lm_head_kernel(const uint16_t 
         const uint16_t *wr = wbase(tile);
 #pragma unroll
         for (int ks = 0; ks < KR; ++ks)
-            if (KSC || ks < KS) bv[ks] = ld_w(wr + ks * wst);
+            if (KSC || ks < KS) bv[ks] = ld_wt<EPI == EPI_SILU>(wr + ks * wst);
     };
     if (t < ntile) issue(t);  // the weight stream first
     // RMSNorm partials and norm weights (L2), then the X image by LDS-DMA
@@ -1018,10 +1027,10 @@ __global__ __launch_bounds__(RD ? 768 : 512) void lm_head_kernel(const uint16_t 
                     acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[ks % AR][i]), as_bf16x8(bv[ks % KR]),
                                                                     acc[i], 0, 0, 0);
                 if constexpr (RD != 0) {  // half-tile ring: this tile's second half, then the next tile's first
-                    if (ks + KR < KSC) bv[ks % KR] = ld_w(wcur + (ks + KR) * wst);
-                    else if (ring) bv[ks % KR] = ld_w(wnext + (ks + KR - KSC) * wst);
+                    if (ks + KR < KSC) bv[ks % KR] = ld_wt<EPI == EPI_SILU>(wcur + (ks + KR) * wst);
+                    else if (ring) bv[ks % KR] = ld_wt<EPI == EPI_SILU>(wnext + (ks + KR - KSC) * wst);
                 } else if (ring) {
-                    bv[ks] = ld_w(wnext + ks * wst);
+                    bv[ks] = ld_wt<EPI == EPI_SILU>(wnext + ks * wst);
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
