@@ -44,7 +44,7 @@ const char *swh_status_string(int status);
 
 /* Launch policy: geometry choices of the decode GEMMs and samplers, for A/B
  * timing and geometry-coverage tests.  Every alternative is bit-identical
- * (tests pin that) except wide_smax and wide_cb, which choose how
+ * (tests pin that) except wide_smax, wide_cb and wide_waves, which choose how
  * wide_gemm splits K and so the fp32 summation order of its dot products
  * (each deterministic for a given policy).  Process-wide, applied by
  * launches issued after the call (a captured graph keeps the geometry it was
@@ -67,6 +67,8 @@ typedef struct swh_launch_policy {
     int32_t xstream;       /* 0: qkv / o through decode_gemm's LDS X image instead of register-streamed X; 1 */
     int32_t lm_ring14;     /* 0: whole-tile weight ring in the fused lm-head sampler at K = 896; 1 */
     int32_t filt_wgs;      /* target workgroups of one filtered-sampler pass, 64..65536; 1024 */
+    int32_t wide_waves;    /* waves per 128-row-class wide_gemm workgroup (16 x waves weight rows):
+                            * 0 auto (the count that fills the CUs best), 6, 7, 8; 0 */
 } swh_launch_policy;
 int swh_launch_policy_default(swh_launch_policy *out);
 int swh_get_launch_policy(swh_launch_policy *out);

@@ -35,27 +35,30 @@ namespace {
 typedef __bf16 bf16x8w __attribute__((ext_vector_type(8)));
 typedef float f32x4w __attribute__((ext_vector_type(4)));
 
-constexpr int kWW = 8;                 // waves per workgroup
-constexpr int kWT = 64 * kWW;          // threads
+constexpr int kWW = 8;                 // waves per workgroup (the widest geometry)
 constexpr int kWKS = 4;                // k-steps (of 32) per round
 constexpr int kWKC = 32 * kWKS;        // k per round: 128 (256-B rows of 16 pieces)
 constexpr int kWXB = 64 * kWKC * 2;    // X bytes of a round (16 KB)
-constexpr int kWXU = kWXB / 16 / kWT;  // X pieces per thread per round (2)
+constexpr int kWXP = kWXB / 16;        // X pieces of a round (1024)
 
-// Geometry per CB = 16-row weight groups per wave: a workgroup owns NB = 128 CB weight
-// rows.  CB 2 halves the X bytes every workgroup ingests per weight byte (the wide-N
-// shapes: Llama-3-8B gate/up and lm head); its ring is 4 rounds deep (VGPR budget:
-// 40 registers per round against 24).
-template <int CB>
+// Geometry per CB = 16-row weight groups per wave and W = waves: a workgroup owns
+// NB = 16 CB W weight rows.  CB 2 halves the X bytes every workgroup ingests per weight
+// byte (the wide-N shapes: Llama-3-8B lm head); its ring is 4 rounds deep (VGPR budget:
+// 40 registers per round against 24).  W 7 / 6 make tile counts that fill the CUs where
+// 8 waves leave some idle (gate/up: 224 tiles of 128 rows, 256 of 112; qkv: 48 x 5
+// splits, 64 x 4 of 96 rows).
+template <int CB, int W = kWW>
 struct WGeo {
-    static constexpr int NB = 16 * CB * kWW;
-    static constexpr int D = CB == 1 ? 7 : 4;  // rounds in flight (register ring depth)
-    static constexpr int LDT = NB + 4;         // epilogue tile row stride (f32)
-    static constexpr int AUX = 64 * LDT * 4;   // the epilogue tile (the two X slots live inside it), then rstd + flag
+    static constexpr int T = 64 * W;                     // threads
+    static constexpr int NB = 16 * CB * W;
+    static constexpr int XU = (kWXP + T - 1) / T;        // X pieces per thread per round (2 or 3)
+    static constexpr int D = CB == 1 ? (XU == 2 ? 7 : 6) : 4;  // rounds in flight (register ring depth)
+    static constexpr int LDT = NB + 4;                   // epilogue tile row stride (f32)
+    // the epilogue tile, which the two X slots live under, then rstd + flag
+    static constexpr int AUX = 64 * LDT * 4 > 2 * kWXB ? 64 * LDT * 4 : 2 * kWXB;
     static constexpr int LDS = AUX + 64 * 4 + 16;
-    static_assert(2 * kWXB <= AUX, "the two X slots must fit under the epilogue tile");
 };
-constexpr int kWNB = WGeo<1>::NB;      // the narrowest tile: eligibility and the packed layout's 16-row groups
+constexpr int kWNB = 16 * kWW;  // the 8-wave tile: eligibility (wcols % 128)
 
 enum : int { WEPI_PLAIN = 0, WEPI_RESIDUAL = 1, WEPI_SILU = 2 };
 
@@ -101,13 +104,14 @@ __device__ __forceinline__ uint4 pack8w(const float *v) {
 // LDS-DMA notes), so the compiler's counted waits keep WD - 1 rounds in
 // flight; one LDS array (a second __shared__ object makes hipcc wait before
 // LDS reads).
-template <int EPI, int NM, bool BIAS, bool PACKED, int CB>
-__global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restrict__ x, const uint16_t *__restrict__ w,
+template <int EPI, int NM, bool BIAS, bool PACKED, int CB, int W>
+__global__ __launch_bounds__(64 * W) void wide_gemm_kernel(const uint16_t *__restrict__ x, const uint16_t *__restrict__ w,
                                                         int M, int N, int K, float eps, const float *__restrict__ ss_in,
                                                         const uint16_t *__restrict__ bias, uint16_t *__restrict__ res,
                                                         float *__restrict__ ss_out, uint16_t *__restrict__ y, int ldy,
                                                         float *__restrict__ slabs, int *__restrict__ counters) {
-    constexpr int NB = WGeo<CB>::NB, WD = WGeo<CB>::D, LDT = WGeo<CB>::LDT, AUX = WGeo<CB>::AUX;
+    using G = WGeo<CB, W>;
+    constexpr int NB = G::NB, WD = G::D, LDT = G::LDT, AUX = G::AUX, kWT = G::T, kWXU = G::XU;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     float *rstd_s = reinterpret_cast<float *>(lds + AUX);
     int *flag_s = reinterpret_cast<int *>(lds + AUX + 64 * 4);
@@ -122,22 +126,24 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
     if constexpr (NM == 2) {
         // 8 lanes per row, 16-B loads 8 deep: one memory latency (a scalar walk of the
         // row's K / 16 partial sums took 5-6 us at K 4096)
-        const int r = tid >> 3, sub = tid & 7, nc4 = K / 64;
-        const float4 *row = reinterpret_cast<const float4 *>(ss_in + (int64_t)min(r, M - 1) * (K / 16));
-        float4 a = float4{0.f, 0.f, 0.f, 0.f};
+        const int sub = tid & 7, nc4 = K / 64;
+        for (int r = tid >> 3; r < 64; r += kWT / 8) {  // whole 8-lane groups per row
+            const float4 *row = reinterpret_cast<const float4 *>(ss_in + (int64_t)min(r, M - 1) * (K / 16));
+            float4 a = float4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 8
-        for (int f = sub; f < nc4; f += 8) {
-            const float4 t = row[f];
-            a.x += t.x;
-            a.y += t.y;
-            a.z += t.z;
-            a.w += t.w;
+            for (int f = sub; f < nc4; f += 8) {
+                const float4 t = row[f];
+                a.x += t.x;
+                a.y += t.y;
+                a.z += t.z;
+                a.w += t.w;
+            }
+            float v = (a.x + a.y) + (a.z + a.w);
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            if (sub == 0) rstd_s[r] = rsqrtf(v / (float)K + eps);
         }
-        float v = (a.x + a.y) + (a.z + a.w);
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        v += __shfl_xor(v, 4);
-        if (sub == 0) rstd_s[r] = rsqrtf(v / (float)K + eps);
     }
 
     // ---- operands: a register ring WD rounds deep per thread (X pieces + this wave's weight
@@ -167,8 +173,8 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
     }
     const uint16_t *xp[kWXU];
 #pragma unroll
-    for (int u = 0; u < kWXU; ++u) {
-        const int id = tid + kWT * u, row = id >> 4;
+    for (int u = 0; u < kWXU; ++u) {  // pieces past the round (W 6 / 7) repeat the last one, never stored
+        const int id = min(tid + kWT * u, kWXP - 1), row = id >> 4;
         xp[u] = x + (int64_t)min(row, M - 1) * K + kbase + (id & 15) * 8;
     }
     u32x4 xr[WD][kWXU];  // vector type, not the uint4 struct: an aggregate copy kept the ring in scratch
@@ -193,7 +199,8 @@ __global__ __launch_bounds__(kWT) void wide_gemm_kernel(const uint16_t *__restri
         unsigned char *xs = lds + ((r) & 1) * kWXB;                                                             \
         _Pragma("unroll") for (int u = 0; u < kWXU; ++u) {                                                      \
             const int id = tid + kWT * u, row = id >> 4;                                                        \
-            *reinterpret_cast<u32x4 *>(xs + row * (kWKC * 2) + (((id & 15) ^ (row & 15)) * 16)) = xr[D][u];    \
+            if (kWXU * kWT == kWXP || id < kWXP)                                                                \
+                *reinterpret_cast<u32x4 *>(xs + row * (kWKC * 2) + (((id & 15) ^ (row & 15)) * 16)) = xr[D][u]; \
         }                                                                                                       \
         wide_lds_barrier(); /* X(r) visible; every wave has left round r - 2 (same slot) */                     \
         _Pragma("unroll") for (int s = 0; s < kWKS; ++s) {                                                      \
@@ -412,12 +419,37 @@ int wide_cb(int64_t wcols, int64_t K, const swh_launch_policy &pol) {
     return wide_split(wcols / WGeo<2>::NB, K, pol.wide_smax) == 1 ? 2 : 1;
 }
 
-template <int EPI, int NM, bool BIAS, bool PACKED, int CB>
+// Waves per 128-row-class workgroup (16 W weight rows).  Where 8-wave tiles need no K
+// split, the W in 8, 7, 6 dividing wcols whose tiles fill whole rounds of the CUs best
+// (8 on ties): Llama-3-8B gate/up, 224 tiles of 128 rows -> 256 of 112, 48.1 -> 44.2 us.
+// A split shape keeps 8 (qkv as 64 x 4 splits of 96 rows instead of 48 x 5: 17.4 ->
+// 18.1 us; profiles/r5_waves_graph.log).  The launch policy's wide_waves forces one
+// where it divides wcols (A/B).
+int wide_waves(int64_t wcols, int64_t K, const swh_launch_policy &pol) {
+    if (pol.wide_waves) return wcols % (16 * pol.wide_waves) == 0 ? pol.wide_waves : kWW;
+    if (wcols % (16 * kWW) == 0 && wide_split(wcols / (16 * kWW), K, pol.wide_smax) > 1) return kWW;
+    int best = kWW;
+    double bu = -1.0;
+    const int64_t cus = cu_count();
+    for (int w : {8, 7, 6}) {
+        if (wcols % (16 * w)) continue;
+        const int64_t ncb = wcols / (16 * w);
+        if (wide_split(ncb, K, pol.wide_smax) > 1) continue;
+        const double u = (double)ncb / (double)(((ncb + cus - 1) / cus) * cus);
+        if (u > bu + 1e-9) {
+            bu = u;
+            best = w;
+        }
+    }
+    return best;
+}
+
+template <int EPI, int NM, bool BIAS, bool PACKED, int CB, int W>
 int launch_wide(dim3 grid, hipStream_t st, const uint16_t *x, const uint16_t *w, int M, int N, int K, float eps,
                 const float *ss_in, const uint16_t *bias, uint16_t *res, float *ss_out, uint16_t *y, int ldy,
                 float *slabs, int *counters) {
-    if (!lds_opt_in<&wide_gemm_kernel<EPI, NM, BIAS, PACKED, CB>>()) return SWH_E_LAUNCH;  // > 64 KB LDS
-    wide_gemm_kernel<EPI, NM, BIAS, PACKED, CB><<<grid, kWT, WGeo<CB>::LDS, st>>>(
+    if (!lds_opt_in<&wide_gemm_kernel<EPI, NM, BIAS, PACKED, CB, W>>()) return SWH_E_LAUNCH;  // > 64 KB LDS
+    wide_gemm_kernel<EPI, NM, BIAS, PACKED, CB, W><<<grid, WGeo<CB, W>::T, WGeo<CB, W>::LDS, st>>>(
         x, w, M, N, K, eps, ss_in, bias, res, ss_out, y, ldy, slabs, counters);
     return launch_status();
 }
@@ -434,17 +466,23 @@ bool wide_gemm_eligible(int64_t M, int64_t N, int64_t K, int32_t silu) {
 // Bytes of fp32 slabs the split-K reduction needs (0 when the shape is not eligible or S == 1).
 int64_t wide_gemm_slab_bytes(int64_t M, int64_t N, int64_t K, int32_t silu) {
     if (!wide_gemm_eligible(M, N, K, silu)) return 0;
-    // 128-row tiles (the only ones that split) at the largest split the policy allows
+    // 16 W-row tiles (CB 1, the only ones that split) at the largest split the policy allows
     const int64_t wcols = silu ? 2 * N : N;
-    const int s = wide_split(wcols / kWNB, K, 8);
-    return s > 1 ? wcols / kWNB * s * 64 * kWNB * (int64_t)sizeof(float) : 0;
+    int64_t most = 0;
+    for (int w : {8, 7, 6}) {
+        if (wcols % (16 * w)) continue;
+        const int s = wide_split(wcols / (16 * w), K, 8);
+        const int64_t b = s > 1 ? wcols * s * 64 * (int64_t)sizeof(float) : 0;
+        most = b > most ? b : most;
+    }
+    return most;
 }
 
-template <bool P, int CB>
+template <bool P, int CB, int WV>
 int dispatch_wide(dim3 grid, hipStream_t st, const uint16_t *X, const uint16_t *W, int m, int n, int k, float eps,
                   const float *ss_in, const uint16_t *B, uint16_t *R, float *ss_out, uint16_t *Y, int ld, float *slabs,
                   int *ctr, bool silu) {
-#define SWH_WL(E, NMV, BI) launch_wide<E, NMV, BI, P, CB>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr)
+#define SWH_WL(E, NMV, BI) launch_wide<E, NMV, BI, P, CB, WV>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr)
     if (silu) return ss_in ? SWH_WL(WEPI_SILU, 2, false) : SWH_WL(WEPI_SILU, 0, false);
     if (R) return SWH_WL(WEPI_RESIDUAL, 0, false);
     if (B) return ss_in ? SWH_WL(WEPI_PLAIN, 2, true) : SWH_WL(WEPI_PLAIN, 0, true);
@@ -467,7 +505,8 @@ int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, flo
     auto *Y = static_cast<uint16_t *>(y);
     const int m = (int)M, n = (int)N, k = (int)K, ld = (int)ldy;
     const int cb = wide_cb(wcols, K, pol);
-    const int64_t nb = (int64_t)kWNB * cb, ncb = wcols / nb;
+    const int wv = cb == 1 ? wide_waves(wcols, K, pol) : kWW;
+    const int64_t nb = 16 * (int64_t)wv * cb, ncb = wcols / nb;
     const int s = cb == 1 ? wide_split(ncb, K, pol.wide_smax) : 1;
     if (ncb * (int64_t)sizeof(int) > counter_bytes) return 1;
     float *slabs = nullptr;
@@ -477,12 +516,12 @@ int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, flo
     }
     int *ctr = static_cast<int *>(workspace);
     const dim3 grid((unsigned)ncb, (unsigned)s);
-    if (cb == 2) {
-        if (packed) return dispatch_wide<true, 2>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr, silu);
-        return dispatch_wide<false, 2>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr, silu);
-    }
-    if (packed) return dispatch_wide<true, 1>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr, silu);
-    return dispatch_wide<false, 1>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr, silu);
+#define SWH_WD(PK, CBV, WVV) dispatch_wide<PK, CBV, WVV>(grid, st, X, W, m, n, k, eps, ss_in, B, R, ss_out, Y, ld, slabs, ctr, silu)
+    if (cb == 2) return packed ? SWH_WD(true, 2, 8) : SWH_WD(false, 2, 8);
+    if (wv == 7) return packed ? SWH_WD(true, 1, 7) : SWH_WD(false, 1, 7);
+    if (wv == 6) return packed ? SWH_WD(true, 1, 6) : SWH_WD(false, 1, 6);
+    return packed ? SWH_WD(true, 1, 8) : SWH_WD(false, 1, 8);
+#undef SWH_WD
 }
 
 namespace {

@@ -1576,6 +1576,56 @@ def test_wide_gemm_tilings_agree(ops, dev, name, N, K, launch_policy):
 
 
 
+@pytest.mark.parametrize("name,N,K,silu,waves", [("gate_up", 14336, 4096, True, (8, 7)),
+                                                  ("qkv", 6144, 4096, False, (8, 6)),
+                                                  ("wide_res", 5376, 4096, False, (8, 7, 6)),
+                                                  ("long_k_res", 5376, 14336, False, (8, 7, 6))])
+def test_wide_gemm_wave_counts_agree(ops, dev, name, N, K, silu, waves, launch_policy):
+    """wide_gemm with 16 W weight rows per workgroup (W = 8, 7, 6 waves: the
+    launch policy's wide_waves; the default picks the count whose grid fills the
+    CUs) computes the same GEMM: within bf16 output rounding of the fp32 product
+    for each W, deterministic for each, differing only in the K split (fp32
+    summation order); folded norm, SiLU gate, residual + partial sums."""
+    from swh_trl_amd import nn_ops
+    g = _gen(39)
+    M = 64
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
+    ss = x.float().view(M, K // 16, 16).pow(2).sum(-1).contiguous()
+    rstd = torch.rsqrt(ss.sum(-1, keepdim=True) / K + 1e-5)
+    w = (torch.randn(2 * N if silu else N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(dev)
+    wp = nn_ops.wide_pack(w, silu=silu)
+    residual = name.endswith("_res")
+    s0 = torch.randn(M, N, generator=g).to(torch.bfloat16).to(dev)
+    prod = x.float() @ w.float().t()
+
+    def run():
+        if residual:
+            s, sso = s0.clone(), torch.empty(M, N // 16, device=dev)
+            nn_ops.wide_gemm_packed(x, wp, N, residual=s, ss_out=sso)
+            return s, sso
+        return nn_ops.wide_gemm_packed(x, wp, N, silu=silu, ss_in=ss, eps=1e-5), None
+
+    outs = {}
+    for wv in waves:
+        launch_policy(wide_waves=wv)
+        y, sso = run()
+        y2, sso2 = run()
+        assert torch.equal(y, y2) and (sso is None or torch.equal(sso, sso2)), wv
+        if residual:
+            ref = (s0.float() + prod.to(torch.bfloat16).float()).to(torch.bfloat16).float()
+            assert (y.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item() + 2e-2, wv
+            torch.testing.assert_close(sso, y.float().view(M, N // 16, 16).pow(2).sum(-1), rtol=1e-5, atol=1e-4)
+        elif silu:
+            gu = (prod * rstd).to(torch.bfloat16)
+            ref = torch.nn.functional.silu(gu[:, :N].float()).to(torch.bfloat16).float() * gu[:, N:].float()
+            torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
+        else:
+            torch.testing.assert_close(y.float(), prod * rstd, rtol=1e-2, atol=2e-2)
+        outs[wv] = y.float()
+    for wv in waves[1:]:
+        assert (outs[wv] != outs[waves[0]]).float().mean().item() < 0.05, wv
+
+
 @pytest.mark.parametrize("B,Hkv,G", [(64, 2, 8), (24, 2, 8), (12, 1, 4)])
 def test_attn_decode_l3_warmup_is_result_neutral(ops, dev, B, Hkv, G):
     """swh_attn_decode_l3 (warm-up workgroups reading {ptr, bytes/16, 0} ranges on
