@@ -1287,8 +1287,18 @@ __global__ __launch_bounds__(256) void lm_sample_finalize_kernel(const LmPart *_
 // load of a round is issued before the RoPE prologue.
 // ---------------------------------------------------------------------------
 typedef short bf16x4s __attribute__((ext_vector_type(4)));
-constexpr int kAttnThreads = 512;
-constexpr int kAttnWaves = kAttnThreads / 64;
+#ifndef SWH_ATTN_T128
+#define SWH_ATTN_T128 256
+#endif
+#ifndef SWH_ATTN_T64
+#define SWH_ATTN_T64 512
+#endif
+// Threads of a decode-attention workgroup (one (kv head, row)).  At D = 128 (Llama-3-8B:
+// 512 workgroups, 164 VGPRs) four waves let two workgroups share a CU, so one streams
+// while the other runs its prologue / merge: 41.3 -> 37.4 us per layer, decode step
+// 4857 -> 4737 us (two waves: 42.7, three: 38.1; profiles/r5_att4w_graph.log,
+// r5_att2w_graph.log).  At D = 64 (the 0.5B bench, 128 workgroups) eight.
+constexpr int attn_threads(int D) { return D == 128 ? SWH_ATTN_T128 : SWH_ATTN_T64; }
 
 __device__ __forceinline__ bf16x4s lds_read_tr16(const uint16_t *p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -1316,17 +1326,19 @@ __device__ __forceinline__ int64_t frag_at(int64_t b, int c, int K) {
     return (((b >> 4) * (K >> 5) + (c >> 5)) * 64 + ((c >> 3) & 3) * 16 + (b & 15)) * 8 + (c & 7);
 }
 
-// Occupancy at D = 128 (Llama-3-8B), measured (profiles/r5_att_ab.log): 164 VGPRs, one
-// workgroup per CU.  Two per CU by a 128-VGPR bound spill (62 us against 41.5 us per
-// launch, Q fragments re-read from LDS 60 us); 4 key blocks per wave per round (256
-// VGPRs) 44.8 us.
+// Occupancy at D = 128 (Llama-3-8B), measured (profiles/r5_att_ab.log): 164 VGPRs.  With
+// eight waves one workgroup per CU; two per CU by a 128-VGPR bound spill (62 us against
+// 41.5 us per launch, Q fragments re-read from LDS 60 us); 4 key blocks per wave per
+// round (256 VGPRs) 44.8 us.  Four-wave workgroups (attn_threads) put two on a CU
+// without either: 37.4 us.
 template <int D, int GQ>
-__global__ __launch_bounds__(kAttnThreads) void attn_decode_kernel(
+__global__ __launch_bounds__(attn_threads(D)) void attn_decode_kernel(
     const uint16_t *__restrict__ qkv, uint16_t *__restrict__ kc, uint16_t *__restrict__ vc,
     const float *__restrict__ rcos, const float *__restrict__ rsin, const int32_t *__restrict__ plen,
     const int32_t *__restrict__ state, int Hq, int Hkv, int Tmax, float scale, uint16_t *__restrict__ out,
     AttnPrefetch pf) {
     static_assert(GQ <= 16, "a kv head serves at most 16 query heads");
+    constexpr int kAttnThreads = attn_threads(D), kAttnWaves = kAttnThreads / 64;
     constexpr int DC = D / 32;                 // 32-dim chunks: k-steps of K Q^T
     constexpr int DB = D / 16;                 // 16-dim blocks of O^T
     constexpr int JB = (D == 64) ? 4 : 2;      // key blocks per wave per round (pairs for P V)
@@ -1574,7 +1586,7 @@ int launch_attn(const uint16_t *q, uint16_t *kc, uint16_t *vc, const float *rc, 
         extra = (pf.nwg + Hkv - 1) / Hkv;
         if (B + extra > 65535) extra = 0;
     }
-    attn_decode_kernel<D, GQ><<<dim3((unsigned)Hkv, (unsigned)(B + extra)), kAttnThreads, 0, s>>>(
+    attn_decode_kernel<D, GQ><<<dim3((unsigned)Hkv, (unsigned)(B + extra)), attn_threads(D), 0, s>>>(
         q, kc, vc, rc, rs, pl, st, Hq, Hkv, Tmax, scale, o, pf);
     return launch_status();
 }
