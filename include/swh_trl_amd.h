@@ -581,7 +581,11 @@ int swh_lm_head_sample_step(const void *x, const void *w, int64_t M, int64_t V, 
                             int64_t *cur_tokens, const void *embed, void *x_next, float *ss_next, void *workspace,
                             int64_t workspace_bytes, void *stream);
 /* The two entries above over the folded lm-head weight packed by swh_frag_pack
- * (norm_w NULL: the row scale comes from ss_in; K % 128 == 0): same draws. */
+ * (norm_w NULL: the row scale comes from ss_in; K % 128 == 0): same draws.
+ * K > 1024 (Llama-3-8B): the same order as swh_wide_pack writes, through the
+ * bandwidth-regime GEMM's 256-row tiles with the sampler as their epilogue, for
+ * M <= 64 and V % 256 == 0 (else SWH_E_ARG: logits + swh_sample_step); the
+ * draws equal swh_sample_step over the logits those tiles write. */
 int swh_lm_head_sample_fragw(const void *x, const void *w, int64_t M, int64_t V, int64_t K, float eps,
                              const float *ss_in, const swh_sample_params *params, const uint64_t *rng,
                              const int32_t *step, int32_t *finished, int64_t *out_tokens, int64_t out_ld,

@@ -276,6 +276,12 @@ __device__ __forceinline__ SoftState block_soft(SoftState s, float *red) {
 }
 
 // ---- Philox4x32-10 (Salmon et al. SC'11); matches oracle/c/philox_ref.c ----
+// one (row, workgroup) partial of the fused lm-head samplers: the best Gumbel key and its column
+struct LmPart {
+    float key;
+    int32_t idx;
+};
+
 struct U4 {
     uint32_t x, y, z, w;
 };

@@ -36,6 +36,9 @@ int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, flo
 int64_t wide_gemm_slab_bytes(int64_t M, int64_t N, int64_t K, int32_t silu);
 bool wide_gemm_eligible(int64_t M, int64_t N, int64_t K, int32_t silu);
 int wide_pack(const void *src, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, hipStream_t stream);
+int wide_lm_sample(const void *x, const void *w, int64_t M, int64_t V, int64_t K, float eps, const float *ss_in,
+                   const swh_sample_params &p, const uint64_t *rng, const int32_t *step, LmPart *part, int *pstride,
+                   hipStream_t stream);
 int frag_pack(const void *src, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, hipStream_t stream);
 
 namespace {
@@ -796,10 +799,6 @@ constexpr int kLmMaxKS = 32;  // K <= 1024
 // tiles into per-row Gumbel-max bests (the unfiltered swh_sample_step: EOS
 // suppression, temperature, greedy) and writes one partial per row; the
 // Philox block at counter {col, row >> 2} holds the four rows a lane owns.
-struct LmPart {
-    float key;
-    int32_t idx;
-};
 struct LmSample {
     swh_sample_params p;
     const uint64_t *rng;
@@ -2071,15 +2070,15 @@ extern "C" int swh_frag_pack(const void *w, const void *norm_w, int64_t N, int64
 }
 
 // [partials (M x per x 8 LmPart) | 256 B: the finalize ticket (zero at allocation)]
-static int64_t lm_part_bytes(int64_t M) {
+static int64_t lm_part_bytes(int64_t M, int64_t V = 0) {
     const int64_t nmt = (M + 63) / 64, per = cu_count() / nmt > 0 ? cu_count() / nmt : 1;
-    return (M * per * 8 * (int64_t)sizeof(LmPart) + 255) / 256 * 256;
+    const int64_t wide = V / 256 + 1;  // the wide sampler's partials per row (K > 1024)
+    return (M * (per * 8 > wide ? per * 8 : wide) * (int64_t)sizeof(LmPart) + 255) / 256 * 256;
 }
 
 extern "C" int64_t swh_lm_head_sample_workspace_bytes(int64_t M, int64_t V, int64_t K) {
-    (void)V;
     (void)K;
-    return lm_part_bytes(M) + 256;
+    return lm_part_bytes(M, V) + 256;
 }
 
 static int lm_head_sample_impl(const void *x, const void *w, int64_t M, int64_t V, int64_t K, const void *norm_w,
@@ -2088,8 +2087,11 @@ static int lm_head_sample_impl(const void *x, const void *w, int64_t M, int64_t 
                                int64_t *cur_tokens, void *workspace, int64_t workspace_bytes, LmNext nx, void *stream,
                                int fw = 0) {
     if (fw && (norm_w || K % 128)) return SWH_E_ARG;  // fragment order: folded weight (ss_in row scale) only
+    // K > 1024 (Llama-3-8B): a fragment-order (= wide_pack order) weight through wide_gemm's
+    // 256-row tiles with the sampler epilogue, M <= 64, V % 256 == 0
+    const bool wide = fw && K > 32 * kLmMaxKS;
     if (!x || !w || !params || !rng || !step || !finished || !out_tokens || !workspace || M <= 0 || V <= 0 ||
-        K <= 0 || K % 64 || K > 32 * kLmMaxKS || V % 16 || V >= ((int64_t)1 << 31) || M > (1 << 20))
+        K <= 0 || K % 64 || (K > 32 * kLmMaxKS && !wide) || V % 16 || V >= ((int64_t)1 << 31) || M > (1 << 20))
         return SWH_E_ARG;
     const swh_sample_params p = *params;
     const bool filtered = !p.greedy && ((p.top_k > 0 && p.top_k < V) || p.top_p < 1.0f || p.min_p > 0.f);
@@ -2100,6 +2102,16 @@ static int lm_head_sample_impl(const void *x, const void *w, int64_t M, int64_t 
     if ((norm_w && (reinterpret_cast<uintptr_t>(norm_w) & 15)) || (ss_in && (reinterpret_cast<uintptr_t>(ss_in) & 15)))
         return SWH_E_ARG;
     hipStream_t s = static_cast<hipStream_t>(stream);
+    if (wide) {
+        int pstride = 0;
+        LmPart *part = static_cast<LmPart *>(workspace);
+        const int rc = wide_lm_sample(x, w, M, V, K, eps, ss_in, p, rng, step, part, &pstride, s);
+        if (rc == 1) return SWH_E_ARG;  // not a wide shape: logits + swh_sample_step
+        if (rc != SWH_OK) return rc;
+        lm_sample_finalize_kernel<<<dim3((unsigned)M), 256, 0, s>>>(part, pstride, p, step, finished, out_tokens,
+                                                                   out_ld, cur_tokens, (int)V, nx);
+        return launch_status();
+    }
     const int64_t nmt = (M + 63) / 64, per = cu_count() / nmt > 0 ? cu_count() / nmt : 1;
     const int nm = norm_w ? 1 : (ss_in ? 2 : 0);
     const GemmLds L = gemm_lds(1, 64, 8, (int)K, (int)K, nm, false);
@@ -2174,7 +2186,7 @@ static int lm_head_sample_step_impl(const void *x, const void *w, int64_t M, int
     if ((reinterpret_cast<uintptr_t>(embed) | reinterpret_cast<uintptr_t>(x_next)) & 15) return SWH_E_ARG;
     if (workspace_bytes < swh_lm_head_sample_workspace_bytes(M, V, K)) return SWH_E_ARG;
     LmNext nx{static_cast<const uint16_t *>(embed), static_cast<uint16_t *>(x_next), ss_next, step,
-              reinterpret_cast<int32_t *>(static_cast<char *>(workspace) + lm_part_bytes(M)), (int)K, (int)M};
+              reinterpret_cast<int32_t *>(static_cast<char *>(workspace) + lm_part_bytes(M, V)), (int)K, (int)M};
     return lm_head_sample_impl(x, w, M, V, K, norm_w, eps, ss_in, params, rng, step, finished, out_tokens, out_ld,
                                cur_tokens, workspace, workspace_bytes, nx, stream, fw);
 }

@@ -29,6 +29,9 @@ int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, flo
 int64_t wide_gemm_slab_bytes(int64_t M, int64_t N, int64_t K, int32_t silu);
 bool wide_gemm_eligible(int64_t M, int64_t N, int64_t K, int32_t silu);
 int wide_pack(const void *src, const void *norm_w, int64_t N, int64_t K, int32_t silu, void *dst, hipStream_t stream);
+int wide_lm_sample(const void *x, const void *w, int64_t M, int64_t V, int64_t K, float eps, const float *ss_in,
+                   const swh_sample_params &p, const uint64_t *rng, const int32_t *step, LmPart *part, int *pstride,
+                   hipStream_t stream);
 
 namespace {
 
@@ -60,7 +63,17 @@ struct WGeo {
 };
 constexpr int kWNB = 16 * kWW;  // the 8-wave tile: eligibility (wcols % 128)
 
-enum : int { WEPI_PLAIN = 0, WEPI_RESIDUAL = 1, WEPI_SILU = 2 };
+enum : int { WEPI_PLAIN = 0, WEPI_RESIDUAL = 1, WEPI_SILU = 2, WEPI_SAMPLE = 3, WEPI_SAMPLE_T = 4 };
+
+// The fused lm-head sampler's operands (WEPI_SAMPLE: the unfiltered swh_sample_step per
+// element of the tile, _T with the temperature division): one LmPart per (row, workgroup).
+struct WSample {
+    swh_sample_params p;
+    const uint64_t *rng;
+    const int32_t *step;
+    LmPart *part;  // [M][pstride]
+    int pstride;
+};
 
 // Phase timestamps for tools/wide_probe.py (a build with SWH_WIDE_TRACE_ON defined,
 // tools/build_variant.py): wall clock (100 MHz) of thread 0 at each phase boundary.
@@ -109,7 +122,8 @@ __global__ __launch_bounds__(64 * W) void wide_gemm_kernel(const uint16_t *__res
                                                         int M, int N, int K, float eps, const float *__restrict__ ss_in,
                                                         const uint16_t *__restrict__ bias, uint16_t *__restrict__ res,
                                                         float *__restrict__ ss_out, uint16_t *__restrict__ y, int ldy,
-                                                        float *__restrict__ slabs, int *__restrict__ counters) {
+                                                        float *__restrict__ slabs, int *__restrict__ counters,
+                                                        WSample smp) {
     using G = WGeo<CB, W>;
     constexpr int NB = G::NB, WD = G::D, LDT = G::LDT, AUX = G::AUX, kWT = G::T, kWXU = G::XU;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -340,7 +354,72 @@ __global__ __launch_bounds__(64 * W) void wide_gemm_kernel(const uint16_t *__res
     __syncthreads();
 
     // ---- epilogue
-    if constexpr (EPI == WEPI_SILU) {
+    if constexpr (EPI >= WEPI_SAMPLE) {
+        // lm head + sampler (no logits): thread (row quad q, columns tid / 16 + 32 u) draws the
+        // Gumbel keys of rows 4 q .. 4 q + 3 from the Philox block {col, q} exactly as
+        // swh_sample_step does from the bf16 logit (EOS suppression, temperature, greedy),
+        // keeps the best per row, and the workgroup's 64 bests go out as one partial each
+        const int32_t step = *smp.step;
+        const uint64_t seed = smp.rng[0], ctr = smp.rng[1] + (uint64_t)step;
+        const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32), clo = (uint32_t)ctr, chi = (uint32_t)(ctr >> 32);
+        const bool suppress = step < smp.p.min_new_tokens;
+        const float temp = smp.p.temperature;
+        const int q = tid & 15;
+        float bk[4] = {kNegInf, kNegInf, kNegInf, kNegInf};
+        int32_t bi[4] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
+        float sc[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sc[e] = NM == 2 ? rstd_s[4 * q + e] : 1.f;
+        for (int c = tid >> 4; c < NB; c += kWT / 16) {
+            const int col = cb * NB + c;
+            float mask_add = 0.f;
+            if (suppress) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (e < smp.p.n_eos && col == smp.p.eos_ids[e]) mask_add = kNegInf;
+            }
+            U4 rw{0u, 0u, 0u, 0u};
+            if (!smp.p.greedy) rw = philox4x32_10(U4{(uint32_t)col, (uint32_t)q, clo, chi}, k0, k1);
+            const uint32_t wd[4] = {rw.x, rw.y, rw.z, rw.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float z = round_bf16(tile[(4 * q + e) * LDT + c] * sc[e]);  // the bf16 logit
+                if constexpr (EPI == WEPI_SAMPLE_T) z = z / temp;
+                float key = smp.p.greedy ? z : z - fast_log(-fast_log(u01_from_bits(wd[e])));
+                key += mask_add;
+                const bool better = (key > bk[e]) | ((key == bk[e]) & (col < bi[e]));
+                bk[e] = better ? key : bk[e];
+                bi[e] = better ? col : bi[e];
+            }
+        }
+        // the 4 lanes of a wave with this quad, then the waves through LDS (the tile is read)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int o = 16; o < 64; o <<= 1) {
+                const float k2 = __shfl_xor(bk[e], o);
+                const int32_t c2 = __shfl_xor(bi[e], o);
+                if (k2 > bk[e] || (k2 == bk[e] && (uint32_t)c2 < (uint32_t)bi[e])) {
+                    bk[e] = k2;
+                    bi[e] = c2;
+                }
+            }
+        __syncthreads();
+        LmPart *wpart = reinterpret_cast<LmPart *>(lds);  // [W][64]
+        if (lane < 16) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) wpart[wid * 64 + 4 * q + e] = LmPart{bk[e], bi[e]};
+        }
+        __syncthreads();
+        if (tid < 64 && tid < M) {
+            LmPart b = wpart[tid];
+            for (int v = 1; v < W; ++v) {
+                const LmPart o = wpart[v * 64 + tid];
+                if (o.key > b.key || (o.key == b.key && (uint32_t)o.idx < (uint32_t)b.idx)) b = o;
+            }
+            smp.part[(int64_t)tid * smp.pstride + cb] = b;
+        }
+    } else if constexpr (EPI == WEPI_SILU) {
         // 64 rows x 8 groups of 8 output columns: tile columns 16 g + c (gate) and 16 g + 8 + c (up)
         for (int idx = tid; idx < 64 * (NB / 16); idx += kWT) {
             const int r = idx / (NB / 16), g = idx % (NB / 16);
@@ -447,10 +526,10 @@ int wide_waves(int64_t wcols, int64_t K, const swh_launch_policy &pol) {
 template <int EPI, int NM, bool BIAS, bool PACKED, int CB, int W>
 int launch_wide(dim3 grid, hipStream_t st, const uint16_t *x, const uint16_t *w, int M, int N, int K, float eps,
                 const float *ss_in, const uint16_t *bias, uint16_t *res, float *ss_out, uint16_t *y, int ldy,
-                float *slabs, int *counters) {
+                float *slabs, int *counters, const WSample &smp = WSample{}) {
     if (!lds_opt_in<&wide_gemm_kernel<EPI, NM, BIAS, PACKED, CB, W>>()) return SWH_E_LAUNCH;  // > 64 KB LDS
     wide_gemm_kernel<EPI, NM, BIAS, PACKED, CB, W><<<grid, WGeo<CB, W>::T, WGeo<CB, W>::LDS, st>>>(
-        x, w, M, N, K, eps, ss_in, bias, res, ss_out, y, ldy, slabs, counters);
+        x, w, M, N, K, eps, ss_in, bias, res, ss_out, y, ldy, slabs, counters, smp);
     return launch_status();
 }
 
@@ -522,6 +601,29 @@ int wide_gemm(const void *x, const void *w, int64_t M, int64_t N, int64_t K, flo
     if (wv == 6) return packed ? SWH_WD(true, 1, 6) : SWH_WD(false, 1, 6);
     return packed ? SWH_WD(true, 1, 8) : SWH_WD(false, 1, 8);
 #undef SWH_WD
+}
+
+// lm head + unfiltered sampler over a wide_pack'ed weight [V, K] (folded norm: ss_in row
+// scale), 256-row tiles without a K split: one LmPart per (row, tile) into part, *pstride =
+// V / 256 partials per row for the finalize.  1 = not served (the caller takes logits +
+// swh_sample_step), else a SWH status.
+int wide_lm_sample(const void *x, const void *w, int64_t M, int64_t V, int64_t K, float eps, const float *ss_in,
+                   const swh_sample_params &p, const uint64_t *rng, const int32_t *step, LmPart *part, int *pstride,
+                   hipStream_t st) {
+    if (!wide_gemm_eligible(M, V, K, 0) || V % WGeo<2>::NB) return 1;
+    const int ncb = (int)(V / WGeo<2>::NB);
+    WSample smp{p, rng, step, part, ncb};
+    *pstride = ncb;
+    const dim3 grid((unsigned)ncb, 1u);
+    const auto *X = static_cast<const uint16_t *>(x);
+    const auto *Wt = static_cast<const uint16_t *>(w);
+    const int m = (int)M, n = (int)V, k = (int)K;
+    const bool tdiv = !p.greedy && p.temperature != 1.0f;
+#define SWH_WS(E, NMV) launch_wide<E, NMV, false, true, 2, kWW>(grid, st, X, Wt, m, n, k, eps, ss_in, nullptr, nullptr, \
+                                                              nullptr, nullptr, 0, nullptr, nullptr, smp)
+    if (ss_in) return tdiv ? SWH_WS(WEPI_SAMPLE_T, 2) : SWH_WS(WEPI_SAMPLE, 2);
+    return tdiv ? SWH_WS(WEPI_SAMPLE_T, 0) : SWH_WS(WEPI_SAMPLE, 0);
+#undef SWH_WS
 }
 
 namespace {

@@ -226,8 +226,13 @@ class DecodeEngine:
     def _fused_sample(self) -> bool:
         """lm head + sampler in one kernel (no logits): unfiltered sampling
         without the per-token log-prob output."""
+        # K > 1024 (the wide-tile sampler): opt-in — its kernels sum 46 us less per step than
+        # logits + sample_step, yet the Llama-3-8B decode step measured 4809-4818 against
+        # 4775-4777 us (profiles/r5_wsamp_ab.log), so logits + sample_step stay the default
+        wide = "lm" in self.packed and os.environ.get("SWH_FUSED_SAMPLE_WIDE", "0") == "1"
         return (self.fused and not self.want_logp and os.environ.get("SWH_FUSED_SAMPLE", "1") != "0" and
-                nn_ops.lm_head_sample_supported(self.params, self.cfg.vocab_size, self.cfg.hidden_size))
+                nn_ops.lm_head_sample_supported(self.params, self.cfg.vocab_size, self.cfg.hidden_size,
+                                                wide_rows=self.B if wide else 0))
 
     def _projections(self) -> dict:
         """name -> (N, K, silu, RMSNorm weight name or None) of the decode GEMMs."""
@@ -287,9 +292,12 @@ class DecodeEngine:
         return self._weight(name), self.model.p[norm]
 
     def _lm_head_weight(self):
-        """(weight, norm_w, fragment order?) the fused lm-head sampler reads."""
+        """(weight, norm_w, fragment order?) the fused lm-head sampler reads
+        (the wide_pack copy is in the same fragment order)."""
         if "lm" in self.fragw:
             return self.fragw["lm"], None, 1
+        if "lm" in self.packed:
+            return self.packed["lm"], None, 1
         return (*self._normed("lm", "norm"), False)
 
     def _proj(self, name: str, x: torch.Tensor, **kw):

@@ -311,11 +311,18 @@ def wide_gemm_packed(x: torch.Tensor, w_packed: torch.Tensor, N: int, *, eps: fl
     return residual if residual is not None else y
 
 
-def lm_head_sample_supported(params, V: int, K: int) -> bool:
+def lm_head_sample_supported(params, V: int, K: int, wide_rows: int = 0) -> bool:
     """The fused lm-head sampler covers unfiltered sampling (temperature,
-    greedy, EOS suppression); the rest goes through logits + sample_step."""
+    greedy, EOS suppression); the rest goes through logits + sample_step.
+    K <= 1024: the tile kernel (any weight order); K > 1024: wide_gemm's
+    256-row tiles over a fragment-order (wide_pack) weight, for wide_rows
+    (the batch, <= 64) rows and V % 256 == 0 (wide_rows 0: not available)."""
     filtered = not params.greedy and ((0 < params.top_k < V) or params.top_p < 1.0 or params.min_p > 0.0)
-    return (not filtered and params.repetition_penalty == 1.0 and K % 64 == 0 and K <= 1024 and V % 16 == 0)
+    if filtered or params.repetition_penalty != 1.0 or K % 64 or V % 16:
+        return False
+    if K <= 1024:
+        return True
+    return bool(wide_rows) and V % 256 == 0 and wide_gemm_eligible(wide_rows, V, K)
 
 
 def lm_head_sample(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Tensor, step: torch.Tensor,
@@ -324,12 +331,12 @@ def lm_head_sample(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Tensor, 
                    workspace: Optional[torch.Tensor] = None, fragw: int = 0) -> torch.Tensor:
     """lm head + the unfiltered sampler in one pass, no logits tensor
     (include/swh_trl_amd.h swh_lm_head_sample; fragw 1: w packed by frag_pack,
-    swh_lm_head_sample_fragw).  Writes out_tokens[:, *step], cur_tokens,
+    or the flat wide_pack copy at K > 1024, swh_lm_head_sample_fragw).  Writes out_tokens[:, *step], cur_tokens,
     finished; returns out_tokens."""
     import ctypes
     _dev(x, "lm_head_sample")
     M, K = x.shape
-    V = w.shape[0]
+    V = w.numel() // K  # [V, K], or the flat wide_pack copy
     need = _lib.load().swh_lm_head_sample_workspace_bytes(M, V, K)
     if workspace is None or workspace.numel() < need:
         workspace = torch.empty(need, dtype=torch.uint8, device=x.device)
@@ -354,7 +361,7 @@ def lm_head_sample_step(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Ten
     import ctypes
     _dev(x, "lm_head_sample_step")
     M, K = x.shape
-    V = w.shape[0]
+    V = w.numel() // K  # [V, K], or the flat wide_pack copy
     if workspace.numel() < _lib.load().swh_lm_head_sample_workspace_bytes(M, V, K):
         raise ValueError("lm_head_sample_step: workspace too small")
     if fragw and norm_w is not None:

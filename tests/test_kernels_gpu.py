@@ -1157,6 +1157,48 @@ def test_lm_head_sample_equals_logits_then_sampler(ops, dev, kw, M, V, fold):
         assert not torch.isin(out_b[:, step], torch.tensor(eos, device=dev)).any()
 
 
+@pytest.mark.parametrize("kw", [dict(), dict(temperature=0.7), dict(greedy=True), dict(min_new_tokens=5),
+                                dict(temperature=1.3, min_new_tokens=1)])
+@pytest.mark.parametrize("M,V", [(64, 4096), (37, 8192), (64, 128256)])
+def test_lm_head_sample_wide_equals_logits_then_sampler(ops, dev, kw, M, V, launch_policy):
+    """K > 1024 (Llama-3-8B, hidden 4096): the fused sampler over the wide_pack'ed
+    folded lm-head weight (wide_gemm's 256-row tiles, sampler epilogue, one
+    partial per row and tile) draws, bit for bit, the token swh_sample_step draws
+    from the bf16 logits the same tiles write, with EOS suppression, pad-after-EOS
+    and the finished flags."""
+    from swh_trl_amd import nn_ops
+    g = _gen(37)
+    H = 4096
+    x = torch.randn(M, H, generator=g).to(torch.bfloat16).to(dev)
+    w = (torch.randn(V, H, generator=g) * 0.05).to(torch.bfloat16).to(dev)
+    nw = (1 + 0.1 * torch.randn(H, generator=g)).to(torch.bfloat16).to(dev)
+    ss = x.float().view(M, H // 16, 16).pow(2).sum(-1).contiguous()
+    eos = [3, 77]
+    w[3] += 0.02  # make EOS likely so suppression and bookkeeping matter
+    wp = nn_ops.wide_pack(w, nw)
+    params = ops.make_sample_params(eos_token_ids=eos, pad_token_id=5, **kw)
+    step = 2
+    rng = torch.tensor([321, 54], dtype=torch.int64, device=dev)
+    stp = torch.tensor([step], dtype=torch.int32, device=dev)
+    fin0 = (torch.arange(M) % 7 == 0).int().to(dev)
+    assert nn_ops.lm_head_sample_supported(params, V, H, wide_rows=M)
+    launch_policy(wide_cb=2)  # the logits through the same 256-row tiles (no K split)
+    logits = nn_ops.wide_gemm_packed(x, wp, V, eps=1e-6, ss_in=ss)
+    out_a = torch.full((M, 4), -1, dtype=torch.int64, device=dev)
+    cur_a = torch.empty(M, dtype=torch.int64, device=dev)
+    fin_a = fin0.clone()
+    ops.sample_step(logits, params, rng, stp, fin_a, out_a, cur_a)
+    out_b = torch.full((M, 4), -1, dtype=torch.int64, device=dev)
+    cur_b = torch.empty(M, dtype=torch.int64, device=dev)
+    fin_b = fin0.clone()
+    nn_ops.lm_head_sample(x, wp, params, rng, stp, fin_b, out_b, cur_b, eps=1e-6, ss_in=ss, fragw=True)
+    assert torch.equal(out_b, out_a)
+    assert torch.equal(cur_b, cur_a)
+    assert torch.equal(fin_b, fin_a)
+    if kw.get("min_new_tokens", 0) > step:
+        assert not torch.isin(out_b[:, step], torch.tensor(eos, device=dev)).any()
+
+
 def test_lm_head_sample_refuses_filtered(ops, dev):
     from swh_trl_amd import nn_ops
     x = torch.zeros(4, 896, dtype=torch.bfloat16, device=dev)
