@@ -343,6 +343,17 @@ def test_ppo_trainer_train_runs(dev):
         assert log[k] == log[k], k  # finite
 
 
+def test_ppo_final_checkpoint_when_steps_not_multiple_of_save_steps(dev, tmp_path):
+    """DefaultFlowCallback's end-of-training branch (the reference PPOTrainer's
+    default callbacks): with save_strategy 'steps', the last update saves even
+    when num_total_batches is not a multiple of save_steps."""
+    import os
+    tr, _ = _trainer(dev, total_episodes=24, save_steps=2, output_dir=str(tmp_path))
+    state = tr.train()
+    assert state.global_step == tr.args.num_total_batches == 3
+    assert os.path.isdir(tmp_path / "checkpoint-2") and os.path.isdir(tmp_path / "checkpoint-3")
+
+
 @pytest.mark.parametrize("width", WIDTHS)
 def test_ppo_fused_micro_batches_equal_separate(dev, width):
     """A mini-batch's GA micro-batches in one fused pass give the gradient of GA
