@@ -226,10 +226,9 @@ class DecodeEngine:
     def _fused_sample(self) -> bool:
         """lm head + sampler in one kernel (no logits): unfiltered sampling
         without the per-token log-prob output."""
-        # K > 1024 (the wide-tile sampler): opt-in — its kernels sum 46 us less per step than
-        # logits + sample_step, yet the Llama-3-8B decode step measured 4809-4818 against
-        # 4775-4777 us (profiles/r5_wsamp_ab.log), so logits + sample_step stay the default
-        wide = "lm" in self.packed and os.environ.get("SWH_FUSED_SAMPLE_WIDE", "0") == "1"
+        # K > 1024: the wide-tile sampler (config 5's step 9.744 -> 9.682 s,
+        # profiles/r5_wsamp_step_ab.log); SWH_FUSED_SAMPLE_WIDE=0 keeps logits + sample_step
+        wide = "lm" in self.packed and os.environ.get("SWH_FUSED_SAMPLE_WIDE", "1") != "0"
         return (self.fused and not self.want_logp and os.environ.get("SWH_FUSED_SAMPLE", "1") != "0" and
                 nn_ops.lm_head_sample_supported(self.params, self.cfg.vocab_size, self.cfg.hidden_size,
                                                 wide_rows=self.B if wide else 0))
@@ -558,8 +557,11 @@ class DecodeEngine:
             out[name] = {"avg_us": timed(fn, n, per_step), "bytes_per_launch": float(nbytes),
                          "launches_per_step": per_step}
         self.state[0] = step_index
-        out["decode_step"] = {"avg_us": timed(lambda i: self._step_fused(), 2, 1), "bytes_per_launch": None,
+        # the whole step the decode graph replays: with logits + sample_step that includes the
+        # sampler and the step advance (the replays advance the step counter either way)
+        out["decode_step"] = {"avg_us": timed(lambda i: self._step(), 2, 1), "bytes_per_launch": None,
                               "launches_per_step": 1}
+        self.state[0] = step_index
         return out
 
     # ------------------------------------------------------------------ prefill
