@@ -806,7 +806,8 @@ class CausalLM:
         """Per-token log-probs (differentiable, fp32) and entropies (no grad) of
         `ids` under softmax(lm_head(hidden) / T), chunked over rows."""
         if chunk_rows is None:
-            chunk_rows = max(1, min(4096, (1 << 30) // self.cfg.vocab_size))
+            cap = int(os.environ.get("SWH_LOGP_CHUNK", "4096"))  # A/B (tools/train_kernels.py)
+            chunk_rows = max(1, min(cap, (1 << 30) // self.cfg.vocab_size))
         lp, ent = _LMHeadLogp.apply(hidden, self.lm_weight(), self._lm_grad(), ids, float(temperature),
                                     bool(compute_entropy), int(chunk_rows))
         return lp, (ent if compute_entropy else None)
