@@ -69,6 +69,8 @@ typedef struct swh_launch_policy {
     int32_t filt_wgs;      /* target workgroups of one filtered-sampler pass, 64..65536; 1024 */
     int32_t wide_waves;    /* waves per 128-row-class wide_gemm workgroup (16 x waves weight rows):
                             * 0 auto (the count that fills the CUs best), 6, 7, 8; 0 */
+    int32_t attn_pair;     /* 1: decode attention at D = 128 on one workgroup per (kv head, two rows),
+                            * a shared GRPO prompt's keys read once for both; 0: one per row; 1 */
 } swh_launch_policy;
 int swh_launch_policy_default(swh_launch_policy *out);
 int swh_get_launch_policy(swh_launch_policy *out);

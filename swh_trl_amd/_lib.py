@@ -46,7 +46,7 @@ class LaunchPolicy(C.Structure):
     _fields_ = [("wide_kmin", c_i64), ("wide_gemm", c_i32), ("wide_smax", c_i32), ("wide_cb", c_i32),
                 ("gemm_ms", c_i32), ("gemm_cb", c_i32), ("gemm_s", c_i32), ("gemm_persist", c_i32),
                 ("gemm_wn", c_i32), ("gemm_tile", c_i32), ("gemm_nw", c_i32), ("xstream", c_i32),
-                ("lm_ring14", c_i32), ("filt_wgs", c_i32), ("wide_waves", c_i32)]
+                ("lm_ring14", c_i32), ("filt_wgs", c_i32), ("wide_waves", c_i32), ("attn_pair", c_i32)]
 
 
 # name -> (restype, argtypes)
@@ -181,7 +181,8 @@ def load() -> C.CDLL:
 # another policy later calls set_launch_policy / launch_policy(...).
 _ENV_POLICY = {"SWH_WIDE_KMIN": "wide_kmin", "SWH_WIDE_GEMM": "wide_gemm", "SWH_WIDE_SMAX": "wide_smax",
                "SWH_WIDE_CB": "wide_cb", "SWH_GEMM_NW": "gemm_nw", "SWH_XSTREAM": "xstream",
-               "SWH_LM_RING14": "lm_ring14", "SWH_FILT_WGS": "filt_wgs", "SWH_WIDE_WAVES": "wide_waves"}
+               "SWH_LM_RING14": "lm_ring14", "SWH_FILT_WGS": "filt_wgs", "SWH_WIDE_WAVES": "wide_waves",
+               "SWH_ATTN_PAIR": "attn_pair"}
 
 
 def _geometry_fields(cfg: str) -> dict:

@@ -1575,6 +1575,297 @@ __global__ __launch_bounds__(attn_threads(D)) void attn_decode_kernel(
 #undef SWH_ATTN_ISSUE
 }
 
+// ---------------------------------------------------------------------------
+// Row-pair decode attention (D = 128, 2 GQ <= 16: Llama-3-8B): one 8-wave workgroup
+// per (kv head, two consecutive rows).  The MFMA's 16 query columns hold both rows'
+// heads (row A in columns 0 .. GQ-1, row B in GQ .. 2 GQ-1), so when the rows share a
+// GRPO group's prompt (prompt_row and prompt length equal) its keys and values are
+// loaded ONCE and scored for both rows; each row's own keys follow with the other
+// row's columns masked to -inf (their online-softmax state untouched).  One wave of
+// 256 workgroups instead of two of 512 halves the exposed argument / RoPE / merge
+// phases as well (timing probe: 37.8 -> 32.3 us per layer, profiles/r5_pair_graph.log).
+// Same per-column arithmetic as attn_decode_kernel (scores, online softmax, P V,
+// fixed-order wave merge), with the keys visited in another order.
+// ---------------------------------------------------------------------------
+template <int D, int GQ>
+__global__ __launch_bounds__(512) void attn_decode_pair_kernel(
+    const uint16_t *__restrict__ qkv, uint16_t *__restrict__ kc, uint16_t *__restrict__ vc,
+    const float *__restrict__ rcos, const float *__restrict__ rsin, const int32_t *__restrict__ plen,
+    const int32_t *__restrict__ state, int Hq, int Hkv, int Tmax, float scale, uint16_t *__restrict__ out,
+    AttnPrefetch pf) {
+    static_assert(2 * GQ <= 16, "two rows' query heads in the 16 MFMA columns");
+    constexpr int NT = 512, NW = NT / 64;
+    constexpr int DC = D / 32, DB = D / 16, JB = 2, KPR = JB * 16 * NW, HD = D / 2;
+    constexpr int VS = D + (D == 64 ? 8 : 16);
+    __shared__ __attribute__((aligned(16))) uint16_t q_s[16 * D];
+    __shared__ __attribute__((aligned(16))) uint16_t kn_s[2][D];
+    __shared__ __attribute__((aligned(16))) uint16_t vn_s[2][D];
+    constexpr int kRed = 16 * (D + 2) * 4, kVt = 32 * VS * 2;
+    constexpr int kSlot = (kRed > kVt ? kRed : kVt) / 16 * 16;
+    __shared__ __attribute__((aligned(16))) unsigned char slot_s[NW][kSlot];
+    auto red_s = [&](int w2, int h) -> float * { return reinterpret_cast<float *>(slot_s[w2]) + h * (D + 2); };
+
+    const int kvh = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int g = lane >> 4, c16 = lane & 15;
+    const int npairs = (pf.rows + 1) / 2;
+    if ((int)blockIdx.y >= npairs) {  // an Infinity Cache warm-up workgroup
+        if (pf.jobs)
+            l3_warm_share<NT>(pf.jobs, pf.njobs, (blockIdx.y - npairs) * gridDim.x + blockIdx.x,
+                              (gridDim.y - npairs) * gridDim.x, pf.sink);
+        return;
+    }
+    const int step = state[0] - 1, P = state[1];
+    const int slot_new = P + step;
+    const int64_t bA = 2 * (int64_t)blockIdx.y;
+    const bool hasB = bA + 1 < pf.rows;
+    const int64_t bB = hasB ? bA + 1 : bA;
+    const int plA = plen[bA], plB = plen[bB];
+    const bool okA = !(step < 0 || slot_new >= Tmax || plA < 0 || plA > P);
+    const bool okB = hasB && !(step < 0 || slot_new >= Tmax || plB < 0 || plB > P);
+    if (!okA || (hasB && !okB)) {  // never write outside the cache: NaN rows, fail loudly
+        for (int r = 0; r < (hasB ? 2 : 1); ++r) {
+            const int64_t b = bA + r;
+            for (int idx = tid; idx < GQ * D; idx += NT)
+                out[pf.ofrag ? frag_at(b, kvh * GQ * D + idx, Hq * D) : b * (int64_t)Hq * D + kvh * GQ * D + idx] =
+                    0x7fc0;
+        }
+        return;
+    }
+    const int64_t prA = pf.prow ? (int64_t)min(max(pf.prow[bA], 0), pf.rows - 1) : bA;
+    const int64_t prB = pf.prow ? (int64_t)min(max(pf.prow[bB], 0), pf.rows - 1) : bB;
+    const bool shared = hasB && prA == prB && plA == plB && plA > 0;  // one prompt for both rows
+    const int nA = slot_new - (P - plA) + 1, nB = slot_new - (P - plB) + 1;  // keys incl. the new one
+    auto cbase = [&](int64_t r) -> int64_t { return (r * Hkv + kvh) * (int64_t)Tmax * D; };
+    const int64_t cbA = cbase(bA), cbB = cbase(bB);
+
+    // key segments: [lo, hi) of a row's key numbering (prompt keys first), read from the
+    // prompt row's cache below pl and the row's own cache from pl on; columns [clo, chi)
+    struct Seg {
+        int lo, hi, pl, n, clo, chi, fresh;  // fresh: 0 none, 1 row A's new key, 2 row B's
+        const uint16_t *kb, *vb, *kbp, *vbp;
+    };
+    const int stA = P - plA, stB = P - plB;
+    const uint16_t *kA = kc + cbA + (int64_t)stA * D + g * 8, *vA = vc + cbA + (int64_t)stA * D + g * 8;
+    const uint16_t *kB = kc + cbB + (int64_t)stB * D + g * 8, *vB = vc + cbB + (int64_t)stB * D + g * 8;
+    const uint16_t *kpA = kc + cbase(prA) + (int64_t)stA * D + g * 8, *vpA = vc + cbase(prA) + (int64_t)stA * D + g * 8;
+    const uint16_t *kpB = kc + cbase(prB) + (int64_t)stB * D + g * 8, *vpB = vc + cbase(prB) + (int64_t)stB * D + g * 8;
+    // A row's keys are always visited as its prompt [0, pl), then its own [pl, n), with the
+    // same round boundaries, so a column's result does not depend on whether the pair
+    // shares its prompt (shared: one prompt segment scored for both rows' columns).  No
+    // dynamic indexing (a segment array lived in scratch): the segments as values.
+    const Seg sP{0, plA, plA, 0x7fffffff, 0, 2 * GQ, 0, kA, vA, kpA, vpA};
+    const Seg sAp{0, plA, plA, 0x7fffffff, 0, GQ, 0, kA, vA, kpA, vpA};
+    const Seg sAo{plA, nA, plA, nA, 0, GQ, 1, kA, vA, kpA, vpA};
+    const Seg sBp{0, hasB ? plB : 0, plB, 0x7fffffff, GQ, 2 * GQ, 0, kB, vB, kpB, vpB};
+    const Seg sBo{plB, hasB ? nB : plB, plB, nB, GQ, 2 * GQ, 2, kB, vB, kpB, vpB};
+    const Seg s0 = shared ? sP : sAp;
+
+    u32x4 kr[JB][DC], vr[JB][DC];
+    // A run visits the 16-key blocks of a virtual list: part X's keys [X.lo, X.hi) padded to
+    // whole blocks, then part Y's [Y.lo, Y.hi); each block belongs to one part (wave-uniform),
+    // so both rows' own keys share rounds.  blk(k0v) -> the part's Seg and key index.
+#define SWH_PAIR_BLOCK(X_, Y_, k0v_, S_, k0_)                                                     \
+    const int p1_ = ((X_).hi - (X_).lo + 15) / 16 * 16;                                           \
+    const bool iny_ = (k0v_) >= p1_;                                                              \
+    const Seg S_ = iny_ ? (Y_) : (X_);                                                            \
+    const int k0_ = iny_ ? (Y_).lo + (k0v_) - p1_ : (X_).lo + (k0v_);
+#define SWH_PAIR_ISSUE(X_, Y_, base_)                                                             \
+    _Pragma("unroll") for (int i = 0; i < JB; ++i) {                                              \
+        SWH_PAIR_BLOCK(X_, Y_, (base_) + (wid + i * NW) * 16, S_, k0_)                            \
+        if (k0_ < S_.hi) {                                                                        \
+            const int kk = max(min(k0_ + c16, min(S_.hi, S_.n - 1) - 1), 0);                      \
+            const uint16_t *ks_ = kk < S_.pl ? S_.kbp : S_.kb;                                    \
+            const uint16_t *vs_ = kk < S_.pl ? S_.vbp : S_.vb;                                    \
+            _Pragma("unroll") for (int c = 0; c < DC; ++c) {                                      \
+                kr[i][c] = *reinterpret_cast<const u32x4 *>(ks_ + (int64_t)kk * D + c * 32);      \
+                vr[i][c] = *reinterpret_cast<const u32x4 *>(vs_ + (int64_t)kk * D + c * 32);      \
+            }                                                                                     \
+        }                                                                                         \
+    }
+    const Seg s_none{0, 0, 0, 0, 0, 0, 0, kA, vA, kA, vA};
+    SWH_PAIR_ISSUE(s0, s_none, 0)  // the first segment's KV stream is in flight during RoPE
+
+    // RoPE of both rows' query heads (columns 0 .. 2 GQ - 1) and new keys; new values
+    for (int idx = tid; idx < 2 * (GQ + 1) * HD; idx += NT) {
+        const int r = idx / ((GQ + 1) * HD), rem = idx - r * (GQ + 1) * HD;
+        const int hh = rem / HD, i = rem - hh * HD;
+        const int64_t b = r ? bB : bA;
+        const int pos = (r ? plB : plA) + step;
+        const uint16_t *row = qkv + b * (int64_t)(Hq + 2 * Hkv) * D;
+        const float c = rcos[(int64_t)pos * HD + i], s = rsin[(int64_t)pos * HD + i];
+        const uint16_t *src = (hh < GQ) ? row + (kvh * GQ + hh) * D : row + (Hq + kvh) * D;
+        const float x1 = bf16_bits_to_f32(src[i]), x2 = bf16_bits_to_f32(src[i + HD]);
+        const uint16_t o1 = f32_to_bf16_bits(round_bf16(x1 * c) + round_bf16(-x2 * s));
+        const uint16_t o2 = f32_to_bf16_bits(round_bf16(x2 * c) + round_bf16(x1 * s));
+        if (hh < GQ) {
+            q_s[(r * GQ + hh) * D + i] = o1;
+            q_s[(r * GQ + hh) * D + i + HD] = o2;
+        } else {
+            kn_s[r][i] = o1;
+            kn_s[r][i + HD] = o2;
+        }
+    }
+    for (int idx = 2 * GQ * D + tid; idx < 16 * D; idx += NT) q_s[idx] = 0;
+    for (int d = tid; d < 2 * D; d += NT) {
+        const int r = d / D;
+        vn_s[r][d - r * D] = qkv[(r ? bB : bA) * (int64_t)(Hq + 2 * Hkv) * D + (Hq + Hkv + kvh) * D + d - r * D];
+    }
+    lds_barrier();
+    for (int d = tid; d < (hasB ? 2 : 1) * D; d += NT) {  // KV append of both rows
+        const int r = d / D, e = d - r * D;
+        const int64_t cb = r ? cbB : cbA;
+        kc[cb + (int64_t)slot_new * D + e] = kn_s[r][e];
+        vc[cb + (int64_t)slot_new * D + e] = vn_s[r][e];
+    }
+
+    u32x4 qb[DC];
+#pragma unroll
+    for (int c = 0; c < DC; ++c) qb[c] = *reinterpret_cast<const u32x4 *>(q_s + c16 * D + c * 32 + g * 8);
+    float m = kNegInf, l = 0.f;
+    f32x4 o[DB];
+#pragma unroll
+    for (int d = 0; d < DB; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint16_t *vt = reinterpret_cast<uint16_t *>(slot_s[wid]);
+
+    bool first = true;
+    auto run = [&](const Seg &X, const Seg &Y) __attribute__((always_inline)) {
+        const int vlen = (X.hi - X.lo + 15) / 16 * 16 + (Y.hi - Y.lo);
+        if (X.hi <= X.lo && Y.hi <= Y.lo) return;
+        for (int base = 0; base < vlen; base += KPR) {
+            if (!first) {
+                SWH_PAIR_ISSUE(X, Y, base)
+            }
+            first = false;
+            f32x4 sc[JB];
+            float mx = m;
+            bool live[JB];  // block i holds some key (wave-uniform)
+#pragma unroll
+            for (int i = 0; i < JB; ++i) {
+                SWH_PAIR_BLOCK(X, Y, base + (wid + i * NW) * 16, S, k0)
+                const bool colv = c16 >= S.clo && c16 < S.chi;  // this lane's column scores these keys
+                sc[i] = f32x4{kNegInf, kNegInf, kNegInf, kNegInf};
+                live[i] = k0 < S.hi;
+                if (k0 < S.hi) {  // wave-uniform
+                    const bool fresh = S.fresh && (k0 + c16 == S.n - 1);  // the new key/value, from LDS
+                    const int fr = S.fresh == 2 ? 1 : 0;
+#pragma unroll
+                    for (int c = 0; c < DC; ++c) {
+                        const u32x4 kn = *reinterpret_cast<const u32x4 *>(kn_s[fr] + c * 32 + g * 8);
+                        const u32x4 vn = *reinterpret_cast<const u32x4 *>(vn_s[fr] + c * 32 + g * 8);
+                        kr[i][c] = fresh ? kn : kr[i][c];
+                        vr[i][c] = fresh ? vn : vr[i][c];
+                    }
+                    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int c = 0; c < DC; ++c)
+                        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kr[i][c]),
+                                                                      __builtin_bit_cast(bf16x8, qb[c]), acc, 0, 0, 0);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        sc[i][r] = (colv && k0 + 4 * g + r < S.hi) ? acc[r] * scale : kNegInf;
+                        mx = fmaxf(mx, sc[i][r]);
+                    }
+                }
+            }
+            mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
+            mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+            const float corr = (mx == kNegInf) ? 1.f : expf(m - mx);
+            l *= corr;
+#pragma unroll
+            for (int d = 0; d < DB; ++d) o[d] *= corr;
+            m = mx;
+#pragma unroll
+            for (int i = 0; i < JB; i += 2) {
+                if (live[i] || live[i + 1]) {  // wave-uniform
+                    float pj[8];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        pj[r] = (mx == kNegInf) ? 0.f : expf(sc[i][r] - mx);
+                        pj[4 + r] = (mx == kNegInf) ? 0.f : expf(sc[i + 1][r] - mx);
+                        l += pj[r] + pj[4 + r];
+                    }
+#pragma unroll
+                    for (int c = 0; c < DC; ++c) {
+                        *reinterpret_cast<u32x4 *>(vt + c16 * VS + c * 32 + g * 8) =
+                            live[i] ? vr[i][c] : u32x4{0u, 0u, 0u, 0u};
+                        *reinterpret_cast<u32x4 *>(vt + (16 + c16) * VS + c * 32 + g * 8) =
+                            live[i + 1] ? vr[i + 1][c] : u32x4{0u, 0u, 0u, 0u};
+                    }
+                    uint32_t pb[4];
+#pragma unroll
+                    for (int h = 0; h < 4; ++h)
+                        pb[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{pj[2 * h], pj[2 * h + 1]}, bf16x2));
+                    const bf16x8 pbf = __builtin_bit_cast(bf16x8, u32x4{pb[0], pb[1], pb[2], pb[3]});
+                    const int q = c16 >> 2, pq = c16 & 3;
+#pragma unroll
+                    for (int d = 0; d < DB; ++d) {
+                        const bf16x4s lo = lds_read_tr16(vt + (4 * g + q) * VS + d * 16 + 4 * pq);
+                        const bf16x4s hi = lds_read_tr16(vt + (16 + 4 * g + q) * VS + d * 16 + 4 * pq);
+                        const bf16x8 va = __builtin_bit_cast(
+                            bf16x8, u32x4{__builtin_bit_cast(uint2, lo).x, __builtin_bit_cast(uint2, lo).y,
+                                          __builtin_bit_cast(uint2, hi).x, __builtin_bit_cast(uint2, hi).y});
+                        o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pbf, o[d], 0, 0, 0);
+                    }
+                }
+            }
+        }
+    };
+    run(s0, s_none);
+    if (!shared) run(sBp, s_none);
+    run(sAo, sBo);  // both rows' own keys: A's blocks, then B's, sharing rounds
+#undef SWH_PAIR_ISSUE
+#undef SWH_PAIR_BLOCK
+    l += __shfl_xor(l, 16, kWave);
+    l += __shfl_xor(l, 32, kWave);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    float *rec = red_s(wid, c16);
+#pragma unroll
+    for (int d = 0; d < DB; ++d)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rec[d * 16 + 4 * g + r] = o[d][r];
+    if (g == 0) {
+        rec[D] = m;
+        rec[D + 1] = l;
+    }
+    __syncthreads();
+    auto merged = [&](int h, int d) -> uint16_t {  // the waves' (m, l, acc) of column h, dim d
+        float mxw = kNegInf;
+#pragma unroll
+        for (int w2 = 0; w2 < NW; ++w2) mxw = fmaxf(mxw, red_s(w2, h)[D]);
+        float Ls = 0.f, A = 0.f;
+#pragma unroll
+        for (int w2 = 0; w2 < NW; ++w2) {
+            const float *rw = red_s(w2, h);
+            const float mq = rw[D];
+            if (mq == kNegInf) continue;
+            const float cq = expf(mq - mxw);
+            Ls = fmaf(rw[D + 1], cq, Ls);
+            A = fmaf(rw[d], cq, A);
+        }
+        return f32_to_bf16_bits(A / Ls);
+    };
+    const int nrow = hasB ? 2 : 1;
+    if (pf.ofrag) {
+        for (int idx = tid; idx < nrow * GQ * D; idx += NT) {  // GQ * D % 64 == 0: whole waves per row
+            const int h = idx / D, d = idx - h * D, r = h / GQ;
+            const uint32_t v = merged(h, d);
+            const uint32_t p2 = v | (__shfl_down(v, 1, kWave) << 16);
+            const uint32_t p4 = __shfl_down(p2, 2, kWave);
+            const uint32_t p6 = __shfl_down(p2, 4, kWave), p8 = __shfl_down(p2, 6, kWave);
+            if ((lane & 7) == 0)
+                *reinterpret_cast<uint4 *>(out + frag_at(bA + r, (kvh * GQ + h - r * GQ) * D + d, Hq * D)) =
+                    uint4{p2, p4, p6, p8};
+        }
+    } else {
+        for (int idx = tid; idx < nrow * GQ * D; idx += NT) {
+            const int h = idx / D, d = idx - h * D, r = h / GQ;
+            out[(bA + r) * (int64_t)Hq * D + (kvh * GQ + h - r * GQ) * D + d] = merged(h, d);
+        }
+    }
+}
+
 template <int D, int GQ>
 int launch_attn(const uint16_t *q, uint16_t *kc, uint16_t *vc, const float *rc, const float *rs, const int32_t *pl,
                 const int32_t *st, int64_t B, int Hq, int Hkv, int Tmax, float scale, uint16_t *o, hipStream_t s,
@@ -1584,6 +1875,15 @@ int launch_attn(const uint16_t *q, uint16_t *kc, uint16_t *vc, const float *rc, 
     if (pf.jobs) {
         extra = (pf.nwg + Hkv - 1) / Hkv;
         if (B + extra > 65535) extra = 0;
+    }
+    if constexpr (D == 128 && 2 * GQ <= 16) {
+        if (launch_policy().attn_pair) {  // row pairs: (B + 1) / 2 grid rows, then the warm-up rows
+            const int64_t pairs = (B + 1) / 2;
+            if (pairs + extra > 65535) extra = 0;
+            attn_decode_pair_kernel<D, GQ><<<dim3((unsigned)Hkv, (unsigned)(pairs + extra)), 512, 0, s>>>(
+                q, kc, vc, rc, rs, pl, st, Hq, Hkv, Tmax, scale, o, pf);
+            return launch_status();
+        }
     }
     attn_decode_kernel<D, GQ><<<dim3((unsigned)Hkv, (unsigned)(B + extra)), attn_threads(D), 0, s>>>(
         q, kc, vc, rc, rs, pl, st, Hq, Hkv, Tmax, scale, o, pf);

@@ -34,6 +34,7 @@ swh_launch_policy default_policy() {
     p.xstream = 1;
     p.lm_ring14 = 1;
     p.filt_wgs = 1024;
+    p.attn_pair = 1;
     return p;
 }
 std::mutex g_policy_mu;
@@ -76,7 +77,8 @@ extern "C" int swh_set_launch_policy(const swh_launch_policy *p) {
                   : (!in(p->gemm_cb, {1, 2, 4}) || p->gemm_s < 1 || p->gemm_s > 8 || !in(p->gemm_persist, {0, 1}) ||
                      !in(p->gemm_wn, {1, 2, 4}))) ||
         !in(p->gemm_tile, {0, 1}) || !in(p->gemm_nw, {0, 4, 8, 16}) || !in(p->xstream, {0, 1}) ||
-        !in(p->lm_ring14, {0, 1}) || p->filt_wgs < 64 || p->filt_wgs > 65536 || !in(p->wide_waves, {0, 6, 7, 8}))
+        !in(p->lm_ring14, {0, 1}) || p->filt_wgs < 64 || p->filt_wgs > 65536 || !in(p->wide_waves, {0, 6, 7, 8}) ||
+        !in(p->attn_pair, {0, 1}))
         return SWH_E_ARG;
     std::lock_guard<std::mutex> g(g_policy_mu);
     g_policy = *p;

@@ -152,8 +152,8 @@ def test_launch_policy_roundtrip_and_validation(lib):
     from swh_trl_amd import _lib
     d = _lib.LaunchPolicy()
     assert lib.swh_launch_policy_default(ctypes.byref(d)) == 0
-    assert (d.wide_kmin, d.wide_gemm, d.wide_smax, d.xstream, d.lm_ring14, d.filt_wgs, d.wide_waves) == \
-        (2048, 1, 8, 1, 1, 1024, 0)
+    assert (d.wide_kmin, d.wide_gemm, d.wide_smax, d.xstream, d.lm_ring14, d.filt_wgs, d.wide_waves,
+            d.attn_pair) == (2048, 1, 8, 1, 1, 1024, 0, 1)
     before = _lib.get_launch_policy()
     try:
         with _lib.launch_policy(gemm_cfg="4,2,1,1", xstream=0, wide_cb=2, wide_waves=7):
@@ -161,7 +161,7 @@ def test_launch_policy_roundtrip_and_validation(lib):
             assert (p["gemm_ms"], p["gemm_cb"], p["gemm_s"], p["gemm_persist"], p["gemm_wn"]) == (4, 2, 1, 1, 1)
             assert p["xstream"] == 0 and p["wide_cb"] == 2 and p["wide_waves"] == 7
         assert _lib.get_launch_policy() == before
-        for bad in ({"wide_smax": 9}, {"wide_cb": 3}, {"gemm_cfg": "3,1,1"}, {"gemm_nw": 5}, {"filt_wgs": 1}, {"wide_waves": 5},
+        for bad in ({"wide_smax": 9}, {"wide_cb": 3}, {"gemm_cfg": "3,1,1"}, {"gemm_nw": 5}, {"filt_wgs": 1}, {"wide_waves": 5}, {"attn_pair": 2},
                     {"gemm_cb": 2}):  # a geometry field without gemm_ms
             with pytest.raises(ValueError):
                 _lib.set_launch_policy(**bad)

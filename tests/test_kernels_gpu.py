@@ -883,6 +883,67 @@ def test_attn_decode_shared_prompt_rows(ops, dev, D, Hkv, G, P, step):
     assert torch.equal(a, c)
 
 
+@pytest.mark.parametrize("G,U,P,step,shared", [(8, 8, 256, 300, True), (8, 3, 64, 5, True), (3, 3, 33, 17, True),
+                                                (8, 2, 40, 9, False)])
+def test_attn_decode_pair_matches_per_row(ops, dev, G, U, P, step, shared, launch_policy):
+    """D = 128 row-pair attention (attn_pair: two rows per workgroup, a shared
+    prompt's keys read once for both) against one workgroup per row: the same
+    appended K/V slots bit for bit, outputs (row-major and fragment order) within
+    fp32 summation-order noise of each other and of the fp32 reference; odd row
+    counts and pairs straddling two groups (G 3) included; without prompt rows too."""
+    from swh_trl_amd import nn_ops
+    g = _gen(26)
+    D, Hkv, Hq = 128, 8, 32
+    B, Tmax = U * G, P + step + 8
+    plen = torch.tensor([max(1, P - (u * 7) % P) for u in range(U)], dtype=torch.int32).repeat_interleave(G).to(dev)
+    kc = torch.randn(B, Hkv, Tmax, D, generator=g).to(torch.bfloat16).to(dev)
+    vc = torch.randn(B, Hkv, Tmax, D, generator=g).to(torch.bfloat16).to(dev)
+    qkv = torch.randn(B, (Hq + 2 * Hkv) * D, generator=g).to(torch.bfloat16).to(dev)
+    cos, sin = _rope_tables(D, 4096, 5e5, dev)
+    state = torch.tensor([step + 1, P], dtype=torch.int32, device=dev)
+    prow = torch.arange(0, B, G, device=dev).repeat_interleave(G).to(torch.int32) if shared else None
+    res = {}
+    for pair in (1, 0):
+        launch_policy(attn_pair=pair)
+        k2, v2 = kc.clone(), vc.clone()
+        o = nn_ops.attn_decode(qkv, k2, v2, cos, sin, plen, state, Hq, Hkv, D, D ** -0.5, prompt_row=prow)
+        of = None
+        if B % 16 == 0:
+            k3, v3 = kc.clone(), vc.clone()
+            of = nn_ops.attn_decode(qkv, k3, v3, cos, sin, plen, state, Hq, Hkv, D, D ** -0.5, prompt_row=prow,
+                                    out_frag=True)
+            assert torch.equal(k3, k2) and torch.equal(v3, v2)
+        res[pair] = (o, of, k2, v2)
+    (o1, f1, k1, v1), (o0, f0, k0, v0) = res[1], res[0]
+    assert torch.equal(k1, k0) and torch.equal(v1, v0)
+    assert not torch.isnan(o1.float()).any()
+    # the keys meet the waves in another order: fp32 summation noise, then one bf16 rounding
+    torch.testing.assert_close(o1.float(), o0.float(), rtol=2e-2, atol=2e-2)
+    if f1 is not None:
+        torch.testing.assert_close(f1.float(), f0.float(), rtol=2e-2, atol=2e-2)
+    # fp32 reference of every row
+    slot = P + step
+    q = qkv[:, :Hq * D].view(B, Hq, D).float().cpu()
+    kn = qkv[:, Hq * D:(Hq + Hkv) * D].view(B, Hkv, D).float().cpu()
+    c, s_ = cos.cpu(), sin.cpu()
+    kfull, vfull = k1.float().cpu(), v1.float().cpu()
+    ref = torch.empty(B, Hq, D)
+    for b in range(B):
+        pl = int(plen[b])
+        pos = pl + step
+        cc, ss = torch.cat([c[pos], c[pos]]), torch.cat([s_[pos], s_[pos]])
+        rot = lambda x: torch.cat([-x[..., D // 2:], x[..., :D // 2]], -1)  # noqa: E731
+        qb = ((q[b] * cc).bfloat16().float() + (rot(q[b]) * ss).bfloat16().float()).bfloat16().float()
+        pr = int(prow[b]) if shared else b
+        keys = torch.cat([kfull[pr, :, P - pl:P], kfull[b, :, P:slot + 1]], 1)  # [Hkv, n, D]
+        vals = torch.cat([vfull[pr, :, P - pl:P], vfull[b, :, P:slot + 1]], 1)
+        kq = keys.repeat_interleave(Hq // Hkv, 0)
+        vq = vals.repeat_interleave(Hq // Hkv, 0)
+        att = torch.softmax((qb[:, None, :] * kq).sum(-1) * D ** -0.5, -1)
+        ref[b] = (att[..., None] * vq).sum(1)
+    torch.testing.assert_close(o1.float().cpu().view(B, Hq, D), ref, rtol=3e-2, atol=3e-2)
+
+
 @pytest.mark.parametrize("D,Hkv,Hq,B", [(64, 2, 14, 64), (128, 8, 32, 32)])
 def test_attn_decode_frag_output_feeds_o_proj(ops, dev, D, Hkv, Hq, B):
     """swh_attn_decode_shared_frag with out_frag = 1 writes exactly the row-major
