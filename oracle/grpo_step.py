@@ -114,9 +114,24 @@ def per_token_logps(model, prompt_ids, prompt_mask, completion_ids, completion_m
     return lp, ent
 
 
+def _rewards_per_func(reward_fn, ids, mask, reward_weights):
+    """grpo_trainer.py:1446-1498 + :1918: one column per reward function (a function's
+    None becomes NaN, :1485-1487), the weights of GRPOConfig.reward_weights (ones by
+    default).  `reward_fn` is one callable (ids, mask) -> list of floats, or a list of
+    them (several reward functions)."""
+    fns = list(reward_fn) if isinstance(reward_fn, (list, tuple)) else [reward_fn]
+    cols = [torch.tensor([float("nan") if x is None else float(x) for x in f(ids, mask)], dtype=torch.float32)
+            for f in fns]
+    w = torch.ones(len(fns)) if reward_weights is None else torch.tensor(reward_weights, dtype=torch.float32)
+    if w.numel() != len(fns):
+        raise ValueError("Number of reward weights must match number of reward functions")
+    return torch.stack(cols, 1), w
+
+
 def score_generation(model, g: dict, reward_fn: Callable, *, num_generations: int, temperature=1.0,
                      eos_token_id=None, scale_rewards=True, beta=0.0, ref_model=None, need_old: bool = False,
-                     per_device_train_batch_size: Optional[int] = None):
+                     per_device_train_batch_size: Optional[int] = None, mask_truncated_completions: bool = False,
+                     reward_weights=None):
     """The scoring half of _generate_and_score_completions (grpo_trainer.py:1812-1938) on a
     generation batch g = {prompt_ids, prompt_mask, completion_ids}: EOS mask, rewards,
     group advantages, the old-policy log-probs when the steps are not aligned with the
@@ -126,11 +141,15 @@ def score_generation(model, g: dict, reward_fn: Callable, *, num_generations: in
 
     Data parallel: g["world_completion_ids"] (every rank's completions in rank order, the
     accelerate gather of :1497) and g["rank"]: rewards and advantages are formed on the
-    global batch and this rank keeps its slice (:1914-1938)."""
+    global batch and this rank keeps its slice (:1914-1938).
+
+    mask_truncated_completions (:1829-1831): rows without EOS get an all-zero mask for
+    scoring and training; the lengths (:1826) and the reward functions' completion ids
+    (:1821-1823) are taken before that zeroing."""
     eos = eos_token_id if eos_token_id is not None else -1
     cids = g["completion_ids"]
     B = cids.shape[0]
-    mask, lengths, _ = trl_ref.completion_mask_from_eos(cids, eos)
+    mask, lengths, _ = trl_ref.completion_mask_from_eos(cids, eos, mask_truncated_completions)
     all_ids = g.get("world_completion_ids")
     if all_ids is None:
         all_ids, r0 = cids, 0
@@ -138,8 +157,8 @@ def score_generation(model, g: dict, reward_fn: Callable, *, num_generations: in
         r0 = int(g["rank"]) * B
         assert torch.equal(all_ids[r0:r0 + B], cids)
     all_mask, _, _ = trl_ref.completion_mask_from_eos(all_ids, eos)
-    rewards = torch.tensor([float(x) for x in reward_fn(all_ids, all_mask)], dtype=torch.float32).view(-1, 1)
-    adv, _, _, _, _ = trl_ref.group_advantages(rewards, torch.ones(1), num_generations, scale_rewards)
+    rpf, w = _rewards_per_func(reward_fn, all_ids, all_mask, reward_weights)
+    adv, rewards, _, _, _ = trl_ref.group_advantages(rpf, w, num_generations, scale_rewards)
     adv = adv[r0:r0 + B]
     bs = per_device_train_batch_size or B
 
@@ -159,7 +178,7 @@ def score_generation(model, g: dict, reward_fn: Callable, *, num_generations: in
             raise ValueError("beta != 0 needs ref_model")
         ref = scored(ref_model).cpu()
     return {"p": g["prompt_ids"], "pm": g["prompt_mask"], "c": cids, "cm": mask, "a": adv, "old": old, "ref": ref,
-            "rewards": rewards, "lengths": lengths}
+            "rewards": rewards.view(-1, 1), "rewards_per_func": rpf, "lengths": lengths}
 
 
 def grpo_train(model, optimizer, generations, reward_fn: Callable, *, num_generations: int, C: int,
@@ -167,7 +186,8 @@ def grpo_train(model, optimizer, generations, reward_fn: Callable, *, num_genera
                steps_per_generation: Optional[int] = None, num_iterations: int = 1, temperature=1.0,
                eos_token_id=None, beta=0.0, epsilon=0.2, epsilon_high=None, loss_type="bnpo",
                importance_sampling_level="token", scale_rewards=True, max_grad_norm=1.0, ref_model=None,
-               capture: bool = False):
+               delta=None, top_entropy_quantile: float = 1.0, mask_truncated_completions: bool = False,
+               reward_weights=None, capture: bool = False):
     """`n_steps` optimizer steps of the transformers Trainer around GRPOTrainer, with the
     reference's buffering (_prepare_inputs, grpo_trainer.py:1411-1444): a new generation
     every steps_per_generation * num_iterations micro-steps, shuffled (the permutation is
@@ -176,6 +196,13 @@ def grpo_train(model, optimizer, generations, reward_fn: Callable, *, num_genera
     log-probs enter when GA is not a multiple of that period (:1854-1869).  Each micro-batch
     is a separate forward/backward of loss / GA (model_accepts_loss_kwargs False), then
     clip_grad_norm_ and the optimizer step.
+
+    The GRPO knobs follow the reference where it applies them: epsilon_high and delta
+    (two-sided clipping, :2110-2118), top_entropy_quantile (:2079-2082: the per-micro-
+    batch quantile over the entropies that entropy_from_logits returns in the logits'
+    dtype, utils.py:1465-1490, i.e. bf16 entropies for a bf16 model),
+    mask_truncated_completions (:1829-1831), several reward functions with
+    reward_weights and None -> NaN (:1485-1487, :1918), scale_rewards (:1929-1930).
 
     generations: iterable of {prompt_ids, prompt_mask, completion_ids, perm} consumed when a
     generation is due.  Returns one dict per optimizer step: loss (sum of the micro losses /
@@ -188,14 +215,16 @@ def grpo_train(model, optimizer, generations, reward_fn: Callable, *, num_genera
     it = iter(generations)
     buffered, micro_step, gens, out = None, 0, [], []
     for _ in range(n_steps):
-        losses, lps = [], []
+        losses, lps, emasks = [], [], []
         for _ in range(GA):
             if micro_step % generate_every == 0 or buffered is None:
                 g = next(it)
                 sc = score_generation(model, g, reward_fn, num_generations=num_generations,
                                       temperature=temperature, eos_token_id=eos_token_id,
                                       scale_rewards=scale_rewards, beta=beta, ref_model=ref_model,
-                                      need_old=need_old, per_device_train_batch_size=per_device_train_batch_size)
+                                      need_old=need_old, per_device_train_batch_size=per_device_train_batch_size,
+                                      mask_truncated_completions=mask_truncated_completions,
+                                      reward_weights=reward_weights)
                 gens.append(sc)
                 keys = ("p", "pm", "c", "cm", "a", "old", "ref")
                 shuffled = trl_ref.permute_sequence_dict({k: sc[k] for k in keys}, g["perm"])
@@ -204,8 +233,13 @@ def grpo_train(model, optimizer, generations, reward_fn: Callable, *, num_genera
             mb = {k: (None if v is None else v.to(dev)) for k, v in buffered[micro_step % spg].items()}
             micro_step += 1
             lp, ent = per_token_logps(model, mb["p"], mb["pm"], mb["c"], mb["cm"], temperature)
+            emask = None
+            if top_entropy_quantile < 1.0:  # :2079-2082
+                emask = trl_ref.get_high_entropy_mask(ent, mb["cm"], 1 - top_entropy_quantile)
+                emasks.append(emask.cpu())
             loss, _ = trl_ref.grpo_loss(lp, mb["a"], mb["cm"], old_per_token_logps=mb["old"],
-                                        ref_per_token_logps=mb["ref"], entropies=ent, beta=beta,
+                                        ref_per_token_logps=mb["ref"], entropy_mask=emask, entropies=ent,
+                                        beta=beta, delta=delta,
                                         epsilon_low=epsilon, epsilon_high=epsilon_high or epsilon,
                                         loss_type=loss_type, importance_sampling_level=importance_sampling_level,
                                         max_completion_length=C)
@@ -220,6 +254,8 @@ def grpo_train(model, optimizer, generations, reward_fn: Callable, *, num_genera
         rec = {"loss": sum(losses), "grad_norm": float(total), "losses": losses}
         if capture:
             rec.update(logps=torch.cat(lps), grads=grads)
+            if emasks:
+                rec["entropy_mask"] = torch.cat(emasks)
         out.append(rec)
     if out:
         out[0]["gens"] = gens

@@ -1617,21 +1617,24 @@ __global__ __launch_bounds__(512) void attn_decode_pair_kernel(
     }
     const int step = state[0] - 1, P = state[1];
     const int slot_new = P + step;
-    const int64_t bA = 2 * (int64_t)blockIdx.y;
-    const bool hasB = bA + 1 < pf.rows;
-    const int64_t bB = hasB ? bA + 1 : bA;
-    const int plA = plen[bA], plB = plen[bB];
-    const bool okA = !(step < 0 || slot_new >= Tmax || plA < 0 || plA > P);
-    const bool okB = hasB && !(step < 0 || slot_new >= Tmax || plB < 0 || plB > P);
-    if (!okA || (hasB && !okB)) {  // never write outside the cache: NaN rows, fail loudly
-        for (int r = 0; r < (hasB ? 2 : 1); ++r) {
-            const int64_t b = bA + r;
-            for (int idx = tid; idx < GQ * D; idx += NT)
-                out[pf.ofrag ? frag_at(b, kvh * GQ * D + idx, Hq * D) : b * (int64_t)Hq * D + kvh * GQ * D + idx] =
-                    0x7fc0;
-        }
-        return;
+    // never write outside the cache: a row with an out-of-range length or step gets NaN
+    // (fails loudly) and no KV append; its partner row still runs, alone
+    const int64_t b0 = 2 * (int64_t)blockIdx.y;
+    const bool has1 = b0 + 1 < pf.rows;
+    const int pl0 = plen[b0], pl1 = has1 ? plen[b0 + 1] : 0;
+    const bool ok0 = !(step < 0 || slot_new >= Tmax || pl0 < 0 || pl0 > P);
+    const bool ok1 = has1 && !(step < 0 || slot_new >= Tmax || pl1 < 0 || pl1 > P);
+    for (int r = 0; r < (has1 ? 2 : 1); ++r) {
+        if (r ? ok1 : ok0) continue;
+        const int64_t b = b0 + r;
+        for (int idx = tid; idx < GQ * D; idx += NT)
+            out[pf.ofrag ? frag_at(b, kvh * GQ * D + idx, Hq * D) : b * (int64_t)Hq * D + kvh * GQ * D + idx] = 0x7fc0;
     }
+    if (!ok0 && !ok1) return;
+    const int64_t bA = ok0 ? b0 : b0 + 1;
+    const bool hasB = ok0 && ok1;
+    const int64_t bB = hasB ? bA + 1 : bA;
+    const int plA = ok0 ? pl0 : pl1, plB = hasB ? pl1 : plA;
     const int64_t prA = pf.prow ? (int64_t)min(max(pf.prow[bA], 0), pf.rows - 1) : bA;
     const int64_t prB = pf.prow ? (int64_t)min(max(pf.prow[bB], 0), pf.rows - 1) : bB;
     const bool shared = hasB && prA == prB && plA == plB && plA > 0;  // one prompt for both rows
@@ -1812,6 +1815,7 @@ __global__ __launch_bounds__(512) void attn_decode_pair_kernel(
         }
     };
     run(s0, s_none);
+    first = false;  // s0 may be empty (a zero-length prompt): the next run issues its own first round
     if (!shared) run(sBp, s_none);
     run(sAo, sBo);  // both rows' own keys: A's blocks, then B's, sharing rounds
 #undef SWH_PAIR_ISSUE

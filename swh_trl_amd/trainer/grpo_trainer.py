@@ -527,8 +527,15 @@ class GRPOTrainer:
         if width < completion_ids.shape[1]:
             completion_ids = completion_ids[:, :width].contiguous()
             completion_mask = completion_mask[:, :width].contiguous()
+        # the reward functions see each completion up to its first EOS even when
+        # mask_truncated_completions zeroes the row's training mask: the reference builds
+        # completion_ids_list (:1821-1823) before the zeroing (:1829-1831)
+        reward_mask = completion_mask
+        if self.mask_truncated_completions:
+            reward_mask = (torch.arange(completion_ids.shape[1], device=self.device)[None, :]
+                           < lengths[:, None]).to(torch.int32)
         rewards_per_func = self._calculate_rewards(examples, prompts_text, prompt_ids, prompt_mask, completion_ids,
-                                                   completion_mask)
+                                                   reward_mask)
         _trace("rewards")
         # grpo_trainer.py:1494-1497 / :1933-1938: the rewards of every rank are gathered
         # (a group of G completions may straddle ranks), the advantages are formed on
@@ -794,11 +801,17 @@ class GRPOTrainer:
             r0 += r
         emask = None
         if self.top_entropy_quantile < 1.0:
+            # :2079-2082, per micro-batch (segment).  The reference thresholds the entropies
+            # entropy_from_logits returns in the logits' dtype (utils.py:1465-1490): for a bf16
+            # model those are bf16 values, whose ties decide which tokens sit at the quantile,
+            # so the fp32 entropies of the fused kernel are rounded to the model dtype first
+            from . import utils as _u
+            ent_q = ent.to(self.model.dtype) if self.model.dtype != torch.float32 else ent
             emask = torch.zeros_like(batch["completion_mask"], dtype=torch.bool)
-            from .utils import get_high_entropy_mask
             for j in range(len(micro)):
                 sl = seg == j
-                emask[sl] = get_high_entropy_mask(ent[sl], batch["completion_mask"][sl], 1 - self.top_entropy_quantile)
+                emask[sl] = _u.get_high_entropy_mask(ent_q[sl], batch["completion_mask"][sl],
+                                                     1 - self.top_entropy_quantile)
         kw = dict(old_per_token_logps=batch.get("old_per_token_logps"),
                   ref_per_token_logps=batch.get("ref_per_token_logps"), entropy_mask=emask, entropies=ent,
                   row_scale=row_scale, segments=seg, num_segments=len(micro), beta=self.beta,

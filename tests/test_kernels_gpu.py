@@ -883,19 +883,27 @@ def test_attn_decode_shared_prompt_rows(ops, dev, D, Hkv, G, P, step):
     assert torch.equal(a, c)
 
 
-@pytest.mark.parametrize("G,U,P,step,shared", [(8, 8, 256, 300, True), (8, 3, 64, 5, True), (3, 3, 33, 17, True),
-                                                (8, 2, 40, 9, False)])
-def test_attn_decode_pair_matches_per_row(ops, dev, G, U, P, step, shared, launch_policy):
+@pytest.mark.parametrize("G,U,P,step,shared,zero", [(8, 8, 256, 300, True, False), (8, 3, 64, 5, True, False),
+                                                     (3, 3, 33, 17, True, False), (8, 2, 40, 9, False, False),
+                                                     (3, 3, 33, 17, True, True), (8, 2, 40, 9, False, True)])
+def test_attn_decode_pair_matches_per_row(ops, dev, G, U, P, step, shared, zero, launch_policy):
     """D = 128 row-pair attention (attn_pair: two rows per workgroup, a shared
     prompt's keys read once for both) against one workgroup per row: the same
     appended K/V slots bit for bit, outputs (row-major and fragment order) within
     fp32 summation-order noise of each other and of the fp32 reference; odd row
-    counts and pairs straddling two groups (G 3) included; without prompt rows too."""
+    counts and pairs straddling two groups (G 3) included; without prompt rows too.
+    zero: zero-length prompts (the first group's, or row 0 alone beside a row that
+    has a prompt), whose first key segment is empty."""
     from swh_trl_amd import nn_ops
     g = _gen(26)
     D, Hkv, Hq = 128, 8, 32
     B, Tmax = U * G, P + step + 8
     plen = torch.tensor([max(1, P - (u * 7) % P) for u in range(U)], dtype=torch.int32).repeat_interleave(G).to(dev)
+    if zero:
+        if shared:
+            plen[:G] = 0
+        else:
+            plen[0] = 0
     kc = torch.randn(B, Hkv, Tmax, D, generator=g).to(torch.bfloat16).to(dev)
     vc = torch.randn(B, Hkv, Tmax, D, generator=g).to(torch.bfloat16).to(dev)
     qkv = torch.randn(B, (Hq + 2 * Hkv) * D, generator=g).to(torch.bfloat16).to(dev)
@@ -942,6 +950,37 @@ def test_attn_decode_pair_matches_per_row(ops, dev, G, U, P, step, shared, launc
         att = torch.softmax((qb[:, None, :] * kq).sum(-1) * D ** -0.5, -1)
         ref[b] = (att[..., None] * vq).sum(1)
     torch.testing.assert_close(o1.float().cpu().view(B, Hq, D), ref, rtol=3e-2, atol=3e-2)
+
+
+def test_attn_decode_pair_bad_row_poisons_only_itself(ops, dev, launch_policy):
+    """A row whose prompt length is out of range gets NaN and no KV append; its
+    pair partner runs alone and equals the per-row kernel's result (rows 2 and 5
+    bad: the first and the second row of a pair)."""
+    from swh_trl_amd import nn_ops
+    g = _gen(27)
+    D, Hkv, Hq, B, P, step = 128, 8, 32, 8, 40, 9
+    Tmax = P + step + 8
+    plen = torch.tensor([40, 33, 41, 20, 7, -1, 40, 1], dtype=torch.int32, device=dev)
+    kc = torch.randn(B, Hkv, Tmax, D, generator=g).to(torch.bfloat16).to(dev)
+    vc = torch.randn(B, Hkv, Tmax, D, generator=g).to(torch.bfloat16).to(dev)
+    qkv = torch.randn(B, (Hq + 2 * Hkv) * D, generator=g).to(torch.bfloat16).to(dev)
+    cos, sin = _rope_tables(D, 4096, 5e5, dev)
+    state = torch.tensor([step + 1, P], dtype=torch.int32, device=dev)
+    res = {}
+    for pair in (1, 0):
+        launch_policy(attn_pair=pair)
+        k2, v2 = kc.clone(), vc.clone()
+        o = nn_ops.attn_decode(qkv, k2, v2, cos, sin, plen, state, Hq, Hkv, D, D ** -0.5)
+        res[pair] = (o.float().cpu().view(B, Hq, D), k2.cpu(), v2.cpu())
+    (o1, k1, v1), (o0, k0, v0) = res[1], res[0]
+    bad = torch.tensor([False, False, True, False, False, True, False, False])
+    assert bool(o1[bad].isnan().all()) and bool(o0[bad].isnan().all())
+    assert not bool(o1[~bad].isnan().any())
+    torch.testing.assert_close(o1[~bad], o0[~bad], rtol=2e-2, atol=2e-2)
+    assert torch.equal(k1, k0) and torch.equal(v1, v0)
+    slot = P + step
+    assert torch.equal(k1[bad][:, :, slot], kc.cpu()[bad][:, :, slot])  # no append for the bad rows
+    assert not torch.equal(k1[~bad][:, :, slot], kc.cpu()[~bad][:, :, slot])
 
 
 @pytest.mark.parametrize("D,Hkv,Hq,B", [(64, 2, 14, 64), (128, 8, 32, 32)])

@@ -85,3 +85,57 @@ def test_grpo_step_is_one_step_of_the_loop():
     assert loss1 == rec["loss"] and torch.equal(out1["logps"], rec["logps"])
     for (k, a), b in zip(m1.named_parameters(), m2.parameters()):
         assert torch.equal(a, b), k
+
+
+def _reward_none(cids, cmask):
+    return [None if i % 3 == 0 else float(m.sum()) for i, m in enumerate(cmask)]
+
+
+def test_knobs_mask_truncated_rewards_and_weights():
+    """mask_truncated_completions (grpo_trainer.py:1829-1831) zeroes the rows without
+    EOS after the lengths and the reward functions' ids were taken (:1821-1826);
+    several reward functions are weighted and nan-summed (:1918), None -> NaN."""
+    cfg = tiny_qwen2(128, 1)
+    G, P, C, MB, GA = 4, 6, 10, 4, 2
+    m, opt = _model(cfg)
+    g = _gen(0, MB * GA, G, P, C, cfg.vocab_size)
+    recs = og.grpo_train(m, opt, [g], [_reward, _reward_none], num_generations=G, C=C,
+                         per_device_train_batch_size=MB, gradient_accumulation_steps=GA, n_steps=1,
+                         eos_token_id=EOS, mask_truncated_completions=True, reward_weights=[1.0, 0.25],
+                         scale_rewards=False, capture=True)
+    sc = recs[0]["gens"][0]
+    has_eos = (g["completion_ids"] == EOS).any(1)
+    assert torch.equal(sc["cm"].sum(1) > 0, has_eos) and int(has_eos.sum()) == 1
+    assert int(sc["lengths"][0]) == 6 and bool((sc["lengths"][1:] == C).all())  # lengths before the zeroing
+    rpf = sc["rewards_per_func"]
+    assert bool(rpf[0::3, 1].isnan().all()) and torch.equal(rpf[1::3, 1], torch.full_like(rpf[1::3, 1], float(C)))
+    r = torch.nansum(rpf * torch.tensor([1.0, 0.25]), 1)
+    torch.testing.assert_close(sc["rewards"].view(-1), r)
+    adv = r - r.view(-1, G).mean(1).repeat_interleave(G)  # scale_rewards=False (:1929-1930)
+    torch.testing.assert_close(sc["a"], adv)
+
+
+def test_knobs_entropy_mask_and_clipping_defaults():
+    """top_entropy_quantile 1.0 / delta None / epsilon_high None are the default loop;
+    top_entropy_quantile q keeps about (1 - q) of each micro-batch's valid tokens; a
+    delta above every ratio changes nothing."""
+    cfg = tiny_qwen2(128, 1)
+    G, P, C, MB, GA = 4, 6, 10, 4, 2
+    g = _gen(2, MB * GA, G, P, C, cfg.vocab_size)
+
+    def run(**kw):
+        m, opt = _model(cfg)
+        return og.grpo_train(m, opt, [g], _reward, num_generations=G, C=C, per_device_train_batch_size=MB,
+                             gradient_accumulation_steps=GA, n_steps=2, num_iterations=2, eos_token_id=EOS,
+                             capture=True, **kw)
+    base = run()
+    same = run(top_entropy_quantile=1.0, delta=1e9, epsilon_high=0.2)
+    for a, b in zip(base, same):
+        assert a["loss"] == b["loss"] and "entropy_mask" not in a and "entropy_mask" not in b
+    q = run(top_entropy_quantile=0.25)
+    em = q[0]["entropy_mask"]
+    frac = em.float().sum() / (MB * GA * C - 4)  # row 0 of the rollout stops at its EOS (token 5)
+    assert 0.2 <= float(frac) <= 0.35, float(frac)
+    assert q[0]["loss"] != base[0]["loss"]
+    clipped = run(delta=1.0001, epsilon=0.01)
+    assert clipped[1]["loss"] != base[1]["loss"]

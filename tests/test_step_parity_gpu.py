@@ -80,7 +80,7 @@ def _weights(model):
 
 
 def product_run(cfg, dtype, n_steps, *, std, lr, G=4, P=12, C=24, MB=8, GA=2, seed=11, n_prompts=None,
-                min_new_tokens=4, gen_extra=None, **grpo_kw):
+                min_new_tokens=4, gen_extra=None, reward_funcs=None, **grpo_kw):
     """n_steps GRPOTrainer optimizer steps; captures every generation (its
     output and the shuffle permutation drawn after it), every training pass's
     log-probs, and the loss / grad norm / gradients / weights of every step."""
@@ -102,10 +102,10 @@ def product_run(cfg, dtype, n_steps, *, std, lr, G=4, P=12, C=24, MB=8, GA=2, se
                                          **(gen_extra or {})},
                       **grpo_kw)
     model = CausalLM(cfg, dev, seed=3, init_std=std, dtype=dtype)
-    tr = GRPOTrainer(model=model, reward_funcs=_reward_product, args=args, train_dataset=ds)
+    tr = GRPOTrainer(model=model, reward_funcs=reward_funcs or _reward_product, args=args, train_dataset=ds)
     assert tr.model.dtype == dtype
     w0 = _weights(tr.model)
-    cap = {"gens": [], "logps": [], "masks": []}
+    cap = {"gens": [], "logps": [], "masks": [], "emasks": []}
     gen_fn = tr._generate_and_score_completions
 
     def gen_capture(examples):
@@ -125,25 +125,23 @@ def product_run(cfg, dtype, n_steps, *, std, lr, G=4, P=12, C=24, MB=8, GA=2, se
             cap["masks"].append(batch["completion_mask"].detach().cpu().clone())
         return lp, ent
 
+    from swh_trl_amd import ops as _ops
+    loss_fn = _ops.grpo_loss
+
+    def loss_capture(logp, adv, cmask, **kw):  # the entropy mask the trainer hands the loss kernel
+        if kw.get("entropy_mask") is not None:
+            cap["emasks"].append(kw["entropy_mask"].detach().cpu().clone())
+        return loss_fn(logp, adv, cmask, **kw)
+
     tr._generate_and_score_completions = gen_capture
     tr._completion_logps = lp_capture
+    _ops.grpo_loss = loss_capture
     steps = []
-    for _ in range(n_steps):
-        out = tr.training_step_group()
-        torch.cuda.synchronize()
-        # old-policy log-probs scored by the training pass itself (the policy had not stepped
-        # since the generation) live in the buffered micro-batches: back to generation order
-        for mb in tr._buffered_inputs or []:
-            if "old_per_token_logps" in mb and "_row_index" in mb:
-                for ri, row in zip(mb["_row_index"].tolist(), mb["old_per_token_logps"].detach().cpu()):
-                    g = cap["gens"][ri // mb["completion_ids"].shape[0] // spg]
-                    if "old_per_token_logps" not in g:
-                        g["old_per_token_logps"] = torch.zeros(g["completion_ids"].shape)
-                    g["old_per_token_logps"][ri % g["completion_ids"].shape[0]] = row
-        steps.append({"loss": float(out["loss"]), "grad_norm": float(out["grad_norm"]),
-                      "grads": _grads_by_name(tr.model), "w": _weights(tr.model),
-                      "logps": cap["logps"][-1], "mask": cap["masks"][-1],
-                      "seg_metrics": tr._metrics["train"]["_met"][-1].detach().cpu().clone()})
+    try:
+        for _ in range(n_steps):
+            steps.append(_product_step(tr, cap, spg))
+    finally:
+        _ops.grpo_loss = loss_fn
     hip_attn = tr.model._hip_attn
     eng = tr._engine
     engine = {"B": eng.B, "fused_sample": bool(getattr(eng, "fused", False) and eng._fused_sample()),
@@ -154,7 +152,28 @@ def product_run(cfg, dtype, n_steps, *, std, lr, G=4, P=12, C=24, MB=8, GA=2, se
             "geometry": dict(G=G, C=C, MB=MB, GA=GA)}
 
 
-def oracle_run(cfg, w0, dtype, prod, n_steps, *, lr, beta=0.0, loss_type="bnpo", device="cpu", **grpo_kw):
+def _product_step(tr, cap, spg):
+    """One optimizer step of the trainer and what the checks compare."""
+    out = tr.training_step_group()
+    torch.cuda.synchronize()
+    # old-policy log-probs scored by the training pass itself (the policy had not stepped
+    # since the generation) live in the buffered micro-batches: back to generation order
+    for mb in tr._buffered_inputs or []:
+        if "old_per_token_logps" in mb and "_row_index" in mb:
+            for ri, row in zip(mb["_row_index"].tolist(), mb["old_per_token_logps"].detach().cpu()):
+                g = cap["gens"][ri // mb["completion_ids"].shape[0] // spg]
+                if "old_per_token_logps" not in g:
+                    g["old_per_token_logps"] = torch.zeros(g["completion_ids"].shape)
+                g["old_per_token_logps"][ri % g["completion_ids"].shape[0]] = row
+    return {"loss": float(out["loss"]), "grad_norm": float(out["grad_norm"]),
+            "grads": _grads_by_name(tr.model), "w": _weights(tr.model),
+            "logps": cap["logps"][-1], "mask": cap["masks"][-1],
+            "emask": cap["emasks"][-1] if cap["emasks"] else None,
+            "seg_metrics": tr._metrics["train"]["_met"][-1].detach().cpu().clone()}
+
+
+def oracle_run(cfg, w0, dtype, prod, n_steps, *, lr, beta=0.0, loss_type="bnpo", device="cpu", reward_fn=None,
+               **grpo_kw):
     """The reference loop (oracle/grpo_step.py grpo_train) in `dtype` — on the host, or
     for the 8B width with torch's own device kernels (the same restatement; the host
     would take minutes) — from the product's initial weights, over its rollouts."""
@@ -170,7 +189,7 @@ def oracle_run(cfg, w0, dtype, prod, n_steps, *, lr, beta=0.0, loss_type="bnpo",
     opt = torch.optim.AdamW(hf.parameters(), lr=lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, foreach=False)
     gens = [{"prompt_ids": g["prompt_ids"], "prompt_mask": g["prompt_mask"].long(),
              "completion_ids": g["completion_ids"], "perm": g["perm"]} for g in prod["gens"]]
-    recs = og.grpo_train(hf, opt, gens, _reward_oracle, num_generations=geo["G"], C=geo["C"],
+    recs = og.grpo_train(hf, opt, gens, reward_fn or _reward_oracle, num_generations=geo["G"], C=geo["C"],
                          per_device_train_batch_size=geo["MB"], gradient_accumulation_steps=geo["GA"],
                          n_steps=n_steps, eos_token_id=EOS, beta=beta, loss_type=loss_type, ref_model=ref,
                          capture=True, **grpo_kw)
@@ -439,3 +458,91 @@ def test_bench_layout_bf16_step_matches_oracle():
     orc_bf = oracle_run(cfg, prod["w0"], torch.bfloat16, prod, 1, lr=lr, device="cuda:0")
     orc_32 = oracle_run(cfg, prod["w0"], torch.float32, prod, 1, lr=lr, device="cuda:0")
     _check_bf16("bench-layout-0.5b-width", prod, orc_bf, orc_32)
+
+
+# ---------------------------------------------------------------------------------------------
+# The GRPO knobs the default configuration leaves off, through the trainer's own wiring
+# (grpo_trainer.py:1829-1831 mask_truncated_completions, :1485-1487 None -> NaN, :1918 reward
+# weights, :1929-1930 scale_rewards, :2079-2082 top_entropy_quantile, :2110-2118 epsilon_high
+# and delta), two optimizer steps over one buffered rollout (num_iterations 2), so the second
+# step's ratios leave 1 and the clipping bites.
+# ---------------------------------------------------------------------------------------------
+
+def _reward_len_product(prompts=None, completions=None, completion_ids=None, **kw):
+    # the completion's length up to its first EOS: a truncated row counts its full width in the
+    # reference (completion_ids_list is built before mask_truncated_completions, :1821-1831);
+    # None for some rows (nansum over the weighted functions, :1918)
+    return [None if sum(c) % 4 == 0 else float(len(c) % 5) for c in completion_ids]
+
+
+def _reward_len_oracle(cids, cmask):
+    out = []
+    for r, m in zip(cids, cmask):
+        c = r[m.bool()].tolist()
+        out.append(None if sum(c) % 4 == 0 else float(len(c) % 5))
+    return out
+
+
+KNOBS = dict(num_iterations=2, top_entropy_quantile=0.7, delta=1.04, epsilon=0.02, epsilon_high=0.03,
+             mask_truncated_completions=True, reward_weights=[1.0, 0.5], scale_rewards=False)
+
+
+def _knob_runs(cfg, dtype, *, std, lr, device="cpu", **kw):
+    prod = product_run(cfg, dtype, 2, std=std, lr=lr, reward_funcs=[_reward_product, _reward_len_product],
+                       **KNOBS, **kw)
+    orcs = []
+    for od in ([torch.float32] if dtype == torch.float32 else [torch.bfloat16, torch.float32]):
+        orcs.append(oracle_run(cfg, prod["w0"], od, prod, 2, lr=lr, device=device,
+                               reward_fn=[_reward_oracle, _reward_len_oracle], **KNOBS))
+    g = prod["gens"][0]
+    cm, has_eos = g["completion_mask"], (g["completion_ids"] == EOS).any(1)
+    # the knobs are exercised: some rows truncated (all-zero mask), some not; some rewards None
+    assert bool((cm.sum(1) == 0).any()) and bool((cm.sum(1) > 0).any()), cm.sum(1)
+    assert torch.equal(cm.sum(1) > 0, has_eos)
+    rpf = orcs[0][0]["gens"][0]["rewards_per_func"]
+    assert bool(rpf[:, 1].isnan().any()) and bool((~rpf[:, 1].isnan()).any())
+    # the entropy mask keeps roughly the top 30 % of each micro-batch's valid tokens
+    for st in prod["steps"]:
+        assert st["emask"] is not None and st["emask"].shape == st["mask"].shape
+        assert not bool((st["emask"] & ~st["mask"].bool()).any())
+    # clipping happened in the second step (ratios moved past 1 -/+ epsilon)
+    clip = prod["steps"][1]["seg_metrics"][:, 3:6].sum().item()
+    return prod, orcs, clip
+
+
+def test_grpo_knobs_fp32_matches_oracle():
+    """Every knob on, fp32 (vocabulary 16 so about a third of the rows stop at EOS): masks,
+    advantages, the entropy masks, log-probs, losses, gradients and weights against the
+    oracle loop within the fp32 bounds of _check_fp32."""
+    from swh_trl_amd.engine.config import tiny_qwen2
+    cfg = tiny_qwen2(16, 2)
+    lr = 1e-2
+    prod, (orc,), clip = _knob_runs(cfg, torch.float32, std=0.05, lr=lr)
+    assert clip > 0, clip
+    for s, (st, o) in enumerate(zip(prod["steps"], orc)):
+        assert torch.equal(st["emask"], o["entropy_mask"].bool()), (s, (st["emask"] ^ o["entropy_mask"]).sum())
+    _check_fp32("knobs-fp32", prod, orc, lr)
+
+
+def test_grpo_knobs_bf16_benched_path_matches_oracle():
+    """Every knob on the benched bf16 path (Qwen2.5-0.5B width, 2 layers, HIP training
+    attention, shared-prompt forward, fused lm-head log-prob) with a 64-token vocabulary
+    so that rows stop at EOS.  The entropy quantile runs on bf16 entropies as the
+    reference's does; ties at the threshold can still differ from the reference's bf16
+    arithmetic, so the entropy-masked set is bounded by the reference's own bf16-vs-fp32
+    difference: |M_prod xor M_bf16| <= 2 |M_bf16 xor M_fp32| + 1 % of the valid tokens.
+    Log-probs, losses and gradients within _check_bf16's bounds."""
+    import dataclasses
+    from swh_trl_amd.engine.config import DecoderConfig
+    cfg = dataclasses.replace(DecoderConfig(num_hidden_layers=2), vocab_size=64)
+    lr = 2e-3
+    prod, (orc_bf, orc_32), clip = _knob_runs(cfg, torch.bfloat16, std=0.02, lr=lr, device="cuda:0")
+    assert prod["hip_attn"]
+    print("knobs-bf16 clip sums step 2:", clip)
+    for s, (st, ob, o32) in enumerate(zip(prod["steps"], orc_bf, orc_32)):
+        valid = int(st["mask"].sum())
+        d_pb = int((st["emask"] ^ ob["entropy_mask"].bool()).sum())
+        d_ref = int((ob["entropy_mask"].bool() ^ o32["entropy_mask"].bool()).sum())
+        print(f"step {s}: entropy-mask differences product/bf16 {d_pb}, bf16/fp32 {d_ref}, valid {valid}")
+        assert d_pb <= 2 * d_ref + 0.01 * valid, (s, d_pb, d_ref, valid)
+    _check_bf16("knobs-bf16-0.5b-width", prod, orc_bf, orc_32)
