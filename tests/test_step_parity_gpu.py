@@ -483,7 +483,7 @@ def _reward_len_oracle(cids, cmask):
     return out
 
 
-KNOBS = dict(num_iterations=2, top_entropy_quantile=0.7, delta=1.04, epsilon=0.02, epsilon_high=0.03,
+KNOBS = dict(num_iterations=2, top_entropy_quantile=0.7, delta=1.015, epsilon=0.008, epsilon_high=0.012,
              mask_truncated_completions=True, reward_weights=[1.0, 0.5], scale_rewards=False)
 
 
@@ -516,7 +516,7 @@ def test_grpo_knobs_fp32_matches_oracle():
     oracle loop within the fp32 bounds of _check_fp32."""
     from swh_trl_amd.engine.config import tiny_qwen2
     cfg = tiny_qwen2(16, 2)
-    lr = 1e-2
+    lr = 3e-3
     prod, (orc,), clip = _knob_runs(cfg, torch.float32, std=0.05, lr=lr)
     assert clip > 0, clip
     for s, (st, o) in enumerate(zip(prod["steps"], orc)):
