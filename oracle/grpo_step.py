@@ -187,7 +187,7 @@ def grpo_train(model, optimizer, generations, reward_fn: Callable, *, num_genera
                eos_token_id=None, beta=0.0, epsilon=0.2, epsilon_high=None, loss_type="bnpo",
                importance_sampling_level="token", scale_rewards=True, max_grad_norm=1.0, ref_model=None,
                delta=None, top_entropy_quantile: float = 1.0, mask_truncated_completions: bool = False,
-               reward_weights=None, capture: bool = False):
+               reward_weights=None, micro_steps_per_epoch: Optional[int] = None, capture: bool = False):
     """`n_steps` optimizer steps of the transformers Trainer around GRPOTrainer, with the
     reference's buffering (_prepare_inputs, grpo_trainer.py:1411-1444): a new generation
     every steps_per_generation * num_iterations micro-steps, shuffled (the permutation is
@@ -204,6 +204,11 @@ def grpo_train(model, optimizer, generations, reward_fn: Callable, *, num_genera
     mask_truncated_completions (:1829-1831), several reward functions with
     reward_weights and None -> NaN (:1485-1487, :1918), scale_rewards (:1929-1930).
 
+    micro_steps_per_epoch (len of the train dataloader): the transformers Trainer ends an
+    epoch whose micro-batches are not a multiple of GA with an update over the remainder,
+    each micro loss divided by that remainder (trainer.py _run_epoch: `remainder`,
+    current_gradient_accumulation_steps; training_step's loss / it).
+
     generations: iterable of {prompt_ids, prompt_mask, completion_ids, perm} consumed when a
     generation is due.  Returns one dict per optimizer step: loss (sum of the micro losses /
     GA), grad_norm, and with capture the micro-batch log-probs in training order ("logps"),
@@ -216,7 +221,8 @@ def grpo_train(model, optimizer, generations, reward_fn: Callable, *, num_genera
     buffered, micro_step, gens, out = None, 0, [], []
     for _ in range(n_steps):
         losses, lps, emasks = [], [], []
-        for _ in range(GA):
+        n_acc = GA if not micro_steps_per_epoch else min(GA, micro_steps_per_epoch - micro_step % micro_steps_per_epoch)
+        for _ in range(n_acc):
             if micro_step % generate_every == 0 or buffered is None:
                 g = next(it)
                 sc = score_generation(model, g, reward_fn, num_generations=num_generations,
@@ -243,8 +249,8 @@ def grpo_train(model, optimizer, generations, reward_fn: Callable, *, num_genera
                                         epsilon_low=epsilon, epsilon_high=epsilon_high or epsilon,
                                         loss_type=loss_type, importance_sampling_level=importance_sampling_level,
                                         max_completion_length=C)
-            (loss / GA).backward()
-            losses.append(float(loss.detach()) / GA)
+            (loss / n_acc).backward()
+            losses.append(float(loss.detach()) / n_acc)
             lps.append(lp.detach().cpu())
         grads = ({n: p.grad.detach().cpu().clone() for n, p in model.named_parameters() if p.grad is not None}
                  if capture else None)

@@ -586,13 +586,13 @@ class GRPOTrainer:
         k3 KL is exactly 0 and the first ratio exactly 1, as in the reference); the
         others need the generation-time pass.  Generation slot j (of
         steps_per_generation) is first used at micro-step k0 + j, in optimizer step
-        (k0 + j) // GA."""
+        _update_index(k0 + j) (GA micro-steps per update, the epoch's last one shorter)."""
         a = self.args
         if mode != "train":
             return False, False
-        GA = a.gradient_accumulation_steps
-        k0, s0 = self._step, self._step // GA
-        slot_steps = [(k0 + j) // GA for j in range(a.steps_per_generation)]
+        k0 = self._step
+        s0 = self._update_index(k0)
+        slot_steps = [self._update_index(k0 + j) for j in range(a.steps_per_generation)]
         eager_old = self._needs_old_logps() and any(st != s0 for st in slot_steps)
         eager_ref = False
         if self.beta != 0.0 and a.sync_ref_model:
@@ -733,15 +733,16 @@ class GRPOTrainer:
         return lp
 
     # ------------------------------------------------------------------ loss over fused micro-batches
-    def _loss_backward(self, micro: list[dict], train: bool = True) -> dict:
+    def _loss_backward(self, micro: list[dict], train: bool = True, accum: Optional[int] = None) -> dict:
         """One forward/backward over the given micro-batches.  Segment j keeps
         micro-batch j's own normaliser (bnpo tokens / grpo rows), every row is
         scaled by 1/GA as the Trainer's loss division — the gradient equals the
-        reference's GA separate backward passes.  train=False: the evaluation
+        reference's GA separate backward passes (`accum`: the micro-batches of this
+        update, fewer than GA at a short epoch end).  train=False: the evaluation
         loss (prediction_step, grpo_trainer.py:2177-2183: compute_loss under
         no_grad, no GA division), forward only."""
         a = self.args
-        GA = a.gradient_accumulation_steps if train else 1
+        GA = (accum or a.gradient_accumulation_steps) if train else 1
         orig = micro
         R_each = [m["completion_ids"].shape[0] for m in micro]
         W = max(m["completion_ids"].shape[1] for m in micro)
@@ -874,9 +875,12 @@ class GRPOTrainer:
         return cb
 
     def training_step_group(self) -> dict:
-        """One optimizer step: GA micro-batches (fused), DP all-reduce, clip, AdamW."""
+        """One optimizer step: GA micro-batches (fused), DP all-reduce, clip, AdamW.
+        The last update of an epoch takes the remaining micro-batches when the epoch's
+        count is not a multiple of GA, its loss divided by their number (transformers
+        Trainer._run_epoch: `remainder`, current_gradient_accumulation_steps)."""
         a = self.args
-        GA = a.gradient_accumulation_steps
+        GA = self._update_size(self._step)
         self.model.zero_grad()
         micro = [self._next_micro_batch() for _ in range(GA)]
         outs = []
@@ -890,7 +894,7 @@ class GRPOTrainer:
             if ar is not None and gi == len(groups) - 1:
                 self.model.on_layer_grads = self._bucket_release(ar)
             try:
-                outs.append(self._loss_backward(grp))
+                outs.append(self._loss_backward(grp, accum=GA))
             finally:
                 self.model.on_layer_grads = None
         if ar is not None:
@@ -1188,19 +1192,24 @@ class GRPOTrainer:
         GA = self.args.gradient_accumulation_steps
         return max(1, -(-self._micro_steps_per_epoch() // GA))
 
-    def _check_epoch_remainder(self, total: int) -> None:
-        """The transformers Trainer closes every epoch with an update over the
-        remaining micro-batches (fewer than GA, loss / their count).  This loop
-        always accumulates GA micro-batches, so a run that would cross an epoch
-        end with a remainder is refused instead of trained differently."""
-        a = self.args
-        GA, mse = a.gradient_accumulation_steps, self._micro_steps_per_epoch()
-        if mse % GA and total * GA > mse:
-            raise ValueError(
-                f"{mse} micro-batches per epoch (generation batches x steps_per_generation x num_iterations) is not a "
-                f"multiple of gradient_accumulation_steps ({GA}): the reference Trainer ends each epoch with a shorter "
-                "accumulation, which the MI355X trainer does not implement; choose steps_per_generation / "
-                "gradient_accumulation_steps so that GA divides it, or max_steps within the first epoch")
+    def _epoch_micro_steps(self) -> Optional[int]:
+        """Micro-steps per epoch, None without a training dataset (no epochs)."""
+        return self._micro_steps_per_epoch() if self.train_dataset is not None else None
+
+    def _update_size(self, k: int) -> int:
+        """Micro-batches of the update that starts at micro-step k: GA, or the epoch's
+        remainder for its last update (transformers Trainer._run_epoch)."""
+        GA, mse = self.args.gradient_accumulation_steps, self._epoch_micro_steps()
+        if not mse:
+            return GA
+        return min(GA, mse - k % mse)
+
+    def _update_index(self, k: int) -> int:
+        """The optimizer step (0-based, since training began) micro-step k belongs to."""
+        GA, mse = self.args.gradient_accumulation_steps, self._epoch_micro_steps()
+        if not mse:
+            return k // GA
+        return (k // mse) * (-(-mse // GA)) + (k % mse) // GA
 
     @staticmethod
     def _interval(x, total: int) -> int:
@@ -1223,7 +1232,6 @@ class GRPOTrainer:
                 raise ValueError(f"No valid checkpoint found in output directory ({a.output_dir})")
             self._load_checkpoint(d)
         total = self._total_steps()
-        self._check_epoch_remainder(total)
         st = self.state
         st.max_steps = total
         st.num_train_epochs = int(math.ceil(total / self._steps_per_epoch()))
@@ -1245,7 +1253,7 @@ class GRPOTrainer:
             self.control = cb.call("on_step_begin")
             out = self.training_step_group()
             loss_sum += out["loss"].detach().float()
-            st.epoch = st.global_step / self._steps_per_epoch()
+            st.epoch = self._step / self._micro_steps_per_epoch()  # Trainer: epoch + (step + 1) / steps_in_epoch
             # DefaultFlowCallback.on_step_end, then the user's callbacks may change the decisions
             c, gs = self.control, st.global_step
             if (gs == 1 and a.logging_first_step) or gs % log_every == 0:

@@ -365,8 +365,9 @@ def test_grpo_epoch_accounting_follows_trainer():
     """transformers Trainer.set_initial_training_values over GRPO's dataloader
     (grpo_trainer.py:1063-1130: batches of per_device x spg, RepeatSampler repeating
     each generation batch spg x num_iterations times): optimizer steps per epoch =
-    ceil(micro-steps / GA).  A run whose epoch ends with fewer than GA micro-batches
-    (the Trainer's shorter last accumulation) is refused, not trained differently."""
+    ceil(micro-steps / GA).  An epoch whose micro-batches are not a multiple of GA
+    ends with a shorter update over the remainder (Trainer._run_epoch `remainder`);
+    the next epoch's updates start at its first micro-batch."""
     import types
 
     from swh_trl_amd.trainer.grpo_trainer import GRPOTrainer
@@ -375,18 +376,31 @@ def test_grpo_epoch_accounting_follows_trainer():
         a = GRPOConfig(**kw)
         ns = types.SimpleNamespace(args=a, num_generations=a.num_generations, num_iterations=a.num_iterations,
                                    train_dataset=list(range(n_prompts)))
-        for name in ("_micro_steps_per_epoch", "_steps_per_epoch", "_total_steps", "_check_epoch_remainder"):
+        for name in ("_micro_steps_per_epoch", "_steps_per_epoch", "_total_steps", "_epoch_micro_steps",
+                     "_update_size", "_update_index"):
             setattr(ns, name, types.MethodType(getattr(GRPOTrainer, name), ns))
         return ns
+
+    def updates(t, n):  # (first micro-step, size) of the first n updates, as training_step_group takes them
+        k, out = 0, []
+        for u in range(n):
+            size = t._update_size(k)
+            assert all(t._update_index(k + j) == u for j in range(size))
+            out.append((k, size))
+            k += size
+        return out
 
     # default: spg = GA, so every epoch is whole accumulations
     t = fake(20, per_device_train_batch_size=8, gradient_accumulation_steps=2, num_generations=4, num_train_epochs=2)
     assert t._micro_steps_per_epoch() == (20 // 4) * 2 and t._steps_per_epoch() == 5 and t._total_steps() == 10
-    t._check_epoch_remainder(t._total_steps())
-    # spg 2, GA 4, 3 generation batches per epoch: 6 micro-steps = 4 + a remainder of 2
+    assert updates(t, 10) == [(2 * u, 2) for u in range(10)]
+    # spg 2, GA 4, 3 generation batches per epoch: 6 micro-steps = 4 + a remainder of 2, per epoch
     t = fake(6, per_device_train_batch_size=4, gradient_accumulation_steps=4, steps_per_generation=2,
-             num_generations=4, num_train_epochs=1)
-    assert t._micro_steps_per_epoch() == 6 and t._steps_per_epoch() == 2
-    with pytest.raises(ValueError, match="not a multiple of gradient_accumulation_steps"):
-        t._check_epoch_remainder(t._total_steps())
-    t._check_epoch_remainder(1)  # max_steps inside the first epoch: no remainder is ever reached
+             num_generations=4, num_train_epochs=2)
+    assert t._micro_steps_per_epoch() == 6 and t._steps_per_epoch() == 2 and t._total_steps() == 4
+    assert updates(t, 4) == [(0, 4), (4, 2), (6, 4), (10, 2)]
+    # GA larger than an epoch: one short update per epoch
+    t = fake(4, per_device_train_batch_size=4, gradient_accumulation_steps=8, steps_per_generation=2,
+             num_generations=4, num_train_epochs=3)
+    assert t._micro_steps_per_epoch() == 4 and t._steps_per_epoch() == 1 and t._total_steps() == 3
+    assert updates(t, 3) == [(0, 4), (4, 4), (8, 4)]
