@@ -219,6 +219,9 @@ def main():
     from swh_trl_amd import profiling
     from swh_trl_amd.engine.config import qwen2_5_0_5b
     from swh_trl_amd.trainer import GRPOConfig, GRPOTrainer
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import _env  # A/B switches from the environment (SWH_TRACE, SWH_LIB_PATH, policy, EngineOptions fields)
+    _env.apply()
 
     rank, world, local = sd.init_from_env()
     if world != args.gpus:
@@ -240,6 +243,7 @@ def main():
                     max_steps=steps + warm, logging_steps=10 ** 9, seed=0, shuffle_dataset=True,
                     generation_kwargs=gen_kw)
     tr = GRPOTrainer(model=cfg, reward_funcs=dummy_reward, args=gc, train_dataset=ds)
+    tr.model.options = _env.options()  # the defaults unless an A/B switch is set
     tr.state.max_steps = steps + warm
     tb = time.perf_counter()
     for i in range(warm):

@@ -10,9 +10,10 @@
  *     detected on the host before anything is launched;
  *   - no hidden mutable state: the library holds only (1) per-device facts
  *     queried once per device under std::call_once (CU count, each kernel's
- *     dynamic-LDS opt-in) and (2) the launch policy below, set explicitly by
- *     swh_set_launch_policy and read under a lock; it never reads the
- *     environment.  Entry points are re-entrant across host threads, streams
+ *     dynamic-LDS opt-in) and (2) the launch policy below, one per host thread
+ *     (thread_local), set explicitly by swh_set_launch_policy; nothing is
+ *     process-wide and mutable, and it never reads the environment.  Entry
+ *     points are re-entrant across host threads, streams
  *     and devices, and safe to capture into a hipGraph (the decode step is
  *     captured and replayed).
  *
@@ -45,10 +46,12 @@ const char *swh_status_string(int status);
 /* Launch policy: geometry choices of the decode GEMMs and samplers, for A/B
  * timing and geometry-coverage tests.  Every alternative is bit-identical
  * (tests pin that) except wide_smax, wide_cb and wide_waves, which choose how
- * wide_gemm splits K and so the fp32 summation order of its dot products
- * (each deterministic for a given policy).  Process-wide, applied by
- * launches issued after the call (a captured graph keeps the geometry it was
- * captured with).  *_workspace_bytes size for the policy in force when they are
+ * wide_gemm splits K, and attn_pair, which chooses how the D = 128 decode
+ * attention's waves split the keys: these change the fp32 summation order
+ * (each deterministic for a given policy).  Per host thread: a thread's policy
+ * starts at the defaults and applies to the launches that thread issues after
+ * the call (a captured graph keeps the geometry it was captured with); other
+ * threads are not affected.  *_workspace_bytes size for the policy in force when they are
  * called; a launch whose geometry needs more workspace than it is given returns
  * SWH_E_ARG and writes nothing.  gemm_ms 0 means "the cost model decides" (the
  * other geometry fields must then be 0). */

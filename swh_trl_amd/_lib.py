@@ -41,8 +41,10 @@ class GRPOLossParams(C.Structure):
 
 
 class LaunchPolicy(C.Structure):
-    """swh_launch_policy (include/swh_trl_amd.h): geometry choices that change no
-    result (every alternative is bit-identical), set explicitly."""
+    """swh_launch_policy (include/swh_trl_amd.h): geometry choices of the decode
+    GEMMs, attention and samplers, set explicitly and held per host thread.  Every
+    alternative is bit-identical except wide_smax, wide_cb, wide_waves and
+    attn_pair, which change the fp32 summation order (each deterministic)."""
     _fields_ = [("wide_kmin", c_i64), ("wide_gemm", c_i32), ("wide_smax", c_i32), ("wide_cb", c_i32),
                 ("gemm_ms", c_i32), ("gemm_cb", c_i32), ("gemm_s", c_i32), ("gemm_persist", c_i32),
                 ("gemm_wn", c_i32), ("gemm_tile", c_i32), ("gemm_nw", c_i32), ("xstream", c_i32),
@@ -153,6 +155,15 @@ SIGNATURES = {
 
 _lib = None
 _lock = threading.Lock()
+_path = [LIB_PATH]
+
+
+def set_library_path(path: str) -> None:
+    """Load another build of the library (A/B timing of two builds, tools only);
+    must precede the first load()."""
+    if _lib is not None and os.path.abspath(path) != os.path.abspath(_path[0]):
+        raise RuntimeError("swh_trl_amd library already loaded from " + _path[0])
+    _path[0] = path
 
 
 def load() -> C.CDLL:
@@ -162,7 +173,7 @@ def load() -> C.CDLL:
         return _lib
     with _lock:
         if _lib is None:
-            path = os.environ.get("SWH_LIB_PATH", LIB_PATH)  # A/B timing of two builds (tools only)
+            path = _path[0]
             if not os.path.exists(path):
                 raise RuntimeError(f"{path} is missing: build it with `python swh_trl_amd/build.py` "
                                    "(the swh_trl_amd ops have no CPU fallback)")
@@ -172,17 +183,7 @@ def load() -> C.CDLL:
                 fn.restype = res
                 fn.argtypes = args
             _lib = lib
-            _policy_from_env(lib)
     return _lib
-
-
-# Tools-only A/B switches of the launch policy, read ONCE when the library is
-# loaded (the library itself never reads the environment).  A process that wants
-# another policy later calls set_launch_policy / launch_policy(...).
-_ENV_POLICY = {"SWH_WIDE_KMIN": "wide_kmin", "SWH_WIDE_GEMM": "wide_gemm", "SWH_WIDE_SMAX": "wide_smax",
-               "SWH_WIDE_CB": "wide_cb", "SWH_GEMM_NW": "gemm_nw", "SWH_XSTREAM": "xstream",
-               "SWH_LM_RING14": "lm_ring14", "SWH_FILT_WGS": "filt_wgs", "SWH_WIDE_WAVES": "wide_waves",
-               "SWH_ATTN_PAIR": "attn_pair"}
 
 
 def _geometry_fields(cfg: str) -> dict:
@@ -196,19 +197,8 @@ def _geometry_fields(cfg: str) -> dict:
     return dict(zip(("gemm_ms", "gemm_cb", "gemm_s", "gemm_persist", "gemm_wn"), v))
 
 
-def _policy_from_env(lib) -> None:
-    kw = {f: int(os.environ[e]) for e, f in _ENV_POLICY.items() if os.environ.get(e)}
-    if os.environ.get("SWH_GEMM_CFG"):
-        kw.update(_geometry_fields(os.environ["SWH_GEMM_CFG"]))
-    if kw:
-        p = LaunchPolicy()
-        lib.swh_get_launch_policy(C.byref(p))
-        for k, v in kw.items():
-            setattr(p, k, v)
-        check(lib.swh_set_launch_policy(C.byref(p)), "swh_set_launch_policy")
-
-
 def get_launch_policy() -> dict:
+    """The calling thread's launch policy (the library holds one per host thread)."""
     p = LaunchPolicy()
     check(load().swh_get_launch_policy(C.byref(p)), "swh_get_launch_policy")
     return {f: getattr(p, f) for f, _ in LaunchPolicy._fields_}
@@ -236,7 +226,8 @@ def set_launch_policy(**fields) -> dict:
 
 class launch_policy:
     """Context manager: `with launch_policy(xstream=0): ...` runs the block's
-    launches (and graph captures) under the given policy, then restores it."""
+    launches (and graph captures) on this thread under the given policy, then
+    restores the thread's previous one.  Other threads keep their own."""
 
     def __init__(self, **fields):
         self.fields = fields

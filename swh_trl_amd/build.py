@@ -15,8 +15,8 @@ CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libswh_trl_amd.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "swh_trl_amd.h")
-ARCH = os.environ.get("SWH_OFFLOAD_ARCH", "gfx950")
-HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"  # MI355X (CDNA4) only
+HIPCC = "/opt/rocm/bin/hipcc"
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function",
          "-munsafe-fp-atomics"]
 

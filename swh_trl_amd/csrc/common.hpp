@@ -307,13 +307,13 @@ inline int launch_status() { return hipGetLastError() == hipSuccess ? SWH_OK : S
 
 // ---- the library's host-side state (csrc/lib.hip) ------------------------------
 // Per-device facts, each queried once per device under std::call_once, and the
-// launch policy of swh_set_launch_policy (a copy read under a lock).  Nothing
+// calling thread's launch policy of swh_set_launch_policy (thread_local).  Nothing
 // else in the library outlives a call, and nothing reads the environment.
 constexpr int kMaxDevices = 64;
 constexpr int kMaxDynLds = 160 * 1024;  // gfx950 LDS per workgroup
 
 int cu_count();                        // current device's CUs (256 if the query fails)
-swh_launch_policy launch_policy();     // a snapshot of the process-wide policy
+swh_launch_policy launch_policy();     // the calling thread's policy
 bool lds_opt_in_once(const void *kernel, std::once_flag *once, bool *ok);
 
 // Opt a kernel into > 64 KB of dynamic LDS, once per (kernel, device): the

@@ -1,5 +1,6 @@
 // Library identity, status strings, and the library's only host-side state:
-// per-device facts (call_once per device) and the explicit launch policy.
+// per-device facts (call_once per device) and the explicit launch policy of the
+// calling thread (thread_local: no process-wide mutable state).
 #include "common.hpp"
 
 namespace swh {
@@ -37,8 +38,9 @@ swh_launch_policy default_policy() {
     p.attn_pair = 1;
     return p;
 }
-std::mutex g_policy_mu;
-swh_launch_policy g_policy = default_policy();
+// each host thread holds its own policy (the defaults until it sets one), so two
+// callers in one process cannot change each other's geometry or output bits
+thread_local swh_launch_policy t_policy = default_policy();
 
 bool in(int32_t v, std::initializer_list<int32_t> ok) {
     for (int32_t o : ok)
@@ -47,10 +49,7 @@ bool in(int32_t v, std::initializer_list<int32_t> ok) {
 }
 }  // namespace
 
-swh_launch_policy launch_policy() {
-    std::lock_guard<std::mutex> g(g_policy_mu);
-    return g_policy;
-}
+swh_launch_policy launch_policy() { return t_policy; }
 
 }  // namespace swh
 
@@ -80,8 +79,7 @@ extern "C" int swh_set_launch_policy(const swh_launch_policy *p) {
         !in(p->lm_ring14, {0, 1}) || p->filt_wgs < 64 || p->filt_wgs > 65536 || !in(p->wide_waves, {0, 6, 7, 8}) ||
         !in(p->attn_pair, {0, 1}))
         return SWH_E_ARG;
-    std::lock_guard<std::mutex> g(g_policy_mu);
-    g_policy = *p;
+    t_policy = *p;
     return SWH_OK;
 }
 

@@ -15,6 +15,13 @@ import torch
 import torch.distributed as dist
 
 
+def world_size_from_env() -> int:
+    """WORLD_SIZE of the launcher (torchrun / bench.py), 1 without one: the
+    process count the configs derive their global batch from, before (or
+    without) a process group — accelerate's num_processes."""
+    return int(os.environ.get("WORLD_SIZE", "1"))
+
+
 def init_from_env(backend: str | None = None):
     """Initialise torch.distributed from RANK/WORLD_SIZE/MASTER_* (torchrun).
     Returns (rank, world_size, device_index).  No-op for a single process.
@@ -22,7 +29,7 @@ def init_from_env(backend: str | None = None):
     device_index is LOCAL_RANK (one process per GPU).  On gloo with more ranks
     than visible devices (tests rehearsing N ranks on one GPU) ranks share
     devices round-robin; RCCL refuses that, so the nccl backend raises."""
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = world_size_from_env()
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if backend is None:  # SWH_DIST_BACKEND: tests run gloo ranks that share one GPU

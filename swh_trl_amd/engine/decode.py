@@ -22,7 +22,6 @@ from __future__ import annotations
 
 import contextlib
 import gc
-import os
 from typing import Optional
 
 import torch
@@ -31,6 +30,7 @@ from .. import _lib, nn_ops, ops
 from ..profiling import trace as _trace
 from .._lib import call
 from .model import CausalLM
+from .options import EngineOptions
 
 
 class EarlyExitPoll:
@@ -82,10 +82,30 @@ def _capture(graph: "torch.cuda.CUDAGraph"):
             gc.enable()
 
 
+def _under_policy(fn):
+    """Run an engine method's launches and graph captures under the launch policy
+    the engine was built with (its routing and weight packing were decided by it;
+    ADVICE r5): the library's policy is per host thread, set for the call and
+    restored after it."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrapped(self, *a, **kw):
+        with _lib.launch_policy(**self.policy):
+            return fn(self, *a, **kw)
+    return wrapped
+
+
 class DecodeEngine:
     def __init__(self, model: CausalLM, batch_size: int, max_prompt_len: int, max_new_tokens: int,
-                 use_graph: bool = True, fused: Optional[bool] = None):
+                 use_graph: bool = True, fused: Optional[bool] = None, options: Optional[EngineOptions] = None):
+        """`options`: the engine's mechanism choices (default: the model's,
+        engine/options.py).  The engine snapshots the calling thread's launch policy
+        (the library's kernel geometry, which also decides the weight copies packed
+        below) and runs every launch and graph capture of its own under it."""
         c = model.cfg
+        o = self.options = options if options is not None else model.options
+        self.policy = _lib.get_launch_policy()
         if model.dtype != torch.bfloat16:
             raise ValueError("DecodeEngine: the decode kernels read bf16 weights (pass a bf16 copy of an fp32 model)")
         self.model, self.cfg = model, c
@@ -119,23 +139,23 @@ class DecodeEngine:
         self.out_logp = torch.zeros(B, max_new_tokens, device=dev, dtype=torch.float32)
         self.plen = torch.zeros(B, device=dev, dtype=torch.int32)
         # GRPO's G copies of a prompt read one copy of its prompt K/V in the decode attention
-        # (swh_attn_decode_shared; SWH_DECODE_SHARED_KV=0: every row its own copy)
-        self.shared_kv = os.environ.get("SWH_DECODE_SHARED_KV", "1") != "0"
+        # (swh_attn_decode_shared; options.shared_kv False: every row its own copy)
+        self.shared_kv = o.shared_kv
         self._own_rows = torch.arange(B, device=dev, dtype=torch.int32)
         self.prow = self._own_rows.clone()
         self.seen = torch.zeros(B, (c.vocab_size + 31) // 32, device=dev, dtype=torch.int32)
         self.ws = torch.empty(ops._lib.load().swh_sample_workspace_bytes(B, c.vocab_size), device=dev,
                               dtype=torch.uint8)
         self.cos, self.sin = model.rope(self.Tmax + 1)
-        self.use_graph = use_graph and os.environ.get("SWH_DECODE_GRAPH", "1") != "0"
+        self.use_graph = use_graph and o.decode_graph
         ks = (c.hidden_size, c.intermediate_size, c.q_dim)
-        self.fused = (fused if fused is not None else os.environ.get("SWH_DECODE_FUSED", "1") != "0") and \
+        self.fused = (fused if fused is not None else o.fused) and \
             all(k % 128 == 0 for k in ks) and c.hidden_size % 16 == 0 and c.qkv_dim % 16 == 0
         # Folded RMSNorm weights: W' = bf16(W * w_norm) for the normed projections,
         # so the decode GEMMs scale rows by rstd in the epilogue instead of
         # normalising X in every workgroup (rounding differs from transformers'
-        # bf16(w * bf16(x * rstd)) at the last bf16 bit; SWH_DECODE_FOLD=0 keeps it)
-        self.fold = self.fused and os.environ.get("SWH_DECODE_FOLD", "1") != "0"
+        # bf16(w * bf16(x * rstd)) at the last bf16 bit; options.fold_norm False keeps it)
+        self.fold = self.fused and o.fold_norm
         self.fw = {}
         if self.fold:
             L = c.num_hidden_layers
@@ -144,14 +164,14 @@ class DecodeEngine:
                 self.fw[f"l{i}.gu_w"] = torch.empty_like(model.p[f"l{i}.gu_w"])
             self.fw["lm"] = torch.empty_like(model.lm_weight())
         # the launch policy's route to the bandwidth-regime GEMM (the library decides by it too)
-        pol = _lib.get_launch_policy()
+        pol = self.policy
         wide_on, kmin = bool(pol["wide_gemm"]), int(pol["wide_kmin"])
         # Bandwidth-regime projections (Llama-3-8B widths: K >= the policy's wide_kmin, >= 1024 weight
         # rows) read a copy of their weight in wide_gemm's fragment order (contiguous 4 KB
         # runs per wave and round instead of 16 rows 64 B each, csrc/wide_gemm.hip), the
-        # folded norm applied while packing; SWH_WIDE_PACK=0 keeps the row-major weights
+        # folded norm applied while packing; options.wide_pack False keeps the row-major weights
         self.packed = {}
-        if self.fold and os.environ.get("SWH_WIDE_PACK", "1") != "0" and wide_on:
+        if self.fold and o.wide_pack and wide_on:
             for name, (N, K, silu, _norm) in self._projections().items():
                 if K >= kmin and nn_ops.wide_gemm_eligible(B, N, K, silu):
                     self.packed[name] = torch.empty(N * K * (2 if silu else 1), **bf)
@@ -160,11 +180,11 @@ class DecodeEngine:
         # Fragment-order copies of the per-layer projections at the 0.5B widths (qkv and
         # gate/up folded with their RMSNorm weight, o, down): each weight load of a wave is
         # one contiguous 1 KB run instead of 16 rows x 64 B (swh_frag_pack /
-        # swh_decode_gemm_fragw, bit-identical results); SWH_FRAGW=0 keeps the row-major
+        # swh_decode_gemm_fragw, bit-identical results); options.fragw False keeps the row-major
         # weights.  Not the shapes decode_gemm hands to the row-major wide GEMM (those keep
         # its result).  The lm head's copy serves the fused sampler and the logits path alike.
         self.fragw = {}
-        if self.fused and os.environ.get("SWH_FRAGW", "1") != "0":
+        if self.fused and o.fragw:
             for name, (N, K, silu, norm) in self._projections().items():
                 if norm is not None and not self.fold:
                     continue
@@ -174,30 +194,30 @@ class DecodeEngine:
                     self.fragw[name] = torch.empty(rows, K, **bf)
                     self.fw.pop(name, None)  # served by the fragment-order copy only
         # gate/up writes its SiLU output in the fragment order down_proj reads (register-
-        # streamed, no LDS image; down 8.9 -> 6.9-7.6 us at 0.5B); SWH_ACT_FRAG=0 keeps it row-major
-        self.act_frag = (os.environ.get("SWH_ACT_FRAG", "1") != "0" and B % 16 == 0 and
+        # streamed, no LDS image; down 8.9 -> 6.9-7.6 us at 0.5B); options.act_frag False: row-major
+        self.act_frag = (o.act_frag and B % 16 == 0 and
                          all(f"l{i}.gu_w" in self.fragw and f"l{i}.down_w" in self.fragw
                              for i in range(c.num_hidden_layers)) and c.intermediate_size % 32 == 0 and
                          c.hidden_size <= 1024 and c.intermediate_size <= 4864 and  # tile gate/up, <= 19 k-steps/wave
                          c.intermediate_size // 8 >= torch.cuda.get_device_properties(dev).multi_processor_count)
         # the attention writes its output in the fragment order o_proj reads (register-
-        # streamed A operand as contiguous 1 KB runs); SWH_ATT_FRAG=0 keeps it row-major
-        self.att_frag = (os.environ.get("SWH_ATT_FRAG", "1") != "0" and B % 16 == 0 and c.q_dim % 32 == 0 and
+        # streamed A operand as contiguous 1 KB runs); options.att_frag False keeps it row-major
+        self.att_frag = (o.att_frag and B % 16 == 0 and c.q_dim % 32 == 0 and
                          all(f"l{i}.o_w" in self.fragw for i in range(c.num_hidden_layers)))
         self.graph = None
         self.graph_k = None
         self._prefill_graphs = {}
-        self.steps_per_graph = max(1, int(os.environ.get("SWH_DECODE_GRAPH_STEPS", "8")))
+        self.steps_per_graph = o.graph_steps
         self._graph_params = None
         self.params = ops.make_sample_params()
         self.want_logp = False
         # Infinity Cache warm-up carried by the attention launch (swh_attn_decode_l3): its
         # B x Hkv workgroups leave CUs idle, extra workgroups on them read the weights of
-        # the projections that follow (SWH_DECODE_L3_ATTN = workgroups, 0: off;
-        # SWH_DECODE_L3_SET: comma list of o, down, gu, qkv (this layer), qkv1, o1, gu1,
-        # down1 (next layer))
-        self.l3_set = os.environ.get("SWH_DECODE_L3_SET", "o,down,qkv1")
-        self.l3_attn = int(os.environ.get("SWH_DECODE_L3_ATTN", str(self._l3_attn_default()))) if self.fused else 0
+        # the projections that follow (options.l3_attn = workgroups, 0: off, None: the
+        # default; options.l3_set: comma list of o, down, gu, qkv (this layer), qkv1, o1,
+        # gu1, down1 (next layer))
+        self.l3_set = o.l3_set
+        self.l3_attn = (self._l3_attn_default() if o.l3_attn is None else int(o.l3_attn)) if self.fused else 0
         self._l3a_jobs = None
         self._exit_poll = EarlyExitPoll(self.finished)
         self.steps_run = 0  # decode steps the last generate() ran (early exit: fewer than max_new_tokens - 1)
@@ -227,9 +247,9 @@ class DecodeEngine:
         """lm head + sampler in one kernel (no logits): unfiltered sampling
         without the per-token log-prob output."""
         # K > 1024: the wide-tile sampler (config 5's step 9.744 -> 9.682 s,
-        # profiles/r5_wsamp_step_ab.log); SWH_FUSED_SAMPLE_WIDE=0 keeps logits + sample_step
-        wide = "lm" in self.packed and os.environ.get("SWH_FUSED_SAMPLE_WIDE", "1") != "0"
-        return (self.fused and not self.want_logp and os.environ.get("SWH_FUSED_SAMPLE", "1") != "0" and
+        # profiles/r5_wsamp_step_ab.log); options.fused_sample_wide False keeps logits + sample_step
+        wide = "lm" in self.packed and self.options.fused_sample_wide
+        return (self.fused and not self.want_logp and self.options.fused_sample and
                 nn_ops.lm_head_sample_supported(self.params, self.cfg.vocab_size, self.cfg.hidden_size,
                                                 wide_rows=self.B if wide else 0))
 
@@ -475,6 +495,7 @@ class DecodeEngine:
 
     # ------------------------------------------------------------------ live kernel timing
     @torch.no_grad()
+    @_under_policy
     def kernel_timings(self, step_index: int, reps: int = 20, iters: int = 3) -> dict:
         """Device time of each kernel of one fused decode step at sampler index
         `step_index` (attention over P + step_index keys), plus the whole step.
@@ -566,13 +587,14 @@ class DecodeEngine:
 
     # ------------------------------------------------------------------ prefill
     @staticmethod
-    def _unique_prompts(prompt_ids: torch.Tensor, prompt_mask: torch.Tensor, group_size: int = 0):
+    def _unique_prompts(prompt_ids: torch.Tensor, prompt_mask: torch.Tensor, group_size: int = 0,
+                        dedup: bool = True):
         """(representative row per distinct prompt, inverse map row -> distinct
         prompt), or None when every row differs.  GRPO rolls out G copies of
         each prompt (RepeatSampler, grpo_trainer.py:97-192): the prefill runs
         once per distinct prompt and its K/V and last-position logits are
         broadcast to the copies (row-independent arithmetic, same values)."""
-        if os.environ.get("SWH_PREFILL_DEDUP", "1") == "0":
+        if not dedup:
             return None
         B = prompt_ids.shape[0]
         if group_size > 1 and B % group_size == 0:  # the caller's layout: G consecutive copies (checked)
@@ -622,9 +644,9 @@ class DecodeEngine:
         last position.  Positions follow generate(): cumsum(mask) - 1.  Copies
         of one prompt are prefilled once (`_unique_prompts`).  The forward is
         captured into a HIP graph per (rows, P, padded) and replayed from
-        static input buffers (SWH_PREFILL_GRAPH=0: eager)."""
+        static input buffers (options.decode_graph False: eager)."""
         m = self.model
-        dedup = self._unique_prompts(prompt_ids, prompt_mask, group_size)
+        dedup = self._unique_prompts(prompt_ids, prompt_mask, group_size, self.options.prefill_dedup)
         inv = rep = None
         if dedup is not None:
             rep, inv = dedup
@@ -638,7 +660,7 @@ class DecodeEngine:
             saved = m.grad
             m.grad = None  # no grad accumulation in prefill
             try:
-                if not (self.use_graph and os.environ.get("SWH_PREFILL_GRAPH", "1") != "0"):
+                if not self.use_graph:
                     self._prefill_body(prompt_ids, prompt_mask, inv, rep, padded)
                     return
                 key = (tuple(prompt_ids.shape), inv is None, padded)
@@ -667,6 +689,7 @@ class DecodeEngine:
 
     # ------------------------------------------------------------------ generate
     @torch.no_grad()
+    @_under_policy
     def generate(self, prompt_ids: torch.Tensor, prompt_mask: torch.Tensor, max_new_tokens: int, *,
                  temperature=1.0, top_p=1.0, top_k=None, min_p=None, repetition_penalty=1.0, greedy=False,
                  min_new_tokens=0, eos_token_id=None, pad_token_id=None, seed: int = 0, offset: int = 0,

@@ -25,7 +25,6 @@ host sync) and the HIP sampler (`swh_sample_step`).
 from __future__ import annotations
 
 import math
-import os
 import warnings
 from typing import Optional
 
@@ -171,8 +170,9 @@ class GPT2LM(CausalLM):
 
     supports_shared_prefix = False  # the grouped forward is the Qwen2 / Llama layer
 
-    def _check_attention(self):
-        self._hip_attn = False  # SDPA: head_dim 16 (config 1) is below the MFMA attention tile
+    @property
+    def _hip_attn(self) -> bool:
+        return False  # SDPA: head_dim 16 (config 1) is below the MFMA attention tile
 
     def layer_range(self, i: int) -> tuple[int, int]:
         start = self.layout[f"l{i}.ln_1_w"][0]
@@ -249,7 +249,7 @@ class GPT2LM(CausalLM):
         B, L, H = h.shape
         nh, hd = c.num_attention_heads, c.head_dim
         qkv = _Linear.apply(h, self.p[f"l{i}.attn_w"], self.p[f"l{i}.attn_b"], self._gv(f"l{i}.attn_w"),
-                            self._gv(f"l{i}.attn_b"))
+                            self._gv(f"l{i}.attn_b"), self.options)
         q, k, v = qkv.view(B, L, 3, nh, hd).permute(2, 0, 3, 1, 4).unbind(0)  # [B, nh, L, hd] each
         if kv_out is not None:
             kv_out(i, k, v)
@@ -259,14 +259,14 @@ class GPT2LM(CausalLM):
             o = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, scale=hd ** -0.5)
         o = o.transpose(1, 2).reshape(B, L, H)
         return _Linear.apply(o, self.p[f"l{i}.proj_w"], self.p[f"l{i}.proj_b"], self._gv(f"l{i}.proj_w"),
-                             self._gv(f"l{i}.proj_b"))
+                             self._gv(f"l{i}.proj_b"), self.options)
 
     def _mlp(self, i, h):
         f = _Linear.apply(h, self.p[f"l{i}.fc_w"], self.p[f"l{i}.fc_b"], self._gv(f"l{i}.fc_w"),
-                          self._gv(f"l{i}.fc_b"))
+                          self._gv(f"l{i}.fc_b"), self.options)
         a = GeluNewFn.apply(f)
         return _Linear.apply(a, self.p[f"l{i}.mproj_w"], self.p[f"l{i}.mproj_b"], self._gv(f"l{i}.mproj_w"),
-                             self._gv(f"l{i}.mproj_b"))
+                             self._gv(f"l{i}.mproj_b"), self.options)
 
     def hidden_states(self, ids: torch.Tensor, positions: Optional[torch.Tensor] = None,
                       key_mask: Optional[torch.Tensor] = None, kv_out=None, max_pos: Optional[int] = None,
@@ -342,7 +342,7 @@ class GPT2DecodeEngine:
         self.P = torch.zeros(1, device=dev, dtype=torch.int64)       # prompt width (cache slots [0, P))
         self.seen = torch.zeros(B, (c.vocab_size + 31) // 32, device=dev, dtype=torch.int32)
         self.ws = torch.empty(_load_lib().swh_sample_workspace_bytes(B, c.vocab_size), device=dev, dtype=torch.uint8)
-        self.use_graph = use_graph and os.environ.get("SWH_DECODE_GRAPH", "1") != "0"
+        self.use_graph = use_graph and model.options.decode_graph
         self.graph = None
         self._graph_params = None
         self.params = ops.make_sample_params()

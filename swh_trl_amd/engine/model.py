@@ -16,7 +16,6 @@ MLP, rotate-half RoPE with bf16 cos/sin, GQA attention scaled by D^-0.5.
 from __future__ import annotations
 
 import math
-import os
 from typing import Optional
 
 import torch
@@ -26,6 +25,8 @@ from .. import nn_ops
 from .._lib import call
 from ..ops import _dtype_code, _stream
 from .config import DecoderConfig
+from .options import DEFAULT as DEFAULT_OPTIONS
+from .options import EngineOptions
 
 _ALIGN = 64  # elements; keeps every view 128-byte aligned
 
@@ -34,12 +35,13 @@ _DW_STREAMS: dict = {}
 
 
 def _dw_stream(dev: torch.device):
-    """Side stream for the weight-gradient launches (SWH_DW_STREAM=0: inline).
+    """Side stream for the weight-gradient launches (1.4 ms of the 0.5B half-step
+    against inline).
     The backward's critical path is dX -> next layer; dW of a layer is a leaf, so
     it runs beside the chain (each launch waits for the compute stream's
     progress so far) and the compute stream joins it once, after backward
     (`dw_sync`).  Accumulation order into the gradient views is unchanged."""
-    if dev.type != "cuda" or os.environ.get("SWH_DW_STREAM", "1") == "0":
+    if dev.type != "cuda":
         return None
     st = _DW_STREAMS.get(dev.index)
     if st is None:
@@ -66,7 +68,6 @@ def dw_sync(dev: torch.device):
     _SIDE_GEMM.pop(dev.index, None)
 
 
-_GEMM_FENCE = os.environ.get("SWH_GEMM_FENCE", "1") != "0"  # A/B only: 0 can deadlock (below)
 _SIDE_GEMM: dict = {}  # device index -> event after the last library GEMM issued on the side stream
 
 
@@ -90,7 +91,7 @@ def _main_gemm_fence(dev: torch.device) -> None:
     overlap; the side GEMMs still overlap the compute stream's HIP kernels
     (norm / SiLU / attention / log-prob backward)."""
     ev = _SIDE_GEMM.pop(dev.index, None) if dev.type == "cuda" else None
-    if ev is not None and _GEMM_FENCE:
+    if ev is not None:
         torch.cuda.current_stream(dev).wait_event(ev)
 
 
@@ -127,10 +128,10 @@ class _Linear(torch.autograd.Function):
     side stream."""
 
     @staticmethod
-    def forward(ctx, x, w, b, gw, gb):
+    def forward(ctx, x, w, b, gw, gb, opts):
         ctx.save_for_backward(x, w)
-        ctx.gw, ctx.gb = gw, gb
-        if _tgemm_serves(w.shape[0], w.shape[1]) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
+        ctx.gw, ctx.gb, ctx.opts = gw, gb, opts
+        if _tgemm_serves(opts, w.shape[0], w.shape[1]) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
             x2 = x.reshape(-1, x.shape[-1])
             if nn_ops.gemm_nt_eligible(x2, w) and (b is None or b.dtype == torch.bfloat16):
                 return nn_ops.gemm_nt(x2, w, b).view(*x.shape[:-1], w.shape[0])
@@ -143,7 +144,7 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dy2 = dy.reshape(-1, dy.shape[-1])
             wt = None
-            if _tgemm_serves(w.shape[0], w.shape[1]) and w.shape[1] % 128 == 0 and w.shape[0] % 64 == 0 \
+            if _tgemm_serves(ctx.opts, w.shape[0], w.shape[1]) and w.shape[1] % 128 == 0 and w.shape[0] % 64 == 0 \
                     and dy.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
                 wt = w.t().contiguous()  # dy w = dy (w^T)^T: the transposed weight (N K elements) as B
             if wt is not None and nn_ops.gemm_nt_eligible(dy2, wt):
@@ -152,42 +153,37 @@ class _Linear(torch.autograd.Function):
                 _main_gemm_fence(dy.device)
                 dx = dy @ w
         if ctx.gw is not None:
-            _accumulate_dw(ctx.gw, ctx.gb, dy, x)
-        return dx, None, None, None, None
+            _accumulate_dw(ctx.gw, ctx.gb, dy, x, ctx.opts)
+        return dx, None, None, None, None, None
 
 
 # swh_gemm_nt / swh_gemm_tn (csrc/tgemm.hip) for the narrow projections (qkv, o:
-# N, K <= 1536).  SWH_TGEMM = off | wgrad (the weight gradients only) | all (also
-# the forward and input-gradient GEMMs).  A/B: tools/bench_tgemm.py, tools/train_kernels.py.
-_TGEMM = os.environ.get("SWH_TGEMM", "wgrad")
+# N, K <= 1536).  EngineOptions.tgemm = off | wgrad (the weight gradients only) | all
+# (also the forward and input-gradient GEMMs).  A/B: tools/bench_tgemm.py, tools/train_kernels.py.
 _TGEMM_MAX_N = 1536
-_TGEMM_SPLITS = int(os.environ.get("SWH_TGEMM_SPLITS", "8"))
-# the qkv bias gradient from gemm_tn's staged dY (1) or a separate swh_colsum_partials pass (0, A/B)
-_TN_COLSUM = os.environ.get("SWH_TN_COLSUM", "1") != "0"
-if _TGEMM not in ("off", "wgrad", "all"):
-    raise ValueError(f"SWH_TGEMM={_TGEMM!r}: expected off | wgrad | all")
 
 
-def _tgemm_serves(n_out: int, k_in: int, wgrad: bool = False) -> bool:
-    on = _TGEMM == "all" or (wgrad and _TGEMM == "wgrad")
+def _tgemm_serves(opts: EngineOptions, n_out: int, k_in: int, wgrad: bool = False) -> bool:
+    on = opts.tgemm == "all" or (wgrad and opts.tgemm == "wgrad")
     return on and n_out <= _TGEMM_MAX_N and k_in <= _TGEMM_MAX_N
 
 
-def _accumulate_dw(gw, gb, dy, x):
+def _accumulate_dw(gw, gb, dy, x, opts: EngineOptions = DEFAULT_OPTIONS):
     """gw += dy^T x (and gb += column sums of dy) on the weight-gradient stream."""
     with _OnStream(_dw_stream(dy.device)) as side:
         side.keep(dy, x)
         dy2 = dy.reshape(-1, dy.shape[-1])
         x2 = x.reshape(-1, x.shape[-1])
         S = _dw_split(dy2.shape[0], dy2.shape[1] * x2.shape[1])
-        if _tgemm_serves(dy2.shape[1], x2.shape[1], wgrad=True) and gw.is_contiguous() and nn_ops.gemm_tn_eligible(dy2, x2):
+        if _tgemm_serves(opts, dy2.shape[1], x2.shape[1], wgrad=True) and gw.is_contiguous() and \
+                nn_ops.gemm_tn_eligible(dy2, x2):
             # fp32 partials over 8 token ranges (one per XCD), folded in order (no fence needed:
             # the kernel is not persistent).  The partials are allocated on this side stream,
             # so the caching allocator reuses their block only for later side-stream work:
             # released here, not kept to the end of the backward (~33 MB per layer at 0.5B)
             # (the bias gradient's token sums come out of the same kernel's staged dY)
-            fused = gb is not None and gb.is_contiguous() and _TN_COLSUM
-            nn_ops.gemm_tn_accumulate(gw.view(dy2.shape[1], x2.shape[1]), dy2, x2, _TGEMM_SPLITS,
+            fused = gb is not None and gb.is_contiguous()
+            nn_ops.gemm_tn_accumulate(gw.view(dy2.shape[1], x2.shape[1]), dy2, x2, opts.tgemm_splits,
                                       bias_grad=gb if fused else None)
             if gb is not None and not fused:
                 bias_grad_accumulate(dy2, gb)
@@ -231,8 +227,8 @@ def _dw_split(tokens: int, outputs: int) -> int:
     bench step's 17408 tokens with the fold included (tools/gemm_eff.py): qkv
     (1.03M outputs) S 8 66 us against 147 at S 1; o (0.80M) S 2 75 us against
     134 at S 8, where the fold of eight partials dominates; down (4.4M) S 2-8
-    200 us against 251.  SWH_DW_SPLIT=0 keeps the single GEMM."""
-    if os.environ.get("SWH_DW_SPLIT", "1") == "0" or tokens < 8192:
+    200 us against 251."""
+    if tokens < 8192:
         return 1
     if outputs <= 900_000:
         return 2
@@ -304,7 +300,7 @@ class _RMSNorm(torch.autograd.Function):
         return _norm_backward(x, w, rstd, dy, None, ctx.gw), None, None, None
 
 
-_NORM_RPB = int(os.environ.get("SWH_NORM_RPB", "32"))
+_NORM_RPB = 32  # rows per workgroup of the norm weight-gradient partials
 
 
 def _norm_backward(x, w, rstd, dy, dres, gw):
@@ -462,8 +458,9 @@ class CausalLM:
     (one scalar per position: the PPO value / reward model head)."""
 
     def __init__(self, cfg: DecoderConfig, device, head: str = "lm", dtype=torch.bfloat16, seed: Optional[int] = 0,
-                 init_std: float = 0.02, trainable: bool = True):
+                 init_std: float = 0.02, trainable: bool = True, options: Optional[EngineOptions] = None):
         self.cfg, self.device, self.head, self.dtype = cfg, torch.device(device), head, dtype
+        self.options = options if options is not None else DEFAULT_OPTIONS
         self.layout: dict[str, tuple[int, tuple]] = {}
         off = 0
 
@@ -489,13 +486,8 @@ class CausalLM:
         self._rope = None
         # backward hook: called with layer index i once layer i's weight gradients are final
         self.on_layer_grads = None
-        # full-sequence attention on csrc/attn.hip (fwd 95 + bwd 395 us per layer at the GRPO
-        # shape against aotriton's 150 + 430, rocprofv3 of tools/bench_attn.py); SWH_ATTN=torch
-        # selects torch SDPA for A/B.  The MFMA kernel is bf16: an fp32 model (the
-        # reference-precision mode) runs SDPA
         if dtype not in (torch.bfloat16, torch.float32):
             raise ValueError(f"CausalLM dtype {dtype}: bf16 (the product path) or float32 (reference precision)")
-        self._check_attention()
 
     def _build_layout(self, add):
         """Weights in flat-buffer order: add(name, *shape) per tensor."""
@@ -517,9 +509,14 @@ class CausalLM:
         elif not cfg.tie_word_embeddings:
             add("lm_head", V, H)
 
-    def _check_attention(self):
-        self._hip_attn = (nn_ops.attention_supported(self.cfg.head_dim) and self.dtype == torch.bfloat16
-                          and os.environ.get("SWH_ATTN", "hip") != "torch")
+    @property
+    def _hip_attn(self) -> bool:
+        """Full-sequence attention on csrc/attn.hip (fwd 95 + bwd 395 us per layer at the GRPO
+        shape against aotriton's 150 + 430, rocprofv3 of tools/bench_attn.py);
+        options.hip_attention False selects torch SDPA for A/B.  The MFMA kernel is bf16:
+        an fp32 model (the reference-precision mode) runs SDPA."""
+        return (nn_ops.attention_supported(self.cfg.head_dim) and self.dtype == torch.bfloat16
+                and self.options.hip_attention)
 
     def layer_range(self, i: int) -> tuple[int, int]:
         """[start, end) of layer i's parameters (and gradients) in the flat buffers."""
@@ -638,7 +635,7 @@ class CausalLM:
         B, L, _ = x.shape
         Hq, Hkv, D = c.num_attention_heads, c.num_key_value_heads, c.head_dim
         qkv = _Linear.apply(h, self.p[f"l{i}.qkv_w"], self.p.get(f"l{i}.qkv_b"), self._gv(f"l{i}.qkv_w"),
-                            self._gv(f"l{i}.qkv_b"))
+                            self._gv(f"l{i}.qkv_b"), self.options)
         # split + rotate-half RoPE + [B, H, L, D] layout in one kernel each way
         q, k, v = nn_ops.QKVRopeFn.apply(qkv, positions, cos_t, sin_t, Hq, Hkv, D)
         if kv_out is not None:
@@ -665,11 +662,11 @@ class CausalLM:
     def _post_attention(self, i, x, o):
         """o-proj, residual + post-attention norm, the SiLU-gated MLP: (x + o, MLP output)."""
         c = self.cfg
-        o = _Linear.apply(o, self.p[f"l{i}.o_w"], None, self._gv(f"l{i}.o_w"), None)
+        o = _Linear.apply(o, self.p[f"l{i}.o_w"], None, self._gv(f"l{i}.o_w"), None, self.options)
         x, h = _AddRMSNorm.apply(x, o, self.p[f"l{i}.ln_post"], self._gv(f"l{i}.ln_post"), c.rms_norm_eps)
-        gu = _Linear.apply(h, self.p[f"l{i}.gu_w"], None, self._gv(f"l{i}.gu_w"), None)
+        gu = _Linear.apply(h, self.p[f"l{i}.gu_w"], None, self._gv(f"l{i}.gu_w"), None, self.options)
         a = nn_ops.SiluMulFn.apply(gu)
-        d = _Linear.apply(a, self.p[f"l{i}.down_w"], None, self._gv(f"l{i}.down_w"), None)
+        d = _Linear.apply(a, self.p[f"l{i}.down_w"], None, self._gv(f"l{i}.down_w"), None, self.options)
         return x, d
 
     def _mask(self, key_mask, L: int, padded: bool, device):
@@ -739,7 +736,7 @@ class CausalLM:
             else:
                 x, h = _AddRMSNorm.apply(x, d, self.p[f"l{i}.ln_in"], self._gv(f"l{i}.ln_in"), eps)
             qkv = _Linear.apply(h, self.p[f"l{i}.qkv_w"], self.p.get(f"l{i}.qkv_b"), self._gv(f"l{i}.qkv_w"),
-                                self._gv(f"l{i}.qkv_b"))
+                                self._gv(f"l{i}.qkv_b"), self.options)
             if self._hip_attn:
                 # one node for both segments' RoPE; the attention reads the group's prompt
                 # Q/K/V in place and writes the token-major o_proj input (no cat / copies)
@@ -799,14 +796,14 @@ class CausalLM:
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """lm head (bf16 logits) on selected hidden states [.., H]."""
-        return _Linear.apply(hidden, self.lm_weight(), None, self._lm_grad(), None)
+        return _Linear.apply(hidden, self.lm_weight(), None, self._lm_grad(), None, self.options)
 
     def logp_entropy(self, hidden: torch.Tensor, ids: torch.Tensor, temperature: float = 1.0,
                      compute_entropy: bool = True, chunk_rows: Optional[int] = None):
         """Per-token log-probs (differentiable, fp32) and entropies (no grad) of
         `ids` under softmax(lm_head(hidden) / T), chunked over rows."""
         if chunk_rows is None:
-            cap = int(os.environ.get("SWH_LOGP_CHUNK", "4096"))  # A/B (tools/train_kernels.py)
+            cap = self.options.logp_chunk  # A/B: tools/train_kernels.py
             chunk_rows = max(1, min(cap, (1 << 30) // self.cfg.vocab_size))
         lp, ent = _LMHeadLogp.apply(hidden, self.lm_weight(), self._lm_grad(), ids, float(temperature),
                                     bool(compute_entropy), int(chunk_rows))
@@ -814,4 +811,4 @@ class CausalLM:
 
     def scores(self, hidden: torch.Tensor) -> torch.Tensor:
         """score head (value / reward), bf16 [..] as the transformers score Linear."""
-        return _Linear.apply(hidden, self.p["score"], None, self._gv("score"), None).squeeze(-1)
+        return _Linear.apply(hidden, self.p["score"], None, self._gv("score"), None, self.options).squeeze(-1)

@@ -53,7 +53,7 @@ class RefDecodeEngine:
         self.seen = torch.zeros(B, (c.vocab_size + 31) // 32, device=dev, dtype=torch.int32)
         self.ws = torch.empty(_load_lib().swh_sample_workspace_bytes(B, c.vocab_size), device=dev, dtype=torch.uint8)
         self.cos, self.sin = model.rope(self.Tmax + 1)   # fp32 [T, D/2] (exact fp32 values for an fp32 model)
-        self.use_graph = use_graph and os.environ.get("SWH_DECODE_GRAPH", "1") != "0"
+        self.use_graph = use_graph and model.options.decode_graph
         self.graph = None
         self._graph_params = None
         self.params = ops.make_sample_params()

@@ -8,11 +8,11 @@ records the winner.  This module ships the winners measured on MI355X for the
 engine's shapes (`tuning/gemm_mi355x.csv`) and loads them, so a run never
 tunes on the clock.  Same arithmetic, different kernel choice.
 
-    SWH_GEMM_TUNING = use (default) | tune | off
-    SWH_GEMM_TABLE  = path of the table (default: the shipped one)
+    enable(mode="use" (default) | "tune" | "off", path=the shipped table)
 
 `tune` times every solution of every GEMM shape met in the process and writes
-the table at exit (tools: `python bench.py` under SWH_GEMM_TUNING=tune).
+the table at exit (tools: `python bench.py` under SWH_GEMM_TUNING=tune, which
+bench.py / the tools turn into the call's arguments).
 """
 from __future__ import annotations
 
@@ -23,14 +23,14 @@ TABLE = os.path.join(HERE, "tuning", "gemm_mi355x.csv")
 _done = False
 
 
-def enable(mode: str | None = None) -> str:
+def enable(mode: str | None = None, path: str | None = None) -> str:
     """Turn the table on for this process (idempotent).  Returns the mode used:
     'off' also when the table is missing or was written by another
     torch/ROCm/hipBLASLt build (its validators do not match)."""
     global _done
     import torch
-    mode = mode or os.environ.get("SWH_GEMM_TUNING", "use")
-    path = os.environ.get("SWH_GEMM_TABLE", TABLE)
+    mode = mode or "use"
+    path = path or TABLE
     if _done or mode == "off" or not torch.cuda.is_available():
         return "off"
     tun = torch.cuda.tunable
@@ -51,6 +51,6 @@ def enable(mode: str | None = None) -> str:
             tun.enable(False)
             return "off"
     else:
-        raise ValueError(f"SWH_GEMM_TUNING={mode!r}: expected use | tune | off")
+        raise ValueError(f"gemm tuning mode {mode!r}: expected use | tune | off")
     _done = True
     return mode

@@ -6,7 +6,6 @@ runs (third-party code reached from grpo_trainer.py:1804 and :1249).
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
@@ -567,10 +566,10 @@ _AUX_STREAMS: dict = {}
 
 
 def _aux_stream(dev: torch.device):
-    """Second stream for the dK/dV half of the attention backward (SWH_ATTN_SPLIT=0:
-    one stream).  Every tensor it touches was allocated on, and is joined back to,
-    the calling stream before the backward returns."""
-    if dev.type != "cuda" or os.environ.get("SWH_ATTN_SPLIT", "1") == "0":
+    """Second stream for the dK/dV half of the attention backward.  Every tensor it
+    touches was allocated on, and is joined back to, the calling stream before the
+    backward returns."""
+    if dev.type != "cuda":
         return None
     st = _AUX_STREAMS.get(dev.index)
     if st is None:

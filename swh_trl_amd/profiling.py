@@ -4,7 +4,6 @@ switches it on for the timed region.  Replaces the reference's wall-clock
 `profiling_context` (trl/extras/profiling.py:31-100) for device work."""
 from __future__ import annotations
 
-import os
 import sys
 import time
 from collections import defaultdict
@@ -51,13 +50,20 @@ def summary() -> dict:
     return out
 
 
-_TRACE = os.environ.get("SWH_TRACE", "0") == "1"
+_TRACE = [False]
 _T0 = [time.time()]
 
 
+def set_trace(on: bool) -> None:
+    """Synchronised phase timings on stderr (diagnostics only; tools and bench.py
+    turn it on, e.g. from SWH_TRACE=1)."""
+    _TRACE[0] = bool(on)
+    _T0[0] = time.time()
+
+
 def trace(msg: str):
-    """SWH_TRACE=1: synchronised phase timings on stderr (diagnostics only)."""
-    if _TRACE:
+    """A phase line when tracing is on (`set_trace`)."""
+    if _TRACE[0]:
         import torch
         torch.cuda.synchronize()
         now = time.time()

@@ -7,15 +7,11 @@ hub, data-loader workers, ... kept in `extra`) and raise otherwise, e.g.
 switches raise, as those paths are out of scope."""
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass, field
 from typing import Any, Optional
 
+from ..dist import world_size_from_env as _world_size
 from .training_args import split_known
-
-
-def _world_size() -> int:
-    return int(os.environ.get("WORLD_SIZE", "1"))
 
 
 @dataclass

@@ -670,7 +670,8 @@ class GRPOTrainer:
         logits_to_keep=C+1, drop the last position, /T, selective_log_softmax
         and entropy_from_logits — lm head + log-prob + entropy fused and
         row-chunked (engine/model.py `_LMHeadLogp`)."""
-        grp = self._prompt_groups(batch) if getattr(model, "supports_shared_prefix", False) else None
+        grp = (self._prompt_groups(batch) if getattr(model, "supports_shared_prefix", False)
+               and model.options.shared_prefix else None)
         if grp is not None:
             # the G copies of each prompt share one prompt forward (CausalLM.hidden_states_grouped)
             perm, G = grp
@@ -701,10 +702,7 @@ class GRPOTrainer:
         generation's (`row_index`): a training pass over a whole shuffled
         generation then runs every row at the position the generation-time
         scoring pass gave it, so both see the same GEMM / attention layout and
-        produce the same bits whatever the kernels' row-position dependence.
-        SWH_SHARED_PREFIX=0 keeps the per-row forward."""
-        if os.environ.get("SWH_SHARED_PREFIX", "1") == "0":
-            return None
+        produce the same bits whatever the kernels' row-position dependence."""
         # the trainer's batches carry host copies ("_" keys: no device sync); device ids are
         # read back once (tools / tests that build batches by hand)
         gid = batch.get("_prompt_group", batch.get("prompt_group"))

@@ -7,7 +7,6 @@ only where they cannot change the result (trainer/training_args.py, kept in
 `extra`) and raise otherwise."""
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass, field
 from typing import Any, Optional
 

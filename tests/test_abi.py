@@ -175,9 +175,9 @@ def test_launch_policy_roundtrip_and_validation(lib):
 def test_host_entry_points_are_thread_safe(lib):
     """Host-side entry points (eligibility, workspace sizing over the cost model
     and the per-device CU table, the policy) called from 8 host threads at once,
-    while another thread flips the launch policy, agree with single-threaded
-    answers: the per-device tables are initialised under std::call_once and the
-    policy is read under a lock."""
+    while another thread flips its own launch policy, agree with single-threaded
+    answers: the per-device tables are initialised under std::call_once and each
+    thread holds its own policy."""
     import threading
 
     from swh_trl_amd import _lib
@@ -223,7 +223,8 @@ def test_host_entry_points_are_thread_safe(lib):
 def test_library_holds_no_hidden_state():
     """csrc/ reads no environment variable and declares no mutable static
     outside the call_once-guarded per-device tables (csrc/lib.hip, the LDS
-    opt-in of common.hpp) and the lock-guarded launch policy."""
+    opt-in of common.hpp); the launch policy is thread_local (one per host
+    thread), nothing process-wide."""
     csrc = os.path.join(ROOT, "swh_trl_amd", "csrc")
     allowed = {("lib.hip", "static std::once_flag once[kMaxDevices];"), ("lib.hip", "static int cus[kMaxDevices];"),
                ("common.hpp", "static std::once_flag once[kMaxDevices];"),
@@ -239,4 +240,68 @@ def test_library_holds_no_hidden_state():
                 found.add((f, code))
     assert found == allowed, found ^ allowed
     lib_src = open(os.path.join(csrc, "lib.hip")).read()
-    assert "std::lock_guard<std::mutex>" in lib_src and "std::call_once" in lib_src
+    assert "thread_local swh_launch_policy" in lib_src and "std::call_once" in lib_src
+    assert "g_policy" not in lib_src and "std::mutex" not in lib_src
+
+
+def test_launch_policy_is_per_thread(lib):
+    """Two host threads hold their own launch policies: a thread's set does not
+    reach another thread, a new thread starts at the defaults, and each thread
+    reads back exactly what it set (include/swh_trl_amd.h: no process-wide
+    mutable state)."""
+    import threading
+
+    from swh_trl_amd import _lib
+    d = _lib.LaunchPolicy()
+    lib.swh_launch_policy_default(ctypes.byref(d))
+    default = {f: getattr(d, f) for f, _ in _lib.LaunchPolicy._fields_}
+    before = _lib.get_launch_policy()
+    barrier = threading.Barrier(2, timeout=30)
+    seen, errors = {}, []
+
+    def worker(name, fields):
+        try:
+            seen[name + ".start"] = _lib.get_launch_policy()
+            _lib.set_launch_policy(**fields)
+            barrier.wait()  # both threads have set theirs
+            for _ in range(100):
+                p = _lib.get_launch_policy()
+                assert all(p[k] == v for k, v in fields.items()), (name, p)
+            barrier.wait()
+            seen[name + ".end"] = _lib.get_launch_policy()
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    ta = threading.Thread(target=worker, args=("a", {"xstream": 0, "wide_cb": 1, "attn_pair": 0}))
+    tb = threading.Thread(target=worker, args=("b", {"xstream": 1, "wide_cb": 2, "filt_wgs": 512}))
+    ta.start()
+    tb.start()
+    ta.join()
+    tb.join()
+    assert not errors, errors
+    assert seen["a.start"] == default and seen["b.start"] == default
+    assert seen["a.end"]["wide_cb"] == 1 and seen["b.end"]["wide_cb"] == 2 and seen["b.end"]["attn_pair"] == 1
+    assert _lib.get_launch_policy() == before  # this thread untouched
+
+
+def test_product_reads_no_environment():
+    """The product's configuration is explicit (engine/options.py EngineOptions,
+    the per-thread launch policy, call arguments): no module under swh_trl_amd/
+    reads os.environ / os.getenv, except dist.py's launcher contract
+    (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*, torchrun's)."""
+    import ast
+    pkg = os.path.join(ROOT, "swh_trl_amd")
+    bad = []
+    for dirpath, _, files in os.walk(pkg):
+        for fn in files:
+            if not fn.endswith(".py"):
+                continue
+            path = os.path.join(dirpath, fn)
+            rel = os.path.relpath(path, ROOT)
+            if rel == os.path.join("swh_trl_amd", "dist.py"):
+                continue
+            for node in ast.walk(ast.parse(open(path).read())):
+                if isinstance(node, ast.Attribute) and node.attr in ("environ", "getenv", "putenv") and \
+                        isinstance(node.value, ast.Name) and node.value.id == "os":
+                    bad.append(f"{rel}:{node.lineno}")
+    assert not bad, bad

@@ -85,7 +85,7 @@ def test_dp_groups_straddling_ranks():
     assert got[0][2] == got[1][2]
 
 
-def _oracle_worker(rank, world, port, q, out_dir, pdb, ga, loss_type):
+def _oracle_worker(rank, world, port, q, out_dir, pdb, ga, loss_type, G=4):
     """One fp32 GRPO step on this rank; saves its rollout, shuffle permutation, the
     all-reduced gradient and its log line for the parent's oracle check."""
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
@@ -99,7 +99,7 @@ def _oracle_worker(rank, world, port, q, out_dir, pdb, ga, loss_type):
         def rew(prompts=None, completions=None, completion_ids=None, **kw):
             return [float(len(set(c)) % 5) for c in completion_ids]
 
-        args = GRPOConfig(per_device_train_batch_size=pdb, gradient_accumulation_steps=ga, num_generations=4,
+        args = GRPOConfig(per_device_train_batch_size=pdb, gradient_accumulation_steps=ga, num_generations=G,
                           max_prompt_length=8, max_completion_length=16, max_steps=1, learning_rate=1e-3,
                           lr_scheduler_type="constant", loss_type=loss_type, shuffle_dataset=False,
                           generation_kwargs={"eos_token_id": 1, "pad_token_id": 0, "min_new_tokens": 4},
@@ -137,23 +137,25 @@ def _oracle_worker(rank, world, port, q, out_dir, pdb, ga, loss_type):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("pdb,ga,loss_type", [(8, 2, "bnpo"), (2, 1, "bnpo"), (4, 2, "grpo")],
-                         ids=["whole-groups-bnpo", "straddling-bnpo", "whole-groups-grpo"])
-def test_dp_averaged_gradient_equals_mean_of_oracle_rank_gradients(tmp_path, pdb, ga, loss_type):
-    """two fp32 ranks, one step.  The gradient each rank holds after the
+@pytest.mark.parametrize("world,pdb,ga,G,loss_type", [(2, 8, 2, 4, "bnpo"), (2, 2, 1, 4, "bnpo"), (2, 4, 2, 4, "grpo"),
+                                                      (4, 16, 4, 8, "bnpo")],
+                         ids=["whole-groups-bnpo", "straddling-bnpo", "whole-groups-grpo", "bench-split-4-ranks"])
+def test_dp_averaged_gradient_equals_mean_of_oracle_rank_gradients(tmp_path, world, pdb, ga, G, loss_type):
+    """fp32 ranks, one step.  The gradient each rank holds after the
     overlapped all-reduce equals the mean over ranks of the oracle's gradient on that
     rank's own split (oracle/grpo_step.py grpo_train): rewards gathered across ranks,
     advantages on the global batch sliced per rank (grpo_trainer.py:1497, :1933-1938;
     pdb 2 with G 4 puts every group across both ranks) and the loss normalised by the
     rank-local token count under bnpo (grpo_config.py:500-503).  The loss metrics of
-    the log are the reference's cross-rank gathers: both ranks log the same values."""
+    the log are the reference's cross-rank gathers: every rank logs the same values.
+    bench-split-4-ranks: four ranks at the bench's per-rank split (8 prompts x G 8 = 64
+    rows per rank, micro-batch 16 x GA 4), the 4-rank case of cfg4's data path."""
     from oracle import grpo_step as og
     from swh_trl_amd.engine import tiny_qwen2
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 33500 + (os.getpid() % 1000) + 13 * pdb + ga
-    ps = [ctx.Process(target=_oracle_worker, args=(r, world, port, q, str(tmp_path), pdb, ga, loss_type))
+    port = 33500 + (os.getpid() % 1000) + 13 * pdb + ga + 101 * world
+    ps = [ctx.Process(target=_oracle_worker, args=(r, world, port, q, str(tmp_path), pdb, ga, loss_type, G))
           for r in range(world)]
     for p in ps:
         p.start()
@@ -162,9 +164,10 @@ def test_dp_averaged_gradient_equals_mean_of_oracle_rank_gradients(tmp_path, pdb
         p.join(timeout=60)
     assert all(v == "ok" for v in got.values()), got
     runs = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
-    assert runs[0]["log"] == runs[1]["log"]
-    for k in runs[0]["grads"]:
-        assert torch.equal(runs[0]["grads"][k], runs[1]["grads"][k]), k  # one averaged gradient
+    for r in range(1, world):
+        assert runs[0]["log"] == runs[r]["log"]
+        for k in runs[0]["grads"]:
+            assert torch.equal(runs[0]["grads"][k], runs[r]["grads"][k]), k  # one averaged gradient
     all_ids = torch.cat([r["gen"]["completion_ids"] for r in runs])
 
     def rew(cids, cmask):
@@ -179,7 +182,7 @@ def test_dp_averaged_gradient_equals_mean_of_oracle_rank_gradients(tmp_path, pdb
         g = {"prompt_ids": run["gen"]["prompt_ids"], "prompt_mask": run["gen"]["prompt_mask"].long(),
              "completion_ids": run["gen"]["completion_ids"], "perm": run["perm"], "world_completion_ids": all_ids,
              "rank": r}
-        rec = og.grpo_train(hf, opt, [g], rew, num_generations=4, C=16, per_device_train_batch_size=pdb,
+        rec = og.grpo_train(hf, opt, [g], rew, num_generations=G, C=16, per_device_train_batch_size=pdb,
                             gradient_accumulation_steps=ga, n_steps=1, eos_token_id=1, loss_type=loss_type,
                             capture=True)[0]
         torch.testing.assert_close(run["gen"]["advantages"], rec["gens"][0]["a"], rtol=0, atol=1e-6)
@@ -187,7 +190,7 @@ def test_dp_averaged_gradient_equals_mean_of_oracle_rank_gradients(tmp_path, pdb
     for k, mine in runs[0]["grads"].items():
         if k not in per_rank[0]:
             continue
-        want = (per_rank[0][k] + per_rank[1][k]) / 2
+        want = sum(p[k] for p in per_rank) / world
         rel = ((mine.float() - want).norm() / want.norm().clamp_min(1e-20)).item()
         assert rel <= 1e-3, (k, rel)
 
@@ -252,22 +255,24 @@ def test_dp_resume_restores_each_rank_state(tmp_path):
     assert res[0] == res[1] == full[0]
 
 
-def test_bench_launches_n_ranks_itself():
-    """`python bench.py --gpus 2` (no torchrun environment) starts two ranks
-    itself; rank 0 prints one line with n_gpus 2 and the world size the process
-    group reports.  gloo here: RCCL needs one GPU per rank and this box has one."""
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_launches_n_ranks_itself(n):
+    """`python bench.py --gpus N` (no torchrun environment) starts N ranks itself;
+    rank 0 prints one line with n_gpus N and the world size the process group
+    reports.  gloo here, every rank on the one GPU of this box: RCCL needs one GPU
+    per rank.  Weak scaling: the global batch is N x 64 rows."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, SWH_DIST_BACKEND="gloo")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)
-    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--layers", "2", "--steps", "1", "--warmup", "1",
-                        "--no-cpu-baseline"], cwd=root, env=env, capture_output=True, text=True, timeout=600)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", str(n), "--layers", "2", "--steps", "1", "--warmup",
+                        "1", "--no-cpu-baseline"], cwd=root, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     line = json.loads(lines[0])
-    assert line["n_gpus"] == 2 and line["ranks_seen"] == 2 and line["backend"] == "gloo"
-    assert line["config"]["global_batch"] == 128 and line["value"] > 0
+    assert line["n_gpus"] == n and line["ranks_seen"] == n and line["backend"] == "gloo"
+    assert line["config"]["global_batch"] == 64 * n and line["value"] > 0
 
 
 def _rccl_worker(port, q):

@@ -18,6 +18,12 @@ def dev():
     return torch.device("cuda:0")
 
 
+def _opts(**kw):
+    """EngineOptions with the given fields (the engine's explicit configuration)."""
+    from swh_trl_amd.engine.options import EngineOptions
+    return EngineOptions(**kw)
+
+
 def _tiny(dev, seed=0, layers=2, vocab=1024):
     from swh_trl_amd.engine import CausalLM, tiny_qwen2
     cfg = tiny_qwen2(vocab, layers)
@@ -95,18 +101,18 @@ def test_decode_graph_equals_eager_and_full_forward(dev):
     assert agree.all(), (~agree).nonzero()[:5]
 
 
-def test_fused_decode_step_matches_unfused(dev, monkeypatch):
+def test_fused_decode_step_matches_unfused(dev):
     """The 5-kernel fused decode layer equals the unfused (hipBLASLt + separate
     norm/SiLU/residual) step on the same state, within bf16 rounding."""
     from swh_trl_amd.engine import DecodeEngine
-    monkeypatch.setenv("SWH_FUSED_SAMPLE", "0")  # keep the logits of the decode step
     m = _tiny(dev, seed=7, layers=2)
     B, P, C = 6, 9, 4
     ids = torch.randint(0, m.cfg.vocab_size, (B, P), device=dev)
     mask = torch.ones(B, P, dtype=torch.int32, device=dev)
     outs = []
     for fused in (True, False):
-        e = DecodeEngine(m, B, P, C, use_graph=False, fused=fused)
+        e = DecodeEngine(m, B, P, C, use_graph=False, fused=fused,
+                         options=_opts(fused_sample=False))  # keep the logits of the decode step
         assert e.fused == fused
         e.generate(ids, mask, 2, greedy=True)  # prefill + one decode step
         outs.append(e.logits_buf.float().clone())
@@ -115,7 +121,7 @@ def test_fused_decode_step_matches_unfused(dev, monkeypatch):
 
 
 @pytest.mark.parametrize("kw", [dict(greedy=True), dict(temperature=0.9, min_new_tokens=3)])
-def test_fused_sampler_generation_equals_logits_path(dev, monkeypatch, kw):
+def test_fused_sampler_generation_equals_logits_path(dev, kw):
     """Whole graph-captured generations: lm head + sampler fused (no logits)
     and lm head -> logits -> sample_step draw identical token sequences."""
     from swh_trl_amd.engine import DecodeEngine
@@ -126,8 +132,7 @@ def test_fused_sampler_generation_equals_logits_path(dev, monkeypatch, kw):
     mask = torch.ones(B, P, dtype=torch.int32, device=dev)
     outs = []
     for flag in ("1", "0"):
-        monkeypatch.setenv("SWH_FUSED_SAMPLE", flag)
-        e = DecodeEngine(m, B, P, C)
+        e = DecodeEngine(m, B, P, C, options=_opts(fused_sample=flag == "1"))
         assert e._fused_sample() == (flag == "1") or not e.fused
         toks, _ = e.generate(ids, mask, C, seed=5, eos_token_id=2, pad_token_id=0, **kw)
         outs.append(toks)
@@ -167,14 +172,13 @@ def _greedy_divergence_report(m, ids, mine, ref, max_ulps):
 
 @pytest.mark.parametrize("shape", ["tiny", "qwen2.5-0.5b-width"])
 @pytest.mark.parametrize("fold", ["1", "0"])
-def test_greedy_matches_transformers_generate(dev, monkeypatch, shape, fold):
+def test_greedy_matches_transformers_generate(dev, shape, fold):
     """Greedy ids vs transformers bf16 generate: equal up to the first step
     whose two candidate logits are a bf16 tie (<= 2 ulps apart in fp32), at the
     tiny preset and at the real Qwen2.5-0.5B width (H 896, V 151936, 14:2
     heads, 2 layers); folded decode RMSNorm (default) and the exact form."""
     from swh_trl_amd.engine import CausalLM, DecodeEngine
     from swh_trl_amd.engine.config import DecoderConfig
-    monkeypatch.setenv("SWH_DECODE_FOLD", fold)
     if shape == "tiny":
         m = _tiny(dev, seed=3)
         B, P, C = 4, 10, 32
@@ -185,7 +189,7 @@ def test_greedy_matches_transformers_generate(dev, monkeypatch, shape, fold):
     g = torch.Generator().manual_seed(3)
     ids = torch.randint(0, m.cfg.vocab_size, (B, P), generator=g).to(dev)
     mask = torch.ones(B, P, dtype=torch.int64, device=dev)
-    eng = DecodeEngine(m, B, P, C)
+    eng = DecodeEngine(m, B, P, C, options=_opts(fold_norm=fold == "1"))
     mine, _ = eng.generate(ids, mask, C, greedy=True)
     with torch.no_grad():
         ref = hf.generate(input_ids=ids, attention_mask=mask, max_new_tokens=C, do_sample=False,
@@ -333,7 +337,7 @@ def test_grpo_trainer_smoke(dev):
 
 
 @pytest.mark.parametrize("left_pad", [False, True])
-def test_prefill_dedup_matches_full_prefill(dev, monkeypatch, left_pad):
+def test_prefill_dedup_matches_full_prefill(dev, left_pad):
     """GRPO groups: G copies of each prompt are prefilled once, their K/V
     written to the group's first row, which the decode attention reads for
     every row of the group (`eng.prow`).  The K/V each row attends to and the
@@ -353,8 +357,7 @@ def test_prefill_dedup_matches_full_prefill(dev, monkeypatch, left_pad):
     assert DecodeEngine._unique_prompts(ids, mask) is not None
     outs = {}
     for flag in ("1", "0"):
-        monkeypatch.setenv("SWH_PREFILL_DEDUP", flag)
-        eng = DecodeEngine(m, n * G, P, C)
+        eng = DecodeEngine(m, n * G, P, C, options=_opts(prefill_dedup=flag == "1"))
         eng.state[0], eng.state[1] = 0, P
         eng._prefill(ids, mask)
         kv, lg = eng.kv[:, :, eng.prow.long(), :, :P].clone(), eng.logits_buf.clone()
@@ -396,7 +399,7 @@ def test_layer_grad_hooks_fire_when_layer_grads_are_final(dev):
         assert torch.equal(snaps[i], m.grad[s:e]) and snaps[i].abs().sum() > 0
 
 
-def test_fold_kernel_equals_torch_mul_and_group_dedup(dev, monkeypatch):
+def test_fold_kernel_equals_torch_mul_and_group_dedup(dev):
     """swh_fold_norm (all folded decode weights in one launch) is bit-identical
     to torch's bf16 W * w, and so are the fragment-order copies (folded while
     packing) after unpacking; the group-size hint gives the same prefill plan
@@ -407,14 +410,12 @@ def test_fold_kernel_equals_torch_mul_and_group_dedup(dev, monkeypatch):
     with torch.no_grad():
         for k in ("l0.ln_in", "l1.ln_post", "norm"):
             m.p[k].copy_(1 + 0.1 * torch.randn_like(m.p[k].float()).to(m.p[k].dtype))
-    monkeypatch.setenv("SWH_FRAGW", "0")
-    eng = DecodeEngine(m, 8, 6, 4)
+    eng = DecodeEngine(m, 8, 6, 4, options=_opts(fragw=False))
     eng.refresh_folded()
     p = m.p
     assert torch.equal(eng.fw["l0.qkv_w"], p["l0.qkv_w"] * p["l0.ln_in"])
     assert torch.equal(eng.fw["l1.gu_w"], p["l1.gu_w"] * p["l1.ln_post"])
     assert torch.equal(eng.fw["lm"], m.lm_weight() * p["norm"])
-    monkeypatch.setenv("SWH_FRAGW", "1")
     eng2 = DecodeEngine(m, 8, 6, 4)
     eng2.refresh_folded()
     assert set(eng2.fragw) >= {"l0.qkv_w", "l1.gu_w", "l1.down_w", "lm"} and "l0.qkv_w" not in eng2.fw
@@ -430,8 +431,8 @@ def test_fold_kernel_equals_torch_mul_and_group_dedup(dev, monkeypatch):
     assert torch.equal(ids[rep2][inv2], ids)
 
 
-def test_hip_attention_path_matches_sdpa_path(dev, monkeypatch):
-    """The model with csrc/attn.hip attention (SWH_ATTN=hip) against the SDPA
+def test_hip_attention_path_matches_sdpa_path(dev):
+    """The model with csrc/attn.hip attention (options.hip_attention) against the SDPA
     path: hidden states with left padding and weight gradients agree within
     bf16 tolerance."""
     from swh_trl_amd.engine import CausalLM, tiny_qwen2
@@ -441,8 +442,7 @@ def test_hip_attention_path_matches_sdpa_path(dev, monkeypatch):
     km[1, :9] = 0
     outs = {}
     for mode in ("torch", "hip"):
-        monkeypatch.setenv("SWH_ATTN", mode)
-        m = CausalLM(tiny_qwen2(1024, 2), dev, seed=12, init_std=0.05)
+        m = CausalLM(tiny_qwen2(1024, 2), dev, seed=12, init_std=0.05, options=_opts(hip_attention=mode == "hip"))
         assert m._hip_attn == (mode == "hip")
         m.zero_grad()
         h = m.hidden_states(ids, key_mask=km)
@@ -662,9 +662,9 @@ def test_shared_prompt_forward_matches_per_row(dev, dtype, left_pad):
     assert rel <= tol, rel
 
 
-def test_act_frag_generates_identically(dev, monkeypatch):
+def test_act_frag_generates_identically(dev):
     """The decode step with gate/up writing its activation in fragment order and
-    down_proj reading it register-streamed (SWH_ACT_FRAG=1) generates the same
+    down_proj reading it register-streamed (options.act_frag) generates the same
     tokens and log-probs as the row-major activation."""
     from swh_trl_amd.engine import CausalLM, DecoderConfig, DecodeEngine
     cfg = DecoderConfig(vocab_size=1024, hidden_size=256, intermediate_size=2048, num_hidden_layers=2,
@@ -677,8 +677,7 @@ def test_act_frag_generates_identically(dev, monkeypatch):
     mask = torch.ones(B, P, dtype=torch.int64, device=dev)
     outs = {}
     for flag in ("1", "0"):
-        monkeypatch.setenv("SWH_ACT_FRAG", flag)
-        eng = DecodeEngine(m, B, P, C)
+        eng = DecodeEngine(m, B, P, C, options=_opts(act_frag=flag == "1"))
         assert eng.act_frag == (flag == "1")
         outs[flag] = (eng.generate(ids, mask, C, greedy=True),
                       eng.generate(ids, mask, C, temperature=0.9, seed=3, return_logp=True))
@@ -689,9 +688,9 @@ def test_act_frag_generates_identically(dev, monkeypatch):
                 assert torch.equal(x, y)
 
 
-def test_att_frag_generates_identically(dev, monkeypatch):
+def test_att_frag_generates_identically(dev):
     """The decode step with the attention writing its output in o_proj's
-    fragment order (SWH_ATT_FRAG=1) generates the same tokens and log-probs as
+    fragment order (options.att_frag) generates the same tokens and log-probs as
     the row-major output, greedy and sampled, left padding included."""
     from swh_trl_amd.engine import CausalLM, DecodeEngine, tiny_qwen2
     m = CausalLM(tiny_qwen2(1024, 2), dev, seed=5)
@@ -702,8 +701,7 @@ def test_att_frag_generates_identically(dev, monkeypatch):
     mask[4, :3] = 0
     outs = {}
     for flag in ("1", "0"):
-        monkeypatch.setenv("SWH_ATT_FRAG", flag)
-        eng = DecodeEngine(m, B, P, C)
+        eng = DecodeEngine(m, B, P, C, options=_opts(att_frag=flag == "1"))
         assert eng.att_frag == (flag == "1")
         outs[flag] = (eng.generate(ids, mask, C, greedy=True),
                       eng.generate(ids, mask, C, temperature=0.9, seed=3, return_logp=True))
@@ -714,10 +712,10 @@ def test_att_frag_generates_identically(dev, monkeypatch):
                 assert torch.equal(x, y)
 
 
-def test_fragw_projections_generate_identically(dev, monkeypatch):
+def test_fragw_projections_generate_identically(dev):
     """DecodeEngine with o_proj / down_proj read from fragment-order copies
     (swh_frag_pack + swh_decode_gemm_fragw, refreshed every generate()) gives
-    the same tokens and log-probs as the row-major weights (SWH_FRAGW=0),
+    the same tokens and log-probs as the row-major weights (options.fragw False),
     greedy and sampled, also after the weights changed between generations."""
     from swh_trl_amd.engine import CausalLM, DecodeEngine, tiny_qwen2
     m = CausalLM(tiny_qwen2(1024, 2), dev, seed=7)
@@ -728,8 +726,7 @@ def test_fragw_projections_generate_identically(dev, monkeypatch):
     mask[2, :5] = 0
     outs = {}
     for flag in ("1", "0"):
-        monkeypatch.setenv("SWH_FRAGW", flag)
-        eng = DecodeEngine(m, B, P, C)
+        eng = DecodeEngine(m, B, P, C, options=_opts(fragw=flag == "1"))
         assert ("l1.down_w" in eng.fragw and "l0.o_w" in eng.fragw) == (flag == "1")
         greedy = eng.generate(ids, mask, C, greedy=True)
         sampled = eng.generate(ids, mask, C, temperature=0.9, seed=11)
@@ -750,11 +747,11 @@ def test_fragw_projections_generate_identically(dev, monkeypatch):
 
 
 @pytest.mark.parametrize("kmin", ["2048", "1024"])
-def test_packed_wide_projections_generate_identically(dev, monkeypatch, kmin, launch_policy):
+def test_packed_wide_projections_generate_identically(dev, kmin, launch_policy):
     """DecodeEngine with the bandwidth-regime projections on packed weights
-    (swh_wide_pack + swh_wide_gemm_packed; SWH_WIDE_KMIN 2048 packs down,
+    (swh_wide_pack + swh_wide_gemm_packed; launch policy wide_kmin 2048 packs down,
     1024 packs every projection and the lm head) generates the same tokens and
-    log-probs as the row-major weights (SWH_WIDE_PACK=0), greedy and sampled."""
+    log-probs as the row-major weights (options.wide_pack False), greedy and sampled."""
     from swh_trl_amd.engine import DecodeEngine
     m = _tiny_llama(dev, seed=5)
     g = torch.Generator().manual_seed(5)
@@ -765,8 +762,7 @@ def test_packed_wide_projections_generate_identically(dev, monkeypatch, kmin, la
     launch_policy(wide_kmin=int(kmin))
     outs = {}
     for pack in ("1", "0"):
-        monkeypatch.setenv("SWH_WIDE_PACK", pack)
-        eng = DecodeEngine(m, B, P, C)
+        eng = DecodeEngine(m, B, P, C, options=_opts(wide_pack=pack == "1"))
         if pack == "1":
             assert "l0.down_w" in eng.packed and (kmin == "2048") == ("l0.qkv_w" not in eng.packed)
         else:
@@ -804,10 +800,10 @@ def test_graph_recapture_after_generation_is_clean(dev):
     assert torch.equal(out, out2) and torch.equal(lp, lp2)
 
 
-def test_shared_prompt_kv_generates_identically(dev, monkeypatch):
+def test_shared_prompt_kv_generates_identically(dev):
     """GRPO groups (G copies of each prompt, left padding in one group): the
     decode attention reading each group's prompt K/V from one row
-    (SWH_DECODE_SHARED_KV, default) generates the same tokens and log-probs as
+    (options.shared_kv, default) generates the same tokens and log-probs as
     every row keeping its own copy."""
     from swh_trl_amd.engine import DecodeEngine
     m = _tiny(dev, seed=13, layers=2)
@@ -818,8 +814,7 @@ def test_shared_prompt_kv_generates_identically(dev, monkeypatch):
     mask[G:2 * G, :3] = 0
     outs = {}
     for shared in ("1", "0"):
-        monkeypatch.setenv("SWH_DECODE_SHARED_KV", shared)
-        eng = DecodeEngine(m, U * G, P, C)
+        eng = DecodeEngine(m, U * G, P, C, options=_opts(shared_kv=shared == "1"))
         r = (eng.generate(ids, mask, C, temperature=0.9, seed=3, group_size=G),
              eng.generate(ids, mask, C, temperature=0.9, seed=4, return_logp=True, group_size=G))
         if shared == "1":
@@ -935,7 +930,7 @@ def test_generation_is_run_to_run_deterministic(dev):
         assert len(hs) == 1, (kw, hs)
 
 
-def test_attn_l3_warmup_generates_identically(dev, monkeypatch):
+def test_attn_l3_warmup_generates_identically(dev):
     """The attention launch carrying Infinity Cache warm-up workgroups
     (swh_attn_decode_l3: o / down of this layer, qkv of the next) generates the
     same tokens and log-probs as the plain attention launch."""
@@ -948,9 +943,7 @@ def test_attn_l3_warmup_generates_identically(dev, monkeypatch):
     mask[5, :4] = 0
     outs = {}
     for nwg, sel in (("128", "o,down,qkv1"), ("37", "gu,o1,down1"), ("0", "")):
-        monkeypatch.setenv("SWH_DECODE_L3_ATTN", nwg)
-        monkeypatch.setenv("SWH_DECODE_L3_SET", sel)
-        eng = DecodeEngine(m, B, P, C)
+        eng = DecodeEngine(m, B, P, C, options=_opts(l3_attn=int(nwg), l3_set=sel))
         outs[nwg] = (eng.generate(ids, mask, C, greedy=True),
                      eng.generate(ids, mask, C, temperature=0.9, seed=3, return_logp=True))
         del eng
@@ -963,7 +956,7 @@ def test_attn_l3_warmup_generates_identically(dev, monkeypatch):
 
 def test_lm_ring14_generates_identically(dev, launch_policy):
     """The fused lm-head sampler with the half-tile weight ring and 12 waves
-    per workgroup (SWH_LM_RING14=1, K = 896) draws the same tokens as the
+    per workgroup (launch policy lm_ring14, K = 896) draws the same tokens as the
     whole-tile ring, greedy and sampled, across several tiles per wave."""
     from swh_trl_amd.engine import CausalLM, DecoderConfig, DecodeEngine
     cfg = DecoderConfig(vocab_size=65536, hidden_size=896, intermediate_size=1024, num_hidden_layers=1,

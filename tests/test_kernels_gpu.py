@@ -1336,7 +1336,7 @@ def test_decode_gemm_folded_norm(ops, dev, M, N, K, silu):
 @pytest.mark.parametrize("M,N,K", [(64, 896, 896), (64, 896, 4864), (37, 896, 4864), (5, 256, 512), (64, 896, 2048)])
 def test_xstream_residual_equals_lds_image_kernel(ops, dev, M, N, K, launch_policy):
     """o_proj / down_proj with X fragments streamed into registers
-    (xstream_gemm_kernel) vs decode_gemm_kernel's LDS image (SWH_XSTREAM=0):
+    (xstream_gemm_kernel) vs decode_gemm_kernel's LDS image (launch policy xstream 0):
     the new residual rows and their chunk sums of squares are bit-identical
     (same k split, same wave merge tree), and equal the fp32 reference within
     bf16 rounding."""
@@ -1371,7 +1371,7 @@ def test_decode_gemm_fragw_equals_row_major(ops, dev, M, N, K, kind, cfg, launch
     and swh_decode_gemm_fragw on it bit-identical to swh_decode_gemm on the
     row-major weight: residual + chunk sums of squares (o / down), folded norm
     + bias (qkv), plain — under the cost model's geometry and forced split-K /
-    32-row / persistent ones (SWH_GEMM_CFG)."""
+    32-row / persistent ones (launch policy gemm_cfg)."""
     from swh_trl_amd import nn_ops
     g = _gen(53)
     x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
@@ -1438,7 +1438,7 @@ def test_act_frag_gate_up_to_down_equals_row_major(ops, dev, M):
 def test_xstream_qkv_equals_lds_image_kernel(ops, dev, M, N, K, launch_policy):
     """The qkv projection (folded RMSNorm row scale from the producer's chunk
     sums, bias) with X fragments streamed into registers equals
-    decode_gemm_kernel's LDS-image form bit for bit (SWH_XSTREAM=0), and the
+    decode_gemm_kernel's LDS-image form bit for bit (launch policy xstream 0), and the
     reference within the fold's rounding."""
     from swh_trl_amd import nn_ops
     g = _gen(47)
@@ -1697,7 +1697,7 @@ def test_wide_gemm_packed_rejects_ineligible(ops, dev):
 @pytest.mark.parametrize("name,N,K", [("gate_up", 14336, 4096), ("lm_head", 128256, 4096), ("plain", 16384, 2048)])
 def test_wide_gemm_tilings_agree(ops, dev, name, N, K, launch_policy):
     """The two wide_gemm tilings (128 and 256 weight rows per workgroup,
-    SWH_WIDE_CB=1/2) compute the same GEMM: they differ only in the K split,
+    policy wide_cb 1/2) compute the same GEMM: they differ only in the K split,
     i.e. in fp32 summation order."""
     from swh_trl_amd import nn_ops
     g = _gen(37)
@@ -1891,3 +1891,51 @@ def test_gemm_tn_partials_row_order_and_splits(dev):
     c = torch.zeros(256, 384, device=dev)
     nn_ops.gemm_tn_accumulate(c, dy, x, 2)
     torch.testing.assert_close(c, a, rtol=1e-5, atol=1e-6)
+
+
+def test_two_threads_with_different_policies_keep_their_own_results(ops, dev):
+    """The launch policy is per host thread: two threads launching the same
+    wide_gemm concurrently on their own streams, one under wide_cb 1 and one
+    under wide_cb 2 (different K splits, so different fp32 summation orders),
+    each reproduce bit for bit the result their policy gives single-threaded,
+    every repetition."""
+    import threading
+
+    from swh_trl_amd import _lib, nn_ops
+    g = _gen(41)
+    M, N, K = 64, 14336, 4096
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
+    ss = x.float().view(M, K // 16, 16).pow(2).sum(-1).contiguous()
+    w = (torch.randn(2 * N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(dev)
+    wp = nn_ops.wide_pack(w, silu=True)
+    want = {}
+    for cb in (1, 2):
+        with _lib.launch_policy(wide_cb=cb):
+            want[cb] = nn_ops.wide_gemm_packed(x, wp, N, silu=True, ss_in=ss, eps=1e-5)
+    torch.cuda.synchronize()
+    assert not torch.equal(want[1], want[2])  # the policies do change the bits
+    errors, outs = [], {1: [], 2: []}
+    barrier = threading.Barrier(2, timeout=60)
+
+    def worker(cb):
+        try:
+            torch.cuda.set_device(dev)
+            _lib.set_launch_policy(wide_cb=cb)
+            st = torch.cuda.Stream(device=dev)
+            barrier.wait()
+            with torch.cuda.stream(st):
+                for _ in range(20):
+                    outs[cb].append(nn_ops.wide_gemm_packed(x, wp, N, silu=True, ss_in=ss, eps=1e-5))
+            st.synchronize()
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(cb,)) for cb in (1, 2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+    for cb in (1, 2):
+        assert len(outs[cb]) == 20 and all(torch.equal(o, want[cb]) for o in outs[cb]), cb
+    assert _lib.get_launch_policy()["wide_cb"] == 0  # the main thread kept its own (default) policy

@@ -14,6 +14,8 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import _env  # noqa: E402  (tools only: A/B switches from the environment)
+_env.apply()
 
 
 def main():
@@ -21,7 +23,7 @@ def main():
     from swh_trl_amd.engine.config import DecoderConfig
     layers = int(os.environ.get("AB_LAYERS", "4"))
     dev = torch.device("cuda:0")
-    m = CausalLM(DecoderConfig(num_hidden_layers=layers), dev, seed=7, init_std=0.02)
+    m = CausalLM(DecoderConfig(num_hidden_layers=layers), dev, seed=7, init_std=0.02, options=_env.options())
     B, P, C, G = 64, 128, 96, 8
     g = torch.Generator().manual_seed(1234)
     ids = torch.randint(0, m.cfg.vocab_size, (B // G, P), generator=g).repeat_interleave(G, 0).to(dev)

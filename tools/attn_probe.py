@@ -22,6 +22,8 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import _env  # noqa: E402  (tools only: A/B switches from the environment)
+_env.apply()
 SO = os.environ.get("SWH_PROBE_SO", os.path.join(ROOT, "tools", "_probe", "libgemm_probe.so"))
 PHASES = ["issued", "rope", "loop", "merge", "exit"]
 

@@ -15,6 +15,8 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import _env  # noqa: E402  (tools only: A/B switches from the environment)
+_env.apply()
 
 
 def main():
@@ -38,6 +40,7 @@ def main():
                     model_init_kwargs={"torch_dtype": "float32"},
                     generation_kwargs={"min_new_tokens": 16, "eos_token_id": 1, "pad_token_id": 0})
     tr = GRPOTrainer(model=gpt2_config(), reward_funcs=rew, args=gc, train_dataset=ds)
+    tr.model.options = _env.options()
     tr.state.max_steps = args.steps + args.warmup
     for _ in range(args.warmup):
         tr.training_step_group()

@@ -13,6 +13,8 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import _env  # noqa: E402  (tools only: A/B switches from the environment)
+_env.apply()
 
 
 def _time(fn, reps=20, iters=3):
@@ -224,7 +226,7 @@ def main():
 
     t0 = time.time()
     cfg = qwen2_5_0_5b()
-    m = CausalLM(cfg, torch.device("cuda:0"), trainable=False)
+    m = CausalLM(cfg, torch.device("cuda:0"), trainable=False, options=_env.options())
     B, P, C = args.batch, 128, 256
     eng = DecodeEngine(m, B, P, C)
     g = torch.Generator().manual_seed(0)

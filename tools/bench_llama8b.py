@@ -17,6 +17,8 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import _env  # noqa: E402  (tools only: A/B switches from the environment)
+_env.apply()
 
 
 def main():
@@ -60,6 +62,7 @@ def main():
     import threading
     threading.Thread(target=heartbeat, daemon=True).start()
     tr = GRPOTrainer(model=cfg, reward_funcs=rew, args=gc, train_dataset=ds)
+    tr.model.options = _env.options()
     print(f"[llama8b] init {time.perf_counter() - t0:.1f}s, "
           f"{torch.cuda.memory_allocated() / 2**30:.1f} GiB allocated", file=sys.stderr, flush=True)
     tr.state.max_steps = args.steps + args.warmup

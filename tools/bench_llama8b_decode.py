@@ -15,6 +15,8 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import _env  # noqa: E402  (tools only: A/B switches from the environment)
+_env.apply()
 
 
 def main():
@@ -27,7 +29,7 @@ def main():
     from swh_trl_amd.engine import CausalLM, DecodeEngine, llama3_8b
     t0 = time.perf_counter()
     cfg = llama3_8b()
-    m = CausalLM(cfg, torch.device("cuda:0"), seed=0, init_std=0.02)
+    m = CausalLM(cfg, torch.device("cuda:0"), seed=0, init_std=0.02, options=_env.options())
     eng = DecodeEngine(m, args.B, args.P, args.step + 8)
     g = torch.Generator().manual_seed(0)
     G = 1 if args.distinct else 8  # config 5: 8 prompts x G 8 generations per GPU

@@ -16,6 +16,8 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import _env  # noqa: E402  (tools only: A/B switches from the environment)
+_env.apply()
 
 
 def main():
@@ -43,6 +45,7 @@ def main():
                    total_episodes=n, learning_rate=3e-6, stop_token_id=151645, pad_token_id=151643,
                    eos_token_id=151645, seed=0)
     tr = PPOTrainer(pc, None, cfg, None, rm_cfg, ds, cfg)
+    tr.policy_model.options = _env.options()
     tr.state.global_step = 0
     from bench import kernel_roofline
     from swh_trl_amd import profiling

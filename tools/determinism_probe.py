@@ -8,6 +8,8 @@ import tempfile
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import _env  # noqa: E402  (tools only: A/B switches from the environment)
+_env.apply()
 from swh_trl_amd.engine import CausalLM, tiny_qwen2  # noqa: E402
 from swh_trl_amd.trainer import GRPOConfig, GRPOTrainer  # noqa: E402
 from swh_trl_amd.trainer import checkpoint as ck  # noqa: E402
@@ -26,7 +28,8 @@ def run(out, steps, save, resume=None):
                       max_prompt_length=8, max_completion_length=16, max_steps=steps, learning_rate=1e-3,
                       save_steps=1 if save else 10 ** 9, logging_steps=1, seed=3, weight_decay=0.01,
                       generation_kwargs={"eos_token_id": 1, "pad_token_id": 0})
-    tr = GRPOTrainer(model=CausalLM(cfg, dev, seed=4, init_std=0.05), reward_funcs=rew, args=args, train_dataset=ds)
+    tr = GRPOTrainer(model=CausalLM(cfg, dev, seed=4, init_std=0.05, options=_env.options()), reward_funcs=rew, args=args, train_dataset=ds)
+    tr.model.options = _env.options()
     caps = []
     gen = tr._generate_and_score_completions
 

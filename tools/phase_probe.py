@@ -14,6 +14,8 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import _env  # noqa: E402  (tools only: A/B switches from the environment)
+_env.apply()
 
 
 def main():
@@ -32,7 +34,7 @@ def main():
     import dataclasses
     cfg = dataclasses.replace(PRESETS[args.preset](), num_hidden_layers=args.layers)
     dev = torch.device("cuda:0")
-    m = CausalLM(cfg, dev, seed=0)
+    m = CausalLM(cfg, dev, seed=0, options=_env.options())
     g = torch.Generator().manual_seed(0)
     ids = torch.randint(0, cfg.vocab_size, (args.B, args.L), generator=g).to(dev)
     P = args.P

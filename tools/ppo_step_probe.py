@@ -14,6 +14,8 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
+import _env  # noqa: E402  (tools only: A/B switches from the environment)
+_env.apply()
 
 import test_ppo_gpu as T  # noqa: E402
 from oracle import ppo_step, trl_ref  # noqa: E402

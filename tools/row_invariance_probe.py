@@ -21,6 +21,8 @@ import torch
 import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import _env  # noqa: E402  (tools only: A/B switches from the environment)
+_env.apply()
 from swh_trl_amd import gemm_tuning, ops  # noqa: E402
 from swh_trl_amd.engine import build_model  # noqa: E402
 from swh_trl_amd.engine.config import llama3_8b, qwen2_5_0_5b  # noqa: E402
@@ -77,8 +79,8 @@ def probe(name, cfg, U, G, P, C):
     print(f"  logp kernel: permuted rows differing {int((lp2 != lp[perm]).sum())}, entropy off vs on "
           f"{int((lp3 != lp).sum())}", flush=True)
 
-    model = build_model(cfg, dev, seed=3, trainable=True)
-    ref = build_model(cfg, dev, seed=None, trainable=False)
+    model = build_model(cfg, dev, seed=3, trainable=True, options=_env.options())
+    ref = build_model(cfg, dev, seed=None, trainable=False, options=_env.options())
     ref.copy_from(model)
     gg = torch.Generator().manual_seed(5)
     pids = torch.randint(2, V, (U, P), generator=gg).repeat_interleave(G, 0).to(dev)

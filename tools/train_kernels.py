@@ -15,6 +15,8 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import _env  # noqa: E402  (tools only: A/B switches from the environment)
+_env.apply()
 
 
 def main():
@@ -43,6 +45,7 @@ def main():
                     max_prompt_length=P, max_completion_length=C, learning_rate=1e-6, save_strategy="no",
                     max_steps=10, seed=0, generation_kwargs={"eos_token_id": 151645, "pad_token_id": 151643})
     tr = GRPOTrainer(model=cfg, reward_funcs=rew, args=gc, train_dataset=ds)
+    tr.model.options = _env.options()
     dev = tr.device
     prompt = torch.randint(0, cfg.vocab_size, (B // G, P), generator=g).repeat_interleave(G, 0).to(dev)
     comp = torch.randint(0, cfg.vocab_size - 1000, (B, C), generator=g).to(dev)

@@ -16,6 +16,8 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import _env  # noqa: E402  (tools only: A/B switches from the environment)
+_env.apply()
 
 SHAPES = {  # name: (N, K, silu, epilogue)
     "qkv": (6144, 4096, False, "norm"),
