@@ -601,6 +601,26 @@ int swh_lm_head_sample_step_fragw(const void *x, const void *w, int64_t M, int64
                                   int64_t *cur_tokens, const void *embed, void *x_next, float *ss_next,
                                   void *workspace, int64_t workspace_bytes, void *stream);
 
+/* The fused lm-head sampler that also writes the drawn token's log-prob under the
+ * processed distribution, out_logp[b * out_ld + *step] = z - logsumexp(z) over the
+ * row's processed scores z (logits / T with EOS suppression; greedy: the logits),
+ * as swh_sample_step's out_logp does over materialised logits: each tile also
+ * folds a per-row (max, sum e^(z - max)), merged in the finalize; the drawn
+ * score is recovered from its Gumbel key (within one fp32 rounding).  Same draws
+ * as swh_lm_head_sample.  frag_weights 0: W row-major ([V, K], norm_w or ss_in
+ * as swh_lm_head_sample), 1: the frag_pack order (norm_w NULL, ss_in).  embed
+ * NULL: no next-step input and *step is not advanced (swh_lm_head_sample);
+ * otherwise as swh_lm_head_sample_step.  K <= 1024 (the tile kernel) only: K >
+ * 1024 is SWH_E_ARG (logits + swh_sample_step).  Replaces the rollout log-probs
+ * PPO computes from the generation's scores (trl/trainer/utils.py:1092-1094
+ * output_scores, ppo_trainer.py:440 selective_log_softmax of logits / (T + 1e-7))
+ * with no extra pass over the logits. */
+int swh_lm_head_sample_logp(const void *x, const void *w, int64_t M, int64_t V, int64_t K, const void *norm_w,
+                            float eps, const float *ss_in, int32_t frag_weights, const swh_sample_params *params,
+                            const uint64_t *rng, int32_t *step, int32_t *finished, int64_t *out_tokens, int64_t out_ld,
+                            int64_t *cur_tokens, float *out_logp, const void *embed, void *x_next, float *ss_next,
+                            void *workspace, int64_t workspace_bytes, void *stream);
+
 /* swh_attn_decode_shared_frag whose launch also carries >= l3_wgs Infinity Cache
  * warm-up workgroups (rounded up to whole grid rows of Hkv) on the CUs the
  * attention's B x Hkv workgroups leave idle: they read the l3_njobs (<= 8)

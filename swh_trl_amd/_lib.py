@@ -140,6 +140,9 @@ SIGNATURES = {
     "swh_lm_head_sample_step_fragw": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_f32, c_vp, C.POINTER(SampleParams),
                                               c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
                                               c_vp]),
+    "swh_lm_head_sample_logp": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_f32, c_vp, c_i32,
+                                        C.POINTER(SampleParams), c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
+                                        c_vp, c_vp, c_vp, c_i64, c_vp]),
     "swh_decode_gemm": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_f32, c_vp, c_vp, c_i32, c_vp, c_i64,
                                 c_vp, c_vp, c_vp, c_i64, c_vp]),
     "swh_wide_gemm_eligible": (c_i32, [c_i64, c_i64, c_i64, c_i32]),

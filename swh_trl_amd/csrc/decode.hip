@@ -807,7 +807,28 @@ struct LmSample {
     int pstride;
     int fw = 0;    // weights in the swh_frag_pack layout (tile t = 16-row group t)
     int yf = 0;    // SiLU output in the fragment order down_proj's A operand reads (N % 32 == 0)
+    float2 *lpart = nullptr;  // log-prob variants: [M][pstride] (max, sum e^(z - max)) of the processed scores
 };
+
+// Reductions over one 16-lane DPP row (the 16 column lanes of a C-layout row group):
+// quad_perm xor 1, quad_perm xor 2, row_half_mirror, row_mirror.  Every stage pairs
+// lanes symmetrically, so all 16 lanes end with bit-identical values.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_max(float v) {
+    v = fmaxf(v, dpp_f<0xB1>(v));
+    v = fmaxf(v, dpp_f<0x4E>(v));
+    v = fmaxf(v, dpp_f<0x141>(v));
+    return fmaxf(v, dpp_f<0x140>(v));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+    v += dpp_f<0xB1>(v);
+    v += dpp_f<0x4E>(v);
+    v += dpp_f<0x141>(v);
+    return v + dpp_f<0x140>(v);
+}
 
 // KSC: K / 32 at compile time (0 = read from K): with a constant trip count the
 // compiler pipelines the A-fragment LDS reads across k-steps and waits on each
@@ -817,7 +838,10 @@ struct LmSample {
 // tile per wave (the k-steps ks + RD of the same tile, then the next tile's, refill each
 // register), which fits three 12-wave... waves per SIMD: 768-thread workgroups.
 // SAMPLE: 0 a plain GEMM epilogue, 1 the fused sampler, 2 the fused sampler with the
-// temperature division (T != 1)
+// temperature division (T != 1); 3 / 4: 1 / 2 plus the log-normaliser of the processed
+// scores (the drawn token's log-prob, swh_lm_head_sample_logp): per tile and row a
+// 16-lane max and sum of e^(z - max), folded into one running (max, sum) per lane —
+// lane rl owns row 16 (rl >> 2) + 4 g + (rl & 3) — so the state costs two registers
 template <int NM, int EPI, bool BIAS, int SAMPLE, int KSC, int RD = 0>
 __global__ __launch_bounds__(RD ? 768 : 512) void lm_head_kernel(const uint16_t *__restrict__ x, const uint16_t *__restrict__ w,
                                                       int M, int N, int K, const uint16_t *__restrict__ norm_w,
@@ -972,11 +996,13 @@ __global__ __launch_bounds__(RD ? 768 : 512) void lm_head_kernel(const uint16_t 
         lds_barrier();
     }
     // sampler state: per lane the best (key, column) of its 16 rows 16 i + 4 g + e
+    constexpr bool TDIV = SAMPLE == 2 || SAMPLE == 4, LOGP = SAMPLE >= 3;
     float bk[4][4];
     int32_t bi[4][4];
     uint32_t k0 = 0, k1 = 0, clo = 0, chi = 0;
     bool suppress = false;
     float temp = 1.f;
+    float lm_run = kNegInf, ls_run = 0.f;  // LOGP: the owned row's running (max, sum e^(z - max))
     if constexpr (SAMPLE) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -1058,6 +1084,7 @@ __global__ __launch_bounds__(RD ? 768 : 512) void lm_head_kernel(const uint16_t 
                 for (int e = 0; e < 4; ++e)
                     if (e < smp.p.n_eos && col == smp.p.eos_ids[e]) mask_add = kNegInf;
             }
+            float own_m = kNegInf, own_s = 0.f;  // LOGP: this tile's (max, sum) of the lane's owned row
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 U4 rw{0u, 0u, 0u, 0u};
@@ -1066,7 +1093,15 @@ __global__ __launch_bounds__(RD ? 768 : 512) void lm_head_kernel(const uint16_t 
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     float z = round_bf16(acc[i][e] * rsr[i][e]);  // the bf16 logit
-                    if constexpr (SAMPLE == 2) z = z / temp;
+                    if constexpr (TDIV) z = z / temp;
+                    if constexpr (LOGP) {  // the processed score z + mask over the row's 16 tile columns
+                        const float zp = z + mask_add;
+                        const float mx = row16_max(zp);
+                        const float sx = row16_sum(fast_exp(fmaxf(zp - mx, -1.0e4f)));
+                        const bool own = rl == 4 * i + e;
+                        own_m = own ? mx : own_m;
+                        own_s = own ? sx : own_s;
+                    }
                     float key = smp.p.greedy ? z : z - fast_log(-fast_log(u01_from_bits(wd[e])));
                     key += mask_add;
                     // branch-free: a lane's columns grow with t, so the index tie-break only
@@ -1074,6 +1109,13 @@ __global__ __launch_bounds__(RD ? 768 : 512) void lm_head_kernel(const uint16_t 
                     const bool better = (key > bk[i][e]) | ((key == bk[i][e]) & (col < bi[i][e]));
                     bk[i][e] = better ? key : bk[i][e];
                     bi[i][e] = better ? col : bi[i][e];
+                }
+            }
+            if constexpr (LOGP) {  // fold the tile into the owned row's running state
+                if (own_m != kNegInf) {
+                    const float nm = fmaxf(lm_run, own_m);
+                    ls_run = (lm_run == kNegInf ? 0.f : ls_run * fast_exp(lm_run - nm)) + own_s * fast_exp(own_m - nm);
+                    lm_run = nm;
                 }
             }
         } else if constexpr (EPI == EPI_SILU && !SWH_SILU_ST16) {
@@ -1146,7 +1188,9 @@ __global__ __launch_bounds__(RD ? 768 : 512) void lm_head_kernel(const uint16_t 
         // through LDS (the X image is free once every wave is past its tiles):
         // one partial per (row, workgroup) for the finalize
         LmPart *wpart = reinterpret_cast<LmPart *>(xs);  // [NW][64]
+        float2 *wsoft = reinterpret_cast<float2 *>(xs + NW * 64 * sizeof(LmPart));  // LOGP: [NW][64]
         __syncthreads();
+        if constexpr (LOGP) wsoft[wid * 64 + 16 * (rl >> 2) + 4 * g + (rl & 3)] = float2{lm_run, ls_run};
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1172,6 +1216,11 @@ __global__ __launch_bounds__(RD ? 768 : 512) void lm_head_kernel(const uint16_t 
                 if (o.key > bpart.key || (o.key == bpart.key && (uint32_t)o.idx < (uint32_t)bpart.idx)) bpart = o;
             }
             smp.part[(int64_t)(m0 + tid) * smp.pstride + wg] = bpart;
+            if constexpr (LOGP) {
+                SoftState st = soft_init();
+                for (int q = 0; q < NW; ++q) st = soft_merge(st, SoftState{wsoft[q * 64 + tid].x, wsoft[q * 64 + tid].y, 0.f});
+                smp.lpart[(int64_t)(m0 + tid) * smp.pstride + wg] = float2{st.m, st.s1};
+            }
         }
     }
     SWH_GEMM_TRACE(6);
@@ -1192,23 +1241,41 @@ struct LmNext {
 
 // Merge the per-wave partials of a row; EOS / pad bookkeeping as
 // swh_sample_step's finalize (csrc/sampler.hip).
+// LOGP (lpart, out_logp non-null): the row's (max, sum) partials are merged too and
+// out_logp[b, step] = z - max - log(sum) for the drawn column's processed score z,
+// recovered as key + log(-log(u)) of the same Philox draw (the key itself when greedy):
+// within an fp32 rounding of the key (~1e-6 at |z| ~ 10) of the score the logits path sees.
 __global__ __launch_bounds__(256) void lm_sample_finalize_kernel(const LmPart *__restrict__ part, int P,
                                                                  swh_sample_params p, const int32_t *__restrict__ step_p,
                                                                  int32_t *__restrict__ finished,
                                                                  int64_t *__restrict__ out_tokens, int64_t out_ld,
-                                                                 int64_t *__restrict__ cur_tokens, int V, LmNext nx) {
+                                                                 int64_t *__restrict__ cur_tokens, int V, LmNext nx,
+                                                                 const float2 *__restrict__ lpart = nullptr,
+                                                                 float *__restrict__ out_logp = nullptr,
+                                                                 const uint64_t *__restrict__ rng = nullptr) {
     __shared__ float kk[4];
     __shared__ int32_t ii[4];
+    __shared__ float sm[4], ssum[4];
     __shared__ int64_t tok_s;
     const int64_t b = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const bool logp = lpart && out_logp;
     float k = kNegInf;
     int32_t c = 0x7fffffff;
+    SoftState st = soft_init();
     for (int q = tid; q < P; q += 256) {
         const LmPart v = part[b * P + q];
         if (v.key > k || (v.key == k && (uint32_t)v.idx < (uint32_t)c)) {
             k = v.key;
             c = v.idx;
+        }
+        if (logp) st = soft_merge(st, SoftState{lpart[b * P + q].x, lpart[b * P + q].y, 0.f});
+    }
+    if (logp) {
+        st = wave_soft(st);
+        if (lane == 0) {
+            sm[wid] = st.m;
+            ssum[wid] = st.s1;
         }
     }
 #pragma unroll
@@ -1233,6 +1300,20 @@ __global__ __launch_bounds__(256) void lm_sample_finalize_kernel(const LmPart *_
             }
         if (c < 0 || c >= V) c = 0;  // fully masked row (cannot happen with min_tokens_to_keep=1)
         const int32_t step = *step_p;
+        if (logp) {
+            SoftState r = soft_init();
+            for (int q = 0; q < 4; ++q) r = soft_merge(r, SoftState{sm[q], ssum[q], 0.f});
+            float z = k;
+            if (!p.greedy) {
+                const uint64_t seed = rng[0], ctr = rng[1] + (uint64_t)step;
+                const U4 w4 = philox4x32_10(U4{(uint32_t)c, (uint32_t)(b >> 2), (uint32_t)ctr, (uint32_t)(ctr >> 32)},
+                                            (uint32_t)seed, (uint32_t)(seed >> 32));
+                const uint32_t q = (uint32_t)(b & 3);
+                const uint32_t bits = q == 0 ? w4.x : q == 1 ? w4.y : q == 2 ? w4.z : w4.w;
+                z = k + fast_log(-fast_log(u01_from_bits(bits)));
+            }
+            out_logp[b * out_ld + step] = (z - r.m) - fast_log(r.s1);
+        }
         int64_t tok = c;
         if (p.pad_token_id >= 0 && finished[b] != 0) tok = p.pad_token_id;
         bool is_eos = false;
@@ -2124,13 +2205,13 @@ template <int NM, int EPI, bool BIAS, int SAMPLE>
 int launch_lm(dim3 grid, size_t lds, hipStream_t s, const uint16_t *X, const uint16_t *W, int M, int N, int K,
               const uint16_t *NWt, float eps, const float *ss_in, const uint16_t *Bs, uint16_t *Y, int ldy,
               const LmSample &smp) {
-    if constexpr (SAMPLE == 1) {  // the division instantiation when the rows are sampled at T != 1
+    if constexpr (SAMPLE == 1 || SAMPLE == 3) {  // the division instantiation when the rows are sampled at T != 1
         if (!smp.p.greedy && smp.p.temperature != 1.0f)
-            return launch_lm<NM, EPI, BIAS, 2>(grid, lds, s, X, W, M, N, K, NWt, eps, ss_in, Bs, Y, ldy, smp);
+            return launch_lm<NM, EPI, BIAS, SAMPLE + 1>(grid, lds, s, X, W, M, N, K, NWt, eps, ss_in, Bs, Y, ldy, smp);
     }
     switch (K / 32) {
     case 28:
-        if (SAMPLE && lm_ring14())
+        if ((SAMPLE == 1 || SAMPLE == 2) && lm_ring14())  // (the log-prob variants spill at 768 threads)
             return launch_lm_ks<NM, EPI, BIAS, SAMPLE, 28, 14>(grid, lds, s, X, W, M, N, K, NWt, eps, ss_in, Bs, Y, ldy,
                                                                smp);
         return launch_lm_ks<NM, EPI, BIAS, SAMPLE, 28>(grid, lds, s, X, W, M, N, K, NWt, eps, ss_in, Bs, Y, ldy, smp);
@@ -2373,7 +2454,8 @@ extern "C" int swh_frag_pack(const void *w, const void *norm_w, int64_t N, int64
     return frag_pack(w, norm_w, N, K, silu, dst, static_cast<hipStream_t>(stream));
 }
 
-// [partials (M x per x 8 LmPart) | 256 B: the finalize ticket (zero at allocation)]
+// [partials (M x per x 8 LmPart) | 256 B: the finalize ticket (zero at allocation) |
+//  the log-prob variant's (max, sum) partials, M x per x 8 float2]
 static int64_t lm_part_bytes(int64_t M, int64_t V = 0) {
     const int64_t nmt = (M + 63) / 64, per = cu_count() / nmt > 0 ? cu_count() / nmt : 1;
     const int64_t wide = V / 256 + 1;  // the wide sampler's partials per row (K > 1024)
@@ -2382,15 +2464,16 @@ static int64_t lm_part_bytes(int64_t M, int64_t V = 0) {
 
 extern "C" int64_t swh_lm_head_sample_workspace_bytes(int64_t M, int64_t V, int64_t K) {
     (void)K;
-    return lm_part_bytes(M, V) + 256;
+    return 2 * lm_part_bytes(M, V) + 256;  // sizeof(float2) == sizeof(LmPart)
 }
 
 static int lm_head_sample_impl(const void *x, const void *w, int64_t M, int64_t V, int64_t K, const void *norm_w,
                                float eps, const float *ss_in, const swh_sample_params *params, const uint64_t *rng,
                                const int32_t *step, int32_t *finished, int64_t *out_tokens, int64_t out_ld,
                                int64_t *cur_tokens, void *workspace, int64_t workspace_bytes, LmNext nx, void *stream,
-                               int fw = 0) {
+                               int fw = 0, float *out_logp = nullptr) {
     if (fw && (norm_w || K % 128)) return SWH_E_ARG;  // fragment order: folded weight (ss_in row scale) only
+    if (out_logp && fw && K > 32 * kLmMaxKS) return SWH_E_ARG;  // log-probs: the tile kernel (K <= 1024) only
     // K > 1024 (Llama-3-8B): a fragment-order (= wide_pack order) weight through wide_gemm's
     // 256-row tiles with the sampler epilogue, M <= 64, V % 256 == 0
     const bool wide = fw && K > 32 * kLmMaxKS;
@@ -2421,18 +2504,25 @@ static int lm_head_sample_impl(const void *x, const void *w, int64_t M, int64_t 
     const GemmLds L = gemm_lds(1, 64, 8, (int)K, (int)K, nm, false);
     const dim3 grid((unsigned)(per * nmt));
     LmSample smp{p, rng, step, static_cast<LmPart *>(workspace), (int)per, fw};  // one partial per (row, workgroup)
+    if (out_logp)
+        smp.lpart = reinterpret_cast<float2 *>(static_cast<char *>(workspace) + lm_part_bytes(M, V) + 256);
     const auto *X = static_cast<const uint16_t *>(x);
     const auto *W = static_cast<const uint16_t *>(w);
     const auto *NWt = static_cast<const uint16_t *>(norm_w);
-    const int rc = nm == 1   ? launch_lm<1, EPI_PLAIN, false, true>(grid, (size_t)L.total, s, X, W, (int)M, (int)V, (int)K,
-                                                                   NWt, eps, ss_in, nullptr, nullptr, 0, smp)
-                   : nm == 2 ? launch_lm<2, EPI_PLAIN, false, true>(grid, (size_t)L.total, s, X, W, (int)M, (int)V, (int)K,
-                                                                   nullptr, eps, ss_in, nullptr, nullptr, 0, smp)
-                             : launch_lm<0, EPI_PLAIN, false, true>(grid, (size_t)L.total, s, X, W, (int)M, (int)V, (int)K,
-                                                                   nullptr, eps, nullptr, nullptr, nullptr, 0, smp);
+    const size_t lds = (size_t)L.total;
+    const int iM = (int)M, iV = (int)V, iK = (int)K;
+    int rc;
+    if (out_logp)
+        rc = nm == 1   ? launch_lm<1, EPI_PLAIN, false, 3>(grid, lds, s, X, W, iM, iV, iK, NWt, eps, ss_in, nullptr, nullptr, 0, smp)
+             : nm == 2 ? launch_lm<2, EPI_PLAIN, false, 3>(grid, lds, s, X, W, iM, iV, iK, nullptr, eps, ss_in, nullptr, nullptr, 0, smp)
+                       : launch_lm<0, EPI_PLAIN, false, 3>(grid, lds, s, X, W, iM, iV, iK, nullptr, eps, nullptr, nullptr, nullptr, 0, smp);
+    else
+        rc = nm == 1   ? launch_lm<1, EPI_PLAIN, false, 1>(grid, lds, s, X, W, iM, iV, iK, NWt, eps, ss_in, nullptr, nullptr, 0, smp)
+             : nm == 2 ? launch_lm<2, EPI_PLAIN, false, 1>(grid, lds, s, X, W, iM, iV, iK, nullptr, eps, ss_in, nullptr, nullptr, 0, smp)
+                       : launch_lm<0, EPI_PLAIN, false, 1>(grid, lds, s, X, W, iM, iV, iK, nullptr, eps, nullptr, nullptr, nullptr, 0, smp);
     if (rc != SWH_OK) return rc;
     lm_sample_finalize_kernel<<<dim3((unsigned)M), 256, 0, s>>>(smp.part, smp.pstride, p, step, finished, out_tokens,
-                                                               out_ld, cur_tokens, (int)V, nx);
+                                                               out_ld, cur_tokens, (int)V, nx, smp.lpart, out_logp, rng);
     return launch_status();
 }
 
@@ -2521,4 +2611,26 @@ extern "C" int swh_lm_head_sample_step_fragw(const void *x, const void *w, int64
                                              int64_t workspace_bytes, void *stream) {
     return lm_head_sample_step_impl(x, w, M, V, K, nullptr, eps, ss_in, params, rng, step, finished, out_tokens,
                                     out_ld, cur_tokens, embed, x_next, ss_next, workspace, workspace_bytes, stream, 1);
+}
+
+// The fused sampler with the drawn token's log-prob under the processed distribution
+// (SAMPLE 3 / 4 of lm_head_kernel): one entry for both weight orders, with or without
+// the next step's input (embed null: none, the step counter is not advanced).
+extern "C" int swh_lm_head_sample_logp(const void *x, const void *w, int64_t M, int64_t V, int64_t K,
+                                       const void *norm_w, float eps, const float *ss_in, int32_t frag_weights,
+                                       const swh_sample_params *params, const uint64_t *rng, int32_t *step,
+                                       int32_t *finished, int64_t *out_tokens, int64_t out_ld, int64_t *cur_tokens,
+                                       float *out_logp, const void *embed, void *x_next, float *ss_next,
+                                       void *workspace, int64_t workspace_bytes, void *stream) {
+    if (!out_logp || (frag_weights & ~1) || K > 32 * kLmMaxKS) return SWH_E_ARG;
+    LmNext nx{};
+    if (embed) {
+        if (!x_next || !cur_tokens || K % 16) return SWH_E_ARG;
+        if ((reinterpret_cast<uintptr_t>(embed) | reinterpret_cast<uintptr_t>(x_next)) & 15) return SWH_E_ARG;
+        if (workspace_bytes < swh_lm_head_sample_workspace_bytes(M, V, K)) return SWH_E_ARG;
+        nx = LmNext{static_cast<const uint16_t *>(embed), static_cast<uint16_t *>(x_next), ss_next, step,
+                    reinterpret_cast<int32_t *>(static_cast<char *>(workspace) + lm_part_bytes(M, V)), (int)K, (int)M};
+    }
+    return lm_head_sample_impl(x, w, M, V, K, norm_w, eps, ss_in, params, rng, step, finished, out_tokens, out_ld,
+                               cur_tokens, workspace, workspace_bytes, nx, stream, frag_weights, out_logp);
 }

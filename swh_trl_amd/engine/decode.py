@@ -244,14 +244,15 @@ class DecodeEngine:
         return self._fused_sample()
 
     def _fused_sample(self) -> bool:
-        """lm head + sampler in one kernel (no logits): unfiltered sampling
-        without the per-token log-prob output."""
+        """lm head + sampler in one kernel (no logits): unfiltered sampling, with
+        the per-token log-prob output too at K <= 1024 (swh_lm_head_sample_logp;
+        PPO's rollout log-probs without the logits write and sample_step)."""
         # K > 1024: the wide-tile sampler (config 5's step 9.744 -> 9.682 s,
         # profiles/r5_wsamp_step_ab.log); options.fused_sample_wide False keeps logits + sample_step
         wide = "lm" in self.packed and self.options.fused_sample_wide
-        return (self.fused and not self.want_logp and self.options.fused_sample and
+        return (self.fused and self.options.fused_sample and
                 nn_ops.lm_head_sample_supported(self.params, self.cfg.vocab_size, self.cfg.hidden_size,
-                                                wide_rows=self.B if wide else 0))
+                                                wide_rows=self.B if wide else 0, logp=self.want_logp))
 
     def _projections(self) -> dict:
         """name -> (N, K, silu, RMSNorm weight name or None) of the decode GEMMs."""
@@ -422,7 +423,8 @@ class DecodeEngine:
             w, nw, fr = self._lm_head_weight()
             nn_ops.lm_head_sample_step(self.s, w, self.params, self.rng, self.state[0:1], self.finished,
                                        self.out, self.cur, p["embed"], self.s, ss, norm_w=nw, eps=eps, ss_in=ss,
-                                       workspace=self.sample_ws, fragw=fr)
+                                       workspace=self.sample_ws, fragw=fr,
+                                       out_logp=self.out_logp if self.want_logp else None)
         else:
             self._proj("lm", self.s, y=self.logits_buf, ss_in=ss)
 

@@ -310,28 +310,41 @@ def wide_gemm_packed(x: torch.Tensor, w_packed: torch.Tensor, N: int, *, eps: fl
     return residual if residual is not None else y
 
 
-def lm_head_sample_supported(params, V: int, K: int, wide_rows: int = 0) -> bool:
+def lm_head_sample_supported(params, V: int, K: int, wide_rows: int = 0, logp: bool = False) -> bool:
     """The fused lm-head sampler covers unfiltered sampling (temperature,
     greedy, EOS suppression); the rest goes through logits + sample_step.
-    K <= 1024: the tile kernel (any weight order); K > 1024: wide_gemm's
-    256-row tiles over a fragment-order (wide_pack) weight, for wide_rows
-    (the batch, <= 64) rows and V % 256 == 0 (wide_rows 0: not available)."""
+    K <= 1024: the tile kernel (any weight order), also with the drawn tokens'
+    log-probs (logp); K > 1024: wide_gemm's 256-row tiles over a fragment-order
+    (wide_pack) weight, for wide_rows (the batch, <= 64) rows and V % 256 == 0
+    (wide_rows 0: not available), without log-probs."""
     filtered = not params.greedy and ((0 < params.top_k < V) or params.top_p < 1.0 or params.min_p > 0.0)
     if filtered or params.repetition_penalty != 1.0 or K % 64 or V % 16:
         return False
     if K <= 1024:
         return True
+    if logp:
+        return False
     return bool(wide_rows) and V % 256 == 0 and wide_gemm_eligible(wide_rows, V, K)
+
+
+def _check_logp_out(out_logp: torch.Tensor, out_tokens: torch.Tensor) -> None:
+    """The log-prob output shares out_tokens' row stride (out_ld) and shape."""
+    if (out_logp.dtype != torch.float32 or out_logp.shape != out_tokens.shape
+            or out_logp.stride() != out_tokens.stride() or out_logp.device != out_tokens.device):
+        raise ValueError("lm_head_sample: out_logp must be fp32 with out_tokens' shape and strides")
 
 
 def lm_head_sample(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Tensor, step: torch.Tensor,
                    finished: torch.Tensor, out_tokens: torch.Tensor, cur_tokens: Optional[torch.Tensor] = None, *,
                    norm_w: Optional[torch.Tensor] = None, eps: float = 1e-6, ss_in: Optional[torch.Tensor] = None,
-                   workspace: Optional[torch.Tensor] = None, fragw: int = 0) -> torch.Tensor:
+                   workspace: Optional[torch.Tensor] = None, fragw: int = 0,
+                   out_logp: Optional[torch.Tensor] = None) -> torch.Tensor:
     """lm head + the unfiltered sampler in one pass, no logits tensor
     (include/swh_trl_amd.h swh_lm_head_sample; fragw 1: w packed by frag_pack,
     or the flat wide_pack copy at K > 1024, swh_lm_head_sample_fragw).  Writes out_tokens[:, *step], cur_tokens,
-    finished; returns out_tokens."""
+    finished; returns out_tokens.  out_logp (fp32, the layout of out_tokens): also the
+    drawn tokens' log-probs under the processed distribution (swh_lm_head_sample_logp,
+    K <= 1024)."""
     import ctypes
     _dev(x, "lm_head_sample")
     M, K = x.shape
@@ -339,9 +352,16 @@ def lm_head_sample(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Tensor, 
     need = _lib.load().swh_lm_head_sample_workspace_bytes(M, V, K)
     if workspace is None or workspace.numel() < need:
         workspace = torch.empty(need, dtype=torch.uint8, device=x.device)
-    head = (x.data_ptr(), w.data_ptr(), M, V, K) + (() if fragw else (_p(norm_w),)) + (float(eps), _p(ss_in))
     if fragw and norm_w is not None:
         raise ValueError("lm_head_sample: a fragment-order weight carries the folded norm (norm_w must be None)")
+    if out_logp is not None:
+        _check_logp_out(out_logp, out_tokens)
+        call("swh_lm_head_sample_logp", x.data_ptr(), w.data_ptr(), M, V, K, _p(norm_w), float(eps), _p(ss_in),
+             int(bool(fragw)), ctypes.byref(params), rng.data_ptr(), step.data_ptr(), finished.data_ptr(),
+             out_tokens.data_ptr(), out_tokens.stride(0), _p(cur_tokens), out_logp.data_ptr(), None, None, None,
+             workspace.data_ptr(), workspace.numel(), _stream())
+        return out_tokens
+    head = (x.data_ptr(), w.data_ptr(), M, V, K) + (() if fragw else (_p(norm_w),)) + (float(eps), _p(ss_in))
     call("swh_lm_head_sample_fragw" if fragw else "swh_lm_head_sample", *head,
          ctypes.byref(params), rng.data_ptr(), step.data_ptr(), finished.data_ptr(), out_tokens.data_ptr(),
          out_tokens.stride(0), _p(cur_tokens), workspace.data_ptr(), workspace.numel(), _stream())
@@ -352,11 +372,13 @@ def lm_head_sample_step(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Ten
                         finished: torch.Tensor, out_tokens: torch.Tensor, cur_tokens: torch.Tensor,
                         embed: torch.Tensor, x_next: torch.Tensor, ss_next: Optional[torch.Tensor], *,
                         norm_w: Optional[torch.Tensor] = None, eps: float = 1e-6, ss_in: Optional[torch.Tensor] = None,
-                        workspace: torch.Tensor, fragw: int = 0) -> torch.Tensor:
+                        workspace: torch.Tensor, fragw: int = 0,
+                        out_logp: Optional[torch.Tensor] = None) -> torch.Tensor:
     """lm_head_sample + the next step's input: x_next = embed[drawn token]
     (+ RMSNorm partials ss_next) and *step += 1 once every row has read it
     (include/swh_trl_amd.h swh_lm_head_sample_step).  `workspace` must have
-    been zeroed once at allocation."""
+    been zeroed once at allocation.  out_logp: the drawn tokens' log-probs too
+    (swh_lm_head_sample_logp, K <= 1024)."""
     import ctypes
     _dev(x, "lm_head_sample_step")
     M, K = x.shape
@@ -365,6 +387,13 @@ def lm_head_sample_step(x: torch.Tensor, w: torch.Tensor, params, rng: torch.Ten
         raise ValueError("lm_head_sample_step: workspace too small")
     if fragw and norm_w is not None:
         raise ValueError("lm_head_sample_step: a fragment-order weight carries the folded norm (norm_w must be None)")
+    if out_logp is not None:
+        _check_logp_out(out_logp, out_tokens)
+        call("swh_lm_head_sample_logp", x.data_ptr(), w.data_ptr(), M, V, K, _p(norm_w), float(eps), _p(ss_in),
+             int(bool(fragw)), ctypes.byref(params), rng.data_ptr(), step.data_ptr(), finished.data_ptr(),
+             out_tokens.data_ptr(), out_tokens.stride(0), cur_tokens.data_ptr(), out_logp.data_ptr(),
+             embed.data_ptr(), x_next.data_ptr(), _p(ss_next), workspace.data_ptr(), workspace.numel(), _stream())
+        return out_tokens
     head = (x.data_ptr(), w.data_ptr(), M, V, K) + (() if fragw else (_p(norm_w),)) + (float(eps), _p(ss_in))
     call("swh_lm_head_sample_step_fragw" if fragw else "swh_lm_head_sample_step", *head,
          ctypes.byref(params), rng.data_ptr(), step.data_ptr(), finished.data_ptr(), out_tokens.data_ptr(),

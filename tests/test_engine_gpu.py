@@ -139,6 +139,32 @@ def test_fused_sampler_generation_equals_logits_path(dev, kw):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("kw", [dict(temperature=1.0 + 1e-7), dict(temperature=0.7, min_new_tokens=3),
+                                dict(greedy=True)])
+def test_fused_sampler_log_probs_equal_logits_path(dev, kw):
+    """return_logp rollouts (PPO, ppo_trainer.py:440): the fused lm-head sampler with
+    the log-prob epilogue (swh_lm_head_sample_logp) draws the same tokens as the
+    logits -> sample_step path and its per-token log-probs agree within 1e-5; the
+    unfused engine path keeps the logits (the reference's selective_log_softmax of
+    logits / (T + 1e-7))."""
+    from swh_trl_amd.engine import DecodeEngine
+    m = _tiny(dev, seed=18, layers=2)
+    B, P, C = 16, 12, 20
+    g = torch.Generator().manual_seed(18)
+    ids = torch.randint(0, m.cfg.vocab_size, (B, P), generator=g).to(dev)
+    mask = torch.ones(B, P, dtype=torch.int32, device=dev)
+    mask[3, :4] = 0
+    outs = []
+    for fused in (True, False):
+        e = DecodeEngine(m, B, P, C, options=_opts(fused_sample=fused))
+        toks, lp = e.generate(ids, mask, C, seed=9, eos_token_id=2, pad_token_id=0, return_logp=True, **kw)
+        assert e._fused_sample() == fused
+        outs.append((toks, lp))
+    assert torch.equal(outs[0][0], outs[1][0])
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-6, atol=1e-5)
+    assert bool((outs[0][1] <= 0).all())
+
+
 def _greedy_divergence_report(m, ids, mine, ref, max_ulps):
     """Greedy ids of the engine vs transformers bf16 generate, row by row.
 

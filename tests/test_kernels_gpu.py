@@ -1255,6 +1255,24 @@ def test_lm_head_sample_equals_logits_then_sampler(ops, dev, kw, M, V, fold):
     assert torch.equal(fin_b, fin_a)
     if kw.get("min_new_tokens", 0) > step:
         assert not torch.isin(out_b[:, step], torch.tensor(eos, device=dev)).any()
+    # the log-prob variant (swh_lm_head_sample_logp): the same draws, and the drawn tokens'
+    # log-probs under the processed distribution as swh_sample_step computes them from
+    # the materialised logits (fp32 summation order and the score recovered from its key)
+    lp_a = torch.zeros(M, 4, dtype=torch.float32, device=dev)
+    out_a2, fin_a2 = torch.full_like(out_a, -1), fin0.clone()
+    ops.sample_step(logits, params, rng, stp, fin_a2, out_a2, torch.empty_like(cur_a), out_logp=lp_a)
+    lp_c = torch.zeros(M, 4, dtype=torch.float32, device=dev)
+    out_c, cur_c, fin_c = torch.full_like(out_a, -1), torch.empty_like(cur_a), fin0.clone()
+    if fold == "fragw":
+        nn_ops.lm_head_sample(x, nn_ops.frag_pack(w), params, rng, stp, fin_c, out_c, cur_c, eps=1e-6, ss_in=ss,
+                              fragw=True, out_logp=lp_c)
+    else:
+        nn_ops.lm_head_sample(x, w, params, rng, stp, fin_c, out_c, cur_c, norm_w=nw, eps=1e-6, ss_in=ss,
+                              out_logp=lp_c)
+    assert torch.equal(out_c, out_a) and torch.equal(cur_c, cur_a) and torch.equal(fin_c, fin_a)
+    assert bool((lp_a[:, step] <= 0).all())
+    torch.testing.assert_close(lp_c[:, step], lp_a[:, step], rtol=1e-6, atol=1e-5)
+    assert torch.equal(lp_c[:, :step], lp_a[:, :step]) and torch.equal(lp_c[:, step + 1:], lp_a[:, step + 1:])
 
 
 @pytest.mark.parametrize("kw", [dict(), dict(temperature=0.7), dict(greedy=True), dict(min_new_tokens=5),
@@ -1895,47 +1913,47 @@ def test_gemm_tn_partials_row_order_and_splits(dev):
 
 def test_two_threads_with_different_policies_keep_their_own_results(ops, dev):
     """The launch policy is per host thread: two threads launching the same
-    wide_gemm concurrently on their own streams, one under wide_cb 1 and one
-    under wide_cb 2 (different K splits, so different fp32 summation orders),
-    each reproduce bit for bit the result their policy gives single-threaded,
-    every repetition."""
+    wide_gemm concurrently on their own streams, one under wide_smax 1 (no K
+    split) and one under wide_smax 8 (the qkv shape split over workgroups, so
+    another fp32 summation order), each reproduce bit for bit the result their
+    policy gives single-threaded, every repetition."""
     import threading
 
     from swh_trl_amd import _lib, nn_ops
     g = _gen(41)
-    M, N, K = 64, 14336, 4096
+    M, N, K = 64, 6144, 4096
     x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
     ss = x.float().view(M, K // 16, 16).pow(2).sum(-1).contiguous()
-    w = (torch.randn(2 * N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(dev)
-    wp = nn_ops.wide_pack(w, silu=True)
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(dev)
+    wp = nn_ops.wide_pack(w)
     want = {}
-    for cb in (1, 2):
-        with _lib.launch_policy(wide_cb=cb):
-            want[cb] = nn_ops.wide_gemm_packed(x, wp, N, silu=True, ss_in=ss, eps=1e-5)
+    for cb in (1, 8):
+        with _lib.launch_policy(wide_smax=cb):
+            want[cb] = nn_ops.wide_gemm_packed(x, wp, N, ss_in=ss, eps=1e-5)
     torch.cuda.synchronize()
-    assert not torch.equal(want[1], want[2])  # the policies do change the bits
-    errors, outs = [], {1: [], 2: []}
+    assert not torch.equal(want[1], want[8])  # the policies do change the bits
+    errors, outs = [], {1: [], 8: []}
     barrier = threading.Barrier(2, timeout=60)
 
     def worker(cb):
         try:
             torch.cuda.set_device(dev)
-            _lib.set_launch_policy(wide_cb=cb)
+            _lib.set_launch_policy(wide_smax=cb)
             st = torch.cuda.Stream(device=dev)
             barrier.wait()
             with torch.cuda.stream(st):
                 for _ in range(20):
-                    outs[cb].append(nn_ops.wide_gemm_packed(x, wp, N, silu=True, ss_in=ss, eps=1e-5))
+                    outs[cb].append(nn_ops.wide_gemm_packed(x, wp, N, ss_in=ss, eps=1e-5))
             st.synchronize()
         except Exception as e:  # noqa: BLE001
             errors.append(repr(e))
 
-    ts = [threading.Thread(target=worker, args=(cb,)) for cb in (1, 2)]
+    ts = [threading.Thread(target=worker, args=(cb,)) for cb in (1, 8)]
     for t in ts:
         t.start()
     for t in ts:
         t.join()
     assert not errors, errors
-    for cb in (1, 2):
+    for cb in (1, 8):
         assert len(outs[cb]) == 20 and all(torch.equal(o, want[cb]) for o in outs[cb]), cb
-    assert _lib.get_launch_policy()["wide_cb"] == 0  # the main thread kept its own (default) policy
+    assert _lib.get_launch_policy()["wide_smax"] == 8  # the main thread kept its own (default) policy
