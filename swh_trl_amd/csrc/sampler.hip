@@ -466,6 +466,225 @@ int choose_split(int64_t B, int64_t V) {
     return S;
 }
 
+// ---------------------------------------------------------------------------
+// Filtered, bf16 logits without a repetition penalty: one top-k or one top-p
+// threshold (min-p as in the general path).  Processing (EOS suppression, / T)
+// is monotone in the bf16 logit, so the threshold is a 16-bit radix select over
+// the order-preserving key of the bf16 BITS (two 8-bit digits, 256 bins) instead
+// of three digits over the fp32 score, and the per-row select runs in the
+// prologue of the pass that needs it — every split workgroup of a row sums the
+// row's S partial histograms in the same fixed order, so all agree — instead of
+// in separate launches: soft, digit 0, digit 1, draw (4 launches + the finalize,
+// against 10).  The kept set, ties at the threshold included, and the draws are
+// those of the general path.
+// ---------------------------------------------------------------------------
+constexpr int kBins16 = 256;
+
+__device__ __forceinline__ uint32_t ord_key16(float x) {  // x holds a bf16 value exactly
+    const uint32_t u = __float_as_uint(x) >> 16;
+    return (u & 0x8000u) ? (~u & 0xffffu) : (u | 0x8000u);
+}
+
+struct Filt16Row {
+    float M, lse;     // row max and log-normaliser of the processed scores
+    float above;      // weight strictly above the selected digit-0 bin
+    int32_t thr;      // the resolved key prefix (digit 0: bin << 8; final: the 16-bit threshold key)
+    int32_t active;   // 0: the filter keeps everything
+};
+
+// The row's (max, lse) from the S soft partials (fixed order).
+__device__ __forceinline__ void row_soft16(const float2 *__restrict__ psoft, int64_t b, int S, float &M, float &lse) {
+    SoftState a = soft_init();
+    for (int q = 0; q < S; ++q) a = soft_merge(a, SoftState{psoft[b * S + q].x, psoft[b * S + q].y, 0.f});
+    M = a.m;
+    lse = a.m + fast_log(a.s1);
+}
+
+// Select over the S partial 256-bin histograms of row b (kSplitThreads == 256 threads,
+// thread t owns bin t): the highest bin whose weight from the top reaches `target`
+// given `above0` above all bins.  Returns the bin (-1: total below target) and the
+// weight strictly above it; `lowest`: the lowest non-empty bin (the level-1 fallback).
+__device__ __forceinline__ int select16(const float *__restrict__ phist, int64_t b, int S, float above0, float target,
+                                        float &above, int &lowest, float *scan, int *sel) {
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6, nw = kSplitThreads >> 6;
+    float h = 0.f;
+    for (int q = 0; q < S; ++q) h += phist[(b * S + q) * (int64_t)kBins16 + t];  // splits in fixed order
+    if (t == 0) {
+        sel[0] = -1;
+        sel[1] = kBins16;
+    }
+    float v = h;  // inclusive suffix scan over lanes (higher lanes = higher bins)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const float u = __shfl_down(v, o, kWave);
+        if (lane + o < 64) v += u;
+    }
+    if (lane == 63) scan[wid] = 0.f;
+    if (lane == 0) scan[wid] = v;
+    __syncthreads();
+    float after = 0.f;
+    for (int w = wid + 1; w < nw; ++w) after += scan[w];
+    const float a = above0 + (v - h) + after;  // weight strictly above bin t
+    if (h > 0.f && a + h >= target) atomicMax(&sel[0], t);
+    if (h > 0.f) atomicMin(&sel[1], t);
+    __syncthreads();
+    const int bin = sel[0];
+    if (bin == t) scan[nw] = a;
+    const int lo = sel[1];
+    if (bin < 0 && lo == t) scan[nw] = a;
+    __syncthreads();
+    above = scan[nw];
+    lowest = lo;
+    const int r = bin;
+    __syncthreads();  // scan / sel are reused by the caller
+    return r;
+}
+
+// Digit LVL's partial histogram over split blockIdx.x.  LVL 0: weights e^(z - lse)
+// (top-p) or 1 (top-k) of the processed scores, binned by the top byte of the key;
+// LVL 1: the prologue resolves digit 0 (and writes the row state once), then bins
+// the low byte of the keys under that prefix.
+template <bool EXPW, int LVL>
+__global__ __launch_bounds__(kSplitThreads) void filt16_hist_kernel(
+    const uint16_t *__restrict__ logits, int64_t V, int64_t ld, swh_sample_params p, const int32_t *__restrict__ step_p,
+    int64_t chunk, const float2 *__restrict__ psoft, const float *__restrict__ phist0, float target,
+    Filt16Row *__restrict__ rows, float *__restrict__ phist) {
+    __shared__ unsigned long long hist[kBins16];
+    __shared__ float scan[kSplitThreads / kWave + 1];
+    __shared__ int sel[2];
+    const int64_t b = blockIdx.y;
+    const int t = threadIdx.x, S = gridDim.x;
+    float M, lse;
+    row_soft16(psoft, b, S, M, lse);
+    int prefix = 0;
+    if constexpr (LVL == 1) {
+        float above;
+        int lowest;
+        const int bin = select16(phist0, b, S, 0.f, target, above, lowest, scan, sel);
+        if (bin < 0) {  // the filter's total weight stays below its target: keep everything
+            if (blockIdx.x == 0 && t == 0) rows[b] = Filt16Row{M, lse, 0.f, 0, 0};
+            return;
+        }
+        prefix = bin;
+        if (blockIdx.x == 0 && t == 0) rows[b] = Filt16Row{M, lse, above, bin << 8, 1};
+    }
+    hist[t] = 0ull;
+    __syncthreads();
+    const Proc pr = make_proc(p, *step_p, nullptr);
+    int64_t beg, end;
+    split_range(V, chunk, beg, end);
+    int run_bin = -1;
+    unsigned long long run_w = 0ull;
+    row_foreach<SWH_BF16, false>(logits + b * ld, beg, end, t, kSplitThreads, [&](int64_t j, float x) {
+        const float z = pr(j, x);
+        if (z == kNegInf) return;
+        const uint32_t k = ord_key16(x);
+        if (LVL == 1 && (int)(k >> 8) != prefix) return;
+        const int bin = LVL == 0 ? (int)(k >> 8) : (int)(k & 0xffu);
+        const unsigned long long w = (unsigned long long)((EXPW ? fast_exp(z - lse) : 1.0f) * kHistScale);
+        if (bin == run_bin) {
+            run_w += w;
+        } else {
+            if (run_bin >= 0) atomicAdd(&hist[run_bin], run_w);
+            run_bin = bin;
+            run_w = w;
+        }
+    });
+    if (run_bin >= 0) atomicAdd(&hist[run_bin], run_w);
+    __syncthreads();
+    phist[(b * S + blockIdx.x) * (int64_t)kBins16 + t] = (float)((double)hist[t] * (1.0 / 1099511627776.0));
+}
+
+// Final pass over split blockIdx.x: the prologue resolves digit 1 (the 16-bit
+// threshold key), then min-p and the Gumbel-max draw among the survivors, with the
+// survivors' (max, sum) for the finalize's log-prob.
+__global__ __launch_bounds__(kSplitThreads) void filt16_draw_kernel(
+    const uint16_t *__restrict__ logits, int64_t V, int64_t ld, swh_sample_params p, const uint64_t *__restrict__ rng,
+    const int32_t *__restrict__ step_p, int64_t chunk, const float2 *__restrict__ psoft, const float *__restrict__ phist1,
+    float target, int filtered, const Filt16Row *__restrict__ rows, Partial *__restrict__ part,
+    float *__restrict__ scores_out) {
+    __shared__ float red[5 * (kSplitThreads / kWave)];
+    __shared__ float scan[kSplitThreads / kWave + 1];
+    __shared__ int sel[2];
+    const int64_t b = blockIdx.y;
+    const int S = gridDim.x;
+    float M, lse;
+    row_soft16(psoft, b, S, M, lse);
+    int thr = -1;  // keys >= thr survive (-1: all)
+    if (filtered) {
+        const Filt16Row r = rows[b];
+        if (r.active) {
+            float above;
+            int lowest;
+            int bin = select16(phist1, b, S, r.above, target, above, lowest, scan, sel);
+            if (bin < 0) bin = lowest < kBins16 ? lowest : 0;
+            thr = r.thr | bin;
+        }
+    }
+    float lo = kNegInf;
+    if (p.min_p > 0.f) lo = M + logf(p.min_p);  // p_j < min_p * p_max  <=>  z_j < M + ln(min_p)
+    const int32_t step = *step_p;
+    const Proc pr = make_proc(p, step, nullptr);
+    const uint64_t seed = rng[0], ctr = rng[1] + (uint64_t)step;
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    int64_t beg, end;
+    split_range(V, chunk, beg, end);
+    SoftState sf = soft_init();
+    float bk = kNegInf;
+    int32_t bi = 0x7fffffff;
+    float *srow = scores_out ? scores_out + b * V : nullptr;
+    row_foreach<SWH_BF16, false>(logits + b * ld, beg, end, threadIdx.x, kSplitThreads, [&](int64_t j, float x) {
+        float z = pr(j, x);
+        if ((int)ord_key16(x) < thr || !(z >= lo)) z = kNegInf;
+        if (srow) srow[j] = z;
+        if (z == kNegInf) return;
+        soft_fold<1>(sf, &z);
+        best_merge(bk, bi, z + gumbel_at(k0, k1, j, b, ctr), (int32_t)j);
+    });
+    block_partial(sf, bk, bi, red);
+    if (threadIdx.x == 0) part[b * S + blockIdx.x] = Partial{sf.m, sf.s1, bk, bi};
+}
+
+// true when the 16-bit path serves these parameters (one threshold, no penalty, bf16)
+inline bool filt16_serves(const swh_sample_params &p, int64_t V) {
+    const bool topk = p.top_k > 0 && p.top_k < V, topp = p.top_p < 1.0f;
+    return p.repetition_penalty == 1.0f && !(topk && topp);
+}
+
+int launch_filtered16(const uint16_t *lg, int64_t B, int64_t V, int64_t ld, const swh_sample_params &p,
+                      const uint64_t *rng, const int32_t *step, void *workspace, float *scores_out, hipStream_t s) {
+    const int target_wgs = launch_policy().filt_wgs;
+    int S = 1;
+    while (S < kFiltSplit && B * S < target_wgs && V / (S * 2) >= 2048) S *= 2;
+    int64_t chunk = (V + S - 1) / S;
+    chunk = (chunk + 7) / 8 * 8;
+    const FiltWs w = filt_ws(workspace, B);
+    Partial *part = static_cast<Partial *>(workspace);
+    auto *rows = reinterpret_cast<Filt16Row *>(w.row);  // sizeof(Filt16Row) <= sizeof(FiltRow)
+    float *h0 = w.hist, *h1 = w.hist + B * kFiltSplit * (int64_t)kBins16;
+    const dim3 gs((unsigned)S, (unsigned)B);
+    filt_soft_kernel<SWH_BF16><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, nullptr, 0, chunk, nullptr, w.soft);
+    const bool topk = p.top_k > 0 && p.top_k < V, topp = p.top_p < 1.0f;
+    const bool filtered = topk || topp;
+    const float target = topk ? (float)p.top_k : p.top_p;
+    if (filtered) {
+        if (topk) {
+            filt16_hist_kernel<false, 0><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, chunk, w.soft, nullptr, target,
+                                                                      rows, h0);
+            filt16_hist_kernel<false, 1><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, chunk, w.soft, h0, target,
+                                                                      rows, h1);
+        } else {
+            filt16_hist_kernel<true, 0><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, chunk, w.soft, nullptr, target,
+                                                                     rows, h0);
+            filt16_hist_kernel<true, 1><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, chunk, w.soft, h0, target,
+                                                                     rows, h1);
+        }
+    }
+    filt16_draw_kernel<<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, rng, step, chunk, w.soft, h1, target,
+                                                    filtered ? 1 : 0, rows, part, scores_out);
+    return S;
+}
+
 template <int DT>
 int launch_filtered(const typename Elem<DT>::T *lg, int64_t B, int64_t V, int64_t ld, const swh_sample_params &p,
                     const uint64_t *rng, const int32_t *step, const uint32_t *seen, int64_t words, void *workspace,
@@ -536,7 +755,10 @@ extern "C" int swh_sample_step(const void *logits, int dtype, int64_t B, int64_t
 #define SWH_SAMPLE_LAUNCH(DTC, TY)                                                                              \
     do {                                                                                                        \
         const TY *lg = static_cast<const TY *>(logits);                                                         \
-        if (filtered) {                                                                                         \
+        if (filtered && DTC == SWH_BF16 && filt16_serves(p, V)) {                                              \
+            S = launch_filtered16(reinterpret_cast<const uint16_t *>(lg), B, V, ld, p, rng, step, workspace,    \
+                                  scores_out, s);                                                               \
+        } else if (filtered) {                                                                                  \
             S = launch_filtered<DTC>(lg, B, V, ld, p, rng, step, seen, words, workspace, scores_out, s);         \
         } else {                                                                                                \
             S = choose_split(B, V);                                                                             \

@@ -595,6 +595,29 @@ def test_filtered_sampler_is_run_to_run_deterministic(ops, dev, kw):
         assert torch.equal(tok, ref[0]) and torch.equal(lp, ref[1])
 
 
+@pytest.mark.parametrize("kw", [dict(top_p=0.9), dict(top_p=0.5, temperature=0.7), dict(top_k=50),
+                                dict(top_k=1000, temperature=1.3), dict(top_p=0.8, min_p=0.05),
+                                dict(top_p=0.95, min_new_tokens=3), dict(top_k=151936)])
+@pytest.mark.parametrize("B,V,scale", [(64, 151936, 3.0), (8, 32000, 0.5), (5, 4096, 8.0)])
+def test_filtered_bf16_path_equals_general_path(ops, dev, kw, B, V, scale):
+    """bf16 logits with one top-k or top-p threshold take the 16-bit-key radix path
+    (csrc/sampler.hip launch_filtered16: 2 digits over the bf16 bits, the per-row
+    selects in the next pass's prologue); the same values as fp32 logits take the
+    general 3-digit path over the fp32 scores.  Kept sets (ties at the threshold
+    included), draws and processed scores are identical, the log-probs agree to
+    fp32 summation order; EOS suppression (min_new_tokens) and a top-k that keeps
+    everything included."""
+    g = _gen(45)
+    logits = (torch.randn(B, V, generator=g) * scale).to(torch.bfloat16)
+    params = ops.make_sample_params(eos_token_ids=[3], **kw)
+    t16, _, lp16, sc16, _ = _run_sampler(ops, dev, logits, params, scores=True)
+    t32, _, lp32, sc32, _ = _run_sampler(ops, dev, logits.float(), params, scores=True)
+    assert torch.equal(torch.isfinite(sc16), torch.isfinite(sc32))
+    assert torch.equal(sc16, sc32)
+    assert torch.equal(t16, t32)
+    torch.testing.assert_close(lp16, lp32, rtol=1e-6, atol=1e-6)
+
+
 def test_sampler_distribution_chi2(ops, dev):
     """Empirical frequencies over 4096 independent draws match softmax(z)."""
     V, N = 16, 4096

@@ -20,13 +20,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--numel", type=int, default=494_032_768)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--weight-decay", type=float, default=0.01)
+    ap.add_argument("--no-clip", action="store_true")
     a = ap.parse_args()
     from swh_trl_amd import _lib
     from swh_trl_amd.optim import FlatAdamW
     _lib.load()
     dev = torch.device("cuda:0")
     n = a.numel
-    opt = FlatAdamW(n, dev, lr=1e-6, weight_decay=0.01, max_grad_norm=1.0, no_decay_ranges=[(0, 4096)])
+    opt = FlatAdamW(n, dev, lr=1e-6, weight_decay=a.weight_decay, max_grad_norm=None if a.no_clip else 1.0,
+                    no_decay_ranges=[(0, 4096)])
     grad = (torch.randn(n, device=dev) * 1e-3).to(torch.bfloat16)
     model = torch.empty(n, device=dev, dtype=torch.bfloat16)
     for _ in range(3):
@@ -46,7 +49,8 @@ def main():
     tn, tu = 1000 * tn / a.reps, 1000 * tu / a.reps
     # step() runs its own grad-norm pass first: the update alone is tu - tn
     upd = tu - tn
-    print(f"lib {os.environ.get('SWH_LIB_PATH', 'main')}: numel {n}: grad-norm {tn:.1f} us "
+    print(f"lib {os.environ.get('SWH_LIB_PATH', 'main')}: numel {n} wd {a.weight_decay} clip {not a.no_clip}: "
+          f"grad-norm {tn:.1f} us "
           f"({2 * n / tn / 1e3:.0f} GB/s), update {upd:.1f} us ({28 * n / upd / 1e3:.0f} GB/s)", flush=True)
 
 
