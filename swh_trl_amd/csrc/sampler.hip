@@ -519,8 +519,7 @@ __device__ __forceinline__ int select16(const float *__restrict__ phist, int64_t
         const float u = __shfl_down(v, o, kWave);
         if (lane + o < 64) v += u;
     }
-    if (lane == 63) scan[wid] = 0.f;
-    if (lane == 0) scan[wid] = v;
+    if (lane == 0) scan[wid] = v;  // the wave's total
     __syncthreads();
     float after = 0.f;
     for (int w = wid + 1; w < nw; ++w) after += scan[w];

@@ -161,7 +161,9 @@ def test_fused_sampler_log_probs_equal_logits_path(dev, kw):
         assert e._fused_sample() == fused
         outs.append((toks, lp))
     assert torch.equal(outs[0][0], outs[1][0])
-    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-6, atol=1e-5)
+    # both log-normalisers are fp32 sums in different orders over scores of this tiny
+    # model's magnitude (|z| ~ 40 greedy): a few fp32 ulps of the scores, not of the log-prob
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-6, atol=4e-5)
     assert bool((outs[0][1] <= 0).all())
 
 
