@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--weight-decay", type=float, default=0.01)
     ap.add_argument("--no-clip", action="store_true")
+    ap.add_argument("--pairs", action="store_true", help="two optimizers alternating (PPO: policy + value)")
     a = ap.parse_args()
     from swh_trl_amd import _lib
     from swh_trl_amd.optim import FlatAdamW
@@ -35,6 +36,25 @@ def main():
     for _ in range(3):
         opt.step(grad, model)
     torch.cuda.synchronize()
+    if a.pairs:  # PPO's two flat buffers stepped back to back, each timed on its own
+        opt2 = FlatAdamW(n, dev, lr=1e-6, weight_decay=a.weight_decay, max_grad_norm=None if a.no_clip else 1.0,
+                         no_decay_ranges=[(0, 4096)])
+        grad2 = grad.clone()
+        model2 = torch.empty_like(model)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        t1 = t2 = 0.0
+        for _ in range(a.reps):
+            ev[0].record()
+            opt.step(grad, model)
+            ev[1].record()
+            opt2.step(grad2, model2)
+            ev[2].record()
+            ev[2].synchronize()
+            t1 += ev[0].elapsed_time(ev[1])
+            t2 += ev[1].elapsed_time(ev[2])
+        t1, t2 = 1000 * t1 / a.reps, 1000 * t2 / a.reps
+        print(f"pairs: step incl. grad-norm: first {t1:.1f} us, second {t2:.1f} us "
+              f"({28 * n / t1 / 1e3:.0f} / {28 * n / t2 / 1e3:.0f} GB/s incl. the norm pass)", flush=True)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     tn = tu = 0.0
     for _ in range(a.reps):
