@@ -302,6 +302,20 @@ __device__ __forceinline__ float u01_from_bits(uint32_t w) {
     return ((float)(w >> 8) + 0.5f) * (1.0f / 16777216.0f);
 }
 
+// Gumbel noise g = -log(-log u) of the uniform u = ((w >> 8) + 0.5) 2^-24 (the sampler
+// stream, oracle/c/philox_ref.c).  For u within a few 2^-24 of 1, v_log_f32(u) returns 0
+// and -log(0) made g = +inf: that element won the draw whatever its logit (about 1 % of
+// the rows of a 151936-wide step).  There -log(u) = -log(1 - d) is taken from its series
+// in d = 1 - u (exact in fp32: ((2^24 - 1 - (w >> 8)) + 0.5) 2^-24), d + d^2/2 + d^3/3,
+// whose next term is below 2^-23 relative for d < 2^-7.
+__device__ __forceinline__ float gumbel_from_bits(uint32_t w) {
+    const uint32_t m = w >> 8;
+    const float u = ((float)m + 0.5f) * (1.0f / 16777216.0f);
+    const float d = ((float)(16777215u - m) + 0.5f) * (1.0f / 16777216.0f);
+    const float t = d < 0.0078125f ? d * fmaf(d, fmaf(d, 1.0f / 3.0f, 0.5f), 1.0f) : -fast_log(u);
+    return -fast_log(t);
+}
+
 // ---- launch helpers -----------------------------------------------------------
 inline int launch_status() { return hipGetLastError() == hipSuccess ? SWH_OK : SWH_E_LAUNCH; }
 

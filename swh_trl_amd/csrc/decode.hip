@@ -1102,7 +1102,7 @@ __global__ __launch_bounds__(RD ? 768 : 512) void lm_head_kernel(const uint16_t 
                         own_m = own ? mx : own_m;
                         own_s = own ? sx : own_s;
                     }
-                    float key = smp.p.greedy ? z : z - fast_log(-fast_log(u01_from_bits(wd[e])));
+                    float key = smp.p.greedy ? z : z + gumbel_from_bits(wd[e]);
                     key += mask_add;
                     // branch-free: a lane's columns grow with t, so the index tie-break only
                     // ever fires against the initial (-inf, INT_MAX) entry
@@ -1310,7 +1310,7 @@ __global__ __launch_bounds__(256) void lm_sample_finalize_kernel(const LmPart *_
                                             (uint32_t)seed, (uint32_t)(seed >> 32));
                 const uint32_t q = (uint32_t)(b & 3);
                 const uint32_t bits = q == 0 ? w4.x : q == 1 ? w4.y : q == 2 ? w4.z : w4.w;
-                z = k + fast_log(-fast_log(u01_from_bits(bits)));
+                z = k - gumbel_from_bits(bits);
             }
             out_logp[b * out_ld + step] = (z - r.m) - fast_log(r.s1);
         }

@@ -74,8 +74,7 @@ __device__ __forceinline__ float gumbel_at(uint32_t k0, uint32_t k1, int64_t j, 
                                k0, k1);
     const int q = (int)(row & 3);
     const uint32_t bits = q == 0 ? w.x : q == 1 ? w.y : q == 2 ? w.z : w.w;
-    const float u = u01_from_bits(bits);
-    return -fast_log(-fast_log(u));
+    return gumbel_from_bits(bits);
 }
 
 // best-key merge: larger key wins, ties -> smaller index (torch.argmax order)

@@ -385,7 +385,7 @@ __global__ __launch_bounds__(64 * W) void wide_gemm_kernel(const uint16_t *__res
             for (int e = 0; e < 4; ++e) {
                 float z = round_bf16(tile[(4 * q + e) * LDT + c] * sc[e]);  // the bf16 logit
                 if constexpr (EPI == WEPI_SAMPLE_T) z = z / temp;
-                float key = smp.p.greedy ? z : z - fast_log(-fast_log(u01_from_bits(wd[e])));
+                float key = smp.p.greedy ? z : z + gumbel_from_bits(wd[e]);
                 key += mask_add;
                 const bool better = (key > bk[e]) | ((key == bk[e]) & (col < bi[e]));
                 bk[e] = better ? key : bk[e];

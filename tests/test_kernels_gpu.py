@@ -618,6 +618,38 @@ def test_filtered_bf16_path_equals_general_path(ops, dev, kw, B, V, scale):
     torch.testing.assert_close(lp16, lp32, rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("kw", [dict(), dict(temperature=0.7), dict(top_p=0.99)])
+def test_sampler_gumbel_near_one_uniform_does_not_win(ops, dev, dtype, kw):
+    """A uniform within a few 2^-24 of 1 made -log(-log u) = +inf in fp32 (v_log_f32
+    returns 0 there), so that element won whatever its logit — about 1 % of the rows of
+    a 151936-wide step.  Rows whose stream holds such a uniform get a -30 logit at that
+    column and +10 at another: the draw must take the +10 column (the float64 Gumbel-max
+    of the oracle does), and its log-prob stays finite."""
+    lib = _oracle_lib()
+    V, seed, offset = 151936, 7, 11
+    rows, cols = [], []
+    for b in range(256):
+        u = _uniforms(lib, seed, offset, b, V)
+        j = int(u.argmax())
+        if float(u[j]) >= 1.0 - 4.0 / 16777216.0:
+            rows.append(b)
+            cols.append(j)
+    assert rows, "no near-one uniform in 256 rows (expected ~4)"
+    B = max(rows) + 1
+    logits = torch.zeros(B, V)
+    win = torch.zeros(B, dtype=torch.int64)
+    for b, j in zip(rows, cols):
+        logits[b, j] = -30.0
+        win[b] = (j + 1) % V
+        logits[b, win[b]] = 10.0
+    tok, _, lp, _, _ = _run_sampler(ops, dev, logits.to(dtype), ops.make_sample_params(**kw), seed=seed, offset=offset)
+    for b, j in zip(rows, cols):
+        assert int(tok[b]) != j, (b, j)
+        assert int(tok[b]) == int(win[b]), (b, int(tok[b]))
+    assert bool(torch.isfinite(lp[rows]).all())
+
+
 def test_sampler_distribution_chi2(ops, dev):
     """Empirical frequencies over 4096 independent draws match softmax(z)."""
     V, N = 16, 4096
