@@ -642,7 +642,7 @@ def test_sampler_gumbel_near_one_uniform_does_not_win(ops, dev, dtype, kw):
     for b, j in zip(rows, cols):
         logits[b, j] = -30.0
         win[b] = (j + 1) % V
-        logits[b, win[b]] = 10.0
+        logits[b, win[b]] = 40.0
     tok, _, lp, _, _ = _run_sampler(ops, dev, logits.to(dtype), ops.make_sample_params(**kw), seed=seed, offset=offset)
     for b, j in zip(rows, cols):
         assert int(tok[b]) != j, (b, j)
