@@ -325,6 +325,15 @@ int swh_dw_reduce(const void *parts, int32_t S, int64_t n, void *grad, int32_t d
  * dimensions multiples of 8 elements, pointers 16-B aligned; else SWH_E_ARG. */
 int swh_gemm_nt(const void *A, const void *B, const void *bias, void *C, int64_t M, int64_t N, int64_t K,
                 int64_t lda, int64_t ldb, int64_t ldc, void *stream);
+/* The same product for the wide projections (gate/up forward, the lm head of the
+ * log-prob pass, the down input gradient against a transposed weight copy):
+ * 256 x 256 tiles, one workgroup per CU, an eight-phase K loop (csrc/tgemm256.hip).
+ * bf16 in and out, fp32 accumulation in ascending K (16-k MFMA steps), so a row's
+ * result does not depend on its tile.  N % 8 == 0, K % 64 == 0, lda / ldb
+ * multiples of 8 and ldc of 4 elements, A / B 16-B and C / bias 8-B aligned,
+ * M * lda and N * ldb < 2^32; else SWH_E_ARG. */
+int swh_gemm_nt256(const void *A, const void *B, const void *bias, void *C, int64_t M, int64_t N, int64_t K,
+                   int64_t lda, int64_t ldb, int64_t ldc, void *stream);
 /* Their weight gradient dW[N, K] += dY[M, N]^T X[M, K] (the AccumulateGrad of
  * the same nn.Linear weights), in two launches: swh_gemm_tn_partials writes
  * part[s][N][K] (fp32) = the sum over split s's tokens (S ranges of whole

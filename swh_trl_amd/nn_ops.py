@@ -201,6 +201,39 @@ def gemm_nt(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = Non
     return out
 
 
+def gemm_nt256_eligible(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> bool:
+    """Shapes swh_gemm_nt256 serves: bf16, N % 8 == 0, K % 64 == 0, unit inner strides,
+    32-bit staged offsets."""
+    ok = (x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 2 and w.dim() == 2
+          and x.shape[1] == w.shape[1] and w.shape[0] % 8 == 0 and w.shape[1] % 64 == 0 and w.shape[1] > 0
+          and x.stride(1) == 1 and w.stride(1) == 1 and x.stride(0) % 8 == 0 and w.stride(0) % 8 == 0
+          and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
+          and x.shape[0] * x.stride(0) < 2 ** 32 and w.shape[0] * w.stride(0) < 2 ** 32)
+    if ok and out is not None:
+        ok = (out.dtype == torch.bfloat16 and out.dim() == 2 and tuple(out.shape) == (x.shape[0], w.shape[0])
+              and out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 8 == 0)
+    return ok
+
+
+def gemm_nt256(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x w^T (+ bias) on the wide training GEMM (include/swh_trl_amd.h
+    swh_gemm_nt256): x [M, K], w [N, K], bf16."""
+    _dev(x, "gemm_nt256")
+    if not gemm_nt256_eligible(x, w, out):
+        raise ValueError(f"gemm_nt256: unsupported operands {tuple(x.shape)} x {tuple(w.shape)}")
+    M, K = x.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=x.dtype)
+    if bias is not None and (bias.dtype != torch.bfloat16 or not bias.is_contiguous() or bias.numel() != N
+                             or bias.data_ptr() % 8):
+        raise ValueError("gemm_nt256: bias must be a contiguous, 8-B aligned bf16 vector of N elements")
+    call("swh_gemm_nt256", x.data_ptr(), w.data_ptr(), _p(bias), out.data_ptr(), M, N, K, x.stride(0), w.stride(0),
+         out.stride(0), _stream())
+    return out
+
+
 def gemm_tn_eligible(dy: torch.Tensor, x: torch.Tensor) -> bool:
     """Shapes swh_gemm_tn_partials serves: bf16 [M, N] / [M, K], M % 64, N and K % 128."""
     return (dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dy.dim() == 2 and x.dim() == 2

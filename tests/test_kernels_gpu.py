@@ -1913,6 +1913,47 @@ def test_gemm_nt_row_invariant_and_strided(dev):
     assert torch.equal(out[:, 64:320], full)
 
 
+@pytest.mark.parametrize("M,N,K,bias", [(17408, 9728, 896, False), (4096, 151936, 896, False), (17408, 4864, 896, True),
+                                        (300, 136, 64, False), (257, 264, 128, True), (1, 8, 192, False),
+                                        (513, 1000, 960, True), (2048, 896, 4864, False)])
+def test_gemm_nt256_matches_fp32_product(dev, M, N, K, bias):
+    """swh_gemm_nt256 (the wide training projections: gate/up forward, the lm head,
+    the down input gradient) against the fp32 product of the same bf16 operands,
+    within one bf16 rounding plus the fp32 summation-order difference; ragged M and
+    N tiles, one- and two-tile K loops."""
+    from swh_trl_amd import _lib, nn_ops
+    _lib.load()
+    g = _gen(13)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(torch.bfloat16).to(dev)
+    b = (torch.randn(N, generator=g) * 0.1).to(torch.bfloat16).to(dev) if bias else None
+    y = nn_ops.gemm_nt256(x, w, b)
+    ref = x.float() @ w.float().t() + (b.float() if bias else 0)
+    bound = ref.abs() * 2.0 ** -8 + 1e-4 * float(ref.abs().max())
+    excess = ((y.float() - ref).abs() - bound).max()
+    assert float(excess) <= 0, float(excess)
+
+
+def test_gemm_nt256_row_invariant_and_strided(dev):
+    """A row's result does not depend on its place in the batch or on its tile
+    (fixed K order), strided operands and output views give the same bits, and the
+    columns of a ragged last tile equal those of a full one."""
+    from swh_trl_amd import _lib, nn_ops
+    _lib.load()
+    g = _gen(14)
+    x = torch.randn(700, 1024, generator=g).to(torch.bfloat16).to(dev)
+    w = (torch.randn(520, 896, generator=g) * 0.05).to(torch.bfloat16).to(dev)
+    xs = x[:, :896]  # lda 1024
+    full = nn_ops.gemm_nt256(xs, w)
+    perm = torch.randperm(700, generator=g).to(dev)
+    assert torch.equal(nn_ops.gemm_nt256(xs.contiguous()[perm], w), full[perm])
+    assert torch.equal(nn_ops.gemm_nt256(xs[129:300].contiguous(), w), full[129:300])
+    assert torch.equal(nn_ops.gemm_nt256(xs, w[264:].contiguous()), full[:, 264:])
+    out = torch.empty(700, 640, device=dev, dtype=torch.bfloat16)
+    nn_ops.gemm_nt256(xs, w, out=out[:, 64:584])
+    assert torch.equal(out[:, 64:584], full)
+
+
 @pytest.mark.parametrize("M,N,K,S,dtype", [(17408, 1152, 896, 8, torch.bfloat16), (17408, 896, 896, 4, torch.float32),
                                            (640, 128, 256, 3, torch.bfloat16), (128, 256, 128, 5, torch.float32)])
 def test_gemm_tn_weight_gradient_matches_fp32(dev, M, N, K, S, dtype):
