@@ -347,6 +347,14 @@ int swh_gemm_nt256(const void *A, const void *B, const void *bias, void *C, int6
 int swh_gemm_tn_partials(const void *dY, const void *X, float *part, float *colsum, int64_t M, int64_t N, int64_t K,
                          int64_t lddy, int64_t ldx, int32_t S, void *stream);
 int swh_gemm_tn_fold(const float *part, int32_t S, int64_t n, void *grad, int32_t dtype, void *stream);
+/* The weight gradient on the swh_gemm_nt256 schedule (csrc/tgemm256.hip): part[s][N][K]
+ * (fp32) = dY[tokens of split s]^T X, 256 x 256 tiles of (N, K), the tokens read
+ * through ds_read_b64_tr_b16; S ranges of whole 64-token steps, each summed in
+ * ascending token order; folded into the gradient by swh_gemm_tn_fold.  M % 64 == 0,
+ * N and K % 16 == 0, leading dimensions multiples of 8 elements, pointers 16-B
+ * aligned, M * ld * 2 < 2^31 bytes per operand; else SWH_E_ARG. */
+int swh_gemm_tn256_partials(const void *dY, const void *X, float *part, int64_t M, int64_t N, int64_t K, int64_t lddy,
+                            int64_t ldx, int32_t S, void *stream);
 /* dst_f32[i] += src[i] (bf16/f32) — accumulate micro-batch grads in fp32. */
 int swh_accumulate(float *dst, const void *src, int dtype, int64_t N, float scale, void *stream);
 

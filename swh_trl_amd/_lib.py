@@ -94,6 +94,7 @@ SIGNATURES = {
     "swh_gemm_nt": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp]),
     "swh_gemm_nt256": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp]),
     "swh_gemm_tn_partials": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp]),
+    "swh_gemm_tn256_partials": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp]),
     "swh_gemm_tn_fold": (c_i32, [c_vp, c_i32, c_i64, c_vp, c_i32, c_vp]),
     "swh_ema_mix": (c_i32, [c_vp, c_vp, c_i32, c_i64, c_f32, c_f32, c_vp]),
     "swh_rmsnorm_fwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_vp, c_vp, c_i32, c_vp]),

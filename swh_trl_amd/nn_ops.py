@@ -234,6 +234,36 @@ def gemm_nt256(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = 
     return out
 
 
+def gemm_tn256_eligible(dy: torch.Tensor, x: torch.Tensor) -> bool:
+    """Shapes swh_gemm_tn256_partials serves: bf16 [M, N] / [M, K], M % 64, N and K % 16,
+    31-bit byte offsets per operand."""
+    return (dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dy.dim() == 2 and x.dim() == 2
+            and dy.shape[0] == x.shape[0] and dy.shape[0] % 64 == 0 and dy.shape[1] % 16 == 0
+            and x.shape[1] % 16 == 0 and dy.stride(1) == 1 and x.stride(1) == 1 and dy.stride(0) % 8 == 0
+            and x.stride(0) % 8 == 0 and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0
+            and dy.shape[0] * dy.stride(0) * 2 < 2 ** 31 and x.shape[0] * x.stride(0) * 2 < 2 ** 31)
+
+
+def gemm_tn256_accumulate(grad: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, splits: int) -> torch.Tensor:
+    """grad [N, K] += dy^T x over the tokens on the 256 x 256 schedule
+    (include/swh_trl_amd.h swh_gemm_tn256_partials + swh_gemm_tn_fold): `splits`
+    token ranges in fp32 partials, folded in order and rounded once into grad.
+    Returns the partials buffer (keep it alive until the stream has run the launches)."""
+    _dev(dy, "gemm_tn256_accumulate")
+    if not gemm_tn256_eligible(dy, x):
+        raise ValueError(f"gemm_tn256_accumulate: unsupported operands {tuple(dy.shape)} / {tuple(x.shape)}")
+    M, N = dy.shape
+    K = x.shape[1]
+    if grad.numel() != N * K or not grad.is_contiguous():
+        raise ValueError("gemm_tn256_accumulate: grad must be a contiguous [N, K] view")
+    part = torch.empty(splits * N * K, device=dy.device, dtype=torch.float32)
+    call("swh_gemm_tn256_partials", dy.data_ptr(), x.data_ptr(), part.data_ptr(), M, N, K, dy.stride(0), x.stride(0),
+         int(splits), _stream())
+    call("swh_gemm_tn_fold", part.data_ptr(), int(splits), N * K, grad.data_ptr(),
+         _dtype_code(grad, "gemm_tn256_accumulate"), _stream())
+    return part
+
+
 def gemm_tn_eligible(dy: torch.Tensor, x: torch.Tensor) -> bool:
     """Shapes swh_gemm_tn_partials serves: bf16 [M, N] / [M, K], M % 64, N and K % 128."""
     return (dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dy.dim() == 2 and x.dim() == 2

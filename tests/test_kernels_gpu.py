@@ -1954,6 +1954,47 @@ def test_gemm_nt256_row_invariant_and_strided(dev):
     assert torch.equal(out[:, 64:584], full)
 
 
+@pytest.mark.parametrize("M,N,K,S,dtype", [(17408, 9728, 896, 5, torch.bfloat16), (17408, 896, 4864, 10, torch.float32),
+                                           (4096, 2000, 896, 1, torch.float32), (640, 272, 144, 3, torch.bfloat16),
+                                           (128, 16, 16, 5, torch.float32), (64, 512, 256, 1, torch.bfloat16)])
+def test_gemm_tn256_weight_gradient_matches_fp64(dev, M, N, K, S, dtype):
+    """swh_gemm_tn256_partials + swh_gemm_tn_fold (the wide weight gradients) against
+    grad + dY^T X in fp64 from the same bf16 operands: fp32 partial sums over token
+    ranges (S larger than the 64-token steps leaves empty splits), ragged N and K
+    tiles, one rounding into the gradient dtype."""
+    from swh_trl_amd import _lib, nn_ops
+    _lib.load()
+    g = _gen(15)
+    dy = (torch.randn(M, N, generator=g) * 0.05).to(torch.bfloat16)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    g0 = (torch.randn(N, K, generator=g) * 0.5).to(dtype)
+    ref = g0.double() + dy.double().t() @ x.double()
+    grad = g0.to(dev)
+    nn_ops.gemm_tn256_accumulate(grad, dy.to(dev), x.to(dev), S)
+    got = grad.cpu().double()
+    ulp = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -22
+    bound = ref.abs() * ulp + 1e-5 * float(ref.abs().max()) * (M / 4096) ** 0.5
+    excess = ((got - ref).abs() - bound).max()
+    assert float(excess) <= 0, float(excess)
+
+
+def test_gemm_tn256_equals_split_sums(dev):
+    """The split partials are plain token-range sums: S = 1 over a range equals the
+    partial of that range inside an S = 4 launch (same tokens, same order), bit for bit;
+    strided operands give the same bits."""
+    from swh_trl_amd import _lib, nn_ops
+    _lib.load()
+    g = _gen(16)
+    dy = (torch.randn(1024, 576, generator=g) * 0.05).to(torch.bfloat16).to(dev)
+    xw = torch.randn(1024, 640, generator=g).to(torch.bfloat16).to(dev)
+    x = xw[:, :528]  # ldx 640
+    p4 = nn_ops.gemm_tn256_accumulate(torch.zeros(576, 528, device=dev), dy, x, 4).view(4, 576, 528)
+    p1 = nn_ops.gemm_tn256_accumulate(torch.zeros(576, 528, device=dev), dy[256:512].contiguous(),
+                                      x[256:512].contiguous(), 1).view(576, 528)
+    torch.cuda.synchronize()
+    assert torch.equal(p4[1], p1)
+
+
 @pytest.mark.parametrize("M,N,K,S,dtype", [(17408, 1152, 896, 8, torch.bfloat16), (17408, 896, 896, 4, torch.float32),
                                            (640, 128, 256, 3, torch.bfloat16), (128, 256, 128, 5, torch.float32)])
 def test_gemm_tn_weight_gradient_matches_fp32(dev, M, N, K, S, dtype):
