@@ -205,6 +205,17 @@ struct SoftState {
 };
 __device__ __forceinline__ SoftState soft_init() { return {kNegInf, 0.f, 0.f}; }
 
+// Branch-free online (max, sum e^(z - max)) fold of one value for the streaming
+// draw passes (no entropy term; z may be -inf).  Equal to soft_fold<1>'s (m, s1):
+// for z <= m the rescale factor is e^0 = 1; the clamps turn the -inf - -inf NaNs of
+// an empty state into e^-1e4 = 0.  Multiply and add stay separate roundings, as there.
+__device__ __forceinline__ void soft_fold1(float &m, float &s1, float z) {
+    const float mn = fmaxf(m, z);
+    const float f = fast_exp(fmaxf(m - mn, -1.0e4f)), e = fast_exp(fmaxf(z - mn, -1.0e4f));
+    s1 = __fadd_rn(__fmul_rn(s1, f), e);
+    m = mn;
+}
+
 // Merge b into a.
 __device__ __forceinline__ SoftState soft_merge(SoftState a, SoftState b) {
     if (b.m == kNegInf) return a;
@@ -312,8 +323,10 @@ __device__ __forceinline__ float gumbel_from_bits(uint32_t w) {
     const uint32_t m = w >> 8;
     const float u = ((float)m + 0.5f) * (1.0f / 16777216.0f);
     const float d = ((float)(16777215u - m) + 0.5f) * (1.0f / 16777216.0f);
-    const float t = d < 0.0078125f ? d * fmaf(d, fmaf(d, 1.0f / 3.0f, 0.5f), 1.0f) : -fast_log(u);
-    return -fast_log(t);
+    // both branches evaluated, one select: a divergent branch here cost the streaming draw
+    // passes more than the series
+    const float ts = d * fmaf(d, fmaf(d, 1.0f / 3.0f, 0.5f), 1.0f), tl = -fast_log(u);
+    return -fast_log(d < 0.0078125f ? ts : tl);
 }
 
 // ---- launch helpers -----------------------------------------------------------

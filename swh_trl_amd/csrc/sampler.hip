@@ -7,8 +7,10 @@
 //   temperature -> top-k -> top-p -> min-p -> categorical draw / argmax ->
 //   pad-after-EOS bookkeeping.
 // The draw is Gumbel-max, argmax_j (z_j - log(-log u_j)), with u_j from a
-// Philox4x32-10 stream (key = seed, ctr = {j>>2, row, base+step}); that is an
-// exact sample of softmax(z) in one streaming pass, no sort, no cumsum.
+// Philox4x32-10 stream (key = seed, ctr = {j, row >> 2, base + step}, word row & 3);
+// that is an exact sample of softmax(z) in one streaming pass, no sort, no cumsum.
+// The unfiltered and the general filtered draw passes take four rows per
+// workgroup, so one Philox call serves the four rows of a column.
 //
 // Two kernels:
 //  * unfiltered rows (no top-k/top-p/min-p): the row is split over S
@@ -28,7 +30,9 @@ namespace {
 
 constexpr int kSplitThreads = 256;
 constexpr int kFiltThreads = 1024;
-constexpr int kMaxSplit = 64;
+constexpr int kMaxSplit = 64;       // row splits of the soft / digit passes
+constexpr int kMaxDrawSplit = 256;  // splits per row quad of the draw passes (partials per row)
+constexpr int kDrawWgs = 1024;      // draw-pass workgroups aimed at (row quads x splits; 512-2048 measured)
 
 struct Partial {
     float m, s1, best;
@@ -40,9 +44,11 @@ struct Proc {
     int32_t greedy, suppress, n_eos;
     int32_t eos[4];
     const uint32_t *seen;  // row bitmap or null
-    __device__ __forceinline__ float operator()(int64_t j, float x) const {
+    __device__ __forceinline__ float operator()(int64_t j, float x) const { return at(j, x, seen); }
+    // the same processing with another row's bitmap (the four-row draw passes)
+    __device__ __forceinline__ float at(int64_t j, float x, const uint32_t *sn) const {
         float z = x;
-        if (seen && ((seen[j >> 5] >> (j & 31)) & 1u)) z = (z < 0.f) ? z * rep : z / rep;
+        if (sn && ((sn[j >> 5] >> (j & 31)) & 1u)) z = (z < 0.f) ? z * rep : z / rep;
         if (suppress) {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
@@ -120,39 +126,146 @@ __device__ __forceinline__ void block_partial(SoftState &st, float &bk, int32_t 
     bi = i;
 }
 
+// The draw passes visit four rows (a row quad 4 q .. 4 q + 3) per workgroup: one
+// Philox4x32-10 call at counter {j, q, ctr} yields the Gumbel words of column j for
+// all four rows (word i: row 4 q + i, the stream gumbel_at defines), a quarter of the
+// per-element Philox work of one row per workgroup.  f(j, x[4]) gets the four rows'
+// values of column j; rows past B repeat row B - 1 (their results are not written).
+template <int DT, typename F>
+__device__ __forceinline__ void row4_foreach(const typename Elem<DT>::T *logits, int64_t ld, int64_t b0, int64_t B,
+                                             int64_t begin, int64_t end, int tid, int nthreads, F &&f) {
+    using T = typename Elem<DT>::T;
+    constexpr int PV = kPerVec<DT>;
+    if (end <= begin) return;
+    const T *rw[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rw[i] = logits + (b0 + i < B ? b0 + i : B - 1) * ld;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(rw[0] + begin);
+    const bool vec = ((ld * (int64_t)sizeof(T)) & 15) == 0 && (a & (sizeof(T) - 1)) == 0;  // rows share alignment
+    int64_t head = vec ? (int64_t)(((16 - (a & 15)) & 15) / sizeof(T)) : end - begin;
+    if (head > end - begin) head = end - begin;
+    float x[4];
+    for (int64_t j = begin + tid; j < begin + head; j += nthreads) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[i] = Elem<DT>::load(rw[i] + j);
+        f(j, x);
+    }
+    const int64_t bv = begin + head;
+    const int64_t nvec = vec ? (end - bv) / PV : 0;
+    auto body = [&](const uint4 (&raw)[4], int64_t j0) {
+        float xs[4][PV];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) unpack16<DT>(raw[i], xs[i]);
+#pragma unroll
+        for (int k = 0; k < PV; ++k) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[i] = xs[i][k];
+            f(j0 + k, x);
+        }
+    };
+    // one vector of each of the four rows per trip (four loads in flight): the body is
+    // instantiated PV times only — an unrolled second vector doubled the kernel past the
+    // instruction cache
+    for (int64_t v = tid; v < nvec; v += nthreads) {
+        uint4 raw[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) raw[i] = reinterpret_cast<const uint4 *>(rw[i] + bv)[v];
+        body(raw, bv + v * PV);
+    }
+    for (int64_t j = bv + nvec * PV + tid; j < end; j += nthreads) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[i] = Elem<DT>::load(rw[i] + j);
+        f(j, x);
+    }
+}
+
+__device__ __forceinline__ void philox_col(uint32_t k0, uint32_t k1, int64_t j, int64_t quad, uint64_t ctr,
+                                           uint32_t (&wd)[4]) {
+    const U4 w = philox4x32_10(U4{(uint32_t)j, (uint32_t)quad, (uint32_t)ctr, (uint32_t)(ctr >> 32)}, k0, k1);
+    wd[0] = w.x;
+    wd[1] = w.y;
+    wd[2] = w.z;
+    wd[3] = w.w;
+}
+
+// Draw-pass state of four rows, updated without branches (a filtered-out element
+// arrives as z = key = -inf and changes nothing, except that a chunk with no
+// survivor reports its first column with key -inf, which every survivor beats);
+// flush() writes the rows' block partials.
+struct Draw4 {
+    float m[4], s1[4], bk[4];
+    int32_t bi[4];
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            m[i] = kNegInf;
+            s1[i] = 0.f;
+            bk[i] = kNegInf;
+            bi[i] = 0x7fffffff;
+        }
+    }
+    __device__ __forceinline__ void add(int i, float z, float key, int32_t j) {
+        soft_fold1(m[i], s1[i], z);
+        const bool win = (key > bk[i]) | ((key == bk[i]) & ((uint32_t)j < (uint32_t)bi[i]));  // no short-circuit branch
+        bk[i] = win ? key : bk[i];
+        bi[i] = win ? j : bi[i];
+    }
+    __device__ __forceinline__ void flush(float *red, int64_t b0, int64_t B, int S, int s, Partial *part) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            SoftState st{m[i], s1[i], 0.f};
+            block_partial(st, bk[i], bi[i], red);
+            if (threadIdx.x == 0 && b0 + i < B) part[(b0 + i) * S + s] = Partial{st.m, st.s1, bk[i], bi[i]};
+        }
+    }
+};
+
+__device__ __forceinline__ void split_range(int64_t V, int64_t chunk, int64_t &beg, int64_t &end) {
+    beg = (int64_t)blockIdx.x * chunk;
+    end = beg + chunk < V ? beg + chunk : V;
+}
+
+// draw-pass splits per row quad, for about kDrawWgs workgroups
+inline int draw_split(int64_t B, int64_t V) {
+    const int64_t quads = (B + 3) / 4;
+    int S = 1;
+    while (S < kMaxDrawSplit && quads * S < kDrawWgs && V / (S * 2) >= 512) S *= 2;
+    return S;
+}
+
 // ---------------------------------------------------------------------------
 // Unfiltered: split rows.
 // ---------------------------------------------------------------------------
 template <int DT>
 __global__ __launch_bounds__(kSplitThreads) void sample_split_kernel(
-    const typename Elem<DT>::T *__restrict__ logits, int64_t V, int64_t ld, swh_sample_params p,
+    const typename Elem<DT>::T *__restrict__ logits, int64_t V, int64_t ld, int64_t B, swh_sample_params p,
     const uint64_t *__restrict__ rng, const int32_t *__restrict__ step_p, const uint32_t *__restrict__ seen,
     int64_t words, int64_t chunk, Partial *__restrict__ part, float *__restrict__ scores_out) {
     __shared__ float red[5 * (kSplitThreads / kWave)];
-    const int64_t b = blockIdx.y;
-    const int S = gridDim.x;
-    const int s = blockIdx.x;
+    const int64_t q = blockIdx.y, b0 = 4 * q;
+    const int S = gridDim.x, s = blockIdx.x;
     const int32_t step = *step_p;
-    const Proc pr = make_proc(p, step, seen ? seen + b * words : nullptr);
+    const Proc pr = make_proc(p, step, nullptr);
+    const bool pen = p.repetition_penalty != 1.0f && seen;
+    float *const srow = scores_out ? scores_out + b0 * V : nullptr;  // rows b0 .. b0 + 3 at V apart
     const uint64_t seed = rng[0], ctr = rng[1] + (uint64_t)step;
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-    const auto *row = logits + b * ld;
-    const int64_t beg = (int64_t)s * chunk;
-    const int64_t end = beg + chunk < V ? beg + chunk : V;
-    SoftState st = soft_init();
-    float bk = kNegInf;
-    int32_t bi = 0x7fffffff;
-    float *srow = scores_out ? scores_out + b * V : nullptr;
-    row_foreach<DT, false>(row, beg, end, threadIdx.x, kSplitThreads, [&](int64_t j, float x) {
-        const float z = pr(j, x);
-        if (srow) srow[j] = z;
-        if (z == kNegInf) return;
-        soft_fold<1>(st, &z);
-        const float key = p.greedy ? z : z + gumbel_at(k0, k1, j, b, ctr);
-        best_merge(bk, bi, key, (int32_t)j);
+    int64_t beg, end;
+    split_range(V, chunk, beg, end);
+    Draw4 d;
+    d.init();
+    row4_foreach<DT>(logits, ld, b0, B, beg, end, threadIdx.x, kSplitThreads, [&](int64_t j, const float (&x)[4]) {
+        uint32_t wd[4] = {0u, 0u, 0u, 0u};
+        if (!p.greedy) philox_col(k0, k1, j, q, ctr, wd);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t b = b0 + i < B ? b0 + i : B - 1;
+            const float z = pr.at(j, x[i], pen ? seen + b * words : nullptr);
+            if (srow && b0 + i < B) srow[i * V + j] = z;
+            d.add(i, z, p.greedy ? z : z + gumbel_from_bits(wd[i]), (int32_t)j);
+        }
     });
-    block_partial(st, bk, bi, red);
-    if (threadIdx.x == 0) part[b * S + s] = Partial{st.m, st.s1, bk, bi};
+    d.flush(red, b0, B, S, s, part);
 }
 
 // ---------------------------------------------------------------------------
@@ -194,7 +307,7 @@ struct FiltWs {
 };
 
 inline FiltWs filt_ws(void *ws, int64_t B) {
-    char *base = static_cast<char *>(ws) + B * kMaxSplit * (int64_t)sizeof(Partial);
+    char *base = static_cast<char *>(ws) + B * kMaxDrawSplit * (int64_t)sizeof(Partial);
     FiltWs w;
     w.row = reinterpret_cast<FiltRow *>(base);
     base += B * (int64_t)sizeof(FiltRow);
@@ -202,11 +315,6 @@ inline FiltWs filt_ws(void *ws, int64_t B) {
     base += B * kFiltSplit * (int64_t)sizeof(float2);
     w.hist = reinterpret_cast<float *>(base);
     return w;
-}
-
-__device__ __forceinline__ void split_range(int64_t V, int64_t chunk, int64_t &beg, int64_t &end) {
-    beg = (int64_t)blockIdx.x * chunk;
-    end = beg + chunk < V ? beg + chunk : V;
 }
 
 // (max, sum) of the processed scores >= the row threshold (st null: all) over split blockIdx.x
@@ -369,39 +477,46 @@ __global__ __launch_bounds__(kFiltThreads) void filt_select_kernel(FiltRow *__re
     }
 }
 
-// Final pass over split blockIdx.x: min-p, then the Gumbel-max draw among the survivors
+// Final pass over split blockIdx.x of a row quad: min-p, then the Gumbel-max draw among the survivors
 template <int DT>
 __global__ __launch_bounds__(kSplitThreads) void filt_draw_kernel(
-    const typename Elem<DT>::T *__restrict__ logits, int64_t V, int64_t ld, swh_sample_params p,
+    const typename Elem<DT>::T *__restrict__ logits, int64_t V, int64_t ld, int64_t B, swh_sample_params p,
     const uint64_t *__restrict__ rng, const int32_t *__restrict__ step_p, const uint32_t *__restrict__ seen,
     int64_t words, int64_t chunk, const FiltRow *__restrict__ st, Partial *__restrict__ part,
     float *__restrict__ scores_out) {
     __shared__ float red[5 * (kSplitThreads / kWave)];
-    const int64_t b = blockIdx.y;
+    const int64_t q = blockIdx.y, b0 = 4 * q;
     const int32_t step = *step_p;
-    const Proc pr = make_proc(p, step, seen ? seen + b * words : nullptr);
-    const FiltRow r = st[b];
-    float lo = r.lo;
-    // min-p: p_j < min_p * p_max  <=>  z_j < M + ln(min_p)
-    if (p.min_p > 0.f) lo = fmaxf(lo, r.M + logf(p.min_p));
+    const Proc pr = make_proc(p, step, nullptr);
+    const bool pen = p.repetition_penalty != 1.0f && seen;
+    float lo[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const FiltRow r = st[b0 + i < B ? b0 + i : B - 1];
+        lo[i] = r.lo;
+        // min-p: p_j < min_p * p_max  <=>  z_j < M + ln(min_p)
+        if (p.min_p > 0.f) lo[i] = fmaxf(lo[i], r.M + logf(p.min_p));
+    }
+    float *const srow = scores_out ? scores_out + b0 * V : nullptr;
     const uint64_t seed = rng[0], ctr = rng[1] + (uint64_t)step;
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     int64_t beg, end;
     split_range(V, chunk, beg, end);
-    SoftState sf = soft_init();
-    float bk = kNegInf;
-    int32_t bi = 0x7fffffff;
-    float *srow = scores_out ? scores_out + b * V : nullptr;
-    row_foreach<DT, false>(logits + b * ld, beg, end, threadIdx.x, kSplitThreads, [&](int64_t j, float x) {
-        float z = pr(j, x);
-        if (!(z >= lo)) z = kNegInf;
-        if (srow) srow[j] = z;
-        if (z == kNegInf) return;
-        soft_fold<1>(sf, &z);
-        best_merge(bk, bi, z + gumbel_at(k0, k1, j, b, ctr), (int32_t)j);
+    Draw4 d;
+    d.init();
+    row4_foreach<DT>(logits, ld, b0, B, beg, end, threadIdx.x, kSplitThreads, [&](int64_t j, const float (&x)[4]) {
+        uint32_t wd[4];
+        philox_col(k0, k1, j, q, ctr, wd);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t b = b0 + i < B ? b0 + i : B - 1;
+            float z = pr.at(j, x[i], pen ? seen + b * words : nullptr);
+            if (!(z >= lo[i])) z = kNegInf;
+            if (srow && b0 + i < B) srow[i * V + j] = z;
+            d.add(i, z, z + gumbel_from_bits(wd[i]), (int32_t)j);
+        }
     });
-    block_partial(sf, bk, bi, red);
-    if (threadIdx.x == 0) part[b * gridDim.x + blockIdx.x] = Partial{sf.m, sf.s1, bk, bi};
+    d.flush(red, b0, B, gridDim.x, blockIdx.x, part);
 }
 
 // ---------------------------------------------------------------------------
@@ -718,9 +833,12 @@ int launch_filtered(const typename Elem<DT>::T *lg, int64_t B, int64_t V, int64_
             filt_select_kernel<<<gr, kFiltThreads, 0, s>>>(w.row, w.hist, S, lvl, p.top_p);
         }
     }
-    filt_draw_kernel<DT><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, rng, step, seen, words, chunk, w.row, part,
-                                                      scores_out);
-    return S;
+    const int Sd = draw_split(B, V);
+    int64_t cd = (V + Sd - 1) / Sd;
+    cd = (cd + 7) / 8 * 8;
+    filt_draw_kernel<DT><<<dim3((unsigned)Sd, (unsigned)((B + 3) / 4)), kSplitThreads, 0, s>>>(
+        lg, V, ld, B, p, rng, step, seen, words, cd, w.row, part, scores_out);
+    return Sd;
 }
 
 }  // namespace
@@ -730,7 +848,7 @@ using namespace swh;
 
 extern "C" int64_t swh_sample_workspace_bytes(int64_t B, int64_t V) {
     (void)V;  // [split partials | filtered rows: state, (max, sum) partials, digit histograms]
-    return B * kMaxSplit * (int64_t)sizeof(Partial) + B * (int64_t)sizeof(FiltRow) +
+    return B * kMaxDrawSplit * (int64_t)sizeof(Partial) + B * (int64_t)sizeof(FiltRow) +
            B * kFiltSplit * (int64_t)sizeof(float2) + B * kFiltSplit * kBins * (int64_t)sizeof(float);
 }
 
@@ -759,11 +877,11 @@ extern "C" int swh_sample_step(const void *logits, int dtype, int64_t B, int64_t
         } else if (filtered) {                                                                                  \
             S = launch_filtered<DTC>(lg, B, V, ld, p, rng, step, seen, words, workspace, scores_out, s);         \
         } else {                                                                                                \
-            S = choose_split(B, V);                                                                             \
+            S = draw_split(B, V);                                                                               \
             int64_t chunk = (V + S - 1) / S;                                                                    \
             chunk = (chunk + 7) / 8 * 8;                                                                        \
-            sample_split_kernel<DTC><<<dim3((unsigned)S, (unsigned)B), dim3(kSplitThreads), 0, s>>>(            \
-                lg, V, ld, p, rng, step, seen, words, chunk, part, scores_out);                                 \
+            sample_split_kernel<DTC><<<dim3((unsigned)S, (unsigned)((B + 3) / 4)), dim3(kSplitThreads), 0, s>>>( \
+                lg, V, ld, B, p, rng, step, seen, words, chunk, part, scores_out);                              \
         }                                                                                                       \
         sample_finalize_kernel<DTC><<<dim3((unsigned)B), dim3(64), 0, s>>>(lg, V, ld, p, step, S, part,         \
                                                                              finished, seen, words, out_tokens, \
