@@ -616,6 +616,14 @@ def test_filtered_bf16_path_equals_general_path(ops, dev, kw, B, V, scale):
     assert torch.equal(sc16, sc32)
     assert torch.equal(t16, t32)
     torch.testing.assert_close(lp16, lp32, rtol=1e-6, atol=1e-6)
+    # the log-probs against float64 over the kept set (the device sums run in fp32)
+    kept = torch.isfinite(sc32)
+    z = torch.where(kept, sc32.double(), torch.tensor(float("-inf"), dtype=torch.float64))
+    exact = z.gather(1, t32.view(-1, 1)).squeeze(1) - torch.logsumexp(z, 1)
+    torch.testing.assert_close(lp16.double(), exact, rtol=2e-6, atol=2e-6)
+    # without the scores output (the rollout's call) the draws and log-probs are the same
+    t16n, _, lp16n, _, _ = _run_sampler(ops, dev, logits, params)
+    assert torch.equal(t16n, t16) and torch.equal(lp16n, lp16)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
