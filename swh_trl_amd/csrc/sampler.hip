@@ -220,6 +220,49 @@ struct Draw4 {
     }
 };
 
+// row_foreach in groups of up to kPerVec<DT> consecutive columns: f(j0, x[PV], n) with
+// x[k] the value of column j0 + k for k < n (the rest unset), so a pass can fold a
+// whole vector at once (one online-softmax rescale per vector instead of per element).
+template <int DT, typename F>
+__device__ __forceinline__ void row_foreach_vec(const typename Elem<DT>::T *row, int64_t begin, int64_t end, int tid,
+                                                int nthreads, F &&f) {
+    using T = typename Elem<DT>::T;
+    constexpr int PV = kPerVec<DT>;
+    if (end <= begin) return;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(row + begin);
+    int64_t head = (int64_t)(((16 - (a & 15)) & 15) / sizeof(T));
+    if ((a & (sizeof(T) - 1)) != 0) head = end - begin;
+    if (head > end - begin) head = end - begin;
+    float x[PV];
+    for (int64_t j = begin + tid; j < begin + head; j += nthreads) {
+        x[0] = Elem<DT>::load(row + j);
+        f(j, x, 1);
+    }
+    const int64_t b0 = begin + head;
+    const int64_t nvec = (end - b0) / PV;
+    const uint4 *vp = reinterpret_cast<const uint4 *>(row + b0);
+    constexpr int U = 4;
+    int64_t v = tid;
+    for (; v + (U - 1) * (int64_t)nthreads < nvec; v += U * (int64_t)nthreads) {
+        uint4 raw[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) raw[u] = vp[v + u * nthreads];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            unpack16<DT>(raw[u], x);
+            f(b0 + (v + u * nthreads) * PV, x, PV);
+        }
+    }
+    for (; v < nvec; v += nthreads) {
+        unpack16<DT>(vp[v], x);
+        f(b0 + v * PV, x, PV);
+    }
+    for (int64_t j = b0 + nvec * PV + tid; j < end; j += nthreads) {
+        x[0] = Elem<DT>::load(row + j);
+        f(j, x, 1);
+    }
+}
+
 __device__ __forceinline__ void split_range(int64_t V, int64_t chunk, int64_t &beg, int64_t &end) {
     beg = (int64_t)blockIdx.x * chunk;
     end = beg + chunk < V ? beg + chunk : V;
@@ -330,11 +373,17 @@ __global__ __launch_bounds__(kSplitThreads) void filt_soft_kernel(
     int64_t beg, end;
     split_range(V, chunk, beg, end);
     SoftState sf = soft_init();
-    row_foreach<DT, false>(logits + b * ld, beg, end, threadIdx.x, kSplitThreads, [&](int64_t j, float x) {
-        float z = pr(j, x);
-        if (!(z >= lo)) z = kNegInf;
-        soft_fold<1>(sf, &z);
-    });
+    constexpr int PV = kPerVec<DT>;
+    row_foreach_vec<DT>(logits + b * ld, beg, end, threadIdx.x, kSplitThreads,
+                        [&](int64_t j0, const float (&x)[PV], int n) {
+                            float z[PV];
+#pragma unroll
+                            for (int k = 0; k < PV; ++k) {
+                                const float zk = k < n ? pr(j0 + k, x[k]) : kNegInf;
+                                z[k] = zk >= lo ? zk : kNegInf;
+                            }
+                            soft_fold<PV>(sf, z);  // one rescale per vector
+                        });
     sf = block_soft(sf, red);
     if (threadIdx.x == 0) psoft[b * gridDim.x + blockIdx.x] = float2{sf.m, sf.s1};
 }
@@ -746,14 +795,21 @@ __global__ __launch_bounds__(kSplitThreads) void filt16_draw_kernel(
     float bk = kNegInf;
     int32_t bi = 0x7fffffff;
     float *srow = scores_out ? scores_out + b * V : nullptr;
-    row_foreach<SWH_BF16, false>(logits + b * ld, beg, end, threadIdx.x, kSplitThreads, [&](int64_t j, float x) {
-        float z = pr(j, x);
-        if ((int)ord_key16(x) < thr || !(z >= lo)) z = kNegInf;
-        if (srow) srow[j] = z;
-        if (z == kNegInf) return;
-        soft_fold<1>(sf, &z);
-        best_merge(bk, bi, z + gumbel_at(k0, k1, j, b, ctr), (int32_t)j);
-    });
+    row_foreach_vec<SWH_BF16>(logits + b * ld, beg, end, threadIdx.x, kSplitThreads,
+                              [&](int64_t j0, const float (&x)[8], int n) {
+                                  float z[8];
+#pragma unroll
+                                  for (int k = 0; k < 8; ++k) {
+                                      const float zk = k < n ? pr(j0 + k, x[k]) : kNegInf;
+                                      z[k] = ((int)ord_key16(x[k]) < thr || !(zk >= lo)) ? kNegInf : zk;
+                                      if (srow && k < n) srow[j0 + k] = z[k];
+                                  }
+                                  soft_fold<8>(sf, z);  // one rescale per vector
+#pragma unroll
+                                  for (int k = 0; k < 8; ++k)
+                                      if (z[k] != kNegInf)
+                                          best_merge(bk, bi, z[k] + gumbel_at(k0, k1, j0 + k, b, ctr), (int32_t)(j0 + k));
+                              });
     block_partial(sf, bk, bi, red);
     if (threadIdx.x == 0) part[b * S + blockIdx.x] = Partial{sf.m, sf.s1, bk, bi};
 }
