@@ -1,11 +1,15 @@
-// C[M, N] = A[M, K] · B[N, K]^T (+ bias[N]) for the wide training projections
-// (gate/up forward, the lm head, the down input gradient through a transposed
-// weight copy), where csrc/tgemm.hip's 128 x 128 two-stage loop reaches 0.7
-// PFLOP/s and hipBLASLt 1.0-1.1.
+// C[M, N] = A[M, K] · B[N, K]^T (+ bias[N]) and the token-split weight gradient
+// dY^T X for the wide training projections (gate/up forward, the lm head, the down
+// input gradient through a transposed weight copy), where csrc/tgemm.hip's
+// 128 x 128 two-stage loop reaches 0.7 PFLOP/s and hipBLASLt 1.0-1.1.  Measured
+// (DESIGN.md §14e): 1.32 PFLOP/s at 8192^3, but slower than hipBLASLt at the bench
+// step's K = 896 shapes and at par on the weight gradients, so the engine does not
+// route to these entry points; they stay as tested kernels with tools/bench_nt256.py.
 //
 // 256 x 256 output tiles, 8 waves of 128 x 64 (2 along M x 4 along N) on
-// v_mfma_f32_16x16x32_bf16, 64-wide K tiles staged by LDS-DMA (global_load_lds,
-// 16 B per lane) into two 64 KB buffers (one workgroup per CU).  A K tile is four
+// v_mfma_f32_16x16x32_bf16, 64-wide K tiles staged by LDS-DMA (buffer_load ... lds
+// through one buffer descriptor per staged run, 16 B per lane) into two 64 KB
+// buffers (one workgroup per CU).  A K tile is four
 // phases, one per quadrant (64 rows x 32 columns) of a wave's 128 x 64 block, in
 // the order (top, left), (top, right), (bottom, right), (bottom, left), so each
 // phase changes one operand half.  Every phase: raw s_barrier, the LDS fragment
