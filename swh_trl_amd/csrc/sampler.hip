@@ -657,6 +657,10 @@ struct Filt16Row {
 
 // The row's (max, lse) from the S soft partials (fixed order).
 __device__ __forceinline__ void row_soft16(const float2 *__restrict__ psoft, int64_t b, int S, float &M, float &lse) {
+    if (!psoft) {  // a top-k without min-p weighs nothing by the scores: no soft pass ran
+        M = lse = 0.f;
+        return;
+    }
     SoftState a = soft_init();
     for (int q = 0; q < S; ++q) a = soft_merge(a, SoftState{psoft[b * S + q].x, psoft[b * S + q].y, 0.f});
     M = a.m;
@@ -832,15 +836,17 @@ int launch_filtered16(const uint16_t *lg, int64_t B, int64_t V, int64_t ld, cons
     auto *rows = reinterpret_cast<Filt16Row *>(w.row);  // sizeof(Filt16Row) <= sizeof(FiltRow)
     float *h0 = w.hist, *h1 = w.hist + B * kFiltSplit * (int64_t)kBins16;
     const dim3 gs((unsigned)S, (unsigned)B);
-    filt_soft_kernel<SWH_BF16><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, nullptr, 0, chunk, nullptr, w.soft);
     const bool topk = p.top_k > 0 && p.top_k < V, topp = p.top_p < 1.0f;
     const bool filtered = topk || topp;
     const float target = topk ? (float)p.top_k : p.top_p;
+    // the row max / log-normaliser: top-p weights and min-p need them; a count threshold does not
+    const float2 *soft = (topp || p.min_p > 0.f) ? w.soft : nullptr;
+    if (soft) filt_soft_kernel<SWH_BF16><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, nullptr, 0, chunk, nullptr, w.soft);
     if (filtered) {
         if (topk) {
-            filt16_hist_kernel<false, 0><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, chunk, w.soft, nullptr, target,
+            filt16_hist_kernel<false, 0><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, chunk, soft, nullptr, target,
                                                                       rows, h0);
-            filt16_hist_kernel<false, 1><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, chunk, w.soft, h0, target,
+            filt16_hist_kernel<false, 1><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, chunk, soft, h0, target,
                                                                       rows, h1);
         } else {
             filt16_hist_kernel<true, 0><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, chunk, w.soft, nullptr, target,
@@ -849,7 +855,7 @@ int launch_filtered16(const uint16_t *lg, int64_t B, int64_t V, int64_t ld, cons
                                                                      rows, h1);
         }
     }
-    filt16_draw_kernel<<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, rng, step, chunk, w.soft, h1, target,
+    filt16_draw_kernel<<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, rng, step, chunk, soft, h1, target,
                                                     filtered ? 1 : 0, rows, part, scores_out);
     return S;
 }
