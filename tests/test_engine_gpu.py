@@ -253,6 +253,10 @@ def test_greedy_bench_layout_first_divergence_is_a_bf16_tie(dev):
     # how far the rows agree (first divergence per row, or the whole completion)
     agree = [C if t is None else t for _, t, _ in rep]
     print("bench-layout greedy agreement per prompt (tokens):", agree)
+    # a floor under the agreement (measured on MI355X: [2, 118, 140, 92, 231, 2, 256, 110], mean 119
+    # of 256): each divergence is already a <= 2-ulp tie above; the floor catches a change that moves
+    # the first ties much earlier while staying within that bound
+    assert sum(agree) / len(agree) >= 64, agree
 
 
 def test_sampled_rollout_is_reproducible_and_respects_min_new_tokens(dev):
