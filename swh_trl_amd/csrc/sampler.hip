@@ -672,10 +672,14 @@ __device__ __forceinline__ void row_soft16(const float2 *__restrict__ psoft, int
 // given `above0` above all bins.  Returns the bin (-1: total below target) and the
 // weight strictly above it; `lowest`: the lowest non-empty bin (the level-1 fallback).
 __device__ __forceinline__ int select16(const float *__restrict__ phist, int64_t b, int S, float above0, float target,
-                                        float &above, int &lowest, float *scan, int *sel) {
+                                        float &above, int &lowest, float *scan, int *sel,
+                                        const float *fs = nullptr) {
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6, nw = kSplitThreads >> 6;
     float h = 0.f;
-    for (int q = 0; q < S; ++q) h += phist[(b * S + q) * (int64_t)kBins16 + t];  // splits in fixed order
+    for (int q = 0; q < S; ++q) {  // splits in fixed order; fs: each split's weight scale (LDS)
+        const float v = phist[(b * S + q) * (int64_t)kBins16 + t];
+        h += fs ? v * fs[q] : v;
+    }
     if (t == 0) {
         sel[0] = -1;
         sel[1] = kBins16;
@@ -724,9 +728,14 @@ __global__ __launch_bounds__(kSplitThreads) void filt16_hist_kernel(
     row_soft16(psoft, b, S, M, lse);
     int prefix = 0;
     if constexpr (LVL == 1) {
+        // top-p: the digit-0 partials weigh e^(z - m_s) by their own split max (filt16_soft_hist0_kernel);
+        // e^(m_s - lse) puts them on the row's scale
+        __shared__ float fs[kFiltSplit];
+        if (EXPW && t < S) fs[t] = fast_exp(psoft[b * S + t].x - lse);
+        __syncthreads();
         float above;
         int lowest;
-        const int bin = select16(phist0, b, S, 0.f, target, above, lowest, scan, sel);
+        const int bin = select16(phist0, b, S, 0.f, target, above, lowest, scan, sel, EXPW ? fs : nullptr);
         if (bin < 0) {  // the filter's total weight stays below its target: keep everything
             if (blockIdx.x == 0 && t == 0) rows[b] = Filt16Row{M, lse, 0.f, 0, 0};
             return;
@@ -758,6 +767,62 @@ __global__ __launch_bounds__(kSplitThreads) void filt16_hist_kernel(
     });
     if (run_bin >= 0) atomicAdd(&hist[run_bin], run_w);
     __syncthreads();
+    phist[(b * S + blockIdx.x) * (int64_t)kBins16 + t] = (float)((double)hist[t] * (1.0 / 1099511627776.0));
+}
+
+// Top-p, split blockIdx.x: the soft partial (split max m_s, sum e^(z - m_s)) and the
+// digit-0 histogram in ONE launch — the split's max first (a read of its chunk), then
+// the histogram weighs e^(z - m_s) (2^-40 fixed point, as filt16_hist_kernel) while the
+// sum accumulates; the digit-1 pass rescales each split's bins by e^(m_s - lse).  The
+// second read of the chunk comes from the caches.
+__global__ __launch_bounds__(kSplitThreads) void filt16_soft_hist0_kernel(
+    const uint16_t *__restrict__ logits, int64_t V, int64_t ld, swh_sample_params p, const int32_t *__restrict__ step_p,
+    int64_t chunk, float2 *__restrict__ psoft, float *__restrict__ phist) {
+    __shared__ unsigned long long hist[kBins16];
+    __shared__ float red[5 * (kSplitThreads / kWave)];
+    const int64_t b = blockIdx.y;
+    const int t = threadIdx.x, S = gridDim.x;
+    const Proc pr = make_proc(p, *step_p, nullptr);
+    int64_t beg, end;
+    split_range(V, chunk, beg, end);
+    const uint16_t *row = logits + b * ld;
+    float m = kNegInf;
+    row_foreach_vec<SWH_BF16>(row, beg, end, t, kSplitThreads, [&](int64_t j0, const float (&x)[8], int n) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (k < n) m = fmaxf(m, pr(j0 + k, x[k]));
+    });
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, kWave));
+    if ((t & 63) == 0) red[t >> 6] = m;
+    hist[t] = 0ull;
+    __syncthreads();
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    static_assert(kSplitThreads == 4 * kWave, "four waves");
+    __syncthreads();  // red is reused by block_soft
+    float sum = 0.f;
+    int run_bin = -1;
+    unsigned long long run_w = 0ull;
+    if (m != kNegInf) {
+        row_foreach<SWH_BF16, false>(row, beg, end, t, kSplitThreads, [&](int64_t j, float x) {
+            const float z = pr(j, x);
+            if (z == kNegInf) return;
+            const float e = fast_exp(z - m);
+            sum += e;
+            const int bin = (int)(ord_key16(x) >> 8);
+            const unsigned long long w = (unsigned long long)(e * kHistScale);
+            if (bin == run_bin) {
+                run_w += w;
+            } else {
+                if (run_bin >= 0) atomicAdd(&hist[run_bin], run_w);
+                run_bin = bin;
+                run_w = w;
+            }
+        });
+    }
+    if (run_bin >= 0) atomicAdd(&hist[run_bin], run_w);
+    const SoftState st = block_soft(SoftState{m, sum, 0.f}, red);  // equal maxima: the sums add
+    if (t == 0) psoft[b * S + blockIdx.x] = float2{st.m, st.s1};
     phist[(b * S + blockIdx.x) * (int64_t)kBins16 + t] = (float)((double)hist[t] * (1.0 / 1099511627776.0));
 }
 
@@ -841,7 +906,8 @@ int launch_filtered16(const uint16_t *lg, int64_t B, int64_t V, int64_t ld, cons
     const float target = topk ? (float)p.top_k : p.top_p;
     // the row max / log-normaliser: top-p weights and min-p need them; a count threshold does not
     const float2 *soft = (topp || p.min_p > 0.f) ? w.soft : nullptr;
-    if (soft) filt_soft_kernel<SWH_BF16><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, nullptr, 0, chunk, nullptr, w.soft);
+    if (soft && !topp) filt_soft_kernel<SWH_BF16><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, nullptr, 0, chunk,
+                                                                               nullptr, w.soft);
     if (filtered) {
         if (topk) {
             filt16_hist_kernel<false, 0><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, chunk, soft, nullptr, target,
@@ -849,8 +915,7 @@ int launch_filtered16(const uint16_t *lg, int64_t B, int64_t V, int64_t ld, cons
             filt16_hist_kernel<false, 1><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, chunk, soft, h0, target,
                                                                       rows, h1);
         } else {
-            filt16_hist_kernel<true, 0><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, chunk, w.soft, nullptr, target,
-                                                                     rows, h0);
+            filt16_soft_hist0_kernel<<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, chunk, w.soft, h0);
             filt16_hist_kernel<true, 1><<<gs, kSplitThreads, 0, s>>>(lg, V, ld, p, step, chunk, w.soft, h0, target,
                                                                      rows, h1);
         }
