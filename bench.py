@@ -145,7 +145,7 @@ def cpu_cfg1(threads: int, steps: int = 2) -> dict:
 
 
 # PMC passes of the shipped build (tools/gpu_pmc.sh + tools/pmc_summary.py); SWH_PMC_FILE overrides
-PMC_FILE = os.environ.get("SWH_PMC_FILE", os.path.join(ROOT, "profiles", "r5_v10_pmc_decode.json"))
+PMC_FILE = os.environ.get("SWH_PMC_FILE", os.path.join(ROOT, "profiles", "r6_final_pmc_decode.json"))
 
 
 def pmc_traffic(kernel: str):
